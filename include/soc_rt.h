@@ -1,0 +1,332 @@
+/*
+ * soc_rt.h — C ABI of the MI355X-native screen-space deferred-shading and post-processing
+ * passes of lukasino1214/soc_real_time_renderer.
+ *
+ * Every entry point below replaces ONE render-graph task of the reference (a Daxa task struct whose
+ * callback() records a fullscreen draw / compute dispatch). The reference file:line of the task that
+ * each function replaces is cited next to it. Shader-level semantics (sampling, formats, quirks
+ * Q1..Q12 of SURVEY.md §8a) are documented in DESIGN.md.
+ *
+ * Conventions:
+ *   - The caller owns all device memory. No function allocates on the hot path, and none keeps a
+ *     pointer after it returns.
+ *   - Calls are stream-ordered and asynchronous on the given HIP stream; the caller synchronises.
+ *   - Return value: 0 on success, < 0 on error (SOC_E_*); soc_last_error_string() gives the
+ *     message of the calling thread's last error. No C++ exception crosses this ABI.
+ *   - Images are pitch-linear, row-major, y = 0 is the TOP row (the reference's uv.y = 0).
+ *   - `const soc_globals* g` is a HOST pointer to the per-frame globals (mirror of ShaderGlobals,
+ *     src/graphics/shared.inl:47-131). Only the fields a pass reads are consumed; they are packed
+ *     into the kernel arguments at call time (the reference memcpy's the whole block into a UBO
+ *     ring slot, src/graphics/renderer.cpp:648-657).
+ */
+#ifndef SOC_RT_H
+#define SOC_RT_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SOC_RT_ABI_VERSION 1
+
+/* Error codes. */
+#define SOC_OK 0
+#define SOC_E_INVALID_ARG (-1)   /* null pointer, bad format, bad extent            */
+#define SOC_E_SHAPE (-2)         /* image extents inconsistent with the pass        */
+#define SOC_E_HIP (-3)           /* a HIP runtime call failed (launch, memcpy, ...) */
+#define SOC_E_UNSUPPORTED (-4)   /* format / configuration not implemented          */
+
+struct ihipStream_t;
+typedef struct ihipStream_t* soc_stream; /* == hipStream_t; NULL = the null stream */
+
+/* Image formats: the reference's Vulkan formats (src/graphics/renderer.cpp:348-470). */
+typedef enum soc_format {
+    SOC_FMT_RGBA16F = 1,     /* R16G16B16A16_SFLOAT, 8 B/px (albedo, emissive, normal, color, velocity, bloom mips) */
+    SOC_FMT_D32F = 2,        /* D32_SFLOAT, 4 B/px (depth, sun shadow map)                                      */
+    SOC_FMT_R8_UNORM = 3,    /* R8_UNORM, 1 B/px (ssao, ssao blur)                                              */
+    SOC_FMT_RGBA8_UNORM = 4, /* R8G8B8A8_UNORM, 4 B/px (clouds, noise texture, headless swapchain)              */
+    SOC_FMT_RGBA8_SRGB = 5,  /* R8G8B8A8_SRGB, 4 B/px (optional headless swapchain with sRGB encode on store)   */
+    SOC_FMT_RGBA32F = 6      /* R32G32B32A32_SFLOAT, 16 B/px (debug / exact tone-map output)                     */
+} soc_format;
+
+/* A borrowed view of a 2-D image in device memory (host memory for the CPU oracle). */
+typedef struct soc_img {
+    void* data;
+    int32_t width;
+    int32_t height;
+    int32_t pitch_bytes; /* bytes between rows; >= width * bytes_per_pixel(format) */
+    int32_t format;      /* soc_format */
+} soc_img;
+
+/* --- Globals: POD mirror of ShaderGlobals (src/graphics/shared.inl:5-131). ----------------------
+ * Matrices are glm-layout column-major float[16] (m[col*4 + row]). Daxa sampler / image ids and the
+ * AutoExposure buffer pointer are not part of this struct: samplers are fixed by the pass contract
+ * (DESIGN.md "Sampling contract") and images/buffers are explicit arguments. */
+typedef struct soc_point_light {   /* shared.inl:5-9 */
+    float position[3];
+    float color[3];
+    float intensity;
+} soc_point_light;
+
+typedef struct soc_spot_light {    /* shared.inl:13-20 */
+    float position[3];
+    float direction[3];
+    float color[3];
+    float intensity;
+    float cut_off;
+    float outer_cut_off;
+} soc_spot_light;
+
+typedef struct soc_sun_info {      /* shared.inl:24-37 */
+    float projection_matrix[16];
+    float view_matrix[16];
+    float projection_view_matrix[16];
+    float terrain_y_clip_trick[4];
+    float position[3];
+    float direction[3];
+    float exponential_factor;
+    float darkening_factor;
+    float bias;
+    float intensity;
+} soc_sun_info;
+
+#define SOC_MAX_POINT_LIGHTS 128
+#define SOC_MAX_SPOT_LIGHTS 128
+#define SOC_AUTO_EXPOSURE_BIN_COUNT 256
+#define SOC_SSAO_MAX_KERNEL 26
+
+typedef struct soc_globals {       /* shared.inl:47-131 */
+    float camera_projection_matrix[16];
+    float camera_inverse_projection_matrix[16];
+    float camera_view_matrix[16];
+    float camera_inverse_view_matrix[16];
+    float camera_projection_view_matrix[16];
+    float camera_inverse_projection_view_matrix[16];
+
+    float camera_previous_projection_matrix[16];
+    float camera_previous_inverse_projection_matrix[16];
+    float camera_previous_view_matrix[16];
+    float camera_previous_inverse_view_matrix[16];
+    float camera_previous_projection_view_matrix[16];
+    float camera_previous_inverse_projection_view_matrix[16];
+
+    float jitter[2];
+    float previous_jitter[2];
+
+    float camera_position[3];
+    float camera_near_clip;
+    float camera_far_clip;
+
+    int32_t resolution[2];
+    float elapsed_time;
+    float delta_time;
+    uint32_t frame_counter;
+
+    soc_sun_info sun_info;
+
+    uint32_t point_light_count;
+    uint32_t spot_light_count;
+    soc_point_light point_lights[SOC_MAX_POINT_LIGHTS];
+    soc_spot_light spot_lights[SOC_MAX_SPOT_LIGHTS];
+
+    float terrain_offset[3];
+    float terrain_scale[2];
+    float terrain_height_scale;
+    float terrain_midpoint;
+    float terrain_delta;
+    float terrain_min_depth;
+    float terrain_max_depth;
+    int32_t terrain_min_tess_level;
+    int32_t terrain_max_tess_level;
+    float terrain_y_clip_trick[4];
+    float terrain_previous_y_clip_trick[4];
+
+    float filter_radius;           /* bloom (unused by the reference shaders) */
+
+    float ssao_bias;
+    float ssao_radius;
+    int32_t ssao_kernel_size;
+
+    float ambient[3];
+    float ambient_occlussion_strength;
+    float emissive_bloom_strength;
+
+    float focal_length;            /* depth of field (disabled in the reference graph) */
+    float plane_in_focus;
+    float aperture;
+
+    float adjustment_speed;
+    float log_min_luminance;
+    float log_max_luminance;
+    float target_luminance;
+
+    float saturation;
+    float agxDs_linear_section;
+    float peak;
+    float compression;
+} soc_globals;
+
+/* AutoExposure buffer (shared.inl:39-45), device memory, caller-owned. */
+typedef struct soc_auto_exposure {
+    float exposure;
+    uint32_t histogram_buckets[SOC_AUTO_EXPOSURE_BIN_COUNT];
+} soc_auto_exposure;
+
+/* --- Library / ABI introspection ---------------------------------------------------------------- */
+int32_t soc_abi_version(void);
+size_t soc_abi_sizeof(const char* type_name);                        /* "soc_globals", "soc_img", ... */
+int64_t soc_abi_offsetof(const char* type_name, const char* field);  /* -1 if unknown */
+const char* soc_last_error_string(void);
+const char* soc_device_arch(void);                                   /* "gfx950" the kernels were built for */
+
+/* --- Host-side globals feed (native C++, no GPU needed) ----------------------------------------- */
+/* Renderer defaults: renderer.cpp:72-133 (terrain, ssao, composition, dof, auto exposure incl. the
+ * log_min/log_max re-derivation of :103-104, tone mapping, sun ortho/lookAt/dir of :109-133). */
+int soc_globals_init_defaults(soc_globals* g, int32_t width, int32_t height);
+
+/* Camera state of ControlledCamera3D (camera.hpp:105-119): position + rotation (x = yaw, y = pitch). */
+typedef struct soc_camera {
+    float position[3];
+    float rotation[3];
+    float fov_degrees;   /* Camera3D::fov  = 90  (camera.hpp:74) */
+    float near_clip;     /* Camera3D::near = 0.1 */
+    float far_clip;      /* Camera3D::far  = 1000 */
+} soc_camera;
+
+/* One Application::update() (application.cpp:109-165) without input: rebuilds the camera view
+ * (camera.cpp:40-56) and projection (camera.cpp:6-10, Y flip), the R2 jitter (period 32, :113-127,
+ * applied to proj[3][0..1], :129-131), shifts current -> previous matrices, and advances
+ * delta_time / elapsed_time / frame_counter. *jitter_index is advanced like the reference's. */
+int soc_globals_frame_update(soc_globals* g, const soc_camera* cam, int32_t width, int32_t height,
+                             float delta_time, uint32_t* jitter_index);
+
+/* glm restatements used by the feed (exported for tests): column-major float[16]. */
+void soc_mat4_perspective_rh_no(float out[16], float fovy_radians, float aspect, float znear, float zfar);
+void soc_mat4_ortho_rh_no(float out[16], float l, float r, float b, float t, float znear, float zfar);
+void soc_mat4_look_at_rh(float out[16], const float eye[3], const float center[3], const float up[3]);
+void soc_mat4_inverse(float out[16], const float m[16]);
+void soc_mat4_mul(float out[16], const float a[16], const float b[16]);
+
+/* --- ★ Passes (one per reference task) ---------------------------------------------------------- */
+
+/* BloomDownsampleTask (src/graphics/tasks/bloom_downsample.inl:19-68, shader :107-141):
+ * 13-tap COD:AW filter of `higher_mip` written to `lower_mip` (any size ratio; exact 1:1 and 2:1
+ * fast paths). RGBA16F -> RGBA16F. */
+int soc_bloom_downsample(const soc_globals* g, soc_img higher_mip, soc_img lower_mip, soc_stream stream);
+
+/* BloomUpsampleTask (bloom_upsample.inl:19-77, shader :98-127): 9-tap tent of `lower_mip` that
+ * OVERWRITES `higher_mip` (CLEAR + ONE/ONE blend == overwrite, quirk Q5). RGBA16F -> RGBA16F. */
+int soc_bloom_upsample(const soc_globals* g, soc_img lower_mip, soc_img higher_mip, soc_stream stream);
+
+/* Whole bloom chain as scheduled by renderer.cpp:1024-1062: down(emissive->mip0), down(mip i ->
+ * mip i+1), up(mip i -> mip i-1), up(mip0 -> emissive). `mips` holds mip_count images (4 in the
+ * reference, renderer.hpp:51). */
+int soc_bloom_chain(const soc_globals* g, soc_img emissive, const soc_img* mips, int32_t mip_count,
+                    soc_stream stream);
+
+/* SSAOGenerationTask (ssao_generation.inl:20-68, shader :176-214): half-res R8 ambient occlusion from
+ * full-res depth (D32F) and normal (RGBA16F). `target` is (W/2)x(H/2) R8_UNORM. `noise_table` is an
+ * optional device workspace of (target.w * target.h * 2) floats holding the per-pixel random vector
+ * of :184-188 (a pure function of uv and the normal-image size, filled by
+ * soc_ssao_prepare_noise); pass NULL to evaluate it inline. */
+int soc_ssao_prepare_noise(soc_img normal, soc_img target, float* noise_table, soc_stream stream);
+int soc_ssao_generation(const soc_globals* g, soc_img depth, soc_img normal, soc_img target,
+                        const float* noise_table, soc_stream stream);
+
+/* SSAOBlurTask (ssao_blur.inl:19-70, shader :91-106): 4x4 box, offsets -2..+1. R8 -> R8. */
+int soc_ssao_blur(const soc_globals* g, soc_img ssao, soc_img target, soc_stream stream);
+
+/* CloudRenderingTask (cloud_rendering.inl:27-54, shader :441-481): atmosphere + volumetric clouds on
+ * sky pixels (depth == 1), constant (0.2,0.4,1.0) elsewhere. `noise` is the 64x64 RGBA8 or R8
+ * noise texture (assets/Clouds/noise.png, REPEAT). target: RGBA8_UNORM full-res (quirk Q6). */
+int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img noise, soc_img target, soc_stream stream);
+
+/* CompositionTask (composition.inl:29-79, shader :162-225): deferred lighting with the sun ESM
+ * shadow, point/spot lights, ambient * AO^strength, emissive * strength, clouds on sky pixels.
+ * `d_globals` is a DEVICE copy of *g (soc_upload_globals) and is only read when the frame has
+ * point or spot lights (it may be NULL otherwise). Writes RGBA16F `target`. */
+int soc_composition(const soc_globals* g, const soc_globals* d_globals, soc_img target, soc_img albedo,
+                    soc_img emissive, soc_img normal, soc_img depth, soc_img ssao, soc_img shadow,
+                    soc_img clouds, soc_stream stream);
+
+/* GenerateLuminanceHistogramTask (generate_luminance_histogram.inl:23-47, shader :59-78): adds the
+ * frame's 256-bin log-luminance histogram into d_auto_exposure->histogram_buckets. */
+int soc_generate_luminance_histogram(const soc_globals* g, soc_img hdr, soc_auto_exposure* d_auto_exposure,
+                                     soc_stream stream);
+
+/* ResolveLuminanceHistogramTask (resolve_luminance_histogram.inl:20-43, shader :56-80): weighted mean
+ * of the bins -> exposure (exponential adaptation), then clears the bins.
+ * total_pixels == 0 -> resolution.x*resolution.y (reference). wide_accumulator != 0 -> 64-bit
+ * weighted sum (multi-GPU all-reduced bins); 0 -> reference u32 wrap semantics. */
+int soc_resolve_luminance_histogram(const soc_globals* g, soc_auto_exposure* d_auto_exposure,
+                                    uint64_t total_pixels, int32_t wide_accumulator, soc_stream stream);
+
+/* TemporalAntiAliasingTask (temporal_antialiasing.inl:54-116, shader :137-190). Writes RGBA16F
+ * `target`. If `velocity_history_out` has data != NULL, the kernel also writes a copy of
+ * current_velocity into it (fused CopyImageTask of renderer.cpp:1191-1198); it must not alias
+ * previous_velocity. */
+int soc_temporal_antialiasing(const soc_globals* g, soc_img target, soc_img current_color,
+                              soc_img previous_color, soc_img current_velocity, soc_img previous_velocity,
+                              soc_img depth, soc_img velocity_history_out, soc_stream stream);
+
+/* CopyImageTask (temporal_antialiasing.inl:16-37): same-format, same-extent image copy. */
+int soc_copy_image(soc_img target, soc_img source, soc_stream stream);
+
+/* ToneMappingTask (tone_mapping.inl:20-70, shader :145-176): AgX-DS with exposure from
+ * d_auto_exposure->exposure. target: RGBA8_UNORM / RGBA8_SRGB / RGBA16F / RGBA32F. */
+int soc_tone_mapping(const soc_globals* g, soc_img color, const soc_auto_exposure* d_auto_exposure,
+                     soc_img target, soc_stream stream);
+
+/* Device copy of the globals block (the reference's per-frame UBO upload, renderer.cpp:648-657). */
+int soc_upload_globals(const soc_globals* g, soc_globals* d_globals, soc_stream stream);
+
+/* --- Render graph (host C++ mirror of Renderer::rebuild_task_graph, renderer.cpp:929-1235) ------ */
+
+/* Frame images. The caller allocates them (device memory) and keeps them alive. */
+typedef struct soc_frame_images {
+    soc_img albedo, emissive, normal, depth, velocity;  /* G-buffer (produced upstream) */
+    soc_img shadow;                                     /* sun shadow map, D32F 4096^2 */
+    soc_img noise;                                      /* clouds noise 64^2 */
+    soc_img bloom_mips[4];                              /* RGBA16F W,W/2,W/4,W/8 */
+    soc_img ssao, ssao_blur;                            /* R8 (W/2)x(H/2) */
+    soc_img clouds;                                     /* RGBA8 WxH */
+    soc_img color;                                      /* RGBA16F composition output */
+    soc_img history_color[2];                           /* RGBA16F TAA resolved / previous (ping-pong) */
+    soc_img history_velocity[2];                        /* RGBA16F previous velocity (ping-pong) */
+    soc_img output;                                     /* tone-mapped framebuffer (RGBA8) */
+    float* ssao_noise_table;                            /* optional (ssao.w*ssao.h*2 floats) or NULL */
+    soc_auto_exposure* auto_exposure;                   /* device */
+    soc_globals* d_globals;                             /* device copy of the globals */
+} soc_frame_images;
+
+typedef struct soc_renderer soc_renderer;
+
+/* Phases of one frame. The luminance all-reduce of a multi-GPU run sits between PRE and POST. */
+#define SOC_PHASE_PRE_EXPOSURE 1   /* bloom, ssao, blur, clouds, composition, histogram */
+#define SOC_PHASE_POST_EXPOSURE 2  /* resolve, taa (+ fused velocity history), tone mapping */
+#define SOC_PHASE_ALL 3
+
+/* flags */
+#define SOC_RENDERER_TIMING 1      /* record hipEvents around every pass (GPUMetric, gpu_metric.cpp:18-42) */
+
+soc_renderer* soc_renderer_create(const soc_frame_images* images, uint32_t flags);
+void soc_renderer_destroy(soc_renderer* r);
+int soc_renderer_execute(soc_renderer* r, const soc_globals* g, int32_t phase, soc_stream stream);
+/* Histogram normalisation for a multi-GPU resolve: total pixels over all ranks (0 = this frame). */
+int soc_renderer_set_exposure_pixels(soc_renderer* r, uint64_t total_pixels, int32_t wide_accumulator);
+int32_t soc_renderer_pass_count(const soc_renderer* r);
+const char* soc_renderer_pass_name(const soc_renderer* r, int32_t index);
+const char* soc_renderer_pass_group(const soc_renderer* r, int32_t index);   /* renderer.cpp:558-588 names */
+/* Milliseconds of pass `index` in the most recent executed frame (needs SOC_RENDERER_TIMING and a
+ * completed stream); < 0 if unavailable. */
+float soc_renderer_pass_ms(soc_renderer* r, int32_t index);
+/* Index (0/1) of the history_color slot holding this frame's TAA result (= tone-map input). */
+int32_t soc_renderer_current_history(const soc_renderer* r);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SOC_RT_H */

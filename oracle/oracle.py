@@ -1,0 +1,157 @@
+"""ctypes binding of the CPU oracle (oracle/build/libsoc_oracle.so).
+
+TEST INFRASTRUCTURE ONLY — imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg,
+never by the product package. Arrays are numpy, host memory; signatures mirror include/soc_rt.h.
+Parity vs the reference itself is unpinned (see soc_oracle.h).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from soc_real_time_renderer_amd import _abi
+from soc_real_time_renderer_amd._abi import AutoExposure, Globals, SocImg
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "libsoc_oracle.so")
+
+_LIB = None
+_G = C.POINTER(Globals)
+_IMG = SocImg
+_FUNCS = {
+    "soc_oracle_bloom_downsample": (C.c_int, [_G, _IMG, _IMG]),
+    "soc_oracle_bloom_upsample": (C.c_int, [_G, _IMG, _IMG]),
+    "soc_oracle_ssao_generation": (C.c_int, [_G, _IMG, _IMG, _IMG]),
+    "soc_oracle_ssao_blur": (C.c_int, [_G, _IMG, _IMG]),
+    "soc_oracle_cloud_rendering": (C.c_int, [_G, _IMG, _IMG, _IMG]),
+    "soc_oracle_composition": (C.c_int, [_G] + [_IMG] * 8),
+    "soc_oracle_generate_luminance_histogram": (C.c_int, [_G, _IMG, C.POINTER(AutoExposure)]),
+    "soc_oracle_resolve_luminance_histogram": (C.c_int, [_G, C.POINTER(AutoExposure), C.c_uint64, C.c_int32]),
+    "soc_oracle_temporal_antialiasing": (C.c_int, [_G] + [_IMG] * 6),
+    "soc_oracle_tone_mapping": (C.c_int, [_G, _IMG, C.POINTER(AutoExposure), _IMG]),
+    "soc_oracle_luminance_bin": (C.c_uint32, [C.c_float] * 5),
+    "soc_oracle_log2": (C.c_float, [C.c_float]),
+    "soc_oracle_f32_to_f16": (C.c_uint16, [C.c_float]),
+    "soc_oracle_f16_to_f32": (C.c_float, [C.c_uint16]),
+    "soc_oracle_clouds_counters": (None, [C.POINTER(C.c_uint64)]),
+    "soc_oracle_num_threads": (C.c_int, []),
+}
+
+
+def build() -> str:
+    """Compile the oracle with its Makefile (gcc, OpenMP). Returns the library path."""
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+def lib() -> C.CDLL:
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        l = C.CDLL(LIB_PATH)
+        _abi.bind(l, _FUNCS)
+        _LIB = l
+    return _LIB
+
+
+def _img(a, fmt=None) -> SocImg:
+    from soc_real_time_renderer_amd import img  # layout helper only (no GPU work)
+    return img(a, fmt)
+
+
+def _rc(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"oracle {what} failed rc={rc}")
+
+
+def bloom_downsample(g, hi, lo):
+    _rc(lib().soc_oracle_bloom_downsample(C.byref(g), _img(hi), _img(lo)), "bloom_downsample")
+
+
+def bloom_upsample(g, lo, hi):
+    _rc(lib().soc_oracle_bloom_upsample(C.byref(g), _img(lo), _img(hi)), "bloom_upsample")
+
+
+def bloom_chain(g, emissive, mips):
+    bloom_downsample(g, emissive, mips[0])
+    for i in range(len(mips) - 1):
+        bloom_downsample(g, mips[i], mips[i + 1])
+    for i in range(len(mips) - 1, 0, -1):
+        bloom_upsample(g, mips[i], mips[i - 1])
+    bloom_upsample(g, mips[0], emissive)
+
+
+def ssao_generation(g, depth, normal, target):
+    _rc(lib().soc_oracle_ssao_generation(C.byref(g), _img(depth), _img(normal), _img(target)), "ssao_generation")
+
+
+def ssao_blur(g, ssao, target):
+    _rc(lib().soc_oracle_ssao_blur(C.byref(g), _img(ssao), _img(target)), "ssao_blur")
+
+
+def cloud_rendering(g, depth, noise, target):
+    _rc(lib().soc_oracle_cloud_rendering(C.byref(g), _img(depth), _img(noise), _img(target)), "cloud_rendering")
+
+
+def clouds_counters():
+    a = (C.c_uint64 * 4)()
+    lib().soc_oracle_clouds_counters(a)
+    return [int(v) for v in a]
+
+
+def composition(g, target, albedo, emissive, normal, depth, ssao, shadow, clouds):
+    _rc(lib().soc_oracle_composition(C.byref(g), _img(target), _img(albedo), _img(emissive), _img(normal), _img(depth),
+                                     _img(ssao), _img(shadow), _img(clouds)), "composition")
+
+
+def generate_luminance_histogram(g, hdr, ae: AutoExposure):
+    _rc(lib().soc_oracle_generate_luminance_histogram(C.byref(g), _img(hdr), C.byref(ae)), "histogram")
+
+
+def resolve_luminance_histogram(g, ae: AutoExposure, total_pixels=0, wide=False):
+    _rc(lib().soc_oracle_resolve_luminance_histogram(C.byref(g), C.byref(ae), int(total_pixels), int(bool(wide))),
+        "resolve")
+
+
+def temporal_antialiasing(g, target, cur, prev, vel, pvel, depth):
+    _rc(lib().soc_oracle_temporal_antialiasing(C.byref(g), _img(target), _img(cur), _img(prev), _img(vel), _img(pvel),
+                                               _img(depth)), "taa")
+
+
+def tone_mapping(g, color, ae: AutoExposure, target, target_format=None):
+    _rc(lib().soc_oracle_tone_mapping(C.byref(g), _img(color), C.byref(ae), _img(target, target_format)), "tone_mapping")
+
+
+def luminance_bin(r, g, b, log_min, log_max) -> int:
+    return int(lib().soc_oracle_luminance_bin(r, g, b, log_min, log_max))
+
+
+def log2(x: float) -> float:
+    return float(lib().soc_oracle_log2(x))
+
+
+def num_threads() -> int:
+    return int(lib().soc_oracle_num_threads())
+
+
+def frame(g, fr: dict, ae: AutoExposure, total_pixels=0, wide=False, hist=0):
+    """One full hot-path frame on the CPU (renderer.cpp:1024-1217 order), numpy frame dict as
+    soc_real_time_renderer_amd.alloc_frame lays out (host arrays). Returns the history slot written."""
+    bloom_chain(g, fr["emissive"], fr["bloom_mips"])
+    ssao_generation(g, fr["depth"], fr["normal"], fr["ssao"])
+    ssao_blur(g, fr["ssao"], fr["ssao_blur"])
+    cloud_rendering(g, fr["depth"], fr["noise"], fr["clouds"])
+    composition(g, fr["color"], fr["albedo"], fr["emissive"], fr["normal"], fr["depth"], fr["ssao_blur"], fr["shadow"],
+                fr["clouds"])
+    generate_luminance_histogram(g, fr["color"], ae)
+    resolve_luminance_histogram(g, ae, total_pixels, wide)
+    q = 1 - hist
+    temporal_antialiasing(g, fr["history_color"][q], fr["color"], fr["history_color"][hist], fr["velocity"],
+                          fr["history_velocity"][hist], fr["depth"])
+    fr["history_velocity"][q][...] = fr["velocity"]
+    tone_mapping(g, fr["history_color"][q], ae, fr["output"], fr.get("output_format"))
+    return q

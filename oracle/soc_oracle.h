@@ -1,0 +1,54 @@
+/*
+ * soc_oracle.h — CPU restatement ("oracle") of the reference's screen-space passes.
+ *
+ * TEST INFRASTRUCTURE ONLY. Nothing in the product path (soc_real_time_renderer_amd/) may link,
+ * load or call this code. Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use
+ * it, as the checker and as the timed CPU baseline.
+ *
+ * Parity status: the reference (Vulkan/GLSL via Daxa) cannot be built or run here
+ * and ships no tests, golden vectors or fixtures. The restatement is therefore
+ * pinned by hand-derived known-answer tests of the reference formulas (tests/test_oracle_kat.py)
+ * and by an independent numpy restatement (tools/np_oracle.py) — "parity unpinned" against a run
+ * of the reference itself.
+ *
+ * Functions take the same arguments as the C ABI in include/soc_rt.h, with HOST pointers.
+ */
+#ifndef SOC_ORACLE_H
+#define SOC_ORACLE_H
+
+#include "../include/soc_rt.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int soc_oracle_bloom_downsample(const soc_globals* g, soc_img higher_mip, soc_img lower_mip);
+int soc_oracle_bloom_upsample(const soc_globals* g, soc_img lower_mip, soc_img higher_mip);
+int soc_oracle_ssao_generation(const soc_globals* g, soc_img depth, soc_img normal, soc_img target);
+int soc_oracle_ssao_blur(const soc_globals* g, soc_img ssao, soc_img target);
+int soc_oracle_cloud_rendering(const soc_globals* g, soc_img depth, soc_img noise, soc_img target);
+int soc_oracle_composition(const soc_globals* g, soc_img target, soc_img albedo, soc_img emissive,
+                           soc_img normal, soc_img depth, soc_img ssao, soc_img shadow, soc_img clouds);
+int soc_oracle_generate_luminance_histogram(const soc_globals* g, soc_img hdr, soc_auto_exposure* ae);
+int soc_oracle_resolve_luminance_histogram(const soc_globals* g, soc_auto_exposure* ae,
+                                           uint64_t total_pixels, int32_t wide_accumulator);
+int soc_oracle_temporal_antialiasing(const soc_globals* g, soc_img target, soc_img current_color,
+                                     soc_img previous_color, soc_img current_velocity,
+                                     soc_img previous_velocity, soc_img depth);
+int soc_oracle_tone_mapping(const soc_globals* g, soc_img color, const soc_auto_exposure* ae, soc_img target);
+
+/* Scalar helpers exposed for known-answer tests. */
+uint32_t soc_oracle_luminance_bin(float r, float g, float b, float log_min, float log_max);
+float soc_oracle_log2(float x);
+uint16_t soc_oracle_f32_to_f16(float x);
+float soc_oracle_f16_to_f32(uint16_t h);
+/* Per-sky-pixel operation tallies of the clouds pass (filled by the last soc_oracle_cloud_rendering
+ * call with counting enabled): [0]=sky pixels, [1]=cloud-march steps with density, [2]=get_clouds
+ * evaluations, [3]=noise taps. */
+void soc_oracle_clouds_counters(uint64_t out[4]);
+int soc_oracle_num_threads(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

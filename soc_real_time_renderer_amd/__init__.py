@@ -1,0 +1,320 @@
+"""MI355X-native screen-space deferred shading + post-processing for lukasino1214/soc_real_time_renderer.
+
+The product path is the HIP pass library ``lib/libsoc_rt.so`` (C ABI: ``include/soc_rt.h``), built for
+gfx950 by ``__graft_entry__.build()``. This module is a thin host binding over that ABI: torch provides
+device memory and streams; every pass runs in the library. There is no CPU fallback — if the library
+is missing, importing the pass functions raises.
+
+Pass functions mirror the reference's task structs (src/graphics/tasks/*.inl); see include/soc_rt.h
+for the file:line each replaces.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional
+
+import numpy as np
+import torch  # noqa: F401  (loads the HIP runtime first: libsoc_rt.so then shares it)
+
+from . import _abi
+from ._abi import (FMT_D32F, FMT_R8_UNORM, FMT_RGBA8_SRGB, FMT_RGBA8_UNORM, FMT_RGBA16F, FMT_RGBA32F,
+                   PHASE_ALL, PHASE_POST_EXPOSURE, PHASE_PRE_EXPOSURE, AutoExposure, Camera, FrameImages, Globals,
+                   SocImg)
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libsoc_rt.so")
+
+__all__ = ["SocError", "lib", "img", "Globals", "Camera", "AutoExposure", "globals_defaults", "frame_update",
+           "bloom_downsample", "bloom_upsample", "bloom_chain", "ssao_prepare_noise", "ssao_generation",
+           "ssao_blur", "cloud_rendering", "composition", "generate_luminance_histogram",
+           "resolve_luminance_histogram", "temporal_antialiasing", "copy_image", "tone_mapping", "upload_globals",
+           "Renderer", "FMT_RGBA16F", "FMT_D32F", "FMT_R8_UNORM", "FMT_RGBA8_UNORM", "FMT_RGBA8_SRGB",
+           "FMT_RGBA32F", "PHASE_PRE_EXPOSURE", "PHASE_POST_EXPOSURE", "PHASE_ALL"]
+
+
+class SocError(RuntimeError):
+    def __init__(self, rc: int, msg: str):
+        super().__init__(f"[soc rc={rc}] {msg}")
+        self.rc = rc
+
+
+_LIB: Optional[C.CDLL] = None
+
+
+def lib() -> C.CDLL:
+    """The HIP pass library; raises if it has not been built (no fallback path exists)."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        l = C.CDLL(LIB_PATH)
+        _abi.bind(l, _abi.FUNCTIONS)
+        _abi.bind(l, _abi.DEBUG_FUNCTIONS)
+        _LIB = l
+    return _LIB
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise SocError(rc, f"{what}: {lib().soc_last_error_string().decode(errors='replace')}")
+
+
+# ------------------------------------------------------------------------------------------------
+# images
+# ------------------------------------------------------------------------------------------------
+def infer_format(shape, dtype) -> int:
+    nd = len(shape)
+    if dtype in (torch.float16, np.float16) and nd == 3 and shape[2] == 4:
+        return FMT_RGBA16F
+    if dtype in (torch.float32, np.float32) and nd == 2:
+        return FMT_D32F
+    if dtype in (torch.float32, np.float32) and nd == 3 and shape[2] == 4:
+        return FMT_RGBA32F
+    if dtype in (torch.uint8, np.uint8) and nd == 2:
+        return FMT_R8_UNORM
+    if dtype in (torch.uint8, np.uint8) and nd == 3 and shape[2] == 4:
+        return FMT_RGBA8_UNORM
+    raise ValueError(f"cannot infer image format for shape {tuple(shape)} dtype {dtype}")
+
+
+def img(t, fmt: Optional[int] = None) -> SocImg:
+    """soc_img view of an (H, W[, 4]) torch tensor (device or host) or numpy array; rows may be padded."""
+    if t is None:
+        return SocImg(None, 0, 0, 0, 0)
+    if isinstance(t, torch.Tensor):
+        f = fmt or infer_format(tuple(t.shape), t.dtype)
+        if t.dim() == 3 and t.stride(2) != 1 or t.stride(1) != (t.shape[2] if t.dim() == 3 else 1):
+            raise ValueError("image tensor must have contiguous pixels (only the row stride may be padded)")
+        pitch = t.stride(0) * t.element_size()
+        return SocImg(t.data_ptr(), int(t.shape[1]), int(t.shape[0]), int(pitch), f)
+    a = t
+    f = fmt or infer_format(a.shape, a.dtype.type)
+    if not a.flags["C_CONTIGUOUS"] and a.strides[1] != a.itemsize * (a.shape[2] if a.ndim == 3 else 1):
+        raise ValueError("numpy image must have contiguous pixels")
+    return SocImg(a.ctypes.data, int(a.shape[1]), int(a.shape[0]), int(a.strides[0]), f)
+
+
+def _stream(stream) -> Optional[int]:
+    if stream is None:
+        return torch.cuda.current_stream().cuda_stream
+    if isinstance(stream, torch.cuda.Stream):
+        return stream.cuda_stream
+    return int(stream)
+
+
+def _gp(g: Globals):
+    return C.byref(g)
+
+
+def _ptr(t) -> Optional[int]:
+    if t is None:
+        return None
+    if isinstance(t, torch.Tensor):
+        return t.data_ptr()
+    return int(t)
+
+
+# ------------------------------------------------------------------------------------------------
+# globals feed
+# ------------------------------------------------------------------------------------------------
+def globals_defaults(width: int, height: int) -> Globals:
+    """Renderer defaults (renderer.cpp:72-133) for a width x height frame."""
+    g = Globals()
+    _check(lib().soc_globals_init_defaults(C.byref(g), width, height), "soc_globals_init_defaults")
+    return g
+
+
+def make_camera(position, rotation=(0.0, 0.0, 0.0), fov=90.0, near=0.1, far=1000.0) -> Camera:
+    c = Camera()
+    c.position[:] = [float(v) for v in position]
+    c.rotation[:] = [float(v) for v in rotation]
+    c.fov_degrees, c.near_clip, c.far_clip = fov, near, far
+    return c
+
+
+def frame_update(g: Globals, camera: Camera, width: int, height: int, delta_time: float, jitter_index: C.c_uint32) -> None:
+    """One Application::update() (application.cpp:109-165)."""
+    _check(lib().soc_globals_frame_update(C.byref(g), C.byref(camera), width, height, delta_time, C.byref(jitter_index)),
+           "soc_globals_frame_update")
+
+
+def auto_exposure_buffer(device="cuda", exposure: float = 0.0) -> torch.Tensor:
+    """Device AutoExposure block (shared.inl:39-45) as 257 int32 words: [exposure f32 bits, 256 bins]."""
+    t = torch.zeros(1 + _abi.BIN_COUNT, dtype=torch.int32, device=device)
+    t[0] = int(np.array([exposure], dtype=np.float32).view(np.int32)[0])
+    return t
+
+
+def exposure_of(ae: torch.Tensor) -> float:
+    return float(ae[0:1].cpu().view(torch.float32).item())
+
+
+# ------------------------------------------------------------------------------------------------
+# passes (one per reference task; see include/soc_rt.h)
+# ------------------------------------------------------------------------------------------------
+def bloom_downsample(g, higher_mip, lower_mip, stream=None):
+    _check(lib().soc_bloom_downsample(_gp(g), img(higher_mip), img(lower_mip), _stream(stream)), "bloom_downsample")
+
+
+def bloom_upsample(g, lower_mip, higher_mip, stream=None):
+    _check(lib().soc_bloom_upsample(_gp(g), img(lower_mip), img(higher_mip), _stream(stream)), "bloom_upsample")
+
+
+def bloom_chain(g, emissive, mips, stream=None):
+    arr = (SocImg * len(mips))(*[img(m) for m in mips])
+    _check(lib().soc_bloom_chain(_gp(g), img(emissive), arr, len(mips), _stream(stream)), "bloom_chain")
+
+
+def ssao_prepare_noise(normal, target, table, stream=None):
+    _check(lib().soc_ssao_prepare_noise(img(normal), img(target), _ptr(table), _stream(stream)), "ssao_prepare_noise")
+
+
+def ssao_generation(g, depth, normal, target, noise_table=None, stream=None):
+    _check(lib().soc_ssao_generation(_gp(g), img(depth), img(normal), img(target), _ptr(noise_table), _stream(stream)),
+           "ssao_generation")
+
+
+def ssao_blur(g, ssao, target, stream=None):
+    _check(lib().soc_ssao_blur(_gp(g), img(ssao), img(target), _stream(stream)), "ssao_blur")
+
+
+def cloud_rendering(g, depth, noise, target, stream=None):
+    _check(lib().soc_cloud_rendering(_gp(g), img(depth), img(noise), img(target), _stream(stream)), "cloud_rendering")
+
+
+def composition(g, target, albedo, emissive, normal, depth, ssao, shadow, clouds, d_globals=None, stream=None):
+    _check(lib().soc_composition(_gp(g), _ptr(d_globals), img(target), img(albedo), img(emissive), img(normal),
+                                 img(depth), img(ssao), img(shadow), img(clouds), _stream(stream)), "composition")
+
+
+def generate_luminance_histogram(g, hdr, auto_exposure, stream=None):
+    _check(lib().soc_generate_luminance_histogram(_gp(g), img(hdr), _ptr(auto_exposure), _stream(stream)),
+           "generate_luminance_histogram")
+
+
+def resolve_luminance_histogram(g, auto_exposure, total_pixels=0, wide=False, stream=None):
+    _check(lib().soc_resolve_luminance_histogram(_gp(g), _ptr(auto_exposure), int(total_pixels), int(bool(wide)),
+                                                 _stream(stream)), "resolve_luminance_histogram")
+
+
+def temporal_antialiasing(g, target, current_color, previous_color, current_velocity, previous_velocity, depth,
+                          velocity_history_out=None, stream=None):
+    _check(lib().soc_temporal_antialiasing(_gp(g), img(target), img(current_color), img(previous_color),
+                                           img(current_velocity), img(previous_velocity), img(depth),
+                                           img(velocity_history_out), _stream(stream)), "temporal_antialiasing")
+
+
+def copy_image(target, source, stream=None):
+    _check(lib().soc_copy_image(img(target), img(source), _stream(stream)), "copy_image")
+
+
+def tone_mapping(g, color, auto_exposure, target, target_format=None, stream=None):
+    _check(lib().soc_tone_mapping(_gp(g), img(color), _ptr(auto_exposure), img(target, target_format),
+                                  _stream(stream)), "tone_mapping")
+
+
+def upload_globals(g, d_globals, stream=None):
+    _check(lib().soc_upload_globals(_gp(g), _ptr(d_globals), _stream(stream)), "upload_globals")
+
+
+def globals_device_buffer(device="cuda") -> torch.Tensor:
+    return torch.zeros(C.sizeof(Globals), dtype=torch.uint8, device=device)
+
+
+# ------------------------------------------------------------------------------------------------
+# render graph
+# ------------------------------------------------------------------------------------------------
+def alloc_frame(width: int, height: int, device="cuda", output_format=FMT_RGBA8_UNORM, noise_table=True):
+    """Device images of one frame (renderer.cpp:310-513 formats/extents). G-buffer inputs included."""
+    W, H = width, height
+    hw, hh = W // 2, H // 2
+    f16 = dict(dtype=torch.float16, device=device)
+    t = {
+        "albedo": torch.zeros(H, W, 4, **f16), "emissive": torch.zeros(H, W, 4, **f16),
+        "normal": torch.zeros(H, W, 4, **f16), "depth": torch.ones(H, W, dtype=torch.float32, device=device),
+        "velocity": torch.zeros(H, W, 4, **f16),
+        "shadow": torch.ones(4096, 4096, dtype=torch.float32, device=device),
+        "noise": torch.zeros(64, 64, 4, dtype=torch.uint8, device=device),
+        "bloom_mips": [torch.zeros(max(H >> i, 1), max(W >> i, 1), 4, **f16) for i in range(4)],
+        "ssao": torch.zeros(hh, hw, dtype=torch.uint8, device=device),
+        "ssao_blur": torch.zeros(hh, hw, dtype=torch.uint8, device=device),
+        "clouds": torch.zeros(H, W, 4, dtype=torch.uint8, device=device),
+        "color": torch.zeros(H, W, 4, **f16),
+        "history_color": [torch.zeros(H, W, 4, **f16) for _ in range(2)],
+        "history_velocity": [torch.zeros(H, W, 4, **f16) for _ in range(2)],
+        "auto_exposure": auto_exposure_buffer(device),
+        "d_globals": globals_device_buffer(device),
+    }
+    if output_format in (FMT_RGBA8_UNORM, FMT_RGBA8_SRGB):
+        t["output"] = torch.zeros(H, W, 4, dtype=torch.uint8, device=device)
+    elif output_format == FMT_RGBA16F:
+        t["output"] = torch.zeros(H, W, 4, **f16)
+    else:
+        t["output"] = torch.zeros(H, W, 4, dtype=torch.float32, device=device)
+    t["output_format"] = output_format
+    t["ssao_noise_table"] = torch.zeros(hh * hw * 2, dtype=torch.float32, device=device) if noise_table else None
+    return t
+
+
+class Renderer:
+    """Host render graph (C++ soc_renderer): the live passes of Renderer::rebuild_task_graph in order."""
+
+    def __init__(self, frame: dict, timing: bool = False, stream=None):
+        self.frame = frame
+        fi = FrameImages()
+        for k in ("albedo", "emissive", "normal", "depth", "velocity", "shadow", "noise", "ssao", "ssao_blur", "clouds",
+                  "color"):
+            setattr(fi, k, img(frame[k]))
+        for i in range(4):
+            fi.bloom_mips[i] = img(frame["bloom_mips"][i])
+        for i in range(2):
+            fi.history_color[i] = img(frame["history_color"][i])
+            fi.history_velocity[i] = img(frame["history_velocity"][i])
+        fi.output = img(frame["output"], frame.get("output_format"))
+        fi.ssao_noise_table = _ptr(frame.get("ssao_noise_table"))
+        fi.auto_exposure = _ptr(frame["auto_exposure"])
+        fi.d_globals = _ptr(frame.get("d_globals"))
+        self._fi = fi
+        h = lib().soc_renderer_create(C.byref(fi), _abi.RENDERER_TIMING if timing else 0)
+        if not h:
+            raise SocError(-1, lib().soc_last_error_string().decode())
+        self.handle = h
+        if frame.get("ssao_noise_table") is not None:
+            ssao_prepare_noise(frame["normal"], frame["ssao"], frame["ssao_noise_table"], stream)
+
+    def execute(self, g: Globals, phase: int = PHASE_ALL, stream=None) -> None:
+        _check(lib().soc_renderer_execute(self.handle, _gp(g), phase, _stream(stream)), "soc_renderer_execute")
+
+    def set_exposure_pixels(self, total_pixels: int, wide: bool) -> None:
+        _check(lib().soc_renderer_set_exposure_pixels(self.handle, int(total_pixels), int(bool(wide))),
+               "soc_renderer_set_exposure_pixels")
+
+    def pass_names(self):
+        n = lib().soc_renderer_pass_count(self.handle)
+        return [lib().soc_renderer_pass_name(self.handle, i).decode() for i in range(n)]
+
+    def pass_groups(self):
+        n = lib().soc_renderer_pass_count(self.handle)
+        return [lib().soc_renderer_pass_group(self.handle, i).decode() for i in range(n)]
+
+    def pass_ms(self):
+        n = lib().soc_renderer_pass_count(self.handle)
+        return [float(lib().soc_renderer_pass_ms(self.handle, i)) for i in range(n)]
+
+    def current_history(self) -> int:
+        return int(lib().soc_renderer_current_history(self.handle))
+
+    def resolved(self) -> torch.Tensor:
+        return self.frame["history_color"][self.current_history()]
+
+    def close(self):
+        if getattr(self, "handle", None):
+            lib().soc_renderer_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,245 @@
+// bloom.hip — BloomDownsampleTask / BloomUpsampleTask (src/graphics/tasks/bloom_downsample.inl:107-141,
+// bloom_upsample.inl:98-127) as gfx950 kernels.
+//
+// Every tap is a bilinear sample under the sampling contract. The 8-bit fixed-point tap coordinate
+// `fx` is either derived from the float uv exactly as the oracle does (generic path) or, for the
+// exact 1:1, 2:1 and 1:2 size ratios the reference's mip chain uses (renderer.cpp:492-513), written
+// down analytically (fast paths); both then go through the same clamp rule and lerp arithmetic, so
+// the fast paths are bit-identical to the generic one (extents <= 8192).
+// All tap weights are powers of two, so the RGBA16F results are bit-identical to the oracle's.
+#include "soc_internal.hpp"
+
+namespace soc {
+
+namespace {
+
+constexpr int BX = 64, BY = 4;
+
+// Clamp rule of the sampling contract applied to an 8-bit fixed-point texel coordinate.
+__device__ __forceinline__ Axis axis_from_fixed(int fx, int n) {
+    int i = fx >> 8;
+    float w = (float)(fx & 255) * (1.0f / 256.0f);
+    if (i < 0) { i = 0; w = 0.0f; }
+    else if (i >= n - 1) { i = n - 2; w = 1.0f; }
+    if (n == 1) { i = 0; w = 0.0f; }
+    Axis a;
+    a.i0 = i;
+    a.i1 = min(i + 1, n - 1);
+    a.w = w;
+    return a;
+}
+
+// Float-uv -> fixed coordinate, identical arithmetic to axis_clamp / the oracle.
+__device__ __forceinline__ int fixed_from_uv(float u, int n) {
+#pragma clang fp contract(off)
+    float t = u * (float)n;
+    t = t - 0.5f;
+    t = fminf(fmaxf(t, -2.0f), (float)n + 1.0f);
+    return (int)floorf(t * 256.0f + 0.5f);
+}
+
+__device__ __forceinline__ f3 tap(const DImg& im, const Axis& ax, const Axis& ay) {
+    const uint2* r0 = row_ptr<uint2>(im, ay.i0);
+    const uint2* r1 = row_ptr<uint2>(im, ay.i1);
+    f4 a = unpack_h4(r0[ax.i0]), b = unpack_h4(r0[ax.i1]), c = unpack_h4(r1[ax.i0]), d = unpack_h4(r1[ax.i1]);
+    return f3{bilerp1(a.x, b.x, c.x, d.x, ax.w, ay.w), bilerp1(a.y, b.y, c.y, d.y, ax.w, ay.w),
+              bilerp1(a.z, b.z, c.z, d.z, ax.w, ay.w)};
+}
+
+// Exact texel at clamped integer coordinates (a tap whose weights are 0/1).
+__device__ __forceinline__ f3 point(const DImg& im, int x, int y) {
+    x = min(max(x, 0), im.w - 1);
+    y = min(max(y, 0), im.h - 1);
+    f4 v = fetch_h4(im, x, y);
+    return f3{v.x, v.y, v.z};
+}
+
+__device__ __forceinline__ void store_rgb1(const DImg& im, int x, int y, f3 c) {
+    row_ptr_w<uint2>(im, y)[x] = pack_h4(f4{c.x, c.y, c.z, 1.0f});
+}
+
+// out = e*0.125 + (a+c+g+i)*0.03125 + (b+d+f+h)*0.0625 + (j+k+l+m)*0.125   (:137-140)
+__device__ __forceinline__ float down13(float a, float b, float c, float d, float e, float f, float g, float h, float i,
+                                        float j, float k, float l, float m) {
+    float r = e * 0.125f;
+    r += (a + c + g + i) * 0.03125f;
+    r += (b + d + f + h) * 0.0625f;
+    r += (j + k + l + m) * 0.125f;
+    return r;
+}
+
+// out = (e*4 + (b+d+f+h)*2 + (a+c+g+i)) / 16   (bloom_upsample.inl:122-125)
+__device__ __forceinline__ float up9(float a, float b, float c, float d, float e, float f, float g, float h, float i) {
+    float r = e * 4.0f;
+    r += (b + d + f + h) * 2.0f;
+    r += (a + c + g + i);
+    r *= 1.0f / 16.0f;
+    return r;
+}
+
+#define SOC_DOWN13(A, B, C, D, E, F, G, H, I, J, K, L, M)                                                   \
+    f3{down13(A.x, B.x, C.x, D.x, E.x, F.x, G.x, H.x, I.x, J.x, K.x, L.x, M.x),                           \
+       down13(A.y, B.y, C.y, D.y, E.y, F.y, G.y, H.y, I.y, J.y, K.y, L.y, M.y),                           \
+       down13(A.z, B.z, C.z, D.z, E.z, F.z, G.z, H.z, I.z, J.z, K.z, L.z, M.z)}
+#define SOC_UP9(A, B, C, D, E, F, G, H, I)                                                                  \
+    f3{up9(A.x, B.x, C.x, D.x, E.x, F.x, G.x, H.x, I.x), up9(A.y, B.y, C.y, D.y, E.y, F.y, G.y, H.y, I.y), \
+       up9(A.z, B.z, C.z, D.z, E.z, F.z, G.z, H.z, I.z)}
+
+// ------------------------------------------------------------------------------------------------
+// downsample
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void bloom_down_generic(DImg src, DImg dst, float sxt, float syt) {
+    const int x = blockIdx.x * BX + threadIdx.x, y = blockIdx.y * BY + threadIdx.y;
+    if (x >= dst.w || y >= dst.h) return;
+    const float u = centre_uv(x, dst.w), v = centre_uv(y, dst.h);
+    const float X = sxt, Y = syt;
+    auto S = [&](float uu, float vv) {
+        return tap(src, axis_from_fixed(fixed_from_uv(uu, src.w), src.w), axis_from_fixed(fixed_from_uv(vv, src.h), src.h));
+    };
+    f3 a = S(u - 2 * X, v + 2 * Y), b = S(u, v + 2 * Y), c = S(u + 2 * X, v + 2 * Y);
+    f3 d = S(u - 2 * X, v), e = S(u, v), f = S(u + 2 * X, v);
+    f3 g = S(u - 2 * X, v - 2 * Y), h = S(u, v - 2 * Y), i = S(u + 2 * X, v - 2 * Y);
+    f3 j = S(u - X, v + Y), k = S(u + X, v + Y), l = S(u - X, v - Y), m = S(u + X, v - Y);
+    store_rgb1(dst, x, y, SOC_DOWN13(a, b, c, d, e, f, g, h, i, j, k, l, m));
+}
+
+// src and dst have the same extent: every tap lands on a texel centre (weights 0/1).
+__global__ __launch_bounds__(256) void bloom_down_same(DImg src, DImg dst) {
+    const int x = blockIdx.x * BX + threadIdx.x, y = blockIdx.y * BY + threadIdx.y;
+    if (x >= dst.w || y >= dst.h) return;
+    // uv.y + 2*texel is the row BELOW (y grows downward in texel space as uv.y grows).
+    f3 a = point(src, x - 2, y + 2), b = point(src, x, y + 2), c = point(src, x + 2, y + 2);
+    f3 d = point(src, x - 2, y), e = point(src, x, y), f = point(src, x + 2, y);
+    f3 g = point(src, x - 2, y - 2), h = point(src, x, y - 2), i = point(src, x + 2, y - 2);
+    f3 j = point(src, x - 1, y + 1), k = point(src, x + 1, y + 1), l = point(src, x - 1, y - 1), m = point(src, x + 1, y - 1);
+    store_rgb1(dst, x, y, SOC_DOWN13(a, b, c, d, e, f, g, h, i, j, k, l, m));
+}
+
+// src is exactly twice dst: every tap is the w = 0.5 blend of a 2x2 block starting at 2x + k.
+__global__ __launch_bounds__(256) void bloom_down_half(DImg src, DImg dst) {
+    const int x = blockIdx.x * BX + threadIdx.x, y = blockIdx.y * BY + threadIdx.y;
+    if (x >= dst.w || y >= dst.h) return;
+    auto AX = [&](int k) { return axis_from_fixed(256 * (2 * x + k) + 128, src.w); };
+    auto AY = [&](int k) { return axis_from_fixed(256 * (2 * y + k) + 128, src.h); };
+    const Axis xm2 = AX(-2), xm1 = AX(-1), x0 = AX(0), xp1 = AX(1), xp2 = AX(2);
+    const Axis ym2 = AY(-2), ym1 = AY(-1), y0 = AY(0), yp1 = AY(1), yp2 = AY(2);
+    f3 a = tap(src, xm2, yp2), b = tap(src, x0, yp2), c = tap(src, xp2, yp2);
+    f3 d = tap(src, xm2, y0), e = tap(src, x0, y0), f = tap(src, xp2, y0);
+    f3 g = tap(src, xm2, ym2), h = tap(src, x0, ym2), i = tap(src, xp2, ym2);
+    f3 j = tap(src, xm1, yp1), k = tap(src, xp1, yp1), l = tap(src, xm1, ym1), m = tap(src, xp1, ym1);
+    store_rgb1(dst, x, y, SOC_DOWN13(a, b, c, d, e, f, g, h, i, j, k, l, m));
+}
+
+// ------------------------------------------------------------------------------------------------
+// upsample (result overwrites the destination: quirk Q5)
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void bloom_up_generic(DImg src, DImg dst, float X, float Y) {
+    const int x = blockIdx.x * BX + threadIdx.x, y = blockIdx.y * BY + threadIdx.y;
+    if (x >= dst.w || y >= dst.h) return;
+    const float u = centre_uv(x, dst.w), v = centre_uv(y, dst.h);
+    auto S = [&](float uu, float vv) {
+        return tap(src, axis_from_fixed(fixed_from_uv(uu, src.w), src.w), axis_from_fixed(fixed_from_uv(vv, src.h), src.h));
+    };
+    f3 a = S(u - X, v + Y), b = S(u, v + Y), c = S(u + X, v + Y);
+    f3 d = S(u - X, v), e = S(u, v), f = S(u + X, v);
+    f3 g = S(u - X, v - Y), h = S(u, v - Y), i = S(u + X, v - Y);
+    store_rgb1(dst, x, y, SOC_UP9(a, b, c, d, e, f, g, h, i));
+}
+
+__global__ __launch_bounds__(256) void bloom_up_same(DImg src, DImg dst) {
+    const int x = blockIdx.x * BX + threadIdx.x, y = blockIdx.y * BY + threadIdx.y;
+    if (x >= dst.w || y >= dst.h) return;
+    f3 a = point(src, x - 1, y + 1), b = point(src, x, y + 1), c = point(src, x + 1, y + 1);
+    f3 d = point(src, x - 1, y), e = point(src, x, y), f = point(src, x + 1, y);
+    f3 g = point(src, x - 1, y - 1), h = point(src, x, y - 1), i = point(src, x + 1, y - 1);
+    store_rgb1(dst, x, y, SOC_UP9(a, b, c, d, e, f, g, h, i));
+}
+
+// dst is exactly twice src: the lower-mip coordinate of tap k is X/2 - 0.25 + k (weights 3/4, 1/4).
+__global__ __launch_bounds__(256) void bloom_up_double(DImg src, DImg dst) {
+    const int x = blockIdx.x * BX + threadIdx.x, y = blockIdx.y * BY + threadIdx.y;
+    if (x >= dst.w || y >= dst.h) return;
+    auto AX = [&](int k) { return axis_from_fixed(128 * x - 64 + 256 * k, src.w); };
+    auto AY = [&](int k) { return axis_from_fixed(128 * y - 64 + 256 * k, src.h); };
+    const Axis xm = AX(-1), x0 = AX(0), xp = AX(1), ym = AY(-1), y0 = AY(0), yp = AY(1);
+    f3 a = tap(src, xm, yp), b = tap(src, x0, yp), c = tap(src, xp, yp);
+    f3 d = tap(src, xm, y0), e = tap(src, x0, y0), f = tap(src, xp, y0);
+    f3 g = tap(src, xm, ym), h = tap(src, x0, ym), i = tap(src, xp, ym);
+    store_rgb1(dst, x, y, SOC_UP9(a, b, c, d, e, f, g, h, i));
+}
+
+constexpr int kFastMax = 8192;
+
+}  // namespace
+
+int launch_bloom_down(const soc_img& hi, const soc_img& lo, hipStream_t s, int force_generic) {
+    dim3 blk(BX, BY), grd(ceil_div(lo.width, BX), ceil_div(lo.height, BY));
+    DImg src = dimg(hi), dst = dimg(lo);
+    const bool small = hi.width <= kFastMax && hi.height <= kFastMax;
+    if (!force_generic && small && hi.width == lo.width && hi.height == lo.height) {
+        bloom_down_same<<<grd, blk, 0, s>>>(src, dst);
+    } else if (!force_generic && small && hi.width == 2 * lo.width && hi.height == 2 * lo.height) {
+        bloom_down_half<<<grd, blk, 0, s>>>(src, dst);
+    } else {
+        bloom_down_generic<<<grd, blk, 0, s>>>(src, dst, 1.0f / (float)hi.width, 1.0f / (float)hi.height);
+    }
+    return check_launch("bloom_downsample");
+}
+
+int launch_bloom_up(const soc_img& lo, const soc_img& hi, hipStream_t s, int force_generic) {
+    dim3 blk(BX, BY), grd(ceil_div(hi.width, BX), ceil_div(hi.height, BY));
+    DImg src = dimg(lo), dst = dimg(hi);
+    const bool small = hi.width <= kFastMax && hi.height <= kFastMax;
+    if (!force_generic && small && hi.width == lo.width && hi.height == lo.height) {
+        bloom_up_same<<<grd, blk, 0, s>>>(src, dst);
+    } else if (!force_generic && small && hi.width == 2 * lo.width && hi.height == 2 * lo.height) {
+        bloom_up_double<<<grd, blk, 0, s>>>(src, dst);
+    } else {
+        bloom_up_generic<<<grd, blk, 0, s>>>(src, dst, 1.0f / (float)lo.width, 1.0f / (float)lo.height);
+    }
+    return check_launch("bloom_upsample");
+}
+
+}  // namespace soc
+
+using namespace soc;
+
+static int bloom_args(const soc_img& a, const soc_img& b, const char* pass) {
+    int rc = check_img(a, SOC_FMT_RGBA16F, pass, "source");
+    if (rc) return rc;
+    rc = check_img(b, SOC_FMT_RGBA16F, pass, "target");
+    if (rc) return rc;
+    if (a.data == b.data) return set_error(SOC_E_INVALID_ARG, "%s: source and target alias", pass);
+    return SOC_OK;
+}
+
+extern "C" int soc_bloom_downsample(const soc_globals* g, soc_img higher_mip, soc_img lower_mip, soc_stream stream) {
+    (void)g;
+    int rc = bloom_args(higher_mip, lower_mip, "soc_bloom_downsample");
+    if (rc) return rc;
+    return launch_bloom_down(higher_mip, lower_mip, hs(stream), 0);
+}
+
+extern "C" int soc_bloom_upsample(const soc_globals* g, soc_img lower_mip, soc_img higher_mip, soc_stream stream) {
+    (void)g;
+    int rc = bloom_args(lower_mip, higher_mip, "soc_bloom_upsample");
+    if (rc) return rc;
+    return launch_bloom_up(lower_mip, higher_mip, hs(stream), 0);
+}
+
+// Test hook: force the generic (float-uv) tap path to cross-check the fast paths.
+extern "C" int soc_debug_bloom_generic(int32_t up, soc_img a, soc_img b, soc_stream stream) {
+    int rc = bloom_args(a, b, "soc_debug_bloom_generic");
+    if (rc) return rc;
+    return up ? launch_bloom_up(a, b, hs(stream), 1) : launch_bloom_down(a, b, hs(stream), 1);
+}
+
+extern "C" int soc_bloom_chain(const soc_globals* g, soc_img emissive, const soc_img* mips, int32_t mip_count,
+                               soc_stream stream) {
+    if (!mips || mip_count < 1) return set_error(SOC_E_INVALID_ARG, "soc_bloom_chain: need >= 1 mip");
+    int rc = soc_bloom_downsample(g, emissive, mips[0], stream);
+    for (int i = 0; !rc && i < mip_count - 1; ++i) rc = soc_bloom_downsample(g, mips[i], mips[i + 1], stream);
+    for (int i = mip_count - 1; !rc && i > 0; --i) rc = soc_bloom_upsample(g, mips[i], mips[i - 1], stream);
+    if (!rc) rc = soc_bloom_upsample(g, mips[0], emissive, stream);
+    return rc;
+}

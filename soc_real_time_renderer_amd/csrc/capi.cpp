@@ -1,0 +1,640 @@
+// capi.cpp — host side of the C ABI: errors, ABI introspection, the globals feed (glm / camera / jitter
+// restatements of application.cpp, camera.cpp and renderer.cpp), and the render graph that orders the
+// passes as Renderer::rebuild_task_graph does (renderer.cpp:929-1235).
+//
+// Compiled with -ffp-contract=off: the host fp32 math (AgX matrices, sun view-projection, glm
+// restatements) performs exactly the roundings the oracle's C performs.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "soc_internal.hpp"
+
+namespace soc {
+
+static thread_local std::string t_error;
+
+int set_error(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    t_error = buf;
+    return code;
+}
+
+void clear_error() { t_error.clear(); }
+
+int check_img(const soc_img& im, int fmt, const char* pass, const char* what) {
+    if (!img_ok(im))
+        return set_error(SOC_E_INVALID_ARG, "%s: %s image invalid (data=%p %dx%d pitch=%d fmt=%d)", pass, what, im.data,
+                         im.width, im.height, im.pitch_bytes, im.format);
+    if (fmt > 0 && im.format != fmt)
+        return set_error(SOC_E_INVALID_ARG, "%s: %s image has format %d, expected %d", pass, what, im.format, fmt);
+    return SOC_OK;
+}
+
+int check_launch(const char* pass) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return set_error(SOC_E_HIP, "%s: kernel launch failed: %s", pass, hipGetErrorString(e));
+    return SOC_OK;
+}
+
+void mat4_mul_host(float out[16], const float a[16], const float b[16]) {
+    float t[16];
+    for (int c = 0; c < 4; ++c)
+        for (int r = 0; r < 4; ++r)
+            t[c * 4 + r] = a[0 * 4 + r] * b[c * 4 + 0] + a[1 * 4 + r] * b[c * 4 + 1] + a[2 * 4 + r] * b[c * 4 + 2] +
+                           a[3 * 4 + r] * b[c * 4 + 3];
+    std::memcpy(out, t, sizeof t);
+}
+
+// ---- AgX matrices (tone_mapping.inl:103-163), fp32, same operation order as the shader ----------
+namespace {
+struct H3 { float x, y, z; };
+struct H2 { float x, y; };
+
+void mat3_mul(float* out, const float* a, const float* b) {
+    float t[9];
+    for (int c = 0; c < 3; ++c)
+        for (int r = 0; r < 3; ++r) t[c * 3 + r] = a[0 * 3 + r] * b[c * 3 + 0] + a[1 * 3 + r] * b[c * 3 + 1] + a[2 * 3 + r] * b[c * 3 + 2];
+    std::memcpy(out, t, sizeof t);
+}
+void mat3_inverse(float* o, const float* m) {
+#define M(c, r) m[(c) * 3 + (r)]
+    float det = M(0, 0) * (M(1, 1) * M(2, 2) - M(2, 1) * M(1, 2)) - M(1, 0) * (M(0, 1) * M(2, 2) - M(2, 1) * M(0, 2)) +
+                M(2, 0) * (M(0, 1) * M(1, 2) - M(1, 1) * M(0, 2));
+    float od = 1.0f / det;
+    float t[9];
+    t[0 * 3 + 0] = +(M(1, 1) * M(2, 2) - M(2, 1) * M(1, 2)) * od;
+    t[1 * 3 + 0] = -(M(1, 0) * M(2, 2) - M(2, 0) * M(1, 2)) * od;
+    t[2 * 3 + 0] = +(M(1, 0) * M(2, 1) - M(2, 0) * M(1, 1)) * od;
+    t[0 * 3 + 1] = -(M(0, 1) * M(2, 2) - M(2, 1) * M(0, 2)) * od;
+    t[1 * 3 + 1] = +(M(0, 0) * M(2, 2) - M(2, 0) * M(0, 2)) * od;
+    t[2 * 3 + 1] = -(M(0, 0) * M(2, 1) - M(2, 0) * M(0, 1)) * od;
+    t[0 * 3 + 2] = +(M(0, 1) * M(1, 2) - M(1, 1) * M(0, 2)) * od;
+    t[1 * 3 + 2] = -(M(0, 0) * M(1, 2) - M(1, 0) * M(0, 2)) * od;
+    t[2 * 3 + 2] = +(M(0, 0) * M(1, 1) - M(1, 0) * M(0, 1)) * od;
+#undef M
+    std::memcpy(o, t, sizeof t);
+}
+H3 unproject(H2 xy) {  // xyYToXYZ(vec3(xy, 1))
+    float Y = 1.0f;
+    float X = (xy.x * Y) / xy.y;
+    float Z = ((1.0f - xy.x - xy.y) * Y) / xy.y;
+    return H3{X, Y, Z};
+}
+void primaries_to_matrix(float* out, H2 r, H2 g, H2 b, H2 w) {
+    H3 R = unproject(r), G = unproject(g), B = unproject(b), W = unproject(w);
+    float temp[9] = {R.x, 1.0f, R.z, G.x, 1.0f, G.z, B.x, 1.0f, B.z};
+    float it[9];
+    mat3_inverse(it, temp);
+    H3 s = H3{it[0] * W.x + it[3] * W.y + it[6] * W.z, it[1] * W.x + it[4] * W.y + it[7] * W.z,
+              it[2] * W.x + it[5] * W.y + it[8] * W.z};
+    float m[9] = {R.x * s.x, R.y * s.x, R.z * s.x, G.x * s.y, G.y * s.y, G.z * s.y, B.x * s.z, B.y * s.z, B.z * s.z};
+    std::memcpy(out, m, sizeof m);
+}
+H2 mix2(H2 a, H2 b, float t) { return H2{a.x * (1.0f - t) + b.x * t, a.y * (1.0f - t) + b.y * t}; }
+}  // namespace
+
+void agx_matrices(float compression, float M[9], float Minv[9]) {
+    const H2 xr{0.64f, 0.33f}, xg{0.3f, 0.6f}, xb{0.15f, 0.06f}, xw{0.3127f, 0.3290f};
+    float srgb_to_xyz[9], adjusted_to_xyz[9], xyz_to_adjusted[9];
+    primaries_to_matrix(srgb_to_xyz, xr, xg, xb, xw);
+    const float sf = 1.0f / (1.0f - compression);
+    primaries_to_matrix(adjusted_to_xyz, mix2(xw, xr, sf), mix2(xw, xg, sf), mix2(xw, xb, sf), xw);
+    mat3_inverse(xyz_to_adjusted, adjusted_to_xyz);
+    mat3_mul(M, srgb_to_xyz, xyz_to_adjusted);
+    mat3_inverse(Minv, M);
+}
+
+}  // namespace soc
+
+using namespace soc;
+
+// =================================================================================================
+// ABI introspection
+// =================================================================================================
+namespace {
+struct FieldInfo { const char* type; const char* field; size_t offset; };
+#define F(T, f) {#T, #f, offsetof(T, f)}
+const FieldInfo kFields[] = {
+    F(soc_img, data), F(soc_img, width), F(soc_img, height), F(soc_img, pitch_bytes), F(soc_img, format),
+    F(soc_auto_exposure, exposure), F(soc_auto_exposure, histogram_buckets),
+    F(soc_sun_info, projection_matrix), F(soc_sun_info, view_matrix), F(soc_sun_info, projection_view_matrix),
+    F(soc_sun_info, terrain_y_clip_trick), F(soc_sun_info, position), F(soc_sun_info, direction),
+    F(soc_sun_info, exponential_factor), F(soc_sun_info, darkening_factor), F(soc_sun_info, bias), F(soc_sun_info, intensity),
+    F(soc_point_light, position), F(soc_point_light, color), F(soc_point_light, intensity),
+    F(soc_spot_light, position), F(soc_spot_light, direction), F(soc_spot_light, color), F(soc_spot_light, intensity),
+    F(soc_spot_light, cut_off), F(soc_spot_light, outer_cut_off),
+    F(soc_camera, position), F(soc_camera, rotation), F(soc_camera, fov_degrees), F(soc_camera, near_clip), F(soc_camera, far_clip),
+    F(soc_globals, camera_projection_matrix), F(soc_globals, camera_inverse_projection_matrix),
+    F(soc_globals, camera_view_matrix), F(soc_globals, camera_inverse_view_matrix),
+    F(soc_globals, camera_projection_view_matrix), F(soc_globals, camera_inverse_projection_view_matrix),
+    F(soc_globals, camera_previous_projection_matrix), F(soc_globals, camera_previous_inverse_projection_matrix),
+    F(soc_globals, camera_previous_view_matrix), F(soc_globals, camera_previous_inverse_view_matrix),
+    F(soc_globals, camera_previous_projection_view_matrix), F(soc_globals, camera_previous_inverse_projection_view_matrix),
+    F(soc_globals, jitter), F(soc_globals, previous_jitter), F(soc_globals, camera_position), F(soc_globals, camera_near_clip),
+    F(soc_globals, camera_far_clip), F(soc_globals, resolution), F(soc_globals, elapsed_time), F(soc_globals, delta_time),
+    F(soc_globals, frame_counter), F(soc_globals, sun_info), F(soc_globals, point_light_count), F(soc_globals, spot_light_count),
+    F(soc_globals, point_lights), F(soc_globals, spot_lights), F(soc_globals, terrain_offset), F(soc_globals, terrain_scale),
+    F(soc_globals, terrain_height_scale), F(soc_globals, terrain_midpoint), F(soc_globals, terrain_delta),
+    F(soc_globals, terrain_min_depth), F(soc_globals, terrain_max_depth), F(soc_globals, terrain_min_tess_level),
+    F(soc_globals, terrain_max_tess_level), F(soc_globals, terrain_y_clip_trick), F(soc_globals, terrain_previous_y_clip_trick),
+    F(soc_globals, filter_radius), F(soc_globals, ssao_bias), F(soc_globals, ssao_radius), F(soc_globals, ssao_kernel_size),
+    F(soc_globals, ambient), F(soc_globals, ambient_occlussion_strength), F(soc_globals, emissive_bloom_strength),
+    F(soc_globals, focal_length), F(soc_globals, plane_in_focus), F(soc_globals, aperture), F(soc_globals, adjustment_speed),
+    F(soc_globals, log_min_luminance), F(soc_globals, log_max_luminance), F(soc_globals, target_luminance),
+    F(soc_globals, saturation), F(soc_globals, agxDs_linear_section), F(soc_globals, peak), F(soc_globals, compression),
+    F(soc_frame_images, albedo), F(soc_frame_images, emissive), F(soc_frame_images, normal), F(soc_frame_images, depth),
+    F(soc_frame_images, velocity), F(soc_frame_images, shadow), F(soc_frame_images, noise), F(soc_frame_images, bloom_mips),
+    F(soc_frame_images, ssao), F(soc_frame_images, ssao_blur), F(soc_frame_images, clouds), F(soc_frame_images, color),
+    F(soc_frame_images, history_color), F(soc_frame_images, history_velocity), F(soc_frame_images, output),
+    F(soc_frame_images, ssao_noise_table), F(soc_frame_images, auto_exposure), F(soc_frame_images, d_globals),
+};
+#undef F
+}  // namespace
+
+extern "C" int32_t soc_abi_version(void) { return SOC_RT_ABI_VERSION; }
+
+extern "C" size_t soc_abi_sizeof(const char* t) {
+    if (!t) return 0;
+    std::string s(t);
+    if (s == "soc_img") return sizeof(soc_img);
+    if (s == "soc_globals") return sizeof(soc_globals);
+    if (s == "soc_sun_info") return sizeof(soc_sun_info);
+    if (s == "soc_point_light") return sizeof(soc_point_light);
+    if (s == "soc_spot_light") return sizeof(soc_spot_light);
+    if (s == "soc_auto_exposure") return sizeof(soc_auto_exposure);
+    if (s == "soc_camera") return sizeof(soc_camera);
+    if (s == "soc_frame_images") return sizeof(soc_frame_images);
+    return 0;
+}
+
+extern "C" int64_t soc_abi_offsetof(const char* t, const char* f) {
+    if (!t || !f) return -1;
+    for (const auto& e : kFields)
+        if (!std::strcmp(e.type, t) && !std::strcmp(e.field, f)) return (int64_t)e.offset;
+    return -1;
+}
+
+extern "C" const char* soc_last_error_string(void) { return t_error.c_str(); }
+extern "C" const char* soc_device_arch(void) { return "gfx950"; }
+
+// =================================================================================================
+// glm restatements (glm 0.9.9 / 1.0 scalar code paths, RH_NO clip control: quirk Q1)
+// =================================================================================================
+extern "C" void soc_mat4_mul(float out[16], const float a[16], const float b[16]) { mat4_mul_host(out, a, b); }
+
+static inline void ident(float* m) {
+    std::memset(m, 0, 16 * sizeof(float));
+    m[0] = m[5] = m[10] = m[15] = 1.0f;
+}
+
+extern "C" void soc_mat4_perspective_rh_no(float out[16], float fovy, float aspect, float zNear, float zFar) {
+    const float tanHalfFovy = std::tan(fovy / 2.0f);
+    std::memset(out, 0, 16 * sizeof(float));
+    out[0 * 4 + 0] = 1.0f / (aspect * tanHalfFovy);
+    out[1 * 4 + 1] = 1.0f / tanHalfFovy;
+    out[2 * 4 + 2] = -(zFar + zNear) / (zFar - zNear);
+    out[2 * 4 + 3] = -1.0f;
+    out[3 * 4 + 2] = -(2.0f * zFar * zNear) / (zFar - zNear);
+}
+
+extern "C" void soc_mat4_ortho_rh_no(float out[16], float l, float r, float b, float t, float zNear, float zFar) {
+    ident(out);
+    out[0 * 4 + 0] = 2.0f / (r - l);
+    out[1 * 4 + 1] = 2.0f / (t - b);
+    out[2 * 4 + 2] = -2.0f / (zFar - zNear);
+    out[3 * 4 + 0] = -(r + l) / (r - l);
+    out[3 * 4 + 1] = -(t + b) / (t - b);
+    out[3 * 4 + 2] = -(zFar + zNear) / (zFar - zNear);
+}
+
+namespace {
+struct V3h { float x, y, z; };
+inline V3h sub(V3h a, V3h b) { return V3h{a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline float dot(V3h a, V3h b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+inline V3h cross(V3h a, V3h b) { return V3h{a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y}; }
+inline V3h normalize(V3h v) {  // glm: v * inversesqrt(dot(v, v)), inversesqrt = 1 / sqrt
+    float s = 1.0f / std::sqrt(dot(v, v));
+    return V3h{v.x * s, v.y * s, v.z * s};
+}
+}  // namespace
+
+extern "C" void soc_mat4_look_at_rh(float out[16], const float eye_[3], const float center_[3], const float up_[3]) {
+    const V3h eye{eye_[0], eye_[1], eye_[2]}, center{center_[0], center_[1], center_[2]}, up{up_[0], up_[1], up_[2]};
+    const V3h f = normalize(sub(center, eye));
+    const V3h s = normalize(cross(f, up));
+    const V3h u = cross(s, f);
+    ident(out);
+    out[0 * 4 + 0] = s.x; out[1 * 4 + 0] = s.y; out[2 * 4 + 0] = s.z;
+    out[0 * 4 + 1] = u.x; out[1 * 4 + 1] = u.y; out[2 * 4 + 1] = u.z;
+    out[0 * 4 + 2] = -f.x; out[1 * 4 + 2] = -f.y; out[2 * 4 + 2] = -f.z;
+    out[3 * 4 + 0] = -dot(s, eye);
+    out[3 * 4 + 1] = -dot(u, eye);
+    out[3 * 4 + 2] = dot(f, eye);
+}
+
+// glm compute_inverse<4,4> (func_matrix.inl), scalar path.
+extern "C" void soc_mat4_inverse(float out[16], const float mm[16]) {
+#define m(c, r) mm[(c) * 4 + (r)]
+    const float Coef00 = m(2, 2) * m(3, 3) - m(3, 2) * m(2, 3);
+    const float Coef02 = m(1, 2) * m(3, 3) - m(3, 2) * m(1, 3);
+    const float Coef03 = m(1, 2) * m(2, 3) - m(2, 2) * m(1, 3);
+    const float Coef04 = m(2, 1) * m(3, 3) - m(3, 1) * m(2, 3);
+    const float Coef06 = m(1, 1) * m(3, 3) - m(3, 1) * m(1, 3);
+    const float Coef07 = m(1, 1) * m(2, 3) - m(2, 1) * m(1, 3);
+    const float Coef08 = m(2, 1) * m(3, 2) - m(3, 1) * m(2, 2);
+    const float Coef10 = m(1, 1) * m(3, 2) - m(3, 1) * m(1, 2);
+    const float Coef11 = m(1, 1) * m(2, 2) - m(2, 1) * m(1, 2);
+    const float Coef12 = m(2, 0) * m(3, 3) - m(3, 0) * m(2, 3);
+    const float Coef14 = m(1, 0) * m(3, 3) - m(3, 0) * m(1, 3);
+    const float Coef15 = m(1, 0) * m(2, 3) - m(2, 0) * m(1, 3);
+    const float Coef16 = m(2, 0) * m(3, 2) - m(3, 0) * m(2, 2);
+    const float Coef18 = m(1, 0) * m(3, 2) - m(3, 0) * m(1, 2);
+    const float Coef19 = m(1, 0) * m(2, 2) - m(2, 0) * m(1, 2);
+    const float Coef20 = m(2, 0) * m(3, 1) - m(3, 0) * m(2, 1);
+    const float Coef22 = m(1, 0) * m(3, 1) - m(3, 0) * m(1, 1);
+    const float Coef23 = m(1, 0) * m(2, 1) - m(2, 0) * m(1, 1);
+    const float Fac0[4] = {Coef00, Coef00, Coef02, Coef03};
+    const float Fac1[4] = {Coef04, Coef04, Coef06, Coef07};
+    const float Fac2[4] = {Coef08, Coef08, Coef10, Coef11};
+    const float Fac3[4] = {Coef12, Coef12, Coef14, Coef15};
+    const float Fac4[4] = {Coef16, Coef16, Coef18, Coef19};
+    const float Fac5[4] = {Coef20, Coef20, Coef22, Coef23};
+    const float Vec0[4] = {m(1, 0), m(0, 0), m(0, 0), m(0, 0)};
+    const float Vec1[4] = {m(1, 1), m(0, 1), m(0, 1), m(0, 1)};
+    const float Vec2[4] = {m(1, 2), m(0, 2), m(0, 2), m(0, 2)};
+    const float Vec3[4] = {m(1, 3), m(0, 3), m(0, 3), m(0, 3)};
+    float Inv[4][4];
+    for (int i = 0; i < 4; ++i) {
+        Inv[0][i] = Vec1[i] * Fac0[i] - Vec2[i] * Fac1[i] + Vec3[i] * Fac2[i];
+        Inv[1][i] = Vec0[i] * Fac0[i] - Vec2[i] * Fac3[i] + Vec3[i] * Fac4[i];
+        Inv[2][i] = Vec0[i] * Fac1[i] - Vec1[i] * Fac3[i] + Vec3[i] * Fac5[i];
+        Inv[3][i] = Vec0[i] * Fac2[i] - Vec1[i] * Fac4[i] + Vec2[i] * Fac5[i];
+    }
+    const float SignA[4] = {+1.0f, -1.0f, +1.0f, -1.0f}, SignB[4] = {-1.0f, +1.0f, -1.0f, +1.0f};
+    float Inverse[4][4];
+    for (int i = 0; i < 4; ++i) {
+        Inverse[0][i] = Inv[0][i] * SignA[i];
+        Inverse[1][i] = Inv[1][i] * SignB[i];
+        Inverse[2][i] = Inv[2][i] * SignA[i];
+        Inverse[3][i] = Inv[3][i] * SignB[i];
+    }
+    const float Row0[4] = {Inverse[0][0], Inverse[1][0], Inverse[2][0], Inverse[3][0]};
+    const float Dot0[4] = {m(0, 0) * Row0[0], m(0, 1) * Row0[1], m(0, 2) * Row0[2], m(0, 3) * Row0[3]};
+    const float Dot1 = (Dot0[0] + Dot0[1]) + (Dot0[2] + Dot0[3]);
+    const float OneOverDeterminant = 1.0f / Dot1;
+    for (int c = 0; c < 4; ++c)
+        for (int r = 0; r < 4; ++r) out[c * 4 + r] = Inverse[c][r] * OneOverDeterminant;
+#undef m
+}
+
+static inline float radians(float deg) { return deg * 0.01745329251994329576923690768489f; }
+
+// glm::rotateX/Y/Z (gtx/rotate_vector.inl)
+static V3h rotate_x(V3h v, float a) { float c = std::cos(a), s = std::sin(a); return V3h{v.x, v.y * c - v.z * s, v.y * s + v.z * c}; }
+static V3h rotate_y(V3h v, float a) { float c = std::cos(a), s = std::sin(a); return V3h{v.x * c + v.z * s, v.y, -v.x * s + v.z * c}; }
+static V3h rotate_z(V3h v, float a) { float c = std::cos(a), s = std::sin(a); return V3h{v.x * c - v.y * s, v.x * s + v.y * c, v.z}; }
+
+extern "C" int soc_globals_init_defaults(soc_globals* g, int32_t width, int32_t height) {
+    if (!g || width <= 0 || height <= 0) return set_error(SOC_E_INVALID_ARG, "soc_globals_init_defaults: bad args");
+    std::memset(g, 0, sizeof *g);
+    // renderer.cpp:72-107
+    g->terrain_offset[0] = g->terrain_offset[1] = g->terrain_offset[2] = 0.0f;
+    g->terrain_scale[0] = g->terrain_scale[1] = 100.0f;
+    g->terrain_height_scale = 70.0f;
+    g->terrain_midpoint = 0.2f;
+    g->terrain_delta = 8.0f;
+    g->terrain_min_depth = 1.0f;
+    g->terrain_max_depth = 100.0f;
+    g->terrain_min_tess_level = 1;
+    g->terrain_max_tess_level = 3;
+    g->ssao_bias = 0.025f;
+    g->ssao_radius = 0.3f;
+    g->ssao_kernel_size = 26;
+    g->ambient[0] = g->ambient[1] = g->ambient[2] = 0.1f;
+    g->ambient_occlussion_strength = 1.2f;
+    g->emissive_bloom_strength = 2.0f;
+    g->focal_length = 5.0f;
+    g->plane_in_focus = 1.0f;
+    g->aperture = 8.0f;
+    g->adjustment_speed = 1.0f;
+    g->log_min_luminance = -15.0f;
+    g->log_max_luminance = 15.0f;
+    g->target_luminance = 0.2140f;
+    g->elapsed_time = 0.0f;
+    g->log_min_luminance = std::log2(g->target_luminance / std::exp2(g->log_min_luminance));
+    g->log_max_luminance = std::log2(g->target_luminance / std::exp2(g->log_max_luminance));
+    g->saturation = 1.0f;
+    g->agxDs_linear_section = 0.18f;
+    g->peak = 1.0f;
+    g->compression = 0.15f;
+    g->frame_counter = 0;
+    // sun, renderer.cpp:109-133 (angle_direction = {4, 0, 0}, renderer.hpp:67)
+    const V3h light_position{-3.2f, 40.0f, -4.0f};
+    const float planes = 16.0f;
+    float light_projection[16];
+    soc_mat4_ortho_rh_no(light_projection, -planes, planes, -planes, planes, -planes, planes);
+    V3h dir{0.0f, -1.0f, 0.0f};
+    dir = rotate_x(dir, radians(4.0f));
+    dir = rotate_y(dir, radians(0.0f));
+    dir = rotate_z(dir, radians(0.0f));
+    const float eye[3] = {light_position.x, light_position.y, light_position.z};
+    const float center[3] = {light_position.x + dir.x, light_position.y + dir.y, light_position.z + dir.z};
+    const float up[3] = {0.0f, -1.0f, 0.0f};
+    float light_view[16], pv[16];
+    soc_mat4_look_at_rh(light_view, eye, center, up);
+    mat4_mul_host(pv, light_projection, light_view);
+    std::memcpy(g->sun_info.projection_matrix, light_projection, sizeof light_projection);
+    std::memcpy(g->sun_info.view_matrix, light_view, sizeof light_view);
+    std::memcpy(g->sun_info.projection_view_matrix, pv, sizeof pv);
+    for (int r = 0; r < 4; ++r) g->sun_info.terrain_y_clip_trick[r] = pv[1 * 4 + r];  // pv * (0,1,0,0)
+    g->sun_info.position[0] = light_position.x; g->sun_info.position[1] = light_position.y; g->sun_info.position[2] = light_position.z;
+    g->sun_info.direction[0] = dir.x; g->sun_info.direction[1] = dir.y; g->sun_info.direction[2] = dir.z;
+    g->sun_info.exponential_factor = -80.0f;
+    g->sun_info.darkening_factor = 1.0f;
+    g->sun_info.bias = 0.0001f;
+    g->sun_info.intensity = 1.0f;
+    g->resolution[0] = width;
+    g->resolution[1] = height;
+    // Camera3D defaults (camera.hpp:74-75)
+    g->camera_near_clip = 0.1f;
+    g->camera_far_clip = 1000.0f;
+    return SOC_OK;
+}
+
+extern "C" int soc_globals_frame_update(soc_globals* g, const soc_camera* cam, int32_t width, int32_t height, float delta_time,
+                                        uint32_t* jitter_index) {
+    if (!g || !cam || !jitter_index || width <= 0 || height <= 0)
+        return set_error(SOC_E_INVALID_ARG, "soc_globals_frame_update: bad args");
+    // Camera3D::resize (camera.cpp:6-10)
+    float proj[16];
+    const float aspect = (float)width / (float)height;
+    soc_mat4_perspective_rh_no(proj, radians(cam->fov_degrees), aspect, cam->near_clip, cam->far_clip);
+    proj[1 * 4 + 1] *= -1.0f;
+    // ControlledCamera3D::update (camera.cpp:36-56), no input
+    float ry = cam->rotation[1];
+    const float MAX_ROT = 1.56825555556f;
+    if (ry > MAX_ROT) ry = MAX_ROT;
+    if (ry < -MAX_ROT) ry = -MAX_ROT;
+    const float rx = cam->rotation[0];
+    const V3h fwd = normalize(V3h{std::cos(rx) * std::cos(ry), -std::sin(ry), std::sin(rx) * std::cos(ry)});
+    const float eye[3] = {cam->position[0], cam->position[1], cam->position[2]};
+    const float center[3] = {eye[0] + fwd.x, eye[1] + fwd.y, eye[2] + fwd.z};
+    const float up[3] = {0.0f, 1.0f, 0.0f};
+    float view[16];
+    soc_mat4_look_at_rh(view, eye, center, up);
+    // Application::update jitter (application.cpp:113-131)
+    const float gr = 1.32471795724474602596f, a1 = 1.0f / gr, a2 = 1.0f / (gr * gr);
+    auto gmod = [](float x, float y) { return x - y * std::floor(x / y); };
+    const float idx = (float)(*jitter_index);
+    float jx = gmod(0.5f + a1 * (idx + 1.0f), 1.0f) - 0.5f;
+    float jy = gmod(0.5f + a2 * (idx + 1.0f), 1.0f) - 0.5f;
+    jx = jx * (1.0f / (float)width);
+    jy = jy * (1.0f / (float)height);
+    *jitter_index = (*jitter_index + 1) % 32;
+    proj[3 * 4 + 0] += jx;
+    proj[3 * 4 + 1] += jy;
+    float inv_proj[16], inv_view[16], pv[16], inv_pv[16];
+    soc_mat4_inverse(inv_proj, proj);
+    soc_mat4_inverse(inv_view, view);
+    mat4_mul_host(pv, proj, view);
+    mat4_mul_host(inv_pv, inv_proj, inv_view);
+    // shift current -> previous (application.cpp:139-146)
+    std::memcpy(g->camera_previous_projection_matrix, g->camera_projection_matrix, 64);
+    std::memcpy(g->camera_previous_inverse_projection_matrix, g->camera_inverse_projection_matrix, 64);
+    std::memcpy(g->camera_previous_view_matrix, g->camera_view_matrix, 64);
+    std::memcpy(g->camera_previous_inverse_view_matrix, g->camera_inverse_view_matrix, 64);
+    std::memcpy(g->camera_previous_projection_view_matrix, g->camera_projection_view_matrix, 64);
+    std::memcpy(g->camera_previous_inverse_projection_view_matrix, g->camera_inverse_projection_view_matrix, 64);
+    std::memcpy(g->terrain_previous_y_clip_trick, g->terrain_y_clip_trick, 16);
+    std::memcpy(g->previous_jitter, g->jitter, 8);
+    std::memcpy(g->camera_projection_matrix, proj, 64);
+    std::memcpy(g->camera_inverse_projection_matrix, inv_proj, 64);
+    std::memcpy(g->camera_view_matrix, view, 64);
+    std::memcpy(g->camera_inverse_view_matrix, inv_view, 64);
+    std::memcpy(g->camera_projection_view_matrix, pv, 64);
+    std::memcpy(g->camera_inverse_projection_view_matrix, inv_pv, 64);
+    for (int r = 0; r < 4; ++r) g->terrain_y_clip_trick[r] = pv[1 * 4 + r];
+    g->jitter[0] = jx;
+    g->jitter[1] = jy;
+    g->camera_near_clip = cam->near_clip;
+    g->camera_far_clip = cam->far_clip;
+    g->resolution[0] = width;
+    g->resolution[1] = height;
+    for (int i = 0; i < 3; ++i) g->camera_position[i] = cam->position[i];
+    g->delta_time = delta_time;
+    g->elapsed_time += delta_time;
+    g->frame_counter++;
+    return SOC_OK;
+}
+
+extern "C" int soc_upload_globals(const soc_globals* g, soc_globals* d_globals, soc_stream stream) {
+    if (!g || !d_globals) return set_error(SOC_E_INVALID_ARG, "soc_upload_globals: null argument");
+    hipError_t e = hipMemcpyAsync(d_globals, g, sizeof(soc_globals), hipMemcpyHostToDevice, hs(stream));
+    if (e != hipSuccess) return set_error(SOC_E_HIP, "soc_upload_globals: %s", hipGetErrorString(e));
+    return SOC_OK;
+}
+
+// =================================================================================================
+// Render graph (renderer.cpp:929-1235, live passes only; SSR / Hi-Z / DOF are dead or disabled)
+// =================================================================================================
+struct soc_renderer {
+    struct Pass {
+        std::string name, group;
+        int phase;
+        std::function<int(const soc_globals*, hipStream_t)> run;
+        hipEvent_t ev[2] = {nullptr, nullptr};
+        bool recorded = false;
+    };
+    soc_frame_images img{};
+    std::vector<Pass> passes;
+    uint32_t flags = 0;
+    int hist = 0;               // history slot read as "previous" this frame
+    uint64_t total_pixels = 0;  // 0 = this frame
+    int wide = 0;
+    // pinned staging ring for the device globals upload (lights)
+    soc_globals* staging = nullptr;
+    hipEvent_t staging_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    int staging_slot = 0;
+};
+
+namespace {
+void build_passes(soc_renderer* r) {
+    auto& I = r->img;
+    auto add = [&](std::string name, std::string group, int phase, std::function<int(const soc_globals*, hipStream_t)> fn) {
+        soc_renderer::Pass p;
+        p.name = std::move(name);
+        p.group = std::move(group);
+        p.phase = phase;
+        p.run = std::move(fn);
+        r->passes.push_back(std::move(p));
+    };
+    const int nm = 4;
+    // renderer.cpp:1024-1062
+    add("BloomDownsample - 0", "Bloom", SOC_PHASE_PRE_EXPOSURE,
+        [r](const soc_globals* g, hipStream_t s) { return soc_bloom_downsample(g, r->img.emissive, r->img.bloom_mips[0], (soc_stream)s); });
+    for (int i = 0; i < nm - 1; ++i)
+        add("BloomDownsample - " + std::to_string(i + 1), "Bloom", SOC_PHASE_PRE_EXPOSURE, [r, i](const soc_globals* g, hipStream_t s) {
+            return soc_bloom_downsample(g, r->img.bloom_mips[i], r->img.bloom_mips[i + 1], (soc_stream)s);
+        });
+    for (int i = nm - 1; i > 0; --i)
+        add("BloomUpsample - " + std::to_string(i), "Bloom", SOC_PHASE_PRE_EXPOSURE, [r, i](const soc_globals* g, hipStream_t s) {
+            return soc_bloom_upsample(g, r->img.bloom_mips[i], r->img.bloom_mips[i - 1], (soc_stream)s);
+        });
+    add("BloomUpsample - 0", "Bloom", SOC_PHASE_PRE_EXPOSURE,
+        [r](const soc_globals* g, hipStream_t s) { return soc_bloom_upsample(g, r->img.bloom_mips[0], r->img.emissive, (soc_stream)s); });
+    // renderer.cpp:1064-1079
+    add("SSAOGeneration", "Ambient Occlusion", SOC_PHASE_PRE_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
+        return soc_ssao_generation(g, r->img.depth, r->img.normal, r->img.ssao, r->img.ssao_noise_table, (soc_stream)s);
+    });
+    add("SSAOBlur", "Ambient Occlusion", SOC_PHASE_PRE_EXPOSURE,
+        [r](const soc_globals* g, hipStream_t s) { return soc_ssao_blur(g, r->img.ssao, r->img.ssao_blur, (soc_stream)s); });
+    // renderer.cpp:1094-1101
+    add("CloudRendering", "Sky Rendering", SOC_PHASE_PRE_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
+        return soc_cloud_rendering(g, r->img.depth, r->img.noise, r->img.clouds, (soc_stream)s);
+    });
+    // renderer.cpp:1103-1117
+    add("Composition", "Composition", SOC_PHASE_PRE_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
+        const auto& I = r->img;
+        return soc_composition(g, I.d_globals, I.color, I.albedo, I.emissive, I.normal, I.depth, I.ssao_blur, I.shadow, I.clouds,
+                               (soc_stream)s);
+    });
+    // renderer.cpp:1155-1168
+    add("GenerateLuminanceHistogram", "Auto Exposure", SOC_PHASE_PRE_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
+        return soc_generate_luminance_histogram(g, r->img.color, r->img.auto_exposure, (soc_stream)s);
+    });
+    add("ResolveLuminanceHistogram", "Auto Exposure", SOC_PHASE_POST_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
+        return soc_resolve_luminance_histogram(g, r->img.auto_exposure, r->total_pixels, r->wide, (soc_stream)s);
+    });
+    // renderer.cpp:1170-1198: TAA + both history copies (ping-pong + fused velocity history)
+    add("TemporalAntiAliasing", "Temporal Anti-Aliasing", SOC_PHASE_POST_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
+        const auto& I = r->img;
+        const int p = r->hist, q = 1 - r->hist;
+        return soc_temporal_antialiasing(g, I.history_color[q], I.color, I.history_color[p], I.velocity, I.history_velocity[p],
+                                         I.depth, I.history_velocity[q], (soc_stream)s);
+    });
+    // renderer.cpp:1210-1217
+    add("ToneMapping", "Tone Mapping", SOC_PHASE_POST_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
+        const auto& I = r->img;
+        return soc_tone_mapping(g, I.history_color[1 - r->hist], I.auto_exposure, I.output, (soc_stream)s);
+    });
+    (void)I;
+}
+}  // namespace
+
+extern "C" soc_renderer* soc_renderer_create(const soc_frame_images* images, uint32_t flags) {
+    if (!images) {
+        set_error(SOC_E_INVALID_ARG, "soc_renderer_create: null images");
+        return nullptr;
+    }
+    if (!images->auto_exposure) {
+        set_error(SOC_E_INVALID_ARG, "soc_renderer_create: auto_exposure buffer required");
+        return nullptr;
+    }
+    soc_renderer* r = new soc_renderer();
+    r->img = *images;
+    r->flags = flags;
+    build_passes(r);
+    if (flags & SOC_RENDERER_TIMING) {
+        for (auto& p : r->passes) {
+            if (hipEventCreate(&p.ev[0]) != hipSuccess || hipEventCreate(&p.ev[1]) != hipSuccess) {
+                set_error(SOC_E_HIP, "soc_renderer_create: hipEventCreate failed");
+                soc_renderer_destroy(r);
+                return nullptr;
+            }
+        }
+    }
+    return r;
+}
+
+extern "C" void soc_renderer_destroy(soc_renderer* r) {
+    if (!r) return;
+    for (auto& p : r->passes)
+        for (auto& e : p.ev)
+            if (e) (void)hipEventDestroy(e);
+    for (auto& e : r->staging_ev)
+        if (e) (void)hipEventDestroy(e);
+    if (r->staging) (void)hipHostFree(r->staging);
+    delete r;
+}
+
+static int upload_lights(soc_renderer* r, const soc_globals* g, hipStream_t s) {
+    if (!r->img.d_globals) return set_error(SOC_E_INVALID_ARG, "soc_renderer_execute: lights need frame d_globals");
+    if (!r->staging) {
+        if (hipHostMalloc((void**)&r->staging, 4 * sizeof(soc_globals), 0) != hipSuccess)
+            return set_error(SOC_E_HIP, "soc_renderer_execute: hipHostMalloc failed");
+        for (auto& e : r->staging_ev)
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+                return set_error(SOC_E_HIP, "soc_renderer_execute: hipEventCreate failed");
+    }
+    const int slot = r->staging_slot;
+    r->staging_slot = (slot + 1) & 3;
+    (void)hipEventSynchronize(r->staging_ev[slot]);  // slot's previous copy has landed
+    std::memcpy(&r->staging[slot], g, sizeof(soc_globals));
+    hipError_t e = hipMemcpyAsync(r->img.d_globals, &r->staging[slot], sizeof(soc_globals), hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return set_error(SOC_E_HIP, "soc_renderer_execute: globals upload: %s", hipGetErrorString(e));
+    (void)hipEventRecord(r->staging_ev[slot], s);
+    return SOC_OK;
+}
+
+extern "C" int soc_renderer_execute(soc_renderer* r, const soc_globals* g, int32_t phase, soc_stream stream) {
+    if (!r || !g) return set_error(SOC_E_INVALID_ARG, "soc_renderer_execute: null argument");
+    hipStream_t s = hs(stream);
+    if ((phase & SOC_PHASE_PRE_EXPOSURE) && (g->point_light_count || g->spot_light_count)) {
+        int rc = upload_lights(r, g, s);
+        if (rc) return rc;
+    }
+    const bool timing = (r->flags & SOC_RENDERER_TIMING) != 0;
+    for (auto& p : r->passes) {
+        if (!(p.phase & phase)) continue;
+        if (timing) (void)hipEventRecord(p.ev[0], s);
+        int rc = p.run(g, s);
+        if (rc) return rc;
+        if (timing) {
+            (void)hipEventRecord(p.ev[1], s);
+            p.recorded = true;
+        }
+    }
+    if (phase & SOC_PHASE_POST_EXPOSURE) r->hist = 1 - r->hist;   // ping-pong the TAA history
+    return SOC_OK;
+}
+
+extern "C" int soc_renderer_set_exposure_pixels(soc_renderer* r, uint64_t total_pixels, int32_t wide_accumulator) {
+    if (!r) return set_error(SOC_E_INVALID_ARG, "soc_renderer_set_exposure_pixels: null renderer");
+    r->total_pixels = total_pixels;
+    r->wide = wide_accumulator;
+    return SOC_OK;
+}
+
+extern "C" int32_t soc_renderer_pass_count(const soc_renderer* r) { return r ? (int32_t)r->passes.size() : 0; }
+
+extern "C" const char* soc_renderer_pass_name(const soc_renderer* r, int32_t i) {
+    if (!r || i < 0 || i >= (int32_t)r->passes.size()) return nullptr;
+    return r->passes[i].name.c_str();
+}
+
+extern "C" const char* soc_renderer_pass_group(const soc_renderer* r, int32_t i) {
+    if (!r || i < 0 || i >= (int32_t)r->passes.size()) return nullptr;
+    return r->passes[i].group.c_str();
+}
+
+extern "C" float soc_renderer_pass_ms(soc_renderer* r, int32_t i) {
+    if (!r || i < 0 || i >= (int32_t)r->passes.size()) return -1.0f;
+    auto& p = r->passes[i];
+    if (!p.recorded || !p.ev[0]) return -1.0f;
+    float ms = -1.0f;
+    if (hipEventElapsedTime(&ms, p.ev[0], p.ev[1]) != hipSuccess) return -1.0f;
+    return ms;
+}
+
+extern "C" int32_t soc_renderer_current_history(const soc_renderer* r) { return r ? r->hist : -1; }

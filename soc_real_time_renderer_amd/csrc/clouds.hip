@@ -1,0 +1,289 @@
+// clouds.hip — CloudRenderingTask (src/graphics/tasks/cloud_rendering.inl:27-54, shader :92-481):
+// Rayleigh/Mie single scattering (16 x 8 steps) + a 24-step volumetric cloud march with a 10-step
+// sun-visibility march per dense step, on sky pixels only (depth == 1); other pixels get the constant
+// (0.2, 0.4, 1.0). Output RGBA8_UNORM at full resolution (quirk Q6).
+//
+// VALU/transcendental-bound, not HBM-bound. Workgroups are 16x16 pixel tiles (4 waves of 16x4, so
+// sky masks are wave-coherent); a tile with no sky pixel exits after its depth test. Tiles with sky
+// stage the 64x64 noise texture into LDS as packed 2x2 quads (one ds_read_b32 returns the four texels
+// of a bilinear REPEAT tap), 16 KiB per workgroup.
+#include "soc_internal.hpp"
+
+namespace soc {
+namespace {
+
+constexpr int kNoise = 64, kNoiseMask = 63;
+constexpr float kEarthRadius = 6371000.0f, kMinH = 1600.0f, kMaxH = 500.0f + 1600.0f, kSunBrightness = 3.0f;
+constexpr float kPi = 3.14159265358979f;   // acos(-1.0) in fp32
+constexpr float kLn2 = 0.693147182f;       // log(2.0) in fp32
+
+struct CloudParams {
+    Mat4 inv_proj, inv_view;
+    float sun[3];      // -sun_info.direction
+    float cam[3];
+    float res_x_m1, res_y_m1;  // resolution - 1
+    float elapsed;
+    float sun_factor;  // max(min(|sun.x|, |sun.z|) + sun.y, 0)
+    int res_x, res_y;
+};
+
+struct Ctx {
+    const uint32_t* quads;   // LDS
+    float cam_x, cam_z, time;
+};
+
+__device__ __forceinline__ float bayer2(float ax, float ay) {
+    ax = floorf(ax);
+    ay = floorf(ay);
+    return fractf(ax * 0.5f + ay * (ay * 0.75f));
+}
+__device__ __forceinline__ float bayer4(float x, float y) { return bayer2(0.5f * x, 0.5f * y) * 0.25f + bayer2(x, y); }
+__device__ __forceinline__ float bayer8(float x, float y) { return bayer4(0.5f * x, 0.5f * y) * 0.25f + bayer2(x, y); }
+__device__ __forceinline__ float bayer16(float x, float y) { return bayer8(0.5f * x, 0.5f * y) * 0.25f + bayer2(x, y); }
+
+__device__ __forceinline__ float2 rsi(f3 p, f3 d, float radius) {
+    const float PoD = dot3(p, d);
+    const float r2 = radius * radius;
+    float delta = PoD * PoD + r2 - dot3(p, p);
+    if (delta < 0.0f) return float2{-1.0f, -1.0f};
+    delta = sqrtf(delta);
+    return float2{-PoD - delta, -PoD + delta};
+}
+
+// texture(noise, uv).x under REPEAT + the sampling contract, from the LDS quad table.
+__device__ __forceinline__ float noise_tap(const Ctx& cx, float u, float v) {
+    const Axis ax = axis_repeat_pow2(u, kNoise, kNoiseMask), ay = axis_repeat_pow2(v, kNoise, kNoiseMask);
+    const uint32_t q = cx.quads[ay.i0 * kNoise + ax.i0];
+    return bilerp1(unorm8(q & 0xffu), unorm8((q >> 8) & 0xffu), unorm8((q >> 16) & 0xffu), unorm8(q >> 24), ax.w, ay.w);
+}
+
+// get_3d_noise, :219-233
+__device__ __forceinline__ float noise3(const Ctx& cx, f3 pos) {
+    const float p = floorf(pos.z);
+    const float f = pos.z - p;
+    const float inv = 1.0f / 64.0f, zs = 17.0f * inv;
+    const float cu = pos.x * inv + p * zs, cv = pos.y * inv + p * zs;
+    const float a = noise_tap(cx, cu, cv);
+    const float b = noise_tap(cx, cu + zs, cv + zs);
+    return mixf(a, b, f);
+}
+
+// get_clouds, :235-262
+__device__ float get_clouds(const Ctx& cx, f3 p) {
+    const float h = length3(f3{p.x, p.y + kEarthRadius, p.z}) - kEarthRadius;
+    p = f3{p.x + cx.cam_x, h, p.z + cx.cam_z};
+    if (p.y < kMinH || p.y > kMaxH) return 0.0f;
+    const f3 mv = f3{cx.time, 0.0f, cx.time};
+    const f3 cc = p * 0.001f + mv;
+    float n = noise3(cx, cc) * 0.5f;
+    n += noise3(cx, cc * 2.0f + mv) * 0.25f;
+    n += noise3(cx, cc * 7.0f - mv) * 0.125f;
+    n += noise3(cx, (cc + mv) * 16.0f) * 0.0625f;
+    const float hh = p.y - kMinH;
+    const float th = (1.0f - __expf(-0.01f * hh)) * __expf(-0.004f * hh);
+    const float t = clampf((n - 0.55f) / (0.6f - 0.55f), 0.0f, 1.0f);
+    const float clouds = t * t * (3.0f - 2.0f * t) * th;
+    return clouds * 0.03f;
+}
+
+// getSunVisibility, :264-278
+__device__ float sun_visibility(const Ctx& cx, f3 p, f3 sun) {
+    const float rSteps = 500.0f / 10.0f;
+    const f3 inc = sun * rSteps;
+    f3 pos = inc * 0.5f + p;
+    float tr = 0.0f;
+    for (int i = 0; i < 10; i++, pos = pos + inc) tr += get_clouds(cx, pos);
+    return __expf(-tr * rSteps);
+}
+
+__device__ __forceinline__ float hg_phase(float x, float g) {
+    const float g2 = g * g;
+    return 0.25f * ((1.0f - g2) * powf(1.0f + g2 - 2.0f * g * x, -1.5f));
+}
+
+// calculate_atmospheric_scattering_top, :195-217
+__device__ f3 scattering_top(f3 sun) {
+    const f3 rayleigh = f3{0.27f * 1e-5f, 0.5f * 1e-5f, 1.0f * 1e-5f};
+    const f3 mie = f3{0.5e-6f, 0.5e-6f, 0.5e-6f};
+    const f3 total = rayleigh + mie;
+    const float lDotU = dot3(sun, f3{0.0f, 1.0f, 0.0f});
+    const float od = 100000.0f / fmaxf(1.0f * 2.0f - 0.01f, 0.01f);
+    float dl = lDotU * 2.0f;
+    dl = fmaxf(dl + 0.01f, 0.01f);
+    dl = 1.0f / dl;
+    const float odl = 100000.0f * dl;
+    const f3 sv = total * od, sl = total * odl;
+    const f3 av = f3{__expf(-total.x * od), __expf(-total.y * od), __expf(-total.z * od)};
+    const f3 al = f3{__expf(-total.x * odl), __expf(-total.y * odl), __expf(-total.z * odl)};
+    const f3 num = al - av, den = (sl - sv) * kLn2;
+    const f3 absorb = f3{(fabsf(num.x) + 1e-3f) / (fabsf(den.x) + 1e-3f), (fabsf(num.y) + 1e-3f) / (fabsf(den.y) + 1e-3f),
+                         (fabsf(num.z) + 1e-3f) / (fabsf(den.z) + 1e-3f)};
+    const f3 ms = mie * od * 0.25f, rs = rayleigh * od * 0.375f;
+    return (ms + rs) * absorb * kSunBrightness;
+}
+
+// calculate_volumetric_clouds, :307-347
+__device__ f3 volumetric_clouds(const Ctx& cx, f3 dir, f3 sun, f3 color, float dither, f3 sun_color) {
+    if (dir.y < 0.0f) return color;
+    const float rPi = 1.0f / kPi, hPi = kPi * 0.5f, rLOG2 = 1.0f / kLn2;
+    const f3 c0 = f3{0.0f, kEarthRadius, 0.0f};
+    const float bottom = rsi(c0, dir, kEarthRadius + kMinH).y;
+    const float top = rsi(c0, dir, kEarthRadius + kMaxH).y;
+    const f3 start = dir * bottom, end = dir * top;
+    const f3 inc = (end - start) * (1.0f / 24.0f);
+    f3 cp = inc * dither + start;
+    const float stepLength = length3(inc);
+    f3 scattering = f3{0.0f, 0.0f, 0.0f};
+    float transmittance = 1.0f;
+    const float x = dot3(sun, dir);
+    const float phase = mixf(hg_phase(x, -0.5f * 0.8f), hg_phase(x, 0.8f * 0.8f), 0.5f);
+    const f3 sky = scattering_top(sun);
+    for (int i = 0; i < 24; i++, cp = cp + inc) {
+        const float od = get_clouds(cx, cp) * stepLength;
+        if (od <= 0.0f) continue;
+        const float integral = __expf(-1.11f * rLOG2 * od) * (-1.0f / 1.11f) + 1.0f / 1.11f;
+        const float beers = 1.0f - __expf(-(od * kLn2) * 2.0f);
+        const float vis = sun_visibility(cx, cp, sun);
+        const f3 sunl = sun_color * vis * beers * phase * hPi * kSunBrightness;
+        const f3 skyl = sky * 0.25f * rPi;
+        scattering = scattering + (sunl + skyl) * integral * kPi * transmittance;
+        transmittance *= __expf(-od);
+    }
+    const f3 lit = color * transmittance + scattering;
+    const float m = clampf(length3(start) * 0.00001f * 2.5f, 0.0f, 1.0f);
+    return f3{mixf(lit.x, color.x, m), mixf(lit.y, color.y, m), mixf(lit.z, color.z, m)};
+}
+
+// atmosphere, :353-439 (primary ray starts at iTime = elapsed_time: quirk Q10)
+__device__ f3 atmosphere(f3 r, f3 r0, f3 pSun, float iTime) {
+    const float iSun = 22.0f, rPlanet = 6371e3f, rAtmos = 6471e3f, kMie = 21e-6f, shRlh = 8e3f, shMie = 1.2e3f, g0 = 0.758f;
+    const f3 kRlh = f3{5.5e-6f, 13.0e-6f, 22.4e-6f};
+    const float PI = 3.141592f;
+    r = normalize3(r);
+    float2 p = rsi(r0, r, rAtmos);
+    if (p.x > p.y) return f3{0.0f, 0.0f, 0.0f};
+    p.y = fminf(p.y, rsi(r0, r, rPlanet).x);
+    const float iStep = (p.y - p.x) / 16.0f;
+    f3 totalRlh = f3{0, 0, 0}, totalMie = f3{0, 0, 0};
+    float iOdRlh = 0.0f, iOdMie = 0.0f;
+    const float mu = dot3(r, pSun), mumu = mu * mu, gg = g0 * g0;
+    const float pRlh = 3.0f / (16.0f * PI) * (1.0f + mumu);
+    const float pMie = 3.0f / (8.0f * PI) * ((1.0f - gg) * (mumu + 1.0f)) / (powf(1.0f + gg - 2.0f * mu * g0, 1.5f) * (2.0f + gg));
+    const float inv_shR = 1.0f / shRlh, inv_shM = 1.0f / shMie;
+    for (int i = 0; i < 16; i++) {
+        const f3 iPos = r0 + r * (iTime + iStep * 0.5f);
+        const float iHeight = length3(iPos) - rPlanet;
+        const float odR = __expf(-iHeight * inv_shR) * iStep;
+        const float odM = __expf(-iHeight * inv_shM) * iStep;
+        iOdRlh += odR;
+        iOdMie += odM;
+        const float jStep = rsi(iPos, pSun, rAtmos).y / 8.0f;
+        float jTime = 0.0f, jOdR = 0.0f, jOdM = 0.0f;
+#pragma unroll 4
+        for (int j = 0; j < 8; j++) {
+            const f3 jPos = iPos + pSun * (jTime + jStep * 0.5f);
+            const float jHeight = length3(jPos) - rPlanet;
+            jOdR += __expf(-jHeight * inv_shR) * jStep;
+            jOdM += __expf(-jHeight * inv_shM) * jStep;
+            jTime += jStep;
+        }
+        const float fm = kMie * (iOdMie + jOdM);
+        const float fr = iOdRlh + jOdR;
+        const f3 attn = f3{__expf(-(fm + kRlh.x * fr)), __expf(-(fm + kRlh.y * fr)), __expf(-(fm + kRlh.z * fr))};
+        totalRlh = totalRlh + attn * odR;
+        totalMie = totalMie + attn * odM;
+        iTime += iStep;
+    }
+    return ((kRlh * pRlh) * totalRlh + totalMie * (pMie * kMie)) * iSun;
+}
+
+constexpr int TX = 16, TY = 16;
+
+template <bool NOISE_R8>
+__global__ __launch_bounds__(256) void clouds_kernel(DImg depth, DImg noise, DImg target, CloudParams p) {
+    __shared__ uint32_t quads[kNoise * kNoise];
+    const int x = blockIdx.x * TX + threadIdx.x, y = blockIdx.y * TY + threadIdx.y;
+    const int tid = threadIdx.y * TX + threadIdx.x;
+    const bool inside = x < p.res_x && y < p.res_y && x < target.w && y < target.h;
+    float ru = 0.0f, rv = 0.0f;
+    bool sky = false;
+    if (inside) {
+        ru = (float)x / p.res_x_m1;
+        rv = (float)y / p.res_y_m1;
+        sky = sample_f32(depth, ru, rv) == 1.0f;   // textureLod(depth, ray_uv, 0), :458
+    }
+    if (!__syncthreads_or(sky)) {
+        if (inside) row_ptr_w<uint32_t>(target, y)[x] = pack_unorm8x4(f4{0.2f, 0.4f, 1.0f, 1.0f});
+        return;
+    }
+    // stage the noise .x channel as 2x2 REPEAT quads
+    for (int i = tid; i < kNoise * kNoise; i += TX * TY) {
+        const int nx = i & kNoiseMask, ny = i >> 6;
+        const int nx1 = (nx + 1) & kNoiseMask, ny1 = (ny + 1) & kNoiseMask;
+        auto texel = [&](int tx, int ty) -> uint32_t {
+            if (NOISE_R8) return row_ptr<uint8_t>(noise, ty)[tx];
+            return row_ptr<uint32_t>(noise, ty)[tx] & 0xffu;
+        };
+        quads[i] = texel(nx, ny) | (texel(nx1, ny) << 8) | (texel(nx, ny1) << 16) | (texel(nx1, ny1) << 24);
+    }
+    __syncthreads();
+    if (!inside) return;
+    f3 color = f3{0.2f, 0.4f, 1.0f};
+    if (sky) {
+        const float ndx = ru * 2.0f - 1.0f, ndy = rv * 2.0f - 1.0f;
+        const f4 rvs = mul(p.inv_proj, f4{ndx, ndy, -1.0f, 0.0f});
+        const f4 rws = mul(p.inv_view, f4{rvs.x, rvs.y, -1.0f, 0.0f});
+        const f3 dir = normalize3(f3{rws.x, rws.y, rws.z});
+        const f3 sun = f3{p.sun[0], p.sun[1], p.sun[2]};
+        const f3 r0 = f3{0.0f + p.cam[0], 6372e3f + p.cam[1], 0.0f + p.cam[2]};
+        Ctx cx;
+        cx.quads = quads;
+        cx.cam_x = p.cam[0];
+        cx.cam_z = p.cam[2];
+        cx.time = -1.0f * 0.02f * p.elapsed;
+        const float dither = bayer16((float)x, (float)y);
+        color = atmosphere(dir, r0, sun, p.elapsed);
+        color = volumetric_clouds(cx, dir, sun, color, dither, f3{0.8f, 0.8f, 0.8f});
+        color = color * p.sun_factor;
+    }
+    row_ptr_w<uint32_t>(target, y)[x] = pack_unorm8x4(f4{color.x, color.y, color.z, 1.0f});
+}
+
+}  // namespace
+}  // namespace soc
+
+using namespace soc;
+
+extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img noise, soc_img target, soc_stream stream) {
+    static const char* P = "soc_cloud_rendering";
+    if (!g) return set_error(SOC_E_INVALID_ARG, "%s: null globals", P);
+    int rc = check_img(depth, SOC_FMT_D32F, P, "depth");
+    if (!rc) rc = check_img(target, SOC_FMT_RGBA8_UNORM, P, "target");
+    if (!rc) rc = check_img(noise, 0, P, "noise");
+    if (rc) return rc;
+    if (noise.format != SOC_FMT_R8_UNORM && noise.format != SOC_FMT_RGBA8_UNORM)
+        return set_error(SOC_E_UNSUPPORTED, "%s: noise must be R8_UNORM or RGBA8_UNORM", P);
+    if (noise.width != 64 || noise.height != 64)
+        return set_error(SOC_E_SHAPE, "%s: noise texture must be 64x64 (assets/Clouds/noise.png)", P);
+    CloudParams p;
+    p.inv_proj = mat4(g->camera_inverse_projection_matrix);
+    p.inv_view = mat4(g->camera_inverse_view_matrix);
+    for (int i = 0; i < 3; ++i) {
+        p.sun[i] = -g->sun_info.direction[i];
+        p.cam[i] = g->camera_position[i];
+    }
+    p.res_x = g->resolution[0];
+    p.res_y = g->resolution[1];
+    p.res_x_m1 = (float)g->resolution[0] - 1.0f;
+    p.res_y_m1 = (float)g->resolution[1] - 1.0f;
+    p.elapsed = g->elapsed_time;
+    p.sun_factor = fmaxf(fminf(fabsf(p.sun[0]), fabsf(p.sun[2])) + p.sun[1], 0.0f);
+    const int W = std::min(target.width, p.res_x), H = std::min(target.height, p.res_y);
+    if (W <= 0 || H <= 0) return SOC_OK;
+    dim3 blk(TX, TY), grd(ceil_div(W, TX), ceil_div(H, TY));
+    if (noise.format == SOC_FMT_R8_UNORM)
+        clouds_kernel<true><<<grd, blk, 0, hs(stream)>>>(dimg(depth), dimg(noise), dimg(target), p);
+    else
+        clouds_kernel<false><<<grd, blk, 0, hs(stream)>>>(dimg(depth), dimg(noise), dimg(target), p);
+    return check_launch("cloud_rendering");
+}

@@ -1,0 +1,204 @@
+// composition.hip — CompositionTask (src/graphics/tasks/composition.inl:29-79, shader :110-225) as a
+// gfx950 kernel.
+//
+// HBM-bound stream: per pixel it reads depth (4 B), albedo/emissive/normal (8 B each), one bilinear
+// half-res AO tap, one bilinear 4096^2 shadow-map tap and, on sky pixels only, the clouds texel; it
+// writes 8 B of RGBA16F. Fast path: two horizontally adjacent pixels per lane so every G-buffer load
+// and the store are 16 B per lane (one 1 KiB wave-instruction per image row segment), full-res taps
+// are plain loads (a centre sample under the sampling contract is the texel itself). The dead
+// volumetric-fog block (:176-196, zeroed at :196) is not computed.
+#include "soc_internal.hpp"
+
+namespace soc {
+namespace {
+
+struct CompParams {
+    Mat4 inv_proj, inv_view, sun_pv;
+    float sun_dir[3], ambient[3], cam[3];
+    float ef, df, emissive_strength, ao_strength;
+    uint32_t npl, nsl;
+    const soc_globals* __restrict__ dg;  // device globals (lights), may be null when npl == nsl == 0
+};
+
+__device__ __forceinline__ float fast_pow(float x, float y) {
+    // pow(x, y) = exp2(y * log2(x)) on the native transcendental units (as the reference GPU does)
+    return __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x));
+}
+
+// composition.inl:124-139
+__device__ f3 point_light(const soc_point_light& L, f3 frag_color, f3 normal, f3 pos, f3 cam) {
+    f3 lp = mk3(L.position[0], L.position[1], L.position[2]);
+    f3 light_dir = normalize3(lp - pos);
+    float distance = length3(lp - pos);
+    float attenuation = 1.0f / (distance * distance);
+    f3 view_dir = normalize3(cam - pos);
+    f3 halfway = normalize3(light_dir + view_dir);
+    float diffuse = fmaxf(dot3(normal, light_dir), 0.0f);
+    float nh = acosf(dot3(halfway, normal));
+    float ex = nh * 1.0f;
+    ex = -(ex * ex);
+    f3 lc = mk3(L.color[0], L.color[1], L.color[2]);
+    return frag_color * lc * (diffuse + expf(ex)) * attenuation * L.intensity;
+}
+
+// composition.inl:141-160
+__device__ f3 spot_light(const soc_spot_light& L, f3 frag_color, f3 normal, f3 pos, f3 cam) {
+    f3 lp = mk3(L.position[0], L.position[1], L.position[2]);
+    f3 light_dir = normalize3(lp - pos);
+    float theta = dot3(light_dir, normalize3(-mk3(L.direction[0], L.direction[1], L.direction[2])));
+    float epsilon = L.cut_off - L.outer_cut_off;
+    float intensity = clampf((theta - L.outer_cut_off) / epsilon, 0.0f, 1.0f);
+    float distance = length3(lp - pos);
+    float attenuation = 1.0f / (distance * distance);
+    f3 view_dir = normalize3(cam - pos);
+    f3 halfway = normalize3(light_dir + view_dir);
+    float diffuse = fmaxf(dot3(normal, light_dir), 0.0f);
+    float nh = acosf(dot3(halfway, normal));
+    float ex = nh / 1.0f;
+    ex = -(ex * ex);
+    f3 lc = mk3(L.color[0], L.color[1], L.color[2]);
+    return frag_color * lc * (diffuse + expf(ex)) * attenuation * L.intensity * intensity;
+}
+
+// Shading of one pixel given its G-buffer values (composition.inl:164-224).
+__device__ __forceinline__ f4 shade(const CompParams& p, float u, float v, float d, f3 albedo, f3 emissive, f3 n,
+                                    float ssao, const DImg& shadow) {
+    // get_world_position_from_depth, :114-122
+    f4 vs = mul(p.inv_proj, f4{u * 2.0f - 1.0f, v * 2.0f - 1.0f, d, 1.0f});
+    const float rw = vs.w;
+    vs = f4{vs.x / rw, vs.y / rw, vs.z / rw, vs.w / rw};
+    const f4 ws = mul(p.inv_view, vs);
+    const f3 wp = f3{ws.x, ws.y, ws.z};
+    // sun ESM shadow, :166-173
+    const f4 sp = mul(p.sun_pv, f4{wp.x, wp.y, wp.z, 1.0f});
+    const float pcx = __fdividef(sp.x, sp.w) * 0.5f + 0.5f;
+    const float pcy = __fdividef(sp.y, sp.w) * 0.5f + 0.5f;
+    const float pcz = __fdividef(sp.z, sp.w);
+    const float sd = sample_f32(shadow, pcx, pcy);
+    float e = __expf(p.ef * (pcz - sd));
+    if (p.df != 1.0f) e = fast_pow(e, p.df);   // pow(x, 1.0) == x exactly
+    const float sun_shadow = clampf(e, 0.0f, 1.0f);
+
+    const f3 em = emissive * p.emissive_strength;
+    const float occl = fast_pow(ssao, p.ao_strength);
+    const float dd = fmaxf(0.0f, dot3(n, -mk3(p.sun_dir[0], p.sun_dir[1], p.sun_dir[2]))) * sun_shadow;
+    f3 direct = f3{dd, dd, dd};
+    if (p.npl | p.nsl) {
+        const f3 cam = mk3(p.cam[0], p.cam[1], p.cam[2]);
+        for (uint32_t i = 0; i < p.npl; ++i) direct = direct + point_light(p.dg->point_lights[i], albedo, n, wp, cam);
+        for (uint32_t i = 0; i < p.nsl; ++i) direct = direct + spot_light(p.dg->spot_lights[i], albedo, n, wp, cam);
+    }
+    const f3 c = (direct + mk3(p.ambient[0], p.ambient[1], p.ambient[2])) * albedo * occl + em;
+    return f4{c.x, c.y, c.z, 1.0f};
+}
+
+constexpr int BX = 64, BY = 4;
+
+// Fast path: all full-res images share the target extent, width even, rows 16-B aligned.
+__global__ __launch_bounds__(256) void composition_pair(DImg target, DImg albedo, DImg emissive, DImg normal, DImg depth,
+                                                        DImg ssao, DImg shadow, DImg clouds, CompParams p) {
+    const int x = (blockIdx.x * BX + threadIdx.x) * 2, y = blockIdx.y * BY + threadIdx.y;
+    if (x >= target.w || y >= target.h) return;
+    const float v = centre_uv(y, target.h);
+    const float2 d2 = row_ptr<float2>(depth, y)[x >> 1];
+    const uint4 a4 = row_ptr<uint4>(albedo, y)[x >> 1];
+    const uint4 e4 = row_ptr<uint4>(emissive, y)[x >> 1];
+    const uint4 n4 = row_ptr<uint4>(normal, y)[x >> 1];
+    uint2 outp[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const float u = centre_uv(x + k, target.w);
+        const float d = k ? d2.y : d2.x;
+        const f4 al = unpack_h4(k ? uint2{a4.z, a4.w} : uint2{a4.x, a4.y});
+        const f4 em = unpack_h4(k ? uint2{e4.z, e4.w} : uint2{e4.x, e4.y});
+        const f4 nn = unpack_h4(k ? uint2{n4.z, n4.w} : uint2{n4.x, n4.y});
+        f4 c;
+        if (d == 1.0f) {
+            const f4 cl = fetch_rgba8(clouds, x + k, y);
+            c = f4{cl.x, cl.y, cl.z, 1.0f};
+        } else {
+            const float ao = sample_r8(ssao, u, v);
+            c = shade(p, u, v, d, f3{al.x, al.y, al.z}, f3{em.x, em.y, em.z}, f3{nn.x, nn.y, nn.z}, ao, shadow);
+        }
+        outp[k] = pack_h4(c);
+    }
+    row_ptr_w<uint4>(target, y)[x >> 1] = uint4{outp[0].x, outp[0].y, outp[1].x, outp[1].y};
+}
+
+// Generic path: every input is sampled under the sampling contract.
+__global__ __launch_bounds__(256) void composition_generic(DImg target, DImg albedo, DImg emissive, DImg normal,
+                                                           DImg depth, DImg ssao, DImg shadow, DImg clouds, CompParams p) {
+    const int x = blockIdx.x * BX + threadIdx.x, y = blockIdx.y * BY + threadIdx.y;
+    if (x >= target.w || y >= target.h) return;
+    const float u = centre_uv(x, target.w), v = centre_uv(y, target.h);
+    const float d = sample_f32(depth, u, v);
+    f4 c;
+    if (d == 1.0f) {
+        const f4 cl = sample_rgba8(clouds, u, v);
+        c = f4{cl.x, cl.y, cl.z, 1.0f};
+    } else {
+        const f4 al = sample_h4(albedo, u, v), em = sample_h4(emissive, u, v), nn = sample_h4(normal, u, v);
+        c = shade(p, u, v, d, f3{al.x, al.y, al.z}, f3{em.x, em.y, em.z}, f3{nn.x, nn.y, nn.z}, sample_r8(ssao, u, v),
+                  shadow);
+    }
+    row_ptr_w<uint2>(target, y)[x] = pack_h4(c);
+}
+
+bool aligned16(const soc_img& im) {
+    return (reinterpret_cast<uintptr_t>(im.data) & 15u) == 0 && (im.pitch_bytes & 15) == 0;
+}
+
+}  // namespace
+}  // namespace soc
+
+using namespace soc;
+
+extern "C" int soc_composition(const soc_globals* g, const soc_globals* d_globals, soc_img target, soc_img albedo,
+                               soc_img emissive, soc_img normal, soc_img depth, soc_img ssao, soc_img shadow,
+                               soc_img clouds, soc_stream stream) {
+    static const char* P = "soc_composition";
+    if (!g) return set_error(SOC_E_INVALID_ARG, "%s: null globals", P);
+    int rc = check_img(target, SOC_FMT_RGBA16F, P, "target");
+    if (!rc) rc = check_img(albedo, SOC_FMT_RGBA16F, P, "albedo");
+    if (!rc) rc = check_img(emissive, SOC_FMT_RGBA16F, P, "emissive");
+    if (!rc) rc = check_img(normal, SOC_FMT_RGBA16F, P, "normal");
+    if (!rc) rc = check_img(depth, SOC_FMT_D32F, P, "depth");
+    if (!rc) rc = check_img(ssao, SOC_FMT_R8_UNORM, P, "ssao");
+    if (!rc) rc = check_img(shadow, SOC_FMT_D32F, P, "shadow");
+    if (!rc) rc = check_img(clouds, SOC_FMT_RGBA8_UNORM, P, "clouds");
+    if (rc) return rc;
+    CompParams p;
+    p.inv_proj = mat4(g->camera_inverse_projection_matrix);
+    p.inv_view = mat4(g->camera_inverse_view_matrix);
+    mat4_mul_host(p.sun_pv.m, g->sun_info.projection_matrix, g->sun_info.view_matrix);
+    for (int i = 0; i < 3; ++i) {
+        p.sun_dir[i] = g->sun_info.direction[i];
+        p.ambient[i] = g->ambient[i];
+        p.cam[i] = g->camera_position[i];
+    }
+    p.ef = g->sun_info.exponential_factor;
+    p.df = g->sun_info.darkening_factor;
+    p.emissive_strength = g->emissive_bloom_strength;
+    p.ao_strength = g->ambient_occlussion_strength;
+    p.npl = g->point_light_count < SOC_MAX_POINT_LIGHTS ? g->point_light_count : SOC_MAX_POINT_LIGHTS;
+    p.nsl = g->spot_light_count < SOC_MAX_SPOT_LIGHTS ? g->spot_light_count : SOC_MAX_SPOT_LIGHTS;
+    p.dg = d_globals;
+    if ((p.npl || p.nsl) && !d_globals)
+        return set_error(SOC_E_INVALID_ARG, "%s: frame has lights but no device globals (soc_upload_globals)", P);
+
+    const int W = target.width, H = target.height;
+    auto same = [&](const soc_img& im) { return im.width == W && im.height == H; };
+    const bool fast = same(albedo) && same(emissive) && same(normal) && same(depth) && same(clouds) && (W % 2 == 0) &&
+                      W <= 8192 && H <= 8192 && aligned16(target) && aligned16(albedo) && aligned16(emissive) &&
+                      aligned16(normal) && (reinterpret_cast<uintptr_t>(depth.data) & 7u) == 0 && (depth.pitch_bytes & 7) == 0;
+    if (fast) {
+        dim3 blk(BX, BY), grd(ceil_div(W / 2, BX), ceil_div(H, BY));
+        composition_pair<<<grd, blk, 0, hs(stream)>>>(dimg(target), dimg(albedo), dimg(emissive), dimg(normal), dimg(depth),
+                                                      dimg(ssao), dimg(shadow), dimg(clouds), p);
+    } else {
+        dim3 blk(BX, BY), grd(ceil_div(W, BX), ceil_div(H, BY));
+        composition_generic<<<grd, blk, 0, hs(stream)>>>(dimg(target), dimg(albedo), dimg(emissive), dimg(normal),
+                                                         dimg(depth), dimg(ssao), dimg(shadow), dimg(clouds), p);
+    }
+    return check_launch("composition");
+}

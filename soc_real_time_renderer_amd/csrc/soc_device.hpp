@@ -1,0 +1,173 @@
+// soc_device.hpp — device-side helpers shared by the gfx950 pass kernels.
+//
+// Implements the SAMPLING CONTRACT of DESIGN.md §3 (the restatement of the reference's Vulkan
+// linear_sampler / REPEAT sampler and image formats; gfx950 has no texture units, so filtering is
+// VALU work here). Helpers that must be bit-identical to the oracle's arithmetic disable FMA
+// contraction locally (`#pragma clang fp contract(off)`).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace soc {
+
+struct DImg {          // device view of a soc_img
+    char* data;
+    int w, h, pitch;
+};
+
+struct f4 { float x, y, z, w; };
+struct f3 { float x, y, z; };
+
+__device__ __forceinline__ f3 mk3(float x, float y, float z) { return f3{x, y, z}; }
+__device__ __forceinline__ f3 operator+(f3 a, f3 b) { return f3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ f3 operator-(f3 a, f3 b) { return f3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ f3 operator*(f3 a, f3 b) { return f3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+__device__ __forceinline__ f3 operator*(f3 a, float s) { return f3{a.x * s, a.y * s, a.z * s}; }
+__device__ __forceinline__ f3 operator-(f3 a) { return f3{-a.x, -a.y, -a.z}; }
+__device__ __forceinline__ float dot3(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ float length3(f3 a) { return sqrtf(dot3(a, a)); }
+__device__ __forceinline__ f3 normalize3(f3 a) { float l = length3(a); return f3{a.x / l, a.y / l, a.z / l}; }
+__device__ __forceinline__ f3 cross3(f3 a, f3 b) {
+    return f3{a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y};
+}
+__device__ __forceinline__ float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
+__device__ __forceinline__ float mixf(float a, float b, float t) { return a * (1.0f - t) + b * t; }
+__device__ __forceinline__ float fractf(float x) { return x - floorf(x); }
+
+// ---------------------------------------------------------------------------------------------
+// formats
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float h2f(uint16_t h) { return (float)__builtin_bit_cast(_Float16, h); }
+__device__ __forceinline__ uint16_t f2h(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
+
+__device__ __forceinline__ f4 unpack_h4(uint2 v) {
+    return f4{h2f((uint16_t)(v.x & 0xffffu)), h2f((uint16_t)(v.x >> 16)), h2f((uint16_t)(v.y & 0xffffu)),
+              h2f((uint16_t)(v.y >> 16))};
+}
+__device__ __forceinline__ uint2 pack_h4(f4 c) {
+    return uint2{(uint32_t)f2h(c.x) | ((uint32_t)f2h(c.y) << 16), (uint32_t)f2h(c.z) | ((uint32_t)f2h(c.w) << 16)};
+}
+
+__device__ __forceinline__ float unorm8(uint32_t u) { return (float)u * (1.0f / 255.0f); }
+__device__ __forceinline__ uint32_t to_unorm8(float x) { return (uint32_t)rintf(clampf(x, 0.0f, 1.0f) * 255.0f); }
+__device__ __forceinline__ uint32_t pack_unorm8x4(f4 c) {
+    return to_unorm8(c.x) | (to_unorm8(c.y) << 8) | (to_unorm8(c.z) << 16) | (to_unorm8(c.w) << 24);
+}
+
+template <typename T>
+__device__ __forceinline__ const T* row_ptr(const DImg& im, int y) {
+    return reinterpret_cast<const T*>(im.data + (size_t)y * (size_t)im.pitch);
+}
+template <typename T>
+__device__ __forceinline__ T* row_ptr_w(const DImg& im, int y) {
+    return reinterpret_cast<T*>(im.data + (size_t)y * (size_t)im.pitch);
+}
+
+__device__ __forceinline__ f4 fetch_h4(const DImg& im, int x, int y) { return unpack_h4(row_ptr<uint2>(im, y)[x]); }
+__device__ __forceinline__ float fetch_f32(const DImg& im, int x, int y) { return row_ptr<float>(im, y)[x]; }
+__device__ __forceinline__ float fetch_r8(const DImg& im, int x, int y) { return unorm8(row_ptr<uint8_t>(im, y)[x]); }
+__device__ __forceinline__ f4 fetch_rgba8(const DImg& im, int x, int y) {
+    uint32_t v = row_ptr<uint32_t>(im, y)[x];
+    return f4{unorm8(v & 0xffu), unorm8((v >> 8) & 0xffu), unorm8((v >> 16) & 0xffu), unorm8(v >> 24)};
+}
+
+// ---------------------------------------------------------------------------------------------
+// sampling contract (clamp-to-edge, 8-bit sub-texel precision)
+// ---------------------------------------------------------------------------------------------
+// Returns the left tap i0 in [0, n-2] (0 when n == 1) and the weight of tap i0+1 (clamped to n-1).
+// i < 0 maps to (0, w=0) and i >= n-1 to (n-2, w=1): both give the edge texel exactly, as the
+// oracle's "coinciding taps" rule does.
+struct Axis { int i0; int i1; float w; };
+
+__device__ __forceinline__ Axis axis_clamp(float u, int n) {
+#pragma clang fp contract(off)
+    float t = u * (float)n;
+    t = t - 0.5f;
+    t = fminf(fmaxf(t, -2.0f), (float)n + 1.0f);
+    int fx = (int)floorf(t * 256.0f + 0.5f);
+    int i = fx >> 8;
+    float w = (float)(fx & 255) * (1.0f / 256.0f);
+    if (i < 0) { i = 0; w = 0.0f; }
+    else if (i >= n - 1) { i = n - 2; w = 1.0f; }
+    if (n == 1) { i = 0; w = 0.0f; }
+    Axis a;
+    a.i0 = i;
+    a.i1 = min(i + 1, n - 1);
+    a.w = w;
+    return a;
+}
+
+// REPEAT addressing for a power-of-two extent n (mask = n-1).
+__device__ __forceinline__ Axis axis_repeat_pow2(float u, int n, int mask) {
+#pragma clang fp contract(off)
+    float t = u * (float)n;
+    t = t - 0.5f;
+    t = fminf(fmaxf(t, -4194304.0f), 4194304.0f);
+    int fx = (int)floorf(t * 256.0f + 0.5f);
+    int i = fx >> 8;
+    Axis a;
+    a.w = (float)(fx & 255) * (1.0f / 256.0f);
+    a.i0 = i & mask;
+    a.i1 = (i + 1) & mask;
+    return a;
+}
+
+__device__ __forceinline__ float lerp_w(float a, float b, float w) {
+#pragma clang fp contract(off)
+    return a * (1.0f - w) + b * w;
+}
+__device__ __forceinline__ float bilerp1(float a, float b, float c, float d, float wx, float wy) {
+    return lerp_w(lerp_w(a, b, wx), lerp_w(c, d, wx), wy);
+}
+__device__ __forceinline__ f4 bilerp4(f4 a, f4 b, f4 c, f4 d, float wx, float wy) {
+    return f4{bilerp1(a.x, b.x, c.x, d.x, wx, wy), bilerp1(a.y, b.y, c.y, d.y, wx, wy),
+              bilerp1(a.z, b.z, c.z, d.z, wx, wy), bilerp1(a.w, b.w, c.w, d.w, wx, wy)};
+}
+
+__device__ __forceinline__ f4 sample_h4(const DImg& im, float u, float v) {
+    Axis ax = axis_clamp(u, im.w), ay = axis_clamp(v, im.h);
+    const uint2* r0 = row_ptr<uint2>(im, ay.i0);
+    const uint2* r1 = row_ptr<uint2>(im, ay.i1);
+    return bilerp4(unpack_h4(r0[ax.i0]), unpack_h4(r0[ax.i1]), unpack_h4(r1[ax.i0]), unpack_h4(r1[ax.i1]), ax.w, ay.w);
+}
+__device__ __forceinline__ float sample_f32(const DImg& im, float u, float v) {
+    Axis ax = axis_clamp(u, im.w), ay = axis_clamp(v, im.h);
+    const float* r0 = row_ptr<float>(im, ay.i0);
+    const float* r1 = row_ptr<float>(im, ay.i1);
+    return bilerp1(r0[ax.i0], r0[ax.i1], r1[ax.i0], r1[ax.i1], ax.w, ay.w);
+}
+__device__ __forceinline__ float sample_r8(const DImg& im, float u, float v) {
+    Axis ax = axis_clamp(u, im.w), ay = axis_clamp(v, im.h);
+    const uint8_t* r0 = row_ptr<uint8_t>(im, ay.i0);
+    const uint8_t* r1 = row_ptr<uint8_t>(im, ay.i1);
+    return bilerp1(unorm8(r0[ax.i0]), unorm8(r0[ax.i1]), unorm8(r1[ax.i0]), unorm8(r1[ax.i1]), ax.w, ay.w);
+}
+__device__ __forceinline__ f4 sample_rgba8(const DImg& im, float u, float v) {
+    Axis ax = axis_clamp(u, im.w), ay = axis_clamp(v, im.h);
+    return bilerp4(fetch_rgba8(im, ax.i0, ay.i0), fetch_rgba8(im, ax.i1, ay.i0), fetch_rgba8(im, ax.i0, ay.i1),
+                   fetch_rgba8(im, ax.i1, ay.i1), ax.w, ay.w);
+}
+
+// GLSL mat4 * vec4 on a column-major float[16] (kernel-argument copy).
+struct Mat4 { float m[16]; };
+struct Mat3 { float m[9]; };
+
+__device__ __forceinline__ f4 mul(const Mat4& M, f4 v) {
+    const float* m = M.m;
+    return f4{m[0] * v.x + m[4] * v.y + m[8] * v.z + m[12] * v.w, m[1] * v.x + m[5] * v.y + m[9] * v.z + m[13] * v.w,
+              m[2] * v.x + m[6] * v.y + m[10] * v.z + m[14] * v.w, m[3] * v.x + m[7] * v.y + m[11] * v.z + m[15] * v.w};
+}
+__device__ __forceinline__ f3 mul3of4(const Mat4& M, f3 v) {
+    const float* m = M.m;
+    return f3{m[0] * v.x + m[4] * v.y + m[8] * v.z, m[1] * v.x + m[5] * v.y + m[9] * v.z, m[2] * v.x + m[6] * v.y + m[10] * v.z};
+}
+__device__ __forceinline__ f3 mul(const Mat3& M, f3 v) {
+    const float* m = M.m;
+    return f3{m[0] * v.x + m[3] * v.y + m[6] * v.z, m[1] * v.x + m[4] * v.y + m[7] * v.z, m[2] * v.x + m[5] * v.y + m[8] * v.z};
+}
+
+// Pixel-centre uv exactly as the oracle computes it: (x + 0.5) / n, correctly rounded.
+__device__ __forceinline__ float centre_uv(int x, int n) { return ((float)x + 0.5f) / (float)n; }
+
+}  // namespace soc

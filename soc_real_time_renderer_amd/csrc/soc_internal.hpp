@@ -1,0 +1,60 @@
+// soc_internal.hpp — host-side helpers shared by the C-ABI entry points (not part of the ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+
+#include "../../include/soc_rt.h"
+#include "soc_device.hpp"
+
+namespace soc {
+
+// Per-thread last error (soc_last_error_string).
+int set_error(int code, const char* fmt, ...);
+void clear_error();
+
+inline int bytes_per_pixel(int fmt) {
+    switch (fmt) {
+    case SOC_FMT_RGBA16F: return 8;
+    case SOC_FMT_D32F: return 4;
+    case SOC_FMT_R8_UNORM: return 1;
+    case SOC_FMT_RGBA8_UNORM:
+    case SOC_FMT_RGBA8_SRGB: return 4;
+    case SOC_FMT_RGBA32F: return 16;
+    default: return 0;
+    }
+}
+
+inline bool img_ok(const soc_img& im) {
+    int b = bytes_per_pixel(im.format);
+    return im.data != nullptr && im.width > 0 && im.height > 0 && b > 0 && im.pitch_bytes >= im.width * b;
+}
+
+// Validates `im` (and its format when fmt > 0); sets the error string on failure.
+int check_img(const soc_img& im, int fmt, const char* pass, const char* what);
+
+inline DImg dimg(const soc_img& im) { return DImg{static_cast<char*>(im.data), im.width, im.height, im.pitch_bytes}; }
+
+inline Mat4 mat4(const float* m) {
+    Mat4 r;
+    for (int i = 0; i < 16; ++i) r.m[i] = m[i];
+    return r;
+}
+
+inline hipStream_t hs(soc_stream s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Checks the launch that was just issued.
+int check_launch(const char* pass);
+
+inline unsigned ceil_div(unsigned a, unsigned b) { return (a + b - 1) / b; }
+
+// Host fp32 restatements shared with the tone-mapping launcher (bit-identical to the oracle's
+// float code: compiled without FMA contraction).
+void agx_matrices(float compression, float M[9], float Minv[9]);
+void mat4_mul_host(float out[16], const float a[16], const float b[16]);
+
+}  // namespace soc

@@ -1,0 +1,191 @@
+// taa.hip — TemporalAntiAliasingTask (src/graphics/tasks/temporal_antialiasing.inl:54-116, shader
+// :137-190) and CopyImageTask (:16-37) as gfx950 kernels.
+//
+// One lane per output pixel, 64x4 workgroups (a wave reads 3 consecutive 512-B row segments of the
+// colour and depth images; the 3x3 neighbourhood re-reads come from L1). The history copies of the
+// reference graph (renderer.cpp:1182-1198) are removed: the resolved colour ping-pongs between two
+// images owned by the caller, and the current velocity is written to the next frame's velocity
+// history from inside this kernel (velocity_history_out), which saves the separate 16 B/px copy.
+#include "soc_internal.hpp"
+
+namespace soc {
+namespace {
+
+struct TaaParams {
+    float pox, poy;     // 1 / resolution
+    float accum0;       // min(0.1, frame_counter)
+};
+
+constexpr int BX = 64, BY = 4;
+
+__device__ __forceinline__ f4 min4(f4 a, f4 b) { return f4{fminf(a.x, b.x), fminf(a.y, b.y), fminf(a.z, b.z), fminf(a.w, b.w)}; }
+__device__ __forceinline__ f4 max4(f4 a, f4 b) { return f4{fmaxf(a.x, b.x), fmaxf(a.y, b.y), fmaxf(a.z, b.z), fmaxf(a.w, b.w)}; }
+
+// Tail of the shader after the neighbourhood loop (:172-189).
+__device__ __forceinline__ f4 resolve(const TaaParams& p, float u, float v, f4 color, f4 mn, f4 mx, f4 blurred, float2 vel,
+                                      const DImg& prev, const DImg& pvel) {
+    float accum = p.accum0;
+    const float vx = u - vel.x, vy = v - vel.y;
+    f4 acc = sample_h4(prev, vx, vy);
+    if (vx < 0.0f || vy < 0.0f || vx > 1.0f || vy > 1.0f) accum = 1.0f;
+    acc = f4{clampf(acc.x, mn.x, mx.x), clampf(acc.y, mn.y, mx.y), clampf(acc.z, mn.z, mx.z), clampf(acc.w, mn.w, mx.w)};
+    f4 o = f4{color.x * accum + acc.x * (1.0f - accum), color.y * accum + acc.y * (1.0f - accum),
+              color.z * accum + acc.z * (1.0f - accum), color.w * accum + acc.w * (1.0f - accum)};
+    const f4 pv = sample_h4(pvel, vx, vy);
+    const float dvx = pv.x - vel.x, dvy = pv.y - vel.y;
+    const float vlen = sqrtf(dvx * dvx + dvy * dvy);
+    const float dis = clampf((vlen - 0.001f) * 10.0f, 0.0f, 1.0f);
+    return f4{mixf(o.x, blurred.x, dis), mixf(o.y, blurred.y, dis), mixf(o.z, blurred.z, dis), mixf(o.w, blurred.w, dis)};
+}
+
+__device__ __forceinline__ float gauss_w(int idx) {
+    // 1/16 1/8 1/16 / 1/8 1/4 1/8 / 1/16 1/8 1/16
+    return (idx == 4) ? 0.25f : ((idx & 1) ? 0.125f : 0.0625f);
+}
+
+// Fast path: colour, depth and velocity have the target extent (== resolution): every neighbourhood
+// tap is a texel centre (clamped at the border), so plain loads replace the bilinear samples.
+__global__ __launch_bounds__(256) void taa_fast(DImg target, DImg cur, DImg prev, DImg vel, DImg pvel, DImg depth,
+                                                DImg vel_out, TaaParams p) {
+    const int x = blockIdx.x * BX + threadIdx.x, y = blockIdx.y * BY + threadIdx.y;
+    if (x >= target.w || y >= target.h) return;
+    const float u = centre_uv(x, target.w), v = centre_uv(y, target.h);
+    f4 nb5 = f4{0, 0, 0, 0};
+    f4 blurred = f4{0, 0, 0, 0};
+    f4 mn = f4{10.0e5f, 10.0e5f, 10.0e5f, 10.0e5f}, mx = f4{-10.0e5f, -10.0e5f, -10.0e5f, -10.0e5f};
+    float closest = 1.0f;
+    int bx = x, by = y;
+#pragma unroll
+    for (int oy = 1; oy > -2; --oy) {
+        const int sy = min(max(y + oy, 0), target.h - 1);
+        const uint2* crow = row_ptr<uint2>(cur, sy);
+        const float* drow = row_ptr<float>(depth, sy);
+#pragma unroll
+        for (int ox = 1; ox > -2; --ox) {
+            const int idx = (oy + 1) * 3 + (ox + 1);
+            const int sx = min(max(x + ox, 0), target.w - 1);
+            const f4 c = unpack_h4(crow[sx]);
+            const float d = drow[sx];
+            closest = fminf(d, closest);
+            if (closest == d) { bx = sx; by = sy; }
+            mn = min4(c, mn);
+            mx = max4(c, mx);
+            const float gw = gauss_w(idx);
+            blurred = f4{blurred.x + gw * c.x, blurred.y + gw * c.y, blurred.z + gw * c.z, blurred.w + gw * c.w};
+            if (idx == 5) nb5 = c;   // quirk Q7: the (+1, 0) neighbour is "the" colour
+        }
+    }
+    const f4 vv = fetch_h4(vel, bx, by);
+    const f4 o = resolve(p, u, v, nb5, mn, mx, blurred, float2{vv.x, vv.y}, prev, pvel);
+    row_ptr_w<uint2>(target, y)[x] = pack_h4(o);
+    if (vel_out.data) row_ptr_w<uint2>(vel_out, y)[x] = row_ptr<uint2>(vel, y)[x];
+}
+
+__global__ __launch_bounds__(256) void taa_generic(DImg target, DImg cur, DImg prev, DImg vel, DImg pvel, DImg depth,
+                                                   DImg vel_out, TaaParams p) {
+    const int x = blockIdx.x * BX + threadIdx.x, y = blockIdx.y * BY + threadIdx.y;
+    if (x >= target.w || y >= target.h) return;
+    const float u = centre_uv(x, target.w), v = centre_uv(y, target.h);
+    f4 nb5 = f4{0, 0, 0, 0}, blurred = f4{0, 0, 0, 0};
+    f4 mn = f4{10.0e5f, 10.0e5f, 10.0e5f, 10.0e5f}, mx = f4{-10.0e5f, -10.0e5f, -10.0e5f, -10.0e5f};
+    float closest = 1.0f, du = u, dv = v;
+    for (int oy = 1; oy > -2; --oy)
+        for (int ox = 1; ox > -2; --ox) {
+            const int idx = (oy + 1) * 3 + (ox + 1);
+            const float su = u + p.pox * (float)ox, sv = v + p.poy * (float)oy;
+            const f4 c = sample_h4(cur, su, sv);
+            const float d = sample_f32(depth, su, sv);
+            closest = fminf(d, closest);
+            if (closest == d) { du = su; dv = sv; }
+            mn = min4(c, mn);
+            mx = max4(c, mx);
+            const float gw = gauss_w(idx);
+            blurred = f4{blurred.x + gw * c.x, blurred.y + gw * c.y, blurred.z + gw * c.z, blurred.w + gw * c.w};
+            if (idx == 5) nb5 = c;
+        }
+    const f4 vv = sample_h4(vel, du, dv);
+    const f4 o = resolve(p, u, v, nb5, mn, mx, blurred, float2{vv.x, vv.y}, prev, pvel);
+    row_ptr_w<uint2>(target, y)[x] = pack_h4(o);
+    if (vel_out.data && x < vel.w && y < vel.h) row_ptr_w<uint2>(vel_out, y)[x] = row_ptr<uint2>(vel, y)[x];
+}
+
+__global__ __launch_bounds__(256) void copy_rows(const char* __restrict__ src, int spitch, char* __restrict__ dst,
+                                                 int dpitch, int row_bytes, int rows) {
+    const int y = blockIdx.y;
+    if (y >= rows) return;
+    const char* s = src + (size_t)y * spitch;
+    char* d = dst + (size_t)y * dpitch;
+    for (int i = (blockIdx.x * 256 + threadIdx.x) * 16; i < row_bytes; i += gridDim.x * 256 * 16) {
+        if (i + 16 <= row_bytes)
+            *reinterpret_cast<uint4*>(d + i) = *reinterpret_cast<const uint4*>(s + i);
+        else
+            for (int k = i; k < row_bytes; ++k) d[k] = s[k];
+    }
+}
+
+}  // namespace
+}  // namespace soc
+
+using namespace soc;
+
+extern "C" int soc_temporal_antialiasing(const soc_globals* g, soc_img target, soc_img current_color, soc_img previous_color,
+                                         soc_img current_velocity, soc_img previous_velocity, soc_img depth,
+                                         soc_img velocity_history_out, soc_stream stream) {
+    static const char* P = "soc_temporal_antialiasing";
+    if (!g) return set_error(SOC_E_INVALID_ARG, "%s: null globals", P);
+    int rc = check_img(target, SOC_FMT_RGBA16F, P, "target");
+    if (!rc) rc = check_img(current_color, SOC_FMT_RGBA16F, P, "current_color");
+    if (!rc) rc = check_img(previous_color, SOC_FMT_RGBA16F, P, "previous_color");
+    if (!rc) rc = check_img(current_velocity, SOC_FMT_RGBA16F, P, "current_velocity");
+    if (!rc) rc = check_img(previous_velocity, SOC_FMT_RGBA16F, P, "previous_velocity");
+    if (!rc) rc = check_img(depth, SOC_FMT_D32F, P, "depth");
+    if (rc) return rc;
+    if (target.data == current_color.data || target.data == previous_color.data)
+        return set_error(SOC_E_INVALID_ARG, "%s: target aliases an input", P);
+    if (velocity_history_out.data) {
+        rc = check_img(velocity_history_out, SOC_FMT_RGBA16F, P, "velocity_history_out");
+        if (rc) return rc;
+        if (velocity_history_out.data == previous_velocity.data || velocity_history_out.data == current_velocity.data)
+            return set_error(SOC_E_INVALID_ARG, "%s: velocity_history_out aliases a velocity input", P);
+        if (velocity_history_out.width != current_velocity.width || velocity_history_out.height != current_velocity.height)
+            return set_error(SOC_E_SHAPE, "%s: velocity_history_out extent != current_velocity extent", P);
+    }
+    TaaParams p;
+    p.pox = 1.0f / (float)g->resolution[0];
+    p.poy = 1.0f / (float)g->resolution[1];
+    p.accum0 = fminf(0.1f, (float)g->frame_counter);
+    const int W = target.width, H = target.height;
+    auto same = [&](const soc_img& im) { return im.width == W && im.height == H; };
+    const bool fast = W == g->resolution[0] && H == g->resolution[1] && same(current_color) && same(depth) &&
+                      same(current_velocity) && W <= 8192 && H <= 8192;
+    dim3 blk(BX, BY), grd(ceil_div(W, BX), ceil_div(H, BY));
+    DImg vo = velocity_history_out.data ? dimg(velocity_history_out) : DImg{nullptr, 0, 0, 0};
+    if (fast)
+        taa_fast<<<grd, blk, 0, hs(stream)>>>(dimg(target), dimg(current_color), dimg(previous_color), dimg(current_velocity),
+                                              dimg(previous_velocity), dimg(depth), vo, p);
+    else
+        taa_generic<<<grd, blk, 0, hs(stream)>>>(dimg(target), dimg(current_color), dimg(previous_color),
+                                                 dimg(current_velocity), dimg(previous_velocity), dimg(depth), vo, p);
+    return check_launch("temporal_antialiasing");
+}
+
+extern "C" int soc_copy_image(soc_img target, soc_img source, soc_stream stream) {
+    int rc = check_img(target, 0, "soc_copy_image", "target");
+    if (!rc) rc = check_img(source, 0, "soc_copy_image", "source");
+    if (rc) return rc;
+    if (target.format != source.format || target.width != source.width || target.height != source.height)
+        return set_error(SOC_E_SHAPE, "soc_copy_image: format/extent mismatch");
+    const int row_bytes = source.width * bytes_per_pixel(source.format);
+    const bool vec = ((reinterpret_cast<uintptr_t>(source.data) | reinterpret_cast<uintptr_t>(target.data)) & 15u) == 0 &&
+                     (source.pitch_bytes & 15) == 0 && (target.pitch_bytes & 15) == 0;
+    if (!vec) {
+        hipError_t e = hipMemcpy2DAsync(target.data, target.pitch_bytes, source.data, source.pitch_bytes, row_bytes,
+                                        source.height, hipMemcpyDeviceToDevice, hs(stream));
+        if (e != hipSuccess) return set_error(SOC_E_HIP, "soc_copy_image: %s", hipGetErrorString(e));
+        return SOC_OK;
+    }
+    dim3 grd(ceil_div(ceil_div(row_bytes, 16), 256), source.height);
+    copy_rows<<<grd, 256, 0, hs(stream)>>>(static_cast<const char*>(source.data), source.pitch_bytes,
+                                           static_cast<char*>(target.data), target.pitch_bytes, row_bytes, source.height);
+    return check_launch("copy_image");
+}

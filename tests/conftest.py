@@ -1,0 +1,27 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP pass library)")
+
+
+@pytest.fixture(scope="session")
+def soc():
+    import soc_real_time_renderer_amd as m
+    m.lib()
+    return m
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    import oracle as o
+    o.lib()
+    return o

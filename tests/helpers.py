@@ -1,0 +1,76 @@
+"""Shared test helpers: seeded inputs, host frame layout, tolerance checks."""
+import ctypes as C
+
+import numpy as np
+
+import soc_real_time_renderer_amd as soc
+from soc_real_time_renderer_amd import scene
+
+SPONZA_CAMERA = ((-14.0, 2.2, 0.3), (0.0, -0.42, 0.0))
+
+
+def globals_for(W, H, frames=2, camera=SPONZA_CAMERA, dt=0.016, move=0.05, elapsed=None, frame_counter=None):
+    g = soc.globals_defaults(W, H)
+    cam = soc.make_camera(*camera)
+    ji = C.c_uint32(0)
+    for _ in range(frames):
+        soc.frame_update(g, cam, W, H, dt, ji)
+        cam.position[0] += move
+    if elapsed is not None:
+        g.elapsed_time = elapsed
+    if frame_counter is not None:
+        g.frame_counter = frame_counter
+    return g
+
+
+def sponza_inputs(W, H, shadow_size=512, **kw):
+    g = globals_for(W, H, **kw)
+    gb = scene.gbuffer(g, W, H)
+    gb["shadow"] = scene.shadow_map(g, shadow_size)
+    gb["noise"] = scene.noise_texture()
+    return g, gb
+
+
+def random_shadow(size, seed):
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:size, 0:size].astype(np.float32)
+    s = 0.5 + 0.4 * np.sin(xx / 9.0) * np.cos(yy / 13.0) + rng.uniform(-0.02, 0.02, (size, size))
+    return s.astype(np.float32)
+
+
+def random_rgba16(H, W, seed, lo=0.0, hi=4.0, alpha=1.0):
+    rng = np.random.default_rng(seed)
+    a = rng.uniform(lo, hi, (H, W, 4)).astype(np.float32)
+    if alpha is not None:
+        a[..., 3] = alpha
+    return a.astype(np.float16)
+
+
+def f16_close(a, b, atol=1e-3, rtol=2e-3):
+    """|a-b| <= atol + rtol*|b| on RGBA16F images (float16 arrays); NaNs must match."""
+    a = np.asarray(a, np.float32)
+    b = np.asarray(b, np.float32)
+    nan = np.isnan(a) | np.isnan(b)
+    assert (np.isnan(a) == np.isnan(b)).all(), "NaN pattern differs"
+    d = np.abs(a - b)
+    ok = (d <= atol + rtol * np.abs(b)) | nan
+    return ok
+
+
+def host_frame(W, H, gb, output_format=soc.FMT_RGBA8_UNORM):
+    fr = {k: gb[k].copy() for k in ("albedo", "emissive", "normal", "velocity", "depth", "shadow", "noise")}
+    fr["bloom_mips"] = [np.zeros((max(H >> i, 1), max(W >> i, 1), 4), np.float16) for i in range(4)]
+    fr["ssao"] = np.zeros((H // 2, W // 2), np.uint8)
+    fr["ssao_blur"] = np.zeros((H // 2, W // 2), np.uint8)
+    fr["clouds"] = np.zeros((H, W, 4), np.uint8)
+    fr["color"] = np.zeros((H, W, 4), np.float16)
+    fr["history_color"] = [np.zeros((H, W, 4), np.float16) for _ in range(2)]
+    fr["history_velocity"] = [np.zeros((H, W, 4), np.float16) for _ in range(2)]
+    if output_format in (soc.FMT_RGBA8_UNORM, soc.FMT_RGBA8_SRGB):
+        fr["output"] = np.zeros((H, W, 4), np.uint8)
+    elif output_format == soc.FMT_RGBA16F:
+        fr["output"] = np.zeros((H, W, 4), np.float16)
+    else:
+        fr["output"] = np.zeros((H, W, 4), np.float32)
+    fr["output_format"] = output_format
+    return fr

@@ -1,0 +1,82 @@
+"""C-ABI checks (CPU only): the HIP library loads, exports every function include/soc_rt.h declares, and
+its struct layouts match the ctypes mirror. No kernel is launched."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "soc_rt.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    src = re.sub(r"//[^\n]*", "", src)
+    names = set(re.findall(r"\b(soc_[a-z0-9_]+)\s*\(", src))
+    return sorted(names)
+
+
+def test_header_declares_the_pass_api():
+    names = declared_functions()
+    for must in ("soc_composition", "soc_ssao_generation", "soc_ssao_blur", "soc_bloom_downsample", "soc_bloom_upsample",
+                 "soc_cloud_rendering", "soc_generate_luminance_histogram", "soc_resolve_luminance_histogram",
+                 "soc_temporal_antialiasing", "soc_tone_mapping", "soc_last_error_string", "soc_renderer_execute"):
+        assert must in names
+
+
+def test_every_declared_symbol_is_exported(soc):
+    lib = soc.lib()
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_ctypes_table_covers_header():
+    from soc_real_time_renderer_amd import _abi
+    assert set(declared_functions()) == set(_abi.FUNCTIONS)
+
+
+@pytest.mark.parametrize("name", ["soc_img", "soc_globals", "soc_sun_info", "soc_point_light", "soc_spot_light",
+                                  "soc_auto_exposure", "soc_camera", "soc_frame_images"])
+def test_struct_sizes(soc, name):
+    from soc_real_time_renderer_amd import _abi
+    assert soc.lib().soc_abi_sizeof(name.encode()) == C.sizeof(_abi.STRUCTS[name])
+
+
+def test_struct_offsets(soc):
+    from soc_real_time_renderer_amd import _abi
+    lib = soc.lib()
+    checked = 0
+    for tname, st in _abi.STRUCTS.items():
+        for fname, _ in st._fields_:
+            off = lib.soc_abi_offsetof(tname.encode(), fname.encode())
+            assert off == getattr(st, fname).offset, (tname, fname)
+            checked += 1
+    assert checked > 100
+
+
+def test_abi_version_and_arch(soc):
+    lib = soc.lib()
+    assert lib.soc_abi_version() == 1
+    assert lib.soc_device_arch() == b"gfx950"
+
+
+def test_argument_errors_without_gpu(soc):
+    """Validation happens before any HIP call: bad images return SOC_E_INVALID_ARG with a message."""
+    g = soc.globals_defaults(64, 36)
+    bad = soc.SocImg(None, 0, 0, 0, 0)
+    rc = soc.lib().soc_ssao_blur(C.byref(g), bad, bad, None)
+    assert rc == soc._abi.SOC_E_INVALID_ARG
+    assert b"soc_ssao_blur" in soc.lib().soc_last_error_string()
+    with pytest.raises(soc.SocError):
+        soc.cloud_rendering(g, None, None, None, stream=0)
+
+
+def test_library_is_a_gfx950_code_object():
+    """The in-tree .so carries a gfx950 offload bundle (built by __graft_entry__.build)."""
+    so = os.path.join(ROOT, "soc_real_time_renderer_amd", "lib", "libsoc_rt.so")
+    data = open(so, "rb").read()
+    assert b"gfx950" in data
+    assert b"__hip_fatbin" in data or b"HIP_FATBIN" in data or b".hip_fatbin" in data

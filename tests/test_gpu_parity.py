@@ -1,0 +1,313 @@
+"""Parity of every HIP pass against the CPU oracle, called through the C ABI (-m gpu).
+
+Tolerances: bloom, SSAO blur and the histogram are bit-exact; RGBA16F outputs
+|d| <= 1e-3 + 2e-3|ref|; SSAO R8 within 2/255 on >= 99.5 % of pixels and mean |d| <= 0.5/255;
+exposure |d| <= 1e-5; tone-mapped RGBA8 within 1 level on >= 99.9 %; clouds RGBA8 within 2 levels on
+>= 99.5 %.
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import (f16_close, globals_for, host_frame, random_rgba16, random_shadow, sponza_inputs)
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+SIZES = [(64, 36), (97, 55), (512, 512), (1920, 1080)]
+
+
+# ------------------------------------------------------------------------------------------------ bloom
+@pytest.mark.parametrize("W,H", SIZES)
+def test_bloom_passes_bit_exact(soc, oracle, W, H):
+    g = globals_for(W, H)
+    src = random_rgba16(H, W, seed=W)
+    dims = [(max(W >> i, 1), max(H >> i, 1)) for i in range(4)]
+    # down: emissive -> mip0 (1:1), mip0 -> mip1 (2:1 when even)
+    for (sw, sh), (dw, dh) in [((W, H), dims[0]), (dims[0], dims[1]), (dims[1], dims[2])]:
+        s = random_rgba16(sh, sw, seed=sw * 7 + sh)
+        ref = np.zeros((dh, dw, 4), np.float16)
+        oracle.bloom_downsample(g, s, ref)
+        out = torch.zeros(dh, dw, 4, dtype=torch.float16, device=DEV)
+        soc.bloom_downsample(g, dev(s), out)
+        got = host(out)
+        assert np.array_equal(got[..., :3].view(np.uint16), ref[..., :3].view(np.uint16)), (sw, sh, dw, dh)
+    # up: mip1 -> mip0 (1:2), mip0 -> emissive (1:1)
+    for (sw, sh), (dw, dh) in [(dims[1], dims[0]), (dims[0], (W, H)), (dims[3], dims[2])]:
+        s = random_rgba16(sh, sw, seed=sw * 3 + sh)
+        ref = np.zeros((dh, dw, 4), np.float16)
+        oracle.bloom_upsample(g, s, ref)
+        out = torch.zeros(dh, dw, 4, dtype=torch.float16, device=DEV)
+        soc.bloom_upsample(g, dev(s), out)
+        got = host(out)
+        assert np.array_equal(got[..., :3].view(np.uint16), ref[..., :3].view(np.uint16)), (sw, sh, dw, dh)
+    del src
+
+
+@pytest.mark.parametrize("W,H", [(64, 36), (1920, 1080)])
+def test_bloom_fast_paths_equal_generic(soc, W, H):
+    """The analytic 1:1 / 2:1 / 1:2 tap paths give the same bits as the float-uv generic path."""
+    import ctypes as C
+    lib = soc.lib()
+    for up, (sw, sh), (dw, dh) in [(0, (W, H), (W, H)), (0, (W, H), (W // 2, H // 2)), (1, (W // 2, H // 2), (W, H)),
+                                   (1, (W, H), (W, H))]:
+        s = dev(random_rgba16(sh, sw, seed=dw + 11 * up))
+        a = torch.zeros(dh, dw, 4, dtype=torch.float16, device=DEV)
+        b = torch.zeros_like(a)
+        g = globals_for(W, H)
+        (soc.bloom_upsample if up else soc.bloom_downsample)(g, s, a)
+        rc = lib.soc_debug_bloom_generic(up, soc.img(s), soc.img(b), torch.cuda.current_stream().cuda_stream)
+        assert rc == 0
+        assert torch.equal(a[..., :3].view(torch.int16), b[..., :3].view(torch.int16))
+        del C
+
+
+@pytest.mark.parametrize("W,H", [(64, 36), (512, 512), (1920, 1080)])
+def test_bloom_chain_bit_exact(soc, oracle, W, H):
+    g = globals_for(W, H)
+    em = random_rgba16(H, W, seed=5, hi=8.0)
+    mips_h = [np.zeros((max(H >> i, 1), max(W >> i, 1), 4), np.float16) for i in range(4)]
+    em_h = em.copy()
+    oracle.bloom_chain(g, em_h, mips_h)
+    em_d = dev(em)
+    mips_d = [torch.zeros(m.shape, dtype=torch.float16, device=DEV) for m in mips_h]
+    soc.bloom_chain(g, em_d, mips_d)
+    assert np.array_equal(host(em_d)[..., :3].view(np.uint16), em_h[..., :3].view(np.uint16))
+
+
+# ------------------------------------------------------------------------------------------------ ssao
+@pytest.mark.parametrize("W,H", [(128, 72), (97, 55), (1920, 1080)])
+def test_ssao_generation(soc, oracle, W, H):
+    g, gb = sponza_inputs(W, H)
+    ref = np.zeros((H // 2, W // 2), np.uint8)
+    oracle.ssao_generation(g, gb["depth"], gb["normal"], ref)
+    out = torch.zeros(H // 2, W // 2, dtype=torch.uint8, device=DEV)
+    soc.ssao_generation(g, dev(gb["depth"]), dev(gb["normal"]), out)
+    d = np.abs(host(out).astype(np.int32) - ref.astype(np.int32))
+    assert (d <= 2).mean() >= 0.995, (d.max(), (d <= 2).mean())
+    assert d.mean() <= 0.5, d.mean()
+
+
+def test_ssao_noise_table_is_bit_identical(soc):
+    W, H = 256, 144
+    g, gb = sponza_inputs(W, H)
+    depth, normal = dev(gb["depth"]), dev(gb["normal"])
+    a = torch.zeros(H // 2, W // 2, dtype=torch.uint8, device=DEV)
+    b = torch.zeros_like(a)
+    table = torch.zeros((H // 2) * (W // 2) * 2, dtype=torch.float32, device=DEV)
+    soc.ssao_prepare_noise(normal, a, table)
+    soc.ssao_generation(g, depth, normal, a, table)
+    soc.ssao_generation(g, depth, normal, b, None)
+    assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("W,H", [(64, 36), (97, 55), (1920, 1080)])
+def test_ssao_blur_bit_exact(soc, oracle, W, H):
+    g = globals_for(W, H)
+    rng = np.random.default_rng(3)
+    src = rng.integers(0, 256, (H // 2, W // 2), dtype=np.uint8)
+    ref = np.zeros_like(src)
+    oracle.ssao_blur(g, src, ref)
+    out = torch.zeros_like(dev(src))
+    soc.ssao_blur(g, dev(src), out)
+    assert np.array_equal(host(out), ref)
+
+
+# ------------------------------------------------------------------------------------------------ composition
+@pytest.mark.parametrize("W,H", [(64, 36), (97, 55), (512, 288), (1920, 1080)])
+@pytest.mark.parametrize("lights", [0, 3])
+def test_composition(soc, oracle, W, H, lights):
+    g, gb = sponza_inputs(W, H)
+    shadow = random_shadow(256, seed=W)
+    rng = np.random.default_rng(W + lights)
+    ssao = rng.integers(120, 256, (H // 2, W // 2), dtype=np.uint8)
+    clouds = rng.integers(0, 256, (H, W, 4), dtype=np.uint8)
+    g.point_light_count = lights
+    g.spot_light_count = lights
+    for i in range(lights):
+        pl = g.point_lights[i]
+        pl.position[:] = [-10.0 + 5 * i, 2.0, 0.5 * i]
+        pl.color[:] = [1.0, 0.8, 0.6]
+        pl.intensity = 3.0
+        sl = g.spot_lights[i]
+        sl.position[:] = [-6.0 + 4 * i, 4.0, -1.0]
+        sl.direction[:] = [0.3, -1.0, 0.1]
+        sl.color[:] = [0.5, 0.7, 1.0]
+        sl.intensity = 5.0
+        sl.cut_off, sl.outer_cut_off = 0.95, 0.85
+    ref = np.zeros((H, W, 4), np.float16)
+    oracle.composition(g, ref, gb["albedo"], gb["emissive"], gb["normal"], gb["depth"], ssao, shadow, clouds)
+    dg = soc.globals_device_buffer()
+    soc.upload_globals(g, dg)
+    out = torch.zeros(H, W, 4, dtype=torch.float16, device=DEV)
+    soc.composition(g, out, dev(gb["albedo"]), dev(gb["emissive"]), dev(gb["normal"]), dev(gb["depth"]), dev(ssao),
+                    dev(shadow), dev(clouds), d_globals=dg)
+    got = host(out)
+    ok = f16_close(got, ref)
+    assert ok.all(), (ok.mean(), np.argwhere(~ok)[:5])
+    sky = gb["depth"] == 1.0
+    assert np.array_equal(got[sky].view(np.uint16), ref[sky].view(np.uint16))   # sky = clouds texel, exact
+
+
+# ------------------------------------------------------------------------------------------------ exposure
+@pytest.mark.parametrize("W,H", [(64, 36), (97, 55), (1920, 1080), (3840, 2160)])
+def test_histogram_bit_exact(soc, oracle, W, H):
+    g = globals_for(W, H)
+    rng = np.random.default_rng(W)
+    img = np.exp(rng.normal(-1.0, 3.0, (H, W, 4))).astype(np.float16)
+    img[rng.uniform(size=(H, W)) < 0.05] = 0.0          # black pixels -> bin 255 (quirk Q9)
+    img[0, 0] = np.float16(np.nan)
+    ae = soc.AutoExposure()
+    oracle.generate_luminance_histogram(g, img, ae)
+    ref = np.array(ae.histogram_buckets, np.int64)
+    buf = soc.auto_exposure_buffer()
+    soc.generate_luminance_histogram(g, dev(img), buf)
+    got = host(buf)[1:].astype(np.int64)
+    assert got.sum() == W * H
+    assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("wide", [False, True])
+def test_resolve(soc, oracle, wide):
+    g = globals_for(640, 360)
+    rng = np.random.default_rng(1)
+    bins = rng.integers(0, 3000, 256).astype(np.uint32)
+    ae = soc.AutoExposure()
+    ae.exposure = 0.37
+    ae.histogram_buckets[:] = [int(b) for b in bins]
+    total = 640 * 360 * (8 if wide else 1)
+    oracle.resolve_luminance_histogram(g, ae, total if wide else 0, wide)
+    buf = soc.auto_exposure_buffer(exposure=0.37)
+    buf[1:] = torch.from_numpy(bins.astype(np.int32)).to(DEV)
+    soc.resolve_luminance_histogram(g, buf, total if wide else 0, wide)
+    assert abs(soc.exposure_of(buf) - ae.exposure) <= 1e-5
+    assert int(host(buf)[1:].sum()) == 0
+
+
+# ------------------------------------------------------------------------------------------------ TAA
+@pytest.mark.parametrize("W,H", [(64, 36), (97, 55), (1920, 1080)])
+def test_taa(soc, oracle, W, H):
+    g, gb = sponza_inputs(W, H)
+    cur = random_rgba16(H, W, seed=1, hi=3.0)
+    prev = random_rgba16(H, W, seed=2, hi=3.0)
+    pvel = gb["velocity"].copy()
+    pvel[..., :2] += np.float16(0.0015)
+    ref = np.zeros((H, W, 4), np.float16)
+    oracle.temporal_antialiasing(g, ref, cur, prev, gb["velocity"], pvel, gb["depth"])
+    out = torch.zeros(H, W, 4, dtype=torch.float16, device=DEV)
+    vout = torch.zeros(H, W, 4, dtype=torch.float16, device=DEV)
+    soc.temporal_antialiasing(g, out, dev(cur), dev(prev), dev(gb["velocity"]), dev(pvel), dev(gb["depth"]), vout)
+    ok = f16_close(host(out), ref)
+    assert ok.all(), ok.mean()
+    assert np.array_equal(host(vout).view(np.uint16), gb["velocity"].view(np.uint16))
+
+
+# ------------------------------------------------------------------------------------------------ tone mapping
+@pytest.mark.parametrize("W,H", [(64, 36), (97, 55), (1920, 1080)])
+@pytest.mark.parametrize("fmt", ["RGBA8_UNORM", "RGBA32F", "RGBA8_SRGB"])
+def test_tone_mapping(soc, oracle, W, H, fmt):
+    g = globals_for(W, H)
+    img = random_rgba16(H, W, seed=4, lo=-0.5, hi=6.0)
+    ae = soc.AutoExposure()
+    ae.exposure = -0.8
+    F = getattr(soc, "FMT_" + fmt)
+    if fmt == "RGBA32F":
+        ref = np.zeros((H, W, 4), np.float32)
+        out = torch.zeros(H, W, 4, dtype=torch.float32, device=DEV)
+    else:
+        ref = np.zeros((H, W, 4), np.uint8)
+        out = torch.zeros(H, W, 4, dtype=torch.uint8, device=DEV)
+    oracle.tone_mapping(g, img, ae, ref, F)
+    soc.tone_mapping(g, dev(img), soc.auto_exposure_buffer(exposure=-0.8), out, F)
+    got = host(out)
+    if fmt == "RGBA32F":
+        assert np.abs(got - ref).max() <= 2e-3
+    else:
+        d = np.abs(got.astype(np.int32) - ref.astype(np.int32))
+        assert (d <= 1).mean() >= 0.999 and d.max() <= 2
+
+
+# ------------------------------------------------------------------------------------------------ clouds
+@pytest.mark.parametrize("W,H,pitch", [(96, 64, -0.42), (160, 90, -0.9), (480, 270, -0.42)])
+def test_clouds(soc, oracle, W, H, pitch):
+    g, gb = sponza_inputs(W, H, camera=((-14.0, 2.2, 0.3), (0.0, pitch, 0.0)), elapsed=10.0)
+    ref = np.zeros((H, W, 4), np.uint8)
+    oracle.cloud_rendering(g, gb["depth"], gb["noise"], ref)
+    out = torch.zeros(H, W, 4, dtype=torch.uint8, device=DEV)
+    soc.cloud_rendering(g, dev(gb["depth"]), dev(gb["noise"]), out)
+    d = np.abs(host(out).astype(np.int32) - ref.astype(np.int32))
+    assert (d <= 2).mean() >= 0.995, ((d <= 2).mean(), d.max())
+    nonsky = gb["depth"] < 1.0
+    assert (host(out)[nonsky][:, :3] == np.array([51, 102, 255], np.uint8)).all()
+
+
+# ------------------------------------------------------------------------------------------------ full frame
+@pytest.mark.parametrize("W,H,frames", [(256, 144, 3), (1920, 1080, 2)])
+def test_render_graph_frames(soc, oracle, W, H, frames):
+    """Multi-frame render graph (ping-pong TAA history, fused velocity history) vs the oracle frame."""
+    g, gb = sponza_inputs(W, H, elapsed=10.0)
+    fr = soc.alloc_frame(W, H, DEV)
+    for k in ("albedo", "emissive", "normal", "velocity", "depth"):
+        fr[k].copy_(torch.from_numpy(gb[k]))
+    fr["shadow"] = dev(gb["shadow"])
+    fr["noise"].copy_(torch.from_numpy(gb["noise"]))
+    r = soc.Renderer(fr, timing=True)
+    hf = host_frame(W, H, gb)
+    ae = soc.AutoExposure()
+    hist = 0
+    for f in range(frames):
+        emis = dev(gb["emissive"])           # bloom overwrites emissive each frame (quirk Q5)
+        fr["emissive"].copy_(emis)
+        hf["emissive"][...] = gb["emissive"]
+        r.execute(g)
+        hist = oracle.frame(g, hf, ae, hist=hist)
+        torch.cuda.synchronize()
+        assert r.current_history() == hist
+        ok = f16_close(host(fr["color"]), hf["color"], atol=4e-3, rtol=8e-3)
+        assert ok.mean() >= 0.999, (f, ok.mean())
+        d = np.abs(host(fr["output"]).astype(np.int32) - hf["output"].astype(np.int32))
+        assert (d <= 2).mean() >= 0.995, (f, (d <= 2).mean())
+        assert abs(soc.exposure_of(fr["auto_exposure"]) - ae.exposure) <= 1e-4
+    ms = r.pass_ms()
+    assert all(m >= 0 for m in ms) and len(ms) == len(r.pass_names())
+    r.close()
+
+
+# ------------------------------------------------------------------------------------------------ 4K properties
+def test_4k_properties(soc):
+    """Size-independent properties at the benchmark resolution (oracle would take too long)."""
+    W, H = 3840, 2160
+    g = globals_for(W, H)
+    # bloom chain of a constant emissive image stays constant (weights sum to 1, all exact)
+    em = torch.full((H, W, 4), 0.5, dtype=torch.float16, device=DEV)
+    mips = [torch.zeros(H >> i, W >> i, 4, dtype=torch.float16, device=DEV) for i in range(4)]
+    soc.bloom_chain(g, em, mips)
+    assert torch.all(em[..., :3] == 0.5)
+    # blur of a constant AO image is the constant
+    ao = torch.full((H // 2, W // 2), 200, dtype=torch.uint8, device=DEV)
+    out = torch.zeros_like(ao)
+    soc.ssao_blur(g, ao, out)
+    assert torch.all(out == 200)
+    # histogram counts every pixel exactly once
+    buf = soc.auto_exposure_buffer()
+    img = torch.rand(H, W, 4, device=DEV).half()
+    soc.generate_luminance_histogram(g, img, buf)
+    assert int(buf[1:].sum()) == W * H
+    # TAA with identical history, zero velocity, and constant colour returns the colour
+    c = torch.full((H, W, 4), 0.25, dtype=torch.float16, device=DEV)
+    z = torch.zeros(H, W, 4, dtype=torch.float16, device=DEV)
+    d = torch.full((H, W), 0.9, dtype=torch.float32, device=DEV)
+    t = torch.zeros_like(c)
+    soc.temporal_antialiasing(g, t, c, c.clone(), z, z.clone(), d)
+    assert torch.all(t == 0.25)
