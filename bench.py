@@ -1,0 +1,243 @@
+#!/usr/bin/env python
+"""Benchmark: frames/sec + ms/pass of the screen-space hot path (BASELINE.json metric).
+
+One step = one full frame of the reference's live screen-space passes (renderer.cpp:1024-1217): bloom x8,
+SSAO + blur, atmosphere/clouds, composition, luminance histogram (+ RCCL all-reduce when N > 1) +
+resolve, TAA (with the fused velocity history), AgX tone mapping into an RGBA8 framebuffer, at
+3840x2160 on the Sponza-proxy G-buffer (synthetic; Sponza.bin is missing from the reference). Inputs
+are resident in HBM before timing starts. N GPUs: one process per GPU, each renders its own camera
+(frame-per-GPU sharding, SURVEY.md §8e, weak scaling); value = frames of all ranks / max rank time.
+
+Prints ONE JSON line on rank 0. See DESIGN.md §6 for the roofline accounting.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import soc_real_time_renderer_amd as soc  # noqa: E402
+from soc_real_time_renderer_amd import scene  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+SPONZA_CAMERA = ((-14.0, 2.2, 0.3), (0.0, -0.42, 0.0))
+
+
+def camera_for_rank(rank: int):
+    """Rank 0: the canonical Sponza-proxy view; others: seeded poses along the nave (seed 0xC5)."""
+    if rank == 0:
+        return SPONZA_CAMERA
+    rng = np.random.default_rng(0xC5 + rank)
+    pos = (float(rng.uniform(-15.0, 12.0)), float(rng.uniform(1.5, 4.0)), float(rng.uniform(-2.5, 2.5)))
+    rot = (float(rng.choice([0.0, math.pi])) + float(rng.uniform(-0.3, 0.3)), float(rng.uniform(-0.6, -0.2)), 0.0)
+    return pos, rot
+
+
+def make_globals(W, H, camera):
+    g = soc.globals_defaults(W, H)
+    cam = soc.make_camera(*camera)
+    ji = C.c_uint32(0)
+    soc.frame_update(g, cam, W, H, 0.016, ji)
+    cam.position[0] += 0.05
+    soc.frame_update(g, cam, W, H, 0.016, ji)
+    g.elapsed_time = 10.0      # SURVEY.md §8d pinned globals (C3)
+    g.frame_counter = 2
+    return g
+
+
+def algorithmic_bytes(W, H, f_sky):
+    """Bytes each pass must move at the reference formats, per launch."""
+    P = W * H
+    b = {
+        "BloomDownsample - 0": 16.0 * P, "BloomDownsample - 1": (8.0 + 2.0) * P, "BloomDownsample - 2": (2.0 + 0.5) * P,
+        "BloomDownsample - 3": (0.5 + 0.125) * P, "BloomUpsample - 3": (0.125 + 0.5) * P,
+        "BloomUpsample - 2": (0.5 + 2.0) * P, "BloomUpsample - 1": (2.0 + 8.0) * P, "BloomUpsample - 0": 16.0 * P,
+        "SSAOGeneration": 12.25 * P, "SSAOBlur": 0.5 * P, "CloudRendering": 8.0 * P,
+        "Composition": (40.25 + 4.0 * f_sky) * P, "GenerateLuminanceHistogram": 8.0 * P,
+        "ResolveLuminanceHistogram": 2.0 * 1028.0,
+        "TemporalAntiAliasing": 52.0 * P,   # 44 B/px reference TAA + 8 B/px fused velocity history write
+        "ToneMapping": 12.0 * P,
+    }
+    return b
+
+
+def cpu_baseline(W, H, host_inputs, g):
+    """The oracle (plain-C restatement, OpenMP over rows) timed on this box's host cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    oracle.lib()
+    fr = dict(host_inputs)
+    fr["bloom_mips"] = [np.zeros((H >> i, W >> i, 4), np.float16) for i in range(4)]
+    fr["ssao"] = np.zeros((H // 2, W // 2), np.uint8)
+    fr["ssao_blur"] = np.zeros((H // 2, W // 2), np.uint8)
+    fr["clouds"] = np.zeros((H, W, 4), np.uint8)
+    fr["color"] = np.zeros((H, W, 4), np.float16)
+    fr["history_color"] = [np.zeros((H, W, 4), np.float16) for _ in range(2)]
+    fr["history_velocity"] = [np.zeros((H, W, 4), np.float16) for _ in range(2)]
+    fr["output"] = np.zeros((H, W, 4), np.uint8)
+    fr["emissive"] = host_inputs["emissive"].copy()
+    ae = soc.AutoExposure()
+    frames, t_total = 0, 0.0
+    while frames < 1 or (t_total < 10.0 and frames < 3):
+        fr["emissive"][...] = host_inputs["emissive"]
+        t0 = time.perf_counter()
+        oracle.frame(g, fr, ae, hist=frames % 2)
+        t_total += time.perf_counter() - t0
+        frames += 1
+    return {"value": round(frames / t_total, 4), "unit": "frames/sec", "cores": oracle.num_threads(),
+            "kind": "port",
+            "sample": f"{frames} full {W}x{H} frame(s) of all passes (bloom x8, ssao+blur, clouds, composition, "
+                      f"histogram+resolve, taa, tone map) on the oracle, {t_total:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--width", type=int, default=3840)
+    ap.add_argument("--height", type=int, default=2160)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile-frames", type=int, default=20)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+    W, H = args.width, args.height
+
+    # ---- inputs (synthetic Sponza-proxy G-buffer + 4096^2 sun shadow map), resident in HBM ----
+    g = make_globals(W, H, camera_for_rank(rank))
+    gb = scene.gbuffer(g, W, H)
+    shadow = scene.shadow_map(g, 4096)
+    noise = scene.noise_texture()
+    f_sky = float((gb["depth"] == 1.0).mean())
+    fr = soc.alloc_frame(W, H, device, bloom_output=True)
+    for k in ("albedo", "emissive", "normal", "velocity", "depth"):
+        fr[k].copy_(torch.from_numpy(gb[k]))
+    fr["shadow"].copy_(torch.from_numpy(shadow))
+    fr["noise"].copy_(torch.from_numpy(noise))
+    r = soc.Renderer(fr)
+    r.set_exposure_pixels(world * W * H, world > 1)
+    bins = fr["auto_exposure"][1:]
+    names = r.pass_names()
+    groups = r.pass_groups()
+    stream = torch.cuda.current_stream()
+
+    def frame():
+        r.execute(g, soc.PHASE_PRE_EXPOSURE)
+        if world > 1:
+            dist.all_reduce(bins, op=dist.ReduceOp.SUM)     # RCCL over xGMI: 1 KiB luminance histogram
+        r.execute(g, soc.PHASE_POST_EXPOSURE)
+
+    for _ in range(args.warmup):
+        frame()
+    torch.cuda.synchronize()
+
+    # HIP events around the north-star kernels on the launch stream, inside the timed region
+    timed = [names.index("Composition"), names.index("SSAOGeneration")]
+    for i in timed:
+        r.set_pass_timing(i, True)
+    r.reset_timing()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        frame()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    stats_timed = {n: ms for n, _, ms, cnt in r.pass_stats() if cnt}
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    max_elapsed = float(t.item())
+    ms_per_step = max_elapsed / args.steps * 1e3
+    value = world * args.steps / max_elapsed
+
+    # ---- per-pass breakdown (separate, all passes evented) ----
+    r.set_pass_timing(-1, True)
+    r.reset_timing()
+    for _ in range(args.profile_frames):
+        frame()
+    torch.cuda.synchronize()
+    stats = r.pass_stats()
+    ms_pass = {n: round(ms, 4) for n, _, ms, _ in stats}
+    ms_group = {}
+    for n, gname, ms, _ in stats:
+        ms_group[gname] = round(ms_group.get(gname, 0.0) + ms, 4)
+
+    algo = algorithmic_bytes(W, H, f_sky)
+    comp_ms = stats_timed["Composition"]
+    ssao_ms = stats_timed["SSAOGeneration"]
+    achieved = algo["Composition"] / (comp_ms * 1e-3) / 1e9
+    ns_bytes = algo["Composition"] + algo["SSAOGeneration"]
+    ns_us = (comp_ms + ssao_ms) * 1e3
+    pass_gbs = {n: round(algo[n] / (ms * 1e-3) / 1e9, 1) for n, _, ms, _ in stats if ms > 0 and n in algo}
+
+    if world > 1:
+        dist.barrier()
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+
+    out = {
+        "metric": "frames/sec + ms/pass, Sponza 3840x2160 deferred+SSAO+TAA",
+        "value": round(value, 3),
+        "unit": "frames/sec",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32 (fp16/unorm8/d32 storage)",
+        "data": "synthetic (Sponza-proxy G-buffer + 4096^2 sun shadow map, scene_synth.c)",
+        "config": {"workload": f"Sponza-proxy {W}x{H} full screen-space chain (C3): bloom x8, SSAO+blur, "
+                               f"clouds, composition, auto-exposure, TAA, AgX tone map",
+                   "resolution": [W, H], "f_sky": round(f_sky, 4), "parallelism": f"frame-per-gpu x{world}",
+                   "histogram_allreduce": world > 1},
+        "roofline": {"kernel": "Composition", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "algorithmic_bytes_per_launch": int(algo["Composition"]), "avg_launch_us": round(comp_ms * 1e3, 2)},
+        "north_star": {"kernels": ["SSAOGeneration", "Composition"], "us": round(ns_us, 2),
+                       "algorithmic_bytes": int(ns_bytes),
+                       "frac_of_hbm_roofline": round(ns_bytes / (ns_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                       "target_us_at_60pct": round(ns_bytes / (0.6 * HBM_PEAK_GBS * 1e9) * 1e6, 2)},
+        "ms_per_pass": ms_pass,
+        "ms_per_group": ms_group,
+        "gbs_per_pass": pass_gbs,
+    }
+    if not args.no_cpu_baseline and world == 1:
+        host_inputs = dict(gb)
+        host_inputs["shadow"] = shadow
+        host_inputs["noise"] = noise
+        out["cpu_baseline"] = cpu_baseline(W, H, host_inputs, g)
+    else:
+        out["cpu_baseline"] = None
+    print(json.dumps(out), flush=True)
+    r.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -299,6 +299,9 @@ typedef struct soc_frame_images {
     float* ssao_noise_table;                            /* optional (ssao.w*ssao.h*2 floats) or NULL */
     soc_auto_exposure* auto_exposure;                   /* device */
     soc_globals* d_globals;                             /* device copy of the globals */
+    /* Optional target of the last bloom upsample, read by composition as "emissive". data == NULL:
+     * bloom overwrites `emissive` in place, as the reference graph does (renderer.cpp:1055-1062). */
+    soc_img bloom_output;
 } soc_frame_images;
 
 typedef struct soc_renderer soc_renderer;
@@ -319,9 +322,18 @@ int soc_renderer_set_exposure_pixels(soc_renderer* r, uint64_t total_pixels, int
 int32_t soc_renderer_pass_count(const soc_renderer* r);
 const char* soc_renderer_pass_name(const soc_renderer* r, int32_t index);
 const char* soc_renderer_pass_group(const soc_renderer* r, int32_t index);   /* renderer.cpp:558-588 names */
-/* Milliseconds of pass `index` in the most recent executed frame (needs SOC_RENDERER_TIMING and a
- * completed stream); < 0 if unavailable. */
+/* Milliseconds of pass `index` in the most recent executed frame (needs timing enabled for the pass
+ * and a completed stream); < 0 if unavailable. */
 float soc_renderer_pass_ms(soc_renderer* r, int32_t index);
+/* Per-pass timing control: hipEvents bracket a timed pass on the launch stream every frame, kept in
+ * a ring of SOC_RENDERER_TIMING_RING frames. index -1 = every pass. Event creation happens here, not
+ * in soc_renderer_execute. */
+#define SOC_RENDERER_TIMING_RING 256
+int soc_renderer_set_pass_timing(soc_renderer* r, int32_t index, int32_t enable);
+int soc_renderer_reset_timing(soc_renderer* r);
+/* Sum of the pass's durations (ms) over the frames recorded since the last reset (at most the last
+ * SOC_RENDERER_TIMING_RING) and their count. Needs a completed stream. */
+int soc_renderer_pass_stats(soc_renderer* r, int32_t index, float* total_ms, int32_t* frames);
 /* Index (0/1) of the history_color slot holding this frame's TAA result (= tone-map input). */
 int32_t soc_renderer_current_history(const soc_renderer* r);
 

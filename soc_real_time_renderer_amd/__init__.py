@@ -225,7 +225,8 @@ def globals_device_buffer(device="cuda") -> torch.Tensor:
 # ------------------------------------------------------------------------------------------------
 # render graph
 # ------------------------------------------------------------------------------------------------
-def alloc_frame(width: int, height: int, device="cuda", output_format=FMT_RGBA8_UNORM, noise_table=True):
+def alloc_frame(width: int, height: int, device="cuda", output_format=FMT_RGBA8_UNORM, noise_table=True,
+                bloom_output=False):
     """Device images of one frame (renderer.cpp:310-513 formats/extents). G-buffer inputs included."""
     W, H = width, height
     hw, hh = W // 2, H // 2
@@ -254,6 +255,7 @@ def alloc_frame(width: int, height: int, device="cuda", output_format=FMT_RGBA8_
         t["output"] = torch.zeros(H, W, 4, dtype=torch.float32, device=device)
     t["output_format"] = output_format
     t["ssao_noise_table"] = torch.zeros(hh * hw * 2, dtype=torch.float32, device=device) if noise_table else None
+    t["bloom_output"] = torch.zeros(H, W, 4, **f16) if bloom_output else None
     return t
 
 
@@ -275,6 +277,7 @@ class Renderer:
         fi.ssao_noise_table = _ptr(frame.get("ssao_noise_table"))
         fi.auto_exposure = _ptr(frame["auto_exposure"])
         fi.d_globals = _ptr(frame.get("d_globals"))
+        fi.bloom_output = img(frame.get("bloom_output"))
         self._fi = fi
         h = lib().soc_renderer_create(C.byref(fi), _abi.RENDERER_TIMING if timing else 0)
         if not h:
@@ -301,6 +304,21 @@ class Renderer:
     def pass_ms(self):
         n = lib().soc_renderer_pass_count(self.handle)
         return [float(lib().soc_renderer_pass_ms(self.handle, i)) for i in range(n)]
+
+    def set_pass_timing(self, index: int = -1, enable: bool = True) -> None:
+        _check(lib().soc_renderer_set_pass_timing(self.handle, index, int(enable)), "soc_renderer_set_pass_timing")
+
+    def reset_timing(self) -> None:
+        _check(lib().soc_renderer_reset_timing(self.handle), "soc_renderer_reset_timing")
+
+    def pass_stats(self):
+        """[(name, group, mean_ms, frames)] over the frames recorded since reset_timing (stream must be idle)."""
+        out = []
+        for i, (n, gname) in enumerate(zip(self.pass_names(), self.pass_groups())):
+            tot, cnt = C.c_float(0), C.c_int32(0)
+            _check(lib().soc_renderer_pass_stats(self.handle, i, C.byref(tot), C.byref(cnt)), "soc_renderer_pass_stats")
+            out.append((n, gname, (tot.value / cnt.value) if cnt.value else float("nan"), cnt.value))
+        return out
 
     def current_history(self) -> int:
         return int(lib().soc_renderer_current_history(self.handle))

@@ -105,6 +105,7 @@ class FrameImages(C.Structure):
         ("shadow", SocImg), ("noise", SocImg), ("bloom_mips", SocImg * 4), ("ssao", SocImg), ("ssao_blur", SocImg),
         ("clouds", SocImg), ("color", SocImg), ("history_color", SocImg * 2), ("history_velocity", SocImg * 2),
         ("output", SocImg), ("ssao_noise_table", C.c_void_p), ("auto_exposure", C.c_void_p), ("d_globals", C.c_void_p),
+        ("bloom_output", SocImg),
     ]
 
 
@@ -154,6 +155,9 @@ FUNCTIONS = {
     "soc_renderer_pass_group": (C.c_char_p, [_P, C.c_int32]),
     "soc_renderer_pass_ms": (C.c_float, [_P, C.c_int32]),
     "soc_renderer_current_history": (C.c_int32, [_P]),
+    "soc_renderer_set_pass_timing": (_I, [_P, C.c_int32, C.c_int32]),
+    "soc_renderer_reset_timing": (_I, [_P]),
+    "soc_renderer_pass_stats": (_I, [_P, C.c_int32, C.POINTER(C.c_float), C.POINTER(C.c_int32)]),
 }
 
 # not in the public header: test hooks

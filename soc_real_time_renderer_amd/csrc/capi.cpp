@@ -158,6 +158,7 @@ const FieldInfo kFields[] = {
     F(soc_frame_images, ssao), F(soc_frame_images, ssao_blur), F(soc_frame_images, clouds), F(soc_frame_images, color),
     F(soc_frame_images, history_color), F(soc_frame_images, history_velocity), F(soc_frame_images, output),
     F(soc_frame_images, ssao_noise_table), F(soc_frame_images, auto_exposure), F(soc_frame_images, d_globals),
+    F(soc_frame_images, bloom_output),
 };
 #undef F
 }  // namespace
@@ -453,8 +454,9 @@ struct soc_renderer {
         std::string name, group;
         int phase;
         std::function<int(const soc_globals*, hipStream_t)> run;
-        hipEvent_t ev[2] = {nullptr, nullptr};
-        bool recorded = false;
+        bool timed = false;
+        std::vector<hipEvent_t> ev0, ev1;  // ring of SOC_RENDERER_TIMING_RING frames
+        int next = 0, count = 0, last = -1;
     };
     soc_frame_images img{};
     std::vector<Pass> passes;
@@ -491,8 +493,10 @@ void build_passes(soc_renderer* r) {
         add("BloomUpsample - " + std::to_string(i), "Bloom", SOC_PHASE_PRE_EXPOSURE, [r, i](const soc_globals* g, hipStream_t s) {
             return soc_bloom_upsample(g, r->img.bloom_mips[i], r->img.bloom_mips[i - 1], (soc_stream)s);
         });
-    add("BloomUpsample - 0", "Bloom", SOC_PHASE_PRE_EXPOSURE,
-        [r](const soc_globals* g, hipStream_t s) { return soc_bloom_upsample(g, r->img.bloom_mips[0], r->img.emissive, (soc_stream)s); });
+    add("BloomUpsample - 0", "Bloom", SOC_PHASE_PRE_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
+        const soc_img& dst = r->img.bloom_output.data ? r->img.bloom_output : r->img.emissive;
+        return soc_bloom_upsample(g, r->img.bloom_mips[0], dst, (soc_stream)s);
+    });
     // renderer.cpp:1064-1079
     add("SSAOGeneration", "Ambient Occlusion", SOC_PHASE_PRE_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
         return soc_ssao_generation(g, r->img.depth, r->img.normal, r->img.ssao, r->img.ssao_noise_table, (soc_stream)s);
@@ -506,7 +510,8 @@ void build_passes(soc_renderer* r) {
     // renderer.cpp:1103-1117
     add("Composition", "Composition", SOC_PHASE_PRE_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
         const auto& I = r->img;
-        return soc_composition(g, I.d_globals, I.color, I.albedo, I.emissive, I.normal, I.depth, I.ssao_blur, I.shadow, I.clouds,
+        const soc_img& em = I.bloom_output.data ? I.bloom_output : I.emissive;
+        return soc_composition(g, I.d_globals, I.color, I.albedo, em, I.normal, I.depth, I.ssao_blur, I.shadow, I.clouds,
                                (soc_stream)s);
     });
     // renderer.cpp:1155-1168
@@ -545,23 +550,19 @@ extern "C" soc_renderer* soc_renderer_create(const soc_frame_images* images, uin
     r->img = *images;
     r->flags = flags;
     build_passes(r);
-    if (flags & SOC_RENDERER_TIMING) {
-        for (auto& p : r->passes) {
-            if (hipEventCreate(&p.ev[0]) != hipSuccess || hipEventCreate(&p.ev[1]) != hipSuccess) {
-                set_error(SOC_E_HIP, "soc_renderer_create: hipEventCreate failed");
-                soc_renderer_destroy(r);
-                return nullptr;
-            }
-        }
+    if ((flags & SOC_RENDERER_TIMING) && soc_renderer_set_pass_timing(r, -1, 1) != SOC_OK) {
+        soc_renderer_destroy(r);
+        return nullptr;
     }
     return r;
 }
 
 extern "C" void soc_renderer_destroy(soc_renderer* r) {
     if (!r) return;
-    for (auto& p : r->passes)
-        for (auto& e : p.ev)
-            if (e) (void)hipEventDestroy(e);
+    for (auto& p : r->passes) {
+        for (auto e : p.ev0) (void)hipEventDestroy(e);
+        for (auto e : p.ev1) (void)hipEventDestroy(e);
+    }
     for (auto& e : r->staging_ev)
         if (e) (void)hipEventDestroy(e);
     if (r->staging) (void)hipHostFree(r->staging);
@@ -594,15 +595,17 @@ extern "C" int soc_renderer_execute(soc_renderer* r, const soc_globals* g, int32
         int rc = upload_lights(r, g, s);
         if (rc) return rc;
     }
-    const bool timing = (r->flags & SOC_RENDERER_TIMING) != 0;
     for (auto& p : r->passes) {
         if (!(p.phase & phase)) continue;
-        if (timing) (void)hipEventRecord(p.ev[0], s);
+        const int slot = p.next;
+        if (p.timed) (void)hipEventRecord(p.ev0[slot], s);
         int rc = p.run(g, s);
         if (rc) return rc;
-        if (timing) {
-            (void)hipEventRecord(p.ev[1], s);
-            p.recorded = true;
+        if (p.timed) {
+            (void)hipEventRecord(p.ev1[slot], s);
+            p.last = slot;
+            p.next = (slot + 1) % SOC_RENDERER_TIMING_RING;
+            if (p.count < SOC_RENDERER_TIMING_RING) p.count++;
         }
     }
     if (phase & SOC_PHASE_POST_EXPOSURE) r->hist = 1 - r->hist;   // ping-pong the TAA history
@@ -631,10 +634,50 @@ extern "C" const char* soc_renderer_pass_group(const soc_renderer* r, int32_t i)
 extern "C" float soc_renderer_pass_ms(soc_renderer* r, int32_t i) {
     if (!r || i < 0 || i >= (int32_t)r->passes.size()) return -1.0f;
     auto& p = r->passes[i];
-    if (!p.recorded || !p.ev[0]) return -1.0f;
+    if (!p.timed || p.last < 0) return -1.0f;
     float ms = -1.0f;
-    if (hipEventElapsedTime(&ms, p.ev[0], p.ev[1]) != hipSuccess) return -1.0f;
+    if (hipEventElapsedTime(&ms, p.ev0[p.last], p.ev1[p.last]) != hipSuccess) return -1.0f;
     return ms;
+}
+
+extern "C" int soc_renderer_set_pass_timing(soc_renderer* r, int32_t index, int32_t enable) {
+    if (!r) return set_error(SOC_E_INVALID_ARG, "soc_renderer_set_pass_timing: null renderer");
+    const int n = (int)r->passes.size();
+    if (index < -1 || index >= n) return set_error(SOC_E_INVALID_ARG, "soc_renderer_set_pass_timing: bad index %d", index);
+    for (int i = (index < 0 ? 0 : index); i < (index < 0 ? n : index + 1); ++i) {
+        auto& p = r->passes[i];
+        if (enable && p.ev0.empty()) {
+            p.ev0.assign(SOC_RENDERER_TIMING_RING, nullptr);
+            p.ev1.assign(SOC_RENDERER_TIMING_RING, nullptr);
+            for (int k = 0; k < SOC_RENDERER_TIMING_RING; ++k)
+                if (hipEventCreate(&p.ev0[k]) != hipSuccess || hipEventCreate(&p.ev1[k]) != hipSuccess)
+                    return set_error(SOC_E_HIP, "soc_renderer_set_pass_timing: hipEventCreate failed");
+        }
+        p.timed = enable != 0;
+    }
+    return SOC_OK;
+}
+
+extern "C" int soc_renderer_reset_timing(soc_renderer* r) {
+    if (!r) return set_error(SOC_E_INVALID_ARG, "soc_renderer_reset_timing: null renderer");
+    for (auto& p : r->passes) { p.next = 0; p.count = 0; p.last = -1; }
+    return SOC_OK;
+}
+
+extern "C" int soc_renderer_pass_stats(soc_renderer* r, int32_t i, float* total_ms, int32_t* frames) {
+    if (!r || i < 0 || i >= (int32_t)r->passes.size() || !total_ms || !frames)
+        return set_error(SOC_E_INVALID_ARG, "soc_renderer_pass_stats: bad arguments");
+    auto& p = r->passes[i];
+    double sum = 0.0;
+    for (int k = 0; k < p.count; ++k) {
+        float ms = 0.0f;
+        hipError_t e = hipEventElapsedTime(&ms, p.ev0[k], p.ev1[k]);
+        if (e != hipSuccess) return set_error(SOC_E_HIP, "soc_renderer_pass_stats: %s", hipGetErrorString(e));
+        sum += ms;
+    }
+    *total_ms = (float)sum;
+    *frames = p.count;
+    return SOC_OK;
 }
 
 extern "C" int32_t soc_renderer_current_history(const soc_renderer* r) { return r ? r->hist : -1; }

@@ -58,7 +58,6 @@ def test_bloom_passes_bit_exact(soc, oracle, W, H):
 @pytest.mark.parametrize("W,H", [(64, 36), (1920, 1080)])
 def test_bloom_fast_paths_equal_generic(soc, W, H):
     """The analytic 1:1 / 2:1 / 1:2 tap paths give the same bits as the float-uv generic path."""
-    import ctypes as C
     lib = soc.lib()
     for up, (sw, sh), (dw, dh) in [(0, (W, H), (W, H)), (0, (W, H), (W // 2, H // 2)), (1, (W // 2, H // 2), (W, H)),
                                    (1, (W, H), (W, H))]:
@@ -70,7 +69,6 @@ def test_bloom_fast_paths_equal_generic(soc, W, H):
         rc = lib.soc_debug_bloom_generic(up, soc.img(s), soc.img(b), torch.cuda.current_stream().cuda_stream)
         assert rc == 0
         assert torch.equal(a[..., :3].view(torch.int16), b[..., :3].view(torch.int16))
-        del C
 
 
 @pytest.mark.parametrize("W,H", [(64, 36), (512, 512), (1920, 1080)])
