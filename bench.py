@@ -15,7 +15,6 @@ from __future__ import annotations
 import argparse
 import ctypes as C
 import json
-import math
 import os
 import sys
 import time
@@ -28,22 +27,9 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import soc_real_time_renderer_amd as soc  # noqa: E402
-from soc_real_time_renderer_amd import scene  # noqa: E402
+from soc_real_time_renderer_amd import multi_gpu, scene  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
-SPONZA_CAMERA = ((-14.0, 2.2, 0.3), (0.0, -0.42, 0.0))
-
-
-def camera_for_rank(rank: int):
-    """Rank 0: the canonical Sponza-proxy view; others: seeded poses along the nave (seed 0xC5)."""
-    if rank == 0:
-        return SPONZA_CAMERA
-    rng = np.random.default_rng(0xC5 + rank)
-    pos = (float(rng.uniform(-15.0, 12.0)), float(rng.uniform(1.5, 4.0)), float(rng.uniform(-2.5, 2.5)))
-    rot = (float(rng.choice([0.0, math.pi])) + float(rng.uniform(-0.3, 0.3)), float(rng.uniform(-0.6, -0.2)), 0.0)
-    return pos, rot
-
-
 def make_globals(W, H, camera):
     g = soc.globals_defaults(W, H)
     cam = soc.make_camera(*camera)
@@ -112,17 +98,14 @@ def main():
     ap.add_argument("--profile-frames", type=int, default=20)
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    rank, world, local_rank = multi_gpu.env()
     torch.cuda.set_device(local_rank)
     device = torch.device("cuda", local_rank)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+    multi_gpu.init(device)
     W, H = args.width, args.height
 
     # ---- inputs (synthetic Sponza-proxy G-buffer + 4096^2 sun shadow map), resident in HBM ----
-    g = make_globals(W, H, camera_for_rank(rank))
+    g = make_globals(W, H, multi_gpu.camera_for_rank(rank))
     gb = scene.gbuffer(g, W, H)
     shadow = scene.shadow_map(g, 4096)
     noise = scene.noise_texture()
@@ -133,17 +116,14 @@ def main():
     fr["shadow"].copy_(torch.from_numpy(shadow))
     fr["noise"].copy_(torch.from_numpy(noise))
     r = soc.Renderer(fr)
-    r.set_exposure_pixels(world * W * H, world > 1)
+    r.set_exposure_pixels(*multi_gpu.exposure_pixels(world, W, H))
     bins = fr["auto_exposure"][1:]
     names = r.pass_names()
     groups = r.pass_groups()
     stream = torch.cuda.current_stream()
 
     def frame():
-        r.execute(g, soc.PHASE_PRE_EXPOSURE)
-        if world > 1:
-            dist.all_reduce(bins, op=dist.ReduceOp.SUM)     # RCCL over xGMI: 1 KiB luminance histogram
-        r.execute(g, soc.PHASE_POST_EXPOSURE)
+        multi_gpu.render_frame(r, g, bins)     # PRE, RCCL all-reduce of the 1 KiB histogram (N > 1), POST
 
     for _ in range(args.warmup):
         frame()
@@ -165,10 +145,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     stats_timed = {n: ms for n, _, ms, cnt in r.pass_stats() if cnt}
-    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    max_elapsed = float(t.item())
+    max_elapsed = multi_gpu.max_over_ranks(elapsed, device)
     ms_per_step = max_elapsed / args.steps * 1e3
     value = world * args.steps / max_elapsed
 

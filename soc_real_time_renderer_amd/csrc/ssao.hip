@@ -12,18 +12,6 @@
 namespace soc {
 namespace {
 
-// ssao_generation.inl:74-103
-__constant__ float c_kernel[SOC_SSAO_MAX_KERNEL][3] = {
-    {0.2196607f, 0.9032637f, 0.2254677f},   {0.05916681f, 0.2201506f, 0.1430302f},  {-0.4152246f, 0.1320857f, 0.7036734f},
-    {-0.3790807f, 0.1454145f, 0.100605f},   {0.3149606f, -0.1294581f, 0.7044517f},  {-0.1108412f, 0.2162839f, 0.1336278f},
-    {0.658012f, -0.4395972f, 0.2919373f},   {0.5377914f, 0.3112189f, 0.426864f},    {-0.2752537f, 0.07625949f, 0.1273409f},
-    {-0.1915639f, -0.4973421f, 0.3129629f}, {-0.2634767f, 0.5277923f, 0.1107446f},  {0.8242752f, 0.02434147f, 0.06049098f},
-    {0.06262707f, -0.2128643f, 0.03671562f}, {-0.1795662f, -0.3543862f, 0.07924347f}, {0.06039629f, 0.24629f, 0.4501176f},
-    {-0.7786345f, -0.3814852f, 0.2391262f}, {0.2792919f, 0.2487278f, 0.05185341f},  {0.1841383f, 0.1696993f, 0.8936281f},
-    {-0.3479781f, 0.4725766f, 0.719685f},   {-0.1365018f, -0.2513416f, 0.470937f},  {0.1280388f, -0.563242f, 0.3419276f},
-    {-0.4800232f, -0.1899473f, 0.2398808f}, {0.6389147f, 0.1191014f, 0.5271206f},   {0.1932822f, -0.3692099f, 0.6060588f},
-    {-0.3465451f, -0.1654651f, 0.6746758f}, {0.2448421f, -0.1610962f, 0.1289366f}};
-
 struct SsaoParams {
     Mat4 inv_proj;
     Mat4 proj;
@@ -73,7 +61,7 @@ __global__ __launch_bounds__(256) void ssao_noise_kernel(int tw, int th, int noi
 
 typedef float f2a4 __attribute__((ext_vector_type(2))) __attribute__((aligned(4)));
 
-// Bilinear D32 depth at (u, v): the two taps of each row are one 8-byte load (i0 <= w-2).
+// Bilinear D32 depth at (u, v) via the generic contract helper (centre tap).
 __device__ __forceinline__ float depth_tap(const DImg& depth, float u, float v) {
     Axis ax = axis_clamp(u, depth.w), ay = axis_clamp(v, depth.h);
     f2a4 r0 = *reinterpret_cast<const f2a4*>(row_ptr<float>(depth, ay.i0) + ax.i0);
@@ -81,7 +69,34 @@ __device__ __forceinline__ float depth_tap(const DImg& depth, float u, float v) 
     return bilerp1(r0.x, r0.y, r1.x, r1.y, ax.w, ay.w);
 }
 
-template <bool TABLE>
+__device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+
+// ssao_generation.inl:74-103 as compile-time constants (literal operands after unrolling)
+struct KernelTable { float v[SOC_SSAO_MAX_KERNEL][3]; };
+constexpr KernelTable kKernel = {{
+    {0.2196607f, 0.9032637f, 0.2254677f},   {0.05916681f, 0.2201506f, 0.1430302f},  {-0.4152246f, 0.1320857f, 0.7036734f},
+    {-0.3790807f, 0.1454145f, 0.100605f},   {0.3149606f, -0.1294581f, 0.7044517f},  {-0.1108412f, 0.2162839f, 0.1336278f},
+    {0.658012f, -0.4395972f, 0.2919373f},   {0.5377914f, 0.3112189f, 0.426864f},    {-0.2752537f, 0.07625949f, 0.1273409f},
+    {-0.1915639f, -0.4973421f, 0.3129629f}, {-0.2634767f, 0.5277923f, 0.1107446f},  {0.8242752f, 0.02434147f, 0.06049098f},
+    {0.06262707f, -0.2128643f, 0.03671562f}, {-0.1795662f, -0.3543862f, 0.07924347f}, {0.06039629f, 0.24629f, 0.4501176f},
+    {-0.7786345f, -0.3814852f, 0.2391262f}, {0.2792919f, 0.2487278f, 0.05185341f},  {0.1841383f, 0.1696993f, 0.8936281f},
+    {-0.3479781f, 0.4725766f, 0.719685f},   {-0.1365018f, -0.2513416f, 0.470937f},  {0.1280388f, -0.563242f, 0.3419276f},
+    {-0.4800232f, -0.1899473f, 0.2398808f}, {0.6389147f, 0.1191014f, 0.5271206f},   {0.1932822f, -0.3692099f, 0.6060588f},
+    {-0.3465451f, -0.1654651f, 0.6746758f}, {0.2448421f, -0.1610962f, 0.1289366f}}};
+
+// Affine form of one coordinate of the projected sample: c(k) = a0 + a1 kx + a2 ky + a3 kz.
+struct Aff { float a0, a1, a2, a3; };
+__device__ __forceinline__ float aff(const Aff& a, float kx, float ky, float kz) {
+    return __builtin_fmaf(a.a3, kz, __builtin_fmaf(a.a2, ky, __builtin_fmaf(a.a1, kx, a.a0)));
+}
+
+// SSAO tap loop. The sample position s(k) = frag + (TBN k) r is affine in the kernel vector k, so the
+// projected x', y', w' and the sample depth s.z are evaluated as per-pixel affine forms (3 FMAs each)
+// with the texel-space scale of the sampling contract folded in (t = u W - 0.5 = x'/w' * W/2 + (W-1)/2).
+// The bilinear depth tap follows the contract's clamp-to-edge / 8-bit sub-texel quantisation with t
+// clamped to [0, n-1-1/256] (right-edge taps keep 1/256 of the inner texel). This regroups the
+// reference's fp32 roundings; the result stays within the SSAO tolerance of DESIGN.md §5.
+template <bool TABLE, bool SPARSE_IP, bool FULL>
 __global__ __launch_bounds__(256) void ssao_kernel(DImg depth, DImg normal, DImg target, const float2* __restrict__ table,
                                                    SsaoParams p) {
     const int x = blockIdx.x * 16 + threadIdx.x, y = blockIdx.y * 16 + threadIdx.y;
@@ -101,30 +116,55 @@ __global__ __launch_bounds__(256) void ssao_kernel(DImg depth, DImg normal, DImg
     const f3 t = normalize3(rv - n * dot3(rv, n));
     const f3 b = cross3(t, n);
 
-    const float* ip = p.inv_proj.m;
     const float* P = p.proj.m;
+    const float* ip = p.inv_proj.m;
+    const int W = depth.w, H = depth.h;
+    const float r = p.radius;
+    const f3 tr = t * r, br = b * r, nr = n * r;
+    // s(k) = frag + tr kx + br ky + nr kz;  x' = P0 sx + P4 sy + P8 sz + P12, etc.
+    auto proj_aff = [&](int row, float scale) {
+        const float m0 = P[row] * scale, m1 = P[4 + row] * scale, m2 = P[8 + row] * scale, m3 = P[12 + row] * scale;
+        return Aff{m0 * frag.x + m1 * frag.y + m2 * frag.z + m3, m0 * tr.x + m1 * tr.y + m2 * tr.z,
+                   m0 * br.x + m1 * br.y + m2 * br.z, m0 * nr.x + m1 * nr.y + m2 * nr.z};
+    };
+    const Aff ax = proj_aff(0, 0.5f * (float)W), ay = proj_aff(1, 0.5f * (float)H), aw = proj_aff(3, 1.0f);
+    const Aff az = Aff{frag.z + p.bias, tr.z, br.z, nr.z};     // s.z + bias
+    const float cx0 = 0.5f * (float)(W - 1), cy0 = 0.5f * (float)(H - 1);
+    const float tmax_x = (float)(W - 1) - 1.0f / 256.0f, tmax_y = (float)(H - 1) - 1.0f / 256.0f;
+    const int pitch = depth.pitch;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(depth.data, 0, pitch * H, 0x00020000);
     float occ = 0.0f;
 #pragma unroll
     for (int i = 0; i < SOC_SSAO_MAX_KERNEL; ++i) {
-        if (i < p.ksize) {
-        const float kx = c_kernel[i][0], ky = c_kernel[i][1], kz = c_kernel[i][2];
-        f3 s = t * kx + b * ky + n * kz;          // TBN * kernelSamples[i]
-        s = frag + s * p.radius;
-        // offset = projection * vec4(sample, 1); xy /= w; xy = xy * 0.5 + 0.5
-        const float cx = P[0] * s.x + P[4] * s.y + P[8] * s.z + P[12];
-        const float cy = P[1] * s.x + P[5] * s.y + P[9] * s.z + P[13];
-        const float cw = P[3] * s.x + P[7] * s.y + P[11] * s.z + P[15];
-        const float ox = __fdividef(cx, cw) * 0.5f + 0.5f;
-        const float oy = __fdividef(cy, cw) * 0.5f + 0.5f;
-        const float dd = depth_tap(depth, ox, oy);
-        // get_view_position_from_depth(offset.xy, depth).z
-        const float ex = ox * 2.0f - 1.0f, ey = oy * 2.0f - 1.0f;
-        const float vz = ip[2] * ex + ip[6] * ey + ip[10] * dd + ip[14];
-        const float vw = ip[3] * ex + ip[7] * ey + ip[11] * dd + ip[15];
-        const float sd = __fdividef(vz, vw);
-        const float rc = clampf(__fdividef(p.radius, fabsf(frag.z - sd)), 0.0f, 1.0f);
-        const float range = rc * rc * (3.0f - 2.0f * rc);   // smoothstep(0, 1, x)
-        occ += (sd >= s.z + p.bias ? 1.0f : 0.0f) * range;
+        if (FULL || i < p.ksize) {
+            const float kx = kKernel.v[i][0], ky = kKernel.v[i][1], kz = kKernel.v[i][2];
+            const float rw = fast_rcp(aff(aw, kx, ky, kz));
+            float tx = __builtin_fmaf(aff(ax, kx, ky, kz), rw, cx0);
+            float ty = __builtin_fmaf(aff(ay, kx, ky, kz), rw, cy0);
+            tx = fminf(fmaxf(tx, 0.0f), tmax_x);
+            ty = fminf(fmaxf(ty, 0.0f), tmax_y);
+            const int fx = (int)floorf(__builtin_fmaf(tx, 256.0f, 0.5f));
+            const int fy = (int)floorf(__builtin_fmaf(ty, 256.0f, 0.5f));
+            const float wx = (float)(fx & 255) * (1.0f / 256.0f), wy = (float)(fy & 255) * (1.0f / 256.0f);
+            const int off = __mul24(fy >> 8, pitch) + (fx >> 8) * 4;
+            const f2a4 r0 = __builtin_bit_cast(f2a4, __builtin_amdgcn_raw_buffer_load_b64(rsrc, off, 0, 0));
+            const f2a4 r1 = __builtin_bit_cast(f2a4, __builtin_amdgcn_raw_buffer_load_b64(rsrc, off, pitch, 0));
+            const float top = __builtin_fmaf(wx, r0.y - r0.x, r0.x);
+            const float bot = __builtin_fmaf(wx, r1.y - r1.x, r1.x);
+            const float dd = __builtin_fmaf(wy, bot - top, top);
+            float vz, vw;   // get_view_position_from_depth(offset.xy, depth).z
+            if (SPARSE_IP) {
+                vz = __builtin_fmaf(ip[10], dd, ip[14]);
+                vw = __builtin_fmaf(ip[11], dd, ip[15]);
+            } else {
+                const float ex = (tx + 0.5f) * (2.0f / (float)W) - 1.0f, ey = (ty + 0.5f) * (2.0f / (float)H) - 1.0f;
+                vz = ip[2] * ex + ip[6] * ey + ip[10] * dd + ip[14];
+                vw = ip[3] * ex + ip[7] * ey + ip[11] * dd + ip[15];
+            }
+            const float sd = vz * fast_rcp(vw);
+            const float rc = fminf(r * fast_rcp(fabsf(frag.z - sd)), 1.0f);
+            const float range = rc * rc * (3.0f - 2.0f * rc);   // smoothstep(0, 1, x)
+            occ += (sd >= aff(az, kx, ky, kz)) ? range : 0.0f;
         }
     }
     occ = 1.0f - (occ / p.kernel_size_f);
@@ -196,13 +236,23 @@ extern "C" int soc_ssao_generation(const soc_globals* g, soc_img depth, soc_img 
     if (rc) return rc;
     if (depth.width < 2 || depth.height < 2)
         return set_error(SOC_E_SHAPE, "soc_ssao_generation: depth must be at least 2x2");
+    if ((long long)depth.pitch_bytes * depth.height >= (1ll << 31) || depth.pitch_bytes >= (1 << 23))
+        return set_error(SOC_E_SHAPE, "soc_ssao_generation: depth image exceeds the 2 GiB buffer-offset range");
     SsaoParams p = make_params(g, normal);
+    const float* IP = g->camera_inverse_projection_matrix;
+    const bool sip = IP[2] == 0.0f && IP[3] == 0.0f && IP[6] == 0.0f && IP[7] == 0.0f;
     dim3 blk(16, 16), grd(ceil_div(target.width, 16), ceil_div(target.height, 16));
-    if (noise_table)
-        ssao_kernel<true><<<grd, blk, 0, hs(stream)>>>(dimg(depth), dimg(normal), dimg(target),
-                                                       reinterpret_cast<const float2*>(noise_table), p);
-    else
-        ssao_kernel<false><<<grd, blk, 0, hs(stream)>>>(dimg(depth), dimg(normal), dimg(target), nullptr, p);
+    const float2* tb = reinterpret_cast<const float2*>(noise_table);
+    hipStream_t st = hs(stream);
+    DImg dd = dimg(depth), dn = dimg(normal), dt = dimg(target);
+#define SOC_SSAO_LAUNCH(T, B, F) ssao_kernel<T, B, F><<<grd, blk, 0, st>>>(dd, dn, dt, tb, p)
+    const bool full = p.ksize == SOC_SSAO_MAX_KERNEL;
+    if (noise_table && sip && full) SOC_SSAO_LAUNCH(true, true, true);
+    else if (noise_table && sip) SOC_SSAO_LAUNCH(true, true, false);
+    else if (noise_table) SOC_SSAO_LAUNCH(true, false, false);
+    else if (sip && full) SOC_SSAO_LAUNCH(false, true, true);
+    else SOC_SSAO_LAUNCH(false, false, false);
+#undef SOC_SSAO_LAUNCH
     return check_launch("ssao_generation");
 }
 

@@ -1,0 +1,71 @@
+"""Frame-per-GPU sharding with the one real exchange of the path: the luminance-histogram all-reduce.
+
+SURVEY.md §8e: frames are independent units; rank r renders camera r with its own TAA history. Global
+auto-exposure is the only cross-GPU dependency. After GenerateLuminanceHistogram each rank holds 256 u32
+bins, RCCL all-reduces them (1 KiB over xGMI, backend "nccl"), and every rank then resolves the same
+exposure with total_pixels = N*W*H and a 64-bit weighted sum (the reference's u32 sum would overflow
+for 8 frames). The helpers are device-agnostic so the N>1 logic is testable with gloo on CPU.
+"""
+from __future__ import annotations
+
+import math
+import os
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+SPONZA_CAMERA = ((-14.0, 2.2, 0.3), (0.0, -0.42, 0.0))
+
+
+def env() -> Tuple[int, int, int]:
+    """(rank, world_size, local_rank) from the torch.distributed.run environment."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def init(device: Optional[torch.device] = None, backend: str = "nccl") -> None:
+    _, world, _ = env()
+    if world > 1 and not dist.is_initialized():
+        if backend == "nccl":
+            dist.init_process_group(backend, device_id=device)
+        else:
+            dist.init_process_group(backend)
+
+
+def camera_for_rank(rank: int):
+    """Rank 0: the canonical Sponza-proxy view; others: seeded poses along the nave (seed 0xC5 + rank)."""
+    if rank == 0:
+        return SPONZA_CAMERA
+    rng = np.random.default_rng(0xC5 + rank)
+    pos = (float(rng.uniform(-15.0, 12.0)), float(rng.uniform(1.5, 4.0)), float(rng.uniform(-2.5, 2.5)))
+    rot = (float(rng.choice([0.0, math.pi])) + float(rng.uniform(-0.3, 0.3)), float(rng.uniform(-0.6, -0.2)), 0.0)
+    return pos, rot
+
+
+def exposure_pixels(world: int, width: int, height: int) -> Tuple[int, bool]:
+    """(total_pixels, wide_accumulator) for the resolve after the histogram exchange."""
+    return world * width * height, world > 1
+
+
+def exchange_histogram(bins: torch.Tensor, group=None) -> None:
+    """Sum the per-rank 256-bin histograms in place (u32 bins viewed as int32: two's-complement wrap)."""
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(bins, op=dist.ReduceOp.SUM, group=group)
+
+
+def max_over_ranks(x: float, device=None) -> float:
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def render_frame(renderer, g, bins: torch.Tensor, group=None) -> None:
+    """One frame of the sharded path: PRE phase, histogram exchange, POST phase (all on the frame stream)."""
+    from . import PHASE_POST_EXPOSURE, PHASE_PRE_EXPOSURE
+    renderer.execute(g, PHASE_PRE_EXPOSURE)
+    exchange_histogram(bins, group)
+    renderer.execute(g, PHASE_POST_EXPOSURE)
