@@ -240,8 +240,12 @@ int soc_ssao_blur(const soc_globals* g, soc_img ssao, soc_img target, soc_stream
 
 /* CloudRenderingTask (cloud_rendering.inl:27-54, shader :441-481): atmosphere + volumetric clouds on
  * sky pixels (depth == 1), constant (0.2,0.4,1.0) elsewhere. `noise` is the 64x64 RGBA8 or R8
- * noise texture (assets/Clouds/noise.png, REPEAT). target: RGBA8_UNORM full-res (quirk Q6). */
-int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img noise, soc_img target, soc_stream stream);
+ * noise texture (assets/Clouds/noise.png, REPEAT). target: RGBA8_UNORM full-res (quirk Q6).
+ * `workspace` (optional, soc_cloud_rendering_workspace_size bytes of device memory) enables the
+ * two-kernel path: sky pixels are compacted into a list so every lane of the march is a sky pixel. */
+size_t soc_cloud_rendering_workspace_size(int32_t width, int32_t height);
+int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img noise, soc_img target, void* workspace,
+                        soc_stream stream);
 
 /* CompositionTask (composition.inl:29-79, shader :162-225): deferred lighting with the sun ESM
  * shadow, point/spot lights, ambient * AO^strength, emissive * strength, clouds on sky pixels.
@@ -302,6 +306,7 @@ typedef struct soc_frame_images {
     /* Optional target of the last bloom upsample, read by composition as "emissive". data == NULL:
      * bloom overwrites `emissive` in place, as the reference graph does (renderer.cpp:1055-1062). */
     soc_img bloom_output;
+    void* clouds_workspace;                             /* optional, soc_cloud_rendering_workspace_size */
 } soc_frame_images;
 
 typedef struct soc_renderer soc_renderer;

@@ -179,8 +179,13 @@ def ssao_blur(g, ssao, target, stream=None):
     _check(lib().soc_ssao_blur(_gp(g), img(ssao), img(target), _stream(stream)), "ssao_blur")
 
 
-def cloud_rendering(g, depth, noise, target, stream=None):
-    _check(lib().soc_cloud_rendering(_gp(g), img(depth), img(noise), img(target), _stream(stream)), "cloud_rendering")
+def cloud_rendering_workspace(width: int, height: int, device="cuda") -> torch.Tensor:
+    return torch.zeros(int(lib().soc_cloud_rendering_workspace_size(width, height)), dtype=torch.uint8, device=device)
+
+
+def cloud_rendering(g, depth, noise, target, workspace=None, stream=None):
+    _check(lib().soc_cloud_rendering(_gp(g), img(depth), img(noise), img(target), _ptr(workspace), _stream(stream)),
+           "cloud_rendering")
 
 
 def composition(g, target, albedo, emissive, normal, depth, ssao, shadow, clouds, d_globals=None, stream=None):
@@ -256,6 +261,7 @@ def alloc_frame(width: int, height: int, device="cuda", output_format=FMT_RGBA8_
     t["output_format"] = output_format
     t["ssao_noise_table"] = torch.zeros(hh * hw * 2, dtype=torch.float32, device=device) if noise_table else None
     t["bloom_output"] = torch.zeros(H, W, 4, **f16) if bloom_output else None
+    t["clouds_workspace"] = cloud_rendering_workspace(W, H, device)
     return t
 
 
@@ -278,6 +284,7 @@ class Renderer:
         fi.auto_exposure = _ptr(frame["auto_exposure"])
         fi.d_globals = _ptr(frame.get("d_globals"))
         fi.bloom_output = img(frame.get("bloom_output"))
+        fi.clouds_workspace = _ptr(frame.get("clouds_workspace"))
         self._fi = fi
         h = lib().soc_renderer_create(C.byref(fi), _abi.RENDERER_TIMING if timing else 0)
         if not h:

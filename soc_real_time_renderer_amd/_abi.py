@@ -105,7 +105,7 @@ class FrameImages(C.Structure):
         ("shadow", SocImg), ("noise", SocImg), ("bloom_mips", SocImg * 4), ("ssao", SocImg), ("ssao_blur", SocImg),
         ("clouds", SocImg), ("color", SocImg), ("history_color", SocImg * 2), ("history_velocity", SocImg * 2),
         ("output", SocImg), ("ssao_noise_table", C.c_void_p), ("auto_exposure", C.c_void_p), ("d_globals", C.c_void_p),
-        ("bloom_output", SocImg),
+        ("bloom_output", SocImg), ("clouds_workspace", C.c_void_p),
     ]
 
 
@@ -138,7 +138,8 @@ FUNCTIONS = {
     "soc_ssao_prepare_noise": (_I, [_IMG, _IMG, _P, _P]),
     "soc_ssao_generation": (_I, [_G, _IMG, _IMG, _IMG, _P, _P]),
     "soc_ssao_blur": (_I, [_G, _IMG, _IMG, _P]),
-    "soc_cloud_rendering": (_I, [_G, _IMG, _IMG, _IMG, _P]),
+    "soc_cloud_rendering_workspace_size": (C.c_size_t, [C.c_int32, C.c_int32]),
+    "soc_cloud_rendering": (_I, [_G, _IMG, _IMG, _IMG, _P, _P]),
     "soc_composition": (_I, [_G, _P, _IMG, _IMG, _IMG, _IMG, _IMG, _IMG, _IMG, _IMG, _P]),
     "soc_generate_luminance_histogram": (_I, [_G, _IMG, _P, _P]),
     "soc_resolve_luminance_histogram": (_I, [_G, _P, C.c_uint64, C.c_int32, _P]),

@@ -7,6 +7,8 @@
 // down analytically (fast paths); both then go through the same clamp rule and lerp arithmetic, so
 // the fast paths are bit-identical to the generic one (extents <= 8192).
 // All tap weights are powers of two, so the RGBA16F results are bit-identical to the oracle's.
+#include <type_traits>
+
 #include "soc_internal.hpp"
 
 namespace soc {
@@ -61,6 +63,9 @@ __device__ __forceinline__ void store_rgb1(const DImg& im, int x, int y, f3 c) {
 // out = e*0.125 + (a+c+g+i)*0.03125 + (b+d+f+h)*0.0625 + (j+k+l+m)*0.125   (:137-140)
 __device__ __forceinline__ float down13(float a, float b, float c, float d, float e, float f, float g, float h, float i,
                                         float j, float k, float l, float m) {
+    // no contraction: the last add fused into the f16 store would become v_fma_mixlo_f16, a single
+    // rounding to f16 where the oracle rounds to f32 first (1-ulp differences, double rounding)
+#pragma clang fp contract(off)
     float r = e * 0.125f;
     r += (a + c + g + i) * 0.03125f;
     r += (b + d + f + h) * 0.0625f;
@@ -70,6 +75,7 @@ __device__ __forceinline__ float down13(float a, float b, float c, float d, floa
 
 // out = (e*4 + (b+d+f+h)*2 + (a+c+g+i)) / 16   (bloom_upsample.inl:122-125)
 __device__ __forceinline__ float up9(float a, float b, float c, float d, float e, float f, float g, float h, float i) {
+#pragma clang fp contract(off)
     float r = e * 4.0f;
     r += (b + d + f + h) * 2.0f;
     r += (a + c + g + i);
@@ -168,6 +174,209 @@ __global__ __launch_bounds__(256) void bloom_up_double(DImg src, DImg dst) {
     store_rgb1(dst, x, y, SOC_UP9(a, b, c, d, e, f, g, h, i));
 }
 
+// ------------------------------------------------------------------------------------------------
+// register-window kernels: each lane loads the raw RGBA16F texels of its window once (8-B loads, L1
+// shared with its neighbours) and evaluates the taps channel by channel; bilinear taps share their
+// horizontal lerps between taps that use the same row and x-pair. Every tap is computed with exactly
+// the arithmetic of tap()/point() above (same lerps, same order), so results are bit-identical.
+// ------------------------------------------------------------------------------------------------
+template <int C>
+__device__ __forceinline__ float chan(uint2 v) {
+    return C == 0 ? h2f((uint16_t)(v.x & 0xffffu)) : C == 1 ? h2f((uint16_t)(v.x >> 16)) : h2f((uint16_t)(v.y & 0xffffu));
+}
+
+__device__ __forceinline__ uint2 texel_clamped(const DImg& im, int x, int y) {
+    x = min(max(x, 0), im.w - 1);
+    y = min(max(y, 0), im.h - 1);
+    return row_ptr<uint2>(im, y)[x];
+}
+
+__device__ __forceinline__ float lerp_c(float a, float b, float w) {
+#pragma clang fp contract(off)
+    return a * (1.0f - w) + b * w;
+}
+
+__device__ __forceinline__ void store_rgb1_c(const DImg& im, int x, int y, float r, float g, float b) {
+    row_ptr_w<uint2>(im, y)[x] = pack_h4(f4{r, g, b, 1.0f});
+}
+
+// same-size 13-tap downsample, 2x2 output pixels per lane from a 6x6 texel window
+__global__ __launch_bounds__(256) void bloom_down_same_q(DImg src, DImg dst) {
+    const int m = blockIdx.x * BX + threadIdx.x, n = blockIdx.y * BY + threadIdx.y;
+    const int X0 = 2 * m, Y0 = 2 * n;
+    if (X0 >= dst.w || Y0 >= dst.h) return;
+    uint2 T[6][6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int c = 0; c < 6; ++c) T[r][c] = texel_clamped(src, X0 - 2 + c, Y0 - 2 + r);
+    float out[2][2][3];
+    auto run = [&](auto CH) {
+        constexpr int C = decltype(CH)::value;
+        float V[6][6];
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+#pragma unroll
+            for (int c = 0; c < 6; ++c) V[r][c] = chan<C>(T[r][c]);
+#pragma unroll
+        for (int py = 0; py < 2; ++py)
+#pragma unroll
+            for (int px = 0; px < 2; ++px) {
+                // window index of offset o: o + 2 + parity; "+Y" taps are the row below
+                auto P = [&](int ox, int oy) { return V[oy + 2 + py][ox + 2 + px]; };
+                out[py][px][C] = down13(P(-2, 2), P(0, 2), P(2, 2), P(-2, 0), P(0, 0), P(2, 0), P(-2, -2), P(0, -2),
+                                        P(2, -2), P(-1, 1), P(1, 1), P(-1, -1), P(1, -1));
+            }
+    };
+    run(std::integral_constant<int, 0>{});
+    run(std::integral_constant<int, 1>{});
+    run(std::integral_constant<int, 2>{});
+#pragma unroll
+    for (int py = 0; py < 2; ++py)
+#pragma unroll
+        for (int px = 0; px < 2; ++px)
+            if (X0 + px < dst.w && Y0 + py < dst.h)
+                store_rgb1_c(dst, X0 + px, Y0 + py, out[py][px][0], out[py][px][1], out[py][px][2]);
+}
+
+// same-size 9-tap tent upsample, 2x2 output pixels per lane from a 4x4 window
+__global__ __launch_bounds__(256) void bloom_up_same_q(DImg src, DImg dst) {
+    const int m = blockIdx.x * BX + threadIdx.x, n = blockIdx.y * BY + threadIdx.y;
+    const int X0 = 2 * m, Y0 = 2 * n;
+    if (X0 >= dst.w || Y0 >= dst.h) return;
+    uint2 T[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) T[r][c] = texel_clamped(src, X0 - 1 + c, Y0 - 1 + r);
+    float out[2][2][3];
+    auto run = [&](auto CH) {
+        constexpr int C = decltype(CH)::value;
+#pragma unroll
+        for (int py = 0; py < 2; ++py)
+#pragma unroll
+            for (int px = 0; px < 2; ++px) {
+                auto P = [&](int ox, int oy) { return chan<C>(T[oy + 1 + py][ox + 1 + px]); };
+                out[py][px][C] = up9(P(-1, 1), P(0, 1), P(1, 1), P(-1, 0), P(0, 0), P(1, 0), P(-1, -1), P(0, -1), P(1, -1));
+            }
+    };
+    run(std::integral_constant<int, 0>{});
+    run(std::integral_constant<int, 1>{});
+    run(std::integral_constant<int, 2>{});
+#pragma unroll
+    for (int py = 0; py < 2; ++py)
+#pragma unroll
+        for (int px = 0; px < 2; ++px)
+            if (X0 + px < dst.w && Y0 + py < dst.h)
+                store_rgb1_c(dst, X0 + px, Y0 + py, out[py][px][0], out[py][px][1], out[py][px][2]);
+}
+
+// 2:1 downsample: one output per lane, 6x6 source window; the 13 taps are w = 0.5 blends of the 2x2
+// blocks at source offsets 2x+k (k = -2..2), sharing the 30 horizontal lerps. Border pixels use tap().
+__global__ __launch_bounds__(256) void bloom_down_half_w(DImg src, DImg dst) {
+    const int x = blockIdx.x * BX + threadIdx.x, y = blockIdx.y * BY + threadIdx.y;
+    if (x >= dst.w || y >= dst.h) return;
+    const bool interior = 2 * x - 2 >= 0 && 2 * x + 3 <= src.w - 1 && 2 * y - 2 >= 0 && 2 * y + 3 <= src.h - 1;
+    if (!interior) {
+        auto AX = [&](int k) { return axis_from_fixed(256 * (2 * x + k) + 128, src.w); };
+        auto AY = [&](int k) { return axis_from_fixed(256 * (2 * y + k) + 128, src.h); };
+        const Axis xm2 = AX(-2), xm1 = AX(-1), x0 = AX(0), xp1 = AX(1), xp2 = AX(2);
+        const Axis ym2 = AY(-2), ym1 = AY(-1), y0 = AY(0), yp1 = AY(1), yp2 = AY(2);
+        f3 a = tap(src, xm2, yp2), b = tap(src, x0, yp2), c = tap(src, xp2, yp2);
+        f3 d = tap(src, xm2, y0), e = tap(src, x0, y0), f = tap(src, xp2, y0);
+        f3 g = tap(src, xm2, ym2), h = tap(src, x0, ym2), i = tap(src, xp2, ym2);
+        f3 j = tap(src, xm1, yp1), k = tap(src, xp1, yp1), l = tap(src, xm1, ym1), m = tap(src, xp1, ym1);
+        store_rgb1(dst, x, y, SOC_DOWN13(a, b, c, d, e, f, g, h, i, j, k, l, m));
+        return;
+    }
+    uint2 T[6][6];
+    const uint2* base = row_ptr<uint2>(src, 2 * y - 2) + (2 * x - 2);
+    const int pitch8 = src.pitch / 8;
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int c = 0; c < 6; ++c) T[r][c] = base[r * pitch8 + c];
+    float out[3];
+    auto run = [&](auto CH) {
+        constexpr int C = decltype(CH)::value;
+        float Hl[6][5];   // row r, x-pair k+2 = blend of window columns (k+2, k+3)
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+#pragma unroll
+            for (int k = 0; k < 5; ++k) Hl[r][k] = lerp_c(chan<C>(T[r][k]), chan<C>(T[r][k + 1]), 0.5f);
+        auto S = [&](int kx, int ky) { return lerp_c(Hl[ky + 2][kx + 2], Hl[ky + 3][kx + 2], 0.5f); };
+        out[C] = down13(S(-2, 2), S(0, 2), S(2, 2), S(-2, 0), S(0, 0), S(2, 0), S(-2, -2), S(0, -2), S(2, -2), S(-1, 1),
+                        S(1, 1), S(-1, -1), S(1, -1));
+    };
+    run(std::integral_constant<int, 0>{});
+    run(std::integral_constant<int, 1>{});
+    run(std::integral_constant<int, 2>{});
+    store_rgb1_c(dst, x, y, out[0], out[1], out[2]);
+}
+
+// 1:2 upsample: a 2x2 output quad per lane from the 5x5 source window around (m, n). Even outputs use
+// x-pairs (m-2..m) at w = 3/4, odd ones (m-1..m+1) at w = 1/4 (and likewise in y). Border quads use tap().
+__global__ __launch_bounds__(256) void bloom_up_double_q(DImg src, DImg dst) {
+    const int m = blockIdx.x * BX + threadIdx.x, n = blockIdx.y * BY + threadIdx.y;
+    if (m >= src.w || n >= src.h) return;
+    const int X0 = 2 * m, Y0 = 2 * n;
+    const bool interior = m - 2 >= 0 && m + 2 <= src.w - 1 && n - 2 >= 0 && n + 2 <= src.h - 1;
+    if (!interior) {
+#pragma unroll
+        for (int py = 0; py < 2; ++py)
+#pragma unroll
+            for (int px = 0; px < 2; ++px) {
+                const int x = X0 + px, y = Y0 + py;
+                auto AX = [&](int k) { return axis_from_fixed(128 * x - 64 + 256 * k, src.w); };
+                auto AY = [&](int k) { return axis_from_fixed(128 * y - 64 + 256 * k, src.h); };
+                const Axis xm = AX(-1), x0 = AX(0), xp = AX(1), ym = AY(-1), y0 = AY(0), yp = AY(1);
+                f3 a = tap(src, xm, yp), b = tap(src, x0, yp), c = tap(src, xp, yp);
+                f3 d = tap(src, xm, y0), e = tap(src, x0, y0), f = tap(src, xp, y0);
+                f3 g = tap(src, xm, ym), h = tap(src, x0, ym), i = tap(src, xp, ym);
+                store_rgb1(dst, x, y, SOC_UP9(a, b, c, d, e, f, g, h, i));
+            }
+        return;
+    }
+    uint2 T[5][5];
+    const uint2* base = row_ptr<uint2>(src, n - 2) + (m - 2);
+    const int pitch8 = src.pitch / 8;
+#pragma unroll
+    for (int r = 0; r < 5; ++r)
+#pragma unroll
+        for (int c = 0; c < 5; ++c) T[r][c] = base[r * pitch8 + c];
+    float out[2][2][3];
+    auto run = [&](auto CH) {
+        constexpr int C = decltype(CH)::value;
+        float V[5][5];
+#pragma unroll
+        for (int r = 0; r < 5; ++r)
+#pragma unroll
+            for (int c = 0; c < 5; ++c) V[r][c] = chan<C>(T[r][c]);
+#pragma unroll
+        for (int px = 0; px < 2; ++px) {
+            const float wx = px ? 0.25f : 0.75f;
+            float Hl[5][3];   // row r, x-tap k+1: blend of window columns (k+1+px, k+2+px)
+#pragma unroll
+            for (int r = 0; r < 5; ++r)
+#pragma unroll
+                for (int k = 0; k < 3; ++k) Hl[r][k] = lerp_c(V[r][k + px], V[r][k + 1 + px], wx);
+#pragma unroll
+            for (int py = 0; py < 2; ++py) {
+                const float wy = py ? 0.25f : 0.75f;
+                auto S = [&](int kx, int ky) { return lerp_c(Hl[ky + 1 + py][kx + 1], Hl[ky + 2 + py][kx + 1], wy); };
+                out[py][px][C] = up9(S(-1, 1), S(0, 1), S(1, 1), S(-1, 0), S(0, 0), S(1, 0), S(-1, -1), S(0, -1), S(1, -1));
+            }
+        }
+    };
+    run(std::integral_constant<int, 0>{});
+    run(std::integral_constant<int, 1>{});
+    run(std::integral_constant<int, 2>{});
+#pragma unroll
+    for (int py = 0; py < 2; ++py)
+#pragma unroll
+        for (int px = 0; px < 2; ++px) store_rgb1_c(dst, X0 + px, Y0 + py, out[py][px][0], out[py][px][1], out[py][px][2]);
+}
+
 constexpr int kFastMax = 8192;
 
 }  // namespace
@@ -177,9 +386,10 @@ int launch_bloom_down(const soc_img& hi, const soc_img& lo, hipStream_t s, int f
     DImg src = dimg(hi), dst = dimg(lo);
     const bool small = hi.width <= kFastMax && hi.height <= kFastMax;
     if (!force_generic && small && hi.width == lo.width && hi.height == lo.height) {
-        bloom_down_same<<<grd, blk, 0, s>>>(src, dst);
+        dim3 g2(ceil_div(ceil_div(lo.width, 2), BX), ceil_div(ceil_div(lo.height, 2), BY));
+        bloom_down_same_q<<<g2, blk, 0, s>>>(src, dst);
     } else if (!force_generic && small && hi.width == 2 * lo.width && hi.height == 2 * lo.height) {
-        bloom_down_half<<<grd, blk, 0, s>>>(src, dst);
+        bloom_down_half_w<<<grd, blk, 0, s>>>(src, dst);
     } else {
         bloom_down_generic<<<grd, blk, 0, s>>>(src, dst, 1.0f / (float)hi.width, 1.0f / (float)hi.height);
     }
@@ -191,9 +401,11 @@ int launch_bloom_up(const soc_img& lo, const soc_img& hi, hipStream_t s, int for
     DImg src = dimg(lo), dst = dimg(hi);
     const bool small = hi.width <= kFastMax && hi.height <= kFastMax;
     if (!force_generic && small && hi.width == lo.width && hi.height == lo.height) {
-        bloom_up_same<<<grd, blk, 0, s>>>(src, dst);
+        dim3 g2(ceil_div(ceil_div(hi.width, 2), BX), ceil_div(ceil_div(hi.height, 2), BY));
+        bloom_up_same_q<<<g2, blk, 0, s>>>(src, dst);
     } else if (!force_generic && small && hi.width == 2 * lo.width && hi.height == 2 * lo.height) {
-        bloom_up_double<<<grd, blk, 0, s>>>(src, dst);
+        dim3 g2(ceil_div(lo.width, BX), ceil_div(lo.height, BY));
+        bloom_up_double_q<<<g2, blk, 0, s>>>(src, dst);
     } else {
         bloom_up_generic<<<grd, blk, 0, s>>>(src, dst, 1.0f / (float)lo.width, 1.0f / (float)lo.height);
     }

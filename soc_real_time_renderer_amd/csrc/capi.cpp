@@ -158,7 +158,7 @@ const FieldInfo kFields[] = {
     F(soc_frame_images, ssao), F(soc_frame_images, ssao_blur), F(soc_frame_images, clouds), F(soc_frame_images, color),
     F(soc_frame_images, history_color), F(soc_frame_images, history_velocity), F(soc_frame_images, output),
     F(soc_frame_images, ssao_noise_table), F(soc_frame_images, auto_exposure), F(soc_frame_images, d_globals),
-    F(soc_frame_images, bloom_output),
+    F(soc_frame_images, bloom_output), F(soc_frame_images, clouds_workspace),
 };
 #undef F
 }  // namespace
@@ -505,7 +505,7 @@ void build_passes(soc_renderer* r) {
         [r](const soc_globals* g, hipStream_t s) { return soc_ssao_blur(g, r->img.ssao, r->img.ssao_blur, (soc_stream)s); });
     // renderer.cpp:1094-1101
     add("CloudRendering", "Sky Rendering", SOC_PHASE_PRE_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
-        return soc_cloud_rendering(g, r->img.depth, r->img.noise, r->img.clouds, (soc_stream)s);
+        return soc_cloud_rendering(g, r->img.depth, r->img.noise, r->img.clouds, r->img.clouds_workspace, (soc_stream)s);
     });
     // renderer.cpp:1103-1117
     add("Composition", "Composition", SOC_PHASE_PRE_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {

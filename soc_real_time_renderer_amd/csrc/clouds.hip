@@ -50,11 +50,16 @@ __device__ __forceinline__ float2 rsi(f3 p, f3 d, float radius) {
     return float2{-PoD - delta, -PoD + delta};
 }
 
-// texture(noise, uv).x under REPEAT + the sampling contract, from the LDS quad table.
-__device__ __forceinline__ float noise_tap(const Ctx& cx, float u, float v) {
-    const Axis ax = axis_repeat_pow2(u, kNoise, kNoiseMask), ay = axis_repeat_pow2(v, kNoise, kNoiseMask);
-    const uint32_t q = cx.quads[ay.i0 * kNoise + ax.i0];
-    return bilerp1(unorm8(q & 0xffu), unorm8((q >> 8) & 0xffu), unorm8((q >> 16) & 0xffu), unorm8(q >> 24), ax.w, ay.w);
+// texture(noise, uv).x under REPEAT + the sampling contract, from the LDS quad table. The two taps of
+// get_3d_noise sit exactly 17 texels apart in u and v (zStretch = 17/64), so they share one axis
+// computation; the bilinear blend runs on the raw bytes and is scaled by 1/255 once. Both regroup the
+// contract's fp32 roundings; clouds are checked against the RGBA8 tolerance.
+__device__ __forceinline__ float quad_bilerp(uint32_t q, float wx, float wy) {
+    const float c0 = (float)(q & 0xffu), c1 = (float)((q >> 8) & 0xffu);     // v_cvt_f32_ubyte0..3
+    const float c2 = (float)((q >> 16) & 0xffu), c3 = (float)(q >> 24);
+    const float top = __builtin_fmaf(wx, c1 - c0, c0);
+    const float bot = __builtin_fmaf(wx, c3 - c2, c2);
+    return __builtin_fmaf(wy, bot - top, top);
 }
 
 // get_3d_noise, :219-233
@@ -63,9 +68,14 @@ __device__ __forceinline__ float noise3(const Ctx& cx, f3 pos) {
     const float f = pos.z - p;
     const float inv = 1.0f / 64.0f, zs = 17.0f * inv;
     const float cu = pos.x * inv + p * zs, cv = pos.y * inv + p * zs;
-    const float a = noise_tap(cx, cu, cv);
-    const float b = noise_tap(cx, cu + zs, cv + zs);
-    return mixf(a, b, f);
+    const int fx = (int)floorf(__builtin_fmaf(__builtin_fmaf(cu, 64.0f, -0.5f), 256.0f, 0.5f));
+    const int fy = (int)floorf(__builtin_fmaf(__builtin_fmaf(cv, 64.0f, -0.5f), 256.0f, 0.5f));
+    const float wx = (float)(fx & 255) * (1.0f / 256.0f), wy = (float)(fy & 255) * (1.0f / 256.0f);
+    const int ix = (fx >> 8) & kNoiseMask, iy = (fy >> 8) & kNoiseMask;
+    const uint32_t q0 = cx.quads[iy * kNoise + ix];
+    const uint32_t q1 = cx.quads[((iy + 17) & kNoiseMask) * kNoise + ((ix + 17) & kNoiseMask)];
+    const float a = quad_bilerp(q0, wx, wy), b = quad_bilerp(q1, wx, wy);
+    return __builtin_fmaf(f, b - a, a) * (1.0f / 255.0f);
 }
 
 // get_clouds, :235-262
@@ -169,12 +179,12 @@ __device__ f3 atmosphere(f3 r, f3 r0, f3 pSun, float iTime) {
     const float mu = dot3(r, pSun), mumu = mu * mu, gg = g0 * g0;
     const float pRlh = 3.0f / (16.0f * PI) * (1.0f + mumu);
     const float pMie = 3.0f / (8.0f * PI) * ((1.0f - gg) * (mumu + 1.0f)) / (powf(1.0f + gg - 2.0f * mu * g0, 1.5f) * (2.0f + gg));
-    const float inv_shR = 1.0f / shRlh, inv_shM = 1.0f / shMie;
+    const float kR = -1.44269504f / shRlh, kM = -1.44269504f / shMie;   // exp(-h/sh) = exp2(h * kR)
     for (int i = 0; i < 16; i++) {
         const f3 iPos = r0 + r * (iTime + iStep * 0.5f);
         const float iHeight = length3(iPos) - rPlanet;
-        const float odR = __expf(-iHeight * inv_shR) * iStep;
-        const float odM = __expf(-iHeight * inv_shM) * iStep;
+        const float odR = __builtin_amdgcn_exp2f(iHeight * kR) * iStep;
+        const float odM = __builtin_amdgcn_exp2f(iHeight * kM) * iStep;
         iOdRlh += odR;
         iOdMie += odM;
         const float jStep = rsi(iPos, pSun, rAtmos).y / 8.0f;
@@ -183,8 +193,8 @@ __device__ f3 atmosphere(f3 r, f3 r0, f3 pSun, float iTime) {
         for (int j = 0; j < 8; j++) {
             const f3 jPos = iPos + pSun * (jTime + jStep * 0.5f);
             const float jHeight = length3(jPos) - rPlanet;
-            jOdR += __expf(-jHeight * inv_shR) * jStep;
-            jOdM += __expf(-jHeight * inv_shM) * jStep;
+            jOdR += __builtin_amdgcn_exp2f(jHeight * kR) * jStep;
+            jOdM += __builtin_amdgcn_exp2f(jHeight * kM) * jStep;
             jTime += jStep;
         }
         const float fm = kMie * (iOdMie + jOdM);
@@ -199,25 +209,31 @@ __device__ f3 atmosphere(f3 r, f3 r0, f3 pSun, float iTime) {
 
 constexpr int TX = 16, TY = 16;
 
+// Shading of one sky pixel (main(), :445-477).
+__device__ __forceinline__ uint32_t shade_sky(const CloudParams& p, const uint32_t* quads, int x, int y) {
+    const float ru = (float)x / p.res_x_m1, rv = (float)y / p.res_y_m1;
+    const float ndx = ru * 2.0f - 1.0f, ndy = rv * 2.0f - 1.0f;
+    const f4 rvs = mul(p.inv_proj, f4{ndx, ndy, -1.0f, 0.0f});
+    const f4 rws = mul(p.inv_view, f4{rvs.x, rvs.y, -1.0f, 0.0f});
+    const f3 dir = normalize3(f3{rws.x, rws.y, rws.z});
+    const f3 sun = f3{p.sun[0], p.sun[1], p.sun[2]};
+    const f3 r0 = f3{0.0f + p.cam[0], 6372e3f + p.cam[1], 0.0f + p.cam[2]};
+    Ctx cx;
+    cx.quads = quads;
+    cx.cam_x = p.cam[0];
+    cx.cam_z = p.cam[2];
+    cx.time = -1.0f * 0.02f * p.elapsed;
+    const float dither = bayer16((float)x, (float)y);
+    f3 color = atmosphere(dir, r0, sun, p.elapsed);
+    color = volumetric_clouds(cx, dir, sun, color, dither, f3{0.8f, 0.8f, 0.8f});
+    color = color * p.sun_factor;
+    return pack_unorm8x4(f4{color.x, color.y, color.z, 1.0f});
+}
+
+// Stage the noise .x channel as 2x2 REPEAT quads (quad i = texels (x,y), (x+1,y), (x,y+1), (x+1,y+1)).
 template <bool NOISE_R8>
-__global__ __launch_bounds__(256) void clouds_kernel(DImg depth, DImg noise, DImg target, CloudParams p) {
-    __shared__ uint32_t quads[kNoise * kNoise];
-    const int x = blockIdx.x * TX + threadIdx.x, y = blockIdx.y * TY + threadIdx.y;
-    const int tid = threadIdx.y * TX + threadIdx.x;
-    const bool inside = x < p.res_x && y < p.res_y && x < target.w && y < target.h;
-    float ru = 0.0f, rv = 0.0f;
-    bool sky = false;
-    if (inside) {
-        ru = (float)x / p.res_x_m1;
-        rv = (float)y / p.res_y_m1;
-        sky = sample_f32(depth, ru, rv) == 1.0f;   // textureLod(depth, ray_uv, 0), :458
-    }
-    if (!__syncthreads_or(sky)) {
-        if (inside) row_ptr_w<uint32_t>(target, y)[x] = pack_unorm8x4(f4{0.2f, 0.4f, 1.0f, 1.0f});
-        return;
-    }
-    // stage the noise .x channel as 2x2 REPEAT quads
-    for (int i = tid; i < kNoise * kNoise; i += TX * TY) {
+__device__ __forceinline__ void stage_noise(const DImg& noise, uint32_t* quads, int tid, int nthreads) {
+    for (int i = tid; i < kNoise * kNoise; i += nthreads) {
         const int nx = i & kNoiseMask, ny = i >> 6;
         const int nx1 = (nx + 1) & kNoiseMask, ny1 = (ny + 1) & kNoiseMask;
         auto texel = [&](int tx, int ty) -> uint32_t {
@@ -226,27 +242,66 @@ __global__ __launch_bounds__(256) void clouds_kernel(DImg depth, DImg noise, DIm
         };
         quads[i] = texel(nx, ny) | (texel(nx1, ny) << 8) | (texel(nx, ny1) << 16) | (texel(nx1, ny1) << 24);
     }
+}
+
+__device__ __forceinline__ bool is_sky(const CloudParams& p, const DImg& depth, int x, int y) {
+    return sample_f32(depth, (float)x / p.res_x_m1, (float)y / p.res_y_m1) == 1.0f;   // textureLod(depth, ray_uv, 0), :458
+}
+
+// Single-kernel path (no workspace): 16x16 tiles, a tile without sky exits after its depth test.
+template <bool NOISE_R8>
+__global__ __launch_bounds__(256) void clouds_kernel(DImg depth, DImg noise, DImg target, CloudParams p) {
+    __shared__ uint32_t quads[kNoise * kNoise];
+    const int x = blockIdx.x * TX + threadIdx.x, y = blockIdx.y * TY + threadIdx.y;
+    const int tid = threadIdx.y * TX + threadIdx.x;
+    const bool inside = x < p.res_x && y < p.res_y && x < target.w && y < target.h;
+    const bool sky = inside && is_sky(p, depth, x, y);
+    if (!__syncthreads_or(sky)) {
+        if (inside) row_ptr_w<uint32_t>(target, y)[x] = pack_unorm8x4(f4{0.2f, 0.4f, 1.0f, 1.0f});
+        return;
+    }
+    stage_noise<NOISE_R8>(noise, quads, tid, TX * TY);
     __syncthreads();
     if (!inside) return;
-    f3 color = f3{0.2f, 0.4f, 1.0f};
+    row_ptr_w<uint32_t>(target, y)[x] = sky ? shade_sky(p, quads, x, y) : pack_unorm8x4(f4{0.2f, 0.4f, 1.0f, 1.0f});
+}
+
+// Two-kernel path. classify: non-sky pixels get the constant colour; sky pixels are appended to a
+// compact list (one atomic per wave, lanes in ballot order, so a wave's list entries stay one 8x8
+// tile). march: a grid-stride loop over the list, every lane a sky pixel.
+__global__ __launch_bounds__(256) void clouds_classify(DImg depth, DImg target, CloudParams p,
+                                                       uint32_t* __restrict__ counter, uint32_t* __restrict__ list) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+    const int y = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const bool inside = x < p.res_x && y < p.res_y && x < target.w && y < target.h;
+    const bool sky = inside && is_sky(p, depth, x, y);
+    if (inside && !sky) row_ptr_w<uint32_t>(target, y)[x] = pack_unorm8x4(f4{0.2f, 0.4f, 1.0f, 1.0f});
+    const unsigned long long m = __ballot(sky);
+    if (m == 0ull) return;
+    uint32_t base = 0;
+    if (lane == __builtin_ctzll(m)) base = atomicAdd(counter, (uint32_t)__builtin_popcountll(m));
+    base = __shfl(base, __builtin_ctzll(m));
     if (sky) {
-        const float ndx = ru * 2.0f - 1.0f, ndy = rv * 2.0f - 1.0f;
-        const f4 rvs = mul(p.inv_proj, f4{ndx, ndy, -1.0f, 0.0f});
-        const f4 rws = mul(p.inv_view, f4{rvs.x, rvs.y, -1.0f, 0.0f});
-        const f3 dir = normalize3(f3{rws.x, rws.y, rws.z});
-        const f3 sun = f3{p.sun[0], p.sun[1], p.sun[2]};
-        const f3 r0 = f3{0.0f + p.cam[0], 6372e3f + p.cam[1], 0.0f + p.cam[2]};
-        Ctx cx;
-        cx.quads = quads;
-        cx.cam_x = p.cam[0];
-        cx.cam_z = p.cam[2];
-        cx.time = -1.0f * 0.02f * p.elapsed;
-        const float dither = bayer16((float)x, (float)y);
-        color = atmosphere(dir, r0, sun, p.elapsed);
-        color = volumetric_clouds(cx, dir, sun, color, dither, f3{0.8f, 0.8f, 0.8f});
-        color = color * p.sun_factor;
+        const uint32_t rank = (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
+        list[base + rank] = ((uint32_t)y << 16) | (uint32_t)x;
     }
-    row_ptr_w<uint32_t>(target, y)[x] = pack_unorm8x4(f4{color.x, color.y, color.z, 1.0f});
+}
+
+template <bool NOISE_R8>
+__global__ __launch_bounds__(256) void clouds_march(DImg noise, DImg target, CloudParams p,
+                                                    const uint32_t* __restrict__ counter, const uint32_t* __restrict__ list) {
+    __shared__ uint32_t quads[kNoise * kNoise];
+    const uint32_t count = *counter;
+    const uint32_t first = blockIdx.x * 256u;
+    if (first >= count) return;                      // whole workgroup without work: skip the LDS fill
+    stage_noise<NOISE_R8>(noise, quads, threadIdx.x, 256);
+    __syncthreads();
+    for (uint32_t i = first + threadIdx.x; i < count; i += gridDim.x * 256u) {
+        const uint32_t e = list[i];
+        const int x = (int)(e & 0xffffu), y = (int)(e >> 16);
+        row_ptr_w<uint32_t>(target, y)[x] = shade_sky(p, quads, x, y);
+    }
 }
 
 }  // namespace
@@ -254,7 +309,13 @@ __global__ __launch_bounds__(256) void clouds_kernel(DImg depth, DImg noise, DIm
 
 using namespace soc;
 
-extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img noise, soc_img target, soc_stream stream) {
+extern "C" size_t soc_cloud_rendering_workspace_size(int32_t width, int32_t height) {
+    if (width <= 0 || height <= 0) return 0;
+    return 256 + (size_t)width * (size_t)height * sizeof(uint32_t);
+}
+
+extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img noise, soc_img target, void* workspace,
+                                   soc_stream stream) {
     static const char* P = "soc_cloud_rendering";
     if (!g) return set_error(SOC_E_INVALID_ARG, "%s: null globals", P);
     int rc = check_img(depth, SOC_FMT_D32F, P, "depth");
@@ -280,10 +341,34 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
     p.sun_factor = fmaxf(fminf(fabsf(p.sun[0]), fabsf(p.sun[2])) + p.sun[1], 0.0f);
     const int W = std::min(target.width, p.res_x), H = std::min(target.height, p.res_y);
     if (W <= 0 || H <= 0) return SOC_OK;
-    dim3 blk(TX, TY), grd(ceil_div(W, TX), ceil_div(H, TY));
-    if (noise.format == SOC_FMT_R8_UNORM)
-        clouds_kernel<true><<<grd, blk, 0, hs(stream)>>>(dimg(depth), dimg(noise), dimg(target), p);
-    else
-        clouds_kernel<false><<<grd, blk, 0, hs(stream)>>>(dimg(depth), dimg(noise), dimg(target), p);
+    if (W > 65535 || H > 65535) return set_error(SOC_E_SHAPE, "%s: extent above 65535", P);
+    hipStream_t s = hs(stream);
+    const bool r8 = noise.format == SOC_FMT_R8_UNORM;
+    if (!workspace) {
+        dim3 blk(TX, TY), grd(ceil_div(W, TX), ceil_div(H, TY));
+        if (r8) clouds_kernel<true><<<grd, blk, 0, s>>>(dimg(depth), dimg(noise), dimg(target), p);
+        else clouds_kernel<false><<<grd, blk, 0, s>>>(dimg(depth), dimg(noise), dimg(target), p);
+        return check_launch("cloud_rendering");
+    }
+    uint32_t* counter = static_cast<uint32_t*>(workspace);
+    uint32_t* list = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + 256);
+    hipError_t e = hipMemsetAsync(counter, 0, sizeof(uint32_t), s);
+    if (e != hipSuccess) return set_error(SOC_E_HIP, "%s: %s", P, hipGetErrorString(e));
+    clouds_classify<<<dim3(ceil_div(W, 16), ceil_div(H, 16)), 256, 0, s>>>(dimg(depth), dimg(target), p, counter, list);
+    // One resident wave set: every lane loops over the list with a grid stride, so the long per-pixel
+    // march is balanced over all SIMDs instead of running as a second, partially filled round.
+    static int resident = 0;
+    if (!resident) {
+        int dev = 0, cus = 256, per_cu = 0;
+        (void)hipGetDevice(&dev);
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0) cus = prop.multiProcessorCount;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, clouds_march<false>, 256, 0) != hipSuccess || per_cu < 1)
+            per_cu = 4;
+        resident = per_cu * cus;
+    }
+    const int grid = (int)std::min<long long>(resident, ((long long)W * H + 255) / 256);
+    if (r8) clouds_march<true><<<grid, 256, 0, s>>>(dimg(noise), dimg(target), p, counter, list);
+    else clouds_march<false><<<grid, 256, 0, s>>>(dimg(noise), dimg(target), p, counter, list);
     return check_launch("cloud_rendering");
 }

@@ -237,13 +237,15 @@ def test_tone_mapping(soc, oracle, W, H, fmt):
 
 
 # ------------------------------------------------------------------------------------------------ clouds
-@pytest.mark.parametrize("W,H,pitch", [(96, 64, -0.42), (160, 90, -0.9), (480, 270, -0.42)])
-def test_clouds(soc, oracle, W, H, pitch):
+@pytest.mark.parametrize("W,H,pitch", [(96, 64, -0.42), (160, 90, -0.9), (480, 270, -0.42), (1920, 1080, -0.6)])
+@pytest.mark.parametrize("compact", [False, True])
+def test_clouds(soc, oracle, W, H, pitch, compact):
     g, gb = sponza_inputs(W, H, camera=((-14.0, 2.2, 0.3), (0.0, pitch, 0.0)), elapsed=10.0)
     ref = np.zeros((H, W, 4), np.uint8)
     oracle.cloud_rendering(g, gb["depth"], gb["noise"], ref)
     out = torch.zeros(H, W, 4, dtype=torch.uint8, device=DEV)
-    soc.cloud_rendering(g, dev(gb["depth"]), dev(gb["noise"]), out)
+    ws = soc.cloud_rendering_workspace(W, H) if compact else None
+    soc.cloud_rendering(g, dev(gb["depth"]), dev(gb["noise"]), out, ws)
     d = np.abs(host(out).astype(np.int32) - ref.astype(np.int32))
     assert (d <= 2).mean() >= 0.995, ((d <= 2).mean(), d.max())
     nonsky = gb["depth"] < 1.0
