@@ -9,6 +9,12 @@
 // of a bilinear REPEAT tap), 16 KiB per workgroup.
 #include "soc_internal.hpp"
 
+// Profiling builds only (tools/clouds_variants.py): 1 = atmosphere only, 2 = cloud march only,
+// 3 = cloud march without the sun-visibility march. The library is always built with 0.
+#ifndef SOC_CLOUDS_PROFILE
+#define SOC_CLOUDS_PROFILE 0
+#endif
+
 namespace soc {
 namespace {
 
@@ -78,31 +84,57 @@ __device__ __forceinline__ float noise3(const Ctx& cx, f3 pos) {
     return __builtin_fmaf(f, b - a, a) * (1.0f / 255.0f);
 }
 
-// get_clouds, :235-262
-__device__ float get_clouds(const Ctx& cx, f3 p) {
-    const float h = length3(f3{p.x, p.y + kEarthRadius, p.z}) - kEarthRadius;
+// |v| with the hardware square root (1 ulp). Every length in this pass is an Earth-scale distance
+// (|v| ~ 6.4e6 m, ulp 0.5 m), far from the denormal range the full-precision sequence guards.
+__device__ __forceinline__ float hw_length3(f3 v) { return __builtin_amdgcn_sqrtf(dot3(v, v)); }
+
+// Altitude above the planet of a point given relative to the camera's ground point.
+__device__ __forceinline__ float cloud_height(f3 p) { return hw_length3(f3{p.x, p.y + kEarthRadius, p.z}) - kEarthRadius; }
+
+// get_clouds, :235-262, for a point whose altitude h is already known to lie inside the layer.
+// The four octaves carry weights 1/2, 1/4, 1/8, 1/16 and each lies in [0, 1], so once the partial sum
+// plus the largest possible remainder stays below the smoothstep's lower edge 0.55 the result is
+// exactly 0 (smoothstep clamps to 0) and the remaining octaves are skipped. The 1e-4 margin covers the
+// fp32 rounding of the remainder, so the early exits never change a result.
+__device__ float clouds_at(const Ctx& cx, f3 p, float h) {
     p = f3{p.x + cx.cam_x, h, p.z + cx.cam_z};
-    if (p.y < kMinH || p.y > kMaxH) return 0.0f;
     const f3 mv = f3{cx.time, 0.0f, cx.time};
     const f3 cc = p * 0.001f + mv;
     float n = noise3(cx, cc) * 0.5f;
     n += noise3(cx, cc * 2.0f + mv) * 0.25f;
+    if (n < 0.55f - 0.1875f - 1e-4f) return 0.0f;
     n += noise3(cx, cc * 7.0f - mv) * 0.125f;
+    if (n < 0.55f - 0.0625f - 1e-4f) return 0.0f;
     n += noise3(cx, (cc + mv) * 16.0f) * 0.0625f;
     const float hh = p.y - kMinH;
     const float th = (1.0f - __expf(-0.01f * hh)) * __expf(-0.004f * hh);
-    const float t = clampf((n - 0.55f) / (0.6f - 0.55f), 0.0f, 1.0f);
+    const float t = clampf((n - 0.55f) * (1.0f / (0.6f - 0.55f)), 0.0f, 1.0f);
     const float clouds = t * t * (3.0f - 2.0f * t) * th;
     return clouds * 0.03f;
 }
 
-// getSunVisibility, :264-278
+__device__ __forceinline__ float get_clouds(const Ctx& cx, f3 p) {
+    const float h = cloud_height(p);
+    if (h < kMinH || h > kMaxH) return 0.0f;
+    return clouds_at(cx, p, h);
+}
+
+// getSunVisibility, :264-278. When the march starts out moving away from the planet centre
+// ((p + R e_y) . sun > 0) the altitude grows monotonically along it (|a + t s|^2 is convex in t), so
+// once a step leaves the top of the layer every later step returns 0, and stopping there leaves tr
+// unchanged (tr + 0 == tr).
 __device__ float sun_visibility(const Ctx& cx, f3 p, f3 sun) {
     const float rSteps = 500.0f / 10.0f;
     const f3 inc = sun * rSteps;
     f3 pos = inc * 0.5f + p;
     float tr = 0.0f;
-    for (int i = 0; i < 10; i++, pos = pos + inc) tr += get_clouds(cx, pos);
+    if (SOC_CLOUDS_PROFILE == 3) return 1.0f;
+    const bool rising = dot3(f3{p.x, p.y + kEarthRadius, p.z}, sun) > 0.0f;
+    for (int i = 0; i < 10; i++, pos = pos + inc) {
+        const float h = cloud_height(pos);
+        if (h > kMaxH && rising) break;
+        if (h >= kMinH && h <= kMaxH) tr += clouds_at(cx, pos, h);
+    }
     return __expf(-tr * rSteps);
 }
 
@@ -148,9 +180,22 @@ __device__ f3 volumetric_clouds(const Ctx& cx, f3 dir, f3 sun, f3 color, float d
     const float x = dot3(sun, dir);
     const float phase = mixf(hg_phase(x, -0.5f * 0.8f), hg_phase(x, 0.8f * 0.8f), 0.5f);
     const f3 sky = scattering_top(sun);
-    for (int i = 0; i < 24; i++, cp = cp + inc) {
+    // Two passes over the 24 steps so that the expensive sun march runs once per DENSE step of each lane
+    // rather than once per step that is dense in any lane of the wave: pass 1 records the dense steps,
+    // pass 2 visits them in order, re-deriving each od from the same cp bits (same additions) so the
+    // accumulation is the reference loop's, step for step.
+    uint32_t dense = 0;
+    {
+        f3 q = cp;
+        for (int i = 0; i < 24; i++, q = q + inc)
+            if (!(get_clouds(cx, q) * stepLength <= 0.0f)) dense |= 1u << i;
+    }
+    int at = 0;
+    while (dense) {
+        const int i = __builtin_ctz(dense);
+        dense &= dense - 1u;
+        for (; at < i; ++at) cp = cp + inc;
         const float od = get_clouds(cx, cp) * stepLength;
-        if (od <= 0.0f) continue;
         const float integral = __expf(-1.11f * rLOG2 * od) * (-1.0f / 1.11f) + 1.0f / 1.11f;
         const float beers = 1.0f - __expf(-(od * kLn2) * 2.0f);
         const float vis = sun_visibility(cx, cp, sun);
@@ -182,7 +227,7 @@ __device__ f3 atmosphere(f3 r, f3 r0, f3 pSun, float iTime) {
     const float kR = -1.44269504f / shRlh, kM = -1.44269504f / shMie;   // exp(-h/sh) = exp2(h * kR)
     for (int i = 0; i < 16; i++) {
         const f3 iPos = r0 + r * (iTime + iStep * 0.5f);
-        const float iHeight = length3(iPos) - rPlanet;
+        const float iHeight = hw_length3(iPos) - rPlanet;
         const float odR = __builtin_amdgcn_exp2f(iHeight * kR) * iStep;
         const float odM = __builtin_amdgcn_exp2f(iHeight * kM) * iStep;
         iOdRlh += odR;
@@ -192,7 +237,7 @@ __device__ f3 atmosphere(f3 r, f3 r0, f3 pSun, float iTime) {
 #pragma unroll 4
         for (int j = 0; j < 8; j++) {
             const f3 jPos = iPos + pSun * (jTime + jStep * 0.5f);
-            const float jHeight = length3(jPos) - rPlanet;
+            const float jHeight = hw_length3(jPos) - rPlanet;
             jOdR += __builtin_amdgcn_exp2f(jHeight * kR) * jStep;
             jOdM += __builtin_amdgcn_exp2f(jHeight * kM) * jStep;
             jTime += jStep;
@@ -209,25 +254,39 @@ __device__ f3 atmosphere(f3 r, f3 r0, f3 pSun, float iTime) {
 
 constexpr int TX = 16, TY = 16;
 
-// Shading of one sky pixel (main(), :445-477).
-__device__ __forceinline__ uint32_t shade_sky(const CloudParams& p, const uint32_t* quads, int x, int y) {
+// View ray of pixel (x, y): main(), :445-452 (ray_uv = pixel / (resolution - 1), not texel centres).
+__device__ __forceinline__ f3 sky_dir(const CloudParams& p, int x, int y) {
     const float ru = (float)x / p.res_x_m1, rv = (float)y / p.res_y_m1;
     const float ndx = ru * 2.0f - 1.0f, ndy = rv * 2.0f - 1.0f;
     const f4 rvs = mul(p.inv_proj, f4{ndx, ndy, -1.0f, 0.0f});
     const f4 rws = mul(p.inv_view, f4{rvs.x, rvs.y, -1.0f, 0.0f});
-    const f3 dir = normalize3(f3{rws.x, rws.y, rws.z});
-    const f3 sun = f3{p.sun[0], p.sun[1], p.sun[2]};
+    return normalize3(f3{rws.x, rws.y, rws.z});
+}
+
+__device__ __forceinline__ f3 sky_atmosphere(const CloudParams& p, f3 dir) {
+    if (SOC_CLOUDS_PROFILE >= 2) return f3{0.1f, 0.2f, 0.3f};
     const f3 r0 = f3{0.0f + p.cam[0], 6372e3f + p.cam[1], 0.0f + p.cam[2]};
+    return atmosphere(dir, r0, f3{p.sun[0], p.sun[1], p.sun[2]}, p.elapsed);
+}
+
+// Clouds over the atmosphere colour, sun factor, RGBA8 (main(), :466-477).
+__device__ __forceinline__ uint32_t sky_clouds(const CloudParams& p, const uint32_t* quads, int x, int y, f3 dir, f3 color) {
     Ctx cx;
     cx.quads = quads;
     cx.cam_x = p.cam[0];
     cx.cam_z = p.cam[2];
     cx.time = -1.0f * 0.02f * p.elapsed;
     const float dither = bayer16((float)x, (float)y);
-    f3 color = atmosphere(dir, r0, sun, p.elapsed);
-    color = volumetric_clouds(cx, dir, sun, color, dither, f3{0.8f, 0.8f, 0.8f});
+    if (SOC_CLOUDS_PROFILE != 1)
+        color = volumetric_clouds(cx, dir, f3{p.sun[0], p.sun[1], p.sun[2]}, color, dither, f3{0.8f, 0.8f, 0.8f});
     color = color * p.sun_factor;
     return pack_unorm8x4(f4{color.x, color.y, color.z, 1.0f});
+}
+
+// Shading of one sky pixel (main(), :445-477).
+__device__ __forceinline__ uint32_t shade_sky(const CloudParams& p, const uint32_t* quads, int x, int y) {
+    const f3 dir = sky_dir(p, x, y);
+    return sky_clouds(p, quads, x, y, dir, sky_atmosphere(p, dir));
 }
 
 // Stage the noise .x channel as 2x2 REPEAT quads (quad i = texels (x,y), (x+1,y), (x,y+1), (x+1,y+1)).
@@ -266,31 +325,74 @@ __global__ __launch_bounds__(256) void clouds_kernel(DImg depth, DImg noise, DIm
     row_ptr_w<uint32_t>(target, y)[x] = sky ? shade_sky(p, quads, x, y) : pack_unorm8x4(f4{0.2f, 0.4f, 1.0f, 1.0f});
 }
 
-// Two-kernel path. classify: non-sky pixels get the constant colour; sky pixels are appended to a
-// compact list (one atomic per wave, lanes in ballot order, so a wave's list entries stay one 8x8
-// tile). march: a grid-stride loop over the list, every lane a sky pixel.
-__global__ __launch_bounds__(256) void clouds_classify(DImg depth, DImg target, CloudParams p,
+// Three-kernel path, stage 1 (classify). Every pixel first gets the constant non-sky colour (a sky pixel
+// is overwritten by the march later in stream order); sky pixels are appended to a compact list.
+// A workgroup covers a 32x32 tile, each wave a 16x16 quarter, each lane 4 horizontal pixels (one 16-B
+// store). Entries are ordered row-major inside a wave's quarter, so a wave of the march takes a compact
+// 16x4 block. The list offset costs ONE atomic per workgroup that has sky: device-scope atomics on one
+// address serialise across the XCDs (one per wave cost ~95 us at 4K).
+__global__ __launch_bounds__(256) void clouds_classify(DImg depth, DImg target, CloudParams p, int vec_store,
                                                        uint32_t* __restrict__ counter, uint32_t* __restrict__ list) {
+    __shared__ uint32_t wave_total[4];
+    __shared__ uint32_t wg_base;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-    const int y = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
-    const bool inside = x < p.res_x && y < p.res_y && x < target.w && y < target.h;
-    const bool sky = inside && is_sky(p, depth, x, y);
-    if (inside && !sky) row_ptr_w<uint32_t>(target, y)[x] = pack_unorm8x4(f4{0.2f, 0.4f, 1.0f, 1.0f});
-    const unsigned long long m = __ballot(sky);
-    if (m == 0ull) return;
-    uint32_t base = 0;
-    if (lane == __builtin_ctzll(m)) base = atomicAdd(counter, (uint32_t)__builtin_popcountll(m));
-    base = __shfl(base, __builtin_ctzll(m));
-    if (sky) {
-        const uint32_t rank = (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
-        list[base + rank] = ((uint32_t)y << 16) | (uint32_t)x;
+    const int x0 = blockIdx.x * 32 + (wave & 1) * 16 + (lane & 3) * 4;
+    const int y = blockIdx.y * 32 + (wave >> 1) * 16 + (lane >> 2);
+    const int W = min(p.res_x, target.w), H = min(p.res_y, target.h);
+    const uint32_t other = pack_unorm8x4(f4{0.2f, 0.4f, 1.0f, 1.0f});
+    uint32_t mask = 0;   // bit k: pixel (x0 + k, y) is sky
+    if (y < H) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (x0 + k < W && is_sky(p, depth, x0 + k, y)) mask |= 1u << k;
+        uint32_t* row = row_ptr_w<uint32_t>(target, y);
+        if (vec_store && x0 + 3 < W) {
+            *reinterpret_cast<uint4*>(row + x0) = uint4{other, other, other, other};
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (x0 + k < W) row[x0 + k] = other;
+        }
+    }
+    const unsigned long long below = (1ull << lane) - 1ull;
+    uint32_t before = 0, total = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const unsigned long long b = __ballot((mask >> k) & 1u);
+        before += (uint32_t)__builtin_popcountll(b & below);
+        total += (uint32_t)__builtin_popcountll(b);
+    }
+    if (lane == 0) wave_total[wave] = total;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t sum = wave_total[0] + wave_total[1] + wave_total[2] + wave_total[3];
+        wg_base = sum ? atomicAdd(counter, sum) : 0u;
+    }
+    __syncthreads();
+    if (!mask) return;
+    uint32_t at = wg_base + before;
+    for (int w = 0; w < wave; ++w) at += wave_total[w];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if ((mask >> k) & 1u) list[at++] = ((uint32_t)y << 16) | (uint32_t)(x0 + k);
+}
+
+// Three-kernel path, stage 2: the atmosphere of every listed sky pixel (no LDS, few registers, so many
+// more lanes are resident than in the cloud march), kept in fp32 in the workspace.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void clouds_atmosphere(CloudParams p, const uint32_t* __restrict__ counter,
+                                                         const uint32_t* __restrict__ list, float4* __restrict__ atmos) {
+    const uint32_t count = *counter;
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < count; i += gridDim.x * 256u) {
+        const uint32_t e = list[i];
+        const f3 c = sky_atmosphere(p, sky_dir(p, (int)(e & 0xffffu), (int)(e >> 16)));
+        atmos[i] = float4{c.x, c.y, c.z, 0.0f};
     }
 }
 
+// Stage 3: the cloud march over the atmosphere colour, one listed sky pixel per lane (grid stride).
 template <bool NOISE_R8>
-__global__ __launch_bounds__(256) void clouds_march(DImg noise, DImg target, CloudParams p,
-                                                    const uint32_t* __restrict__ counter, const uint32_t* __restrict__ list) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void clouds_march(DImg noise, DImg target, CloudParams p, const uint32_t* __restrict__ counter,
+                                                    const uint32_t* __restrict__ list, const float4* __restrict__ atmos) {
     __shared__ uint32_t quads[kNoise * kNoise];
     const uint32_t count = *counter;
     const uint32_t first = blockIdx.x * 256u;
@@ -300,8 +402,20 @@ __global__ __launch_bounds__(256) void clouds_march(DImg noise, DImg target, Clo
     for (uint32_t i = first + threadIdx.x; i < count; i += gridDim.x * 256u) {
         const uint32_t e = list[i];
         const int x = (int)(e & 0xffffu), y = (int)(e >> 16);
-        row_ptr_w<uint32_t>(target, y)[x] = shade_sky(p, quads, x, y);
+        const float4 a = atmos[i];
+        row_ptr_w<uint32_t>(target, y)[x] = sky_clouds(p, quads, x, y, sky_dir(p, x, y), f3{a.x, a.y, a.z});
     }
+}
+
+// Lanes resident on the device for a 256-thread kernel (grid of one full wave set).
+template <typename K>
+int resident_blocks(K kernel) {
+    int dev = 0, cus = 256, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0) cus = prop.multiProcessorCount;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || per_cu < 1) per_cu = 4;
+    return per_cu * cus;
 }
 
 }  // namespace
@@ -311,7 +425,9 @@ using namespace soc;
 
 extern "C" size_t soc_cloud_rendering_workspace_size(int32_t width, int32_t height) {
     if (width <= 0 || height <= 0) return 0;
-    return 256 + (size_t)width * (size_t)height * sizeof(uint32_t);
+    // counter | list of sky pixels (u32 each) | their atmosphere colours (float4, 16-B aligned)
+    const size_t n = (size_t)width * (size_t)height;
+    return 256 + ((n * sizeof(uint32_t) + 15) & ~(size_t)15) + n * 16;
 }
 
 extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img noise, soc_img target, void* workspace,
@@ -354,21 +470,20 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
     uint32_t* list = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + 256);
     hipError_t e = hipMemsetAsync(counter, 0, sizeof(uint32_t), s);
     if (e != hipSuccess) return set_error(SOC_E_HIP, "%s: %s", P, hipGetErrorString(e));
-    clouds_classify<<<dim3(ceil_div(W, 16), ceil_div(H, 16)), 256, 0, s>>>(dimg(depth), dimg(target), p, counter, list);
-    // One resident wave set: every lane loops over the list with a grid stride, so the long per-pixel
-    // march is balanced over all SIMDs instead of running as a second, partially filled round.
-    static int resident = 0;
-    if (!resident) {
-        int dev = 0, cus = 256, per_cu = 0;
-        (void)hipGetDevice(&dev);
-        hipDeviceProp_t prop;
-        if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0) cus = prop.multiProcessorCount;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, clouds_march<false>, 256, 0) != hipSuccess || per_cu < 1)
-            per_cu = 4;
-        resident = per_cu * cus;
+    const int vec_store = (target.pitch_bytes % 16 == 0) && (reinterpret_cast<uintptr_t>(target.data) % 16 == 0);
+    clouds_classify<<<dim3(ceil_div(W, 32), ceil_div(H, 32)), 256, 0, s>>>(dimg(depth), dimg(target), p, vec_store, counter, list);
+    float4* atmos = reinterpret_cast<float4*>(reinterpret_cast<char*>(list) + (((size_t)W * H * sizeof(uint32_t) + 15) & ~(size_t)15));
+    // One resident wave set per kernel: every lane loops over the list with a grid stride, so the long
+    // per-pixel work is balanced over all SIMDs instead of running as a second, partially filled round.
+    static int resident_atmos = 0, resident_march = 0;
+    if (!resident_atmos) {
+        resident_atmos = resident_blocks(clouds_atmosphere);
+        resident_march = resident_blocks(clouds_march<false>);
     }
-    const int grid = (int)std::min<long long>(resident, ((long long)W * H + 255) / 256);
-    if (r8) clouds_march<true><<<grid, 256, 0, s>>>(dimg(noise), dimg(target), p, counter, list);
-    else clouds_march<false><<<grid, 256, 0, s>>>(dimg(noise), dimg(target), p, counter, list);
+    const long long blocks = ((long long)W * H + 255) / 256;
+    clouds_atmosphere<<<(int)std::min<long long>(resident_atmos, blocks), 256, 0, s>>>(p, counter, list, atmos);
+    const int grid = (int)std::min<long long>(resident_march, blocks);
+    if (r8) clouds_march<true><<<grid, 256, 0, s>>>(dimg(noise), dimg(target), p, counter, list, atmos);
+    else clouds_march<false><<<grid, 256, 0, s>>>(dimg(noise), dimg(target), p, counter, list, atmos);
     return check_launch("cloud_rendering");
 }
