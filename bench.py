@@ -30,6 +30,8 @@ import soc_real_time_renderer_amd as soc  # noqa: E402
 from soc_real_time_renderer_amd import multi_gpu, scene  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
 def make_globals(W, H, camera):
     g = soc.globals_defaults(W, H)
     cam = soc.make_camera(*camera)
@@ -49,6 +51,10 @@ def algorithmic_bytes(W, H, f_sky):
         "BloomDownsample - 0": 16.0 * P, "BloomDownsample - 1": (8.0 + 2.0) * P, "BloomDownsample - 2": (2.0 + 0.5) * P,
         "BloomDownsample - 3": (0.5 + 0.125) * P, "BloomUpsample - 3": (0.125 + 0.5) * P,
         "BloomUpsample - 2": (0.5 + 2.0) * P, "BloomUpsample - 1": (2.0 + 8.0) * P, "BloomUpsample - 0": 16.0 * P,
+        # fused stages (bloom_fused.hip): mip0 / mip2 of the downsweep never leave LDS (stages 3-4
+        # are available through soc_bloom_fused_stage but not scheduled: slower than per-pass)
+        "BloomDownsample - 0+1": (8.0 + 2.0) * P, "BloomDownsample - 2+3": (2.0 + 0.125) * P,
+        "BloomUpsample - 3+2": (0.125 + 0.5 + 2.0) * P, "BloomUpsample - 1+0": (2.0 + 8.0 + 8.0) * P,
         "SSAOGeneration": 12.25 * P, "SSAOBlur": 0.5 * P, "CloudRendering": 8.0 * P,
         "Composition": (40.25 + 4.0 * f_sky) * P, "GenerateLuminanceHistogram": 8.0 * P,
         "ResolveLuminanceHistogram": 2.0 * 1028.0,
@@ -56,6 +62,21 @@ def algorithmic_bytes(W, H, f_sky):
         "ToneMapping": 12.0 * P,
     }
     return b
+
+
+def pmc_traffic(kernel, W, H):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC table (profiles/, written by
+    tools/pmc_summary.py --traffic from a run of this same workload), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as fh:
+        t = json.load(fh)
+    k = t.get("kernels", {}).get(kernel)
+    if not k or list(t.get("resolution", [])) != [W, H]:
+        return None, None
+    return k["hbm_bytes"], os.path.relpath(files[-1], ROOT)
 
 
 def cpu_baseline(W, H, host_inputs, g):
@@ -168,6 +189,7 @@ def main():
     ns_bytes = algo["Composition"] + algo["SSAOGeneration"]
     ns_us = (comp_ms + ssao_ms) * 1e3
     pass_gbs = {n: round(algo[n] / (ms * 1e-3) / 1e9, 1) for n, _, ms, _ in stats if ms > 0 and n in algo}
+    traffic, traffic_src = pmc_traffic("composition_pair", W, H)
 
     if world > 1:
         dist.barrier()
@@ -193,7 +215,8 @@ def main():
                    "resolution": [W, H], "f_sky": round(f_sky, 4), "parallelism": f"frame-per-gpu x{world}",
                    "histogram_allreduce": world > 1},
         "roofline": {"kernel": "Composition", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": int(algo["Composition"]), "avg_launch_us": round(comp_ms * 1e3, 2)},
         "north_star": {"kernels": ["SSAOGeneration", "Composition"], "us": round(ns_us, 2),
                        "algorithmic_bytes": int(ns_bytes),

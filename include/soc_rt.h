@@ -222,9 +222,18 @@ int soc_bloom_upsample(const soc_globals* g, soc_img lower_mip, soc_img higher_m
 
 /* Whole bloom chain as scheduled by renderer.cpp:1024-1062: down(emissive->mip0), down(mip i ->
  * mip i+1), up(mip i -> mip i-1), up(mip0 -> emissive). `mips` holds mip_count images (4 in the
- * reference, renderer.hpp:51). */
+ * reference, renderer.hpp:51). With 4 exactly halving mips the downsweep runs as fused stages 1-2 of
+ * soc_bloom_fused_stage (same bits in every mip and in emissive), otherwise as 4 passes. */
 int soc_bloom_chain(const soc_globals* g, soc_img emissive, const soc_img* mips, int32_t mip_count,
                     soc_stream stream);
+
+/* One stage of the fused bloom chain (4 mips, each exactly half the previous, mips[0] the size of
+ * emissive; SOC_E_UNSUPPORTED otherwise). stage 1: emissive -> mip1 (mip0 stays in LDS);
+ * 2: mip1 -> mip3 (mip2 in LDS); 3: mip3 -> mip2 -> mip1; 4: mip1 -> mip0 -> output; 0: all four.
+ * `output` is the final upsample's target (emissive itself for the in-place reference graph). After
+ * stage 4 every mip and `output` hold exactly what the 8-pass chain leaves there. */
+int soc_bloom_fused_stage(const soc_globals* g, soc_img emissive, const soc_img* mips, int32_t mip_count, soc_img output,
+                          int32_t stage, soc_stream stream);
 
 /* SSAOGenerationTask (ssao_generation.inl:20-68, shader :176-214): half-res R8 ambient occlusion from
  * full-res depth (D32F) and normal (RGBA16F). `target` is (W/2)x(H/2) R8_UNORM. `noise_table` is an
@@ -318,6 +327,7 @@ typedef struct soc_renderer soc_renderer;
 
 /* flags */
 #define SOC_RENDERER_TIMING 1      /* record hipEvents around every pass (GPUMetric, gpu_metric.cpp:18-42) */
+#define SOC_RENDERER_UNFUSED_BLOOM 2  /* bloom downsweep as the reference's 4 passes, not 2 fused stages */
 
 soc_renderer* soc_renderer_create(const soc_frame_images* images, uint32_t flags);
 void soc_renderer_destroy(soc_renderer* r);

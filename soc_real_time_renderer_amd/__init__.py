@@ -166,6 +166,13 @@ def bloom_chain(g, emissive, mips, stream=None):
     _check(lib().soc_bloom_chain(_gp(g), img(emissive), arr, len(mips), _stream(stream)), "bloom_chain")
 
 
+def bloom_fused_stage(g, emissive, mips, output, stage=0, stream=None):
+    """One stage (1-4, 0 = all) of the fused bloom chain (soc_bloom_fused_stage)."""
+    arr = (SocImg * len(mips))(*[img(m) for m in mips])
+    _check(lib().soc_bloom_fused_stage(_gp(g), img(emissive), arr, len(mips), img(output), int(stage), _stream(stream)),
+           "bloom_fused_stage")
+
+
 def ssao_prepare_noise(normal, target, table, stream=None):
     _check(lib().soc_ssao_prepare_noise(img(normal), img(target), _ptr(table), _stream(stream)), "ssao_prepare_noise")
 
@@ -268,7 +275,7 @@ def alloc_frame(width: int, height: int, device="cuda", output_format=FMT_RGBA8_
 class Renderer:
     """Host render graph (C++ soc_renderer): the live passes of Renderer::rebuild_task_graph in order."""
 
-    def __init__(self, frame: dict, timing: bool = False, stream=None):
+    def __init__(self, frame: dict, timing: bool = False, stream=None, fused_bloom: bool = True):
         self.frame = frame
         fi = FrameImages()
         for k in ("albedo", "emissive", "normal", "depth", "velocity", "shadow", "noise", "ssao", "ssao_blur", "clouds",
@@ -286,7 +293,8 @@ class Renderer:
         fi.bloom_output = img(frame.get("bloom_output"))
         fi.clouds_workspace = _ptr(frame.get("clouds_workspace"))
         self._fi = fi
-        h = lib().soc_renderer_create(C.byref(fi), _abi.RENDERER_TIMING if timing else 0)
+        flags = (_abi.RENDERER_TIMING if timing else 0) | (0 if fused_bloom else _abi.RENDERER_UNFUSED_BLOOM)
+        h = lib().soc_renderer_create(C.byref(fi), flags)
         if not h:
             raise SocError(-1, lib().soc_last_error_string().decode())
         self.handle = h

@@ -32,6 +32,7 @@ PHASE_PRE_EXPOSURE = 1
 PHASE_POST_EXPOSURE = 2
 PHASE_ALL = 3
 RENDERER_TIMING = 1
+RENDERER_UNFUSED_BLOOM = 2
 
 Mat4 = C.c_float * 16
 Vec2 = C.c_float * 2
@@ -135,6 +136,7 @@ FUNCTIONS = {
     "soc_bloom_downsample": (_I, [_G, _IMG, _IMG, _P]),
     "soc_bloom_upsample": (_I, [_G, _IMG, _IMG, _P]),
     "soc_bloom_chain": (_I, [_G, _IMG, C.POINTER(SocImg), C.c_int32, _P]),
+    "soc_bloom_fused_stage": (_I, [_G, _IMG, C.POINTER(SocImg), C.c_int32, _IMG, C.c_int32, _P]),
     "soc_ssao_prepare_noise": (_I, [_IMG, _IMG, _P, _P]),
     "soc_ssao_generation": (_I, [_G, _IMG, _IMG, _IMG, _P, _P]),
     "soc_ssao_blur": (_I, [_G, _IMG, _IMG, _P]),

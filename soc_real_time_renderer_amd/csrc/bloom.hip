@@ -7,89 +7,14 @@
 // down analytically (fast paths); both then go through the same clamp rule and lerp arithmetic, so
 // the fast paths are bit-identical to the generic one (extents <= 8192).
 // All tap weights are powers of two, so the RGBA16F results are bit-identical to the oracle's.
+#include <cstdlib>
 #include <type_traits>
 
-#include "soc_internal.hpp"
+#include "bloom_common.hpp"
 
 namespace soc {
 
 namespace {
-
-constexpr int BX = 64, BY = 4;
-
-// Clamp rule of the sampling contract applied to an 8-bit fixed-point texel coordinate.
-__device__ __forceinline__ Axis axis_from_fixed(int fx, int n) {
-    int i = fx >> 8;
-    float w = (float)(fx & 255) * (1.0f / 256.0f);
-    if (i < 0) { i = 0; w = 0.0f; }
-    else if (i >= n - 1) { i = n - 2; w = 1.0f; }
-    if (n == 1) { i = 0; w = 0.0f; }
-    Axis a;
-    a.i0 = i;
-    a.i1 = min(i + 1, n - 1);
-    a.w = w;
-    return a;
-}
-
-// Float-uv -> fixed coordinate, identical arithmetic to axis_clamp / the oracle.
-__device__ __forceinline__ int fixed_from_uv(float u, int n) {
-#pragma clang fp contract(off)
-    float t = u * (float)n;
-    t = t - 0.5f;
-    t = fminf(fmaxf(t, -2.0f), (float)n + 1.0f);
-    return (int)floorf(t * 256.0f + 0.5f);
-}
-
-__device__ __forceinline__ f3 tap(const DImg& im, const Axis& ax, const Axis& ay) {
-    const uint2* r0 = row_ptr<uint2>(im, ay.i0);
-    const uint2* r1 = row_ptr<uint2>(im, ay.i1);
-    f4 a = unpack_h4(r0[ax.i0]), b = unpack_h4(r0[ax.i1]), c = unpack_h4(r1[ax.i0]), d = unpack_h4(r1[ax.i1]);
-    return f3{bilerp1(a.x, b.x, c.x, d.x, ax.w, ay.w), bilerp1(a.y, b.y, c.y, d.y, ax.w, ay.w),
-              bilerp1(a.z, b.z, c.z, d.z, ax.w, ay.w)};
-}
-
-// Exact texel at clamped integer coordinates (a tap whose weights are 0/1).
-__device__ __forceinline__ f3 point(const DImg& im, int x, int y) {
-    x = min(max(x, 0), im.w - 1);
-    y = min(max(y, 0), im.h - 1);
-    f4 v = fetch_h4(im, x, y);
-    return f3{v.x, v.y, v.z};
-}
-
-__device__ __forceinline__ void store_rgb1(const DImg& im, int x, int y, f3 c) {
-    row_ptr_w<uint2>(im, y)[x] = pack_h4(f4{c.x, c.y, c.z, 1.0f});
-}
-
-// out = e*0.125 + (a+c+g+i)*0.03125 + (b+d+f+h)*0.0625 + (j+k+l+m)*0.125   (:137-140)
-__device__ __forceinline__ float down13(float a, float b, float c, float d, float e, float f, float g, float h, float i,
-                                        float j, float k, float l, float m) {
-    // no contraction: the last add fused into the f16 store would become v_fma_mixlo_f16, a single
-    // rounding to f16 where the oracle rounds to f32 first (1-ulp differences, double rounding)
-#pragma clang fp contract(off)
-    float r = e * 0.125f;
-    r += (a + c + g + i) * 0.03125f;
-    r += (b + d + f + h) * 0.0625f;
-    r += (j + k + l + m) * 0.125f;
-    return r;
-}
-
-// out = (e*4 + (b+d+f+h)*2 + (a+c+g+i)) / 16   (bloom_upsample.inl:122-125)
-__device__ __forceinline__ float up9(float a, float b, float c, float d, float e, float f, float g, float h, float i) {
-#pragma clang fp contract(off)
-    float r = e * 4.0f;
-    r += (b + d + f + h) * 2.0f;
-    r += (a + c + g + i);
-    r *= 1.0f / 16.0f;
-    return r;
-}
-
-#define SOC_DOWN13(A, B, C, D, E, F, G, H, I, J, K, L, M)                                                   \
-    f3{down13(A.x, B.x, C.x, D.x, E.x, F.x, G.x, H.x, I.x, J.x, K.x, L.x, M.x),                           \
-       down13(A.y, B.y, C.y, D.y, E.y, F.y, G.y, H.y, I.y, J.y, K.y, L.y, M.y),                           \
-       down13(A.z, B.z, C.z, D.z, E.z, F.z, G.z, H.z, I.z, J.z, K.z, L.z, M.z)}
-#define SOC_UP9(A, B, C, D, E, F, G, H, I)                                                                  \
-    f3{up9(A.x, B.x, C.x, D.x, E.x, F.x, G.x, H.x, I.x), up9(A.y, B.y, C.y, D.y, E.y, F.y, G.y, H.y, I.y), \
-       up9(A.z, B.z, C.z, D.z, E.z, F.z, G.z, H.z, I.z)}
 
 // ------------------------------------------------------------------------------------------------
 // downsample
@@ -180,28 +105,8 @@ __global__ __launch_bounds__(256) void bloom_up_double(DImg src, DImg dst) {
 // horizontal lerps between taps that use the same row and x-pair. Every tap is computed with exactly
 // the arithmetic of tap()/point() above (same lerps, same order), so results are bit-identical.
 // ------------------------------------------------------------------------------------------------
-template <int C>
-__device__ __forceinline__ float chan(uint2 v) {
-    return C == 0 ? h2f((uint16_t)(v.x & 0xffffu)) : C == 1 ? h2f((uint16_t)(v.x >> 16)) : h2f((uint16_t)(v.y & 0xffffu));
-}
-
-__device__ __forceinline__ uint2 texel_clamped(const DImg& im, int x, int y) {
-    x = min(max(x, 0), im.w - 1);
-    y = min(max(y, 0), im.h - 1);
-    return row_ptr<uint2>(im, y)[x];
-}
-
-__device__ __forceinline__ float lerp_c(float a, float b, float w) {
-#pragma clang fp contract(off)
-    return a * (1.0f - w) + b * w;
-}
-
-__device__ __forceinline__ void store_rgb1_c(const DImg& im, int x, int y, float r, float g, float b) {
-    row_ptr_w<uint2>(im, y)[x] = pack_h4(f4{r, g, b, 1.0f});
-}
-
 // same-size 13-tap downsample, 2x2 output pixels per lane from a 6x6 texel window
-__global__ __launch_bounds__(256) void bloom_down_same_q(DImg src, DImg dst) {
+__global__ __launch_bounds__(256) void bloom_down_same_q(DImg src, DImg dst, bool vec) {
     const int m = blockIdx.x * BX + threadIdx.x, n = blockIdx.y * BY + threadIdx.y;
     const int X0 = 2 * m, Y0 = 2 * n;
     if (X0 >= dst.w || Y0 >= dst.h) return;
@@ -231,16 +136,12 @@ __global__ __launch_bounds__(256) void bloom_down_same_q(DImg src, DImg dst) {
     run(std::integral_constant<int, 0>{});
     run(std::integral_constant<int, 1>{});
     run(std::integral_constant<int, 2>{});
-#pragma unroll
-    for (int py = 0; py < 2; ++py)
-#pragma unroll
-        for (int px = 0; px < 2; ++px)
-            if (X0 + px < dst.w && Y0 + py < dst.h)
-                store_rgb1_c(dst, X0 + px, Y0 + py, out[py][px][0], out[py][px][1], out[py][px][2]);
+    store_quad_row(dst, X0, Y0, out[0], vec);
+    store_quad_row(dst, X0, Y0 + 1, out[1], vec);
 }
 
 // same-size 9-tap tent upsample, 2x2 output pixels per lane from a 4x4 window
-__global__ __launch_bounds__(256) void bloom_up_same_q(DImg src, DImg dst) {
+__global__ __launch_bounds__(256) void bloom_up_same_q(DImg src, DImg dst, bool vec) {
     const int m = blockIdx.x * BX + threadIdx.x, n = blockIdx.y * BY + threadIdx.y;
     const int X0 = 2 * m, Y0 = 2 * n;
     if (X0 >= dst.w || Y0 >= dst.h) return;
@@ -263,12 +164,8 @@ __global__ __launch_bounds__(256) void bloom_up_same_q(DImg src, DImg dst) {
     run(std::integral_constant<int, 0>{});
     run(std::integral_constant<int, 1>{});
     run(std::integral_constant<int, 2>{});
-#pragma unroll
-    for (int py = 0; py < 2; ++py)
-#pragma unroll
-        for (int px = 0; px < 2; ++px)
-            if (X0 + px < dst.w && Y0 + py < dst.h)
-                store_rgb1_c(dst, X0 + px, Y0 + py, out[py][px][0], out[py][px][1], out[py][px][2]);
+    store_quad_row(dst, X0, Y0, out[0], vec);
+    store_quad_row(dst, X0, Y0 + 1, out[1], vec);
 }
 
 // 2:1 downsample: one output per lane, 6x6 source window; the 13 taps are w = 0.5 blends of the 2x2
@@ -316,7 +213,7 @@ __global__ __launch_bounds__(256) void bloom_down_half_w(DImg src, DImg dst) {
 
 // 1:2 upsample: a 2x2 output quad per lane from the 5x5 source window around (m, n). Even outputs use
 // x-pairs (m-2..m) at w = 3/4, odd ones (m-1..m+1) at w = 1/4 (and likewise in y). Border quads use tap().
-__global__ __launch_bounds__(256) void bloom_up_double_q(DImg src, DImg dst) {
+__global__ __launch_bounds__(256) void bloom_up_double_q(DImg src, DImg dst, bool vec) {
     const int m = blockIdx.x * BX + threadIdx.x, n = blockIdx.y * BY + threadIdx.y;
     if (m >= src.w || n >= src.h) return;
     const int X0 = 2 * m, Y0 = 2 * n;
@@ -371,13 +268,24 @@ __global__ __launch_bounds__(256) void bloom_up_double_q(DImg src, DImg dst) {
     run(std::integral_constant<int, 0>{});
     run(std::integral_constant<int, 1>{});
     run(std::integral_constant<int, 2>{});
-#pragma unroll
-    for (int py = 0; py < 2; ++py)
-#pragma unroll
-        for (int px = 0; px < 2; ++px) store_rgb1_c(dst, X0 + px, Y0 + py, out[py][px][0], out[py][px][1], out[py][px][2]);
+    store_quad_row(dst, X0, Y0, out[0], vec);
+    store_quad_row(dst, X0, Y0 + 1, out[1], vec);
 }
 
 constexpr int kFastMax = 8192;
+
+// Below this many output pixels the 1:2 upsample runs one pixel per lane (4x the lanes of the quad
+// kernel: small mips need the parallelism more than the shared window). Tuning knob:
+// SOC_BLOOM_QUAD_MIN_PX overrides it.
+long quad_min_px() {
+    static const long v = [] {
+        const char* e = getenv("SOC_BLOOM_QUAD_MIN_PX");
+        return e ? atol(e) : 1L << 20;
+    }();
+    return v;
+}
+
+bool vec16(const soc_img& im) { return im.pitch_bytes % 16 == 0 && reinterpret_cast<uintptr_t>(im.data) % 16 == 0; }
 
 }  // namespace
 
@@ -387,7 +295,7 @@ int launch_bloom_down(const soc_img& hi, const soc_img& lo, hipStream_t s, int f
     const bool small = hi.width <= kFastMax && hi.height <= kFastMax;
     if (!force_generic && small && hi.width == lo.width && hi.height == lo.height) {
         dim3 g2(ceil_div(ceil_div(lo.width, 2), BX), ceil_div(ceil_div(lo.height, 2), BY));
-        bloom_down_same_q<<<g2, blk, 0, s>>>(src, dst);
+        bloom_down_same_q<<<g2, blk, 0, s>>>(src, dst, vec16(lo));
     } else if (!force_generic && small && hi.width == 2 * lo.width && hi.height == 2 * lo.height) {
         bloom_down_half_w<<<grd, blk, 0, s>>>(src, dst);
     } else {
@@ -402,10 +310,14 @@ int launch_bloom_up(const soc_img& lo, const soc_img& hi, hipStream_t s, int for
     const bool small = hi.width <= kFastMax && hi.height <= kFastMax;
     if (!force_generic && small && hi.width == lo.width && hi.height == lo.height) {
         dim3 g2(ceil_div(ceil_div(hi.width, 2), BX), ceil_div(ceil_div(hi.height, 2), BY));
-        bloom_up_same_q<<<g2, blk, 0, s>>>(src, dst);
+        bloom_up_same_q<<<g2, blk, 0, s>>>(src, dst, vec16(hi));
     } else if (!force_generic && small && hi.width == 2 * lo.width && hi.height == 2 * lo.height) {
-        dim3 g2(ceil_div(lo.width, BX), ceil_div(lo.height, BY));
-        bloom_up_double_q<<<g2, blk, 0, s>>>(src, dst);
+        if ((long)hi.width * hi.height < quad_min_px()) {
+            bloom_up_double<<<grd, blk, 0, s>>>(src, dst);
+        } else {
+            dim3 g2(ceil_div(lo.width, BX), ceil_div(lo.height, BY));
+            bloom_up_double_q<<<g2, blk, 0, s>>>(src, dst, vec16(hi));
+        }
     } else {
         bloom_up_generic<<<grd, blk, 0, s>>>(src, dst, 1.0f / (float)lo.width, 1.0f / (float)lo.height);
     }
@@ -446,11 +358,33 @@ extern "C" int soc_debug_bloom_generic(int32_t up, soc_img a, soc_img b, soc_str
     return up ? launch_bloom_up(a, b, hs(stream), 1) : launch_bloom_down(a, b, hs(stream), 1);
 }
 
+extern "C" int soc_bloom_fused_stage(const soc_globals* g, soc_img emissive, const soc_img* mips, int32_t mip_count,
+                                     soc_img output, int32_t stage, soc_stream stream) {
+    (void)g;
+    static const char* P = "soc_bloom_fused_stage";
+    if (!mips) return set_error(SOC_E_INVALID_ARG, "%s: null mips", P);
+    if (stage < 0 || stage > 4) return set_error(SOC_E_INVALID_ARG, "%s: stage %d not in 0..4", P, stage);
+    int rc = check_img(emissive, SOC_FMT_RGBA16F, P, "emissive");
+    if (!rc) rc = check_img(output, SOC_FMT_RGBA16F, P, "output");
+    for (int i = 0; !rc && i < mip_count; ++i) rc = check_img(mips[i], SOC_FMT_RGBA16F, P, "mip");
+    if (rc) return rc;
+    if (!bloom_fused_applicable(emissive, mips, mip_count, output))
+        return set_error(SOC_E_UNSUPPORTED, "%s: needs 4 mips halving exactly from the emissive extent (<= 8192)", P);
+    return launch_bloom_fused(emissive, mips, output, hs(stream), stage);
+}
+
 extern "C" int soc_bloom_chain(const soc_globals* g, soc_img emissive, const soc_img* mips, int32_t mip_count,
                                soc_stream stream) {
     if (!mips || mip_count < 1) return set_error(SOC_E_INVALID_ARG, "soc_bloom_chain: need >= 1 mip");
-    int rc = soc_bloom_downsample(g, emissive, mips[0], stream);
-    for (int i = 0; !rc && i < mip_count - 1; ++i) rc = soc_bloom_downsample(g, mips[i], mips[i + 1], stream);
+    int rc = SOC_OK;
+    if (bloom_fused_applicable(emissive, mips, mip_count, emissive)) {
+        // fused downsweep (stages 1-2), per-pass upsweep: the renderer's default schedule
+        rc = soc_bloom_fused_stage(g, emissive, mips, mip_count, emissive, 1, stream);
+        if (!rc) rc = soc_bloom_fused_stage(g, emissive, mips, mip_count, emissive, 2, stream);
+    } else {
+        rc = soc_bloom_downsample(g, emissive, mips[0], stream);
+        for (int i = 0; !rc && i < mip_count - 1; ++i) rc = soc_bloom_downsample(g, mips[i], mips[i + 1], stream);
+    }
     for (int i = mip_count - 1; !rc && i > 0; --i) rc = soc_bloom_upsample(g, mips[i], mips[i - 1], stream);
     if (!rc) rc = soc_bloom_upsample(g, mips[0], emissive, stream);
     return rc;

@@ -483,12 +483,27 @@ void build_passes(soc_renderer* r) {
     };
     const int nm = 4;
     // renderer.cpp:1024-1062
-    add("BloomDownsample - 0", "Bloom", SOC_PHASE_PRE_EXPOSURE,
-        [r](const soc_globals* g, hipStream_t s) { return soc_bloom_downsample(g, r->img.emissive, r->img.bloom_mips[0], (soc_stream)s); });
-    for (int i = 0; i < nm - 1; ++i)
-        add("BloomDownsample - " + std::to_string(i + 1), "Bloom", SOC_PHASE_PRE_EXPOSURE, [r, i](const soc_globals* g, hipStream_t s) {
-            return soc_bloom_downsample(g, r->img.bloom_mips[i], r->img.bloom_mips[i + 1], (soc_stream)s);
+    const soc_img& bloom_dst = I.bloom_output.data ? I.bloom_output : I.emissive;
+    const bool fused = !(r->flags & SOC_RENDERER_UNFUSED_BLOOM) && bloom_fused_applicable(I.emissive, I.bloom_mips, nm, bloom_dst);
+    if (fused) {
+        // downsweep as 2 fused stages (mip0 / mip2 of the downsweep stay in LDS; bloom_fused.hip); the
+        // upsweep as the reference's 4 passes, which are faster than fused stages 3-4 on gfx950.
+        // Every mip and the output end up with exactly the 8-pass chain's bits.
+        add("BloomDownsample - 0+1", "Bloom", SOC_PHASE_PRE_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
+            return soc_bloom_fused_stage(g, r->img.emissive, r->img.bloom_mips, 4, r->img.emissive, 1, (soc_stream)s);
         });
+        add("BloomDownsample - 2+3", "Bloom", SOC_PHASE_PRE_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
+            return soc_bloom_fused_stage(g, r->img.emissive, r->img.bloom_mips, 4, r->img.emissive, 2, (soc_stream)s);
+        });
+    } else {
+        add("BloomDownsample - 0", "Bloom", SOC_PHASE_PRE_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
+            return soc_bloom_downsample(g, r->img.emissive, r->img.bloom_mips[0], (soc_stream)s);
+        });
+        for (int i = 0; i < nm - 1; ++i)
+            add("BloomDownsample - " + std::to_string(i + 1), "Bloom", SOC_PHASE_PRE_EXPOSURE, [r, i](const soc_globals* g, hipStream_t s) {
+                return soc_bloom_downsample(g, r->img.bloom_mips[i], r->img.bloom_mips[i + 1], (soc_stream)s);
+            });
+    }
     for (int i = nm - 1; i > 0; --i)
         add("BloomUpsample - " + std::to_string(i), "Bloom", SOC_PHASE_PRE_EXPOSURE, [r, i](const soc_globals* g, hipStream_t s) {
             return soc_bloom_upsample(g, r->img.bloom_mips[i], r->img.bloom_mips[i - 1], (soc_stream)s);

@@ -57,4 +57,8 @@ inline unsigned ceil_div(unsigned a, unsigned b) { return (a + b - 1) / b; }
 void agx_matrices(float compression, float M[9], float Minv[9]);
 void mat4_mul_host(float out[16], const float a[16], const float b[16]);
 
+// Fused bloom chain (bloom_fused.hip).
+bool bloom_fused_applicable(const soc_img& emissive, const soc_img* mips, int mip_count, const soc_img& output);
+int launch_bloom_fused(const soc_img& emissive, const soc_img* mips, const soc_img& output, hipStream_t s, int stage);
+
 }  // namespace soc

@@ -177,6 +177,135 @@ __global__ __launch_bounds__(256) void taa_pair(DImg target, DImg cur, DImg prev
     if (vel_out.data) row_ptr_w<uint4>(vel_out, y)[x0 >> 1] = row_ptr<uint4>(vel, y)[x0 >> 1];
 }
 
+// ---- two pixels per lane, reduced instruction count (the pass is VALU-issue bound on gfx950) ----
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+typedef float v2f __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ h2 as_h2(uint32_t u) { return __builtin_bit_cast(h2, u); }
+__device__ __forceinline__ v2f h2f2(h2 h) { return v2f{(float)h.x, (float)h.y}; }
+
+// Bilinear sample with the contract's taps; the lerps are fma(w, b - a, a) (within the RGBA16F
+// tolerance of the pass; the texel selection is exactly the contract's). 16-B row-pair loads.
+__device__ __forceinline__ void sample_pair_rows(const DImg& im, float u, float v, v2f& xy, v2f& zw, bool need_zw) {
+    const Axis ax = axis_clamp(u, im.w), ay = axis_clamp(v, im.h);
+    const u4a8 r0 = *reinterpret_cast<const u4a8*>(row_ptr<uint2>(im, ay.i0) + ax.i0);
+    const u4a8 r1 = *reinterpret_cast<const u4a8*>(row_ptr<uint2>(im, ay.i1) + ax.i0);
+    const v2f wx = v2f{ax.w, ax.w}, wy = v2f{ay.w, ay.w};
+    auto lerp2 = [](v2f a, v2f b, v2f w) { return __builtin_elementwise_fma(w, b - a, a); };
+    {
+        const v2f a = h2f2(as_h2(r0.x)), b = h2f2(as_h2(r0.z)), c = h2f2(as_h2(r1.x)), d = h2f2(as_h2(r1.z));
+        xy = lerp2(lerp2(a, b, wx), lerp2(c, d, wx), wy);
+    }
+    if (need_zw) {
+        const v2f a = h2f2(as_h2(r0.y)), b = h2f2(as_h2(r0.w)), c = h2f2(as_h2(r1.y)), d = h2f2(as_h2(r1.w));
+        zw = lerp2(lerp2(a, b, wx), lerp2(c, d, wx), wy);
+    }
+}
+
+// Same per-pixel result as taa_fast within the RGBA16F tolerance: the neighbourhood min/max run on
+// packed f16 (exact), column-wise and shared by the two pixels; the 3x3 Gaussian is evaluated as
+// column sums (separable weights, different rounding order); the closest-depth texel is chosen with
+// the reference's iteration order and tie rule, exactly.
+__global__ __launch_bounds__(256) void taa_pair2(DImg target, DImg cur, DImg prev, DImg vel, DImg pvel, DImg depth,
+                                                 DImg vel_out, TaaParams p) {
+    const int x0 = (blockIdx.x * BX + threadIdx.x) * 2, y = blockIdx.y * BY + threadIdx.y;
+    if (x0 >= target.w || y >= target.h) return;
+    const int W = target.w, H = target.h;
+    const int xl = max(x0 - 1, 0), xr = min(x0 + 2, W - 1);
+    // slots c = 0..3: columns xl, x0, x0+1, xr; rows r = 0..2: y+1, y, y-1 (clamped)
+    h2 Cxy[3][4], Czw[3][4];
+    float D[3][4];
+    int rows[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        const int sy = min(max(y + 1 - r, 0), H - 1);
+        rows[r] = sy;
+        const uint2* crow = row_ptr<uint2>(cur, sy);
+        const float* drow = row_ptr<float>(depth, sy);
+        const uint4 mid = *reinterpret_cast<const uint4*>(crow + x0);
+        const float2 dmid = *reinterpret_cast<const float2*>(drow + x0);
+        const uint2 L = crow[xl], R = crow[xr];
+        Cxy[r][0] = as_h2(L.x);
+        Czw[r][0] = as_h2(L.y);
+        Cxy[r][1] = as_h2(mid.x);
+        Czw[r][1] = as_h2(mid.y);
+        Cxy[r][2] = as_h2(mid.z);
+        Czw[r][2] = as_h2(mid.w);
+        Cxy[r][3] = as_h2(R.x);
+        Czw[r][3] = as_h2(R.y);
+        D[r][0] = drow[xl];
+        D[r][1] = dmid.x;
+        D[r][2] = dmid.y;
+        D[r][3] = drow[xr];
+    }
+    // column min / max (packed f16) and Gaussian column sums (fp32)
+    h2 nxy[4], nzw[4], xxy[4], xzw[4];
+    v2f sxy[4], szw[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        nxy[c] = __builtin_elementwise_min(__builtin_elementwise_min(Cxy[0][c], Cxy[1][c]), Cxy[2][c]);
+        nzw[c] = __builtin_elementwise_min(__builtin_elementwise_min(Czw[0][c], Czw[1][c]), Czw[2][c]);
+        xxy[c] = __builtin_elementwise_max(__builtin_elementwise_max(Cxy[0][c], Cxy[1][c]), Cxy[2][c]);
+        xzw[c] = __builtin_elementwise_max(__builtin_elementwise_max(Czw[0][c], Czw[1][c]), Czw[2][c]);
+        const v2f q = v2f{0.25f, 0.25f}, hlf = v2f{0.5f, 0.5f};
+        sxy[c] = __builtin_elementwise_fma(h2f2(Cxy[2][c]), q, __builtin_elementwise_fma(h2f2(Cxy[1][c]), hlf, h2f2(Cxy[0][c]) * q));
+        szw[c] = __builtin_elementwise_fma(h2f2(Czw[2][c]), q, __builtin_elementwise_fma(h2f2(Czw[1][c]), hlf, h2f2(Czw[0][c]) * q));
+    }
+    const int colx[4] = {xl, x0, x0 + 1, xr};
+    const float v = centre_uv(y, H);
+    uint2 outp[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int x = x0 + k;
+        const float u = centre_uv(x, W);
+        // closest depth in the reference order (oy = +1..-1, ox = +1..-1), last equal wins
+        float closest = 1.0f;
+        int bc = k + 1, br = 1;
+        bool first = true;
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int ox = 1; ox > -2; --ox) {
+                const int c = k + 1 + ox;
+                const float d = D[r][c];
+                closest = fminf(d, closest);
+                const bool take = closest == d;
+                if (first) { bc = take ? c : bc; br = take ? r : br; first = false; }
+                else { bc = take ? c : bc; br = take ? r : br; }
+            }
+        const int bx = colx[bc], by = rows[br];
+        const h2 mnxy = __builtin_elementwise_min(__builtin_elementwise_min(nxy[k], nxy[k + 1]), nxy[k + 2]);
+        const h2 mnzw = __builtin_elementwise_min(__builtin_elementwise_min(nzw[k], nzw[k + 1]), nzw[k + 2]);
+        const h2 mxxy = __builtin_elementwise_max(__builtin_elementwise_max(xxy[k], xxy[k + 1]), xxy[k + 2]);
+        const h2 mxzw = __builtin_elementwise_max(__builtin_elementwise_max(xzw[k], xzw[k + 1]), xzw[k + 2]);
+        const v2f q = v2f{0.25f, 0.25f}, hlf = v2f{0.5f, 0.5f};
+        const v2f bxy = __builtin_elementwise_fma(sxy[k + 2], q, __builtin_elementwise_fma(sxy[k + 1], hlf, sxy[k] * q));
+        const v2f bzw = __builtin_elementwise_fma(szw[k + 2], q, __builtin_elementwise_fma(szw[k + 1], hlf, szw[k] * q));
+        const v2f cxy = h2f2(Cxy[1][k + 2]), czw = h2f2(Czw[1][k + 2]);   // quirk Q7: the (+1, 0) neighbour
+        const h2 vv = as_h2(row_ptr<uint32_t>(vel, by)[2 * bx]);
+        const float velx = (float)vv.x, vely = (float)vv.y;
+        // resolve (:172-189)
+        float accum = p.accum0;
+        const float vx = u - velx, vy = v - vely;
+        v2f axy, azw, pxy, unused;
+        sample_pair_rows(prev, vx, vy, axy, azw, true);
+        if (vx < 0.0f || vy < 0.0f || vx > 1.0f || vy > 1.0f) accum = 1.0f;
+        axy = __builtin_elementwise_min(__builtin_elementwise_max(axy, h2f2(mnxy)), h2f2(mxxy));
+        azw = __builtin_elementwise_min(__builtin_elementwise_max(azw, h2f2(mnzw)), h2f2(mxzw));
+        const v2f ac = v2f{accum, accum}, ic = v2f{1.0f - accum, 1.0f - accum};
+        const v2f oxy = __builtin_elementwise_fma(cxy, ac, axy * ic), ozw = __builtin_elementwise_fma(czw, ac, azw * ic);
+        sample_pair_rows(pvel, vx, vy, pxy, unused, false);
+        const float dvx = pxy.x - velx, dvy = pxy.y - vely;
+        const float vlen = __builtin_amdgcn_sqrtf(__builtin_fmaf(dvx, dvx, dvy * dvy));
+        const float dis = clampf((vlen - 0.001f) * 10.0f, 0.0f, 1.0f);
+        const v2f dd = v2f{dis, dis};
+        const v2f rxy = __builtin_elementwise_fma(bxy - oxy, dd, oxy), rzw = __builtin_elementwise_fma(bzw - ozw, dd, ozw);
+        outp[k] = pack_h4(f4{rxy.x, rxy.y, rzw.x, rzw.y});
+    }
+    row_ptr_w<uint4>(target, y)[x0 >> 1] = uint4{outp[0].x, outp[0].y, outp[1].x, outp[1].y};
+    if (vel_out.data) row_ptr_w<uint4>(vel_out, y)[x0 >> 1] = row_ptr<uint4>(vel, y)[x0 >> 1];
+}
+
 __global__ __launch_bounds__(256) void taa_generic(DImg target, DImg cur, DImg prev, DImg vel, DImg pvel, DImg depth,
                                                    DImg vel_out, TaaParams p) {
     const int x = blockIdx.x * BX + threadIdx.x, y = blockIdx.y * BY + threadIdx.y;
@@ -263,7 +392,7 @@ extern "C" int soc_temporal_antialiasing(const soc_globals* g, soc_img target, s
                       previous_velocity.width >= 2;
     if (pair) {
         dim3 g2(ceil_div(W / 2, BX), ceil_div(H, BY));
-        taa_pair<<<g2, blk, 0, hs(stream)>>>(dimg(target), dimg(current_color), dimg(previous_color), dimg(current_velocity),
+        taa_pair2<<<g2, blk, 0, hs(stream)>>>(dimg(target), dimg(current_color), dimg(previous_color), dimg(current_velocity),
                                              dimg(previous_velocity), dimg(depth), vo, p);
     } else if (fast)
         taa_fast<<<grd, blk, 0, hs(stream)>>>(dimg(target), dimg(current_color), dimg(previous_color), dimg(current_velocity),
