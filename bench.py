@@ -96,7 +96,7 @@ def cpu_baseline(W, H, host_inputs, g):
     fr["emissive"] = host_inputs["emissive"].copy()
     ae = soc.AutoExposure()
     frames, t_total = 0, 0.0
-    while frames < 1 or (t_total < 10.0 and frames < 3):
+    while frames < 2 or (t_total < 12.0 and frames < 30):
         fr["emissive"][...] = host_inputs["emissive"]
         t0 = time.perf_counter()
         oracle.frame(g, fr, ae, hist=frames % 2)

@@ -9,8 +9,9 @@
 // of a bilinear REPEAT tap), 16 KiB per workgroup.
 #include "soc_internal.hpp"
 
-// Profiling builds only (tools/clouds_variants.py): 1 = atmosphere only, 2 = cloud march only,
-// 3 = cloud march without the sun-visibility march. The library is always built with 0.
+// Profiling builds only (tools/kernel_variants.py): 1 = atmosphere only, 2 = cloud march only,
+// 3 = cloud march without the sun-visibility march, 4 = classify only, 5 = classify only without the
+// list atomic. The library is always built with 0.
 #ifndef SOC_CLOUDS_PROFILE
 #define SOC_CLOUDS_PROFILE 0
 #endif
@@ -264,7 +265,7 @@ __device__ __forceinline__ f3 sky_dir(const CloudParams& p, int x, int y) {
 }
 
 __device__ __forceinline__ f3 sky_atmosphere(const CloudParams& p, f3 dir) {
-    if (SOC_CLOUDS_PROFILE >= 2) return f3{0.1f, 0.2f, 0.3f};
+    if (SOC_CLOUDS_PROFILE == 2 || SOC_CLOUDS_PROFILE == 3) return f3{0.1f, 0.2f, 0.3f};
     const f3 r0 = f3{0.0f + p.cam[0], 6372e3f + p.cam[1], 0.0f + p.cam[2]};
     return atmosphere(dir, r0, f3{p.sun[0], p.sun[1], p.sun[2]}, p.elapsed);
 }
@@ -327,24 +328,29 @@ __global__ __launch_bounds__(256) void clouds_kernel(DImg depth, DImg noise, DIm
 
 // Three-kernel path, stage 1 (classify). Every pixel first gets the constant non-sky colour (a sky pixel
 // is overwritten by the march later in stream order); sky pixels are appended to a compact list.
-// A workgroup covers a 32x32 tile, each wave a 16x16 quarter, each lane 4 horizontal pixels (one 16-B
-// store). Entries are ordered row-major inside a wave's quarter, so a wave of the march takes a compact
-// 16x4 block. The list offset costs ONE atomic per workgroup that has sky: device-scope atomics on one
-// address serialise across the XCDs (one per wave cost ~95 us at 4K).
+// A workgroup covers a 64x16 tile, each wave a 32x8 quarter (every row of a wave one full 128-B line of
+// depth and of the target), each lane 4 horizontal pixels (one 16-B store). Entries are ordered
+// row-major inside a wave's quarter, so a wave of the march takes a compact 32x2 block. The list offset
+// costs ONE atomic per workgroup that has sky: device-scope atomics on one address serialise across
+// the XCDs (one per wave cost ~95 us at 4K).
 __global__ __launch_bounds__(256) void clouds_classify(DImg depth, DImg target, CloudParams p, int vec_store,
                                                        uint32_t* __restrict__ counter, uint32_t* __restrict__ list) {
     __shared__ uint32_t wave_total[4];
     __shared__ uint32_t wg_base;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int x0 = blockIdx.x * 32 + (wave & 1) * 16 + (lane & 3) * 4;
-    const int y = blockIdx.y * 32 + (wave >> 1) * 16 + (lane >> 2);
+    const int x0 = blockIdx.x * 64 + (wave & 1) * 32 + (lane & 7) * 4;
+    const int y = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
     const int W = min(p.res_x, target.w), H = min(p.res_y, target.h);
     const uint32_t other = pack_unorm8x4(f4{0.2f, 0.4f, 1.0f, 1.0f});
     uint32_t mask = 0;   // bit k: pixel (x0 + k, y) is sky
     if (y < H) {
+        // all 16 depth loads issued together (clamped coordinates, no per-pixel branch)
+        float d[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) d[k] = sample_f32(depth, (float)min(x0 + k, W - 1) / p.res_x_m1, (float)y / p.res_y_m1);
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-            if (x0 + k < W && is_sky(p, depth, x0 + k, y)) mask |= 1u << k;
+            if (x0 + k < W && d[k] == 1.0f) mask |= 1u << k;
         uint32_t* row = row_ptr_w<uint32_t>(target, y);
         if (vec_store && x0 + 3 < W) {
             *reinterpret_cast<uint4*>(row + x0) = uint4{other, other, other, other};
@@ -366,7 +372,8 @@ __global__ __launch_bounds__(256) void clouds_classify(DImg depth, DImg target, 
     __syncthreads();
     if (threadIdx.x == 0) {
         const uint32_t sum = wave_total[0] + wave_total[1] + wave_total[2] + wave_total[3];
-        wg_base = sum ? atomicAdd(counter, sum) : 0u;
+        if (SOC_CLOUDS_PROFILE == 5) wg_base = (blockIdx.y * gridDim.x + blockIdx.x) * 1024u;
+        else wg_base = sum ? atomicAdd(counter, sum) : 0u;
     }
     __syncthreads();
     if (!mask) return;
@@ -471,7 +478,7 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
     hipError_t e = hipMemsetAsync(counter, 0, sizeof(uint32_t), s);
     if (e != hipSuccess) return set_error(SOC_E_HIP, "%s: %s", P, hipGetErrorString(e));
     const int vec_store = (target.pitch_bytes % 16 == 0) && (reinterpret_cast<uintptr_t>(target.data) % 16 == 0);
-    clouds_classify<<<dim3(ceil_div(W, 32), ceil_div(H, 32)), 256, 0, s>>>(dimg(depth), dimg(target), p, vec_store, counter, list);
+    clouds_classify<<<dim3(ceil_div(W, 64), ceil_div(H, 16)), 256, 0, s>>>(dimg(depth), dimg(target), p, vec_store, counter, list);
     float4* atmos = reinterpret_cast<float4*>(reinterpret_cast<char*>(list) + (((size_t)W * H * sizeof(uint32_t) + 15) & ~(size_t)15));
     // One resident wave set per kernel: every lane loops over the list with a grid stride, so the long
     // per-pixel work is balanced over all SIMDs instead of running as a second, partially filled round.
@@ -481,6 +488,7 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
         resident_march = resident_blocks(clouds_march<false>);
     }
     const long long blocks = ((long long)W * H + 255) / 256;
+    if (SOC_CLOUDS_PROFILE >= 4) return check_launch("cloud_rendering");
     clouds_atmosphere<<<(int)std::min<long long>(resident_atmos, blocks), 256, 0, s>>>(p, counter, list, atmos);
     const int grid = (int)std::min<long long>(resident_march, blocks);
     if (r8) clouds_march<true><<<grid, 256, 0, s>>>(dimg(noise), dimg(target), p, counter, list, atmos);

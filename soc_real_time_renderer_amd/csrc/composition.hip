@@ -14,6 +14,7 @@ namespace {
 
 struct CompParams {
     Mat4 inv_proj, inv_view, sun_pv;
+    Mat4 sun_clip;        // sun_pv * inv_view * inv_proj: NDC (x, y, depth, 1) -> sun clip space
     float sun_dir[3], ambient[3], cam[3];
     float ef, df, emissive_strength, ao_strength;
     uint32_t npl, nsl;
@@ -61,19 +62,19 @@ __device__ f3 spot_light(const soc_spot_light& L, f3 frag_color, f3 normal, f3 p
 }
 
 // Shading of one pixel given its G-buffer values (composition.inl:164-224).
+// The sun-space position is one projective transform of the NDC point: vs = inv_proj * ndc,
+// ws = inv_view * (vs / vs.w), sp = sun_pv * ws, and pc = sp.xyz / sp.w, so the vs.w division cancels
+// and sun_clip = sun_pv * inv_view * inv_proj (host fp32) gives pc directly (one rcp; within the
+// RGBA16F tolerance). The world position itself is only formed for the light loops.
 __device__ __forceinline__ f4 shade(const CompParams& p, float u, float v, float d, f3 albedo, f3 emissive, f3 n,
                                     float ssao, const DImg& shadow) {
-    // get_world_position_from_depth, :114-122
-    f4 vs = mul(p.inv_proj, f4{u * 2.0f - 1.0f, v * 2.0f - 1.0f, d, 1.0f});
-    const float rw = vs.w;
-    vs = f4{vs.x / rw, vs.y / rw, vs.z / rw, vs.w / rw};
-    const f4 ws = mul(p.inv_view, vs);
-    const f3 wp = f3{ws.x, ws.y, ws.z};
+    const f4 ndc = f4{u * 2.0f - 1.0f, v * 2.0f - 1.0f, d, 1.0f};
     // sun ESM shadow, :166-173
-    const f4 sp = mul(p.sun_pv, f4{wp.x, wp.y, wp.z, 1.0f});
-    const float pcx = __fdividef(sp.x, sp.w) * 0.5f + 0.5f;
-    const float pcy = __fdividef(sp.y, sp.w) * 0.5f + 0.5f;
-    const float pcz = __fdividef(sp.z, sp.w);
+    const f4 sp = mul(p.sun_clip, ndc);
+    const float rsw = __builtin_amdgcn_rcpf(sp.w);
+    const float pcx = sp.x * rsw * 0.5f + 0.5f;
+    const float pcy = sp.y * rsw * 0.5f + 0.5f;
+    const float pcz = sp.z * rsw;
     const float sd = sample_f32(shadow, pcx, pcy);
     float e = __expf(p.ef * (pcz - sd));
     if (p.df != 1.0f) e = fast_pow(e, p.df);   // pow(x, 1.0) == x exactly
@@ -84,6 +85,12 @@ __device__ __forceinline__ f4 shade(const CompParams& p, float u, float v, float
     const float dd = fmaxf(0.0f, dot3(n, -mk3(p.sun_dir[0], p.sun_dir[1], p.sun_dir[2]))) * sun_shadow;
     f3 direct = f3{dd, dd, dd};
     if (p.npl | p.nsl) {
+        // get_world_position_from_depth, :114-122
+        f4 vs = mul(p.inv_proj, ndc);
+        const float rw = __builtin_amdgcn_rcpf(vs.w);
+        vs = f4{vs.x * rw, vs.y * rw, vs.z * rw, 1.0f};
+        const f4 ws = mul(p.inv_view, vs);
+        const f3 wp = f3{ws.x, ws.y, ws.z};
         const f3 cam = mk3(p.cam[0], p.cam[1], p.cam[2]);
         for (uint32_t i = 0; i < p.npl; ++i) direct = direct + point_light(p.dg->point_lights[i], albedo, n, wp, cam);
         for (uint32_t i = 0; i < p.nsl; ++i) direct = direct + spot_light(p.dg->spot_lights[i], albedo, n, wp, cam);
@@ -171,6 +178,11 @@ extern "C" int soc_composition(const soc_globals* g, const soc_globals* d_global
     p.inv_proj = mat4(g->camera_inverse_projection_matrix);
     p.inv_view = mat4(g->camera_inverse_view_matrix);
     mat4_mul_host(p.sun_pv.m, g->sun_info.projection_matrix, g->sun_info.view_matrix);
+    {
+        float t[16];
+        mat4_mul_host(t, p.sun_pv.m, g->camera_inverse_view_matrix);
+        mat4_mul_host(p.sun_clip.m, t, g->camera_inverse_projection_matrix);
+    }
     for (int i = 0; i < 3; ++i) {
         p.sun_dir[i] = g->sun_info.direction[i];
         p.ambient[i] = g->ambient[i];

@@ -141,10 +141,11 @@ __global__ __launch_bounds__(256) void ssao_kernel(DImg depth, DImg normal, DImg
             const float rw = fast_rcp(aff(aw, kx, ky, kz));
             float tx = __builtin_fmaf(aff(ax, kx, ky, kz), rw, cx0);
             float ty = __builtin_fmaf(aff(ay, kx, ky, kz), rw, cy0);
-            tx = fminf(fmaxf(tx, 0.0f), tmax_x);
-            ty = fminf(fmaxf(ty, 0.0f), tmax_y);
-            const int fx = (int)floorf(__builtin_fmaf(tx, 256.0f, 0.5f));
-            const int fy = (int)floorf(__builtin_fmaf(ty, 256.0f, 0.5f));
+            tx = __builtin_amdgcn_fmed3f(tx, 0.0f, tmax_x);   // clamp: one v_med3, no NaN quieting
+            ty = __builtin_amdgcn_fmed3f(ty, 0.0f, tmax_y);
+            // t >= 0, so truncation is the floor
+            const int fx = (int)__builtin_fmaf(tx, 256.0f, 0.5f);
+            const int fy = (int)__builtin_fmaf(ty, 256.0f, 0.5f);
             const float wx = (float)(fx & 255) * (1.0f / 256.0f), wy = (float)(fy & 255) * (1.0f / 256.0f);
             const int off = __mul24(fy >> 8, pitch) + (fx >> 8) * 4;
             const f2a4 r0 = __builtin_bit_cast(f2a4, __builtin_amdgcn_raw_buffer_load_b64(rsrc, off, 0, 0));
@@ -162,7 +163,7 @@ __global__ __launch_bounds__(256) void ssao_kernel(DImg depth, DImg normal, DImg
                 vw = ip[3] * ex + ip[7] * ey + ip[11] * dd + ip[15];
             }
             const float sd = vz * fast_rcp(vw);
-            const float rc = fminf(r * fast_rcp(fabsf(frag.z - sd)), 1.0f);
+            const float rc = __builtin_amdgcn_fmed3f(r * fast_rcp(fabsf(frag.z - sd)), 0.0f, 1.0f);   // >= 0
             const float range = rc * rc * (3.0f - 2.0f * rc);   // smoothstep(0, 1, x)
             occ += (sd >= aff(az, kx, ky, kz)) ? range : 0.0f;
         }

@@ -15,7 +15,8 @@ BUILD = os.path.join(ROOT, "soc_real_time_renderer_amd", "build")
 VAR = os.path.join(BUILD, "variants")
 CASES = {
     "clouds": ("clouds.hip", "SOC_CLOUDS_PROFILE",
-               {0: "full", 1: "atmosphere only", 2: "cloud march only", 3: "cloud march, no sun march"}),
+               {0: "full", 1: "atmosphere only", 2: "cloud march only", 3: "cloud march, no sun march",
+                4: "classify only", 5: "classify only, no atomic"}),
     "bloom4": ("bloom_fused.hip", "SOC_BLOOM_PROFILE",
                {0: "K4 full", 1: "K4 no quad phase", 2: "K4 no output phase", 3: "K4 no global stores"}),
 }
@@ -30,7 +31,7 @@ def build(case):
         o = os.path.join(VAR, f"{case}{k}.o")
         so = os.path.join(VAR, f"libsoc_rt_{case}{k}.so")
         subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17",
-                               "-mcode-object-version=5", f"-D{macro}={k}", "-I" + os.path.join(ROOT, "include"),
+                               "-mcode-object-version=5", "-fno-slp-vectorize", f"-D{macro}={k}", "-I" + os.path.join(ROOT, "include"),
                                "-c", os.path.join(CSRC, src), "-o", o])
         subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", so, o] + objs)
 

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round-end evidence on the GPU box: full GPU test suite, default bench (with CPU baseline),
+# rocprofv3 kernel-trace stats of the bench, PMC FETCH_SIZE / WRITE_SIZE passes -> traffic table.
+# Usage: tools/round_profile.sh <tag>   (outputs under gpurun_out/<tag>_*)
+set -o pipefail
+export TMPDIR=/tmp
+T=${1:-r01}
+mkdir -p gpurun_out
+timeout -k 10 600 python -m pytest tests -q -m gpu > gpurun_out/${T}_tests.log 2>&1
+echo "tests rc=$?"; tail -3 gpurun_out/${T}_tests.log
+timeout -k 10 400 python bench.py > gpurun_out/${T}_bench.json 2> gpurun_out/${T}_bench.err || { echo "bench failed"; tail -5 gpurun_out/${T}_bench.err; exit 1; }
+cat gpurun_out/${T}_bench.json
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_kt -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/${T}_kt.log 2>&1 || { echo "kernel trace failed"; exit 1; }
+for c in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d gpurun_out/${T}_pmc/$c -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --profile-frames 1 > gpurun_out/${T}_pmc_$c.log 2>&1 || { echo "pmc $c failed"; exit 1; }
+done
+python tools/pmc_summary.py gpurun_out/${T}_pmc --traffic gpurun_out/${T}_pmc_traffic.json > gpurun_out/${T}_pmc_summary.json
+echo done
