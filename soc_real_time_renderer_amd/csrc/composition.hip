@@ -4,10 +4,17 @@
 // HBM-bound stream: per pixel it reads depth (4 B), albedo/emissive/normal (8 B each), one bilinear
 // half-res AO tap, one bilinear 4096^2 shadow-map tap and, on sky pixels only, the clouds texel; it
 // writes 8 B of RGBA16F. Fast path: two horizontally adjacent pixels per lane so every G-buffer load
-// and the store are 16 B per lane (one 1 KiB wave-instruction per image row segment), full-res taps
-// are plain loads (a centre sample under the sampling contract is the texel itself). The dead
-// volumetric-fog block (:176-196, zeroed at :196) is not computed.
+// and the store are 16 B per lane, a wave covering a 16x8 pixel block (one 128-B line per image row);
+// the block shape keeps the shadow-map gathers of a wave in a compact 2D patch of the map (measured:
+// 89 -> 75 us at 4K against 128x1 strips). Full-res taps are plain loads (a centre sample under the
+// sampling contract is the texel itself). The dead volumetric-fog block (:176-196, zeroed at :196)
+// is not computed.
 #include "soc_internal.hpp"
+
+// Profiling builds only (tools/kernel_variants.py): 1 = no shadow-map tap, 2 = no AO tap, 3 = neither.
+#ifndef SOC_COMP_PROFILE
+#define SOC_COMP_PROFILE 0
+#endif
 
 namespace soc {
 namespace {
@@ -75,7 +82,7 @@ __device__ __forceinline__ f4 shade(const CompParams& p, float u, float v, float
     const float pcx = sp.x * rsw * 0.5f + 0.5f;
     const float pcy = sp.y * rsw * 0.5f + 0.5f;
     const float pcz = sp.z * rsw;
-    const float sd = sample_f32(shadow, pcx, pcy);
+    const float sd = (SOC_COMP_PROFILE & 1) ? pcx * 0.001f : sample_f32(shadow, pcx, pcy);
     float e = __expf(p.ef * (pcz - sd));
     if (p.df != 1.0f) e = fast_pow(e, p.df);   // pow(x, 1.0) == x exactly
     const float sun_shadow = clampf(e, 0.0f, 1.0f);
@@ -104,7 +111,12 @@ constexpr int BX = 64, BY = 4;
 // Fast path: all full-res images share the target extent, width even, rows 16-B aligned.
 __global__ __launch_bounds__(256) void composition_pair(DImg target, DImg albedo, DImg emissive, DImg normal, DImg depth,
                                                         DImg ssao, DImg shadow, DImg clouds, CompParams p) {
-    const int x = (blockIdx.x * BX + threadIdx.x) * 2, y = blockIdx.y * BY + threadIdx.y;
+    // a wave covers 16x8 pixels (8 lanes x 2 pixels per row, 8 rows): every row segment is one
+    // 128-B line of each G-buffer image, and the wave's shadow-map taps form a compact 2D patch
+    // (a 128x1 strip maps to a line across the 4096^2 map and touches a new line per tap)
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int x = blockIdx.x * 32 + (wave & 1) * 16 + (lane & 7) * 2;
+    const int y = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
     if (x >= target.w || y >= target.h) return;
     const float v = centre_uv(y, target.h);
     const float2 d2 = row_ptr<float2>(depth, y)[x >> 1];
@@ -124,7 +136,7 @@ __global__ __launch_bounds__(256) void composition_pair(DImg target, DImg albedo
             const f4 cl = fetch_rgba8(clouds, x + k, y);
             c = f4{cl.x, cl.y, cl.z, 1.0f};
         } else {
-            const float ao = sample_r8(ssao, u, v);
+            const float ao = (SOC_COMP_PROFILE & 2) ? u : sample_r8(ssao, u, v);
             c = shade(p, u, v, d, f3{al.x, al.y, al.z}, f3{em.x, em.y, em.z}, f3{nn.x, nn.y, nn.z}, ao, shadow);
         }
         outp[k] = pack_h4(c);
@@ -204,8 +216,8 @@ extern "C" int soc_composition(const soc_globals* g, const soc_globals* d_global
                       W <= 8192 && H <= 8192 && aligned16(target) && aligned16(albedo) && aligned16(emissive) &&
                       aligned16(normal) && (reinterpret_cast<uintptr_t>(depth.data) & 7u) == 0 && (depth.pitch_bytes & 7) == 0;
     if (fast) {
-        dim3 blk(BX, BY), grd(ceil_div(W / 2, BX), ceil_div(H, BY));
-        composition_pair<<<grd, blk, 0, hs(stream)>>>(dimg(target), dimg(albedo), dimg(emissive), dimg(normal), dimg(depth),
+        dim3 grd(ceil_div(W, 32), ceil_div(H, 16));
+        composition_pair<<<grd, 256, 0, hs(stream)>>>(dimg(target), dimg(albedo), dimg(emissive), dimg(normal), dimg(depth),
                                                       dimg(ssao), dimg(shadow), dimg(clouds), p);
     } else {
         dim3 blk(BX, BY), grd(ceil_div(W, BX), ceil_div(H, BY));

@@ -2,7 +2,7 @@
 
 Each variant is clouds.hip / bloom_fused.hip compiled with the macro and linked with the other
 objects into build/variants/libsoc_rt_<name><k>.so (ctypes loads them side by side).
-Usage: python tools/kernel_variants.py {clouds|bloom4} [--build-only | --run-only] [--modes 0,2]
+Usage: python tools/kernel_variants.py {clouds|comp|bloom4} [--build-only | --run-only] [--modes 0,2]
 """
 import ctypes as C
 import os
@@ -17,6 +17,8 @@ CASES = {
     "clouds": ("clouds.hip", "SOC_CLOUDS_PROFILE",
                {0: "full", 1: "atmosphere only", 2: "cloud march only", 3: "cloud march, no sun march",
                 4: "classify only", 5: "classify only, no atomic"}),
+    "comp": ("composition.hip", "SOC_COMP_PROFILE",
+             {0: "full", 1: "no shadow tap", 2: "no AO tap", 3: "no shadow, no AO"}),
     "bloom4": ("bloom_fused.hip", "SOC_BLOOM_PROFILE",
                {0: "K4 full", 1: "K4 no quad phase", 2: "K4 no output phase", 3: "K4 no global stores"}),
 }
@@ -46,6 +48,17 @@ def workload(case, lib, dev):
     g = bench.make_globals(W, H, multi_gpu.camera_for_rank(0))
     s = torch.cuda.current_stream()
     P = C.c_void_p
+    if case == "comp":
+        gb = scene.gbuffer(g, W, H)
+        shadow = torch.from_numpy(scene.shadow_map(g, 4096)).to(dev)
+        t = {k: torch.from_numpy(gb[k]).to(dev) for k in ("albedo", "emissive", "normal", "depth")}
+        ssao = torch.full((H // 2, W // 2), 200, dtype=torch.uint8, device=dev)
+        clouds = torch.zeros(H, W, 4, dtype=torch.uint8, device=dev)
+        out = torch.zeros(H, W, 4, dtype=torch.float16, device=dev)
+        lib.soc_composition.argtypes = [P, P] + [_abi.SocImg] * 8 + [P]
+        args = (C.byref(g), None, soc.img(out), soc.img(t["albedo"]), soc.img(t["emissive"]), soc.img(t["normal"]),
+                soc.img(t["depth"]), soc.img(ssao), soc.img(shadow), soc.img(clouds), P(s.cuda_stream))
+        return lambda: lib.soc_composition(*args), (shadow, t, ssao, clouds, out)
     if case == "clouds":
         gb = scene.gbuffer(g, W, H)
         depth = torch.from_numpy(gb["depth"]).to(dev)
