@@ -250,8 +250,10 @@ int soc_ssao_blur(const soc_globals* g, soc_img ssao, soc_img target, soc_stream
 /* CloudRenderingTask (cloud_rendering.inl:27-54, shader :441-481): atmosphere + volumetric clouds on
  * sky pixels (depth == 1), constant (0.2,0.4,1.0) elsewhere. `noise` is the 64x64 RGBA8 or R8
  * noise texture (assets/Clouds/noise.png, REPEAT). target: RGBA8_UNORM full-res (quirk Q6).
- * `workspace` (optional, soc_cloud_rendering_workspace_size bytes of device memory) enables the
- * two-kernel path: sky pixels are compacted into a list so every lane of the march is a sky pixel. */
+ * `workspace` (optional, soc_cloud_rendering_workspace_size(target.width, target.height) bytes of
+ * device memory) enables the compacted path: sky pixels are listed, and the cloud march is split at
+ * its dense steps into (pixel, step) pairs so the sun-visibility marches are spread evenly over the
+ * lanes; the result is bit-identical to the workspace-free single kernel. */
 size_t soc_cloud_rendering_workspace_size(int32_t width, int32_t height);
 int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img noise, soc_img target, void* workspace,
                         soc_stream stream);

@@ -165,49 +165,68 @@ __device__ f3 scattering_top(f3 sun) {
     return (ms + rs) * absorb * kSunBrightness;
 }
 
-// calculate_volumetric_clouds, :307-347
-__device__ f3 volumetric_clouds(const Ctx& cx, f3 dir, f3 sun, f3 color, float dither, f3 sun_color) {
-    if (dir.y < 0.0f) return color;
-    const float rPi = 1.0f / kPi, hPi = kPi * 0.5f, rLOG2 = 1.0f / kLn2;
+// The march of calculate_volumetric_clouds (:307-325): 24 steps between the bottom and top shells.
+struct MarchGeom {
+    f3 start, inc;
+    float stepLength;
+};
+__device__ __forceinline__ MarchGeom march_geometry(f3 dir) {
     const f3 c0 = f3{0.0f, kEarthRadius, 0.0f};
     const float bottom = rsi(c0, dir, kEarthRadius + kMinH).y;
     const float top = rsi(c0, dir, kEarthRadius + kMaxH).y;
-    const f3 start = dir * bottom, end = dir * top;
-    const f3 inc = (end - start) * (1.0f / 24.0f);
-    f3 cp = inc * dither + start;
-    const float stepLength = length3(inc);
+    MarchGeom g;
+    g.start = dir * bottom;
+    const f3 end = dir * top;
+    g.inc = (end - g.start) * (1.0f / 24.0f);
+    g.stepLength = length3(g.inc);
+    return g;
+}
+
+// Per-pixel constants of the scattering sum (:313-319).
+struct MarchShade {
+    float phase;
+    f3 skyl;   // sky * 0.25 / pi
+};
+__device__ __forceinline__ MarchShade march_shade(f3 dir, f3 sun) {
+    const float x = dot3(sun, dir);
+    MarchShade m;
+    m.phase = mixf(hg_phase(x, -0.5f * 0.8f), hg_phase(x, 0.8f * 0.8f), 0.5f);
+    m.skyl = scattering_top(sun) * 0.25f * (1.0f / kPi);
+    return m;
+}
+
+// One dense step of the scattering sum (:326-344), in the reference's order.
+__device__ __forceinline__ void march_accumulate(const MarchShade& ms, f3 sun_color, float od, float vis, f3& scattering,
+                                                 float& transmittance) {
+    const float hPi = kPi * 0.5f, rLOG2 = 1.0f / kLn2;
+    const float integral = __expf(-1.11f * rLOG2 * od) * (-1.0f / 1.11f) + 1.0f / 1.11f;
+    const float beers = 1.0f - __expf(-(od * kLn2) * 2.0f);
+    const f3 sunl = sun_color * vis * beers * ms.phase * hPi * kSunBrightness;
+    scattering = scattering + (sunl + ms.skyl) * integral * kPi * transmittance;
+    transmittance *= __expf(-od);
+}
+
+__device__ __forceinline__ f3 march_finish(const MarchGeom& mg, f3 color, f3 scattering, float transmittance) {
+    const f3 lit = color * transmittance + scattering;
+    const float m = clampf(length3(mg.start) * 0.00001f * 2.5f, 0.0f, 1.0f);
+    return f3{mixf(lit.x, color.x, m), mixf(lit.y, color.y, m), mixf(lit.z, color.z, m)};
+}
+
+// calculate_volumetric_clouds, :307-347 (single-lane form: the no-workspace kernel and the overflow
+// fallback of the pair path)
+__device__ f3 volumetric_clouds(const Ctx& cx, f3 dir, f3 sun, f3 color, float dither, f3 sun_color) {
+    if (dir.y < 0.0f) return color;
+    const MarchGeom mg = march_geometry(dir);
+    const MarchShade ms = march_shade(dir, sun);
+    f3 cp = mg.inc * dither + mg.start;
     f3 scattering = f3{0.0f, 0.0f, 0.0f};
     float transmittance = 1.0f;
-    const float x = dot3(sun, dir);
-    const float phase = mixf(hg_phase(x, -0.5f * 0.8f), hg_phase(x, 0.8f * 0.8f), 0.5f);
-    const f3 sky = scattering_top(sun);
-    // Two passes over the 24 steps so that the expensive sun march runs once per DENSE step of each lane
-    // rather than once per step that is dense in any lane of the wave: pass 1 records the dense steps,
-    // pass 2 visits them in order, re-deriving each od from the same cp bits (same additions) so the
-    // accumulation is the reference loop's, step for step.
-    uint32_t dense = 0;
-    {
-        f3 q = cp;
-        for (int i = 0; i < 24; i++, q = q + inc)
-            if (!(get_clouds(cx, q) * stepLength <= 0.0f)) dense |= 1u << i;
+    for (int i = 0; i < 24; i++, cp = cp + mg.inc) {
+        const float od = get_clouds(cx, cp) * mg.stepLength;
+        if (od <= 0.0f) continue;
+        march_accumulate(ms, sun_color, od, sun_visibility(cx, cp, sun), scattering, transmittance);
     }
-    int at = 0;
-    while (dense) {
-        const int i = __builtin_ctz(dense);
-        dense &= dense - 1u;
-        for (; at < i; ++at) cp = cp + inc;
-        const float od = get_clouds(cx, cp) * stepLength;
-        const float integral = __expf(-1.11f * rLOG2 * od) * (-1.0f / 1.11f) + 1.0f / 1.11f;
-        const float beers = 1.0f - __expf(-(od * kLn2) * 2.0f);
-        const float vis = sun_visibility(cx, cp, sun);
-        const f3 sunl = sun_color * vis * beers * phase * hPi * kSunBrightness;
-        const f3 skyl = sky * 0.25f * rPi;
-        scattering = scattering + (sunl + skyl) * integral * kPi * transmittance;
-        transmittance *= __expf(-od);
-    }
-    const f3 lit = color * transmittance + scattering;
-    const float m = clampf(length3(start) * 0.00001f * 2.5f, 0.0f, 1.0f);
-    return f3{mixf(lit.x, color.x, m), mixf(lit.y, color.y, m), mixf(lit.z, color.z, m)};
+    return march_finish(mg, color, scattering, transmittance);
 }
 
 // atmosphere, :353-439 (primary ray starts at iTime = elapsed_time: quirk Q10)
@@ -396,21 +415,244 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
     }
 }
 
-// Stage 3: the cloud march over the atmosphere colour, one listed sky pixel per lane (grid stride).
-template <bool NOISE_R8>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void clouds_march(DImg noise, DImg target, CloudParams p, const uint32_t* __restrict__ counter,
-                                                    const uint32_t* __restrict__ list, const float4* __restrict__ atmos) {
-    __shared__ uint32_t quads[kNoise * kNoise];
-    const uint32_t count = *counter;
-    const uint32_t first = blockIdx.x * 256u;
-    if (first >= count) return;                      // whole workgroup without work: skip the LDS fill
-    stage_noise<NOISE_R8>(noise, quads, threadIdx.x, 256);
+// ---- balanced cloud march: dense-step pairs ----------------------------------------------------
+// The cost of a sky pixel is dominated by its dense steps (each adds a 10-step sun march), which vary
+// from 0 to 24 between neighbouring screen regions; one pixel per lane leaves the kernel waiting on
+// its heaviest waves. The march is therefore split at the dense steps:
+//   density  one lane per sky pixel: the 24 primary steps -> dense-step mask; the pixel's
+//            (pixel, step) pairs are appended to one of 8 sharded pair lists (one atomic per workgroup)
+//   sunvis   one lane per pair: od and the sun visibility of that step (balanced work)
+//   resolve  one lane per sky pixel: the reference's accumulation over its dense steps, in order
+// Every position is re-derived with the same additions (cp = inc*dither + start, += inc), so od and vis
+// are the bits the single-lane march computes. A workgroup whose pairs do not fit the list marks its
+// pixels for the single-lane march in resolve.
+constexpr int kShards = 8;
+constexpr uint32_t kInline = 0x80000000u;   // pix_mask flag: march this pixel in resolve
+
+struct PairBufs {
+    uint32_t* counts;     // [kShards] pair counts (workspace counter block)
+    uint32_t* pairs;      // [kShards * cap] (list index << 5) | step
+    float2* odvis;        // [kShards * cap] (od, vis)
+    uint32_t* pix_mask;   // [W*H] per list entry: dense-step mask | kInline
+    uint32_t* batch_base; // [W*H/256] per 256-entry batch: physical index of its first pair | kInline
+    uint32_t cap;         // pairs per shard
+};
+
+__device__ __forceinline__ f3 step_position(const MarchGeom& mg, float dither, int step) {
+    f3 cp = mg.inc * dither + mg.start;
+    for (int i = 0; i < step; ++i) cp = cp + mg.inc;
+    return cp;
+}
+
+// Rank of this lane among the lanes of its wave whose mask has step `st`.
+__device__ __forceinline__ uint32_t mask_ballot_rank(uint32_t mask, uint32_t st, uint32_t lane) {
+    const unsigned long long b = __ballot((mask >> st) & 1u);
+    return (uint32_t)__builtin_popcountll(b & ((1ull << lane) - 1ull));
+}
+__device__ __forceinline__ uint32_t pair_offset(const uint32_t (*offs)[4], uint32_t st, uint32_t wave, uint32_t rank) {
+    return offs[st][wave] + rank;
+}
+// Step-major slot offsets of a 256-lane batch: offs[s][w] = number of pairs of steps < s (all waves)
+// plus those of step s in waves < w; offs[24][0] = total. Called by every lane of the workgroup
+// (ballots per wave, then one lane scans the 24 x 4 counts).
+__device__ __forceinline__ void batch_slots(uint32_t mask, uint32_t lane, uint32_t wave, uint32_t (*offs)[4],
+                                            uint32_t& /*unused*/, uint32_t tid) {
+#pragma unroll 1
+    for (uint32_t st = 0; st < 24; ++st) {
+        const unsigned long long b = __ballot((mask >> st) & 1u);
+        if (lane == 0) offs[st][wave] = (uint32_t)__builtin_popcountll(b);
+    }
     __syncthreads();
-    for (uint32_t i = first + threadIdx.x; i < count; i += gridDim.x * 256u) {
+    if (tid == 0) {
+        uint32_t acc = 0;
+        for (int st = 0; st < 24; ++st)
+            for (int w = 0; w < 4; ++w) {
+                const uint32_t c = offs[st][w];
+                offs[st][w] = acc;
+                acc += c;
+            }
+        offs[24][0] = acc;
+    }
+    __syncthreads();
+}
+
+template <bool NOISE_R8>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void clouds_density(
+    DImg noise, CloudParams p, const uint32_t* __restrict__ counter, const uint32_t* __restrict__ list, PairBufs pb) {
+    __shared__ uint32_t quads[kNoise * kNoise];
+    __shared__ uint32_t offs[25][4];
+    __shared__ uint32_t wg_base;
+    const uint32_t count = *counter;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (blockIdx.x * 256u >= count) return;
+    stage_noise<NOISE_R8>(noise, quads, tid, 256);
+    __syncthreads();
+    Ctx cx;
+    cx.quads = quads;
+    cx.cam_x = p.cam[0];
+    cx.cam_z = p.cam[2];
+    cx.time = -1.0f * 0.02f * p.elapsed;
+    const uint32_t shard = blockIdx.x & (kShards - 1);
+    // workgroup-uniform trip count: every lane reaches the barriers of every round
+    for (uint32_t first = blockIdx.x * 256u; first < count; first += gridDim.x * 256u) {
+        const uint32_t i = first + tid;
+        uint32_t mask = 0;
+        if (i < count) {
+            const uint32_t e = list[i];
+            const int x = (int)(e & 0xffffu), y = (int)(e >> 16);
+            const f3 dir = sky_dir(p, x, y);
+            if (SOC_CLOUDS_PROFILE != 1 && !(dir.y < 0.0f)) {
+                const MarchGeom mg = march_geometry(dir);
+                f3 cp = mg.inc * bayer16((float)x, (float)y) + mg.start;
+                for (int s = 0; s < 24; s++, cp = cp + mg.inc)
+                    if (!(get_clouds(cx, cp) * mg.stepLength <= 0.0f)) mask |= 1u << s;
+            }
+        }
+        // pairs in step-major order within the batch (lanes of a sunvis wave then share the step and
+        // march neighbouring rays); one atomic per batch on this workgroup's shard
+        uint32_t slot_base;
+        batch_slots(mask, lane, wave, offs, wg_base, tid);
+        __shared__ uint32_t fail_from;
+        if (tid == 0) {
+            const uint32_t total = offs[24][0];
+            uint32_t base = 0;
+            bool fail = false;
+            if (total) {
+                base = atomicAdd(&pb.counts[shard], total);
+                fail = base + total > pb.cap;
+            }
+            wg_base = fail ? kInline : shard * pb.cap + base;
+            fail_from = fail ? base : pb.cap;
+            pb.batch_base[first >> 8] = wg_base;
+        }
+        __syncthreads();
+        slot_base = wg_base;
+        // an overflowing batch leaves its reserved slots below the capacity empty: mark them
+        for (uint32_t k = fail_from + tid; k < pb.cap && k < fail_from + offs[24][0]; k += 256u)
+            pb.pairs[shard * pb.cap + k] = 0xffffffffu;
+        if (i < count) pb.pix_mask[i] = mask | ((slot_base & kInline) ? kInline : 0u);
+        if (!(slot_base & kInline)) {   // workgroup-uniform
+            // uniform loop: the ballot of every step sees every lane of the wave
+            for (uint32_t st = 0; st < 24; ++st) {
+                const uint32_t rank = mask_ballot_rank(mask, st, lane);
+                if ((mask >> st) & 1u) pb.pairs[slot_base + pair_offset(offs, st, wave, rank)] = (i << 5) | st;
+            }
+        }
+        __syncthreads();   // offs / wg_base are reused next round
+    }
+}
+
+template <bool NOISE_R8>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void clouds_sunvis(
+    DImg noise, CloudParams p, const uint32_t* __restrict__ list, PairBufs pb) {
+    __shared__ uint32_t quads[kNoise * kNoise];
+    __shared__ uint32_t pre[kShards + 1];
+    const uint32_t tid = threadIdx.x;
+    if (tid == 0) {
+        uint32_t acc = 0;
+        for (int k = 0; k < kShards; ++k) {
+            pre[k] = acc;
+            acc += min(pb.counts[k], pb.cap);   // an overflowing workgroup wrote no pairs
+        }
+        pre[kShards] = acc;
+    }
+    __syncthreads();
+    const uint32_t total = pre[kShards];
+    if (blockIdx.x * 256u >= total) return;
+    stage_noise<NOISE_R8>(noise, quads, tid, 256);
+    __syncthreads();
+    Ctx cx;
+    cx.quads = quads;
+    cx.cam_x = p.cam[0];
+    cx.cam_z = p.cam[2];
+    cx.time = -1.0f * 0.02f * p.elapsed;
+    const f3 sun = f3{p.sun[0], p.sun[1], p.sun[2]};
+    for (uint32_t v = blockIdx.x * 256u + tid; v < total; v += gridDim.x * 256u) {
+        int k = 0;
+        while (k + 1 < kShards && v >= pre[k + 1]) ++k;
+        const uint32_t phys = (uint32_t)k * pb.cap + (v - pre[k]);
+        const uint32_t pr = pb.pairs[phys];
+        if (pr == 0xffffffffu) continue;   // slot of an overflowed batch
+        const uint32_t i = pr >> 5, step = pr & 31u;
         const uint32_t e = list[i];
         const int x = (int)(e & 0xffffu), y = (int)(e >> 16);
-        const float4 a = atmos[i];
-        row_ptr_w<uint32_t>(target, y)[x] = sky_clouds(p, quads, x, y, sky_dir(p, x, y), f3{a.x, a.y, a.z});
+        const MarchGeom mg = march_geometry(sky_dir(p, x, y));
+        const f3 cp = step_position(mg, bayer16((float)x, (float)y), (int)step);
+        const float od = get_clouds(cx, cp) * mg.stepLength;
+        const float vis = SOC_CLOUDS_PROFILE == 3 ? 1.0f : sun_visibility(cx, cp, sun);
+        pb.odvis[phys] = float2{od, vis};
+    }
+}
+
+template <bool NOISE_R8>
+__global__ __launch_bounds__(256) void clouds_resolve(DImg noise, DImg target, CloudParams p, const uint32_t* __restrict__ counter,
+                                                      const uint32_t* __restrict__ list, const float4* __restrict__ atmos,
+                                                      PairBufs pb) {
+    __shared__ uint32_t quads[kNoise * kNoise];
+    __shared__ uint32_t offs[25][4];
+    const uint32_t count = *counter;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (blockIdx.x * 256u >= count) return;
+    const f3 sun = f3{p.sun[0], p.sun[1], p.sun[2]}, sun_color = f3{0.8f, 0.8f, 0.8f};
+    uint32_t dummy = 0;
+    for (uint32_t first = blockIdx.x * 256u; first < count; first += gridDim.x * 256u) {
+        const uint32_t i = first + tid;
+        const bool valid = i < count;
+        const uint32_t flagged = valid ? pb.pix_mask[i] : 0u;
+        const uint32_t mask = flagged & ~kInline;
+        const uint32_t base = pb.batch_base[first >> 8];   // workgroup-uniform
+        const bool inl = (base & kInline) != 0u;
+        // the single-lane march of an overflowed batch needs the noise in LDS
+        if (inl) {
+            stage_noise<NOISE_R8>(noise, quads, tid, 256);
+            __syncthreads();
+        } else {
+            batch_slots(mask, lane, wave, offs, dummy, tid);   // the slot layout of clouds_density
+        }
+        uint32_t e = 0;
+        f3 color = f3{0.0f, 0.0f, 0.0f}, dir = f3{0.0f, 1.0f, 0.0f};
+        if (valid) {
+            e = list[i];
+            const float4 a = atmos[i];
+            color = f3{a.x, a.y, a.z};
+            dir = sky_dir(p, (int)(e & 0xffffu), (int)(e >> 16));
+        }
+        const int x = (int)(e & 0xffffu), y = (int)(e >> 16);
+        if (SOC_CLOUDS_PROFILE == 1) {
+        } else if (inl) {
+            if (valid) {
+                Ctx cx;
+                cx.quads = quads;
+                cx.cam_x = p.cam[0];
+                cx.cam_z = p.cam[2];
+                cx.time = -1.0f * 0.02f * p.elapsed;
+                color = volumetric_clouds(cx, dir, sun, color, bayer16((float)x, (float)y), sun_color);
+            }
+        } else {
+            const bool march = valid && !(dir.y < 0.0f);
+            MarchGeom mg{};
+            MarchShade ms{};
+            if (march) {
+                mg = march_geometry(dir);
+                ms = march_shade(dir, sun);
+            }
+            f3 scattering = f3{0.0f, 0.0f, 0.0f};
+            float transmittance = 1.0f;
+            // steps in order; the ballot runs on every lane of the wave (uniform loop)
+            for (uint32_t st = 0; st < 24; ++st) {
+                const uint32_t rank = mask_ballot_rank(mask, st, lane);
+                if (march && ((mask >> st) & 1u)) {
+                    const float2 ov = pb.odvis[base + offs[st][wave] + rank];
+                    march_accumulate(ms, sun_color, ov.x, ov.y, scattering, transmittance);
+                }
+            }
+            if (march) color = march_finish(mg, color, scattering, transmittance);
+        }
+        if (valid) {
+            color = color * p.sun_factor;
+            row_ptr_w<uint32_t>(target, y)[x] = pack_unorm8x4(f4{color.x, color.y, color.z, 1.0f});
+        }
+        __syncthreads();   // offs / quads are reused next round
     }
 }
 
@@ -430,11 +672,46 @@ int resident_blocks(K kernel) {
 
 using namespace soc;
 
+namespace {
+// Workspace: counters (256 B: [0] sky pixels, [8..15] pair counts per shard) | sky list (u32) |
+// atmosphere (float4) | per-pixel dense mask (u32) | per-batch first pair (u32) | pairs (u32) |
+// (od, vis) per pair (float2). Pair capacity 2 per pixel of the image (8 shards).
+// Per 256-entry batch of the list: the physical index of its first pair (or kInline).
+struct CloudWs {
+    uint32_t* counter;
+    uint32_t* list;
+    float4* atmos;
+    PairBufs pb;
+    size_t bytes;
+};
+CloudWs cloud_ws_layout(void* base, size_t n) {
+    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    char* b = static_cast<char*>(base);
+    CloudWs w;
+    size_t off = 256;
+    w.counter = reinterpret_cast<uint32_t*>(b);
+    w.list = reinterpret_cast<uint32_t*>(b + off);
+    off = al(off + n * 4);
+    w.atmos = reinterpret_cast<float4*>(b + off);
+    off = al(off + n * 16);
+    w.pb.counts = w.counter + 8;
+    w.pb.pix_mask = reinterpret_cast<uint32_t*>(b + off);
+    off = al(off + n * 4);
+    w.pb.batch_base = reinterpret_cast<uint32_t*>(b + off);
+    off = al(off + (n / 256 + 1) * 4);
+    w.pb.cap = (uint32_t)((2 * n + kShards - 1) / kShards);
+    w.pb.pairs = reinterpret_cast<uint32_t*>(b + off);
+    off = al(off + (size_t)kShards * w.pb.cap * 4);
+    w.pb.odvis = reinterpret_cast<float2*>(b + off);
+    off = al(off + (size_t)kShards * w.pb.cap * 8);
+    w.bytes = off;
+    return w;
+}
+}  // namespace
+
 extern "C" size_t soc_cloud_rendering_workspace_size(int32_t width, int32_t height) {
     if (width <= 0 || height <= 0) return 0;
-    // counter | list of sky pixels (u32 each) | their atmosphere colours (float4, 16-B aligned)
-    const size_t n = (size_t)width * (size_t)height;
-    return 256 + ((n * sizeof(uint32_t) + 15) & ~(size_t)15) + n * 16;
+    return cloud_ws_layout(nullptr, (size_t)width * (size_t)height).bytes;
 }
 
 extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img noise, soc_img target, void* workspace,
@@ -473,25 +750,36 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
         else clouds_kernel<false><<<grd, blk, 0, s>>>(dimg(depth), dimg(noise), dimg(target), p);
         return check_launch("cloud_rendering");
     }
-    uint32_t* counter = static_cast<uint32_t*>(workspace);
-    uint32_t* list = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + 256);
-    hipError_t e = hipMemsetAsync(counter, 0, sizeof(uint32_t), s);
+    // the caller sized the workspace for the target extent (soc_cloud_rendering_workspace_size)
+    const CloudWs ws = cloud_ws_layout(workspace, (size_t)target.width * (size_t)target.height);
+    uint32_t* counter = ws.counter;
+    uint32_t* list = ws.list;
+    hipError_t e = hipMemsetAsync(counter, 0, 256, s);
     if (e != hipSuccess) return set_error(SOC_E_HIP, "%s: %s", P, hipGetErrorString(e));
     const int vec_store = (target.pitch_bytes % 16 == 0) && (reinterpret_cast<uintptr_t>(target.data) % 16 == 0);
     clouds_classify<<<dim3(ceil_div(W, 64), ceil_div(H, 16)), 256, 0, s>>>(dimg(depth), dimg(target), p, vec_store, counter, list);
-    float4* atmos = reinterpret_cast<float4*>(reinterpret_cast<char*>(list) + (((size_t)W * H * sizeof(uint32_t) + 15) & ~(size_t)15));
-    // One resident wave set per kernel: every lane loops over the list with a grid stride, so the long
-    // per-pixel work is balanced over all SIMDs instead of running as a second, partially filled round.
-    static int resident_atmos = 0, resident_march = 0;
-    if (!resident_atmos) {
-        resident_atmos = resident_blocks(clouds_atmosphere);
-        resident_march = resident_blocks(clouds_march<false>);
+    // One resident wave set per kernel, grid-stride over the list / pairs: the long per-item work is
+    // balanced over all SIMDs instead of running as a second, partially filled round.
+    static int res_atmos = 0, res_density = 0, res_sunvis = 0, res_resolve = 0;
+    if (!res_atmos) {
+        res_atmos = resident_blocks(clouds_atmosphere);
+        res_density = resident_blocks(clouds_density<false>);
+        res_sunvis = resident_blocks(clouds_sunvis<false>);
+        res_resolve = resident_blocks(clouds_resolve<false>);
     }
     const long long blocks = ((long long)W * H + 255) / 256;
     if (SOC_CLOUDS_PROFILE >= 4) return check_launch("cloud_rendering");
-    clouds_atmosphere<<<(int)std::min<long long>(resident_atmos, blocks), 256, 0, s>>>(p, counter, list, atmos);
-    const int grid = (int)std::min<long long>(resident_march, blocks);
-    if (r8) clouds_march<true><<<grid, 256, 0, s>>>(dimg(noise), dimg(target), p, counter, list, atmos);
-    else clouds_march<false><<<grid, 256, 0, s>>>(dimg(noise), dimg(target), p, counter, list, atmos);
+    auto grid = [&](int res, long long items_blocks) { return (int)std::max(1LL, std::min<long long>(res, items_blocks)); };
+    clouds_atmosphere<<<grid(res_atmos, blocks), 256, 0, s>>>(p, counter, list, ws.atmos);
+    const DImg nz = dimg(noise), tg = dimg(target);
+    if (r8) {
+        clouds_density<true><<<grid(res_density, blocks), 256, 0, s>>>(nz, p, counter, list, ws.pb);
+        clouds_sunvis<true><<<grid(res_sunvis, 2 * blocks), 256, 0, s>>>(nz, p, list, ws.pb);
+        clouds_resolve<true><<<grid(res_resolve, blocks), 256, 0, s>>>(nz, tg, p, counter, list, ws.atmos, ws.pb);
+    } else {
+        clouds_density<false><<<grid(res_density, blocks), 256, 0, s>>>(nz, p, counter, list, ws.pb);
+        clouds_sunvis<false><<<grid(res_sunvis, 2 * blocks), 256, 0, s>>>(nz, p, list, ws.pb);
+        clouds_resolve<false><<<grid(res_resolve, blocks), 256, 0, s>>>(nz, tg, p, counter, list, ws.atmos, ws.pb);
+    }
     return check_launch("cloud_rendering");
 }

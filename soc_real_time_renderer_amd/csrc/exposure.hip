@@ -11,6 +11,8 @@
 #include <type_traits>
 #include <algorithm>
 
+#include <cstdlib>
+
 #include "soc_internal.hpp"
 
 namespace soc {
@@ -68,12 +70,22 @@ __global__ __launch_bounds__(kThreads) void histogram_chunks(DImg hdr, int W, in
     __syncthreads();
     const int cpr = W / kPix;                       // chunks per row
     const long long total = (long long)cpr * H;
-    for (long long c = (long long)blockIdx.x * kThreads + tid; c < total; c += (long long)gridDim.x * kThreads) {
+    const long long stride = (long long)gridDim.x * kThreads;
+    // software pipelined: the next chunk's 64 B are in flight while this chunk is binned
+    auto fetch = [&](long long c, uint4 (&q)[kPix / 2]) {
         const int y = (int)(c / cpr), cx = (int)(c - (long long)y * cpr);
         const uint4* p = row_ptr<uint4>(hdr, y) + cx * (kPix / 2);
-        uint4 q[kPix / 2];
 #pragma unroll
         for (int k = 0; k < kPix / 2; ++k) q[k] = p[k];
+    };
+    long long c = (long long)blockIdx.x * kThreads + tid;
+    uint4 nxt[kPix / 2];
+    if (c < total) fetch(c, nxt);
+    for (; c < total; c += stride) {
+        uint4 q[kPix / 2];
+#pragma unroll
+        for (int k = 0; k < kPix / 2; ++k) q[k] = nxt[k];
+        if (c + stride < total) fetch(c + stride, nxt);
         uint32_t cur = 0xffffffffu, run = 0;
 #pragma unroll
         for (int k = 0; k < kPix / 2; ++k) {
@@ -153,7 +165,8 @@ int hist_grid() {
             hipDeviceProp_t prop;
             if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0) cus = prop.multiProcessorCount;
         }
-        g_hist_blocks = 2 * cus;
+        const char* e = getenv("SOC_HIST_BLOCKS_PER_CU");   // tuning knob
+        g_hist_blocks = (e ? atoi(e) : 2) * cus;
     }
     return g_hist_blocks;
 }

@@ -284,6 +284,23 @@ def test_clouds(soc, oracle, W, H, pitch, compact):
     assert (host(out)[nonsky][:, :3] == np.array([51, 102, 255], np.uint8)).all()
 
 
+@pytest.mark.parametrize("W,H,pitch,all_sky", [(320, 180, 0.35, False), (1920, 1080, 0.35, False), (256, 144, 0.9, True)])
+def test_clouds_pair_path_equals_single_lane(soc, W, H, pitch, all_sky):
+    """The workspace path (classify, atmosphere, density / sunvis / resolve over dense-step pairs) gives
+    the single-lane kernel's bits: od and vis are evaluated at the same positions with the same
+    additions and accumulated in the same order. An all-sky frame overflows the pair lists (2 pairs per
+    image pixel) and exercises the per-batch single-lane fallback."""
+    g, gb = sponza_inputs(W, H, camera=((-14.0, 2.2, 0.3), (0.0, pitch, 0.0)), elapsed=10.0)
+    depth = np.ones_like(gb["depth"]) if all_sky else gb["depth"]
+    a = torch.zeros(H, W, 4, dtype=torch.uint8, device=DEV)
+    b = torch.zeros_like(a)
+    ws = soc.cloud_rendering_workspace(W, H)
+    soc.cloud_rendering(g, dev(depth), dev(gb["noise"]), a, None)
+    soc.cloud_rendering(g, dev(depth), dev(gb["noise"]), b, ws)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b), (a != b).float().mean().item()
+
+
 # ------------------------------------------------------------------------------------------------ full frame
 @pytest.mark.parametrize("W,H,frames", [(256, 144, 3), (1920, 1080, 2)])
 def test_render_graph_frames(soc, oracle, W, H, frames):
