@@ -219,10 +219,9 @@ __global__ __launch_bounds__(256) void bloom_up_double_q(DImg src, DImg dst, boo
     const int X0 = 2 * m, Y0 = 2 * n;
     const bool interior = m - 2 >= 0 && m + 2 <= src.w - 1 && n - 2 >= 0 && n + 2 <= src.h - 1;
     if (!interior) {
-#pragma unroll
-        for (int py = 0; py < 2; ++py)
-#pragma unroll
-            for (int px = 0; px < 2; ++px) {
+#pragma unroll 1
+        for (int k = 0; k < 4; ++k) {
+                const int px = k & 1, py = k >> 1;
                 const int x = X0 + px, y = Y0 + py;
                 auto AX = [&](int k) { return axis_from_fixed(128 * x - 64 + 256 * k, src.w); };
                 auto AY = [&](int k) { return axis_from_fixed(128 * y - 64 + 256 * k, src.h); };
@@ -249,21 +248,33 @@ __global__ __launch_bounds__(256) void bloom_up_double_q(DImg src, DImg dst, boo
         for (int r = 0; r < 5; ++r)
 #pragma unroll
             for (int c = 0; c < 5; ++c) V[r][c] = chan<C>(T[r][c]);
+        // four times the horizontal lerps of both parities (exact: RGBA16F texels, bloom_common.hpp)
+        float H0[5][3], H1[5][3];
+#pragma unroll
+        for (int r = 0; r < 5; ++r)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                H0[r][k] = t_w34(V[r][k], V[r][k + 1]);
+                H1[r][k] = t_w14(V[r][k + 1], V[r][k + 2]);
+            }
 #pragma unroll
         for (int px = 0; px < 2; ++px) {
-            const float wx = px ? 0.25f : 0.75f;
-            float Hl[5][3];   // row r, x-tap k+1: blend of window columns (k+1+px, k+2+px)
+            const float (&Hl)[5][3] = px ? H1 : H0;
+            // vertical: py 0 = v_w34(rows ky+1, ky+2), py 1 = v_w14(rows ky+2, ky+3); both use the same
+            // rounded product of row ky+2
+            float S0[3][3], S1[3][3];
 #pragma unroll
-            for (int r = 0; r < 5; ++r)
+            for (int ky = -1; ky <= 1; ++ky)
 #pragma unroll
-                for (int k = 0; k < 3; ++k) Hl[r][k] = lerp_c(V[r][k + px], V[r][k + 1 + px], wx);
-#pragma unroll
-            for (int py = 0; py < 2; ++py) {
-                const float wy = py ? 0.25f : 0.75f;
-                auto S = [&](int kx, int ky) { return lerp_c(Hl[ky + 1 + py][kx + 1], Hl[ky + 2 + py][kx + 1], wy); };
-                out[py][px][C] = up9(S(-1, 1), S(0, 1), S(1, 1), S(-1, 0), S(0, 0), S(1, 0), S(-1, -1), S(0, -1), S(1, -1));
-            }
+                for (int kx = -1; kx <= 1; ++kx) {
+                    const float p = v_prod(Hl[ky + 2][kx + 1]);
+                    S0[ky + 1][kx + 1] = __builtin_fmaf(Hl[ky + 1][kx + 1], 0.0625f, p);
+                    S1[ky + 1][kx + 1] = __builtin_fmaf(Hl[ky + 3][kx + 1], 0.0625f, p);
+                }
+            out[0][px][C] = up9(S0[2][0], S0[2][1], S0[2][2], S0[1][0], S0[1][1], S0[1][2], S0[0][0], S0[0][1], S0[0][2]);
+            out[1][px][C] = up9(S1[2][0], S1[2][1], S1[2][2], S1[1][0], S1[1][1], S1[1][2], S1[0][0], S1[0][1], S1[0][2]);
         }
+        __builtin_amdgcn_sched_barrier(0);   // one channel's window live at a time
     };
     run(std::integral_constant<int, 0>{});
     run(std::integral_constant<int, 1>{});

@@ -116,5 +116,34 @@ __device__ __forceinline__ void store_quad_row(const DImg& im, int X0, int y, co
     if (X0 + 1 < im.w) store_rgb1_c(im, X0 + 1, y, o[1][0], o[1][1], o[1][2]);
 }
 
+// Exact re-associations of lerp_c for the fixed weights of the register-window and fused kernels (no overflow or
+// denormals occur for RGBA16F-origin data):
+//  * w = 1/2: a*0.5 + b*0.5 == (a + b) * 0.5, both products being exact.
+//  * w = 3/4 (1/4) on RGBA16F texels: a*0.25 + b*0.75 == (a + 3b) * 0.25, since 3b is exact for an
+//    11-bit significand; half4_* return the unscaled a + 3b ("t", four times the lerp).
+//  * vertical w = 3/4 (1/4) on two such t: h0*0.25 + round(h1*0.75) with h = t/4, i.e.
+//    fma(t0, 1/16, round(t1 * 3/16)): the same two roundings as lerp_c.
+__device__ __forceinline__ float mid(float a, float b) {
+#pragma clang fp contract(off)
+    return (a + b) * 0.5f;
+}
+__device__ __forceinline__ float t_w34(float a, float b) { return __builtin_fmaf(b, 3.0f, a); }   // 4*lerp(a,b,3/4)
+__device__ __forceinline__ float t_w14(float a, float b) { return __builtin_fmaf(a, 3.0f, b); }   // 4*lerp(a,b,1/4)
+__device__ __forceinline__ float v_w34(float t0, float t1) {
+#pragma clang fp contract(off)
+    const float p = t1 * 0.1875f;
+    return __builtin_fmaf(t0, 0.0625f, p);
+}
+// The rounded product t * 3/16 shared by v_w34 (as t1) and v_w14 (as t0).
+__device__ __forceinline__ float v_prod(float t) {
+#pragma clang fp contract(off)
+    return t * 0.1875f;
+}
+__device__ __forceinline__ float v_w14(float t0, float t1) {
+#pragma clang fp contract(off)
+    const float p = t0 * 0.1875f;
+    return __builtin_fmaf(t1, 0.0625f, p);
+}
+
 }  // namespace
 }  // namespace soc
