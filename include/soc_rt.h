@@ -286,6 +286,17 @@ int soc_temporal_antialiasing(const soc_globals* g, soc_img target, soc_img curr
                               soc_img previous_color, soc_img current_velocity, soc_img previous_velocity,
                               soc_img depth, soc_img velocity_history_out, soc_stream stream);
 
+/* TemporalAntiAliasingTask followed by ToneMappingTask (renderer.cpp:1170-1217) in one launch when
+ * `output` is RGBA8_UNORM at the target extent and the TAA pair path applies: the resolved RGBA16F
+ * pixels are tone-mapped as stored (same AgX device code as soc_tone_mapping), saving the re-read of
+ * `target`. Otherwise the two passes run back to back. Results equal soc_temporal_antialiasing +
+ * soc_tone_mapping. */
+int soc_temporal_antialiasing_tone_mapping(const soc_globals* g, soc_img target, soc_img current_color,
+                                           soc_img previous_color, soc_img current_velocity,
+                                           soc_img previous_velocity, soc_img depth, soc_img velocity_history_out,
+                                           const soc_auto_exposure* d_auto_exposure, soc_img output,
+                                           soc_stream stream);
+
 /* CopyImageTask (temporal_antialiasing.inl:16-37): same-format, same-extent image copy. */
 int soc_copy_image(soc_img target, soc_img source, soc_stream stream);
 
@@ -330,6 +341,8 @@ typedef struct soc_renderer soc_renderer;
 /* flags */
 #define SOC_RENDERER_TIMING 1      /* record hipEvents around every pass (GPUMetric, gpu_metric.cpp:18-42) */
 #define SOC_RENDERER_UNFUSED_BLOOM 2  /* bloom downsweep as the reference's 4 passes, not 2 fused stages */
+#define SOC_RENDERER_SERIAL 4      /* every pass on the caller's stream (no concurrent sky lane) */
+#define SOC_RENDERER_UNFUSED_TONEMAP 8  /* TAA and tone mapping as two passes (default: one launch for RGBA8) */
 
 soc_renderer* soc_renderer_create(const soc_frame_images* images, uint32_t flags);
 void soc_renderer_destroy(soc_renderer* r);
@@ -353,6 +366,10 @@ int soc_renderer_reset_timing(soc_renderer* r);
 int soc_renderer_pass_stats(soc_renderer* r, int32_t index, float* total_ms, int32_t* frames);
 /* Index (0/1) of the history_color slot holding this frame's TAA result (= tone-map input). */
 int32_t soc_renderer_current_history(const soc_renderer* r);
+/* Sky lane on/off (default on unless SOC_RENDERER_SERIAL). On: CloudRendering runs on a renderer-owned
+ * stream of the current device, forked from `stream` at the start of the PRE phase and joined before
+ * Composition, so it overlaps bloom and SSAO. Results are identical either way. */
+int soc_renderer_set_async(soc_renderer* r, int32_t enable);
 
 #ifdef __cplusplus
 }

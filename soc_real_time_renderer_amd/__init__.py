@@ -217,6 +217,16 @@ def temporal_antialiasing(g, target, current_color, previous_color, current_velo
                                            img(velocity_history_out), _stream(stream)), "temporal_antialiasing")
 
 
+def temporal_antialiasing_tone_mapping(g, target, current_color, previous_color, current_velocity, previous_velocity,
+                                       depth, auto_exposure, output, velocity_history_out=None, output_format=None,
+                                       stream=None):
+    """TAA followed by AgX tone mapping into `output` (one launch for an RGBA8_UNORM output)."""
+    _check(lib().soc_temporal_antialiasing_tone_mapping(
+        _gp(g), img(target), img(current_color), img(previous_color), img(current_velocity), img(previous_velocity),
+        img(depth), img(velocity_history_out), _ptr(auto_exposure), img(output, output_format), _stream(stream)),
+        "temporal_antialiasing_tone_mapping")
+
+
 def copy_image(target, source, stream=None):
     _check(lib().soc_copy_image(img(target), img(source), _stream(stream)), "copy_image")
 
@@ -275,7 +285,8 @@ def alloc_frame(width: int, height: int, device="cuda", output_format=FMT_RGBA8_
 class Renderer:
     """Host render graph (C++ soc_renderer): the live passes of Renderer::rebuild_task_graph in order."""
 
-    def __init__(self, frame: dict, timing: bool = False, stream=None, fused_bloom: bool = True):
+    def __init__(self, frame: dict, timing: bool = False, stream=None, fused_bloom: bool = True, sky_lane: bool = True,
+                 fused_tonemap: bool = True):
         self.frame = frame
         fi = FrameImages()
         for k in ("albedo", "emissive", "normal", "depth", "velocity", "shadow", "noise", "ssao", "ssao_blur", "clouds",
@@ -293,7 +304,8 @@ class Renderer:
         fi.bloom_output = img(frame.get("bloom_output"))
         fi.clouds_workspace = _ptr(frame.get("clouds_workspace"))
         self._fi = fi
-        flags = (_abi.RENDERER_TIMING if timing else 0) | (0 if fused_bloom else _abi.RENDERER_UNFUSED_BLOOM)
+        flags = ((_abi.RENDERER_TIMING if timing else 0) | (0 if fused_bloom else _abi.RENDERER_UNFUSED_BLOOM)
+                 | (0 if sky_lane else _abi.RENDERER_SERIAL) | (0 if fused_tonemap else _abi.RENDERER_UNFUSED_TONEMAP))
         h = lib().soc_renderer_create(C.byref(fi), flags)
         if not h:
             raise SocError(-1, lib().soc_last_error_string().decode())
@@ -334,6 +346,10 @@ class Renderer:
             _check(lib().soc_renderer_pass_stats(self.handle, i, C.byref(tot), C.byref(cnt)), "soc_renderer_pass_stats")
             out.append((n, gname, (tot.value / cnt.value) if cnt.value else float("nan"), cnt.value))
         return out
+
+    def set_async(self, enable: bool) -> None:
+        """Sky lane: CloudRendering on a concurrent renderer-owned stream (identical results)."""
+        _check(lib().soc_renderer_set_async(self.handle, int(bool(enable))), "soc_renderer_set_async")
 
     def current_history(self) -> int:
         return int(lib().soc_renderer_current_history(self.handle))

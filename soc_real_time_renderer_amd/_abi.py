@@ -33,6 +33,8 @@ PHASE_POST_EXPOSURE = 2
 PHASE_ALL = 3
 RENDERER_TIMING = 1
 RENDERER_UNFUSED_BLOOM = 2
+RENDERER_SERIAL = 4
+RENDERER_UNFUSED_TONEMAP = 8
 
 Mat4 = C.c_float * 16
 Vec2 = C.c_float * 2
@@ -145,6 +147,7 @@ FUNCTIONS = {
     "soc_composition": (_I, [_G, _P, _IMG, _IMG, _IMG, _IMG, _IMG, _IMG, _IMG, _IMG, _P]),
     "soc_generate_luminance_histogram": (_I, [_G, _IMG, _P, _P]),
     "soc_resolve_luminance_histogram": (_I, [_G, _P, C.c_uint64, C.c_int32, _P]),
+    "soc_temporal_antialiasing_tone_mapping": (_I, [_G, _IMG, _IMG, _IMG, _IMG, _IMG, _IMG, _IMG, _P, _IMG, _P]),
     "soc_temporal_antialiasing": (_I, [_G, _IMG, _IMG, _IMG, _IMG, _IMG, _IMG, _IMG, _P]),
     "soc_copy_image": (_I, [_IMG, _IMG, _P]),
     "soc_tone_mapping": (_I, [_G, _IMG, _P, _IMG, _P]),
@@ -158,6 +161,7 @@ FUNCTIONS = {
     "soc_renderer_pass_group": (C.c_char_p, [_P, C.c_int32]),
     "soc_renderer_pass_ms": (C.c_float, [_P, C.c_int32]),
     "soc_renderer_current_history": (C.c_int32, [_P]),
+    "soc_renderer_set_async": (C.c_int, [_P, C.c_int32]),
     "soc_renderer_set_pass_timing": (_I, [_P, C.c_int32, C.c_int32]),
     "soc_renderer_reset_timing": (_I, [_P]),
     "soc_renderer_pass_stats": (_I, [_P, C.c_int32, C.POINTER(C.c_float), C.POINTER(C.c_int32)]),

@@ -8,6 +8,7 @@
 
 #include <cmath>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <functional>
@@ -39,6 +40,11 @@ int check_img(const soc_img& im, int fmt, const char* pass, const char* what) {
     if (fmt > 0 && im.format != fmt)
         return set_error(SOC_E_INVALID_ARG, "%s: %s image has format %d, expected %d", pass, what, im.format, fmt);
     return SOC_OK;
+}
+
+int tuning_knob(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return e ? atoi(e) : dflt;
 }
 
 int check_launch(const char* pass) {
@@ -454,6 +460,8 @@ struct soc_renderer {
         std::string name, group;
         int phase;
         std::function<int(const soc_globals*, hipStream_t)> run;
+        int lane = 0;        // 1 = the sky lane: runs on the renderer's side stream, concurrently with lane 0
+        bool join = false;   // lane-0 pass that consumes the sky lane's output (waits on its join event)
         bool timed = false;
         std::vector<hipEvent_t> ev0, ev1;  // ring of SOC_RENDERER_TIMING_RING frames
         int next = 0, count = 0, last = -1;
@@ -468,6 +476,13 @@ struct soc_renderer {
     soc_globals* staging = nullptr;
     hipEvent_t staging_ev[4] = {nullptr, nullptr, nullptr, nullptr};
     int staging_slot = 0;
+    // sky lane: CloudRendering is VALU-bound and depends on depth only, so it overlaps the memory-bound
+    // bloom / SSAO passes on a second stream (fork at the frame start, join before Composition) -- the
+    // HIP counterpart of the async-compute queue the reference leaves unused (renderer.cpp:1094-1117)
+    bool async = true;
+    int side_device = -1;
+    hipStream_t side = nullptr;
+    hipEvent_t fork_ev = nullptr, join_ev = nullptr;
 };
 
 namespace {
@@ -522,6 +537,7 @@ void build_passes(soc_renderer* r) {
     add("CloudRendering", "Sky Rendering", SOC_PHASE_PRE_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
         return soc_cloud_rendering(g, r->img.depth, r->img.noise, r->img.clouds, r->img.clouds_workspace, (soc_stream)s);
     });
+    r->passes.back().lane = 1;
     // renderer.cpp:1103-1117
     add("Composition", "Composition", SOC_PHASE_PRE_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
         const auto& I = r->img;
@@ -529,6 +545,7 @@ void build_passes(soc_renderer* r) {
         return soc_composition(g, I.d_globals, I.color, I.albedo, em, I.normal, I.depth, I.ssao_blur, I.shadow, I.clouds,
                                (soc_stream)s);
     });
+    r->passes.back().join = true;
     // renderer.cpp:1155-1168
     add("GenerateLuminanceHistogram", "Auto Exposure", SOC_PHASE_PRE_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
         return soc_generate_luminance_histogram(g, r->img.color, r->img.auto_exposure, (soc_stream)s);
@@ -536,18 +553,30 @@ void build_passes(soc_renderer* r) {
     add("ResolveLuminanceHistogram", "Auto Exposure", SOC_PHASE_POST_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
         return soc_resolve_luminance_histogram(g, r->img.auto_exposure, r->total_pixels, r->wide, (soc_stream)s);
     });
-    // renderer.cpp:1170-1198: TAA + both history copies (ping-pong + fused velocity history)
-    add("TemporalAntiAliasing", "Temporal Anti-Aliasing", SOC_PHASE_POST_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
-        const auto& I = r->img;
-        const int p = r->hist, q = 1 - r->hist;
-        return soc_temporal_antialiasing(g, I.history_color[q], I.color, I.history_color[p], I.velocity, I.history_velocity[p],
-                                         I.depth, I.history_velocity[q], (soc_stream)s);
-    });
-    // renderer.cpp:1210-1217
-    add("ToneMapping", "Tone Mapping", SOC_PHASE_POST_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
-        const auto& I = r->img;
-        return soc_tone_mapping(g, I.history_color[1 - r->hist], I.auto_exposure, I.output, (soc_stream)s);
-    });
+    // renderer.cpp:1170-1198: TAA + both history copies (ping-pong + fused velocity history), and
+    // renderer.cpp:1210-1217: tone mapping, fused into the TAA launch for an RGBA8_UNORM framebuffer
+    const bool fuse_tm = !(r->flags & SOC_RENDERER_UNFUSED_TONEMAP) && I.output.format == SOC_FMT_RGBA8_UNORM;
+    if (fuse_tm) {
+        add("TemporalAntiAliasing+ToneMapping", "Temporal Anti-Aliasing", SOC_PHASE_POST_EXPOSURE,
+            [r](const soc_globals* g, hipStream_t s) {
+                const auto& I = r->img;
+                const int p = r->hist, q = 1 - r->hist;
+                return soc_temporal_antialiasing_tone_mapping(g, I.history_color[q], I.color, I.history_color[p], I.velocity,
+                                                              I.history_velocity[p], I.depth, I.history_velocity[q],
+                                                              I.auto_exposure, I.output, (soc_stream)s);
+            });
+    } else {
+        add("TemporalAntiAliasing", "Temporal Anti-Aliasing", SOC_PHASE_POST_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
+            const auto& I = r->img;
+            const int p = r->hist, q = 1 - r->hist;
+            return soc_temporal_antialiasing(g, I.history_color[q], I.color, I.history_color[p], I.velocity,
+                                             I.history_velocity[p], I.depth, I.history_velocity[q], (soc_stream)s);
+        });
+        add("ToneMapping", "Tone Mapping", SOC_PHASE_POST_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
+            const auto& I = r->img;
+            return soc_tone_mapping(g, I.history_color[1 - r->hist], I.auto_exposure, I.output, (soc_stream)s);
+        });
+    }
     (void)I;
 }
 }  // namespace
@@ -564,6 +593,7 @@ extern "C" soc_renderer* soc_renderer_create(const soc_frame_images* images, uin
     soc_renderer* r = new soc_renderer();
     r->img = *images;
     r->flags = flags;
+    r->async = !(flags & SOC_RENDERER_SERIAL);
     build_passes(r);
     if ((flags & SOC_RENDERER_TIMING) && soc_renderer_set_pass_timing(r, -1, 1) != SOC_OK) {
         soc_renderer_destroy(r);
@@ -581,6 +611,9 @@ extern "C" void soc_renderer_destroy(soc_renderer* r) {
     for (auto& e : r->staging_ev)
         if (e) (void)hipEventDestroy(e);
     if (r->staging) (void)hipHostFree(r->staging);
+    if (r->fork_ev) (void)hipEventDestroy(r->fork_ev);
+    if (r->join_ev) (void)hipEventDestroy(r->join_ev);
+    if (r->side) (void)hipStreamDestroy(r->side);
     delete r;
 }
 
@@ -603,6 +636,41 @@ static int upload_lights(soc_renderer* r, const soc_globals* g, hipStream_t s) {
     return SOC_OK;
 }
 
+static int run_pass(soc_renderer::Pass& p, const soc_globals* g, hipStream_t s) {
+    const int slot = p.next;
+    if (p.timed) (void)hipEventRecord(p.ev0[slot], s);
+    int rc = p.run(g, s);
+    if (rc) return rc;
+    if (p.timed) {
+        (void)hipEventRecord(p.ev1[slot], s);
+        p.last = slot;
+        p.next = (slot + 1) % SOC_RENDERER_TIMING_RING;
+        if (p.count < SOC_RENDERER_TIMING_RING) p.count++;
+    }
+    return SOC_OK;
+}
+
+static int ensure_side_lane(soc_renderer* r) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return set_error(SOC_E_HIP, "soc_renderer_execute: hipGetDevice failed");
+    if (r->side && r->side_device == dev) return SOC_OK;
+    if (r->side) {   // the caller moved to another device: rebuild the lane there
+        (void)hipStreamDestroy(r->side);
+        (void)hipEventDestroy(r->fork_ev);
+        (void)hipEventDestroy(r->join_ev);
+        r->side = nullptr;
+        r->fork_ev = r->join_ev = nullptr;
+    }
+    const char* pe = getenv("SOC_SKY_PRIORITY");   // tuning knob: HIP stream priority of the sky lane
+    if ((pe ? hipStreamCreateWithPriority(&r->side, hipStreamNonBlocking, atoi(pe))
+            : hipStreamCreateWithFlags(&r->side, hipStreamNonBlocking)) != hipSuccess ||
+        hipEventCreateWithFlags(&r->fork_ev, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&r->join_ev, hipEventDisableTiming) != hipSuccess)
+        return set_error(SOC_E_HIP, "soc_renderer_execute: sky lane stream/event creation failed");
+    r->side_device = dev;
+    return SOC_OK;
+}
+
 extern "C" int soc_renderer_execute(soc_renderer* r, const soc_globals* g, int32_t phase, soc_stream stream) {
     if (!r || !g) return set_error(SOC_E_INVALID_ARG, "soc_renderer_execute: null argument");
     hipStream_t s = hs(stream);
@@ -610,20 +678,43 @@ extern "C" int soc_renderer_execute(soc_renderer* r, const soc_globals* g, int32
         int rc = upload_lights(r, g, s);
         if (rc) return rc;
     }
+    // lane-1 passes run on the side stream, ordered after everything already on `s` (fork) and
+    // before the first lane-0 pass marked `join`; every pass still reads and writes the same images
+    const bool lanes = r->async && (phase & SOC_PHASE_PRE_EXPOSURE);
+    if (lanes) {
+        int rc = ensure_side_lane(r);
+        if (rc) return rc;
+        if (hipEventRecord(r->fork_ev, s) != hipSuccess || hipStreamWaitEvent(r->side, r->fork_ev, 0) != hipSuccess)
+            return set_error(SOC_E_HIP, "soc_renderer_execute: sky lane fork failed");
+        for (auto& p : r->passes) {
+            if (p.lane != 1 || !(p.phase & phase)) continue;
+            rc = run_pass(p, g, r->side);
+            if (rc) return rc;
+        }
+        if (hipEventRecord(r->join_ev, r->side) != hipSuccess)
+            return set_error(SOC_E_HIP, "soc_renderer_execute: sky lane join failed");
+    }
+    bool joined = !lanes;
     for (auto& p : r->passes) {
         if (!(p.phase & phase)) continue;
-        const int slot = p.next;
-        if (p.timed) (void)hipEventRecord(p.ev0[slot], s);
-        int rc = p.run(g, s);
-        if (rc) return rc;
-        if (p.timed) {
-            (void)hipEventRecord(p.ev1[slot], s);
-            p.last = slot;
-            p.next = (slot + 1) % SOC_RENDERER_TIMING_RING;
-            if (p.count < SOC_RENDERER_TIMING_RING) p.count++;
+        if (lanes && p.lane == 1) continue;
+        if (p.join && !joined) {
+            if (hipStreamWaitEvent(s, r->join_ev, 0) != hipSuccess)
+                return set_error(SOC_E_HIP, "soc_renderer_execute: sky lane join failed");
+            joined = true;
         }
+        int rc = run_pass(p, g, s);
+        if (rc) return rc;
     }
+    if (!joined && hipStreamWaitEvent(s, r->join_ev, 0) != hipSuccess)   // no consumer this phase: still join
+        return set_error(SOC_E_HIP, "soc_renderer_execute: sky lane join failed");
     if (phase & SOC_PHASE_POST_EXPOSURE) r->hist = 1 - r->hist;   // ping-pong the TAA history
+    return SOC_OK;
+}
+
+extern "C" int soc_renderer_set_async(soc_renderer* r, int32_t enable) {
+    if (!r) return set_error(SOC_E_INVALID_ARG, "soc_renderer_set_async: null renderer");
+    r->async = enable != 0;
     return SOC_OK;
 }
 

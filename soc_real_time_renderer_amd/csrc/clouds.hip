@@ -7,6 +7,8 @@
 // sky masks are wave-coherent); a tile with no sky pixel exits after its depth test. Tiles with sky
 // stage the 64x64 noise texture into LDS as packed 2x2 quads (one ds_read_b32 returns the four texels
 // of a bilinear REPEAT tap), 16 KiB per workgroup.
+#include <cstdlib>
+
 #include "soc_internal.hpp"
 
 // Profiling builds only (tools/kernel_variants.py): 1 = atmosphere only, 2 = cloud march only,
@@ -762,10 +764,13 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
     // balanced over all SIMDs instead of running as a second, partially filled round.
     static int res_atmos = 0, res_density = 0, res_sunvis = 0, res_resolve = 0;
     if (!res_atmos) {
-        res_atmos = resident_blocks(clouds_atmosphere);
-        res_density = resident_blocks(clouds_density<false>);
-        res_sunvis = resident_blocks(clouds_sunvis<false>);
-        res_resolve = resident_blocks(clouds_resolve<false>);
+        const char* ev = getenv("SOC_SKY_SHARE");   // tuning knob: fraction of the resident wave set
+        const double share = ev ? atof(ev) : 1.0;
+        auto scaled = [&](int res) { return std::max(1, (int)(res * share)); };
+        res_atmos = scaled(resident_blocks(clouds_atmosphere));
+        res_density = scaled(resident_blocks(clouds_density<false>));
+        res_sunvis = scaled(resident_blocks(clouds_sunvis<false>));
+        res_resolve = scaled(resident_blocks(clouds_resolve<false>));
     }
     const long long blocks = ((long long)W * H + 255) / 256;
     if (SOC_CLOUDS_PROFILE >= 4) return check_launch("cloud_rendering");

@@ -25,6 +25,7 @@ struct CompParams {
     float sun_dir[3], ambient[3], cam[3];
     float ef, df, emissive_strength, ao_strength;
     uint32_t npl, nsl;
+    int swz;   // XCD-aware tile order (fast path)
     const soc_globals* __restrict__ dg;  // device globals (lights), may be null when npl == nsl == 0
 };
 
@@ -115,8 +116,10 @@ __global__ __launch_bounds__(256) void composition_pair(DImg target, DImg albedo
     // 128-B line of each G-buffer image, and the wave's shadow-map taps form a compact 2D patch
     // (a 128x1 strip maps to a line across the 4096^2 map and touches a new line per tap)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int x = blockIdx.x * 32 + (wave & 1) * 16 + (lane & 7) * 2;
-    const int y = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    int bx, by;
+    xcd_tile(p.swz, bx, by);
+    const int x = bx * 32 + (wave & 1) * 16 + (lane & 7) * 2;
+    const int y = by * 16 + (wave >> 1) * 8 + (lane >> 3);
     if (x >= target.w || y >= target.h) return;
     const float v = centre_uv(y, target.h);
     const float2 d2 = row_ptr<float2>(depth, y)[x >> 1];
@@ -207,6 +210,7 @@ extern "C" int soc_composition(const soc_globals* g, const soc_globals* d_global
     p.npl = g->point_light_count < SOC_MAX_POINT_LIGHTS ? g->point_light_count : SOC_MAX_POINT_LIGHTS;
     p.nsl = g->spot_light_count < SOC_MAX_SPOT_LIGHTS ? g->spot_light_count : SOC_MAX_SPOT_LIGHTS;
     p.dg = d_globals;
+    p.swz = tuning_knob("SOC_SWZ_COMP", 0);
     if ((p.npl || p.nsl) && !d_globals)
         return set_error(SOC_E_INVALID_ARG, "%s: frame has lights but no device globals (soc_upload_globals)", P);
 

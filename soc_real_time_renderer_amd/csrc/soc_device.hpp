@@ -167,6 +167,21 @@ __device__ __forceinline__ f3 mul(const Mat3& M, f3 v) {
     return f3{m[0] * v.x + m[3] * v.y + m[6] * v.z, m[1] * v.x + m[4] * v.y + m[7] * v.z, m[2] * v.x + m[5] * v.y + m[8] * v.z};
 }
 
+// XCD-aware tile order for a 2D grid. Workgroups are dispatched round-robin over the 8 XCDs by linear
+// block id (id % 8); with swz != 0, XCD k's blocks take the contiguous row-major tile range
+// [k n/8, (k+1) n/8), so neighbouring tiles whose halos / gather footprints overlap share one XCD's
+// 4 MiB L2 instead of being spread over all eight. Placement only: every tile is still visited once.
+__device__ __forceinline__ void xcd_tile(int swz, int& tx, int& ty) {
+    const int gx = (int)gridDim.x, n = (int)(gridDim.x * gridDim.y);
+    int id = (int)(blockIdx.y * gridDim.x + blockIdx.x);
+    if (swz) {
+        const int q = n >> 3, r = n & 7, k = id & 7;
+        id = k * q + min(k, r) + (id >> 3);
+    }
+    ty = id / gx;
+    tx = id - ty * gx;
+}
+
 // Pixel-centre uv exactly as the oracle computes it: (x + 0.5) / n, correctly rounded.
 __device__ __forceinline__ float centre_uv(int x, int n) { return ((float)x + 0.5f) / (float)n; }
 

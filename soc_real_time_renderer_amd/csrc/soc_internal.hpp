@@ -47,6 +47,9 @@ inline Mat4 mat4(const float* m) {
 
 inline hipStream_t hs(soc_stream s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Integer tuning knob from the environment (read once per name; `dflt` when unset).
+int tuning_knob(const char* name, int dflt);
+
 // Checks the launch that was just issued.
 int check_launch(const char* pass);
 

@@ -19,6 +19,7 @@ struct SsaoParams {
     float radius, bias, kernel_size_f;
     int ksize;     // loop bound, min(kernel_size, 26)
     int noise_w;   // textureSize(u_normal_image).x
+    int swz;       // XCD-aware tile order
 };
 
 // ssao_generation.inl:139-141 (no FMA contraction: keeps the sin argument as the oracle's)
@@ -99,7 +100,9 @@ __device__ __forceinline__ float aff(const Aff& a, float kx, float ky, float kz)
 template <bool TABLE, bool SPARSE_IP, bool FULL>
 __global__ __launch_bounds__(256) void ssao_kernel(DImg depth, DImg normal, DImg target, const float2* __restrict__ table,
                                                    SsaoParams p) {
-    const int x = blockIdx.x * 16 + threadIdx.x, y = blockIdx.y * 16 + threadIdx.y;
+    int bx, by;
+    xcd_tile(p.swz, bx, by);
+    const int x = bx * 16 + threadIdx.x, y = by * 16 + threadIdx.y;
     if (x >= target.w || y >= target.h) return;
     const float u = centre_uv(x, target.w), v = centre_uv(y, target.h);
 
@@ -210,6 +213,7 @@ SsaoParams make_params(const soc_globals* g, const soc_img& normal) {
     p.kernel_size_f = (float)g->ssao_kernel_size;
     p.ksize = g->ssao_kernel_size < SOC_SSAO_MAX_KERNEL ? g->ssao_kernel_size : SOC_SSAO_MAX_KERNEL;
     p.noise_w = normal.width;
+    p.swz = tuning_knob("SOC_SWZ_SSAO", 0);
     return p;
 }
 

@@ -6,6 +6,7 @@
 // reference graph (renderer.cpp:1182-1198) are removed: the resolved colour ping-pongs between two
 // images owned by the caller, and the current velocity is written to the next frame's velocity
 // history from inside this kernel (velocity_history_out), which saves the separate 16 B/px copy.
+#include "agx.hpp"
 #include "soc_internal.hpp"
 
 namespace soc {
@@ -14,6 +15,7 @@ namespace {
 struct TaaParams {
     float pox, poy;     // 1 / resolution
     float accum0;       // min(0.1, frame_counter)
+    int swz;            // XCD-aware tile order (pair path)
 };
 
 constexpr int BX = 64, BY = 4;
@@ -206,10 +208,22 @@ __device__ __forceinline__ void sample_pair_rows(const DImg& im, float u, float 
 // packed f16 (exact), column-wise and shared by the two pixels; the 3x3 Gaussian is evaluated as
 // column sums (separable weights, different rounding order); the closest-depth texel is chosen with
 // the reference's iteration order and tie rule, exactly.
+// Fused ToneMappingTask (tone_mapping.inl:145-176) epilogue: the resolved RGBA16F pair, exactly as it
+// is stored, goes through the same AgX device function as tonemap_pair into an RGBA8_UNORM image.
+struct TmOut {
+    DImg out;
+    const soc_auto_exposure* ae;
+    TmParams p;
+};
+
+template <bool TM>
 __global__ __launch_bounds__(256) void taa_pair2(DImg target, DImg cur, DImg prev, DImg vel, DImg pvel, DImg depth,
-                                                 DImg vel_out, TaaParams p) {
-    const int x0 = (blockIdx.x * BX + threadIdx.x) * 2, y = blockIdx.y * BY + threadIdx.y;
+                                                 DImg vel_out, TaaParams p, TmOut tm) {
+    int tbx, tby;
+    xcd_tile(p.swz, tbx, tby);
+    const int x0 = (tbx * BX + threadIdx.x) * 2, y = tby * BY + threadIdx.y;
     if (x0 >= target.w || y >= target.h) return;
+    const float exposure = TM ? tm.ae->exposure : 0.0f;
     const int W = target.w, H = target.h;
     const int xl = max(x0 - 1, 0), xr = min(x0 + 2, W - 1);
     // slots c = 0..3: columns xl, x0, x0+1, xr; rows r = 0..2: y+1, y, y-1 (clamped)
@@ -304,6 +318,13 @@ __global__ __launch_bounds__(256) void taa_pair2(DImg target, DImg cur, DImg pre
     }
     row_ptr_w<uint4>(target, y)[x0 >> 1] = uint4{outp[0].x, outp[0].y, outp[1].x, outp[1].y};
     if (vel_out.data) row_ptr_w<uint4>(vel_out, y)[x0 >> 1] = row_ptr<uint4>(vel, y)[x0 >> 1];
+    if (TM) {
+        const float expo = exp2f(exposure);   // pow(2.0, exposure)
+        const f3 c0 = agx(tm.p, unpack_h4(outp[0]), expo);
+        const f3 c1 = agx(tm.p, unpack_h4(outp[1]), expo);
+        row_ptr_w<uint2>(tm.out, y)[x0 >> 1] =
+            uint2{pack_unorm8x4(f4{c0.x, c0.y, c0.z, 1.0f}), pack_unorm8x4(f4{c1.x, c1.y, c1.z, 1.0f})};
+    }
 }
 
 __global__ __launch_bounds__(256) void taa_generic(DImg target, DImg cur, DImg prev, DImg vel, DImg pvel, DImg depth,
@@ -353,9 +374,11 @@ __global__ __launch_bounds__(256) void copy_rows(const char* __restrict__ src, i
 
 using namespace soc;
 
-extern "C" int soc_temporal_antialiasing(const soc_globals* g, soc_img target, soc_img current_color, soc_img previous_color,
-                                         soc_img current_velocity, soc_img previous_velocity, soc_img depth,
-                                         soc_img velocity_history_out, soc_stream stream) {
+namespace {
+// tm != nullptr: launch the fused TAA + tone-map kernel if the pair path applies (returns 1 otherwise,
+// having launched nothing)
+int taa_launch(const soc_globals* g, soc_img target, soc_img current_color, soc_img previous_color, soc_img current_velocity,
+               soc_img previous_velocity, soc_img depth, soc_img velocity_history_out, const TmOut* tm, soc_stream stream) {
     static const char* P = "soc_temporal_antialiasing";
     if (!g) return set_error(SOC_E_INVALID_ARG, "%s: null globals", P);
     int rc = check_img(target, SOC_FMT_RGBA16F, P, "target");
@@ -379,6 +402,7 @@ extern "C" int soc_temporal_antialiasing(const soc_globals* g, soc_img target, s
     p.pox = 1.0f / (float)g->resolution[0];
     p.poy = 1.0f / (float)g->resolution[1];
     p.accum0 = fminf(0.1f, (float)g->frame_counter);
+    p.swz = tuning_knob("SOC_SWZ_TAA", 0);
     const int W = target.width, H = target.height;
     auto same = [&](const soc_img& im) { return im.width == W && im.height == H; };
     const bool fast = W == g->resolution[0] && H == g->resolution[1] && same(current_color) && same(depth) &&
@@ -390,10 +414,16 @@ extern "C" int soc_temporal_antialiasing(const soc_globals* g, soc_img target, s
                       (reinterpret_cast<uintptr_t>(depth.data) & 7u) == 0 && (depth.pitch_bytes & 7) == 0 &&
                       (!velocity_history_out.data || a16(velocity_history_out)) && previous_color.width >= 2 &&
                       previous_velocity.width >= 2;
+    if (tm && !pair) return 1;
     if (pair) {
         dim3 g2(ceil_div(W / 2, BX), ceil_div(H, BY));
-        taa_pair2<<<g2, blk, 0, hs(stream)>>>(dimg(target), dimg(current_color), dimg(previous_color), dimg(current_velocity),
-                                             dimg(previous_velocity), dimg(depth), vo, p);
+        if (tm)
+            taa_pair2<true><<<g2, blk, 0, hs(stream)>>>(dimg(target), dimg(current_color), dimg(previous_color),
+                                                       dimg(current_velocity), dimg(previous_velocity), dimg(depth), vo, p, *tm);
+        else
+            taa_pair2<false><<<g2, blk, 0, hs(stream)>>>(dimg(target), dimg(current_color), dimg(previous_color),
+                                                        dimg(current_velocity), dimg(previous_velocity), dimg(depth), vo, p,
+                                                        TmOut{});
     } else if (fast)
         taa_fast<<<grd, blk, 0, hs(stream)>>>(dimg(target), dimg(current_color), dimg(previous_color), dimg(current_velocity),
                                               dimg(previous_velocity), dimg(depth), vo, p);
@@ -401,6 +431,46 @@ extern "C" int soc_temporal_antialiasing(const soc_globals* g, soc_img target, s
         taa_generic<<<grd, blk, 0, hs(stream)>>>(dimg(target), dimg(current_color), dimg(previous_color),
                                                  dimg(current_velocity), dimg(previous_velocity), dimg(depth), vo, p);
     return check_launch("temporal_antialiasing");
+}
+
+}  // namespace
+
+extern "C" int soc_temporal_antialiasing(const soc_globals* g, soc_img target, soc_img current_color, soc_img previous_color,
+                                         soc_img current_velocity, soc_img previous_velocity, soc_img depth,
+                                         soc_img velocity_history_out, soc_stream stream) {
+    return taa_launch(g, target, current_color, previous_color, current_velocity, previous_velocity, depth,
+                      velocity_history_out, nullptr, stream);
+}
+
+extern "C" int soc_temporal_antialiasing_tone_mapping(const soc_globals* g, soc_img target, soc_img current_color,
+                                                      soc_img previous_color, soc_img current_velocity,
+                                                      soc_img previous_velocity, soc_img depth, soc_img velocity_history_out,
+                                                      const soc_auto_exposure* d_auto_exposure, soc_img output,
+                                                      soc_stream stream) {
+    static const char* P = "soc_temporal_antialiasing_tone_mapping";
+    if (!g || !d_auto_exposure) return set_error(SOC_E_INVALID_ARG, "%s: null globals / auto exposure buffer", P);
+    int rc = check_img(output, 0, P, "output");
+    if (rc) return rc;
+    const bool fusable = output.format == SOC_FMT_RGBA8_UNORM && output.width == target.width &&
+                         output.height == target.height && (reinterpret_cast<uintptr_t>(output.data) & 7u) == 0 &&
+                         (output.pitch_bytes & 7) == 0 && output.data != target.data;
+    if (fusable) {
+        TmOut tm;
+        tm.out = dimg(output);
+        tm.ae = d_auto_exposure;
+        agx_matrices(g->compression, tm.p.M.m, tm.p.Minv.m);
+        tm.p.linear = g->agxDs_linear_section;
+        tm.p.peak = g->peak;
+        tm.p.saturation = g->saturation;
+        rc = taa_launch(g, target, current_color, previous_color, current_velocity, previous_velocity, depth,
+                        velocity_history_out, &tm, stream);
+        if (rc <= 0) return rc;   // launched (or failed validation)
+    }
+    // not fusable: the two passes back to back (same results)
+    rc = taa_launch(g, target, current_color, previous_color, current_velocity, previous_velocity, depth,
+                    velocity_history_out, nullptr, stream);
+    if (rc) return rc;
+    return soc_tone_mapping(g, target, d_auto_exposure, output, stream);
 }
 
 extern "C" int soc_copy_image(soc_img target, soc_img source, soc_stream stream) {

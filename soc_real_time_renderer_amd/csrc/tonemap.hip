@@ -5,34 +5,11 @@
 // on the host (soc::agx_matrices, the same fp32 arithmetic as the shader's PrimariesToMatrix /
 // ComputeCompressionMatrix / inverse) and passed as kernel arguments; 2^exposure is read from the
 // AutoExposure buffer. Two pixels per lane: one 16-B RGBA16F load, one 8-B RGBA8 store.
+#include "agx.hpp"
 #include "soc_internal.hpp"
 
 namespace soc {
 namespace {
-
-struct TmParams {
-    Mat3 M, Minv;
-    float linear, peak, saturation;
-};
-
-// DualSection, :127-137
-__device__ __forceinline__ float dual_section(float x, float linear, float peak) {
-    const float S = peak * linear;
-    if (x < S) return x;
-    const float C = peak / (peak - S);
-    return peak - (peak - S) * __expf((-C * (x - S)) / peak);
-}
-
-__device__ __forceinline__ f3 agx(const TmParams& p, f4 c, float expo) {
-    f3 w = f3{fmaxf(c.x, 0.0f), fmaxf(c.y, 0.0f), fmaxf(c.z, 0.0f)} * expo;
-    w = mul(p.M, w);
-    w = f3{clampf(dual_section(w.x, p.linear, p.peak), 0.0f, 1.0f), clampf(dual_section(w.y, p.linear, p.peak), 0.0f, 1.0f),
-           clampf(dual_section(w.z, p.linear, p.peak), 0.0f, 1.0f)};
-    const float ds = dot3(w, f3{0.2126729f, 0.7151522f, 0.0721750f});
-    w = f3{mixf(ds, w.x, p.saturation), mixf(ds, w.y, p.saturation), mixf(ds, w.z, p.saturation)};
-    w = f3{clampf(w.x, 0.0f, 1.0f), clampf(w.y, 0.0f, 1.0f), clampf(w.z, 0.0f, 1.0f)};
-    return mul(p.Minv, w);
-}
 
 __device__ __forceinline__ float srgb_encode(float c) {
     c = clampf(c, 0.0f, 1.0f);

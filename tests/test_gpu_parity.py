@@ -243,6 +243,30 @@ def test_taa(soc, oracle, W, H):
     assert np.array_equal(host(vout).view(np.uint16), gb["velocity"].view(np.uint16))
 
 
+@pytest.mark.parametrize("W,H", [(64, 36), (97, 55), (1920, 1080)])
+def test_taa_tone_mapping_fused_equals_two_passes(soc, W, H):
+    """The fused TAA + tone-map launch gives the TAA pass's bits and the tone-map pass's bits (97x55:
+    odd width, the two-pass fallback)."""
+    g, gb = sponza_inputs(W, H)
+    cur = dev(random_rgba16(H, W, seed=1, hi=3.0))
+    prev = dev(random_rgba16(H, W, seed=2, hi=3.0))
+    pvel = gb["velocity"].copy()
+    pvel[..., :2] += np.float16(0.0015)
+    vel, pvel, depth = dev(gb["velocity"]), dev(pvel), dev(gb["depth"])
+    ae = soc.auto_exposure_buffer(exposure=0.37)
+    t1 = torch.zeros(H, W, 4, dtype=torch.float16, device=DEV)
+    o1 = torch.zeros(H, W, 4, dtype=torch.uint8, device=DEV)
+    soc.temporal_antialiasing(g, t1, cur, prev, vel, pvel, depth)
+    soc.tone_mapping(g, t1, ae, o1)
+    t2, o2, v2 = torch.zeros_like(t1), torch.zeros_like(o1), torch.zeros_like(t1)
+    soc.temporal_antialiasing_tone_mapping(g, t2, cur, prev, vel, pvel, depth, ae, o2, velocity_history_out=v2)
+    torch.cuda.synchronize()
+    assert torch.equal(t1, t2)
+    assert torch.equal(v2, vel)
+    d = (o1.int() - o2.int()).abs()
+    assert int(d.max()) <= 1 and float((d > 0).float().mean()) < 1e-4
+
+
 # ------------------------------------------------------------------------------------------------ tone mapping
 @pytest.mark.parametrize("W,H", [(64, 36), (97, 55), (1920, 1080)])
 @pytest.mark.parametrize("fmt", ["RGBA8_UNORM", "RGBA32F", "RGBA8_SRGB"])
@@ -360,3 +384,27 @@ def test_4k_properties(soc):
     t = torch.zeros_like(c)
     soc.temporal_antialiasing(g, t, c, c.clone(), z, z.clone(), d)
     assert torch.all(t == 0.25)
+
+
+# ------------------------------------------------------------------------------------------------ sky lane
+def test_render_graph_sky_lane_bit_identical(soc):
+    """The concurrent sky lane (CloudRendering on a renderer-owned stream, joined before Composition)
+    changes scheduling only: 3 frames with and without it give bit-identical images."""
+    W, H = 1920, 1080
+    g, gb = sponza_inputs(W, H, elapsed=10.0)
+    outs = []
+    for lane in (True, False):
+        fr = soc.alloc_frame(W, H, DEV, bloom_output=True)
+        for k in ("albedo", "emissive", "normal", "velocity", "depth"):
+            fr[k].copy_(torch.from_numpy(gb[k]))
+        fr["shadow"] = dev(gb["shadow"])
+        fr["noise"].copy_(torch.from_numpy(gb["noise"]))
+        r = soc.Renderer(fr, sky_lane=lane)
+        for _ in range(3):
+            r.execute(g)
+        torch.cuda.synchronize()
+        outs.append({k: fr[k].clone() for k in ("clouds", "color", "output", "auto_exposure")})
+        outs[-1]["resolved"] = r.resolved().clone()
+        r.close()
+    for k in outs[0]:
+        assert torch.equal(outs[0][k], outs[1][k]), k
