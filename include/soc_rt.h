@@ -266,6 +266,18 @@ int soc_composition(const soc_globals* g, const soc_globals* d_globals, soc_img 
                     soc_img emissive, soc_img normal, soc_img depth, soc_img ssao, soc_img shadow,
                     soc_img clouds, soc_stream stream);
 
+/* CompositionTask followed by GenerateLuminanceHistogramTask (renderer.cpp:1103-1168) in one launch
+ * when the composition pair path applies at g->resolution: the bins of the stored RGBA16F pixels are
+ * accumulated while they are written (bit-identical bins, no re-read of `target`). Otherwise the two
+ * passes run back to back. The bins are ADDED to ae->histogram_buckets, as the histogram pass does.
+ * `scratch`: device, SOC_HISTOGRAM_SCRATCH_WORDS u32, zero-filled by the caller once; every call leaves
+ * it zeroed again (8 partial histograms, folded into the bins by a second small launch). */
+#define SOC_HISTOGRAM_SCRATCH_WORDS 2048
+int soc_composition_luminance_histogram(const soc_globals* g, const soc_globals* d_globals, soc_img target,
+                                        soc_img albedo, soc_img emissive, soc_img normal, soc_img depth,
+                                        soc_img ssao, soc_img shadow, soc_img clouds, soc_auto_exposure* d_auto_exposure,
+                                        uint32_t* scratch, soc_stream stream);
+
 /* GenerateLuminanceHistogramTask (generate_luminance_histogram.inl:23-47, shader :59-78): adds the
  * frame's 256-bin log-luminance histogram into d_auto_exposure->histogram_buckets. */
 int soc_generate_luminance_histogram(const soc_globals* g, soc_img hdr, soc_auto_exposure* d_auto_exposure,
@@ -343,6 +355,7 @@ typedef struct soc_renderer soc_renderer;
 #define SOC_RENDERER_UNFUSED_BLOOM 2  /* bloom downsweep as the reference's 4 passes, not 2 fused stages */
 #define SOC_RENDERER_SERIAL 4      /* every pass on the caller's stream (no concurrent sky lane) */
 #define SOC_RENDERER_UNFUSED_TONEMAP 8  /* TAA and tone mapping as two passes (default: one launch for RGBA8) */
+#define SOC_RENDERER_FUSED_HISTOGRAM 16  /* composition + luminance histogram in one launch */
 
 soc_renderer* soc_renderer_create(const soc_frame_images* images, uint32_t flags);
 void soc_renderer_destroy(soc_renderer* r);

@@ -200,6 +200,19 @@ def composition(g, target, albedo, emissive, normal, depth, ssao, shadow, clouds
                                  img(depth), img(ssao), img(shadow), img(clouds), _stream(stream)), "composition")
 
 
+def histogram_scratch(device="cuda") -> torch.Tensor:
+    """Zeroed scratch of soc_composition_luminance_histogram (SOC_HISTOGRAM_SCRATCH_WORDS u32)."""
+    return torch.zeros(_abi.HISTOGRAM_SCRATCH_WORDS, dtype=torch.int32, device=device)
+
+
+def composition_luminance_histogram(g, target, albedo, emissive, normal, depth, ssao, shadow, clouds, auto_exposure,
+                                    scratch, d_globals=None, stream=None):
+    """Composition + luminance histogram (bins added to auto_exposure's buckets; scratch left zeroed)."""
+    _check(lib().soc_composition_luminance_histogram(
+        _gp(g), _ptr(d_globals), img(target), img(albedo), img(emissive), img(normal), img(depth), img(ssao), img(shadow),
+        img(clouds), _ptr(auto_exposure), _ptr(scratch), _stream(stream)), "composition_luminance_histogram")
+
+
 def generate_luminance_histogram(g, hdr, auto_exposure, stream=None):
     _check(lib().soc_generate_luminance_histogram(_gp(g), img(hdr), _ptr(auto_exposure), _stream(stream)),
            "generate_luminance_histogram")
@@ -286,7 +299,7 @@ class Renderer:
     """Host render graph (C++ soc_renderer): the live passes of Renderer::rebuild_task_graph in order."""
 
     def __init__(self, frame: dict, timing: bool = False, stream=None, fused_bloom: bool = True, sky_lane: bool = True,
-                 fused_tonemap: bool = True):
+                 fused_tonemap: bool = True, fused_histogram: bool = False):
         self.frame = frame
         fi = FrameImages()
         for k in ("albedo", "emissive", "normal", "depth", "velocity", "shadow", "noise", "ssao", "ssao_blur", "clouds",
@@ -305,7 +318,8 @@ class Renderer:
         fi.clouds_workspace = _ptr(frame.get("clouds_workspace"))
         self._fi = fi
         flags = ((_abi.RENDERER_TIMING if timing else 0) | (0 if fused_bloom else _abi.RENDERER_UNFUSED_BLOOM)
-                 | (0 if sky_lane else _abi.RENDERER_SERIAL) | (0 if fused_tonemap else _abi.RENDERER_UNFUSED_TONEMAP))
+                 | (0 if sky_lane else _abi.RENDERER_SERIAL) | (0 if fused_tonemap else _abi.RENDERER_UNFUSED_TONEMAP)
+                 | (_abi.RENDERER_FUSED_HISTOGRAM if fused_histogram else 0))
         h = lib().soc_renderer_create(C.byref(fi), flags)
         if not h:
             raise SocError(-1, lib().soc_last_error_string().decode())

@@ -35,6 +35,8 @@ RENDERER_TIMING = 1
 RENDERER_UNFUSED_BLOOM = 2
 RENDERER_SERIAL = 4
 RENDERER_UNFUSED_TONEMAP = 8
+RENDERER_FUSED_HISTOGRAM = 16
+HISTOGRAM_SCRATCH_WORDS = 2048
 
 Mat4 = C.c_float * 16
 Vec2 = C.c_float * 2
@@ -144,6 +146,7 @@ FUNCTIONS = {
     "soc_ssao_blur": (_I, [_G, _IMG, _IMG, _P]),
     "soc_cloud_rendering_workspace_size": (C.c_size_t, [C.c_int32, C.c_int32]),
     "soc_cloud_rendering": (_I, [_G, _IMG, _IMG, _IMG, _P, _P]),
+    "soc_composition_luminance_histogram": (_I, [_G, _P, _IMG, _IMG, _IMG, _IMG, _IMG, _IMG, _IMG, _IMG, _P, _P, _P]),
     "soc_composition": (_I, [_G, _P, _IMG, _IMG, _IMG, _IMG, _IMG, _IMG, _IMG, _IMG, _P]),
     "soc_generate_luminance_histogram": (_I, [_G, _IMG, _P, _P]),
     "soc_resolve_luminance_histogram": (_I, [_G, _P, C.c_uint64, C.c_int32, _P]),

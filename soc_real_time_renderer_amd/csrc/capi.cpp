@@ -483,9 +483,22 @@ struct soc_renderer {
     int side_device = -1;
     hipStream_t side = nullptr;
     hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+    // 8 partial luminance histograms of the fused composition + histogram pass (renderer-owned, 8 KiB)
+    uint32_t* hist_scratch = nullptr;
 };
 
 namespace {
+int ensure_hist_scratch(soc_renderer* r) {
+    if (r->hist_scratch) return SOC_OK;
+    if (hipMalloc((void**)&r->hist_scratch, SOC_HISTOGRAM_SCRATCH_WORDS * sizeof(uint32_t)) != hipSuccess) {
+        r->hist_scratch = nullptr;
+        return set_error(SOC_E_HIP, "soc_renderer_execute: histogram scratch allocation failed");
+    }
+    if (hipMemset(r->hist_scratch, 0, SOC_HISTOGRAM_SCRATCH_WORDS * sizeof(uint32_t)) != hipSuccess)
+        return set_error(SOC_E_HIP, "soc_renderer_execute: histogram scratch clear failed");
+    return SOC_OK;
+}
+
 void build_passes(soc_renderer* r) {
     auto& I = r->img;
     auto add = [&](std::string name, std::string group, int phase, std::function<int(const soc_globals*, hipStream_t)> fn) {
@@ -538,18 +551,32 @@ void build_passes(soc_renderer* r) {
         return soc_cloud_rendering(g, r->img.depth, r->img.noise, r->img.clouds, r->img.clouds_workspace, (soc_stream)s);
     });
     r->passes.back().lane = 1;
-    // renderer.cpp:1103-1117
-    add("Composition", "Composition", SOC_PHASE_PRE_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
-        const auto& I = r->img;
-        const soc_img& em = I.bloom_output.data ? I.bloom_output : I.emissive;
-        return soc_composition(g, I.d_globals, I.color, I.albedo, em, I.normal, I.depth, I.ssao_blur, I.shadow, I.clouds,
-                               (soc_stream)s);
-    });
-    r->passes.back().join = true;
-    // renderer.cpp:1155-1168
-    add("GenerateLuminanceHistogram", "Auto Exposure", SOC_PHASE_PRE_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
-        return soc_generate_luminance_histogram(g, r->img.color, r->img.auto_exposure, (soc_stream)s);
-    });
+    // renderer.cpp:1103-1117 (composition) and 1155-1162 (histogram): two launches by default, one
+    // with SOC_RENDERER_FUSED_HISTOGRAM (trade-off measured in composition.hip)
+    if (r->flags & SOC_RENDERER_FUSED_HISTOGRAM) {
+        add("Composition+GenerateLuminanceHistogram", "Composition", SOC_PHASE_PRE_EXPOSURE,
+            [r](const soc_globals* g, hipStream_t s) {
+                const auto& I = r->img;
+                const soc_img& em = I.bloom_output.data ? I.bloom_output : I.emissive;
+                int rc = ensure_hist_scratch(r);
+                if (rc) return rc;
+                return soc_composition_luminance_histogram(g, I.d_globals, I.color, I.albedo, em, I.normal, I.depth,
+                                                           I.ssao_blur, I.shadow, I.clouds, I.auto_exposure, r->hist_scratch,
+                                                           (soc_stream)s);
+            });
+        r->passes.back().join = true;
+    } else {
+        add("Composition", "Composition", SOC_PHASE_PRE_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
+            const auto& I = r->img;
+            const soc_img& em = I.bloom_output.data ? I.bloom_output : I.emissive;
+            return soc_composition(g, I.d_globals, I.color, I.albedo, em, I.normal, I.depth, I.ssao_blur, I.shadow, I.clouds,
+                                   (soc_stream)s);
+        });
+        r->passes.back().join = true;
+        add("GenerateLuminanceHistogram", "Auto Exposure", SOC_PHASE_PRE_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
+            return soc_generate_luminance_histogram(g, r->img.color, r->img.auto_exposure, (soc_stream)s);
+        });
+    }
     add("ResolveLuminanceHistogram", "Auto Exposure", SOC_PHASE_POST_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
         return soc_resolve_luminance_histogram(g, r->img.auto_exposure, r->total_pixels, r->wide, (soc_stream)s);
     });
@@ -614,6 +641,7 @@ extern "C" void soc_renderer_destroy(soc_renderer* r) {
     if (r->fork_ev) (void)hipEventDestroy(r->fork_ev);
     if (r->join_ev) (void)hipEventDestroy(r->join_ev);
     if (r->side) (void)hipStreamDestroy(r->side);
+    if (r->hist_scratch) (void)hipFree(r->hist_scratch);
     delete r;
 }
 

@@ -13,51 +13,11 @@
 
 #include <cstdlib>
 
+#include "luminance.hpp"
 #include "soc_internal.hpp"
 
 namespace soc {
 namespace {
-
-constexpr int kBins = SOC_AUTO_EXPOSURE_BIN_COUNT;
-
-__device__ __forceinline__ float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
-__device__ __forceinline__ uint32_t f2u(float f) { return __builtin_bit_cast(uint32_t, f); }
-
-// Deterministic log2 (same operation sequence as soc_oracle_log2).
-__device__ __forceinline__ float det_log2(float x) {
-#pragma clang fp contract(off)
-    if (x != x) return x;
-    if (x < 0.0f) return u2f(0x7fc00000u);
-    if (x == 0.0f) return -__builtin_inff();
-    if (x == __builtin_inff()) return __builtin_inff();
-    uint32_t u = f2u(x);
-    int e = 0;
-    if (u < 0x00800000u) { x = x * 8388608.0f; u = f2u(x); e = -23; }
-    e += (int)(u >> 23) - 127;
-    float m = u2f((u & 0x007fffffu) | 0x3f800000u);
-    if (m > 1.41421356f) { m = m * 0.5f; e += 1; }
-    float f = m - 1.0f;
-    float s = f / (2.0f + f);
-    float s2 = s * s;
-    float p = __builtin_fmaf(s2, 1.0f / 11.0f, 1.0f / 9.0f);
-    p = __builtin_fmaf(s2, p, 1.0f / 7.0f);
-    p = __builtin_fmaf(s2, p, 1.0f / 5.0f);
-    p = __builtin_fmaf(s2, p, 1.0f / 3.0f);
-    p = __builtin_fmaf(s2, p, 1.0f);
-    float ln = (2.0f * s) * p;
-    return __builtin_fmaf(ln, 1.44269504088896341f, (float)e);
-}
-
-__device__ __forceinline__ uint32_t lum_bin(float r, float g, float b, float lmin, float lrange) {
-#pragma clang fp contract(off)
-    float lum = __builtin_fmaf(b, 0.0722f, __builtin_fmaf(g, 0.7152f, r * 0.2126f));
-    if (lum < 1e-3f) lum = 0.0f;
-    float q = (det_log2(lum) - lmin) / lrange;
-    float mapped = __builtin_fmaf(q, (float)(kBins - 1) - 1.0f, 1.0f);
-    if (mapped >= 255.0f) return 255u;
-    if (mapped > 0.0f) return (uint32_t)(int32_t)mapped;
-    return 0u;
-}
 
 constexpr int kThreads = 256, kWaves = kThreads / 64, kPix = 8;
 

@@ -1,0 +1,78 @@
+// luminance.hpp — the luminance-histogram bin of GenerateLuminanceHistogramTask
+// (src/graphics/tasks/generate_luminance_histogram.inl:59-78) as a device function: the bit-exact contract
+// of DESIGN.md §3.4 (explicit-FMA luminance and remap, deterministic log2), identical to the oracle's
+// soc_oracle_luminance_bin. Shared by the histogram pass (exposure.hip) and the fused composition +
+// histogram pass (composition.hip).
+#pragma once
+
+#include "../../include/soc_rt.h"
+#include "soc_device.hpp"
+
+namespace soc {
+
+constexpr int kBins = SOC_AUTO_EXPOSURE_BIN_COUNT;
+
+__device__ __forceinline__ float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
+__device__ __forceinline__ uint32_t f2u(float f) { return __builtin_bit_cast(uint32_t, f); }
+
+// Deterministic log2 (same operation sequence as soc_oracle_log2).
+__device__ __forceinline__ float det_log2(float x) {
+#pragma clang fp contract(off)
+    if (x != x) return x;
+    if (x < 0.0f) return u2f(0x7fc00000u);
+    if (x == 0.0f) return -__builtin_inff();
+    if (x == __builtin_inff()) return __builtin_inff();
+    uint32_t u = f2u(x);
+    int e = 0;
+    if (u < 0x00800000u) { x = x * 8388608.0f; u = f2u(x); e = -23; }
+    e += (int)(u >> 23) - 127;
+    float m = u2f((u & 0x007fffffu) | 0x3f800000u);
+    if (m > 1.41421356f) { m = m * 0.5f; e += 1; }
+    float f = m - 1.0f;
+    float s = f / (2.0f + f);
+    float s2 = s * s;
+    float p = __builtin_fmaf(s2, 1.0f / 11.0f, 1.0f / 9.0f);
+    p = __builtin_fmaf(s2, p, 1.0f / 7.0f);
+    p = __builtin_fmaf(s2, p, 1.0f / 5.0f);
+    p = __builtin_fmaf(s2, p, 1.0f / 3.0f);
+    p = __builtin_fmaf(s2, p, 1.0f);
+    float ln = (2.0f * s) * p;
+    return __builtin_fmaf(ln, 1.44269504088896341f, (float)e);
+}
+
+__device__ __forceinline__ uint32_t lum_bin(float r, float g, float b, float lmin, float lrange) {
+#pragma clang fp contract(off)
+    float lum = __builtin_fmaf(b, 0.0722f, __builtin_fmaf(g, 0.7152f, r * 0.2126f));
+    if (lum < 1e-3f) lum = 0.0f;
+    float q = (det_log2(lum) - lmin) / lrange;
+    float mapped = __builtin_fmaf(q, (float)(kBins - 1) - 1.0f, 1.0f);
+    if (mapped >= 255.0f) return 255u;
+    if (mapped > 0.0f) return (uint32_t)(int32_t)mapped;
+    return 0u;
+}
+
+// Adds the bins of two pixels per lane into an LDS histogram with one LDS atomic per distinct bin of
+// the wave (a ballot loop: neighbouring pixels mostly share a bin, so 2-3 rounds per 16x8 block).
+// Lanes with valid == false contribute nothing; every lane of the wave must call it. (Device atomics per
+// wave instead of the LDS copy measured 186 us at 4K: the hot bins serialise.)
+__device__ __forceinline__ void wave_bin_pair(uint32_t* sh, uint32_t b0, uint32_t b1, bool valid) {
+    uint32_t pend = valid ? 3u : 0u;   // bit 0: pixel 0 pending, bit 1: pixel 1
+    const uint32_t lane = __lane_id();
+    unsigned long long act = __ballot(pend != 0u);
+    while (act) {
+        const int leader = __builtin_ctzll(act);
+        const uint32_t lb0 = (uint32_t)__shfl((int)b0, leader), lb1 = (uint32_t)__shfl((int)b1, leader);
+        const uint32_t lpend = (uint32_t)__shfl((int)pend, leader);
+        const uint32_t B = (lpend & 1u) ? lb0 : lb1;
+        const uint32_t mine = (((pend & 1u) && b0 == B) ? 1u : 0u) + (((pend & 2u) && b1 == B) ? 1u : 0u);
+        if ((pend & 1u) && b0 == B) pend &= ~1u;
+        if ((pend & 2u) && b1 == B) pend &= ~2u;
+        // wave sum of `mine` (0..2 per lane)
+        const unsigned long long m1 = __ballot(mine & 1u), m2 = __ballot(mine & 2u);
+        const uint32_t total = (uint32_t)__builtin_popcountll(m1) + 2u * (uint32_t)__builtin_popcountll(m2);
+        if (lane == (uint32_t)leader) atomicAdd(&sh[B], total);
+        act = __ballot(pend != 0u);
+    }
+}
+
+}  // namespace soc

@@ -190,6 +190,36 @@ def test_composition(soc, oracle, W, H, lights):
     assert np.array_equal(got[sky].view(np.uint16), ref[sky].view(np.uint16))   # sky = clouds texel, exact
 
 
+@pytest.mark.parametrize("W,H", [(64, 36), (98, 56), (97, 55), (1920, 1080), (3840, 2160)])
+def test_composition_histogram_fused(soc, W, H):
+    """One-launch composition + histogram: the colour equals soc_composition's bit-for-bit and the bins
+    equal those the histogram pass computes from it (98x56: partial tiles; 97x55: two-pass fallback).
+    Pre-existing bin counts are added to, not overwritten."""
+    g, gb = sponza_inputs(W, H, elapsed=10.0)
+    rng = np.random.default_rng(W)
+    ssao = dev(rng.integers(120, 256, (H // 2, W // 2), dtype=np.uint8))
+    clouds = dev(rng.integers(0, 256, (H, W, 4), dtype=np.uint8))
+    ins = [dev(gb[k]) for k in ("albedo", "emissive", "normal", "depth")]
+    shadow = dev(gb["shadow"])
+    c1 = torch.zeros(H, W, 4, dtype=torch.float16, device=DEV)
+    soc.composition(g, c1, *ins, ssao, shadow, clouds)
+    a1 = soc.auto_exposure_buffer()
+    a1[1:] = 7
+    soc.generate_luminance_histogram(g, c1, a1)
+    c2 = torch.zeros_like(c1)
+    a2 = soc.auto_exposure_buffer()
+    a2[1:] = 7
+    scratch = soc.histogram_scratch()
+    for _ in range(2):   # the scratch is left zeroed: a second call adds the same bins again
+        soc.composition_luminance_histogram(g, c2, *ins, ssao, shadow, clouds, a2, scratch)
+    torch.cuda.synchronize()
+    assert int(scratch.abs().sum()) == 0
+    a2[1:] = (a2[1:] - 7) // 2 + 7
+    assert torch.equal(c1, c2)
+    assert torch.equal(a1, a2)
+    assert int(a2[1:].sum()) == W * H + 7 * 256
+
+
 # ------------------------------------------------------------------------------------------------ exposure
 @pytest.mark.parametrize("W,H", [(64, 36), (97, 55), (1920, 1080), (3840, 2160)])
 def test_histogram_bit_exact(soc, oracle, W, H):
