@@ -22,6 +22,9 @@ namespace soc {
 namespace {
 
 constexpr int kNoise = 64, kNoiseMask = 63;
+// LDS quad table: 81 x 81 entries (64 + the 17-texel tap offset), so the second tap of get_3d_noise is
+// the first tap's address plus a constant (an immediate ds_read offset) with no wrap arithmetic.
+constexpr int kTap2 = 17, kTW = kNoise + kTap2, kTable = kTW * kTW;
 constexpr float kEarthRadius = 6371000.0f, kMinH = 1600.0f, kMaxH = 500.0f + 1600.0f, kSunBrightness = 3.0f;
 constexpr float kPi = 3.14159265358979f;   // acos(-1.0) in fp32
 constexpr float kLn2 = 0.693147182f;       // log(2.0) in fp32
@@ -61,30 +64,38 @@ __device__ __forceinline__ float2 rsi(f3 p, f3 d, float radius) {
 
 // texture(noise, uv).x under REPEAT + the sampling contract, from the LDS quad table. The two taps of
 // get_3d_noise sit exactly 17 texels apart in u and v (zStretch = 17/64), so they share one axis
-// computation; the bilinear blend runs on the raw bytes and is scaled by 1/255 once. Both regroup the
-// contract's fp32 roundings; clouds are checked against the RGBA8 tolerance.
-__device__ __forceinline__ float quad_bilerp(uint32_t q, float wx, float wy) {
-    const float c0 = (float)(q & 0xffu), c1 = (float)((q >> 8) & 0xffu);     // v_cvt_f32_ubyte0..3
-    const float c2 = (float)((q >> 16) & 0xffu), c3 = (float)(q >> 24);
-    const float top = __builtin_fmaf(wx, c1 - c0, c0);
-    const float bot = __builtin_fmaf(wx, c3 - c2, c2);
-    return __builtin_fmaf(wy, bot - top, top);
+// computation. The bilinear blend of a tap is evaluated EXACTLY in integers on the raw bytes with the
+// contract's 8-bit weights (v_dot2_u32_u16: c0 (256 - wx) + c1 wx per row, then the same across rows;
+// at most 255 * 65536 < 2^24), i.e. without the fp32 rounding of the lerps; both are within the RGBA8
+// tolerance of the pass.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t udot2(uint32_t a, uint32_t b) {
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b), 0u, false);
+}
+// 65536 x bilinear of quad q (bytes c0 c1 / c2 c3) with packed weights wxp = (256 - wx) | wx << 16
+__device__ __forceinline__ uint32_t quad_bilerp_u(uint32_t q, uint32_t wxp, uint32_t wyp) {
+    const uint32_t top = udot2(__builtin_amdgcn_perm(q, q, 0x0c010c00u), wxp);   // c0 | c1 << 16
+    const uint32_t bot = udot2(__builtin_amdgcn_perm(q, q, 0x0c030c02u), wxp);   // c2 | c3 << 16
+    return udot2(top | (bot << 16), wyp);
 }
 
 // get_3d_noise, :219-233
 __device__ __forceinline__ float noise3(const Ctx& cx, f3 pos) {
     const float p = floorf(pos.z);
     const float f = pos.z - p;
-    const float inv = 1.0f / 64.0f, zs = 17.0f * inv;
-    const float cu = pos.x * inv + p * zs, cv = pos.y * inv + p * zs;
-    const int fx = (int)floorf(__builtin_fmaf(__builtin_fmaf(cu, 64.0f, -0.5f), 256.0f, 0.5f));
-    const int fy = (int)floorf(__builtin_fmaf(__builtin_fmaf(cv, 64.0f, -0.5f), 256.0f, 0.5f));
-    const float wx = (float)(fx & 255) * (1.0f / 256.0f), wy = (float)(fy & 255) * (1.0f / 256.0f);
-    const int ix = (fx >> 8) & kNoiseMask, iy = (fy >> 8) & kNoiseMask;
-    const uint32_t q0 = cx.quads[iy * kNoise + ix];
-    const uint32_t q1 = cx.quads[((iy + 17) & kNoiseMask) * kNoise + ((ix + 17) & kNoiseMask)];
-    const float a = quad_bilerp(q0, wx, wy), b = quad_bilerp(q1, wx, wy);
-    return __builtin_fmaf(f, b - a, a) * (1.0f / 255.0f);
+    // fixed-point texel coordinate of the first tap: (u 64 - 0.5) 256 + 0.5 with u = pos.x / 64 + p 17/64,
+    // i.e. 256 pos.x + 4352 p - 127.5 (one rounding instead of four; within the pass tolerance)
+    const float base = __builtin_fmaf(p, 4352.0f, -127.5f);
+    const int fx = (int)floorf(__builtin_fmaf(pos.x, 256.0f, base));
+    const int fy = (int)floorf(__builtin_fmaf(pos.y, 256.0f, base));
+    const uint32_t wx = (uint32_t)fx & 255u, wy = (uint32_t)fy & 255u;
+    const uint32_t wxp = wx * 65535u + 256u, wyp = wy * 65535u + 256u;
+    const uint32_t ix = ((uint32_t)fx >> 8) & kNoiseMask, iy = ((uint32_t)fy >> 8) & kNoiseMask;
+    const uint32_t* t = cx.quads + (iy * (uint32_t)kTW + ix);
+    const uint32_t q0 = t[0], q1 = t[kTap2 * kTW + kTap2];
+    const float a = (float)quad_bilerp_u(q0, wxp, wyp), b = (float)quad_bilerp_u(q1, wxp, wyp);
+    return __builtin_fmaf(f, b - a, a) * (1.0f / (255.0f * 65536.0f));
 }
 
 // |v| with the hardware square root (1 ulp). Every length in this pass is an Earth-scale distance
@@ -197,6 +208,17 @@ __device__ __forceinline__ MarchShade march_shade(f3 dir, f3 sun) {
     return m;
 }
 
+// Position of march step i (:321-333: cp = start + inc * dither, then cp += inc per step) as one fma per
+// component, start + inc (i + dither): i + dither is exact (dither = k/256), so every step carries one
+// rounding instead of the reference's accumulated i additions (within the pass tolerance), and a lane
+// can evaluate any step directly. Every path (single-lane march, density, sunvis) uses this form, so
+// the pair path stays bit-identical to the single-lane march.
+__device__ __forceinline__ f3 step_position(const MarchGeom& mg, float dither, int i) {
+    const float t = (float)i + dither;
+    return f3{__builtin_fmaf(mg.inc.x, t, mg.start.x), __builtin_fmaf(mg.inc.y, t, mg.start.y),
+              __builtin_fmaf(mg.inc.z, t, mg.start.z)};
+}
+
 // One dense step of the scattering sum (:326-344), in the reference's order.
 __device__ __forceinline__ void march_accumulate(const MarchShade& ms, f3 sun_color, float od, float vis, f3& scattering,
                                                  float& transmittance) {
@@ -220,10 +242,10 @@ __device__ f3 volumetric_clouds(const Ctx& cx, f3 dir, f3 sun, f3 color, float d
     if (dir.y < 0.0f) return color;
     const MarchGeom mg = march_geometry(dir);
     const MarchShade ms = march_shade(dir, sun);
-    f3 cp = mg.inc * dither + mg.start;
     f3 scattering = f3{0.0f, 0.0f, 0.0f};
     float transmittance = 1.0f;
-    for (int i = 0; i < 24; i++, cp = cp + mg.inc) {
+    for (int i = 0; i < 24; i++) {
+        const f3 cp = step_position(mg, dither, i);
         const float od = get_clouds(cx, cp) * mg.stepLength;
         if (od <= 0.0f) continue;
         march_accumulate(ms, sun_color, od, sun_visibility(cx, cp, sun), scattering, transmittance);
@@ -247,21 +269,29 @@ __device__ f3 atmosphere(f3 r, f3 r0, f3 pSun, float iTime) {
     const float pRlh = 3.0f / (16.0f * PI) * (1.0f + mumu);
     const float pMie = 3.0f / (8.0f * PI) * ((1.0f - gg) * (mumu + 1.0f)) / (powf(1.0f + gg - 2.0f * mu * g0, 1.5f) * (2.0f + gg));
     const float kR = -1.44269504f / shRlh, kM = -1.44269504f / shMie;   // exp(-h/sh) = exp2(h * kR)
+    // secondary ray: |iPos + pSun t|^2 = A + t (B + t C) with A = |iPos|^2, B = 2 iPos.pSun, C = |pSun|^2
+    // (the rsi of the secondary ray needs the same two dot products), and exp(-h / sh) as
+    // exp2(|jPos| kR - rPlanet kR): per step two fmas, a sqrt and the two exponentials
+    const float C2 = dot3(pSun, pSun), cR = -rPlanet * kR, cM = -rPlanet * kM;
     for (int i = 0; i < 16; i++) {
         const f3 iPos = r0 + r * (iTime + iStep * 0.5f);
-        const float iHeight = hw_length3(iPos) - rPlanet;
-        const float odR = __builtin_amdgcn_exp2f(iHeight * kR) * iStep;
-        const float odM = __builtin_amdgcn_exp2f(iHeight * kM) * iStep;
+        const float A = dot3(iPos, iPos), PoD = dot3(iPos, pSun);
+        const float iLen = __builtin_amdgcn_sqrtf(A);
+        const float odR = __builtin_amdgcn_exp2f(__builtin_fmaf(iLen, kR, cR)) * iStep;
+        const float odM = __builtin_amdgcn_exp2f(__builtin_fmaf(iLen, kM, cM)) * iStep;
         iOdRlh += odR;
         iOdMie += odM;
-        const float jStep = rsi(iPos, pSun, rAtmos).y / 8.0f;
+        // rsi(iPos, pSun, rAtmos).y (:97-106); the secondary ray starts inside the atmosphere
+        float delta = PoD * PoD + rAtmos * rAtmos - A;
+        const float jStep = (delta < 0.0f ? -1.0f : -PoD + __builtin_amdgcn_sqrtf(delta)) / 8.0f;
+        const float B = 2.0f * PoD, half = jStep * 0.5f;
         float jTime = 0.0f, jOdR = 0.0f, jOdM = 0.0f;
 #pragma unroll 4
         for (int j = 0; j < 8; j++) {
-            const f3 jPos = iPos + pSun * (jTime + jStep * 0.5f);
-            const float jHeight = hw_length3(jPos) - rPlanet;
-            jOdR += __builtin_amdgcn_exp2f(jHeight * kR) * jStep;
-            jOdM += __builtin_amdgcn_exp2f(jHeight * kM) * jStep;
+            const float t = jTime + half;
+            const float jLen = __builtin_amdgcn_sqrtf(__builtin_fmaf(t, __builtin_fmaf(t, C2, B), A));
+            jOdR = __builtin_fmaf(__builtin_amdgcn_exp2f(__builtin_fmaf(jLen, kR, cR)), jStep, jOdR);
+            jOdM = __builtin_fmaf(__builtin_amdgcn_exp2f(__builtin_fmaf(jLen, kM, cM)), jStep, jOdM);
             jTime += jStep;
         }
         const float fm = kMie * (iOdMie + jOdM);
@@ -314,14 +344,15 @@ __device__ __forceinline__ uint32_t shade_sky(const CloudParams& p, const uint32
 // Stage the noise .x channel as 2x2 REPEAT quads (quad i = texels (x,y), (x+1,y), (x,y+1), (x+1,y+1)).
 template <bool NOISE_R8>
 __device__ __forceinline__ void stage_noise(const DImg& noise, uint32_t* quads, int tid, int nthreads) {
-    for (int i = tid; i < kNoise * kNoise; i += nthreads) {
-        const int nx = i & kNoiseMask, ny = i >> 6;
-        const int nx1 = (nx + 1) & kNoiseMask, ny1 = (ny + 1) & kNoiseMask;
+    for (int i = tid; i < kTable; i += nthreads) {
+        const int ny = i / kTW, nx = (i - ny * kTW) & kNoiseMask;
+        const int nyw = ny & kNoiseMask;
+        const int nx1 = (nx + 1) & kNoiseMask, ny1 = (nyw + 1) & kNoiseMask;
         auto texel = [&](int tx, int ty) -> uint32_t {
             if (NOISE_R8) return row_ptr<uint8_t>(noise, ty)[tx];
             return row_ptr<uint32_t>(noise, ty)[tx] & 0xffu;
         };
-        quads[i] = texel(nx, ny) | (texel(nx1, ny) << 8) | (texel(nx, ny1) << 16) | (texel(nx1, ny1) << 24);
+        quads[i] = texel(nx, nyw) | (texel(nx1, nyw) << 8) | (texel(nx, ny1) << 16) | (texel(nx1, ny1) << 24);
     }
 }
 
@@ -332,7 +363,7 @@ __device__ __forceinline__ bool is_sky(const CloudParams& p, const DImg& depth, 
 // Single-kernel path (no workspace): 16x16 tiles, a tile without sky exits after its depth test.
 template <bool NOISE_R8>
 __global__ __launch_bounds__(256) void clouds_kernel(DImg depth, DImg noise, DImg target, CloudParams p) {
-    __shared__ uint32_t quads[kNoise * kNoise];
+    __shared__ uint32_t quads[kTable];
     const int x = blockIdx.x * TX + threadIdx.x, y = blockIdx.y * TY + threadIdx.y;
     const int tid = threadIdx.y * TX + threadIdx.x;
     const bool inside = x < p.res_x && y < p.res_y && x < target.w && y < target.h;
@@ -440,11 +471,7 @@ struct PairBufs {
     uint32_t cap;         // pairs per shard
 };
 
-__device__ __forceinline__ f3 step_position(const MarchGeom& mg, float dither, int step) {
-    f3 cp = mg.inc * dither + mg.start;
-    for (int i = 0; i < step; ++i) cp = cp + mg.inc;
-    return cp;
-}
+
 
 // Rank of this lane among the lanes of its wave whose mask has step `st`.
 __device__ __forceinline__ uint32_t mask_ballot_rank(uint32_t mask, uint32_t st, uint32_t lane) {
@@ -479,9 +506,9 @@ __device__ __forceinline__ void batch_slots(uint32_t mask, uint32_t lane, uint32
 }
 
 template <bool NOISE_R8>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void clouds_density(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void clouds_density(
     DImg noise, CloudParams p, const uint32_t* __restrict__ counter, const uint32_t* __restrict__ list, PairBufs pb) {
-    __shared__ uint32_t quads[kNoise * kNoise];
+    __shared__ uint32_t quads[kTable];
     __shared__ uint32_t offs[25][4];
     __shared__ uint32_t wg_base;
     const uint32_t count = *counter;
@@ -505,9 +532,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void c
             const f3 dir = sky_dir(p, x, y);
             if (SOC_CLOUDS_PROFILE != 1 && !(dir.y < 0.0f)) {
                 const MarchGeom mg = march_geometry(dir);
-                f3 cp = mg.inc * bayer16((float)x, (float)y) + mg.start;
-                for (int s = 0; s < 24; s++, cp = cp + mg.inc)
-                    if (!(get_clouds(cx, cp) * mg.stepLength <= 0.0f)) mask |= 1u << s;
+                const float dither = bayer16((float)x, (float)y);
+                for (int s = 0; s < 24; s++)
+                    if (!(get_clouds(cx, step_position(mg, dither, s)) * mg.stepLength <= 0.0f)) mask |= 1u << s;
             }
         }
         // pairs in step-major order within the batch (lanes of a sunvis wave then share the step and
@@ -545,9 +572,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void c
 }
 
 template <bool NOISE_R8>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void clouds_sunvis(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void clouds_sunvis(
     DImg noise, CloudParams p, const uint32_t* __restrict__ list, PairBufs pb) {
-    __shared__ uint32_t quads[kNoise * kNoise];
+    __shared__ uint32_t quads[kTable];
     __shared__ uint32_t pre[kShards + 1];
     const uint32_t tid = threadIdx.x;
     if (tid == 0) {
@@ -590,7 +617,7 @@ template <bool NOISE_R8>
 __global__ __launch_bounds__(256) void clouds_resolve(DImg noise, DImg target, CloudParams p, const uint32_t* __restrict__ counter,
                                                       const uint32_t* __restrict__ list, const float4* __restrict__ atmos,
                                                       PairBufs pb) {
-    __shared__ uint32_t quads[kNoise * kNoise];
+    __shared__ uint32_t quads[kTable];
     __shared__ uint32_t offs[25][4];
     const uint32_t count = *counter;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
