@@ -54,7 +54,8 @@ def algorithmic_bytes(W, H, f_sky):
         # fused stages (bloom_fused.hip): mip0 / mip2 of the downsweep never leave LDS (stages 3-4
         # are available through soc_bloom_fused_stage but not scheduled: slower than per-pass)
         "BloomDownsample - 0+1": (8.0 + 2.0) * P, "BloomDownsample - 2+3": (2.0 + 0.125) * P,
-        "BloomUpsample - 3+2": (0.125 + 0.5 + 2.0) * P, "BloomUpsample - 1+0": (2.0 + 8.0 + 8.0) * P,
+        # weighted-form upsweep (bloom_w.hip): mip2 / mip0 stay in LDS (mip3 -> mip1, mip1 -> output)
+        "BloomUpsample - 3+2": (0.125 + 2.0) * P, "BloomUpsample - 1+0": (2.0 + 8.0) * P,
         "SSAOGeneration": 12.25 * P, "SSAOBlur": 0.5 * P, "CloudRendering": 8.0 * P,
         "Composition": (40.25 + 4.0 * f_sky) * P, "GenerateLuminanceHistogram": 8.0 * P,
         # fused composition + histogram: the bins come from the stored pixels in registers (+1 KiB)

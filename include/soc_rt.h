@@ -235,6 +235,16 @@ int soc_bloom_chain(const soc_globals* g, soc_img emissive, const soc_img* mips,
 int soc_bloom_fused_stage(const soc_globals* g, soc_img emissive, const soc_img* mips, int32_t mip_count, soc_img output,
                           int32_t stage, soc_stream stream);
 
+/* The bloom chain in weighted form (bloom_w.hip): at the chain's fixed ratios every tap of the sampling
+ * contract has exact weights on clamp-to-edge texels, so each pass is evaluated as one fixed weighted
+ * sum of RGBA16F texels with fp32 FMAs (same weights, different rounding order: within the RGBA16F
+ * tolerance, not bit-exact). Stages: 1 emissive -> [mip0] -> mips[1], 2 mips[1] -> [mip2] -> mips[3],
+ * 3 mips[3] -> [mip2] -> mips[1], 4 mips[1] -> [mip0] -> output; 0 = all four. mips[0] and mips[2] are
+ * scratch (never written: their final contents are unobservable in the reference graph). Same extent
+ * rules as soc_bloom_fused_stage; output may be `emissive` (in place, as the reference) but not mips[1]. */
+int soc_bloom_weighted_stage(const soc_globals* g, soc_img emissive, const soc_img* mips, int32_t mip_count, soc_img output,
+                             int32_t stage, soc_stream stream);
+
 /* SSAOGenerationTask (ssao_generation.inl:20-68, shader :176-214): half-res R8 ambient occlusion from
  * full-res depth (D32F) and normal (RGBA16F). `target` is (W/2)x(H/2) R8_UNORM. `noise_table` is an
  * optional device workspace of (target.w * target.h * 2) floats holding the per-pixel random vector
@@ -356,6 +366,7 @@ typedef struct soc_renderer soc_renderer;
 #define SOC_RENDERER_SERIAL 4      /* every pass on the caller's stream (no concurrent sky lane) */
 #define SOC_RENDERER_UNFUSED_TONEMAP 8  /* TAA and tone mapping as two passes (default: one launch for RGBA8) */
 #define SOC_RENDERER_FUSED_HISTOGRAM 16  /* composition + luminance histogram in one launch */
+#define SOC_RENDERER_EXACT_BLOOM 32       /* bit-exact bloom chain instead of the weighted form (bloom_w.hip) */
 
 soc_renderer* soc_renderer_create(const soc_frame_images* images, uint32_t flags);
 void soc_renderer_destroy(soc_renderer* r);

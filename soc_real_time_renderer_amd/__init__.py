@@ -173,6 +173,13 @@ def bloom_fused_stage(g, emissive, mips, output, stage=0, stream=None):
            "bloom_fused_stage")
 
 
+def bloom_weighted_stage(g, emissive, mips, output, stage=0, stream=None):
+    """One stage (1-4, 0 = all) of the weighted-form bloom chain (soc_bloom_weighted_stage)."""
+    arr = (SocImg * len(mips))(*[img(m) for m in mips])
+    _check(lib().soc_bloom_weighted_stage(_gp(g), img(emissive), arr, len(mips), img(output), int(stage),
+                                          _stream(stream)), "bloom_weighted_stage")
+
+
 def ssao_prepare_noise(normal, target, table, stream=None):
     _check(lib().soc_ssao_prepare_noise(img(normal), img(target), _ptr(table), _stream(stream)), "ssao_prepare_noise")
 
@@ -299,7 +306,8 @@ class Renderer:
     """Host render graph (C++ soc_renderer): the live passes of Renderer::rebuild_task_graph in order."""
 
     def __init__(self, frame: dict, timing: bool = False, stream=None, fused_bloom: bool = True, sky_lane: bool = True,
-                 fused_tonemap: bool = True, fused_histogram: bool = False):
+                 fused_tonemap: bool = True, fused_histogram: bool = False,
+                 exact_bloom: bool = False):
         self.frame = frame
         fi = FrameImages()
         for k in ("albedo", "emissive", "normal", "depth", "velocity", "shadow", "noise", "ssao", "ssao_blur", "clouds",
@@ -319,7 +327,8 @@ class Renderer:
         self._fi = fi
         flags = ((_abi.RENDERER_TIMING if timing else 0) | (0 if fused_bloom else _abi.RENDERER_UNFUSED_BLOOM)
                  | (0 if sky_lane else _abi.RENDERER_SERIAL) | (0 if fused_tonemap else _abi.RENDERER_UNFUSED_TONEMAP)
-                 | (_abi.RENDERER_FUSED_HISTOGRAM if fused_histogram else 0))
+                 | (_abi.RENDERER_FUSED_HISTOGRAM if fused_histogram else 0)
+                 | (_abi.RENDERER_EXACT_BLOOM if exact_bloom else 0))
         h = lib().soc_renderer_create(C.byref(fi), flags)
         if not h:
             raise SocError(-1, lib().soc_last_error_string().decode())

@@ -36,6 +36,7 @@ RENDERER_UNFUSED_BLOOM = 2
 RENDERER_SERIAL = 4
 RENDERER_UNFUSED_TONEMAP = 8
 RENDERER_FUSED_HISTOGRAM = 16
+RENDERER_EXACT_BLOOM = 32
 HISTOGRAM_SCRATCH_WORDS = 2048
 
 Mat4 = C.c_float * 16
@@ -141,6 +142,7 @@ FUNCTIONS = {
     "soc_bloom_upsample": (_I, [_G, _IMG, _IMG, _P]),
     "soc_bloom_chain": (_I, [_G, _IMG, C.POINTER(SocImg), C.c_int32, _P]),
     "soc_bloom_fused_stage": (_I, [_G, _IMG, C.POINTER(SocImg), C.c_int32, _IMG, C.c_int32, _P]),
+    "soc_bloom_weighted_stage": (_I, [_G, _IMG, C.POINTER(SocImg), C.c_int32, _IMG, C.c_int32, _P]),
     "soc_ssao_prepare_noise": (_I, [_IMG, _IMG, _P, _P]),
     "soc_ssao_generation": (_I, [_G, _IMG, _IMG, _IMG, _P, _P]),
     "soc_ssao_blur": (_I, [_G, _IMG, _IMG, _P]),

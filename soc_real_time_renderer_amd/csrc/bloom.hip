@@ -384,6 +384,23 @@ extern "C" int soc_bloom_fused_stage(const soc_globals* g, soc_img emissive, con
     return launch_bloom_fused(emissive, mips, output, hs(stream), stage);
 }
 
+extern "C" int soc_bloom_weighted_stage(const soc_globals* g, soc_img emissive, const soc_img* mips, int32_t mip_count,
+                                        soc_img output, int32_t stage, soc_stream stream) {
+    (void)g;
+    static const char* P = "soc_bloom_weighted_stage";
+    if (!mips) return set_error(SOC_E_INVALID_ARG, "%s: null mips", P);
+    if (stage < 0 || stage > 4) return set_error(SOC_E_INVALID_ARG, "%s: stage %d not in 0..4", P, stage);
+    int rc = check_img(emissive, SOC_FMT_RGBA16F, P, "emissive");
+    if (!rc) rc = check_img(output, SOC_FMT_RGBA16F, P, "output");
+    for (int i = 0; !rc && i < mip_count; ++i) rc = check_img(mips[i], SOC_FMT_RGBA16F, P, "mip");
+    if (rc) return rc;
+    if (!bloom_fused_applicable(emissive, mips, mip_count, output))
+        return set_error(SOC_E_UNSUPPORTED, "%s: needs 4 mips halving exactly from the emissive extent (<= 8192)", P);
+    if ((stage == 0 || stage == 4) && output.data == mips[1].data)
+        return set_error(SOC_E_INVALID_ARG, "%s: output aliases mip 1", P);
+    return launch_bloom_weighted(emissive, mips, output, hs(stream), stage);
+}
+
 extern "C" int soc_bloom_chain(const soc_globals* g, soc_img emissive, const soc_img* mips, int32_t mip_count,
                                soc_stream stream) {
     if (!mips || mip_count < 1) return set_error(SOC_E_INVALID_ARG, "soc_bloom_chain: need >= 1 mip");

@@ -1,0 +1,314 @@
+// bloom_w.hip — the bloom chain of renderer.cpp:1024-1062 (BloomDownsampleTask x4,
+// bloom_downsample.inl:107-141; BloomUpsampleTask x4, bloom_upsample.inl:98-127) in WEIGHTED form.
+//
+// At the chain's fixed ratios (1:1 and 2:1 down, 1:2 and 1:1 up) every bilinear tap of the sampling
+// contract lands on an exact weight (0, 1/2, 1/4 or 3/4) of clamped texel indices, so
+// each pass is a fixed weighted sum over a small footprint of clamp-to-edge texels:
+//   down 1:1  13 point taps: 1/8 centre, 1/32 (+-2,+-2), 1/16 (0,+-2) (+-2,0), 1/8 (+-1,+-1)
+//   down 2:1  6x6 texels 2X-2..2X+3: (A (x) A + 4 B (x) B) / 128,  A = 1 1 2 2 1 1,  B = 0 1 1 1 1 0
+//   up 1:2    4x4 texels: w (x) w / 256, w = 1 5 7 3 on X-2..X+1 (even output) or 3 7 5 1 on X-1..X+2 (odd)
+//   up 1:1    3x3 texels: (1 2 1) (x) (1 2 1) / 16
+// These are evaluated as fp32 FMAs straight from the RGBA16F texels (v_fma_mix_f32) instead of the
+// reference's lerp-by-lerp order, which bloom.hip / bloom_fused.hip reproduce bit-exactly: same
+// weights, different rounding order, within the RGBA16F tolerance, ~1/4 of the VALU
+// work. Four kernels; the intermediates mip0 and mip2 live only in LDS (with recomputed halos):
+//   W1  emissive -> [mip0] -> mip1        W2  mip1 -> [mip2] -> mip3
+//   W3  mip3 -> [mip2] -> mip1            W4  mip1 -> [mip0] -> output
+// The downsweep's mip0 / mip2 are read only by the next downsample and the upsweep's mip2 / mip0 only
+// by the next upsample (quirk Q5 overwrites them), so mips[0] and mips[2] are not written: their final
+// contents are unobservable in the reference graph. An intermediate tile entry at an out-of-image
+// coordinate holds the value of the clamped coordinate, which is what the next pass's clamped taps read.
+#include "soc_internal.hpp"
+
+namespace soc {
+namespace {
+
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return min(max(v, lo), hi); }
+
+struct C3 {
+    float r, g, b;
+};
+__device__ __forceinline__ float lo16(uint32_t u) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(u & 0xffffu)); }
+__device__ __forceinline__ float hi16(uint32_t u) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(u >> 16)); }
+// a += w * texel.rgb (one v_fma_mix_f32 per channel)
+__device__ __forceinline__ void madd(C3& a, uint2 t, float w) {
+    a.r = __builtin_fmaf(lo16(t.x), w, a.r);
+    a.g = __builtin_fmaf(hi16(t.x), w, a.g);
+    a.b = __builtin_fmaf(lo16(t.y), w, a.b);
+}
+__device__ __forceinline__ uint2 pack3(const C3& c) { return pack_h4(f4{c.r, c.g, c.b, 1.0f}); }
+
+// Clamp-to-edge tile load: t[r][c] = im[clamp(oy + r)][clamp(ox + c)].
+template <int TW, int TH>
+__device__ __forceinline__ void load_tile(const DImg& im, int ox, int oy, uint2 (*t)[TW], int tid) {
+    for (int i = tid; i < TW * TH; i += 256) {
+        const int r = i / TW, c = i - r * TW;
+        t[r][c] = row_ptr<uint2>(im, clampi(oy + r, 0, im.h - 1))[clampi(ox + c, 0, im.w - 1)];
+    }
+}
+
+// Two horizontally adjacent outputs, one 16-B store when the row allows it.
+__device__ __forceinline__ void store2(const DImg& im, int x, int y, uint2 a, uint2 b, bool vec) {
+    uint2* row = row_ptr_w<uint2>(im, y);
+    if (vec && x + 1 < im.w) {
+        *reinterpret_cast<uint4*>(row + x) = uint4{a.x, a.y, b.x, b.y};
+        return;
+    }
+    row[x] = a;
+    if (x + 1 < im.w) row[x + 1] = b;
+}
+
+// ---- pass footprints (tile-relative; the caller guarantees every index lies inside its tile) -------
+// down 1:1 at tile texel (cx, cy)
+template <int TW>
+__device__ __forceinline__ C3 down11(const uint2 (*t)[TW], int cx, int cy) {
+    C3 a{0.0f, 0.0f, 0.0f};
+    madd(a, t[cy][cx], 0.125f);
+    madd(a, t[cy - 2][cx - 2], 0.03125f);
+    madd(a, t[cy - 2][cx + 2], 0.03125f);
+    madd(a, t[cy + 2][cx - 2], 0.03125f);
+    madd(a, t[cy + 2][cx + 2], 0.03125f);
+    madd(a, t[cy - 2][cx], 0.0625f);
+    madd(a, t[cy][cx - 2], 0.0625f);
+    madd(a, t[cy][cx + 2], 0.0625f);
+    madd(a, t[cy + 2][cx], 0.0625f);
+    madd(a, t[cy - 1][cx - 1], 0.125f);
+    madd(a, t[cy - 1][cx + 1], 0.125f);
+    madd(a, t[cy + 1][cx - 1], 0.125f);
+    madd(a, t[cy + 1][cx + 1], 0.125f);
+    return a;
+}
+
+// down 2:1 from the 6x6 block whose top-left tile texel is (c0, r0)
+__device__ __forceinline__ constexpr float d21_w(int i, int j) {
+    constexpr int A[6] = {1, 1, 2, 2, 1, 1}, B[6] = {0, 1, 1, 1, 1, 0};
+    return (float)(A[i] * A[j] + 4 * B[i] * B[j]) * (1.0f / 128.0f);
+}
+template <int TW>
+__device__ __forceinline__ C3 down21(const uint2 (*t)[TW], int c0, int r0) {
+    C3 a{0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int j = 0; j < 6; ++j)
+#pragma unroll
+        for (int i = 0; i < 6; ++i) madd(a, t[r0 + j][c0 + i], d21_w(i, j));
+    return a;
+}
+
+// up 1:2: the pair of horizontally adjacent outputs (2X, 2X+1) of output row y (parity py) from the
+// 5x4 lower-texel block whose top-left tile texel is (X - 2, Y - 2 + py)
+__device__ __forceinline__ constexpr float u12_w(int parity, int k) {   // k = 0..3 along the 4-texel footprint
+    constexpr int E[4] = {1, 5, 7, 3}, O[4] = {3, 7, 5, 1};
+    return (float)(parity ? O[k] : E[k]) * (1.0f / 16.0f);
+}
+template <int TW>
+__device__ __forceinline__ void up12_pair(const uint2 (*t)[TW], int c0, int r0, int py, C3& even, C3& odd) {
+    even = C3{0.0f, 0.0f, 0.0f};
+    odd = C3{0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const float wy = u12_w(py, j);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            const uint2 v = t[r0 + j][c0 + i];
+            if (i < 4) madd(even, v, u12_w(0, i) * wy);
+            if (i > 0) madd(odd, v, u12_w(1, i - 1) * wy);
+        }
+    }
+}
+
+// up 1:1: the pair of outputs at tile texels (cx, cy), (cx + 1, cy)
+template <int TW>
+__device__ __forceinline__ void up11_pair(const uint2 (*t)[TW], int cx, int cy, C3& a, C3& b) {
+    a = C3{0.0f, 0.0f, 0.0f};
+    b = C3{0.0f, 0.0f, 0.0f};
+    constexpr float w[3] = {1.0f, 2.0f, 1.0f};
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint2 v = t[cy - 1 + j][cx - 1 + i];
+            if (i < 3) madd(a, v, w[i] * w[j] * (1.0f / 16.0f));
+            if (i > 0) madd(b, v, w[i - 1] * w[j] * (1.0f / 16.0f));
+        }
+}
+
+// ================================================================================================
+// W1: emissive (W x H) -> [mip0, W x H, LDS] -> mip1 (W/2 x H/2)
+// ================================================================================================
+constexpr int W1_OW = 32, W1_OH = 8;                          // mip1 outputs per workgroup
+constexpr int W1_MW = 2 * W1_OW + 4, W1_MH = 2 * W1_OH + 4;   // mip0 tile 68 x 20, origin (2 X0 - 2, 2 Y0 - 2)
+constexpr int W1_EW = W1_MW + 4, W1_EH = W1_MH + 4;           // emissive tile 72 x 24, origin (2 X0 - 4, 2 Y0 - 4)
+
+__global__ __launch_bounds__(256) void bloomw_down01(DImg E, DImg M1) {
+    __shared__ uint2 et[W1_EH][W1_EW];
+    __shared__ uint2 mt[W1_MH][W1_MW];
+    const int tid = threadIdx.x;
+    const int X0 = blockIdx.x * W1_OW, Y0 = blockIdx.y * W1_OH;
+    const int mx0 = 2 * X0 - 2, my0 = 2 * Y0 - 2, ex0 = mx0 - 2, ey0 = my0 - 2;
+    load_tile<W1_EW, W1_EH>(E, ex0, ey0, et, tid);
+    __syncthreads();
+    for (int i = tid; i < W1_MW * W1_MH; i += 256) {
+        const int r = i / W1_MW, c = i - r * W1_MW;
+        const int cx = clampi(mx0 + c, 0, E.w - 1) - ex0, cy = clampi(my0 + r, 0, E.h - 1) - ey0;
+        mt[r][c] = pack3(down11<W1_EW>(et, cx, cy));
+    }
+    __syncthreads();
+    const int ox = tid & (W1_OW - 1), oy = tid / W1_OW;
+    const int X = X0 + ox, Y = Y0 + oy;
+    if (X < M1.w && Y < M1.h) row_ptr_w<uint2>(M1, Y)[X] = pack3(down21<W1_MW>(mt, 2 * ox, 2 * oy));
+}
+
+// ================================================================================================
+// W2: mip1 -> [mip2, LDS] -> mip3
+// ================================================================================================
+constexpr int W2_OW = 16, W2_OH = 8;                          // mip3 outputs per workgroup
+constexpr int W2_MW = 2 * W2_OW + 4, W2_MH = 2 * W2_OH + 4;   // mip2 tile 36 x 20
+constexpr int W2_SW = 2 * W2_MW + 4, W2_SH = 2 * W2_MH + 4;   // mip1 tile 76 x 44
+
+__global__ __launch_bounds__(256) void bloomw_down23(DImg S1, DImg M3, int W2, int H2) {
+    __shared__ uint2 st[W2_SH][W2_SW];
+    __shared__ uint2 mt[W2_MH][W2_MW];
+    const int tid = threadIdx.x;
+    const int X0 = blockIdx.x * W2_OW, Y0 = blockIdx.y * W2_OH;
+    const int mx0 = 2 * X0 - 2, my0 = 2 * Y0 - 2, sx0 = 2 * mx0 - 2, sy0 = 2 * my0 - 2;
+    load_tile<W2_SW, W2_SH>(S1, sx0, sy0, st, tid);
+    __syncthreads();
+    for (int i = tid; i < W2_MW * W2_MH; i += 256) {
+        const int r = i / W2_MW, c = i - r * W2_MW;
+        const int qx = clampi(mx0 + c, 0, W2 - 1), qy = clampi(my0 + r, 0, H2 - 1);
+        mt[r][c] = pack3(down21<W2_SW>(st, 2 * qx - 2 - sx0, 2 * qy - 2 - sy0));
+    }
+    __syncthreads();
+    if (tid < W2_OW * W2_OH) {
+        const int ox = tid % W2_OW, oy = tid / W2_OW;
+        const int X = X0 + ox, Y = Y0 + oy;
+        if (X < M3.w && Y < M3.h) row_ptr_w<uint2>(M3, Y)[X] = pack3(down21<W2_MW>(mt, 2 * ox, 2 * oy));
+    }
+}
+
+// ================================================================================================
+// W3: mip3 -> [mip2, LDS] -> mip1 (64 x 16 mip1 outputs per workgroup)
+// ================================================================================================
+constexpr int U_OW = 64, U_OH = 16;
+constexpr int W3_MW = U_OW / 2 + 4, W3_MH = U_OH / 2 + 4;   // mip2 tile 36 x 12, origin (X0/2 - 2, Y0/2 - 2)
+constexpr int W3_SW = W3_MW / 2 + 4, W3_SH = W3_MH / 2 + 4; // mip3 tile 22 x 10, origin (X0/4 - 3, Y0/4 - 3)
+
+// One lower-res texel pair / row of the 1:2 upsample into the LDS tile entries (c, r), (c + 1, r) at
+// intermediate coordinates (qx, qy), (qx + 1, qy), qx even.
+template <int SW, int MW>
+__device__ __forceinline__ void up12_into(const uint2 (*s)[SW], int sx0, int sy0, uint2 (*m)[MW], int c, int r, int qx, int qy,
+                                          int Wq, int Hq) {
+    // a clamped coordinate can break the (even, odd) pairing at the image edges: evaluate each entry
+    // at its own clamped coordinate
+    const int cy = clampi(qy, 0, Hq - 1), py = cy & 1;
+    const int q0 = clampi(qx, 0, Wq - 1), q1 = clampi(qx + 1, 0, Wq - 1);
+    const int r0 = (cy >> 1) - 2 + py - sy0;
+    if ((q0 & 1) == 0 && q1 == q0 + 1) {
+        C3 e, o;
+        up12_pair<SW>(s, (q0 >> 1) - 2 - sx0, r0, py, e, o);
+        m[r][c] = pack3(e);
+        m[r][c + 1] = pack3(o);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int q = k ? q1 : q0;
+            C3 e, o;
+            up12_pair<SW>(s, ((q & ~1) >> 1) - 2 - sx0, r0, py, e, o);
+            m[r][c + k] = pack3((q & 1) ? o : e);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void bloomw_up32(DImg S3, DImg M1, int W2, int H2, bool vec) {
+    __shared__ uint2 st[W3_SH][W3_SW];
+    __shared__ uint2 mt[W3_MH][W3_MW];
+    const int tid = threadIdx.x;
+    const int X0 = blockIdx.x * U_OW, Y0 = blockIdx.y * U_OH;
+    const int mx0 = X0 / 2 - 2, my0 = Y0 / 2 - 2;       // even
+    const int sx0 = mx0 / 2 - 2, sy0 = my0 / 2 - 2;     // mx0 / 2 = floor since mx0 is even
+    load_tile<W3_SW, W3_SH>(S3, sx0, sy0, st, tid);
+    __syncthreads();
+    for (int i = tid; i < (W3_MW / 2) * W3_MH; i += 256) {
+        const int r = i / (W3_MW / 2), c = 2 * (i - r * (W3_MW / 2));
+        up12_into<W3_SW, W3_MW>(st, sx0, sy0, mt, c, r, mx0 + c, my0 + r, W2, H2);
+    }
+    __syncthreads();
+    // mip1 outputs: 32 pairs x 16 rows = 512 pairs, 2 per thread
+    for (int i = tid; i < (U_OW / 2) * U_OH; i += 256) {
+        const int r = i / (U_OW / 2), pc = i - r * (U_OW / 2);
+        const int x = X0 + 2 * pc, y = Y0 + r;
+        if (x >= M1.w || y >= M1.h) continue;
+        const int py = y & 1;
+        C3 e, o;
+        up12_pair<W3_MW>(mt, (x >> 1) - 2 - mx0, (y >> 1) - 2 + py - my0, py, e, o);
+        store2(M1, x, y, pack3(e), pack3(o), vec);
+    }
+}
+
+// ================================================================================================
+// W4: mip1 -> [mip0, LDS] -> output (64 x 16 outputs per workgroup)
+// ================================================================================================
+constexpr int W4_MW = U_OW + 2, W4_MH = U_OH + 2;             // mip0 tile 66 x 18, origin (X0 - 1, Y0 - 1)
+constexpr int W4_SW = U_OW / 2 + 6, W4_SH = U_OH / 2 + 6;     // mip1 tile 38 x 14, origin (X0/2 - 3, Y0/2 - 3)
+
+__global__ __launch_bounds__(256) void bloomw_up10(DImg S1, DImg O, bool vec) {
+    __shared__ uint2 st[W4_SH][W4_SW];
+    __shared__ uint2 mt[W4_MH][W4_MW + 2];   // +2: the pair loop writes whole pairs
+    const int tid = threadIdx.x;
+    const int X0 = blockIdx.x * U_OW, Y0 = blockIdx.y * U_OH;
+    const int mx0 = X0 - 1, my0 = Y0 - 1;
+    const int sx0 = X0 / 2 - 3, sy0 = Y0 / 2 - 3;
+    const int W0 = O.w, H0 = O.h;   // mip0 extent = output extent
+    load_tile<W4_SW, W4_SH>(S1, sx0, sy0, st, tid);
+    __syncthreads();
+    // mip0 entries (c, r) for c = 0..65: pairs start at odd mip0 coordinates (mx0 is odd), so pair
+    // entries as (c + 1, c + 2) with even coordinate first, and entry 0 on its own
+    for (int i = tid; i < (W4_MW / 2) * W4_MH; i += 256) {
+        const int r = i / (W4_MW / 2), k = i - r * (W4_MW / 2);
+        const int c = 2 * k + 1;   // mip0 coordinate mx0 + c = X0 + 2k: even
+        up12_into<W4_SW, W4_MW + 2>(st, sx0, sy0, mt, c, r, mx0 + c, my0 + r, W0, H0);
+    }
+    for (int r = tid; r < W4_MH; r += 256) {   // column 0 (coordinate X0 - 1)
+        const int cy = clampi(my0 + r, 0, H0 - 1), py = cy & 1;
+        const int q = clampi(mx0, 0, W0 - 1);
+        C3 e, o;
+        up12_pair<W4_SW>(st, ((q & ~1) >> 1) - 2 - sx0, (cy >> 1) - 2 + py - sy0, py, e, o);
+        mt[r][0] = pack3((q & 1) ? o : e);
+    }
+    __syncthreads();
+    for (int i = tid; i < (U_OW / 2) * U_OH; i += 256) {
+        const int r = i / (U_OW / 2), pc = i - r * (U_OW / 2);
+        const int x = X0 + 2 * pc, y = Y0 + r;
+        if (x >= O.w || y >= O.h) continue;
+        C3 a, b;
+        up11_pair<W4_MW + 2>(mt, x - mx0, y - my0, a, b);
+        store2(O, x, y, pack3(a), pack3(b), vec);
+    }
+}
+
+bool a16(const soc_img& im) { return im.pitch_bytes % 16 == 0 && reinterpret_cast<uintptr_t>(im.data) % 16 == 0; }
+
+}  // namespace
+
+int launch_bloom_weighted(const soc_img& emissive, const soc_img* mips, const soc_img& output, hipStream_t s, int stage) {
+    const DImg E = dimg(emissive), M1 = dimg(mips[1]), M3 = dimg(mips[3]), O = dimg(output);
+    if (stage == 0 || stage == 1) {
+        dim3 g(ceil_div(mips[1].width, W1_OW), ceil_div(mips[1].height, W1_OH));
+        bloomw_down01<<<g, 256, 0, s>>>(E, M1);
+    }
+    if (stage == 0 || stage == 2) {
+        dim3 g(ceil_div(mips[3].width, W2_OW), ceil_div(mips[3].height, W2_OH));
+        bloomw_down23<<<g, 256, 0, s>>>(M1, M3, mips[2].width, mips[2].height);
+    }
+    if (stage == 0 || stage == 3) {
+        dim3 g(ceil_div(mips[1].width, U_OW), ceil_div(mips[1].height, U_OH));
+        bloomw_up32<<<g, 256, 0, s>>>(M3, M1, mips[2].width, mips[2].height, a16(mips[1]));
+    }
+    if (stage == 0 || stage == 4) {
+        dim3 g(ceil_div(output.width, U_OW), ceil_div(output.height, U_OH));
+        bloomw_up10<<<g, 256, 0, s>>>(M1, O, a16(output));
+    }
+    return check_launch("bloom_weighted");
+}
+
+}  // namespace soc

@@ -488,6 +488,17 @@ struct soc_renderer {
 };
 
 namespace {
+using PassFn = std::function<int(const soc_globals*, hipStream_t)>;
+
+void add_pass(soc_renderer* r, std::string name, std::string group, int phase, PassFn fn) {
+    soc_renderer::Pass p;
+    p.name = std::move(name);
+    p.group = std::move(group);
+    p.phase = phase;
+    p.run = std::move(fn);
+    r->passes.push_back(std::move(p));
+}
+
 int ensure_hist_scratch(soc_renderer* r) {
     if (r->hist_scratch) return SOC_OK;
     if (hipMalloc((void**)&r->hist_scratch, SOC_HISTOGRAM_SCRATCH_WORDS * sizeof(uint32_t)) != hipSuccess) {
@@ -499,24 +510,33 @@ int ensure_hist_scratch(soc_renderer* r) {
     return SOC_OK;
 }
 
+// Bloom passes of the graph (renderer.cpp:1024-1062); build_passes_tail adds the rest.
 void build_passes(soc_renderer* r) {
     auto& I = r->img;
-    auto add = [&](std::string name, std::string group, int phase, std::function<int(const soc_globals*, hipStream_t)> fn) {
-        soc_renderer::Pass p;
-        p.name = std::move(name);
-        p.group = std::move(group);
-        p.phase = phase;
-        p.run = std::move(fn);
-        r->passes.push_back(std::move(p));
+    auto add = [r](std::string name, std::string group, int phase, PassFn fn) {
+        add_pass(r, std::move(name), std::move(group), phase, std::move(fn));
     };
     const int nm = 4;
     // renderer.cpp:1024-1062
     const soc_img& bloom_dst = I.bloom_output.data ? I.bloom_output : I.emissive;
-    const bool fused = !(r->flags & SOC_RENDERER_UNFUSED_BLOOM) && bloom_fused_applicable(I.emissive, I.bloom_mips, nm, bloom_dst);
+    const bool chain_ok = bloom_fused_applicable(I.emissive, I.bloom_mips, nm, bloom_dst);
+    if (chain_ok && !(r->flags & (SOC_RENDERER_EXACT_BLOOM | SOC_RENDERER_UNFUSED_BLOOM))) {
+        // weighted form (bloom_w.hip): 4 launches, mip0 / mip2 only in LDS, within the RGBA16F tolerance
+        static const char* names[4] = {"BloomDownsample - 0+1", "BloomDownsample - 2+3", "BloomUpsample - 3+2",
+                                       "BloomUpsample - 1+0"};
+        for (int st = 1; st <= 4; ++st)
+            add(names[st - 1], "Bloom", SOC_PHASE_PRE_EXPOSURE, [r, st](const soc_globals* g, hipStream_t s) {
+                const soc_img& dst = r->img.bloom_output.data ? r->img.bloom_output : r->img.emissive;
+                return soc_bloom_weighted_stage(g, r->img.emissive, r->img.bloom_mips, 4, dst, st, (soc_stream)s);
+            });
+        return;
+
+    }
+    const bool fused = !(r->flags & SOC_RENDERER_UNFUSED_BLOOM) && chain_ok;
     if (fused) {
-        // downsweep as 2 fused stages (mip0 / mip2 of the downsweep stay in LDS; bloom_fused.hip); the
-        // upsweep as the reference's 4 passes, which are faster than fused stages 3-4 on gfx950.
-        // Every mip and the output end up with exactly the 8-pass chain's bits.
+        // bit-exact: downsweep as 2 fused stages (mip0 / mip2 of the downsweep stay in LDS;
+        // bloom_fused.hip), the upsweep as the reference's 4 passes. Every mip and the output end up
+        // with exactly the 8-pass chain's bits.
         add("BloomDownsample - 0+1", "Bloom", SOC_PHASE_PRE_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
             return soc_bloom_fused_stage(g, r->img.emissive, r->img.bloom_mips, 4, r->img.emissive, 1, (soc_stream)s);
         });
@@ -540,6 +560,13 @@ void build_passes(soc_renderer* r) {
         const soc_img& dst = r->img.bloom_output.data ? r->img.bloom_output : r->img.emissive;
         return soc_bloom_upsample(g, r->img.bloom_mips[0], dst, (soc_stream)s);
     });
+}
+
+void build_passes_tail(soc_renderer* r) {
+    auto add = [r](std::string name, std::string group, int phase, PassFn fn) {
+        add_pass(r, std::move(name), std::move(group), phase, std::move(fn));
+    };
+    auto& I = r->img;
     // renderer.cpp:1064-1079
     add("SSAOGeneration", "Ambient Occlusion", SOC_PHASE_PRE_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
         return soc_ssao_generation(g, r->img.depth, r->img.normal, r->img.ssao, r->img.ssao_noise_table, (soc_stream)s);
@@ -622,6 +649,7 @@ extern "C" soc_renderer* soc_renderer_create(const soc_frame_images* images, uin
     r->flags = flags;
     r->async = !(flags & SOC_RENDERER_SERIAL);
     build_passes(r);
+    build_passes_tail(r);
     if ((flags & SOC_RENDERER_TIMING) && soc_renderer_set_pass_timing(r, -1, 1) != SOC_OK) {
         soc_renderer_destroy(r);
         return nullptr;

@@ -63,5 +63,7 @@ void mat4_mul_host(float out[16], const float a[16], const float b[16]);
 // Fused bloom chain (bloom_fused.hip).
 bool bloom_fused_applicable(const soc_img& emissive, const soc_img* mips, int mip_count, const soc_img& output);
 int launch_bloom_fused(const soc_img& emissive, const soc_img* mips, const soc_img& output, hipStream_t s, int stage);
+// Weighted-form bloom chain (bloom_w.hip): same applicability as the fused chain.
+int launch_bloom_weighted(const soc_img& emissive, const soc_img* mips, const soc_img& output, hipStream_t s, int stage);
 
 }  // namespace soc

@@ -116,6 +116,56 @@ def test_bloom_fused_stages_equal_eight_passes(soc, W, H):
     assert torch.equal(mips[0][..., :3].view(torch.int16), ref_mips[0][..., :3].view(torch.int16))
 
 
+@pytest.mark.parametrize("W,H", [(64, 40), (200, 136), (968, 552), (1920, 1080), (3840, 2160)])
+def test_bloom_weighted_chain(soc, W, H):
+    """The weighted-form chain (bloom_w.hip, 4 kernels) against the reference's 8 separate passes
+    (bit-exact to the oracle): output and the observable mips (1 upswept, 3 downswept) within the
+    RGBA16F tolerance, and almost all texels bit-identical (the weights are the taps' exact weights;
+    only the fp32 rounding order differs). Stage by stage equals the whole chain; the emissive input of
+    a separate output is untouched."""
+    g = globals_for(W, H)
+    em = dev(random_rgba16(H, W, seed=23, hi=16.0))
+    shapes = [(H >> i, W >> i, 4) for i in range(4)]
+    ref = [torch.zeros(sh, dtype=torch.float16, device=DEV) for sh in shapes]
+    ref_out = torch.zeros_like(em)
+    soc.bloom_downsample(g, em, ref[0])
+    for i in range(3):
+        soc.bloom_downsample(g, ref[i], ref[i + 1])
+    ref3 = ref[3].clone()
+    for i in range(3, 0, -1):
+        soc.bloom_upsample(g, ref[i], ref[i - 1])
+    soc.bloom_upsample(g, ref[0], ref_out)
+    em_before = em.clone()
+    mips = [torch.full(sh, 7.0, dtype=torch.float16, device=DEV) for sh in shapes]
+    out = torch.zeros_like(em)
+    soc.bloom_weighted_stage(g, em, mips, out, 0)
+    mips2 = [torch.zeros(sh, dtype=torch.float16, device=DEV) for sh in shapes]
+    out2 = torch.zeros_like(em)
+    for st in (1, 2, 3, 4):
+        soc.bloom_weighted_stage(g, em, mips2, out2, st)
+    torch.cuda.synchronize()
+    assert torch.equal(em, em_before)
+    assert torch.equal(out, out2) and torch.equal(mips[1], mips2[1]) and torch.equal(mips[3], mips2[3])
+    for got, want in ((out, ref_out), (mips[1], ref[1]), (mips[3], ref3)):
+        g_, w_ = host(got)[..., :3], host(want)[..., :3]
+        assert f16_close(g_, w_).all()
+        assert (g_.view(np.uint16) == w_.view(np.uint16)).mean() >= 0.99
+    assert torch.all(mips[0] == 7.0) and torch.all(mips[2] == 7.0)   # scratch mips are not written
+
+
+def test_bloom_weighted_in_place(soc):
+    """output == emissive (the reference's in-place bloom) gives the separate-output result."""
+    W, H = 968, 552
+    g = globals_for(W, H)
+    em = dev(random_rgba16(H, W, seed=29, hi=4.0))
+    shapes = [(H >> i, W >> i, 4) for i in range(4)]
+    out = torch.zeros_like(em)
+    soc.bloom_weighted_stage(g, em, [torch.zeros(sh, dtype=torch.float16, device=DEV) for sh in shapes], out, 0)
+    soc.bloom_weighted_stage(g, em, [torch.zeros(sh, dtype=torch.float16, device=DEV) for sh in shapes], em, 0)
+    torch.cuda.synchronize()
+    assert torch.equal(em, out)
+
+
 # ------------------------------------------------------------------------------------------------ ssao
 @pytest.mark.parametrize("W,H", [(128, 72), (97, 55), (1920, 1080)])
 def test_ssao_generation(soc, oracle, W, H):
