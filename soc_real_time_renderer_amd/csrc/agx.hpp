@@ -10,25 +10,36 @@ namespace soc {
 struct TmParams {
     Mat3 M, Minv;
     float linear, peak, saturation;
+    // DualSection constants (uniform, tm_params_finish): S = peak linear, kexp = -C / peak with
+    // C = peak / (peak - S), folded into exp2: x >= S -> peak - (peak - S) exp2((x - S) kexp log2 e)
+    float S, peak_minus_S, kexp2;
 };
 
 // DualSection, :127-137
-__device__ __forceinline__ float dual_section(float x, float linear, float peak) {
-    const float S = peak * linear;
-    if (x < S) return x;
-    const float C = peak / (peak - S);
-    return peak - (peak - S) * __expf((-C * (x - S)) / peak);
+__device__ __forceinline__ float dual_section(const TmParams& p, float x) {
+    if (x < p.S) return x;
+    return p.peak - p.peak_minus_S * __builtin_amdgcn_exp2f((x - p.S) * p.kexp2);
 }
 
 __device__ __forceinline__ f3 agx(const TmParams& p, f4 c, float expo) {
     f3 w = f3{fmaxf(c.x, 0.0f), fmaxf(c.y, 0.0f), fmaxf(c.z, 0.0f)} * expo;
     w = mul(p.M, w);
-    w = f3{clampf(dual_section(w.x, p.linear, p.peak), 0.0f, 1.0f), clampf(dual_section(w.y, p.linear, p.peak), 0.0f, 1.0f),
-           clampf(dual_section(w.z, p.linear, p.peak), 0.0f, 1.0f)};
-    const float ds = dot3(w, f3{0.2126729f, 0.7151522f, 0.0721750f});
-    w = f3{mixf(ds, w.x, p.saturation), mixf(ds, w.y, p.saturation), mixf(ds, w.z, p.saturation)};
-    w = f3{clampf(w.x, 0.0f, 1.0f), clampf(w.y, 0.0f, 1.0f), clampf(w.z, 0.0f, 1.0f)};
+    w = f3{clampf(dual_section(p, w.x), 0.0f, 1.0f), clampf(dual_section(p, w.y), 0.0f, 1.0f),
+           clampf(dual_section(p, w.z), 0.0f, 1.0f)};
+    if (p.saturation != 1.0f) {   // mix(ds, w, 1) == w and w is already clamped: exact skip (uniform branch)
+        const float ds = dot3(w, f3{0.2126729f, 0.7151522f, 0.0721750f});
+        w = f3{mixf(ds, w.x, p.saturation), mixf(ds, w.y, p.saturation), mixf(ds, w.z, p.saturation)};
+        w = f3{clampf(w.x, 0.0f, 1.0f), clampf(w.y, 0.0f, 1.0f), clampf(w.z, 0.0f, 1.0f)};
+    }
     return mul(p.Minv, w);
+}
+
+// Host: the uniform DualSection constants of a TmParams whose linear / peak / saturation are set.
+inline void tm_params_finish(TmParams& p) {
+    p.S = p.peak * p.linear;
+    p.peak_minus_S = p.peak - p.S;
+    const float C = p.peak / (p.peak - p.S);
+    p.kexp2 = (-C / p.peak) * 1.44269504088896341f;
 }
 
 }  // namespace soc

@@ -187,9 +187,10 @@ __device__ __forceinline__ h2 as_h2(uint32_t u) { return __builtin_bit_cast(h2, 
 __device__ __forceinline__ v2f h2f2(h2 h) { return v2f{(float)h.x, (float)h.y}; }
 
 // Bilinear sample with the contract's taps; the lerps are fma(w, b - a, a) (within the RGBA16F
-// tolerance of the pass; the texel selection is exactly the contract's). 16-B row-pair loads.
-__device__ __forceinline__ void sample_pair_rows(const DImg& im, float u, float v, v2f& xy, v2f& zw, bool need_zw) {
-    const Axis ax = axis_clamp(u, im.w), ay = axis_clamp(v, im.h);
+// tolerance of the pass; the texel selection is exactly the contract's). 16-B row-pair loads. The
+// axes are computed once by the caller for the history colour and velocity (same extent).
+__device__ __forceinline__ void sample_pair_rows(const DImg& im, const Axis& ax, const Axis& ay, v2f& xy, v2f& zw,
+                                                 bool need_zw) {
     const u4a8 r0 = *reinterpret_cast<const u4a8*>(row_ptr<uint2>(im, ay.i0) + ax.i0);
     const u4a8 r1 = *reinterpret_cast<const u4a8*>(row_ptr<uint2>(im, ay.i1) + ax.i0);
     const v2f wx = v2f{ax.w, ax.w}, wy = v2f{ay.w, ay.w};
@@ -202,6 +203,12 @@ __device__ __forceinline__ void sample_pair_rows(const DImg& im, float u, float 
         const v2f a = h2f2(as_h2(r0.y)), b = h2f2(as_h2(r0.w)), c = h2f2(as_h2(r1.y)), d = h2f2(as_h2(r1.w));
         zw = lerp2(lerp2(a, b, wx), lerp2(c, d, wx), wy);
     }
+}
+
+// 1/4 a + 1/2 b + 1/4 c of two f16 channels, fp32 (v_fma_mix_f32 straight from the packed halves)
+__device__ __forceinline__ v2f gauss_col(h2 a, h2 b, h2 c) {
+    return v2f{__builtin_fmaf((float)c.x, 0.25f, __builtin_fmaf((float)b.x, 0.5f, (float)a.x * 0.25f)),
+               __builtin_fmaf((float)c.y, 0.25f, __builtin_fmaf((float)b.y, 0.5f, (float)a.y * 0.25f))};
 }
 
 // Same per-pixel result as taa_fast within the RGBA16F tolerance: the neighbourhood min/max run on
@@ -221,7 +228,7 @@ __global__ __launch_bounds__(256) void taa_pair2(DImg target, DImg cur, DImg pre
                                                  DImg vel_out, TaaParams p, TmOut tm) {
     int tbx, tby;
     xcd_tile(p.swz, tbx, tby);
-    const int x0 = (tbx * BX + threadIdx.x) * 2, y = tby * BY + threadIdx.y;
+    const int x0 = (tbx * (int)blockDim.x + threadIdx.x) * 2, y = tby * (int)blockDim.y + threadIdx.y;
     if (x0 >= target.w || y >= target.h) return;
     const float exposure = TM ? tm.ae->exposure : 0.0f;
     const int W = target.w, H = target.h;
@@ -261,9 +268,8 @@ __global__ __launch_bounds__(256) void taa_pair2(DImg target, DImg cur, DImg pre
         nzw[c] = __builtin_elementwise_min(__builtin_elementwise_min(Czw[0][c], Czw[1][c]), Czw[2][c]);
         xxy[c] = __builtin_elementwise_max(__builtin_elementwise_max(Cxy[0][c], Cxy[1][c]), Cxy[2][c]);
         xzw[c] = __builtin_elementwise_max(__builtin_elementwise_max(Czw[0][c], Czw[1][c]), Czw[2][c]);
-        const v2f q = v2f{0.25f, 0.25f}, hlf = v2f{0.5f, 0.5f};
-        sxy[c] = __builtin_elementwise_fma(h2f2(Cxy[2][c]), q, __builtin_elementwise_fma(h2f2(Cxy[1][c]), hlf, h2f2(Cxy[0][c]) * q));
-        szw[c] = __builtin_elementwise_fma(h2f2(Czw[2][c]), q, __builtin_elementwise_fma(h2f2(Czw[1][c]), hlf, h2f2(Czw[0][c]) * q));
+        sxy[c] = gauss_col(Cxy[0][c], Cxy[1][c], Cxy[2][c]);
+        szw[c] = gauss_col(Czw[0][c], Czw[1][c], Czw[2][c]);
     }
     const int colx[4] = {xl, x0, x0 + 1, xr};
     const float v = centre_uv(y, H);
@@ -302,13 +308,14 @@ __global__ __launch_bounds__(256) void taa_pair2(DImg target, DImg cur, DImg pre
         float accum = p.accum0;
         const float vx = u - velx, vy = v - vely;
         v2f axy, azw, pxy, unused;
-        sample_pair_rows(prev, vx, vy, axy, azw, true);
+        const Axis hax = axis_clamp(vx, prev.w), hay = axis_clamp(vy, prev.h);   // prev and pvel: same extent
+        sample_pair_rows(prev, hax, hay, axy, azw, true);
         if (vx < 0.0f || vy < 0.0f || vx > 1.0f || vy > 1.0f) accum = 1.0f;
         axy = __builtin_elementwise_min(__builtin_elementwise_max(axy, h2f2(mnxy)), h2f2(mxxy));
         azw = __builtin_elementwise_min(__builtin_elementwise_max(azw, h2f2(mnzw)), h2f2(mxzw));
         const v2f ac = v2f{accum, accum}, ic = v2f{1.0f - accum, 1.0f - accum};
         const v2f oxy = __builtin_elementwise_fma(cxy, ac, axy * ic), ozw = __builtin_elementwise_fma(czw, ac, azw * ic);
-        sample_pair_rows(pvel, vx, vy, pxy, unused, false);
+        sample_pair_rows(pvel, hax, hay, pxy, unused, false);
         const float dvx = pxy.x - velx, dvy = pxy.y - vely;
         const float vlen = __builtin_amdgcn_sqrtf(__builtin_fmaf(dvx, dvx, dvy * dvy));
         const float dis = clampf((vlen - 0.001f) * 10.0f, 0.0f, 1.0f);
@@ -413,10 +420,12 @@ int taa_launch(const soc_globals* g, soc_img target, soc_img current_color, soc_
     const bool pair = fast && W % 2 == 0 && a16(target) && a16(current_color) && a16(current_velocity) &&
                       (reinterpret_cast<uintptr_t>(depth.data) & 7u) == 0 && (depth.pitch_bytes & 7) == 0 &&
                       (!velocity_history_out.data || a16(velocity_history_out)) && previous_color.width >= 2 &&
-                      previous_velocity.width >= 2;
+                      previous_velocity.width == previous_color.width && previous_velocity.height == previous_color.height;
     if (tm && !pair) return 1;
     if (pair) {
-        dim3 g2(ceil_div(W / 2, BX), ceil_div(H, BY));
+        // 32 x 8 lanes (64 x 8 pixels): the 3-row neighbourhood reloads 10 rows per 8 instead of 6 per 4
+        const int by = tuning_knob("SOC_TAA_BY", 8), bxl = 256 / by;
+        dim3 blk(bxl, by), g2(ceil_div(W / 2, bxl), ceil_div(H, by));
         if (tm)
             taa_pair2<true><<<g2, blk, 0, hs(stream)>>>(dimg(target), dimg(current_color), dimg(previous_color),
                                                        dimg(current_velocity), dimg(previous_velocity), dimg(depth), vo, p, *tm);
@@ -462,6 +471,7 @@ extern "C" int soc_temporal_antialiasing_tone_mapping(const soc_globals* g, soc_
         tm.p.linear = g->agxDs_linear_section;
         tm.p.peak = g->peak;
         tm.p.saturation = g->saturation;
+        tm_params_finish(tm.p);
         rc = taa_launch(g, target, current_color, previous_color, current_velocity, previous_velocity, depth,
                         velocity_history_out, &tm, stream);
         if (rc <= 0) return rc;   // launched (or failed validation)

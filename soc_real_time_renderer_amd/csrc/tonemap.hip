@@ -90,6 +90,7 @@ extern "C" int soc_tone_mapping(const soc_globals* g, soc_img color, const soc_a
     p.linear = g->agxDs_linear_section;
     p.peak = g->peak;
     p.saturation = g->saturation;
+    tm_params_finish(p);
     switch (target.format) {
     case SOC_FMT_RGBA8_UNORM: launch<SOC_FMT_RGBA8_UNORM>(color, target, ae, p, hs(stream)); break;
     case SOC_FMT_RGBA8_SRGB: launch<SOC_FMT_RGBA8_SRGB>(color, target, ae, p, hs(stream)); break;

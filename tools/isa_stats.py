@@ -10,7 +10,7 @@ src = sys.argv[1]
 pat = sys.argv[2] if len(sys.argv) > 2 else ""
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 with tempfile.TemporaryDirectory() as d:
-    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-mcode-object-version=5",
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-mcode-object-version=5"] + os.environ.get("ISA_FLAGS", "").split() + [
                     "--cuda-device-only", "-S", "-o", os.path.join(d, "k.s"), src], check=True)
     s = open(os.path.join(d, "k.s")).read()
 meta = dict(re.findall(r"\.name:\s+(\S+)\n(?:.*\n){0,40}?\s+\.vgpr_count:\s+(\d+)", s))
