@@ -118,6 +118,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", choices=("c3", "c4"), default="c3",
+                    help="c3: Sponza-proxy full chain (the metric's config); c4: terrain + atmosphere/clouds")
     ap.add_argument("--width", type=int, default=3840)
     ap.add_argument("--height", type=int, default=2160)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -131,10 +133,12 @@ def main():
     multi_gpu.init(device)
     W, H = args.width, args.height
 
-    # ---- inputs (synthetic Sponza-proxy G-buffer + 4096^2 sun shadow map), resident in HBM ----
-    g = make_globals(W, H, multi_gpu.camera_for_rank(rank))
-    gb = scene.gbuffer(g, W, H)
-    shadow = scene.shadow_map(g, 4096)
+    # ---- inputs (synthetic Sponza-proxy or terrain G-buffer + 4096^2 sun shadow map), resident in HBM ----
+    terrain = args.config == "c4"
+    scene_id = scene.TERRAIN if terrain else scene.SPONZA_PROXY
+    g = make_globals(W, H, (multi_gpu.terrain_camera_for_rank if terrain else multi_gpu.camera_for_rank)(rank))
+    gb = scene.gbuffer(g, W, H, scene_id=scene_id)
+    shadow = scene.shadow_map(g, 4096, scene_id=scene_id)
     noise = scene.noise_texture()
     f_sky = float((gb["depth"] == 1.0).mean())
     fr = soc.alloc_frame(W, H, device, bloom_output=True)
@@ -218,9 +222,11 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32 (fp16/unorm8/d32 storage)",
-        "data": "synthetic (Sponza-proxy G-buffer + 4096^2 sun shadow map, scene_synth.c)",
-        "config": {"workload": f"Sponza-proxy {W}x{H} full screen-space chain (C3): bloom x8, SSAO+blur, "
-                               f"clouds, composition, auto-exposure, TAA, AgX tone map",
+        "data": f"synthetic ({'fBm terrain (seed 0x7E44)' if terrain else 'Sponza-proxy'} G-buffer + 4096^2 sun "
+                f"shadow map, scene_synth.c)",
+        "config": {"workload": f"{'Terrain' if terrain else 'Sponza-proxy'} {W}x{H} full screen-space chain "
+                               f"({args.config.upper()}): bloom x8, SSAO+blur, clouds, composition, auto-exposure, "
+                               f"TAA, AgX tone map",
                    "resolution": [W, H], "f_sky": round(f_sky, 4), "parallelism": f"frame-per-gpu x{world}",
                    "histogram_allreduce": world > 1,
                    "sky_lane": "CloudRendering on a concurrent stream, joined before Composition"},

@@ -17,6 +17,8 @@ import torch
 import torch.distributed as dist
 
 SPONZA_CAMERA = ((-14.0, 2.2, 0.3), (0.0, -0.42, 0.0))
+# config C4: above the fBm terrain looking down the diagonal, f_sky ~= 0.5 at 16:9
+TERRAIN_CAMERA = ((20.0, 34.0, 20.0), (0.785, 0.6, 0.0))
 
 
 def env() -> Tuple[int, int, int]:
@@ -42,6 +44,15 @@ def camera_for_rank(rank: int):
     pos = (float(rng.uniform(-15.0, 12.0)), float(rng.uniform(1.5, 4.0)), float(rng.uniform(-2.5, 2.5)))
     rot = (float(rng.choice([0.0, math.pi])) + float(rng.uniform(-0.3, 0.3)), float(rng.uniform(-0.6, -0.2)), 0.0)
     return pos, rot
+
+
+def terrain_camera_for_rank(rank: int):
+    """Rank 0: the canonical C4 view; others: seeded headings and heights over the terrain (seed 0xC4 + rank)."""
+    if rank == 0:
+        return TERRAIN_CAMERA
+    rng = np.random.default_rng(0xC4 + rank)
+    pos = (float(rng.uniform(15.0, 30.0)), float(rng.uniform(32.0, 40.0)), float(rng.uniform(15.0, 30.0)))
+    return pos, (0.785 + float(rng.uniform(-0.5, 0.5)), float(rng.uniform(0.5, 0.7)), 0.0)
 
 
 def exposure_pixels(world: int, width: int, height: int) -> Tuple[int, bool]:

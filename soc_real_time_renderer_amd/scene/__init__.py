@@ -17,6 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(HERE), "lib", "libsoc_scene.so")
 NOISE_PATH = os.path.join(os.path.dirname(HERE), "data", "clouds_noise_64x64.u8")
 SPONZA_PROXY = 0
+TERRAIN = 1          # config C4: fBm terrain grid (seed 0x7E44) rasterised on the host
 
 _LIB = None
 

@@ -37,6 +37,8 @@ typedef struct {
     int n;
 } scene;
 
+enum { SCENE_SPONZA_PROXY = 0, SCENE_TERRAIN = 1 };
+
 enum { M_FLOOR = 0, M_WALL, M_PILLAR, M_GALLERY, M_ROOF, M_LAMP, M_BANNER, M_STATUE, M_COUNT };
 
 static void addbox(scene* s, float x0, float y0, float z0, float x1, float y1, float z1, int mat) {
@@ -178,6 +180,220 @@ static void material(int mat, v3 p, v3 n, float* alb, float* emi) {
     if (mat == M_BANNER && fv > 0.45f && fv < 0.55f) { emi[0] = 0.9f; emi[1] = 0.6f; emi[2] = 0.1f; }
 }
 
+/* ---------------------------------------------------------------------------------------------------
+ * Scene 1: terrain proxy for config C4. The reference draws a 100 x 100 vertex grid of
+ * quad patches over [0, terrain_scale]^2 (renderer.cpp:194-220), tessellated at the maximum level 3
+ * (draw_terrain.inl:150-163) and displaced by (height - terrain_midpoint) * terrain_height_scale
+ * (:185-191); its Terrain/heightmap.exr is missing from the mount, so the height is a deterministic
+ * fBm (seed 0x7E44). The tessellated grid (298 x 298 vertices, 176,418 triangles) is rasterised on the
+ * host: pixel centres, edge functions with a top-left fill rule, z_ndc interpolated affinely in screen
+ * space, LESS_OR_EQUAL in draw order (later triangles win ties), fragments with z_ndc outside [0, 1]
+ * clipped. The G-buffer follows draw_terrain.inl:196-222: albedo (procedural grass / rock / snow by
+ * height and slope, alpha 1), normal = the surface normal (the reference writes its normal map's
+ * texel; the map is generated from the missing heightmap), velocity 0 (as the reference writes),
+ * emissive left at its clear (0, 0, 0, 1).
+ * ------------------------------------------------------------------------------------------------- */
+#define T_SEGS 297                 /* 99 patches x tessellation level 3 */
+#define T_NV (T_SEGS + 1)
+
+static inline float vnoise_hash(int x, int y, uint32_t seed) {
+    uint32_t h = (uint32_t)x * 0x8da6b343u ^ (uint32_t)y * 0xd8163841u ^ seed * 0xcb1ab31fu;
+    h ^= h >> 15; h *= 0x2c1b3c6du; h ^= h >> 12; h *= 0x297a2d39u; h ^= h >> 15;
+    return (float)(h & 0xffffffu) / 16777215.0f;
+}
+
+static float vnoise(float x, float y, uint32_t seed) {
+    const float fx = floorf(x), fy = floorf(y);
+    const int ix = (int)fx, iy = (int)fy;
+    float tx = x - fx, ty = y - fy;
+    tx = tx * tx * (3.0f - 2.0f * tx);
+    ty = ty * ty * (3.0f - 2.0f * ty);
+    const float a = vnoise_hash(ix, iy, seed), b = vnoise_hash(ix + 1, iy, seed);
+    const float c = vnoise_hash(ix, iy + 1, seed), d = vnoise_hash(ix + 1, iy + 1, seed);
+    return (a + (b - a) * tx) + ((c + (d - c) * tx) - (a + (b - a) * tx)) * ty;
+}
+
+/* heightmap value in [0.15, 0.65) at terrain uv in [0, 1]^2: squared fBm (valleys and ridges) */
+static float terrain_height(float u, float v) {
+    float h = 0.0f, amp = 0.5f, freq = 4.0f;
+    for (int o = 0; o < 6; ++o) {
+        h += amp * vnoise(u * freq, v * freq, 0x7E44u + (uint32_t)o);
+        amp *= 0.5f;
+        freq *= 2.03f;
+    }
+    h /= 0.984375f;
+    return 0.15f + 0.5f * h * h;
+}
+
+typedef struct {
+    v3 p[T_NV * T_NV];           /* world positions */
+    int built;
+    float scale_x, scale_z, hscale, mid, off[3];
+} terrain_mesh;
+static terrain_mesh g_terrain;
+
+static const terrain_mesh* get_terrain(const soc_globals* g) {
+    terrain_mesh* t = &g_terrain;
+    if (t->built && t->scale_x == g->terrain_scale[0] && t->scale_z == g->terrain_scale[1] && t->hscale == g->terrain_height_scale &&
+        t->mid == g->terrain_midpoint && t->off[0] == g->terrain_offset[0] && t->off[1] == g->terrain_offset[1] &&
+        t->off[2] == g->terrain_offset[2])
+        return t;
+    t->scale_x = g->terrain_scale[0];
+    t->scale_z = g->terrain_scale[1];
+    t->hscale = g->terrain_height_scale;
+    t->mid = g->terrain_midpoint;
+    memcpy(t->off, g->terrain_offset, sizeof t->off);
+#pragma omp parallel for
+    for (int j = 0; j < T_NV; ++j)
+        for (int i = 0; i < T_NV; ++i) {
+            const float u = (float)i / (float)T_SEGS, v = (float)j / (float)T_SEGS;
+            const float h = (terrain_height(u, v) - t->mid) * t->hscale;
+            t->p[j * T_NV + i] = V(u * t->scale_x - t->off[0], t->off[1] + h, v * t->scale_z - t->off[2]);
+        }
+    t->built = 1;
+    return t;
+}
+
+static v3 terrain_normal(const terrain_mesh* t, float u, float v) {
+    const float e = 1.0f / 1024.0f;
+    const float hx = (terrain_height(u + e, v) - terrain_height(u - e, v)) * t->hscale / (2.0f * e * t->scale_x);
+    const float hz = (terrain_height(u, v + e) - terrain_height(u, v - e)) * t->hscale / (2.0f * e * t->scale_z);
+    return nrm(V(-hx, 1.0f, -hz));
+}
+
+static void terrain_material(float height, v3 n, float u, float v, float* alb) {
+    const float slope = 1.0f - n.y;
+    const float grain = 0.85f + 0.3f * vnoise(u * 900.0f, v * 900.0f, 0x51u);
+    float c[3] = {0.24f, 0.36f, 0.12f};                                   /* grass */
+    if (slope > 0.25f) { c[0] = 0.42f; c[1] = 0.38f; c[2] = 0.33f; }     /* rock */
+    if (height > 24.0f && slope < 0.35f) { c[0] = 0.88f; c[1] = 0.90f; c[2] = 0.93f; }   /* snow */
+    for (int k = 0; k < 3; ++k) alb[k] = c[k] * grain;
+}
+
+/* Rasterise the terrain grid through `pv` (column-major clip transform) into W x H: per pixel the
+ * winning triangle id (-1: none) and its perspective-correct barycentrics (b1, b2). */
+static void terrain_raster(const terrain_mesh* t, const float* pv, int W, int H, float* depth, int* tri, float* b1o,
+                           float* b2o) {
+    const int ntri = 2 * T_SEGS * T_SEGS;
+    float* sx = (float*)malloc(sizeof(float) * 4 * T_NV * T_NV);   /* screen x, y, z_ndc, 1/w per vertex */
+#pragma omp parallel for
+    for (int k = 0; k < T_NV * T_NV; ++k) {
+        float c[4];
+        mat_vec(pv, t->p[k].x, t->p[k].y, t->p[k].z, 1.0f, c);
+        float* o = sx + 4 * k;
+        if (c[3] <= 1e-6f) { o[3] = 0.0f; continue; }
+        const float iw = 1.0f / c[3];
+        o[0] = (c[0] * iw * 0.5f + 0.5f) * (float)W;   /* uv = ndc * 0.5 + 0.5, y = 0 at the top row */
+        o[1] = (c[1] * iw * 0.5f + 0.5f) * (float)H;
+        o[2] = c[2] * iw;
+        o[3] = iw;
+    }
+    const int TS = 32, tx_n = (W + TS - 1) / TS, ty_n = (H + TS - 1) / TS;
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int tile = 0; tile < tx_n * ty_n; ++tile) {
+        const int x0 = (tile % tx_n) * TS, y0 = (tile / tx_n) * TS;
+        const int x1 = x0 + TS < W ? x0 + TS : W, y1 = y0 + TS < H ? y0 + TS : H;
+        for (int y = y0; y < y1; ++y)
+            for (int x = x0; x < x1; ++x) {
+                depth[(size_t)y * W + x] = 1.0f;
+                tri[(size_t)y * W + x] = -1;
+            }
+        for (int id = 0; id < ntri; ++id) {
+            const int q = id >> 1, qi = q % T_SEGS, qj = q / T_SEGS;
+            const int v00 = qj * T_NV + qi, v10 = v00 + 1, v01 = v00 + T_NV, v11 = v01 + 1;
+            const int a = v00, b = (id & 1) ? v11 : v10, c = (id & 1) ? v01 : v11;
+            const float* A = sx + 4 * a; const float* B = sx + 4 * b; const float* Cv = sx + 4 * c;
+            if (A[3] == 0.0f || B[3] == 0.0f || Cv[3] == 0.0f) continue;
+            float minx = fminf(A[0], fminf(B[0], Cv[0])), maxx = fmaxf(A[0], fmaxf(B[0], Cv[0]));
+            float miny = fminf(A[1], fminf(B[1], Cv[1])), maxy = fmaxf(A[1], fmaxf(B[1], Cv[1]));
+            if (maxx < (float)x0 || minx > (float)x1 || maxy < (float)y0 || miny > (float)y1) continue;
+            const float area = (B[0] - A[0]) * (Cv[1] - A[1]) - (B[1] - A[1]) * (Cv[0] - A[0]);
+            if (area == 0.0f) continue;
+            const float sgn = area > 0.0f ? 1.0f : -1.0f, inv_area = 1.0f / area;
+            int px0 = (int)floorf(minx - 0.5f), px1 = (int)ceilf(maxx - 0.5f);
+            int py0 = (int)floorf(miny - 0.5f), py1 = (int)ceilf(maxy - 0.5f);
+            if (px0 < x0) px0 = x0;
+            if (py0 < y0) py0 = y0;
+            if (px1 > x1 - 1) px1 = x1 - 1;
+            if (py1 > y1 - 1) py1 = y1 - 1;
+            for (int y = py0; y <= py1; ++y)
+                for (int x = px0; x <= px1; ++x) {
+                    const float fx = (float)x + 0.5f, fy = (float)y + 0.5f;
+                    /* edge functions, oriented so that inside is >= 0 for either winding */
+                    float e0 = ((Cv[0] - B[0]) * (fy - B[1]) - (Cv[1] - B[1]) * (fx - B[0])) * sgn;
+                    float e1 = ((A[0] - Cv[0]) * (fy - Cv[1]) - (A[1] - Cv[1]) * (fx - Cv[0])) * sgn;
+                    float e2 = ((B[0] - A[0]) * (fy - A[1]) - (B[1] - A[1]) * (fx - A[0])) * sgn;
+                    if (e0 < 0.0f || e1 < 0.0f || e2 < 0.0f) continue;
+                    /* top-left rule for pixels exactly on an edge: keep only the edge whose outward
+                       normal points up or left (shared edges are then covered once) */
+                    if (e0 == 0.0f || e1 == 0.0f || e2 == 0.0f) {
+                        const float* P0[3] = {B, Cv, A};
+                        const float* P1[3] = {Cv, A, B};
+                        const float ev[3] = {e0, e1, e2};
+                        int ok = 1;
+                        for (int k = 0; k < 3; ++k) {
+                            if (ev[k] != 0.0f) continue;
+                            const float dx = (P1[k][0] - P0[k][0]) * sgn, dy = (P1[k][1] - P0[k][1]) * sgn;
+                            if (!((dy < 0.0f) || (dy == 0.0f && dx > 0.0f))) ok = 0;
+                        }
+                        if (!ok) continue;
+                    }
+                    const float w0 = e0 * sgn * inv_area, w1 = e1 * sgn * inv_area, w2 = e2 * sgn * inv_area;
+                    const float z = w0 * A[2] + w1 * B[2] + w2 * Cv[2];
+                    if (z < 0.0f || z > 1.0f) continue;                      /* depth clipping */
+                    const size_t i = (size_t)y * W + x;
+                    if (!(z <= depth[i])) continue;                         /* LESS_OR_EQUAL */
+                    depth[i] = z;
+                    tri[i] = id;
+                    if (b1o) {
+                        const float q0 = w0 * A[3], q1 = w1 * B[3], q2 = w2 * Cv[3], qs = q0 + q1 + q2;
+                        b1o[i] = q1 / qs;
+                        b2o[i] = q2 / qs;
+                    }
+                }
+        }
+    }
+    free(sx);
+}
+
+static void terrain_gbuffer(const soc_globals* g, int W, int H, uint16_t* albedo, uint16_t* emissive, uint16_t* normal,
+                            float* depth, uint16_t* velocity) {
+    const terrain_mesh* t = get_terrain(g);
+    int* tri = (int*)malloc(sizeof(int) * (size_t)W * H);
+    float* b1 = (float*)malloc(sizeof(float) * (size_t)W * H);
+    float* b2 = (float*)malloc(sizeof(float) * (size_t)W * H);
+    terrain_raster(t, g->camera_projection_view_matrix, W, H, depth, tri, b1, b2);
+#pragma omp parallel for schedule(static)
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+            const size_t i = (size_t)y * W + x;
+            put4(emissive + 4 * i, 0, 0, 0, 1);
+            put4(velocity + 4 * i, 0, 0, 0, 1);
+            if (tri[i] < 0) {
+                put4(albedo + 4 * i, 0.2f, 0.4f, 1.0f, 1.0f);
+                put4(normal + 4 * i, 0, 0, 0, 1);
+                continue;
+            }
+            put4(velocity + 4 * i, 0, 0, 0, 0);   /* out_velocity = vec4(0) (draw_terrain.inl:221) */
+            const int id = tri[i], q = id >> 1, qi = q % T_SEGS, qj = q / T_SEGS;
+            /* the triangle's vertex uvs: a = (qi, qj), b = (qi+1, qj+1) or (qi+1, qj), c = (qi, qj+1) or (qi+1, qj+1) */
+            const float ua = (float)qi, va = (float)qj;
+            const float ub = ua + 1.0f, vb = (id & 1) ? va + 1.0f : va;
+            const float uc = (id & 1) ? ua : ua + 1.0f, vc = va + 1.0f;
+            const float w1 = b1[i], w2 = b2[i], w0 = 1.0f - w1 - w2;
+            const float u = (w0 * ua + w1 * ub + w2 * uc) / (float)T_SEGS, v = (w0 * va + w1 * vb + w2 * vc) / (float)T_SEGS;
+            const v3 n = terrain_normal(t, u, v);
+            const float hgt = (terrain_height(u, v) - t->mid) * t->hscale;
+            float alb[3];
+            terrain_material(hgt, n, u, v, alb);
+            put4(albedo + 4 * i, alb[0], alb[1], alb[2], 1.0f);
+            put4(normal + 4 * i, n.x, n.y, n.z, 1.0f);
+        }
+    free(tri);
+    free(b1);
+    free(b2);
+}
+
 static scene g_scene;
 static int g_scene_built = 0;
 
@@ -191,6 +407,10 @@ static const scene* get_scene(int id) {
 int soc_scene_gbuffer(int scene_id, const soc_globals* g, int W, int H, uint16_t* albedo, uint16_t* emissive,
                       uint16_t* normal, float* depth, uint16_t* velocity) {
     if (!g || W <= 0 || H <= 0 || !albedo || !emissive || !normal || !depth || !velocity) return -1;
+    if (scene_id == SCENE_TERRAIN) {
+        terrain_gbuffer(g, W, H, albedo, emissive, normal, depth, velocity);
+        return 0;
+    }
     const scene* s = get_scene(scene_id);
     /* NB: the reference's camera_inverse_projection_view_matrix is inv(P) * inv(V) (application.cpp:136), not
        inv(P*V); unproject with inv(V) * (inv(P) * ndc) as the shaders do. */
@@ -249,6 +469,12 @@ int soc_scene_gbuffer(int scene_id, const soc_globals* g, int W, int H, uint16_t
 /* Sun shadow map S x S (D32, tight rows). */
 int soc_scene_shadow(int scene_id, const soc_globals* g, int S, float* shadow) {
     if (!g || S <= 0 || !shadow) return -1;
+    if (scene_id == SCENE_TERRAIN) {   /* depth only, through the sun's ortho projection * view */
+        int* tri = (int*)malloc(sizeof(int) * (size_t)S * S);
+        terrain_raster(get_terrain(g), g->sun_info.projection_view_matrix, S, S, shadow, tri, NULL, NULL);
+        free(tri);
+        return 0;
+    }
     const scene* s = get_scene(scene_id);
     float ivp[16];
     /* inverse of the sun's projection*view via the library-free closed form is not needed: march the

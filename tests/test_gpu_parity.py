@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import (f16_close, globals_for, host_frame, random_rgba16, random_shadow, sponza_inputs)
+from helpers import (f16_close, globals_for, host_frame, random_rgba16, random_shadow, sponza_inputs, terrain_inputs)
 
 pytestmark = pytest.mark.gpu
 
@@ -406,10 +406,12 @@ def test_clouds_pair_path_equals_single_lane(soc, W, H, pitch, all_sky):
 
 
 # ------------------------------------------------------------------------------------------------ full frame
-@pytest.mark.parametrize("W,H,frames", [(256, 144, 3), (1920, 1080, 2)])
-def test_render_graph_frames(soc, oracle, W, H, frames):
-    """Multi-frame render graph (ping-pong TAA history, fused velocity history) vs the oracle frame."""
-    g, gb = sponza_inputs(W, H, elapsed=10.0)
+@pytest.mark.parametrize("W,H,frames,inputs", [(256, 144, 3, "sponza"), (1920, 1080, 2, "sponza"),
+                                               (320, 180, 2, "terrain"), (960, 540, 2, "terrain")])
+def test_render_graph_frames(soc, oracle, W, H, frames, inputs):
+    """Multi-frame render graph (ping-pong TAA history, fused velocity history) vs the oracle frame, on the
+    Sponza-proxy (C2/C3) and on the terrain (C4: half the frame is sky, so clouds dominate)."""
+    g, gb = (sponza_inputs if inputs == "sponza" else terrain_inputs)(W, H, elapsed=10.0)
     fr = soc.alloc_frame(W, H, DEV)
     for k in ("albedo", "emissive", "normal", "velocity", "depth"):
         fr[k].copy_(torch.from_numpy(gb[k]))
