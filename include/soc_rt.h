@@ -395,6 +395,64 @@ int32_t soc_renderer_current_history(const soc_renderer* r);
  * Composition, so it overlaps bloom and SSAO. Results are identical either way. */
 int soc_renderer_set_async(soc_renderer* r, int32_t enable);
 
+/* --- Rasterisation: depth prepass, G-buffer and sun shadow map ---------------
+ * Replaces the raster producers upstream of the hot path: DepthPrepassTask (depth_prepass.inl:26-120),
+ * GBufferGenerationTask (g_buffer_generation.inl:33-230) and SunShadowDrawTask (sun_shadow_draw.inl:27-91).
+ * A visibility buffer (one u64 per pixel: depth bits << 32 | triangle key) is filled by 64-bit atomicMin,
+ * then one per-pixel resolve writes the reference's G-buffer images. Raster rules (the Vulkan ones the
+ * reference pipelines select): pixel centres, a consistent tie rule for centres on shared edges (each is
+ * covered once), depth clipping to [0, 1], LESS_OR_EQUAL test in draw order
+ * (equal depth: the later triangle wins), culling by facing. Front faces are CLOCKWISE in the framebuffer
+ * (Vulkan area a < 0): the reference culls FRONT for its glTF meshes, whose outward faces are counter-
+ * clockwise as seen, so its pipelines' (Daxa default, not in the mount) front face must be clockwise.
+ * Edge functions are homogeneous (2DH), so geometry behind the eye needs no clipping. The scene is one
+ * mesh (the reference's draws concatenated). */
+typedef struct soc_mesh {              /* device pointers (Vertex, shared.inl:152-157) */
+    const float* positions;            /* vertex_count x float3, object space */
+    const float* normals;              /* vertex_count x float3, object space */
+    const float* uvs;                  /* vertex_count x float2 */
+    const uint32_t* indices;           /* triangle_count x 3 */
+    const uint32_t* materials;         /* triangle_count material indices, or NULL (all 0) */
+    int32_t vertex_count, triangle_count;
+    float model_matrix[16];            /* TransformComponent.model_matrix (column-major) */
+    float normal_matrix[16];           /* TransformComponent.normal_matrix; its upper 3x3 transforms normals */
+} soc_mesh;
+
+/* Material (shared.inl:159-170, as GBufferGeneration's fragment shader reads it, g_buffer_generation.inl:
+ * 189-225): albedo = sample(albedo).rgb * albedo_factor + emissive; emissive = sample(emissive).rgb *
+ * emissive_factor (zero without an emissive image). Textures are RGBA8 (SRGB decoded to linear per
+ * texel), bilinear, REPEAT, level 0 (no mip selection); data == NULL samples white (model.cpp:188). */
+typedef struct soc_material {
+    soc_img albedo, emissive;
+    float albedo_factor[4], emissive_factor[4];
+    int32_t flags;                     /* SOC_MATERIAL_* */
+    int32_t has_emissive;              /* 0: emissive = 0 (has_emissive_image) */
+    int32_t pad[2];
+} soc_material;
+#define SOC_MATERIAL_ZERO_VELOCITY 1   /* write velocity 0 (the terrain draw, draw_terrain.inl:221) */
+
+#define SOC_CULL_NONE 0
+#define SOC_CULL_FRONT 1               /* depth prepass / G-buffer (depth_prepass.inl:45) */
+#define SOC_CULL_BACK 2                /* sun shadow (sun_shadow_draw.inl:46) */
+
+/* Workspace of the raster passes for a mesh (screen-space vertices, large-triangle list). */
+size_t soc_raster_workspace_size(int32_t vertex_count, int32_t triangle_count);
+/* Visibility buffer (u64 per pixel, width*height, tight): clear = 1 resets it to "empty, depth 1.0"
+ * first. `view_projection` is the camera's projection*view (camera_projection_view_matrix). */
+int soc_raster_visibility(const soc_mesh* mesh, const float view_projection[16], int32_t cull,
+                          uint64_t* visibility, int32_t width, int32_t height, int32_t clear,
+                          void* workspace, soc_stream stream);
+/* Depth-only raster into a D32 image (cleared to 1.0), with the pipeline's depth bias: z += slope *
+ * max(|dz/dx|, |dz/dy|) + constant * 2^(e - 23), e = the exponent of the triangle's largest |z|
+ * (sun_shadow_draw.inl:47-50: 1.25 / 1.75). */
+int soc_raster_depth(const soc_mesh* mesh, const float view_projection[16], int32_t cull, float bias_constant,
+                     float bias_slope, soc_img depth, void* workspace, soc_stream stream);
+/* G-buffer from a visibility buffer: depth (D32), albedo / emissive / normal / velocity (RGBA16F), with the
+ * clear values of GBufferGeneration for empty pixels. `d_materials` is a device array. */
+int soc_gbuffer_resolve(const soc_globals* g, const soc_mesh* mesh, const soc_material* d_materials,
+                        int32_t material_count, const uint64_t* visibility, soc_img depth, soc_img albedo,
+                        soc_img emissive, soc_img normal, soc_img velocity, soc_stream stream);
+
 #ifdef __cplusplus
 }
 #endif

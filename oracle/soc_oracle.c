@@ -989,3 +989,284 @@ int soc_oracle_cloud_rendering(const soc_globals* g, soc_img depth, soc_img nois
     g_cloud_counters[0] = c0; g_cloud_counters[1] = c1; g_cloud_counters[2] = c2; g_cloud_counters[3] = c3;
     return SOC_OK;
 }
+
+/* ------------------------------------------------------------------------------------------------ */
+/* Rasterisation: depth prepass / G-buffer / sun shadow                           */
+/* Restates the fixed-function raster the reference pipelines configure (depth_prepass.inl:36-46,    */
+/* g_buffer_generation.inl:50-60, sun_shadow_draw.inl:37-51) under the Vulkan rules: pixel-centre     */
+/* sampling, top-left fill rule, depth clipping to [0, 1], LESS_OR_EQUAL in draw order, culling by    */
+/* the sign of the framebuffer area (counter-clockwise front faces), depth bias m*slope + r*constant. */
+/* Geometry at w <= 1e-6 is dropped (no near-plane clipping). Serial in draw order within each 32x32  */
+/* tile (tiles are independent), so the result is the serial one.                                     */
+/* ------------------------------------------------------------------------------------------------ */
+typedef struct { float x, y, z, w; } rs_vtx;   /* homogeneous screen vertex: X, Y (pixels * w), z_c, w_c */
+typedef struct {
+    v3 r0, r1, r2;   /* sign-normalised edge functions E_i(p) = r_i . (px, py, 1) */
+    float z0, z1, z2, w0, w1, w2, bias;
+    int px0, px1, py0, py1, live;
+} rs_tri;
+
+static inline v4 mat_vec4(const float* m, float x, float y, float z, float w) {
+    return V4(m[0] * x + m[4] * y + m[8] * z + m[12] * w, m[1] * x + m[5] * y + m[9] * z + m[13] * w,
+              m[2] * x + m[6] * y + m[10] * z + m[14] * w, m[3] * x + m[7] * y + m[11] * z + m[15] * w);
+}
+
+/* 2DH rasterisation (Olano & Greer): no division per vertex, so geometry behind the eye needs no
+   clipping; depth clipping per fragment (z_ndc in [0, 1]). X = (x_c/2 + w_c/2) W, Y likewise. */
+static rs_vtx rs_clip_vertex(const float* pos, uint32_t v, const float* model, const float* vp, int W, int H) {
+    v4 wp = mat_vec4(model, pos[3 * v], pos[3 * v + 1], pos[3 * v + 2], 1.0f);
+    v4 c = mat_vec4(vp, wp.x, wp.y, wp.z, wp.w);
+    rs_vtx o;
+    o.x = (c.x * 0.5f + c.w * 0.5f) * (float)W;
+    o.y = (c.y * 0.5f + c.w * 0.5f) * (float)H;
+    o.z = c.z;
+    o.w = c.w;
+    return o;
+}
+
+static inline v3 rs_cross(v3 a, v3 b) { return V3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+
+/* adjugate rows r_i of [v0 v1 v2], det = v0 . r0; facing = sign(det) (= the framebuffer area's sign when
+   every w > 0; Vulkan a = -area/2 < 0 is clockwise = front, see soc_rt.h) */
+static void rs_edges(rs_vtx A, rs_vtx B, rs_vtx C, v3* r0, v3* r1, v3* r2, float* det) {
+    const v3 v0 = V3(A.x, A.y, A.w), v1 = V3(B.x, B.y, B.w), v2 = V3(C.x, C.y, C.w);
+    *r0 = rs_cross(v1, v2);
+    *r1 = rs_cross(v2, v0);
+    *r2 = rs_cross(v0, v1);
+    *det = v0.x * r0->x + v0.y * r0->y + v0.z * r0->z;
+}
+
+static rs_tri rs_setup(rs_vtx A, rs_vtx B, rs_vtx C, int cull, int W, int H, int depth_only, float bc, float bs) {
+    rs_tri t;
+    memset(&t, 0, sizeof t);
+    v3 r0, r1, r2;
+    float det;
+    rs_edges(A, B, C, &r0, &r1, &r2, &det);
+    if (!(det != 0.0f) || det != det) return t;
+    if (cull == SOC_CULL_FRONT && det > 0.0f) return t;
+    if (cull == SOC_CULL_BACK && det < 0.0f) return t;
+    if (det < 0.0f) { r0 = neg3(r0); r1 = neg3(r1); r2 = neg3(r2); }
+    t.r0 = r0; t.r1 = r1; t.r2 = r2;
+    t.z0 = A.z; t.z1 = B.z; t.z2 = C.z;
+    t.w0 = A.w; t.w1 = B.w; t.w2 = C.w;
+    if (A.w > 1e-6f && B.w > 1e-6f && C.w > 1e-6f) {   /* bounding box of the projected vertices */
+        float ax = A.x / A.w, ay = A.y / A.w, bx = B.x / B.w, by = B.y / B.w, cx = C.x / C.w, cy = C.y / C.w;
+        float minx = fminf(ax, fminf(bx, cx)), maxx = fmaxf(ax, fmaxf(bx, cx));
+        float miny = fminf(ay, fminf(by, cy)), maxy = fmaxf(ay, fmaxf(by, cy));
+        t.px0 = (int)floorf(fminf(fmaxf(minx - 0.5f, -1.0f), (float)W)); if (t.px0 < 0) t.px0 = 0;
+        t.px1 = (int)ceilf(fminf(fmaxf(maxx - 0.5f, -1.0f), (float)W)); if (t.px1 > W - 1) t.px1 = W - 1;
+        t.py0 = (int)floorf(fminf(fmaxf(miny - 0.5f, -1.0f), (float)H)); if (t.py0 < 0) t.py0 = 0;
+        t.py1 = (int)ceilf(fminf(fmaxf(maxy - 0.5f, -1.0f), (float)H)); if (t.py1 > H - 1) t.py1 = H - 1;
+    } else {                                           /* a vertex at or behind the eye: whole image */
+        t.px0 = 0; t.px1 = W - 1; t.py0 = 0; t.py1 = H - 1;
+    }
+    if (t.px0 > t.px1 || t.py0 > t.py1) return t;
+    if (depth_only) {   /* z_ndc = (sum z_i r_i) . p / |det| is affine in the pixel position */
+        float adet = fabsf(det);
+        float nx = A.z * r0.x + B.z * r1.x + C.z * r2.x, ny = A.z * r0.y + B.z * r1.y + C.z * r2.y;
+        float m = fmaxf(fabsf(nx / adet), fabsf(ny / adet));
+        float zmax = 0.0f;
+        if (A.w > 0.0f) zmax = fmaxf(zmax, fabsf(A.z / A.w));
+        if (B.w > 0.0f) zmax = fmaxf(zmax, fabsf(B.z / B.w));
+        if (C.w > 0.0f) zmax = fmaxf(zmax, fabsf(C.z / C.w));
+        uint32_t zb;
+        memcpy(&zb, &zmax, 4);
+        uint32_t e = (zb >> 23) & 255u;   /* r = 2^(E - 23), the D32F minimum resolvable difference */
+        float r = (e == 0u || e == 255u) ? 0.0f : ldexpf(1.0f, (int)e - 127 - 23);
+        t.bias = m * bs + r * bc;
+    }
+    t.live = 1;
+    return t;
+}
+
+/* tie rule: an edge owns the centres exactly on it iff its normal points to +x (or +y when vertical);
+   shared edges have exactly negated coefficients, so such a centre is covered once */
+static inline int rs_owns(v3 r) { return r.x > 0.0f || (r.x == 0.0f && r.y > 0.0f); }
+static inline float rs_edge(v3 r, float px, float py) { return r.x * px + r.y * py + r.z; }
+
+static int rs_cover(const rs_tri* t, int x, int y, float* e0, float* e1, float* e2, float* z) {
+    float fx = (float)x + 0.5f, fy = (float)y + 0.5f;
+    *e0 = rs_edge(t->r0, fx, fy);
+    *e1 = rs_edge(t->r1, fx, fy);
+    *e2 = rs_edge(t->r2, fx, fy);
+    if (*e0 < 0.0f || *e1 < 0.0f || *e2 < 0.0f) return 0;
+    if (*e0 == 0.0f && !rs_owns(t->r0)) return 0;
+    if (*e1 == 0.0f && !rs_owns(t->r1)) return 0;
+    if (*e2 == 0.0f && !rs_owns(t->r2)) return 0;
+    float num = *e0 * t->z0 + *e1 * t->z1 + *e2 * t->z2, den = *e0 * t->w0 + *e1 * t->w1 + *e2 * t->w2;
+    if (!(den > 0.0f)) return 0;
+    float zz = num / den;
+    if (zz < 0.0f || zz > 1.0f) return 0;   /* depth clipping */
+    *z = zz + 0.0f;
+    return 1;
+}
+
+static int rs_check_mesh(const soc_mesh* m) {
+    return m && m->positions && m->indices && m->vertex_count >= 0 && m->triangle_count >= 0;
+}
+
+/* Serial raster of the mesh in draw order, 32x32 tiles in parallel. depth_only: D32 target with bias;
+   else: u64 visibility keys (depth bits << 32 | 0xFFFFFFFE - triangle, empty = 1.0 | 0xFFFFFFFF). */
+static void rs_raster(const soc_mesh* mesh, const float* vp, int cull, int W, int H, int depth_only, float bc,
+                      float bs, void* target, size_t pitch) {
+    rs_vtx* sv = (rs_vtx*)malloc(sizeof(rs_vtx) * (size_t)(mesh->vertex_count > 0 ? mesh->vertex_count : 1));
+#pragma omp parallel for
+    for (int v = 0; v < mesh->vertex_count; ++v)
+        sv[v] = rs_clip_vertex(mesh->positions, (uint32_t)v, mesh->model_matrix, vp, W, H);
+    rs_tri* tris = (rs_tri*)malloc(sizeof(rs_tri) * (size_t)(mesh->triangle_count > 0 ? mesh->triangle_count : 1));
+#pragma omp parallel for
+    for (int i = 0; i < mesh->triangle_count; ++i) {
+        const uint32_t* ix = mesh->indices + 3 * (size_t)i;
+        tris[i] = rs_setup(sv[ix[0]], sv[ix[1]], sv[ix[2]], cull, W, H, depth_only, bc, bs);
+    }
+    const int TS = 32, tx_n = (W + TS - 1) / TS, ty_n = (H + TS - 1) / TS;
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int tile = 0; tile < tx_n * ty_n; ++tile) {
+        const int x0 = (tile % tx_n) * TS, y0 = (tile / tx_n) * TS;
+        const int x1 = x0 + TS < W ? x0 + TS : W, y1 = y0 + TS < H ? y0 + TS : H;
+        for (int y = y0; y < y1; ++y)
+            for (int x = x0; x < x1; ++x) {
+                if (depth_only) ((float*)((char*)target + (size_t)y * pitch))[x] = 1.0f;
+                else ((uint64_t*)((char*)target + (size_t)y * pitch))[x] = ((uint64_t)0x3f800000u << 32) | 0xFFFFFFFFu;
+            }
+        for (int id = 0; id < mesh->triangle_count; ++id) {
+            const rs_tri* t = &tris[id];
+            if (!t->live || t->px1 < x0 || t->px0 >= x1 || t->py1 < y0 || t->py0 >= y1) continue;
+            const int ya = t->py0 > y0 ? t->py0 : y0, yb = t->py1 < y1 - 1 ? t->py1 : y1 - 1;
+            const int xa = t->px0 > x0 ? t->px0 : x0, xb = t->px1 < x1 - 1 ? t->px1 : x1 - 1;
+            for (int y = ya; y <= yb; ++y)
+                for (int x = xa; x <= xb; ++x) {
+                    float e0, e1, e2, z;
+                    if (!rs_cover(t, x, y, &e0, &e1, &e2, &z)) continue;
+                    if (depth_only) {
+                        float* d = (float*)((char*)target + (size_t)y * pitch) + x;
+                        float zb = fminf(fmaxf(z + t->bias, 0.0f), 1.0f);
+                        if (zb <= *d) *d = zb;                       /* LESS_OR_EQUAL */
+                    } else {
+                        uint64_t* d = (uint64_t*)((char*)target + (size_t)y * pitch) + x;
+                        float cur = u2f((uint32_t)(*d >> 32));
+                        if (z <= cur) {                              /* LESS_OR_EQUAL: later wins ties */
+                            uint32_t zbits;
+                            memcpy(&zbits, &z, 4);
+                            *d = ((uint64_t)zbits << 32) | (uint64_t)(0xFFFFFFFEu - (uint32_t)id);
+                        }
+                    }
+                }
+        }
+    }
+    free(tris);
+    free(sv);
+}
+
+int soc_oracle_raster_visibility(const soc_mesh* mesh, const float view_projection[16], int32_t cull,
+                                 uint64_t* visibility, int32_t width, int32_t height) {
+    if (!rs_check_mesh(mesh) || !view_projection || !visibility || width <= 0 || height <= 0) return SOC_E_INVALID_ARG;
+    rs_raster(mesh, view_projection, cull, width, height, 0, 0.0f, 0.0f, visibility, (size_t)width * 8);
+    return SOC_OK;
+}
+
+int soc_oracle_raster_depth(const soc_mesh* mesh, const float view_projection[16], int32_t cull, float bias_constant,
+                            float bias_slope, soc_img depth) {
+    if (!rs_check_mesh(mesh) || !view_projection || !valid(&depth) || depth.format != SOC_FMT_D32F) return SOC_E_INVALID_ARG;
+    rs_raster(mesh, view_projection, cull, depth.width, depth.height, 1, bias_constant, bias_slope, depth.data,
+              (size_t)depth.pitch_bytes);
+    return SOC_OK;
+}
+
+/* REPEAT bilinear RGBA8 texture at level 0 (SRGB decoded per texel); no image samples white
+   (the null texture, model.cpp:188). */
+static v4 rs_sample_texture(const soc_img* tex, float u, float v) {
+    if (!tex->data) return V4(1.0f, 1.0f, 1.0f, 1.0f);
+    return sample_repeat(tex, u, v);
+}
+
+static v3 rs_normalize(v3 a) {
+    float l = sqrtf(a.x * a.x + a.y * a.y + a.z * a.z);
+    return V3(a.x / l, a.y / l, a.z / l);
+}
+
+/* GBufferGeneration from the visibility buffer: vertex stage g_buffer_generation.inl:169-178, fragment
+   stage :189-225 (normal map and metallic/roughness not modelled: composition reads neither). */
+int soc_oracle_gbuffer_resolve(const soc_globals* g, const soc_mesh* mesh, const soc_material* materials,
+                               int32_t material_count, const uint64_t* visibility, soc_img depth, soc_img albedo,
+                               soc_img emissive, soc_img normal, soc_img velocity) {
+    if (!g || !rs_check_mesh(mesh) || !mesh->normals || !mesh->uvs || !materials || material_count <= 0 || !visibility ||
+        !valid(&depth) || !valid(&albedo) || !valid(&emissive) || !valid(&normal) || !valid(&velocity))
+        return SOC_E_INVALID_ARG;
+    const int W = depth.width, H = depth.height;
+    const float* M = mesh->model_matrix;
+    const float* vp = g->camera_projection_view_matrix;
+    const float* pvp = g->camera_previous_projection_view_matrix;
+    const float* nm = mesh->normal_matrix;
+    const float n3[9] = {nm[0], nm[1], nm[2], nm[4], nm[5], nm[6], nm[8], nm[9], nm[10]};
+#pragma omp parallel for schedule(static)
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+            const uint64_t key = visibility[(size_t)y * W + x];
+            const uint32_t low = (uint32_t)key;
+            if (low == 0xFFFFFFFFu) {   /* clear values, g_buffer_generation.inl:78-100 */
+                store(&depth, x, y, V4(1.0f, 0, 0, 0));
+                store(&albedo, x, y, V4(0.2f, 0.4f, 1.0f, 1.0f));
+                store(&emissive, x, y, V4(0, 0, 0, 1));
+                store(&normal, x, y, V4(0, 0, 0, 1));
+                store(&velocity, x, y, V4(0, 0, 0, 1));
+                continue;
+            }
+            const uint32_t id = 0xFFFFFFFEu - low;
+            const uint32_t ia = mesh->indices[3 * (size_t)id], ib = mesh->indices[3 * (size_t)id + 1],
+                           ic = mesh->indices[3 * (size_t)id + 2];
+            const rs_vtx A = rs_clip_vertex(mesh->positions, ia, M, vp, W, H);
+            const rs_vtx B = rs_clip_vertex(mesh->positions, ib, M, vp, W, H);
+            const rs_vtx C = rs_clip_vertex(mesh->positions, ic, M, vp, W, H);
+            v3 r0, r1, r2;
+            float det;
+            rs_edges(A, B, C, &r0, &r1, &r2, &det);
+            if (det < 0.0f) { r0 = neg3(r0); r1 = neg3(r1); r2 = neg3(r2); }
+            const float fx = (float)x + 0.5f, fy = (float)y + 0.5f;
+            const float e0 = rs_edge(r0, fx, fy), e1 = rs_edge(r1, fx, fy), e2 = rs_edge(r2, fx, fy);
+            const float es = e0 + e1 + e2;
+            const float b1 = e1 / es, b2 = e2 / es, b0 = 1.0f - b1 - b2;
+            const float* uv = mesh->uvs;
+            const float u = b0 * uv[2 * ia] + b1 * uv[2 * ib] + b2 * uv[2 * ic];
+            const float v = b0 * uv[2 * ia + 1] + b1 * uv[2 * ib + 1] + b2 * uv[2 * ic + 1];
+            const float* nr = mesh->normals;
+            const v3 na = rs_normalize(mat3_mul_v3(n3, V3(nr[3 * ia], nr[3 * ia + 1], nr[3 * ia + 2])));
+            const v3 nb = rs_normalize(mat3_mul_v3(n3, V3(nr[3 * ib], nr[3 * ib + 1], nr[3 * ib + 2])));
+            const v3 nc = rs_normalize(mat3_mul_v3(n3, V3(nr[3 * ic], nr[3 * ic + 1], nr[3 * ic + 2])));
+            const v3 n = rs_normalize(V3(b0 * na.x + b1 * nb.x + b2 * nc.x, b0 * na.y + b1 * nb.y + b2 * nc.y,
+                                         b0 * na.z + b1 * nb.z + b2 * nc.z));
+            uint32_t mi = mesh->materials ? mesh->materials[id] : 0u;
+            if (mi > (uint32_t)(material_count - 1)) mi = (uint32_t)(material_count - 1);
+            const soc_material* m = &materials[mi];
+            v3 em = V3(0, 0, 0);
+            if (m->has_emissive) {
+                v4 e = rs_sample_texture(&m->emissive, u, v);
+                em = V3(e.x * m->emissive_factor[0], e.y * m->emissive_factor[1], e.z * m->emissive_factor[2]);
+            }
+            const v4 al = rs_sample_texture(&m->albedo, u, v);
+            v4 vel = V4(0, 0, 0, 0);
+            if (!(m->flags & SOC_MATERIAL_ZERO_VELOCITY)) {
+                v4 cc[3], pc[3];
+                const uint32_t vi[3] = {ia, ib, ic};
+                for (int k = 0; k < 3; ++k) {
+                    const float* p = mesh->positions + 3 * (size_t)vi[k];
+                    v4 wp = mat_vec4(M, p[0], p[1], p[2], 1.0f);
+                    cc[k] = mat_vec4(vp, wp.x, wp.y, wp.z, wp.w);
+                    pc[k] = mat_vec4(pvp, wp.x, wp.y, wp.z, wp.w);
+                }
+                const float cx = b0 * cc[0].x + b1 * cc[1].x + b2 * cc[2].x, cy = b0 * cc[0].y + b1 * cc[1].y + b2 * cc[2].y;
+                const float cw = b0 * cc[0].w + b1 * cc[1].w + b2 * cc[2].w;
+                const float px = b0 * pc[0].x + b1 * pc[1].x + b2 * pc[2].x, py = b0 * pc[0].y + b1 * pc[1].y + b2 * pc[2].y;
+                const float pw = b0 * pc[0].w + b1 * pc[1].w + b2 * pc[2].w;
+                vel = V4(((cx / cw) * 0.5f + 0.5f) - ((px / pw) * 0.5f + 0.5f),
+                         ((cy / cw) * 0.5f + 0.5f) - ((py / pw) * 0.5f + 0.5f), 0.0f, 1.0f);
+            }
+            store(&depth, x, y, V4(u2f((uint32_t)(key >> 32)), 0, 0, 0));
+            store(&albedo, x, y, V4(al.x * m->albedo_factor[0] + em.x, al.y * m->albedo_factor[1] + em.y,
+                                    al.z * m->albedo_factor[2] + em.z, 1.0f));
+            store(&emissive, x, y, V4(em.x, em.y, em.z, 1.0f));
+            store(&normal, x, y, V4(n.x, n.y, n.z, 1.0f));
+            store(&velocity, x, y, vel);
+        }
+    return SOC_OK;
+}

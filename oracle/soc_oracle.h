@@ -37,6 +37,15 @@ int soc_oracle_temporal_antialiasing(const soc_globals* g, soc_img target, soc_i
                                      soc_img previous_velocity, soc_img depth);
 int soc_oracle_tone_mapping(const soc_globals* g, soc_img color, const soc_auto_exposure* ae, soc_img target);
 
+/* Rasterisation: host-pointer mesh / materials, same arguments as the C ABI. */
+int soc_oracle_raster_visibility(const soc_mesh* mesh, const float view_projection[16], int32_t cull,
+                                 uint64_t* visibility, int32_t width, int32_t height);
+int soc_oracle_raster_depth(const soc_mesh* mesh, const float view_projection[16], int32_t cull, float bias_constant,
+                            float bias_slope, soc_img depth);
+int soc_oracle_gbuffer_resolve(const soc_globals* g, const soc_mesh* mesh, const soc_material* materials,
+                               int32_t material_count, const uint64_t* visibility, soc_img depth, soc_img albedo,
+                               soc_img emissive, soc_img normal, soc_img velocity);
+
 /* Scalar helpers exposed for known-answer tests. */
 uint32_t soc_oracle_luminance_bin(float r, float g, float b, float log_min, float log_max);
 float soc_oracle_log2(float x);

@@ -115,9 +115,24 @@ class FrameImages(C.Structure):
     ]
 
 
+class Mesh(C.Structure):
+    _fields_ = [("positions", C.c_void_p), ("normals", C.c_void_p), ("uvs", C.c_void_p), ("indices", C.c_void_p),
+                ("materials", C.c_void_p), ("vertex_count", C.c_int32), ("triangle_count", C.c_int32),
+                ("model_matrix", Mat4), ("normal_matrix", Mat4)]
+
+
+class Material(C.Structure):
+    _fields_ = [("albedo", SocImg), ("emissive", SocImg), ("albedo_factor", C.c_float * 4),
+                ("emissive_factor", C.c_float * 4), ("flags", C.c_int32), ("has_emissive", C.c_int32),
+                ("pad", C.c_int32 * 2)]
+
+
+CULL_NONE, CULL_FRONT, CULL_BACK = 0, 1, 2
+MATERIAL_ZERO_VELOCITY = 1
+
 STRUCTS = {"soc_img": SocImg, "soc_globals": Globals, "soc_sun_info": SunInfo, "soc_point_light": PointLight,
            "soc_spot_light": SpotLight, "soc_auto_exposure": AutoExposure, "soc_camera": Camera,
-           "soc_frame_images": FrameImages}
+           "soc_frame_images": FrameImages, "soc_mesh": Mesh, "soc_material": Material}
 
 _I = C.c_int
 _P = C.c_void_p
@@ -170,6 +185,11 @@ FUNCTIONS = {
     "soc_renderer_set_pass_timing": (_I, [_P, C.c_int32, C.c_int32]),
     "soc_renderer_reset_timing": (_I, [_P]),
     "soc_renderer_pass_stats": (_I, [_P, C.c_int32, C.POINTER(C.c_float), C.POINTER(C.c_int32)]),
+    "soc_raster_workspace_size": (C.c_size_t, [C.c_int32, C.c_int32]),
+    "soc_raster_visibility": (_I, [C.POINTER(Mesh), C.POINTER(C.c_float), C.c_int32, _P, C.c_int32, C.c_int32,
+                                   C.c_int32, _P, _P]),
+    "soc_raster_depth": (_I, [C.POINTER(Mesh), C.POINTER(C.c_float), C.c_int32, C.c_float, C.c_float, _IMG, _P, _P]),
+    "soc_gbuffer_resolve": (_I, [_G, C.POINTER(Mesh), _P, C.c_int32, _P, _IMG, _IMG, _IMG, _IMG, _IMG, _P]),
 }
 
 # not in the public header: test hooks

@@ -165,6 +165,10 @@ const FieldInfo kFields[] = {
     F(soc_frame_images, history_color), F(soc_frame_images, history_velocity), F(soc_frame_images, output),
     F(soc_frame_images, ssao_noise_table), F(soc_frame_images, auto_exposure), F(soc_frame_images, d_globals),
     F(soc_frame_images, bloom_output), F(soc_frame_images, clouds_workspace),
+    F(soc_mesh, positions), F(soc_mesh, normals), F(soc_mesh, uvs), F(soc_mesh, indices), F(soc_mesh, materials),
+    F(soc_mesh, vertex_count), F(soc_mesh, triangle_count), F(soc_mesh, model_matrix), F(soc_mesh, normal_matrix),
+    F(soc_material, albedo), F(soc_material, emissive), F(soc_material, albedo_factor), F(soc_material, emissive_factor),
+    F(soc_material, flags), F(soc_material, has_emissive),
 };
 #undef F
 }  // namespace
@@ -182,6 +186,8 @@ extern "C" size_t soc_abi_sizeof(const char* t) {
     if (s == "soc_auto_exposure") return sizeof(soc_auto_exposure);
     if (s == "soc_camera") return sizeof(soc_camera);
     if (s == "soc_frame_images") return sizeof(soc_frame_images);
+    if (s == "soc_mesh") return sizeof(soc_mesh);
+    if (s == "soc_material") return sizeof(soc_material);
     return 0;
 }
 

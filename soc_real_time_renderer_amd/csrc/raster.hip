@@ -1,0 +1,520 @@
+// raster.hip — depth prepass / G-buffer / sun-shadow rasterisation for gfx950.
+//
+// Replaces the reference's fixed-function raster producers upstream of the screen-space chain:
+//   DepthPrepassTask      depth_prepass.inl:26-120      (cull FRONT, LESS_OR_EQUAL)
+//   GBufferGenerationTask g_buffer_generation.inl:33-230 (cull FRONT, LESS_OR_EQUAL, depth LOAD)
+//   SunShadowDrawTask     sun_shadow_draw.inl:27-91     (cull BACK, depth bias 1.25 / 1.75)
+// gfx950 has no raster units reachable from HIP, so the raster is a compute visibility buffer:
+//   1. raster_setup     one lane per vertex: object -> world -> clip -> screen (x, y, z_ndc, 1/w)
+//   2. raster_small     one lane per triangle: cull, bounding box; a box of <= SMALL_PIXELS pixels is
+//                       scanned by the lane itself, larger ones are split into CHUNK-pixel work items
+//   3. raster_big       one wave per work item: 64 lanes cover the chunk's pixels
+//   every covered pixel does ONE 64-bit atomicMin of (depth bits << 32 | 0xFFFFFFFE - triangle): with
+//   z >= 0 the float bits order like the depths, and ties keep the LATER triangle, which is exactly the
+//   serial LESS_OR_EQUAL result in draw order. The depth-only variant (shadow map) does a 32-bit
+//   atomicMin of the biased depth bits straight into the D32 image.
+//   4. gbuffer_resolve  one lane per pixel: the winning triangle's perspective-correct barycentrics,
+//                       attribute interpolation and the GBufferGeneration fragment shader
+//                       (g_buffer_generation.inl:189-225).
+// The coverage, depth and barycentric arithmetic is written without FMA contraction and matches the
+// oracle's (oracle/soc_oracle.c, soc_oracle_raster_*) operation for operation, so the visibility buffer
+// and the depth images are bit-exact against it.
+#include "soc_internal.hpp"
+
+namespace soc {
+namespace {
+
+constexpr int SMALL_PIXELS = 64;    // bounding boxes up to this many pixels are scanned by one lane
+constexpr int CHUNK = 1024;         // pixels per large-triangle work item (16 per lane of a wave)
+constexpr uint32_t KEY_EMPTY = 0xFFFFFFFFu;
+
+struct RasterParams {
+    Mat4 model, vp;
+    int width, height, vertex_count, triangle_count;
+    int cull;
+    int depth_only;
+    float bias_constant, bias_slope;
+    uint32_t item_capacity;
+};
+
+// workspace: [float4 clip-space screen vertices[V]] [uint32 counter, pad..] [uint2 items[capacity]]
+struct Workspace {
+    float4* screen;
+    uint32_t* counter;
+    uint2* items;
+    uint32_t capacity;
+};
+
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+inline Workspace carve(void* ws, int V, int T) {
+    char* p = static_cast<char*>(ws);
+    Workspace w;
+    w.screen = reinterpret_cast<float4*>(p);
+    size_t off = align_up((size_t)V * 16, 256);
+    w.counter = reinterpret_cast<uint32_t*>(p + off);
+    off += 256;
+    w.items = reinterpret_cast<uint2*>(p + off);
+    w.capacity = (uint32_t)(4 * (size_t)T + (1u << 20));
+    return w;
+}
+
+// GLSL mat4 * vec4, summed left to right, no contraction (the oracle's mat_vec).
+__device__ __forceinline__ f4 mat_vec_exact(const Mat4& M, float x, float y, float z, float w) {
+#pragma clang fp contract(off)
+    const float* m = M.m;
+    return f4{m[0] * x + m[4] * y + m[8] * z + m[12] * w, m[1] * x + m[5] * y + m[9] * z + m[13] * w,
+              m[2] * x + m[6] * y + m[10] * z + m[14] * w, m[3] * x + m[7] * y + m[11] * z + m[15] * w};
+}
+
+// Homogeneous screen-space vertex (2DH rasterisation, Olano & Greer): X = (x_c/2 + w_c/2) W,
+// Y = (y_c/2 + w_c/2) H (y = 0 top row, uv = ndc * 0.5 + 0.5), Z = z_c, W = w_c. No division, so
+// vertices behind the eye need no geometric clipping; fragments with z_ndc outside [0, 1] are clipped
+// per pixel (Vulkan depth clipping; the reference's RH_NO projection puts z_c = 0 between near and far).
+__device__ __forceinline__ float4 clip_vertex(const float* __restrict__ pos, int v, const Mat4& model, const Mat4& vp,
+                                              int W, int H) {
+#pragma clang fp contract(off)
+    const float px = pos[3 * v], py = pos[3 * v + 1], pz = pos[3 * v + 2];
+    const f4 wp = mat_vec_exact(model, px, py, pz, 1.0f);
+    const f4 c = mat_vec_exact(vp, wp.x, wp.y, wp.z, wp.w);
+    return float4{(c.x * 0.5f + c.w * 0.5f) * (float)W, (c.y * 0.5f + c.w * 0.5f) * (float)H, c.z, c.w};
+}
+
+__device__ __forceinline__ f3 cross_exact(f3 a, f3 b) {
+#pragma clang fp contract(off)
+    return f3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+
+struct TriSetup {
+    f3 r0, r1, r2;          // edge functions E_i(p) = r_i . (px, py, 1), sign-normalised: inside iff all >= 0
+    float z0, z1, z2, w0, w1, w2;
+    float bias;
+    int px0, px1, py0, py1;
+    bool live;
+};
+
+// Triangle setup: the adjugate rows r_i of [v0 v1 v2] (v = (X, Y, W)), det = v0 . r0. Facing is the
+// sign of det (= the sign of the framebuffer area when every w > 0; Vulkan a = -area/2 < 0 is
+// clockwise = front, the reference pipelines' winding: see soc_rt.h). Bounding box from the projected vertices when every w > 1e-6, else the
+// whole image. Depth bias: z_ndc = (sum z_i r_i) . p / |det| is affine in the pixel position.
+__device__ __forceinline__ TriSetup tri_setup(float4 A, float4 B, float4 C, const RasterParams& p) {
+#pragma clang fp contract(off)
+    TriSetup t;
+    t.live = false;
+    const f3 v0{A.x, A.y, A.w}, v1{B.x, B.y, B.w}, v2{C.x, C.y, C.w};
+    f3 r0 = cross_exact(v1, v2), r1 = cross_exact(v2, v0), r2 = cross_exact(v0, v1);
+    const float det = v0.x * r0.x + v0.y * r0.y + v0.z * r0.z;
+    if (!(det != 0.0f) || det != det) return t;
+    if (p.cull == SOC_CULL_FRONT && det > 0.0f) return t;
+    if (p.cull == SOC_CULL_BACK && det < 0.0f) return t;
+    if (det < 0.0f) { r0 = -r0; r1 = -r1; r2 = -r2; }
+    t.r0 = r0; t.r1 = r1; t.r2 = r2;
+    t.z0 = A.z; t.z1 = B.z; t.z2 = C.z;
+    t.w0 = A.w; t.w1 = B.w; t.w2 = C.w;
+    // Bounding box of the triangle clipped to z_c >= 0 (fragments below it are depth-clipped anyway, and
+    // there w > 0 for a perspective or orthographic projection), one pixel of margin: a superset of the
+    // covered centres. The oracle scans the whole image for such triangles; coverage itself is decided
+    // per pixel by the edge functions only, so the results are identical.
+    {
+        const float4 P[3] = {A, B, C};
+        float minx = 3.0e38f, maxx = -3.0e38f, miny = 3.0e38f, maxy = -3.0e38f;
+        bool any = false, wide = false;
+        auto add = [&](float X, float Y, float Wc) {
+            if (!(Wc > 1e-20f)) { wide = true; return; }
+            const float x = X / Wc, y = Y / Wc;
+            minx = fminf(minx, x); maxx = fmaxf(maxx, x);
+            miny = fminf(miny, y); maxy = fmaxf(maxy, y);
+            any = true;
+        };
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const float4 a = P[i], b = P[(i + 1) % 3];
+            if (a.z >= 0.0f) add(a.x, a.y, a.w);
+            if ((a.z >= 0.0f) != (b.z >= 0.0f)) {   // edge crosses z_c = 0
+                const float u = a.z / (a.z - b.z);
+                add(a.x + u * (b.x - a.x), a.y + u * (b.y - a.y), a.w + u * (b.w - a.w));
+            }
+        }
+        if (!any && !wide) return t;   // wholly behind the depth-clip plane
+        const float W = (float)p.width, H = (float)p.height;
+        if (wide || minx != minx || miny != miny || maxx != maxx || maxy != maxy) {
+            t.px0 = 0; t.px1 = p.width - 1; t.py0 = 0; t.py1 = p.height - 1;
+        } else {
+            t.px0 = max(0, (int)floorf(fminf(fmaxf(minx - 1.5f, -1.0f), W)));
+            t.px1 = min(p.width - 1, (int)ceilf(fminf(fmaxf(maxx + 0.5f, -1.0f), W)));
+            t.py0 = max(0, (int)floorf(fminf(fmaxf(miny - 1.5f, -1.0f), H)));
+            t.py1 = min(p.height - 1, (int)ceilf(fminf(fmaxf(maxy + 0.5f, -1.0f), H)));
+        }
+    }
+    if (t.px0 > t.px1 || t.py0 > t.py1) return t;
+    t.bias = 0.0f;
+    if (p.depth_only) {   // Vulkan depth bias: m * slope + r * constant
+        const float adet = fabsf(det);
+        const float nx = A.z * r0.x + B.z * r1.x + C.z * r2.x, ny = A.z * r0.y + B.z * r1.y + C.z * r2.y;
+        const float m = fmaxf(fabsf(nx / adet), fabsf(ny / adet));
+        // r = 2^(E - 23), E the exponent of the largest |z_ndc| at a vertex (in front of the eye)
+        float zmax = 0.0f;
+        if (A.w > 0.0f) zmax = fmaxf(zmax, fabsf(A.z / A.w));
+        if (B.w > 0.0f) zmax = fmaxf(zmax, fabsf(B.z / B.w));
+        if (C.w > 0.0f) zmax = fmaxf(zmax, fabsf(C.z / C.w));
+        const uint32_t ebits = (__float_as_uint(zmax) >> 23) & 255u;
+        const float r = (ebits == 0u || ebits == 255u) ? 0.0f : ldexpf(1.0f, (int)ebits - 127 - 23);
+        t.bias = m * p.bias_slope + r * p.bias_constant;
+    }
+    t.live = true;
+    return t;
+}
+
+// An edge owns the pixel centres exactly on it iff its normal (r.x, r.y) points to +x, or to +y when
+// vertical: shared edges have exactly negated coefficients, so each such centre is covered once.
+__device__ __forceinline__ bool owns(f3 r) { return r.x > 0.0f || (r.x == 0.0f && r.y > 0.0f); }
+
+__device__ __forceinline__ float edge(f3 r, float px, float py) {
+#pragma clang fp contract(off)
+    return r.x * px + r.y * py + r.z;
+}
+
+// Coverage of pixel (x, y): the three edge functions at the pixel centre, the tie rule, then
+// z_ndc = sum E_i z_i / sum E_i w_i and depth clipping. e0..e2 are returned for the barycentrics
+// (perspective-correct b_i = E_i / sum E). z is +0 for a -0 result.
+__device__ __forceinline__ bool cover(const TriSetup& t, int x, int y, float& e0, float& e1, float& e2, float& z) {
+#pragma clang fp contract(off)
+    const float fx = (float)x + 0.5f, fy = (float)y + 0.5f;
+    e0 = edge(t.r0, fx, fy);
+    e1 = edge(t.r1, fx, fy);
+    e2 = edge(t.r2, fx, fy);
+    if (e0 < 0.0f || e1 < 0.0f || e2 < 0.0f) return false;
+    if (e0 == 0.0f && !owns(t.r0)) return false;
+    if (e1 == 0.0f && !owns(t.r1)) return false;
+    if (e2 == 0.0f && !owns(t.r2)) return false;
+    const float num = e0 * t.z0 + e1 * t.z1 + e2 * t.z2, den = e0 * t.w0 + e1 * t.w1 + e2 * t.w2;
+    if (!(den > 0.0f)) return false;   // the pixel sees the triangle's plane behind the eye (or all E = 0)
+    z = num / den;
+    if (z < 0.0f || z > 1.0f) return false;   // depth clipping (NaN passes here and never wins below)
+    z = z + 0.0f;                              // -0 -> +0: the key's bit order needs z >= +0
+    return true;
+}
+
+__device__ __forceinline__ void shade(const TriSetup& t, int id, int x, int y, const RasterParams& p, void* target,
+                                      size_t pitch) {
+    float e0, e1, e2, z;
+    if (!cover(t, x, y, e0, e1, e2, z)) return;
+    if (p.depth_only) {
+#pragma clang fp contract(off)
+        const float zb = fminf(fmaxf(z + t.bias, 0.0f), 1.0f);
+        uint32_t* d = reinterpret_cast<uint32_t*>(static_cast<char*>(target) + (size_t)y * pitch) + x;
+        atomicMin(d, __float_as_uint(zb));
+    } else {
+        const unsigned long long key = ((unsigned long long)__float_as_uint(z) << 32) | (unsigned long long)(0xFFFFFFFEu - (uint32_t)id);
+        unsigned long long* d = reinterpret_cast<unsigned long long*>(static_cast<char*>(target) + (size_t)y * pitch) + x;
+        atomicMin(d, key);
+    }
+}
+
+__device__ __forceinline__ TriSetup load_tri(const Workspace& ws, const uint32_t* __restrict__ idx, int id,
+                                             const RasterParams& p) {
+    const uint32_t a = idx[3 * id], b = idx[3 * id + 1], c = idx[3 * id + 2];
+    return tri_setup(ws.screen[a], ws.screen[b], ws.screen[c], p);
+}
+
+__global__ __launch_bounds__(256) void raster_setup(const float* __restrict__ pos, Workspace ws, RasterParams p) {
+    const int v = blockIdx.x * 256 + threadIdx.x;
+    if (v == 0) *ws.counter = 0u;
+    if (v >= p.vertex_count) return;
+    ws.screen[v] = clip_vertex(pos, v, p.model, p.vp, p.width, p.height);
+}
+
+__global__ __launch_bounds__(256) void raster_clear_vis(unsigned long long* vis, size_t n) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) vis[i] = ((unsigned long long)__float_as_uint(1.0f) << 32) | KEY_EMPTY;
+}
+
+__global__ __launch_bounds__(256) void raster_small(const uint32_t* __restrict__ idx, Workspace ws, RasterParams p,
+                                                    void* target, size_t pitch) {
+    const int id = blockIdx.x * 256 + threadIdx.x;
+    if (id >= p.triangle_count) return;
+    const TriSetup t = load_tri(ws, idx, id, p);
+    if (!t.live) return;
+    const int bw = t.px1 - t.px0 + 1, bh = t.py1 - t.py0 + 1;
+    const long long n = (long long)bw * bh;
+    if (n > SMALL_PIXELS) {
+        const uint32_t chunks = (uint32_t)((n + CHUNK - 1) / CHUNK);
+        const uint32_t base = atomicAdd(ws.counter, chunks);
+        if (base + chunks <= ws.capacity) {
+            for (uint32_t k = 0; k < chunks; ++k) ws.items[base + k] = uint2{(uint32_t)id, k};
+            return;
+        }
+        // work list full: mark the reserved slots that exist as empty, rasterise the box in this lane
+        // (slow, correct)
+        for (uint32_t k = base; k < min(base + chunks, ws.capacity); ++k) ws.items[k] = uint2{0xFFFFFFFFu, 0u};
+    }
+    for (int y = t.py0; y <= t.py1; ++y)
+        for (int x = t.px0; x <= t.px1; ++x) shade(t, id, x, y, p, target, pitch);
+}
+
+// One wave per work item (triangle, chunk): its CHUNK pixels of the bounding box, 64 lanes wide.
+__global__ __launch_bounds__(256) void raster_big(const uint32_t* __restrict__ idx, Workspace ws, RasterParams p,
+                                                  void* target, size_t pitch) {
+    const uint32_t count = min(*ws.counter, ws.capacity);
+    const int lane = threadIdx.x & 63;
+    for (uint32_t it = blockIdx.x * 4 + (threadIdx.x >> 6); it < count; it += gridDim.x * 4) {
+        const uint2 item = ws.items[it];
+        if (item.x == 0xFFFFFFFFu) continue;
+        const TriSetup t = load_tri(ws, idx, (int)item.x, p);
+        const int bw = t.px1 - t.px0 + 1, bh = t.py1 - t.py0 + 1;
+        const long long n = (long long)bw * bh;
+        const long long k0 = (long long)item.y * CHUNK;
+        for (int j = lane; j < CHUNK; j += 64) {
+            const long long k = k0 + j;
+            if (k >= n) break;
+            const int yy = (int)(k / bw), xx = (int)(k - (long long)yy * bw);
+            shade(t, (int)item.x, t.px0 + xx, t.py0 + yy, p, target, pitch);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// G-buffer resolve (g_buffer_generation.inl:161-225)
+// ------------------------------------------------------------------------------------------------
+struct ResolveParams {
+    Mat4 model, vp, prev_vp;
+    Mat3 normal3;
+    int width, height, triangle_count, material_count;
+};
+
+__device__ __forceinline__ float srgb_to_linear(float c) {
+    return c <= 0.04045f ? c / 12.92f : powf((c + 0.055f) / 1.055f, 2.4f);
+}
+
+__device__ __forceinline__ f4 texel_rgba8(const DImg& im, int x, int y, bool srgb) {
+    const uint32_t u = row_ptr<uint32_t>(im, y)[x];
+    const float r = unorm8(u & 255u), g = unorm8((u >> 8) & 255u), b = unorm8((u >> 16) & 255u), a = unorm8(u >> 24);
+    if (!srgb) return f4{r, g, b, a};
+    return f4{srgb_to_linear(r), srgb_to_linear(g), srgb_to_linear(b), a};
+}
+
+// REPEAT addressing for any extent (the sampling contract's 8-bit sub-texel weights).
+__device__ __forceinline__ Axis axis_repeat_any(float u, int n) {
+#pragma clang fp contract(off)
+    float t = u * (float)n;
+    t = t - 0.5f;
+    t = fminf(fmaxf(t, -4194304.0f), 4194304.0f);
+    const int fx = (int)floorf(t * 256.0f + 0.5f);
+    const int i = fx >> 8;
+    Axis a;
+    a.w = (float)(fx & 255) * (1.0f / 256.0f);
+    int r = i % n;
+    if (r < 0) r += n;
+    a.i0 = r;
+    a.i1 = (r + 1) % n;
+    return a;
+}
+
+__device__ __forceinline__ f4 sample_texture(const soc_img& tex, float u, float v) {
+    if (!tex.data) return f4{1.0f, 1.0f, 1.0f, 1.0f};
+    const DImg im{static_cast<char*>(tex.data), tex.width, tex.height, tex.pitch_bytes};
+    const bool srgb = tex.format == SOC_FMT_RGBA8_SRGB;
+    const Axis ax = axis_repeat_any(u, tex.width), ay = axis_repeat_any(v, tex.height);
+    const f4 a = texel_rgba8(im, ax.i0, ay.i0, srgb), b = texel_rgba8(im, ax.i1, ay.i0, srgb);
+    const f4 c = texel_rgba8(im, ax.i0, ay.i1, srgb), d = texel_rgba8(im, ax.i1, ay.i1, srgb);
+    return bilerp4(a, b, c, d, ax.w, ay.w);
+}
+
+__device__ __forceinline__ f3 mat3_vec_exact(const Mat3& M, f3 v) {
+#pragma clang fp contract(off)
+    const float* m = M.m;
+    return f3{m[0] * v.x + m[3] * v.y + m[6] * v.z, m[1] * v.x + m[4] * v.y + m[7] * v.z, m[2] * v.x + m[5] * v.y + m[8] * v.z};
+}
+
+__device__ __forceinline__ f3 normalize_exact(f3 a) {
+#pragma clang fp contract(off)
+    const float l = sqrtf(a.x * a.x + a.y * a.y + a.z * a.z);
+    return f3{a.x / l, a.y / l, a.z / l};
+}
+
+__global__ __launch_bounds__(256) void gbuffer_resolve(soc_mesh mesh, const soc_material* __restrict__ mats,
+                                                       const unsigned long long* __restrict__ vis, DImg depth,
+                                                       DImg albedo, DImg emissive, DImg normal, DImg velocity,
+                                                       ResolveParams p) {
+#pragma clang fp contract(off)
+    const int x = blockIdx.x * 64 + threadIdx.x, y = blockIdx.y * 4 + threadIdx.y;
+    if (x >= p.width || y >= p.height) return;
+    const unsigned long long key = vis[(size_t)y * p.width + x];
+    const uint32_t low = (uint32_t)key;
+    if (low == KEY_EMPTY) {   // clear values (g_buffer_generation.inl:78-100, depth cleared to 1.0)
+        row_ptr_w<float>(depth, y)[x] = 1.0f;
+        row_ptr_w<uint2>(albedo, y)[x] = pack_h4(f4{0.2f, 0.4f, 1.0f, 1.0f});
+        row_ptr_w<uint2>(emissive, y)[x] = pack_h4(f4{0.0f, 0.0f, 0.0f, 1.0f});
+        row_ptr_w<uint2>(normal, y)[x] = pack_h4(f4{0.0f, 0.0f, 0.0f, 1.0f});
+        row_ptr_w<uint2>(velocity, y)[x] = pack_h4(f4{0.0f, 0.0f, 0.0f, 1.0f});
+        return;
+    }
+    const int id = (int)(0xFFFFFFFEu - low);
+    const uint32_t ia = mesh.indices[3 * id], ib = mesh.indices[3 * id + 1], ic = mesh.indices[3 * id + 2];
+    const float4 A = clip_vertex(mesh.positions, ia, p.model, p.vp, p.width, p.height);
+    const float4 B = clip_vertex(mesh.positions, ib, p.model, p.vp, p.width, p.height);
+    const float4 C = clip_vertex(mesh.positions, ic, p.model, p.vp, p.width, p.height);
+    // perspective-correct barycentrics b_i = E_i / sum E from the raster's edge functions
+    const f3 v0{A.x, A.y, A.w}, v1{B.x, B.y, B.w}, v2{C.x, C.y, C.w};
+    f3 r0 = cross_exact(v1, v2), r1 = cross_exact(v2, v0), r2 = cross_exact(v0, v1);
+    const float det = v0.x * r0.x + v0.y * r0.y + v0.z * r0.z;
+    if (det < 0.0f) { r0 = -r0; r1 = -r1; r2 = -r2; }
+    const float fx = (float)x + 0.5f, fy = (float)y + 0.5f;
+    const float e0 = edge(r0, fx, fy), e1 = edge(r1, fx, fy), e2 = edge(r2, fx, fy);
+    const float es = e0 + e1 + e2;
+    const float b1 = e1 / es, b2 = e2 / es, b0 = 1.0f - b1 - b2;
+
+    // vertex stage (g_buffer_generation.inl:169-178): uv, normal_matrix * normal, current/previous clip
+    const float* uv = mesh.uvs;
+    const float u = b0 * uv[2 * ia] + b1 * uv[2 * ib] + b2 * uv[2 * ic];
+    const float v = b0 * uv[2 * ia + 1] + b1 * uv[2 * ib + 1] + b2 * uv[2 * ic + 1];
+    const float* nr = mesh.normals;
+    const f3 na = normalize_exact(mat3_vec_exact(p.normal3, f3{nr[3 * ia], nr[3 * ia + 1], nr[3 * ia + 2]}));
+    const f3 nb = normalize_exact(mat3_vec_exact(p.normal3, f3{nr[3 * ib], nr[3 * ib + 1], nr[3 * ib + 2]}));
+    const f3 nc = normalize_exact(mat3_vec_exact(p.normal3, f3{nr[3 * ic], nr[3 * ic + 1], nr[3 * ic + 2]}));
+    const f3 n = normalize_exact(f3{b0 * na.x + b1 * nb.x + b2 * nc.x, b0 * na.y + b1 * nb.y + b2 * nc.y,
+                                    b0 * na.z + b1 * nb.z + b2 * nc.z});
+    const uint32_t mi = mesh.materials ? min(mesh.materials[id], (uint32_t)(p.material_count - 1)) : 0u;
+    const soc_material& m = mats[mi];
+    f3 em = f3{0.0f, 0.0f, 0.0f};
+    if (m.has_emissive) {
+        const f4 e = sample_texture(m.emissive, u, v);
+        em = f3{e.x * m.emissive_factor[0], e.y * m.emissive_factor[1], e.z * m.emissive_factor[2]};
+    }
+    const f4 al = sample_texture(m.albedo, u, v);
+    f4 vel = f4{0.0f, 0.0f, 0.0f, 0.0f};
+    if (!(m.flags & SOC_MATERIAL_ZERO_VELOCITY)) {
+        const float* ps = mesh.positions;
+        f4 cc[3], pc[3];
+        const uint32_t vi[3] = {ia, ib, ic};
+        for (int k = 0; k < 3; ++k) {
+            const f4 wp = mat_vec_exact(p.model, ps[3 * vi[k]], ps[3 * vi[k] + 1], ps[3 * vi[k] + 2], 1.0f);
+            cc[k] = mat_vec_exact(p.vp, wp.x, wp.y, wp.z, wp.w);
+            pc[k] = mat_vec_exact(p.prev_vp, wp.x, wp.y, wp.z, wp.w);
+        }
+        const float cx = b0 * cc[0].x + b1 * cc[1].x + b2 * cc[2].x, cy = b0 * cc[0].y + b1 * cc[1].y + b2 * cc[2].y;
+        const float cw = b0 * cc[0].w + b1 * cc[1].w + b2 * cc[2].w;
+        const float px = b0 * pc[0].x + b1 * pc[1].x + b2 * pc[2].x, py = b0 * pc[0].y + b1 * pc[1].y + b2 * pc[2].y;
+        const float pw = b0 * pc[0].w + b1 * pc[1].w + b2 * pc[2].w;
+        vel = f4{((cx / cw) * 0.5f + 0.5f) - ((px / pw) * 0.5f + 0.5f), ((cy / cw) * 0.5f + 0.5f) - ((py / pw) * 0.5f + 0.5f),
+                 0.0f, 1.0f};
+    }
+    row_ptr_w<float>(depth, y)[x] = __uint_as_float((uint32_t)(key >> 32));
+    row_ptr_w<uint2>(albedo, y)[x] = pack_h4(f4{al.x * m.albedo_factor[0] + em.x, al.y * m.albedo_factor[1] + em.y,
+                                                al.z * m.albedo_factor[2] + em.z, 1.0f});
+    row_ptr_w<uint2>(emissive, y)[x] = pack_h4(f4{em.x, em.y, em.z, 1.0f});
+    row_ptr_w<uint2>(normal, y)[x] = pack_h4(f4{n.x, n.y, n.z, 1.0f});
+    row_ptr_w<uint2>(velocity, y)[x] = pack_h4(vel);
+}
+
+int check_mesh(const soc_mesh* mesh, const char* pass, bool attributes) {
+    if (!mesh || !mesh->positions || !mesh->indices || mesh->vertex_count < 0 || mesh->triangle_count < 0)
+        return set_error(SOC_E_INVALID_ARG, "%s: null mesh / positions / indices or negative counts", pass);
+    if (attributes && (!mesh->normals || !mesh->uvs))
+        return set_error(SOC_E_INVALID_ARG, "%s: the G-buffer resolve needs normals and uvs", pass);
+    if ((uint32_t)mesh->triangle_count >= 0xFFFFFFFEu)
+        return set_error(SOC_E_SHAPE, "%s: too many triangles for the visibility key", pass);
+    return SOC_OK;
+}
+
+RasterParams make_raster_params(const soc_mesh* mesh, const float* vp, int W, int H, int cull) {
+    RasterParams p{};
+    p.model = mat4(mesh->model_matrix);
+    p.vp = mat4(vp);
+    p.width = W;
+    p.height = H;
+    p.vertex_count = mesh->vertex_count;
+    p.triangle_count = mesh->triangle_count;
+    p.cull = cull;
+    p.item_capacity = (uint32_t)(4 * (size_t)mesh->triangle_count + (1u << 20));
+    return p;
+}
+
+int launch_raster(const soc_mesh* mesh, const RasterParams& p, void* target, size_t pitch, void* workspace,
+                  hipStream_t s, const char* pass) {
+    Workspace ws = carve(workspace, mesh->vertex_count, mesh->triangle_count);
+    raster_setup<<<ceil_div(max(mesh->vertex_count, 1), 256), 256, 0, s>>>(mesh->positions, ws, p);
+    if (mesh->triangle_count > 0) {
+        raster_small<<<ceil_div(mesh->triangle_count, 256), 256, 0, s>>>(mesh->indices, ws, p, target, pitch);
+        raster_big<<<2048, 256, 0, s>>>(mesh->indices, ws, p, target, pitch);
+    }
+    return check_launch(pass);
+}
+
+}  // namespace
+}  // namespace soc
+
+using namespace soc;
+
+extern "C" size_t soc_raster_workspace_size(int32_t vertex_count, int32_t triangle_count) {
+    if (vertex_count < 0 || triangle_count < 0) return 0;
+    return align_up((size_t)vertex_count * 16, 256) + 256 + (4 * (size_t)triangle_count + (1u << 20)) * 8;
+}
+
+extern "C" int soc_raster_visibility(const soc_mesh* mesh, const float view_projection[16], int32_t cull,
+                                     uint64_t* visibility, int32_t width, int32_t height, int32_t clear,
+                                     void* workspace, soc_stream stream) {
+    int rc = check_mesh(mesh, "soc_raster_visibility", false);
+    if (rc) return rc;
+    if (!view_projection || !visibility || !workspace || width <= 0 || height <= 0 || cull < 0 || cull > 2)
+        return set_error(SOC_E_INVALID_ARG, "soc_raster_visibility: null argument, bad extent or cull mode");
+    hipStream_t s = hs(stream);
+    if (clear) {
+        const size_t n = (size_t)width * height;
+        raster_clear_vis<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(reinterpret_cast<unsigned long long*>(visibility), n);
+    }
+    RasterParams p = make_raster_params(mesh, view_projection, width, height, cull);
+    return launch_raster(mesh, p, visibility, (size_t)width * 8, workspace, s, "raster_visibility");
+}
+
+extern "C" int soc_raster_depth(const soc_mesh* mesh, const float view_projection[16], int32_t cull, float bias_constant,
+                                float bias_slope, soc_img depth, void* workspace, soc_stream stream) {
+    int rc = check_mesh(mesh, "soc_raster_depth", false);
+    if (!rc) rc = check_img(depth, SOC_FMT_D32F, "soc_raster_depth", "depth");
+    if (rc) return rc;
+    if (!view_projection || !workspace || cull < 0 || cull > 2)
+        return set_error(SOC_E_INVALID_ARG, "soc_raster_depth: null argument or bad cull mode");
+    hipStream_t s = hs(stream);
+    // depth clear 1.0 (sun_shadow_draw.inl:71-74)
+    if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(depth.data), __builtin_bit_cast(int, 1.0f),
+                          (size_t)depth.pitch_bytes / 4 * depth.height, s) != hipSuccess)
+        return set_error(SOC_E_HIP, "soc_raster_depth: clear failed");
+    RasterParams p = make_raster_params(mesh, view_projection, depth.width, depth.height, cull);
+    p.depth_only = 1;
+    p.bias_constant = bias_constant;
+    p.bias_slope = bias_slope;
+    return launch_raster(mesh, p, depth.data, (size_t)depth.pitch_bytes, workspace, s, "raster_depth");
+}
+
+extern "C" int soc_gbuffer_resolve(const soc_globals* g, const soc_mesh* mesh, const soc_material* d_materials,
+                                   int32_t material_count, const uint64_t* visibility, soc_img depth, soc_img albedo,
+                                   soc_img emissive, soc_img normal, soc_img velocity, soc_stream stream) {
+    int rc = check_mesh(mesh, "soc_gbuffer_resolve", true);
+    if (!rc) rc = check_img(depth, SOC_FMT_D32F, "soc_gbuffer_resolve", "depth");
+    if (!rc) rc = check_img(albedo, SOC_FMT_RGBA16F, "soc_gbuffer_resolve", "albedo");
+    if (!rc) rc = check_img(emissive, SOC_FMT_RGBA16F, "soc_gbuffer_resolve", "emissive");
+    if (!rc) rc = check_img(normal, SOC_FMT_RGBA16F, "soc_gbuffer_resolve", "normal");
+    if (!rc) rc = check_img(velocity, SOC_FMT_RGBA16F, "soc_gbuffer_resolve", "velocity");
+    if (rc) return rc;
+    if (!g || !d_materials || material_count <= 0 || !visibility)
+        return set_error(SOC_E_INVALID_ARG, "soc_gbuffer_resolve: null globals / materials / visibility");
+    const int W = depth.width, H = depth.height;
+    for (const soc_img* im : {&albedo, &emissive, &normal, &velocity})
+        if (im->width != W || im->height != H)
+            return set_error(SOC_E_SHAPE, "soc_gbuffer_resolve: G-buffer images must share the depth extent");
+    ResolveParams p{};
+    p.model = mat4(mesh->model_matrix);
+    p.vp = mat4(g->camera_projection_view_matrix);
+    p.prev_vp = mat4(g->camera_previous_projection_view_matrix);
+    const float* nm = mesh->normal_matrix;   // f32mat3x3(normal_matrix): upper 3x3, column-major
+    const float n3[9] = {nm[0], nm[1], nm[2], nm[4], nm[5], nm[6], nm[8], nm[9], nm[10]};
+    for (int i = 0; i < 9; ++i) p.normal3.m[i] = n3[i];
+    p.width = W;
+    p.height = H;
+    p.triangle_count = mesh->triangle_count;
+    p.material_count = material_count;
+    dim3 blk(64, 4), grd(ceil_div(W, 64), ceil_div(H, 4));
+    gbuffer_resolve<<<grd, blk, 0, hs(stream)>>>(*mesh, d_materials, reinterpret_cast<const unsigned long long*>(visibility),
+                                                 dimg(depth), dimg(albedo), dimg(emissive), dimg(normal), dimg(velocity), p);
+    return check_launch("gbuffer_resolve");
+}

@@ -1,0 +1,133 @@
+"""Host binding of the rasteriser passes (include/soc_rt.h "Rasterisation").
+
+The reference draws its meshes with three raster pipelines: DepthPrepassTask (depth_prepass.inl:26-120),
+GBufferGenerationTask (g_buffer_generation.inl:33-230) and SunShadowDrawTask (sun_shadow_draw.inl:27-91).
+Here they are a visibility-buffer raster + resolve in libsoc_rt.so; this module only packs the mesh and
+material structs (device pointers) and calls the C ABI. The same struct helpers accept numpy arrays so the
+CPU oracle can be driven with host pointers.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _abi, _check, _gp, _ptr, _stream, img, lib
+from ._abi import CULL_BACK, CULL_FRONT, CULL_NONE, FMT_RGBA8_SRGB, MATERIAL_ZERO_VELOCITY, Material, Mesh
+
+__all__ = ["CULL_NONE", "CULL_FRONT", "CULL_BACK", "MATERIAL_ZERO_VELOCITY", "MeshBuffers", "material",
+           "normal_matrix", "materials_device", "raster_visibility", "raster_depth", "gbuffer_resolve",
+           "SHADOW_BIAS_CONSTANT", "SHADOW_BIAS_SLOPE"]
+
+# sun_shadow_draw.inl:47-50 / :81
+SHADOW_BIAS_CONSTANT = 1.25
+SHADOW_BIAS_SLOPE = 1.75
+
+IDENTITY = np.eye(4, dtype=np.float32)
+
+
+def normal_matrix(model) -> np.ndarray:
+    """transpose(inverse(model)) (scene.cpp:69), column-major float32[16]."""
+    m = np.asarray(model, np.float64).reshape(4, 4).T            # M (row-major) from the column-major flat
+    # column-major flat of N = inverse(M)^T is the row-major flat of inverse(M)
+    return np.ascontiguousarray(np.linalg.inv(m).astype(np.float32)).reshape(16)
+
+
+def _colmajor(model) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(model, np.float32).reshape(16))
+
+
+@dataclass
+class MeshBuffers:
+    """A mesh's vertex / index / material-index arrays (torch device tensors or numpy host arrays) and its
+    soc_mesh struct. `model` is a column-major 4x4 (glm layout), identity by default."""
+    positions: object
+    normals: object
+    uvs: object
+    indices: object
+    materials: object = None
+    model: np.ndarray = field(default_factory=lambda: IDENTITY.reshape(16).copy())
+    struct: Mesh = None
+
+    def __post_init__(self):
+        def addr(a):
+            if a is None:
+                return None
+            if isinstance(a, torch.Tensor):
+                assert a.is_contiguous()
+                return a.data_ptr()
+            assert a.flags["C_CONTIGUOUS"]
+            return a.ctypes.data
+        s = Mesh()
+        s.positions, s.normals, s.uvs = addr(self.positions), addr(self.normals), addr(self.uvs)
+        s.indices, s.materials = addr(self.indices), addr(self.materials)
+        s.vertex_count = int(self.positions.shape[0])
+        s.triangle_count = int(self.indices.shape[0])
+        s.model_matrix[:] = _colmajor(self.model).tolist()
+        s.normal_matrix[:] = normal_matrix(self.model).tolist()
+        self.struct = s
+
+    @classmethod
+    def from_numpy(cls, positions, normals, uvs, indices, materials=None, model=None, device="cuda"):
+        t = lambda a, dt: None if a is None else torch.from_numpy(np.ascontiguousarray(a, dt)).to(device)
+        return cls(t(positions, np.float32), t(normals, np.float32), t(uvs, np.float32), t(indices, np.uint32),
+                   t(materials, np.uint32), IDENTITY.reshape(16).copy() if model is None else _colmajor(model))
+
+    def workspace(self, device="cuda") -> torch.Tensor:
+        n = lib().soc_raster_workspace_size(self.struct.vertex_count, self.struct.triangle_count)
+        return torch.empty(n, dtype=torch.uint8, device=device)
+
+
+def material(albedo=None, emissive=None, albedo_factor=(1.0, 1.0, 1.0, 1.0), emissive_factor=(1.0, 1.0, 1.0, 1.0),
+             flags=0, has_emissive: Optional[bool] = None, srgb=True) -> Material:
+    """soc_material: albedo / emissive RGBA8 textures ((H, W, 4) uint8 tensors or arrays; sRGB like the
+    reference's baseColor/emissive images, model.cpp:52-71) or None (white / no emissive)."""
+    m = Material()
+    fmt = FMT_RGBA8_SRGB if srgb else None
+    m.albedo = img(albedo, fmt) if albedo is not None else img(None)
+    m.emissive = img(emissive, fmt) if emissive is not None else img(None)
+    m.albedo_factor[:] = [float(v) for v in albedo_factor]
+    m.emissive_factor[:] = [float(v) for v in emissive_factor]
+    m.flags = int(flags)
+    m.has_emissive = int(emissive is not None if has_emissive is None else has_emissive)
+    return m
+
+
+def materials_device(mats: Sequence[Material], device="cuda") -> torch.Tensor:
+    """Device copy of a soc_material array (raw bytes)."""
+    arr = (Material * len(mats))(*mats)
+    raw = np.frombuffer(bytes(arr), dtype=np.uint8).copy()
+    return torch.from_numpy(raw).to(device)
+
+
+def raster_visibility(mesh: MeshBuffers, view_projection, cull, visibility: torch.Tensor, workspace: torch.Tensor,
+                      clear=True, stream=None):
+    """Depth prepass into an (H, W) int64/uint64 visibility buffer (depth bits << 32 | triangle key)."""
+    H, W = visibility.shape
+    vp = (C.c_float * 16)(*[float(v) for v in np.asarray(view_projection, np.float32).reshape(16)])
+    _check(lib().soc_raster_visibility(C.byref(mesh.struct), vp, int(cull), _ptr(visibility), W, H, int(bool(clear)),
+                                       _ptr(workspace), _stream(stream)), "raster_visibility")
+
+
+def raster_depth(mesh: MeshBuffers, view_projection, cull, depth: torch.Tensor, workspace: torch.Tensor,
+                 bias_constant=0.0, bias_slope=0.0, stream=None):
+    """Depth-only raster into a D32 image (the sun shadow map with SHADOW_BIAS_*)."""
+    vp = (C.c_float * 16)(*[float(v) for v in np.asarray(view_projection, np.float32).reshape(16)])
+    _check(lib().soc_raster_depth(C.byref(mesh.struct), vp, int(cull), float(bias_constant), float(bias_slope),
+                                  img(depth), _ptr(workspace), _stream(stream)), "raster_depth")
+
+
+def gbuffer_resolve(g, mesh: MeshBuffers, d_materials: torch.Tensor, material_count: int, visibility: torch.Tensor,
+                    depth, albedo, emissive, normal, velocity, stream=None):
+    _check(lib().soc_gbuffer_resolve(_gp(g), C.byref(mesh.struct), _ptr(d_materials), int(material_count),
+                                     _ptr(visibility), img(depth), img(albedo), img(emissive), img(normal), img(velocity),
+                                     _stream(stream)), "gbuffer_resolve")
+
+
+def visibility_triangles(vis) -> np.ndarray:
+    """Triangle id per pixel (-1 = empty) of a host visibility buffer (uint64/int64 array)."""
+    low = (np.asarray(vis).view(np.uint64) & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    return np.where(low == 0xFFFFFFFF, -1, 0xFFFFFFFE - low)

@@ -40,6 +40,10 @@ def lib():
             "soc_scene_gbuffer": (C.c_int, [C.c_int, G, C.c_int, C.c_int] + [C.c_void_p] * 5),
             "soc_scene_shadow": (C.c_int, [C.c_int, G, C.c_int, C.c_void_p]),
             "soc_scene_box_count": (C.c_int, [C.c_int]),
+            "soc_scene_mesh_counts": (C.c_int, [C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+            "soc_scene_mesh": (C.c_int, [C.c_int, G] + [C.c_void_p] * 5),
+            "soc_scene_material_count": (C.c_int, [C.c_int]),
+            "soc_scene_material_textures": (C.c_int, [C.c_int, G, C.c_int, C.c_void_p, C.c_void_p]),
         })
         _LIB = l
     return _LIB
@@ -62,6 +66,31 @@ def shadow_map(g: Globals, size: int = 4096, scene_id: int = SPONZA_PROXY) -> np
     if lib().soc_scene_shadow(scene_id, C.byref(g), size, s.ctypes.data):
         raise RuntimeError("soc_scene_shadow failed")
     return s
+
+
+def mesh(g: Globals, scene_id: int = SPONZA_PROXY) -> dict:
+    """The scene as a triangle mesh for the rasteriser: positions/normals (V,3) f32, uvs (V,2) f32,
+    indices (T,3) u32, materials (T,) u32."""
+    nv, nt = C.c_int(), C.c_int()
+    lib().soc_scene_mesh_counts(scene_id, C.byref(nv), C.byref(nt))
+    V, T = nv.value, nt.value
+    out = {"positions": np.zeros((V, 3), np.float32), "normals": np.zeros((V, 3), np.float32),
+           "uvs": np.zeros((V, 2), np.float32), "indices": np.zeros((T, 3), np.uint32),
+           "materials": np.zeros(T, np.uint32)}
+    if lib().soc_scene_mesh(scene_id, C.byref(g), *(out[k].ctypes.data for k in
+                                                    ("positions", "normals", "uvs", "indices", "materials"))):
+        raise RuntimeError("soc_scene_mesh failed")
+    return out
+
+
+def material_textures(g: Globals, size: int, scene_id: int = SPONZA_PROXY):
+    """(M, size, size, 4) uint8 albedo textures (linear values, UNORM) and (M, 3) emissive factors."""
+    m = lib().soc_scene_material_count(scene_id)
+    tex = np.zeros((m, size, size, 4), np.uint8)
+    em = np.zeros((m, 3), np.float32)
+    if lib().soc_scene_material_textures(scene_id, C.byref(g), size, tex.ctypes.data, em.ctypes.data):
+        raise RuntimeError("soc_scene_material_textures failed")
+    return tex, em
 
 
 def noise_texture() -> np.ndarray:

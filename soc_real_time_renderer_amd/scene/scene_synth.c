@@ -513,3 +513,136 @@ int soc_scene_shadow(int scene_id, const soc_globals* g, int S, float* shadow) {
 }
 
 int soc_scene_box_count(int scene_id) { return get_scene(scene_id)->n; }
+
+/* ---------------------------------------------------------------------------------------------------
+ * Scenes as triangle meshes, for the GPU rasteriser (include/soc_rt.h "Rasterisation"):
+ *  - terrain: the tessellated grid above (T_NV^2 vertices, 2*T_SEGS^2 triangles, in terrain_raster's
+ *    order, each wound counter-clockwise seen from above), analytic vertex normals, uv in [0, 1]^2, and its albedo baked into an RGBA8 texture (the
+ *    reference samples its terrain albedo from an image, draw_terrain.inl:196-222);
+ *  - Sponza-proxy: the same boxes, 12 triangles each (faces wound counter-clockwise seen from outside),
+ *    per-face normals, planar uvs in world units (the material() mapping), one material per box kind
+ *    with a tiled procedural texture (0.5 x 0.25 blocks + mortar) of 4 x 4 world units.
+ * ------------------------------------------------------------------------------------------------- */
+int soc_scene_mesh_counts(int scene_id, int* vertices, int* triangles) {
+    if (!vertices || !triangles) return -1;
+    if (scene_id == SCENE_TERRAIN) { *vertices = T_NV * T_NV; *triangles = 2 * T_SEGS * T_SEGS; return 0; }
+    const scene* s = get_scene(scene_id);
+    *vertices = 24 * s->n;
+    *triangles = 12 * s->n;
+    return 0;
+}
+
+int soc_scene_mesh(int scene_id, const soc_globals* g, float* positions, float* normals, float* uvs, uint32_t* indices,
+                   uint32_t* materials) {
+    if (!g || !positions || !normals || !uvs || !indices || !materials) return -1;
+    if (scene_id == SCENE_TERRAIN) {
+        const terrain_mesh* t = get_terrain(g);
+#pragma omp parallel for
+        for (int j = 0; j < T_NV; ++j)
+            for (int i = 0; i < T_NV; ++i) {
+                const int k = j * T_NV + i;
+                const float u = (float)i / (float)T_SEGS, v = (float)j / (float)T_SEGS;
+                const v3 n = terrain_normal(t, u, v);
+                positions[3 * k] = t->p[k].x; positions[3 * k + 1] = t->p[k].y; positions[3 * k + 2] = t->p[k].z;
+                normals[3 * k] = n.x; normals[3 * k + 1] = n.y; normals[3 * k + 2] = n.z;
+                uvs[2 * k] = u; uvs[2 * k + 1] = v;
+            }
+        for (int id = 0; id < 2 * T_SEGS * T_SEGS; ++id) {
+            const int q = id >> 1, qi = q % T_SEGS, qj = q / T_SEGS;
+            const int v00 = qj * T_NV + qi, v10 = v00 + 1, v01 = v00 + T_NV, v11 = v01 + 1;
+            /* counter-clockwise seen from above (outward = up, like the boxes' faces) */
+            indices[3 * id] = (uint32_t)v00;
+            indices[3 * id + 1] = (uint32_t)((id & 1) ? v01 : v11);
+            indices[3 * id + 2] = (uint32_t)((id & 1) ? v11 : v10);
+            materials[id] = 0;
+        }
+        return 0;
+    }
+    const scene* s = get_scene(scene_id);
+    /* face f: axis a = f/2, side = f&1 (0: lo, 1: hi); its 4 corners counter-clockwise seen from outside */
+    for (int bi = 0; bi < s->n; ++bi) {
+        const box* b = &s->b[bi];
+        for (int f = 0; f < 6; ++f) {
+            const int a = f >> 1, hi = f & 1;
+            const int a1 = (a + 1) % 3, a2 = (a + 2) % 3;
+            float lo3[3] = {b->lo.x, b->lo.y, b->lo.z}, hi3[3] = {b->hi.x, b->hi.y, b->hi.z};
+            float nrm[3] = {0, 0, 0};
+            nrm[a] = hi ? 1.0f : -1.0f;
+            /* corners in (a1, a2): (0,0) (1,0) (1,1) (0,1); that order is CCW around +a; reverse for -a */
+            const int c1[4] = {0, 1, 1, 0}, c2[4] = {0, 0, 1, 1};
+            const int base = 24 * bi + 4 * f;
+            for (int k = 0; k < 4; ++k) {
+                const int kk = hi ? k : (3 - k);
+                float p[3];
+                p[a] = hi ? hi3[a] : lo3[a];
+                p[a1] = c1[kk] ? hi3[a1] : lo3[a1];
+                p[a2] = c2[kk] ? hi3[a2] : lo3[a2];
+                float* P = positions + 3 * (base + k);
+                P[0] = p[0]; P[1] = p[1]; P[2] = p[2];
+                float* N = normals + 3 * (base + k);
+                N[0] = nrm[0]; N[1] = nrm[1]; N[2] = nrm[2];
+                /* material(): u = |n.x| > 0.5 ? p.z : p.x, v = |n.y| > 0.5 ? p.z : p.y */
+                uvs[2 * (base + k)] = a == 0 ? p[2] : p[0];
+                uvs[2 * (base + k) + 1] = a == 1 ? p[2] : p[1];
+            }
+            const int tb = 12 * bi + 2 * f;
+            indices[3 * tb] = (uint32_t)base; indices[3 * tb + 1] = (uint32_t)(base + 1); indices[3 * tb + 2] = (uint32_t)(base + 2);
+            indices[3 * tb + 3] = (uint32_t)base; indices[3 * tb + 4] = (uint32_t)(base + 2); indices[3 * tb + 5] = (uint32_t)(base + 3);
+            materials[tb] = materials[tb + 1] = (uint32_t)b->mat;
+        }
+    }
+    return 0;
+}
+
+/* Material textures: terrain -> one size x size RGBA8 albedo over uv [0,1]^2 (terrain_material at texel
+   centres); Sponza-proxy -> M_COUNT stacked size x size RGBA8 tiles covering 4 x 4 world units
+   (block tint + mortar of material(), linear values stored as UNORM). Emissive factors per material
+   go to emissive_rgb (3 floats per material; terrain: 1 material). */
+int soc_scene_material_count(int scene_id) { return scene_id == SCENE_TERRAIN ? 1 : M_COUNT; }
+
+int soc_scene_material_textures(int scene_id, const soc_globals* g, int size, uint8_t* rgba, float* emissive_rgb) {
+    if (!g || size <= 0 || !rgba || !emissive_rgb) return -1;
+    if (scene_id == SCENE_TERRAIN) {
+        const terrain_mesh* t = get_terrain(g);
+#pragma omp parallel for schedule(dynamic, 8)
+        for (int y = 0; y < size; ++y)
+            for (int x = 0; x < size; ++x) {
+                const float u = ((float)x + 0.5f) / (float)size, v = ((float)y + 0.5f) / (float)size;
+                const v3 n = terrain_normal(t, u, v);
+                const float hgt = (terrain_height(u, v) - t->mid) * t->hscale;
+                float alb[3];
+                terrain_material(hgt, n, u, v, alb);
+                uint8_t* o = rgba + 4 * ((size_t)y * size + x);
+                for (int c = 0; c < 3; ++c) {
+                    float cl = alb[c] < 0.0f ? 0.0f : (alb[c] > 1.0f ? 1.0f : alb[c]);
+                    o[c] = (uint8_t)lrintf(cl * 255.0f);
+                }
+                o[3] = 255;
+            }
+        emissive_rgb[0] = emissive_rgb[1] = emissive_rgb[2] = 0.0f;
+        return 0;
+    }
+    for (int m = 0; m < M_COUNT; ++m) {
+#pragma omp parallel for
+        for (int y = 0; y < size; ++y)
+            for (int x = 0; x < size; ++x) {
+                /* texel centre -> world (u, v) in [0, 4): the tile repeats every 4 units */
+                const float u = ((float)x + 0.5f) / (float)size * 4.0f, v = ((float)y + 0.5f) / (float)size * 4.0f;
+                const int bu = (int)floorf(u * 2.0f), bv = (int)floorf(v * 4.0f);
+                const float tint = 0.8f + 0.4f * hash3(bu, bv, m);
+                const float fu = u * 2.0f - floorf(u * 2.0f), fv = v * 4.0f - floorf(v * 4.0f);
+                const float mortar = (fu < 0.04f || fv < 0.06f) ? 0.55f : 1.0f;
+                uint8_t* o = rgba + 4 * (((size_t)m * size + y) * size + x);
+                for (int c = 0; c < 3; ++c) {
+                    float cl = k_base[m][c] * tint * mortar;
+                    cl = cl < 0.0f ? 0.0f : (cl > 1.0f ? 1.0f : cl);
+                    o[c] = (uint8_t)lrintf(cl * 255.0f);
+                }
+                o[3] = 255;
+            }
+        emissive_rgb[3 * m] = m == M_LAMP ? 4.0f : 0.0f;
+        emissive_rgb[3 * m + 1] = m == M_LAMP ? 2.6f : 0.0f;
+        emissive_rgb[3 * m + 2] = m == M_LAMP ? 1.2f : 0.0f;
+    }
+    return 0;
+}

@@ -1,0 +1,142 @@
+"""Rasteriser parity (-m gpu): the HIP visibility buffer, depth-only raster and G-buffer resolve against
+the CPU oracle, through the C ABI.
+
+Tolerances: visibility buffer (depth bits + triangle key) and depth-only images are bit-exact (integer /
+ordered-float work from identically ordered fp32 arithmetic); the G-buffer resolve's RGBA16F outputs
+|d| <= 1e-3 + 2e-3|ref| (the GPU powf of the sRGB decode may differ by an ulp from glibc's).
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import SPONZA_CAMERA, TERRAIN_CAMERA, f16_close, globals_for
+from soc_real_time_renderer_amd import raster, scene
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def scene_meshes(g, scene_id):
+    m = scene.mesh(g, scene_id)
+    host_mesh = raster.MeshBuffers(m["positions"], m["normals"], m["uvs"], m["indices"], m["materials"])
+    dev_mesh = raster.MeshBuffers.from_numpy(m["positions"], m["normals"], m["uvs"], m["indices"], m["materials"])
+    return host_mesh, dev_mesh
+
+
+def soup_mesh(n, seed, big):
+    """n world-space triangles scattered around the Sponza camera (some behind it, some crossing the
+    near plane): small ones, and with big=True a share of huge ones (the wave-per-chunk path)."""
+    rng = np.random.default_rng(seed)
+    cam = np.float32(SPONZA_CAMERA[0])
+    c = cam + rng.uniform(-20, 20, (n, 1, 3)).astype(np.float32)
+    size = rng.uniform(0.02, 0.3, (n, 1, 1))
+    if big:
+        size[: n // 8] = rng.uniform(3.0, 40.0, (n // 8, 1, 1))
+    pos = (c + size * rng.normal(size=(n, 3, 3))).reshape(-1, 3).astype(np.float32)
+    normals = np.tile(np.float32([0, 1, 0]), (len(pos), 1))
+    uvs = pos[:, :2].copy()
+    return pos, normals, uvs, np.arange(3 * n, dtype=np.uint32).reshape(n, 3)
+
+
+@pytest.mark.parametrize("scene_id,camera,W,H", [(scene.TERRAIN, TERRAIN_CAMERA, 512, 288),
+                                                 (scene.SPONZA_PROXY, SPONZA_CAMERA, 512, 288),
+                                                 (scene.TERRAIN, TERRAIN_CAMERA, 1920, 1080),
+                                                 (scene.SPONZA_PROXY, SPONZA_CAMERA, 97, 55)])
+@pytest.mark.parametrize("cull", [raster.CULL_FRONT, raster.CULL_NONE])
+def test_visibility_bit_exact(soc, oracle, scene_id, camera, W, H, cull):
+    g = globals_for(W, H, camera=camera)
+    vp = np.ctypeslib.as_array(g.camera_projection_view_matrix)
+    hm, dm = scene_meshes(g, scene_id)
+    ref = np.zeros((H, W), np.uint64)
+    oracle.raster_visibility(hm, vp, cull, ref)
+    vis = torch.zeros((H, W), dtype=torch.int64, device=DEV)
+    raster.raster_visibility(dm, vp, cull, vis, dm.workspace())
+    got = host(vis).view(np.uint64)
+    assert np.array_equal(got, ref), (got != ref).mean()
+    assert (raster.visibility_triangles(ref) >= 0).mean() > 0.3
+
+
+@pytest.mark.parametrize("n,big", [(8000, False), (3000, True)])
+def test_visibility_triangle_soup_bit_exact(soc, oracle, n, big):
+    """Overlapping triangles of every size (big ones take the wave-per-chunk path) and depths outside
+    [0, 1]: same winners as the serial oracle."""
+    W, H = 1920, 1080
+    g = globals_for(W, H, camera=SPONZA_CAMERA)
+    vp = np.ctypeslib.as_array(g.camera_projection_view_matrix)
+    pos, normals, uvs, idx = soup_mesh(n, 11 + n, big)
+    hm = raster.MeshBuffers(pos, normals, uvs, idx)
+    dm = raster.MeshBuffers.from_numpy(pos, normals, uvs, idx)
+    ref = np.zeros((H, W), np.uint64)
+    oracle.raster_visibility(hm, vp, raster.CULL_NONE, ref)
+    vis = torch.zeros((H, W), dtype=torch.int64, device=DEV)
+    raster.raster_visibility(dm, vp, raster.CULL_NONE, vis, dm.workspace())
+    assert np.array_equal(host(vis).view(np.uint64), ref), (host(vis).view(np.uint64) != ref).mean()
+    assert (raster.visibility_triangles(ref) >= 0).mean() > 0.05
+
+
+def test_visibility_accumulates_without_clear(soc, oracle):
+    """clear = 0 keeps the previous contents: two draws equal one draw of the concatenated mesh when the
+    second mesh's triangle ids continue the first's (here: the same mesh twice -> identical buffer)."""
+    W, H = 256, 144
+    g = globals_for(W, H, camera=SPONZA_CAMERA)
+    vp = np.ctypeslib.as_array(g.camera_projection_view_matrix)
+    _, dm = scene_meshes(g, scene.SPONZA_PROXY)
+    a = torch.zeros((H, W), dtype=torch.int64, device=DEV)
+    ws = dm.workspace()
+    raster.raster_visibility(dm, vp, raster.CULL_FRONT, a, ws)
+    b = a.clone()
+    raster.raster_visibility(dm, vp, raster.CULL_FRONT, b, ws, clear=False)
+    assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("scene_id,S", [(scene.TERRAIN, 1024), (scene.SPONZA_PROXY, 1024), (scene.TERRAIN, 2048)])
+def test_shadow_depth_bit_exact(soc, oracle, scene_id, S):
+    """The sun shadow map (SunShadowDrawTask: cull BACK, bias 1.25 / 1.75) is bit-exact."""
+    g = globals_for(256, 144, camera=TERRAIN_CAMERA if scene_id == scene.TERRAIN else SPONZA_CAMERA)
+    vp = np.ctypeslib.as_array(g.sun_info.projection_view_matrix)
+    hm, dm = scene_meshes(g, scene_id)
+    ref = np.zeros((S, S), np.float32)
+    oracle.raster_depth(hm, vp, raster.CULL_BACK, ref, raster.SHADOW_BIAS_CONSTANT, raster.SHADOW_BIAS_SLOPE)
+    d = torch.zeros((S, S), dtype=torch.float32, device=DEV)
+    raster.raster_depth(dm, vp, raster.CULL_BACK, d, dm.workspace(), raster.SHADOW_BIAS_CONSTANT,
+                        raster.SHADOW_BIAS_SLOPE)
+    got = host(d)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), (got != ref).mean()
+
+
+@pytest.mark.parametrize("scene_id,camera,W,H", [(scene.SPONZA_PROXY, SPONZA_CAMERA, 480, 270),
+                                                 (scene.TERRAIN, TERRAIN_CAMERA, 480, 270),
+                                                 (scene.SPONZA_PROXY, SPONZA_CAMERA, 1920, 1080)])
+def test_gbuffer_resolve(soc, oracle, scene_id, camera, W, H):
+    g = globals_for(W, H, camera=camera)
+    vp = np.ctypeslib.as_array(g.camera_projection_view_matrix)
+    hm, dm = scene_meshes(g, scene_id)
+    tex, em = scene.material_textures(g, 128, scene_id)
+    srgb = scene_id == scene.SPONZA_PROXY   # exercise both texture formats
+    flags = raster.MATERIAL_ZERO_VELOCITY if scene_id == scene.TERRAIN else 0
+    hmats = [raster.material(albedo=tex[i], emissive_factor=tuple(em[i]) + (1.0,), has_emissive=bool(em[i].any()),
+                             flags=flags, srgb=srgb) for i in range(len(tex))]
+    dtex = [torch.from_numpy(tex[i]).to(DEV) for i in range(len(tex))]
+    dmats = [raster.material(albedo=dtex[i], emissive_factor=tuple(em[i]) + (1.0,), has_emissive=bool(em[i].any()),
+                             flags=flags, srgb=srgb) for i in range(len(tex))]
+    dmat = raster.materials_device(dmats)
+    vis = np.zeros((H, W), np.uint64)
+    oracle.raster_visibility(hm, vp, raster.CULL_FRONT, vis)
+    ref = {k: np.zeros((H, W, 4), np.float16) for k in ("albedo", "emissive", "normal", "velocity")}
+    ref["depth"] = np.zeros((H, W), np.float32)
+    oracle.gbuffer_resolve(g, hm, hmats, vis, ref["depth"], ref["albedo"], ref["emissive"], ref["normal"],
+                           ref["velocity"])
+    dvis = torch.zeros((H, W), dtype=torch.int64, device=DEV)
+    raster.raster_visibility(dm, vp, raster.CULL_FRONT, dvis, dm.workspace())
+    out = {k: torch.zeros((H, W, 4), dtype=torch.float16, device=DEV) for k in ("albedo", "emissive", "normal", "velocity")}
+    out["depth"] = torch.zeros((H, W), dtype=torch.float32, device=DEV)
+    raster.gbuffer_resolve(g, dm, dmat, len(dmats), dvis, out["depth"], out["albedo"], out["emissive"], out["normal"],
+                           out["velocity"])
+    assert np.array_equal(host(out["depth"]), ref["depth"])
+    for k in ("albedo", "emissive", "normal", "velocity"):
+        assert f16_close(host(out[k]), ref[k]).all(), k
