@@ -27,7 +27,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import soc_real_time_renderer_amd as soc  # noqa: E402
-from soc_real_time_renderer_amd import multi_gpu, scene  # noqa: E402
+from soc_real_time_renderer_amd import multi_gpu, raster, scene  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 
@@ -125,6 +125,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-frames", type=int, default=20)
     ap.add_argument("--no-sky-lane", action="store_true", help="run CloudRendering on the frame stream too")
+    ap.add_argument("--write-frame", default="", help="write the last frame's tone-mapped framebuffer (PNG)")
+    ap.add_argument("--metrics-jsonl", default="", help="one GPU-metric JSON line per profiled frame")
+    ap.add_argument("--raster", action="store_true",
+                    help="end-to-end frame: rasterise the scene mesh into the G-buffer and the 4096^2 sun shadow "
+                         "map every frame (DepthPrepass / SunShadowDraw / GBufferGeneration in the graph)")
     args = ap.parse_args()
 
     rank, world, local_rank = multi_gpu.env()
@@ -147,6 +152,10 @@ def main():
     fr["shadow"].copy_(torch.from_numpy(shadow))
     fr["noise"].copy_(torch.from_numpy(noise))
     r = soc.Renderer(fr, sky_lane=not args.no_sky_lane)
+    if args.raster:
+        sc = raster.scene_setup(g, scene_id, tex_size=1024, device=device)
+        vis = torch.empty((H, W), dtype=torch.int64, device=device)
+        r.set_raster_scene(sc["mesh"], sc["materials"], sc["material_count"], vis, sc["workspace"], shadow=True)
     r.set_exposure_pixels(*multi_gpu.exposure_pixels(world, W, H))
     bins = fr["auto_exposure"][1:]
     names = r.pass_names()
@@ -185,10 +194,19 @@ def main():
     r.set_async(False)
     r.set_pass_timing(-1, True)
     r.reset_timing()
-    for _ in range(args.profile_frames):
+    metrics_lines = []
+    for i in range(args.profile_frames):
         frame()
+        if args.metrics_jsonl:   # the reference's per-frame "GPU Metric" record (renderer.cpp:769-806)
+            torch.cuda.synchronize()
+            metrics_lines.append(r.metrics_json(i))
     torch.cuda.synchronize()
     stats = r.pass_stats()
+    if args.metrics_jsonl and rank == 0:
+        with open(args.metrics_jsonl, "w") as f:
+            f.write("\n".join(metrics_lines) + "\n")
+    if args.write_frame and rank == 0:   # headless present: the RGBA8 framebuffer to a host image
+        soc.write_png(args.write_frame, soc.read_image(fr["output"]))
     r.set_async(not args.no_sky_lane)
     ms_pass = {n: round(ms, 4) for n, _, ms, _ in stats}
     ms_group = {}
@@ -229,7 +247,10 @@ def main():
                                f"TAA, AgX tone map",
                    "resolution": [W, H], "f_sky": round(f_sky, 4), "parallelism": f"frame-per-gpu x{world}",
                    "histogram_allreduce": world > 1,
-                   "sky_lane": "CloudRendering on a concurrent stream, joined before Composition"},
+                   "sky_lane": "CloudRendering on a concurrent stream, joined before Composition",
+                   "raster": (f"in-frame: DepthPrepass + SunShadowDraw (4096^2) + GBufferGeneration of the "
+                              f"{int(sc['mesh'].struct.triangle_count)}-triangle scene mesh") if args.raster
+                   else "off: G-buffer and shadow map are resident inputs"},
         "roofline": {"kernel": comp, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "traffic_source": traffic_src,

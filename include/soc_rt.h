@@ -453,6 +453,32 @@ int soc_gbuffer_resolve(const soc_globals* g, const soc_mesh* mesh, const soc_ma
                         int32_t material_count, const uint64_t* visibility, soc_img depth, soc_img albedo,
                         soc_img emissive, soc_img normal, soc_img velocity, soc_stream stream);
 
+/* Render-graph raster head (renderer.cpp:965-1021: DepthPrepass, SunShadowDraw, GBufferGeneration): with a
+ * scene set, every PRE phase first rasterises the mesh into the frame's G-buffer images (depth, albedo,
+ * emissive, normal, velocity) and, with `shadow`, the sun shadow map into images.shadow, on the caller's
+ * stream before the sky lane forks. The renderer copies the struct (the arrays stay caller-owned). Passes
+ * are rebuilt: per-pass timing set before this call is re-enabled only through SOC_RENDERER_TIMING. */
+typedef struct soc_raster_scene {
+    soc_mesh mesh;                     /* device arrays */
+    const soc_material* materials;     /* device array */
+    int32_t material_count;
+    int32_t shadow;                    /* 1: SunShadowDraw into images.shadow (cull BACK, bias 1.25 / 1.75) */
+    uint64_t* visibility;              /* width*height u64, device */
+    void* workspace;                   /* soc_raster_workspace_size(mesh) bytes, device */
+} soc_raster_scene;
+int soc_renderer_set_raster_scene(soc_renderer* r, const soc_raster_scene* scene);   /* NULL: clear */
+
+/* --- Headless output and metrics (replaces the swapchain present of tone_mapping.inl:
+ * 172-176 and the ImGui "GPU Metric" window of renderer.cpp:769-806) ------------------------------- */
+/* The most recent frame's timed passes as one JSON object: {"frame", "total_gpu_ms", "groups" (the 12
+ * group names of renderer.cpp:577-588, 0 when absent), "passes"}. Writes at most cap-1 bytes + NUL;
+ * returns the full length (snprintf-style) or < 0. Needs a completed stream. */
+int64_t soc_renderer_metrics_json(soc_renderer* r, uint64_t frame, char* buf, size_t cap);
+/* Device image -> host rows, stream-ordered. */
+int soc_read_image(soc_img image, void* host, int32_t host_pitch_bytes, soc_stream stream);
+/* 8-bit RGBA host image -> PNG file (uncompressed deflate; no external library). */
+int soc_write_png(const char* path, const void* rgba8, int32_t width, int32_t height, int32_t pitch_bytes);
+
 #ifdef __cplusplus
 }
 #endif

@@ -29,7 +29,7 @@ __all__ = ["SocError", "lib", "img", "Globals", "Camera", "AutoExposure", "globa
            "bloom_downsample", "bloom_upsample", "bloom_chain", "ssao_prepare_noise", "ssao_generation",
            "ssao_blur", "cloud_rendering", "composition", "generate_luminance_histogram",
            "resolve_luminance_histogram", "temporal_antialiasing", "copy_image", "tone_mapping", "upload_globals",
-           "Renderer", "FMT_RGBA16F", "FMT_D32F", "FMT_R8_UNORM", "FMT_RGBA8_UNORM", "FMT_RGBA8_SRGB",
+           "Renderer", "read_image", "write_png", "FMT_RGBA16F", "FMT_D32F", "FMT_R8_UNORM", "FMT_RGBA8_UNORM", "FMT_RGBA8_SRGB",
            "FMT_RGBA32F", "PHASE_PRE_EXPOSURE", "PHASE_POST_EXPOSURE", "PHASE_ALL"]
 
 
@@ -178,6 +178,22 @@ def bloom_weighted_stage(g, emissive, mips, output, stage=0, stream=None):
     arr = (SocImg * len(mips))(*[img(m) for m in mips])
     _check(lib().soc_bloom_weighted_stage(_gp(g), img(emissive), arr, len(mips), img(output), int(stage),
                                           _stream(stream)), "bloom_weighted_stage")
+
+
+def read_image(t, stream=None) -> np.ndarray:
+    """Device image (torch tensor view) -> host numpy array of the same shape (soc_read_image), synchronised."""
+    host = np.empty(tuple(t.shape), dtype=t.cpu().numpy().dtype if t.numel() == 0 else
+                    {torch.uint8: np.uint8, torch.float16: np.float16, torch.float32: np.float32}[t.dtype])
+    _check(lib().soc_read_image(img(t), host.ctypes.data, int(host.strides[0]), _stream(stream)), "soc_read_image")
+    torch.cuda.synchronize()
+    return host
+
+
+def write_png(path: str, rgba8: np.ndarray) -> None:
+    """(H, W, 4) uint8 host image -> PNG (soc_write_png)."""
+    a = np.ascontiguousarray(rgba8, np.uint8)
+    _check(lib().soc_write_png(path.encode(), a.ctypes.data, int(a.shape[1]), int(a.shape[0]), int(a.strides[0])),
+           "soc_write_png")
 
 
 def ssao_prepare_noise(normal, target, table, stream=None):
@@ -335,6 +351,33 @@ class Renderer:
         self.handle = h
         if frame.get("ssao_noise_table") is not None:
             ssao_prepare_noise(frame["normal"], frame["ssao"], frame["ssao_noise_table"], stream)
+
+    def set_raster_scene(self, mesh, d_materials, material_count: int, visibility, workspace, shadow: bool = True):
+        """Raster head (DepthPrepass / SunShadowDraw / GBufferGeneration) from a raster.MeshBuffers of device
+        arrays; None clears it (the G-buffer images are inputs again)."""
+        if mesh is None:
+            _check(lib().soc_renderer_set_raster_scene(self.handle, None), "soc_renderer_set_raster_scene")
+            self._scene = None
+            return
+        sc = _abi.RasterScene()
+        sc.mesh = mesh.struct
+        sc.materials = _ptr(d_materials)
+        sc.material_count = int(material_count)
+        sc.shadow = int(bool(shadow))
+        sc.visibility = _ptr(visibility)
+        sc.workspace = _ptr(workspace)
+        self._scene = (mesh, d_materials, visibility, workspace)   # keep the arrays alive
+        _check(lib().soc_renderer_set_raster_scene(self.handle, C.byref(sc)), "soc_renderer_set_raster_scene")
+
+    def metrics_json(self, frame: int = 0) -> str:
+        """The last frame's GPU-metric record (renderer.cpp:769-806) as a JSON string (needs timing and a
+        completed stream)."""
+        n = lib().soc_renderer_metrics_json(self.handle, int(frame), None, 0)
+        if n < 0:
+            _check(int(n), "soc_renderer_metrics_json")
+        buf = C.create_string_buffer(int(n) + 1)
+        lib().soc_renderer_metrics_json(self.handle, int(frame), buf, len(buf))
+        return buf.value.decode()
 
     def execute(self, g: Globals, phase: int = PHASE_ALL, stream=None) -> None:
         _check(lib().soc_renderer_execute(self.handle, _gp(g), phase, _stream(stream)), "soc_renderer_execute")

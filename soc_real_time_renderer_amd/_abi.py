@@ -127,12 +127,18 @@ class Material(C.Structure):
                 ("pad", C.c_int32 * 2)]
 
 
+class RasterScene(C.Structure):
+    _fields_ = [("mesh", Mesh), ("materials", C.c_void_p), ("material_count", C.c_int32), ("shadow", C.c_int32),
+                ("visibility", C.c_void_p), ("workspace", C.c_void_p)]
+
+
 CULL_NONE, CULL_FRONT, CULL_BACK = 0, 1, 2
 MATERIAL_ZERO_VELOCITY = 1
 
 STRUCTS = {"soc_img": SocImg, "soc_globals": Globals, "soc_sun_info": SunInfo, "soc_point_light": PointLight,
            "soc_spot_light": SpotLight, "soc_auto_exposure": AutoExposure, "soc_camera": Camera,
-           "soc_frame_images": FrameImages, "soc_mesh": Mesh, "soc_material": Material}
+           "soc_frame_images": FrameImages, "soc_mesh": Mesh, "soc_material": Material,
+           "soc_raster_scene": RasterScene}
 
 _I = C.c_int
 _P = C.c_void_p
@@ -186,6 +192,10 @@ FUNCTIONS = {
     "soc_renderer_reset_timing": (_I, [_P]),
     "soc_renderer_pass_stats": (_I, [_P, C.c_int32, C.POINTER(C.c_float), C.POINTER(C.c_int32)]),
     "soc_raster_workspace_size": (C.c_size_t, [C.c_int32, C.c_int32]),
+    "soc_renderer_set_raster_scene": (_I, [_P, C.POINTER(RasterScene)]),
+    "soc_renderer_metrics_json": (C.c_int64, [_P, C.c_uint64, C.c_char_p, C.c_size_t]),
+    "soc_read_image": (_I, [_IMG, _P, C.c_int32, _P]),
+    "soc_write_png": (_I, [C.c_char_p, _P, C.c_int32, C.c_int32, C.c_int32]),
     "soc_raster_visibility": (_I, [C.POINTER(Mesh), C.POINTER(C.c_float), C.c_int32, _P, C.c_int32, C.c_int32,
                                    C.c_int32, _P, _P]),
     "soc_raster_depth": (_I, [C.POINTER(Mesh), C.POINTER(C.c_float), C.c_int32, C.c_float, C.c_float, _IMG, _P, _P]),

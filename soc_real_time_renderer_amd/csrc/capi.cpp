@@ -169,6 +169,8 @@ const FieldInfo kFields[] = {
     F(soc_mesh, vertex_count), F(soc_mesh, triangle_count), F(soc_mesh, model_matrix), F(soc_mesh, normal_matrix),
     F(soc_material, albedo), F(soc_material, emissive), F(soc_material, albedo_factor), F(soc_material, emissive_factor),
     F(soc_material, flags), F(soc_material, has_emissive), F(soc_material, pad),
+    F(soc_raster_scene, mesh), F(soc_raster_scene, materials), F(soc_raster_scene, material_count),
+    F(soc_raster_scene, shadow), F(soc_raster_scene, visibility), F(soc_raster_scene, workspace),
 };
 #undef F
 }  // namespace
@@ -188,6 +190,7 @@ extern "C" size_t soc_abi_sizeof(const char* t) {
     if (s == "soc_frame_images") return sizeof(soc_frame_images);
     if (s == "soc_mesh") return sizeof(soc_mesh);
     if (s == "soc_material") return sizeof(soc_material);
+    if (s == "soc_raster_scene") return sizeof(soc_raster_scene);
     return 0;
 }
 
@@ -468,11 +471,14 @@ struct soc_renderer {
         std::function<int(const soc_globals*, hipStream_t)> run;
         int lane = 0;        // 1 = the sky lane: runs on the renderer's side stream, concurrently with lane 0
         bool join = false;   // lane-0 pass that consumes the sky lane's output (waits on its join event)
+        bool head = false;   // raster head: runs on the caller's stream before the sky lane forks
         bool timed = false;
         std::vector<hipEvent_t> ev0, ev1;  // ring of SOC_RENDERER_TIMING_RING frames
         int next = 0, count = 0, last = -1;
     };
     soc_frame_images img{};
+    soc_raster_scene scene{};
+    bool has_scene = false;
     std::vector<Pass> passes;
     uint32_t flags = 0;
     int hist = 0;               // history slot read as "previous" this frame
@@ -514,6 +520,30 @@ int ensure_hist_scratch(soc_renderer* r) {
     if (hipMemset(r->hist_scratch, 0, SOC_HISTOGRAM_SCRATCH_WORDS * sizeof(uint32_t)) != hipSuccess)
         return set_error(SOC_E_HIP, "soc_renderer_execute: histogram scratch clear failed");
     return SOC_OK;
+}
+
+// Raster head of the graph (renderer.cpp:965-1021): depth prepass, sun shadow, G-buffer.
+void build_raster_passes(soc_renderer* r) {
+    if (!r->has_scene) return;
+    auto add = [r](std::string name, std::string group, PassFn fn) {
+        add_pass(r, std::move(name), std::move(group), SOC_PHASE_PRE_EXPOSURE, std::move(fn));
+        r->passes.back().head = true;
+    };
+    add("DepthPrepass", "Depth Prepass", [r](const soc_globals* g, hipStream_t s) {
+        const soc_img& d = r->img.depth;
+        return soc_raster_visibility(&r->scene.mesh, g->camera_projection_view_matrix, SOC_CULL_FRONT,
+                                     r->scene.visibility, d.width, d.height, 1, r->scene.workspace, (soc_stream)s);
+    });
+    if (r->scene.shadow)
+        add("SunShadowDraw", "Shadows", [r](const soc_globals* g, hipStream_t s) {
+            return soc_raster_depth(&r->scene.mesh, g->sun_info.projection_view_matrix, SOC_CULL_BACK, 1.25f, 1.75f,
+                                    r->img.shadow, r->scene.workspace, (soc_stream)s);
+        });
+    add("GBufferGeneration", "Rendering G-Buffer", [r](const soc_globals* g, hipStream_t s) {
+        const soc_frame_images& I = r->img;
+        return soc_gbuffer_resolve(g, &r->scene.mesh, r->scene.materials, r->scene.material_count, r->scene.visibility,
+                                   I.depth, I.albedo, I.emissive, I.normal, I.velocity, (soc_stream)s);
+    });
 }
 
 // Bloom passes of the graph (renderer.cpp:1024-1062); build_passes_tail adds the rest.
@@ -654,6 +684,7 @@ extern "C" soc_renderer* soc_renderer_create(const soc_frame_images* images, uin
     r->img = *images;
     r->flags = flags;
     r->async = !(flags & SOC_RENDERER_SERIAL);
+    build_raster_passes(r);
     build_passes(r);
     build_passes_tail(r);
     if ((flags & SOC_RENDERER_TIMING) && soc_renderer_set_pass_timing(r, -1, 1) != SOC_OK) {
@@ -740,6 +771,12 @@ extern "C" int soc_renderer_execute(soc_renderer* r, const soc_globals* g, int32
         int rc = upload_lights(r, g, s);
         if (rc) return rc;
     }
+    if (phase & SOC_PHASE_PRE_EXPOSURE)
+        for (auto& p : r->passes) {
+            if (!p.head) continue;
+            int rc = run_pass(p, g, s);
+            if (rc) return rc;
+        }
     // lane-1 passes run on the side stream, ordered after everything already on `s` (fork) and
     // before the first lane-0 pass marked `join`; every pass still reads and writes the same images
     const bool lanes = r->async && (phase & SOC_PHASE_PRE_EXPOSURE);
@@ -758,7 +795,7 @@ extern "C" int soc_renderer_execute(soc_renderer* r, const soc_globals* g, int32
     }
     bool joined = !lanes;
     for (auto& p : r->passes) {
-        if (!(p.phase & phase)) continue;
+        if (!(p.phase & phase) || p.head) continue;
         if (lanes && p.lane == 1) continue;
         if (p.join && !joined) {
             if (hipStreamWaitEvent(s, r->join_ev, 0) != hipSuccess)
@@ -771,6 +808,29 @@ extern "C" int soc_renderer_execute(soc_renderer* r, const soc_globals* g, int32
     if (!joined && hipStreamWaitEvent(s, r->join_ev, 0) != hipSuccess)   // no consumer this phase: still join
         return set_error(SOC_E_HIP, "soc_renderer_execute: sky lane join failed");
     if (phase & SOC_PHASE_POST_EXPOSURE) r->hist = 1 - r->hist;   // ping-pong the TAA history
+    return SOC_OK;
+}
+
+extern "C" int soc_renderer_set_raster_scene(soc_renderer* r, const soc_raster_scene* scene) {
+    if (!r) return set_error(SOC_E_INVALID_ARG, "soc_renderer_set_raster_scene: null renderer");
+    if (scene) {
+        if (!scene->materials || scene->material_count <= 0 || !scene->visibility || !scene->workspace ||
+            !scene->mesh.positions || !scene->mesh.normals || !scene->mesh.uvs || !scene->mesh.indices)
+            return set_error(SOC_E_INVALID_ARG, "soc_renderer_set_raster_scene: incomplete scene");
+        if (scene->shadow && !r->img.shadow.data)
+            return set_error(SOC_E_INVALID_ARG, "soc_renderer_set_raster_scene: shadow pass needs images.shadow");
+    }
+    for (auto& p : r->passes) {
+        for (auto e : p.ev0) (void)hipEventDestroy(e);
+        for (auto e : p.ev1) (void)hipEventDestroy(e);
+    }
+    r->passes.clear();
+    r->has_scene = scene != nullptr;
+    if (scene) r->scene = *scene;
+    build_raster_passes(r);
+    build_passes(r);
+    build_passes_tail(r);
+    if (r->flags & SOC_RENDERER_TIMING) return soc_renderer_set_pass_timing(r, -1, 1);
     return SOC_OK;
 }
 
@@ -806,6 +866,44 @@ extern "C" float soc_renderer_pass_ms(soc_renderer* r, int32_t i) {
     float ms = -1.0f;
     if (hipEventElapsedTime(&ms, p.ev0[p.last], p.ev1[p.last]) != hipSuccess) return -1.0f;
     return ms;
+}
+
+// The "GPU Metric" record of the most recent frame (renderer.cpp:769-806): every timed pass's ms, summed
+// into the reference's 12 groups (renderer.cpp:577-588; absent groups are 0), and their total.
+extern "C" int64_t soc_renderer_metrics_json(soc_renderer* r, uint64_t frame, char* buf, size_t cap) {
+    if (!r) return set_error(SOC_E_INVALID_ARG, "soc_renderer_metrics_json: null renderer");
+    static const char* kGroups[12] = {"Depth Prepass", "Composition", "Tone Mapping", "Bloom", "Depth Of Field",
+                                      "Shadows", "Rendering G-Buffer", "Screen Space Reflections", "Ambient Occlusion",
+                                      "Auto Exposure", "Sky Rendering", "Temporal Anti-Aliasing"};
+    double group_ms[12] = {0};
+    double total = 0.0;
+    std::string passes;
+    for (int i = 0; i < (int)r->passes.size(); ++i) {
+        const float ms = soc_renderer_pass_ms(r, i);
+        if (ms < 0.0f) continue;
+        total += ms;
+        char item[160];
+        std::snprintf(item, sizeof item, "%s\"%s\": %.6f", passes.empty() ? "" : ", ", r->passes[i].name.c_str(), ms);
+        passes += item;
+        for (int k = 0; k < 12; ++k)
+            if (r->passes[i].group == kGroups[k]) group_ms[k] += ms;
+    }
+    std::string out = "{\"frame\": " + std::to_string(frame) + ", \"total_gpu_ms\": ";
+    char num[64];
+    std::snprintf(num, sizeof num, "%.6f", total);
+    out += num;
+    out += ", \"groups\": {";
+    for (int k = 0; k < 12; ++k) {
+        std::snprintf(num, sizeof num, "%s\"%s\": %.6f", k ? ", " : "", kGroups[k], group_ms[k]);
+        out += num;
+    }
+    out += "}, \"passes\": {" + passes + "}}";
+    if (buf && cap) {
+        const size_t n = std::min(cap - 1, out.size());
+        std::memcpy(buf, out.data(), n);
+        buf[n] = 0;
+    }
+    return (int64_t)out.size();
 }
 
 extern "C" int soc_renderer_set_pass_timing(soc_renderer* r, int32_t index, int32_t enable) {

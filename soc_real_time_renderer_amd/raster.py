@@ -131,3 +131,19 @@ def visibility_triangles(vis) -> np.ndarray:
     """Triangle id per pixel (-1 = empty) of a host visibility buffer (uint64/int64 array)."""
     low = (np.asarray(vis).view(np.uint64) & np.uint64(0xFFFFFFFF)).astype(np.int64)
     return np.where(low == 0xFFFFFFFF, -1, 0xFFFFFFFE - low)
+
+
+def scene_setup(g, scene_id: int, tex_size: int = 512, device="cuda") -> dict:
+    """Device mesh, textures and material array of a synthetic scene (scene_synth.c): the Sponza-proxy
+    (sRGB tiled textures, emissive lamps) or the terrain (UNORM albedo, velocity 0 as draw_terrain.inl:221)."""
+    from . import scene as _scene
+    m = _scene.mesh(g, scene_id)
+    mesh = MeshBuffers.from_numpy(m["positions"], m["normals"], m["uvs"], m["indices"], m["materials"], device=device)
+    tex, em = _scene.material_textures(g, tex_size, scene_id)
+    terrain = scene_id == _scene.TERRAIN
+    dtex = [torch.from_numpy(tex[i]).to(device) for i in range(len(tex))]
+    mats = [material(albedo=dtex[i], emissive_factor=tuple(float(v) for v in em[i]) + (1.0,),
+                     has_emissive=bool(em[i].any()), flags=MATERIAL_ZERO_VELOCITY if terrain else 0, srgb=not terrain)
+            for i in range(len(tex))]
+    return {"mesh": mesh, "textures": dtex, "materials": materials_device(mats, device), "material_count": len(mats),
+            "host_mesh": m, "host_textures": tex, "emissive": em, "workspace": mesh.workspace(device)}

@@ -39,7 +39,8 @@ def test_ctypes_table_covers_header():
 
 
 @pytest.mark.parametrize("name", ["soc_img", "soc_globals", "soc_sun_info", "soc_point_light", "soc_spot_light",
-                                  "soc_auto_exposure", "soc_camera", "soc_frame_images", "soc_mesh", "soc_material"])
+                                  "soc_auto_exposure", "soc_camera", "soc_frame_images", "soc_mesh", "soc_material",
+                                  "soc_raster_scene"])
 def test_struct_sizes(soc, name):
     from soc_real_time_renderer_amd import _abi
     assert soc.lib().soc_abi_sizeof(name.encode()) == C.sizeof(_abi.STRUCTS[name])

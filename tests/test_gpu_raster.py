@@ -140,3 +140,40 @@ def test_gbuffer_resolve(soc, oracle, scene_id, camera, W, H):
     assert np.array_equal(host(out["depth"]), ref["depth"])
     for k in ("albedo", "emissive", "normal", "velocity"):
         assert f16_close(host(out[k]), ref[k]).all(), k
+
+
+@pytest.mark.parametrize("scene_id,camera", [(scene.SPONZA_PROXY, SPONZA_CAMERA), (scene.TERRAIN, TERRAIN_CAMERA)])
+def test_render_graph_raster_head(soc, scene_id, camera):
+    """DepthPrepass / SunShadowDraw / GBufferGeneration inside the render graph: 3 frames equal the same
+    frames fed with G-buffer + shadow images rasterised by the standalone calls."""
+    W, H = 640, 360
+    g = globals_for(W, H, camera=camera, elapsed=10.0)
+    sc = raster.scene_setup(g, scene_id, tex_size=128)
+    outs = []
+    for in_graph in (True, False):
+        fr = soc.alloc_frame(W, H, DEV, bloom_output=True)
+        fr["noise"].copy_(torch.from_numpy(scene.noise_texture()))
+        fr["shadow"] = torch.zeros((1024, 1024), dtype=torch.float32, device=DEV)
+        vis = torch.zeros((H, W), dtype=torch.int64, device=DEV)
+        r = soc.Renderer(fr)
+        if in_graph:
+            r.set_raster_scene(sc["mesh"], sc["materials"], sc["material_count"], vis, sc["workspace"], shadow=True)
+            names = r.pass_names()
+            assert names[:3] == ["DepthPrepass", "SunShadowDraw", "GBufferGeneration"]
+            assert r.pass_groups()[:3] == ["Depth Prepass", "Shadows", "Rendering G-Buffer"]
+        for _ in range(3):
+            if not in_graph:
+                vp = np.ctypeslib.as_array(g.camera_projection_view_matrix)
+                raster.raster_visibility(sc["mesh"], vp, raster.CULL_FRONT, vis, sc["workspace"])
+                raster.raster_depth(sc["mesh"], np.ctypeslib.as_array(g.sun_info.projection_view_matrix),
+                                    raster.CULL_BACK, fr["shadow"], sc["workspace"], raster.SHADOW_BIAS_CONSTANT,
+                                    raster.SHADOW_BIAS_SLOPE)
+                raster.gbuffer_resolve(g, sc["mesh"], sc["materials"], sc["material_count"], vis, fr["depth"],
+                                       fr["albedo"], fr["emissive"], fr["normal"], fr["velocity"])
+            r.execute(g)
+        torch.cuda.synchronize()
+        outs.append({k: fr[k].clone() for k in ("depth", "albedo", "shadow", "color", "output", "auto_exposure")})
+        r.close()
+    for k in outs[0]:
+        assert torch.equal(outs[0][k], outs[1][k]), k
+    assert (outs[0]["depth"] < 1.0).float().mean() > 0.3
