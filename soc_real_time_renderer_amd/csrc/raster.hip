@@ -7,8 +7,10 @@
 // gfx950 has no raster units reachable from HIP, so the raster is a compute visibility buffer:
 //   1. raster_setup     one lane per vertex: object -> world -> clip -> screen (x, y, z_ndc, 1/w)
 //   2. raster_small     one lane per triangle: cull, bounding box; a box of <= SMALL_PIXELS pixels is
-//                       scanned by the lane itself, larger ones are split into CHUNK-pixel work items
-//   3. raster_big       one wave per work item: 64 lanes cover the chunk's pixels
+//                       scanned by the lane itself, larger ones are split into 32x32-pixel tiles
+//   3. raster_big       one wave per (triangle, tile) work item: tiles that an edge function excludes at
+//                       all four corners (with a rounding margin) are skipped, else 64 lanes cover the
+//                       tile's 1024 pixels
 //   every covered pixel does ONE 64-bit atomicMin of (depth bits << 32 | 0xFFFFFFFE - triangle): with
 //   z >= 0 the float bits order like the depths, and ties keep the LATER triangle, which is exactly the
 //   serial LESS_OR_EQUAL result in draw order. The depth-only variant (shadow map) does a 32-bit
@@ -25,7 +27,7 @@ namespace soc {
 namespace {
 
 constexpr int SMALL_PIXELS = 64;    // bounding boxes up to this many pixels are scanned by one lane
-constexpr int CHUNK = 1024;         // pixels per large-triangle work item (16 per lane of a wave)
+constexpr int TILE = 32;            // large-triangle work item: a 32x32 tile of its bounding box
 constexpr uint32_t KEY_EMPTY = 0xFFFFFFFFu;
 
 struct RasterParams {
@@ -35,6 +37,8 @@ struct RasterParams {
     int depth_only;
     float bias_constant, bias_slope;
     uint32_t item_capacity;
+    int precheck;       // load the target before the atomic (skip it when already nearer)
+    int small_pixels;   // boxes up to this many pixels are scanned by one lane
 };
 
 // workspace: [float4 clip-space screen vertices[V]] [uint32 counter, pad..] [uint2 items[capacity]]
@@ -199,15 +203,17 @@ __device__ __forceinline__ void shade(const TriSetup& t, int id, int x, int y, c
                                       size_t pitch) {
     float e0, e1, e2, z;
     if (!cover(t, x, y, e0, e1, e2, z)) return;
+    // a plain load first: values only decrease, so a stale (larger) value never skips a needed atomic
     if (p.depth_only) {
 #pragma clang fp contract(off)
         const float zb = fminf(fmaxf(z + t.bias, 0.0f), 1.0f);
         uint32_t* d = reinterpret_cast<uint32_t*>(static_cast<char*>(target) + (size_t)y * pitch) + x;
-        atomicMin(d, __float_as_uint(zb));
+        const uint32_t key = __float_as_uint(zb);
+        if (!p.precheck || key < __builtin_nontemporal_load(d)) atomicMin(d, key);
     } else {
         const unsigned long long key = ((unsigned long long)__float_as_uint(z) << 32) | (unsigned long long)(0xFFFFFFFEu - (uint32_t)id);
         unsigned long long* d = reinterpret_cast<unsigned long long*>(static_cast<char*>(target) + (size_t)y * pitch) + x;
-        atomicMin(d, key);
+        if (!p.precheck || key < __builtin_nontemporal_load(d)) atomicMin(d, key);
     }
 }
 
@@ -237,8 +243,8 @@ __global__ __launch_bounds__(256) void raster_small(const uint32_t* __restrict__
     if (!t.live) return;
     const int bw = t.px1 - t.px0 + 1, bh = t.py1 - t.py0 + 1;
     const long long n = (long long)bw * bh;
-    if (n > SMALL_PIXELS) {
-        const uint32_t chunks = (uint32_t)((n + CHUNK - 1) / CHUNK);
+    if (n > p.small_pixels) {
+        const uint32_t chunks = (uint32_t)(((bw + TILE - 1) / TILE) * ((bh + TILE - 1) / TILE));
         const uint32_t base = atomicAdd(ws.counter, chunks);
         if (base + chunks <= ws.capacity) {
             for (uint32_t k = 0; k < chunks; ++k) ws.items[base + k] = uint2{(uint32_t)id, k};
@@ -252,7 +258,15 @@ __global__ __launch_bounds__(256) void raster_small(const uint32_t* __restrict__
         for (int x = t.px0; x <= t.px1; ++x) shade(t, id, x, y, p, target, pitch);
 }
 
-// One wave per work item (triangle, chunk): its CHUNK pixels of the bounding box, 64 lanes wide.
+// Upper bound of the edge function over the pixel centres of [x0, x1] x [y0, y1] (a corner), minus a
+// rounding margin: < 0 means no centre of the tile can pass this edge.
+__device__ __forceinline__ float edge_max(f3 r, float x0, float x1, float y0, float y1) {
+    const float m = fmaxf(fmaxf(edge(r, x0, y0), edge(r, x1, y0)), fmaxf(edge(r, x0, y1), edge(r, x1, y1)));
+    const float slack = 1e-4f * (fabsf(r.x) * fmaxf(fabsf(x0), fabsf(x1)) + fabsf(r.y) * fmaxf(fabsf(y0), fabsf(y1)) + fabsf(r.z));
+    return m + slack;
+}
+
+// One wave per work item (triangle, 32x32 tile of its box): 64 lanes, 2 rows per step.
 __global__ __launch_bounds__(256) void raster_big(const uint32_t* __restrict__ idx, Workspace ws, RasterParams p,
                                                   void* target, size_t pitch) {
     const uint32_t count = min(*ws.counter, ws.capacity);
@@ -261,15 +275,17 @@ __global__ __launch_bounds__(256) void raster_big(const uint32_t* __restrict__ i
         const uint2 item = ws.items[it];
         if (item.x == 0xFFFFFFFFu) continue;
         const TriSetup t = load_tri(ws, idx, (int)item.x, p);
-        const int bw = t.px1 - t.px0 + 1, bh = t.py1 - t.py0 + 1;
-        const long long n = (long long)bw * bh;
-        const long long k0 = (long long)item.y * CHUNK;
-        for (int j = lane; j < CHUNK; j += 64) {
-            const long long k = k0 + j;
-            if (k >= n) break;
-            const int yy = (int)(k / bw), xx = (int)(k - (long long)yy * bw);
-            shade(t, (int)item.x, t.px0 + xx, t.py0 + yy, p, target, pitch);
-        }
+        const int tiles_x = (t.px1 - t.px0 + TILE) / TILE;
+        const int ty = (int)item.y / tiles_x, tx = (int)item.y - ty * tiles_x;
+        const int x0 = t.px0 + tx * TILE, y0 = t.py0 + ty * TILE;
+        const int x1 = min(x0 + TILE - 1, t.px1), y1 = min(y0 + TILE - 1, t.py1);
+        const float fx0 = (float)x0 + 0.5f, fx1 = (float)x1 + 0.5f, fy0 = (float)y0 + 0.5f, fy1 = (float)y1 + 0.5f;
+        if (edge_max(t.r0, fx0, fx1, fy0, fy1) < 0.0f || edge_max(t.r1, fx0, fx1, fy0, fy1) < 0.0f ||
+            edge_max(t.r2, fx0, fx1, fy0, fy1) < 0.0f)
+            continue;
+        const int x = x0 + (lane & 31);
+        if (x > x1) continue;
+        for (int y = y0 + (lane >> 5); y <= y1; y += 2) shade(t, (int)item.x, x, y, p, target, pitch);
     }
 }
 
@@ -286,11 +302,12 @@ __device__ __forceinline__ float srgb_to_linear(float c) {
     return c <= 0.04045f ? c / 12.92f : powf((c + 0.055f) / 1.055f, 2.4f);
 }
 
-__device__ __forceinline__ f4 texel_rgba8(const DImg& im, int x, int y, bool srgb) {
+// lut: srgb_to_linear(unorm8(i)) for i in 0..255 (LDS, filled per workgroup)
+__device__ __forceinline__ f4 texel_rgba8(const DImg& im, int x, int y, bool srgb, const float* lut) {
     const uint32_t u = row_ptr<uint32_t>(im, y)[x];
-    const float r = unorm8(u & 255u), g = unorm8((u >> 8) & 255u), b = unorm8((u >> 16) & 255u), a = unorm8(u >> 24);
-    if (!srgb) return f4{r, g, b, a};
-    return f4{srgb_to_linear(r), srgb_to_linear(g), srgb_to_linear(b), a};
+    const float a = unorm8(u >> 24);
+    if (!srgb) return f4{unorm8(u & 255u), unorm8((u >> 8) & 255u), unorm8((u >> 16) & 255u), a};
+    return f4{lut[u & 255u], lut[(u >> 8) & 255u], lut[(u >> 16) & 255u], a};
 }
 
 // REPEAT addressing for any extent (the sampling contract's 8-bit sub-texel weights).
@@ -310,13 +327,13 @@ __device__ __forceinline__ Axis axis_repeat_any(float u, int n) {
     return a;
 }
 
-__device__ __forceinline__ f4 sample_texture(const soc_img& tex, float u, float v) {
+__device__ __forceinline__ f4 sample_texture(const soc_img& tex, float u, float v, const float* lut) {
     if (!tex.data) return f4{1.0f, 1.0f, 1.0f, 1.0f};
     const DImg im{static_cast<char*>(tex.data), tex.width, tex.height, tex.pitch_bytes};
     const bool srgb = tex.format == SOC_FMT_RGBA8_SRGB;
     const Axis ax = axis_repeat_any(u, tex.width), ay = axis_repeat_any(v, tex.height);
-    const f4 a = texel_rgba8(im, ax.i0, ay.i0, srgb), b = texel_rgba8(im, ax.i1, ay.i0, srgb);
-    const f4 c = texel_rgba8(im, ax.i0, ay.i1, srgb), d = texel_rgba8(im, ax.i1, ay.i1, srgb);
+    const f4 a = texel_rgba8(im, ax.i0, ay.i0, srgb, lut), b = texel_rgba8(im, ax.i1, ay.i0, srgb, lut);
+    const f4 c = texel_rgba8(im, ax.i0, ay.i1, srgb, lut), d = texel_rgba8(im, ax.i1, ay.i1, srgb, lut);
     return bilerp4(a, b, c, d, ax.w, ay.w);
 }
 
@@ -337,6 +354,9 @@ __global__ __launch_bounds__(256) void gbuffer_resolve(soc_mesh mesh, const soc_
                                                        DImg albedo, DImg emissive, DImg normal, DImg velocity,
                                                        ResolveParams p) {
 #pragma clang fp contract(off)
+    __shared__ float lut[256];
+    lut[threadIdx.y * 64 + threadIdx.x] = srgb_to_linear(unorm8(threadIdx.y * 64 + threadIdx.x));
+    __syncthreads();
     const int x = blockIdx.x * 64 + threadIdx.x, y = blockIdx.y * 4 + threadIdx.y;
     if (x >= p.width || y >= p.height) return;
     const unsigned long long key = vis[(size_t)y * p.width + x];
@@ -378,10 +398,10 @@ __global__ __launch_bounds__(256) void gbuffer_resolve(soc_mesh mesh, const soc_
     const soc_material& m = mats[mi];
     f3 em = f3{0.0f, 0.0f, 0.0f};
     if (m.has_emissive) {
-        const f4 e = sample_texture(m.emissive, u, v);
+        const f4 e = sample_texture(m.emissive, u, v, lut);
         em = f3{e.x * m.emissive_factor[0], e.y * m.emissive_factor[1], e.z * m.emissive_factor[2]};
     }
-    const f4 al = sample_texture(m.albedo, u, v);
+    const f4 al = sample_texture(m.albedo, u, v, lut);
     f4 vel = f4{0.0f, 0.0f, 0.0f, 0.0f};
     if (!(m.flags & SOC_MATERIAL_ZERO_VELOCITY)) {
         const float* ps = mesh.positions;
@@ -427,6 +447,8 @@ RasterParams make_raster_params(const soc_mesh* mesh, const float* vp, int W, in
     p.triangle_count = mesh->triangle_count;
     p.cull = cull;
     p.item_capacity = (uint32_t)(4 * (size_t)mesh->triangle_count + (1u << 20));
+    p.precheck = tuning_knob("SOC_RASTER_PRECHECK", 0);
+    p.small_pixels = tuning_knob("SOC_RASTER_SMALL", SMALL_PIXELS);
     return p;
 }
 
