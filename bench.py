@@ -220,7 +220,7 @@ def main():
     ns_bytes = algo[comp] + algo["SSAOGeneration"]
     ns_us = (comp_ms + ssao_ms) * 1e3
     pass_gbs = {n: round(algo[n] / (ms * 1e-3) / 1e9, 1) for n, _, ms, _ in stats if ms > 0 and n in algo}
-    traffic, traffic_src = pmc_traffic("composition_pair<true>" if comp != "Composition" else "composition_pair<false>", W, H)
+    traffic, traffic_src = pmc_traffic("composition_pair<true, false, 0>" if comp != "Composition" else "composition_pair<false, false, 3>", W, H)
 
     if world > 1:
         dist.barrier()

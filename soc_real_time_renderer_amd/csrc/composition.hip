@@ -77,6 +77,7 @@ __device__ f3 spot_light(const soc_spot_light& L, f3 frag_color, f3 normal, f3 p
 // ws = inv_view * (vs / vs.w), sp = sun_pv * ws, and pc = sp.xyz / sp.w, so the vs.w division cancels
 // and sun_clip = sun_pv * inv_view * inv_proj (host fp32) gives pc directly (one rcp; within the
 // RGBA16F tolerance). The world position itself is only formed for the light loops.
+template <bool LIGHTS = true>
 __device__ __forceinline__ f4 shade(const CompParams& p, float u, float v, float d, f3 albedo, f3 emissive, f3 n,
                                     float ssao, const DImg& shadow) {
     const f4 ndc = f4{u * 2.0f - 1.0f, v * 2.0f - 1.0f, d, 1.0f};
@@ -95,7 +96,7 @@ __device__ __forceinline__ f4 shade(const CompParams& p, float u, float v, float
     const float occl = fast_pow(ssao, p.ao_strength);
     const float dd = fmaxf(0.0f, dot3(n, -mk3(p.sun_dir[0], p.sun_dir[1], p.sun_dir[2]))) * sun_shadow;
     f3 direct = f3{dd, dd, dd};
-    if (p.npl | p.nsl) {
+    if (LIGHTS && (p.npl | p.nsl)) {
         // get_world_position_from_depth, :114-122
         f4 vs = mul(p.inv_proj, ndc);
         const float rw = __builtin_amdgcn_rcpf(vs.w);
@@ -123,7 +124,9 @@ constexpr int BX = 64, BY = 4;
 // Measured at 4K: 94 us + a 4 us fold against 77 + 33 us for the two passes. The render graph keeps
 // the two passes by default (SOC_RENDERER_FUSED_HISTOGRAM opts in): the ~12 us (1.5 % of the frame)
 // costs the composition stream its HBM rate (4.4 -> 3.6 TB/s), the north-star measure.
-template <bool HIST>
+// LIGHTS = false: no point / spot lights this frame (the reference default): the light loops are not
+// compiled in, which keeps the kernel at a fraction of the registers (more waves, more loads in flight).
+template <bool HIST, bool LIGHTS, int NT = 0>
 __global__ __launch_bounds__(256) void composition_pair(DImg target, DImg albedo, DImg emissive, DImg normal, DImg depth,
                                                         DImg ssao, DImg shadow, DImg clouds, CompParams p) {
     // a wave covers 16x8 pixels (8 lanes x 2 pixels per row, 8 rows): every row segment is one
@@ -144,10 +147,21 @@ __global__ __launch_bounds__(256) void composition_pair(DImg target, DImg albedo
     uint2 outp[2] = {uint2{0u, 0u}, uint2{0u, 0u}};
     if (inside) {
         const float v = centre_uv(y, target.h);
-        const float2 d2 = row_ptr<float2>(depth, y)[x >> 1];
-        const uint4 a4 = row_ptr<uint4>(albedo, y)[x >> 1];
-        const uint4 e4 = row_ptr<uint4>(emissive, y)[x >> 1];
-        const uint4 n4 = row_ptr<uint4>(normal, y)[x >> 1];
+        float2 d2;
+        uint4 a4, e4, n4;
+        if (NT & 1) {   // once-read streams: non-temporal (keep L2 for the shadow-map / AO gathers)
+            typedef float v2f __attribute__((ext_vector_type(2)));
+            typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+            d2 = __builtin_bit_cast(float2, __builtin_nontemporal_load(reinterpret_cast<const v2f*>(row_ptr<float2>(depth, y)) + (x >> 1)));
+            a4 = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const v4u*>(row_ptr<uint4>(albedo, y)) + (x >> 1)));
+            e4 = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const v4u*>(row_ptr<uint4>(emissive, y)) + (x >> 1)));
+            n4 = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const v4u*>(row_ptr<uint4>(normal, y)) + (x >> 1)));
+        } else {
+            d2 = row_ptr<float2>(depth, y)[x >> 1];
+            a4 = row_ptr<uint4>(albedo, y)[x >> 1];
+            e4 = row_ptr<uint4>(emissive, y)[x >> 1];
+            n4 = row_ptr<uint4>(normal, y)[x >> 1];
+        }
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
             const float u = centre_uv(x + k, target.w);
@@ -161,11 +175,14 @@ __global__ __launch_bounds__(256) void composition_pair(DImg target, DImg albedo
                 c = f4{cl.x, cl.y, cl.z, 1.0f};
             } else {
                 const float ao = (SOC_COMP_PROFILE & 2) ? u : sample_r8(ssao, u, v);
-                c = shade(p, u, v, d, f3{al.x, al.y, al.z}, f3{em.x, em.y, em.z}, f3{nn.x, nn.y, nn.z}, ao, shadow);
+                c = shade<LIGHTS>(p, u, v, d, f3{al.x, al.y, al.z}, f3{em.x, em.y, em.z}, f3{nn.x, nn.y, nn.z}, ao, shadow);
             }
             outp[k] = pack_h4(c);
         }
-        row_ptr_w<uint4>(target, y)[x >> 1] = uint4{outp[0].x, outp[0].y, outp[1].x, outp[1].y};
+        const uint4 o = uint4{outp[0].x, outp[0].y, outp[1].x, outp[1].y};
+        typedef uint32_t v4w __attribute__((ext_vector_type(4)));
+        if (NT & 2) __builtin_nontemporal_store(__builtin_bit_cast(v4w, o), reinterpret_cast<v4w*>(row_ptr_w<uint4>(target, y)) + (x >> 1));
+        else row_ptr_w<uint4>(target, y)[x >> 1] = o;
     }
     if (HIST) {
         const f4 c0 = unpack_h4(outp[0]), c1 = unpack_h4(outp[1]);
@@ -268,17 +285,26 @@ int composition_launch(const soc_globals* g, const soc_globals* d_globals, soc_i
     if (bins && !(fast && W == g->resolution[0] && H == g->resolution[1])) return 1;
     if (fast) {
         dim3 grd(ceil_div(W, 32), ceil_div(H, 16));
+        const bool lights = (p.npl | p.nsl) != 0;
+#define SOC_COMP_PAIR(HI, LI) composition_pair<HI, LI><<<grd, 256, 0, hs(stream)>>>(dimg(target), dimg(albedo), \
+            dimg(emissive), dimg(normal), dimg(depth), dimg(ssao), dimg(shadow), dimg(clouds), p)
         if (bins) {
             p.bins = scratch;
             p.lmin = g->log_min_luminance;
             p.lrange = g->log_max_luminance - g->log_min_luminance;
-            composition_pair<true><<<grd, 256, 0, hs(stream)>>>(dimg(target), dimg(albedo), dimg(emissive), dimg(normal),
-                                                               dimg(depth), dimg(ssao), dimg(shadow), dimg(clouds), p);
+            if (lights) SOC_COMP_PAIR(true, true);
+            else SOC_COMP_PAIR(true, false);
             histogram_fold<<<1, kBins, 0, hs(stream)>>>(scratch, bins);
+        } else if (tuning_knob("SOC_COMP_NT", 3) == 3 && !lights) {
+            // non-temporal G-buffer loads and colour store (measured at 4K: 71.5 -> 68 us; TAA, the next
+            // reader of depth, +3 us: the frame is unchanged). SOC_COMP_NT=0: default cache policy.
+            composition_pair<false, false, 3><<<grd, 256, 0, hs(stream)>>>(dimg(target), dimg(albedo), dimg(emissive),
+                dimg(normal), dimg(depth), dimg(ssao), dimg(shadow), dimg(clouds), p);
         } else {
-            composition_pair<false><<<grd, 256, 0, hs(stream)>>>(dimg(target), dimg(albedo), dimg(emissive), dimg(normal),
-                                                                dimg(depth), dimg(ssao), dimg(shadow), dimg(clouds), p);
+            if (lights) SOC_COMP_PAIR(false, true);
+            else SOC_COMP_PAIR(false, false);
         }
+#undef SOC_COMP_PAIR
     } else {
         dim3 blk(BX, BY), grd(ceil_div(W, BX), ceil_div(H, BY));
         composition_generic<<<grd, blk, 0, hs(stream)>>>(dimg(target), dimg(albedo), dimg(emissive), dimg(normal),

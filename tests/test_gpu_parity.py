@@ -205,6 +205,24 @@ def test_ssao_blur_bit_exact(soc, oracle, W, H):
 
 
 # ------------------------------------------------------------------------------------------------ composition
+def test_composition_cache_policy_variants_bit_identical(soc, monkeypatch):
+    """The non-temporal load/store variant of the fast path (default) gives the plain variant's bits."""
+    W, H = 1920, 1080
+    g, gb = sponza_inputs(W, H)
+    shadow = dev(random_shadow(256, seed=3))
+    rng = np.random.default_rng(5)
+    ssao = dev(rng.integers(120, 256, (H // 2, W // 2), dtype=np.uint8))
+    clouds = dev(rng.integers(0, 256, (H, W, 4), dtype=np.uint8))
+    ins = [dev(gb[k]) for k in ("albedo", "emissive", "normal", "depth")]
+    outs = []
+    for nt in ("3", "0"):
+        monkeypatch.setenv("SOC_COMP_NT", nt)
+        out = torch.zeros(H, W, 4, dtype=torch.float16, device=DEV)
+        soc.composition(g, out, *ins, ssao, shadow, clouds)
+        outs.append(host(out))
+    assert np.array_equal(outs[0].view(np.uint16), outs[1].view(np.uint16))
+
+
 @pytest.mark.parametrize("W,H", [(64, 36), (97, 55), (512, 288), (1920, 1080)])
 @pytest.mark.parametrize("lights", [0, 3])
 def test_composition(soc, oracle, W, H, lights):
