@@ -23,7 +23,7 @@ from ._abi import (FMT_D32F, FMT_R8_UNORM, FMT_RGBA8_SRGB, FMT_RGBA8_UNORM, FMT_
                    SocImg)
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libsoc_rt.so")
+LIB_PATH = os.path.join(PKG_DIR, "lib", os.environ.get("SOC_RT_LIB_VARIANT", "libsoc_rt.so"))   # variant: A/B builds
 
 __all__ = ["SocError", "lib", "img", "Globals", "Camera", "AutoExposure", "globals_defaults", "frame_update",
            "bloom_downsample", "bloom_upsample", "bloom_chain", "ssao_prepare_noise", "ssao_generation",

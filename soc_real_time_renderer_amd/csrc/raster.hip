@@ -27,7 +27,10 @@ namespace soc {
 namespace {
 
 constexpr int SMALL_PIXELS = 64;    // bounding boxes up to this many pixels are scanned by one lane
-constexpr int TILE = 32;            // large-triangle work item: a 32x32 tile of its bounding box
+#ifndef SOC_RASTER_TILE
+#define SOC_RASTER_TILE 32
+#endif
+constexpr int TILE = SOC_RASTER_TILE;   // large-triangle work item: a TILE x TILE tile of its bounding box
 constexpr uint32_t KEY_EMPTY = 0xFFFFFFFFu;
 
 struct RasterParams {
@@ -36,18 +39,21 @@ struct RasterParams {
     int cull;
     int depth_only;
     float bias_constant, bias_slope;
-    uint32_t item_capacity;
     int precheck;       // load the target before the atomic (skip it when already nearer)
     int small_pixels;   // boxes up to this many pixels are scanned by one lane
+    int probe;          // profiling (SOC_RASTER_PROBE): 1 = skip the atomics, 2 = skip raster_big
 };
 
-// workspace: [float4 clip-space screen vertices[V]] [uint32 counter, pad..] [uint2 items[capacity]]
+// workspace: [float4 clip-space screen vertices[V]] [u64 counter, pad..] [uint2 entries[T]]
+// The counter packs (large triangles << 40 | tiles so far): one 64-bit atomicAdd per large triangle
+// returns its entry slot and the first index of its tile range together, so the entries are in
+// increasing range order and a work index finds its triangle by binary search.
 struct Workspace {
     float4* screen;
-    uint32_t* counter;
-    uint2* items;
-    uint32_t capacity;
+    unsigned long long* counter;
+    uint2* entries;   // {triangle, first tile index (low 32 bits of the range start)}
 };
+constexpr int ENTRY_SHIFT = 40;
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
@@ -56,10 +62,10 @@ inline Workspace carve(void* ws, int V, int T) {
     Workspace w;
     w.screen = reinterpret_cast<float4*>(p);
     size_t off = align_up((size_t)V * 16, 256);
-    w.counter = reinterpret_cast<uint32_t*>(p + off);
+    w.counter = reinterpret_cast<unsigned long long*>(p + off);
     off += 256;
-    w.items = reinterpret_cast<uint2*>(p + off);
-    w.capacity = (uint32_t)(4 * (size_t)T + (1u << 20));
+    w.entries = reinterpret_cast<uint2*>(p + off);
+    (void)T;
     return w;
 }
 
@@ -203,6 +209,7 @@ __device__ __forceinline__ void shade(const TriSetup& t, int id, int x, int y, c
                                       size_t pitch) {
     float e0, e1, e2, z;
     if (!cover(t, x, y, e0, e1, e2, z)) return;
+    if (p.probe == 1 && z > -1.0f) return;   // profiling probe: coverage work only, no memory traffic
     // a plain load first: values only decrease, so a stale (larger) value never skips a needed atomic
     if (p.depth_only) {
 #pragma clang fp contract(off)
@@ -225,7 +232,7 @@ __device__ __forceinline__ TriSetup load_tri(const Workspace& ws, const uint32_t
 
 __global__ __launch_bounds__(256) void raster_setup(const float* __restrict__ pos, Workspace ws, RasterParams p) {
     const int v = blockIdx.x * 256 + threadIdx.x;
-    if (v == 0) *ws.counter = 0u;
+    if (v == 0) *ws.counter = 0ull;
     if (v >= p.vertex_count) return;
     ws.screen[v] = clip_vertex(pos, v, p.model, p.vp, p.width, p.height);
 }
@@ -245,14 +252,9 @@ __global__ __launch_bounds__(256) void raster_small(const uint32_t* __restrict__
     const long long n = (long long)bw * bh;
     if (n > p.small_pixels) {
         const uint32_t chunks = (uint32_t)(((bw + TILE - 1) / TILE) * ((bh + TILE - 1) / TILE));
-        const uint32_t base = atomicAdd(ws.counter, chunks);
-        if (base + chunks <= ws.capacity) {
-            for (uint32_t k = 0; k < chunks; ++k) ws.items[base + k] = uint2{(uint32_t)id, k};
-            return;
-        }
-        // work list full: mark the reserved slots that exist as empty, rasterise the box in this lane
-        // (slow, correct)
-        for (uint32_t k = base; k < min(base + chunks, ws.capacity); ++k) ws.items[k] = uint2{0xFFFFFFFFu, 0u};
+        const unsigned long long old = atomicAdd(ws.counter, (1ull << ENTRY_SHIFT) + chunks);
+        ws.entries[old >> ENTRY_SHIFT] = uint2{(uint32_t)id, (uint32_t)old};
+        return;
     }
     for (int y = t.py0; y <= t.py1; ++y)
         for (int x = t.px0; x <= t.px1; ++x) shade(t, id, x, y, p, target, pitch);
@@ -269,12 +271,35 @@ __device__ __forceinline__ float edge_max(f3 r, float x0, float x1, float y0, fl
 // One wave per work item (triangle, 32x32 tile of its box): 64 lanes, 2 rows per step.
 __global__ __launch_bounds__(256) void raster_big(const uint32_t* __restrict__ idx, Workspace ws, RasterParams p,
                                                   void* target, size_t pitch) {
-    const uint32_t count = min(*ws.counter, ws.capacity);
+    const unsigned long long c = *ws.counter;
+    const uint32_t n_entries = (uint32_t)(c >> ENTRY_SHIFT), count = (uint32_t)(c & ((1ull << ENTRY_SHIFT) - 1));
     const int lane = threadIdx.x & 63;
-    for (uint32_t it = blockIdx.x * 4 + (threadIdx.x >> 6); it < count; it += gridDim.x * 4) {
-        const uint2 item = ws.items[it];
-        if (item.x == 0xFFFFFFFFu) continue;
-        const TriSetup t = load_tri(ws, idx, (int)item.x, p);
+    // each wave walks a contiguous slice of the work indices: one binary search for its first entry,
+    // then the entry advances as the slice crosses tile ranges
+    const uint32_t nwaves = gridDim.x * 4, wv = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t per = (count + nwaves - 1) / nwaves;
+    const uint32_t begin = min(count, wv * per), end = min(count, begin + per);
+    if (begin >= end) return;
+    uint32_t lo = 0, hi = n_entries - 1;   // the last entry with first <= begin
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (ws.entries[mid].y <= begin) lo = mid;
+        else hi = mid - 1;
+    }
+    uint32_t e_idx = lo;
+    uint2 e = ws.entries[e_idx];
+    uint32_t next_first = e_idx + 1 < n_entries ? ws.entries[e_idx + 1].y : 0xFFFFFFFFu;
+    TriSetup t = load_tri(ws, idx, (int)e.x, p);
+    for (uint32_t it = begin; it < end; ++it) {
+        if (it >= next_first) {
+            do {
+                ++e_idx;
+                e = ws.entries[e_idx];
+                next_first = e_idx + 1 < n_entries ? ws.entries[e_idx + 1].y : 0xFFFFFFFFu;
+            } while (it >= next_first);
+            t = load_tri(ws, idx, (int)e.x, p);
+        }
+        const uint2 item = uint2{e.x, it - e.y};
         const int tiles_x = (t.px1 - t.px0 + TILE) / TILE;
         const int ty = (int)item.y / tiles_x, tx = (int)item.y - ty * tiles_x;
         const int x0 = t.px0 + tx * TILE, y0 = t.py0 + ty * TILE;
@@ -283,9 +308,9 @@ __global__ __launch_bounds__(256) void raster_big(const uint32_t* __restrict__ i
         if (edge_max(t.r0, fx0, fx1, fy0, fy1) < 0.0f || edge_max(t.r1, fx0, fx1, fy0, fy1) < 0.0f ||
             edge_max(t.r2, fx0, fx1, fy0, fy1) < 0.0f)
             continue;
-        const int x = x0 + (lane & 31);
+        const int x = x0 + (lane % TILE);
         if (x > x1) continue;
-        for (int y = y0 + (lane >> 5); y <= y1; y += 2) shade(t, (int)item.x, x, y, p, target, pitch);
+        for (int y = y0 + lane / TILE; y <= y1; y += 64 / TILE) shade(t, (int)item.x, x, y, p, target, pitch);
     }
 }
 
@@ -446,9 +471,9 @@ RasterParams make_raster_params(const soc_mesh* mesh, const float* vp, int W, in
     p.vertex_count = mesh->vertex_count;
     p.triangle_count = mesh->triangle_count;
     p.cull = cull;
-    p.item_capacity = (uint32_t)(4 * (size_t)mesh->triangle_count + (1u << 20));
     p.precheck = tuning_knob("SOC_RASTER_PRECHECK", 0);
     p.small_pixels = tuning_knob("SOC_RASTER_SMALL", SMALL_PIXELS);
+    p.probe = tuning_knob("SOC_RASTER_PROBE", 0);
     return p;
 }
 
@@ -458,7 +483,7 @@ int launch_raster(const soc_mesh* mesh, const RasterParams& p, void* target, siz
     raster_setup<<<ceil_div(max(mesh->vertex_count, 1), 256), 256, 0, s>>>(mesh->positions, ws, p);
     if (mesh->triangle_count > 0) {
         raster_small<<<ceil_div(mesh->triangle_count, 256), 256, 0, s>>>(mesh->indices, ws, p, target, pitch);
-        raster_big<<<2048, 256, 0, s>>>(mesh->indices, ws, p, target, pitch);
+        if (p.probe != 2) raster_big<<<2048, 256, 0, s>>>(mesh->indices, ws, p, target, pitch);
     }
     return check_launch(pass);
 }
@@ -470,7 +495,7 @@ using namespace soc;
 
 extern "C" size_t soc_raster_workspace_size(int32_t vertex_count, int32_t triangle_count) {
     if (vertex_count < 0 || triangle_count < 0) return 0;
-    return align_up((size_t)vertex_count * 16, 256) + 256 + (4 * (size_t)triangle_count + (1u << 20)) * 8;
+    return align_up((size_t)vertex_count * 16, 256) + 256 + (size_t)triangle_count * 8;
 }
 
 extern "C" int soc_raster_visibility(const soc_mesh* mesh, const float view_projection[16], int32_t cull,
