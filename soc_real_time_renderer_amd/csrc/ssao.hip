@@ -1,8 +1,9 @@
 // ssao.hip — SSAOGenerationTask (src/graphics/tasks/ssao_generation.inl:20-68, shader :128-214) and
 // SSAOBlurTask (ssao_blur.inl:19-70, shader :91-106) as gfx950 kernels.
 //
-// SSAO: one lane per half-res output pixel, 16x16 pixel workgroups (a wave covers 16x4 pixels so the
-// 26 depth gathers of neighbouring lanes share L1/L2 lines). Each tap is a bilinear D32 sample under
+// SSAO: one lane per half-res output pixel, 32x8 pixel workgroups of 32x2-pixel waves (each tap row of
+// a wave spans 64 full-res texels = two 128-B lines, so the 26 depth gathers of neighbouring lanes share
+// L1/L2 lines; measured against 16x4 / 8x8 / 4x16 / 64x1 waves: 126 vs 132 / 144 / 158 / 135 us at 4K). Each tap is a bilinear D32 sample under
 // the sampling contract, fetched as two 8-byte row pairs. The per-pixel random vector of :184-188 is
 // a pure function of (uv, normal-image width): it is either evaluated inline or read from a table
 // filled once per resolution by the SAME device function (soc_ssao_prepare_noise), so both give
@@ -20,6 +21,7 @@ struct SsaoParams {
     int ksize;     // loop bound, min(kernel_size, 26)
     int noise_w;   // textureSize(u_normal_image).x
     int swz;       // XCD-aware tile order
+    int shape;     // wave shape: 3 = 32x2 in 32x8 tiles (default); 0 = 16x4, 1 = 8x8, 2 = 4x16 in 16x16; 4 = 64x1
 };
 
 // ssao_generation.inl:139-141 (no FMA contraction: keeps the sin argument as the oracle's)
@@ -102,7 +104,22 @@ __global__ __launch_bounds__(256) void ssao_kernel(DImg depth, DImg normal, DImg
                                                    SsaoParams p) {
     int bx, by;
     xcd_tile(p.swz, bx, by);
-    const int x = bx * 16 + threadIdx.x, y = by * 16 + threadIdx.y;
+    int lx = threadIdx.x, ly = threadIdx.y;
+    if (p.shape) {
+        const int tid = threadIdx.y * 16 + threadIdx.x, wave = tid >> 6, lane = tid & 63;
+        if (p.shape == 1) { lx = (wave & 1) * 8 + (lane & 7); ly = (wave >> 1) * 8 + (lane >> 3); }
+        else { lx = wave * 4 + (lane & 3); ly = lane >> 2; }
+    }
+    int x = bx * 16 + lx, y = by * 16 + ly;
+    if (p.shape == 3) {   // 32x8 tiles, waves of 32x2
+        const int tid = threadIdx.y * 16 + threadIdx.x;
+        x = bx * 32 + (tid & 31);
+        y = by * 8 + (tid >> 5);
+    } else if (p.shape == 4) {   // 64x4 tiles, waves of 64x1
+        const int tid = threadIdx.y * 16 + threadIdx.x;
+        x = bx * 64 + (tid & 63);
+        y = by * 4 + (tid >> 6);
+    }
     if (x >= target.w || y >= target.h) return;
     const float u = centre_uv(x, target.w), v = centre_uv(y, target.h);
 
@@ -214,6 +231,7 @@ SsaoParams make_params(const soc_globals* g, const soc_img& normal) {
     p.ksize = g->ssao_kernel_size < SOC_SSAO_MAX_KERNEL ? g->ssao_kernel_size : SOC_SSAO_MAX_KERNEL;
     p.noise_w = normal.width;
     p.swz = tuning_knob("SOC_SWZ_SSAO", 0);
+    p.shape = tuning_knob("SOC_SSAO_SHAPE", 3);
     return p;
 }
 
@@ -247,6 +265,8 @@ extern "C" int soc_ssao_generation(const soc_globals* g, soc_img depth, soc_img 
     const float* IP = g->camera_inverse_projection_matrix;
     const bool sip = IP[2] == 0.0f && IP[3] == 0.0f && IP[6] == 0.0f && IP[7] == 0.0f;
     dim3 blk(16, 16), grd(ceil_div(target.width, 16), ceil_div(target.height, 16));
+    if (p.shape == 3) grd = dim3(ceil_div(target.width, 32), ceil_div(target.height, 8));
+    if (p.shape == 4) grd = dim3(ceil_div(target.width, 64), ceil_div(target.height, 4));
     const float2* tb = reinterpret_cast<const float2*>(noise_table);
     hipStream_t st = hs(stream);
     DImg dd = dimg(depth), dn = dimg(normal), dt = dimg(target);

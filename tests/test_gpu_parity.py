@@ -192,6 +192,21 @@ def test_ssao_noise_table_is_bit_identical(soc):
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("W,H", [(97, 55), (1920, 1080)])
+def test_ssao_wave_shapes_bit_identical(soc, monkeypatch, W, H):
+    """Every wave shape (tuning knob SOC_SSAO_SHAPE) computes each pixel the same way."""
+    g, gb = sponza_inputs(W, H)
+    depth, normal = dev(gb["depth"]), dev(gb["normal"])
+    outs = []
+    for shape in ("3", "0", "1", "2", "4"):
+        monkeypatch.setenv("SOC_SSAO_SHAPE", shape)
+        out = torch.zeros(H // 2, W // 2, dtype=torch.uint8, device=DEV)
+        soc.ssao_generation(g, depth, normal, out)
+        outs.append(host(out))
+    for o in outs[1:]:
+        assert np.array_equal(o, outs[0])
+
+
 @pytest.mark.parametrize("W,H", [(64, 36), (97, 55), (1920, 1080)])
 def test_ssao_blur_bit_exact(soc, oracle, W, H):
     g = globals_for(W, H)
