@@ -448,10 +448,12 @@ int soc_raster_visibility(const soc_mesh* mesh, const float view_projection[16],
 int soc_raster_depth(const soc_mesh* mesh, const float view_projection[16], int32_t cull, float bias_constant,
                      float bias_slope, soc_img depth, void* workspace, soc_stream stream);
 /* G-buffer from a visibility buffer: depth (D32), albedo / emissive / normal / velocity (RGBA16F), with the
- * clear values of GBufferGeneration for empty pixels. `d_materials` is a device array. */
+ * clear values of GBufferGeneration for empty pixels. `d_materials` is a device array. `workspace`
+ * (soc_raster_workspace_size bytes, may be the raster's) lets the vertex stage run once per vertex;
+ * NULL evaluates it per pixel. Same bits either way. */
 int soc_gbuffer_resolve(const soc_globals* g, const soc_mesh* mesh, const soc_material* d_materials,
                         int32_t material_count, const uint64_t* visibility, soc_img depth, soc_img albedo,
-                        soc_img emissive, soc_img normal, soc_img velocity, soc_stream stream);
+                        soc_img emissive, soc_img normal, soc_img velocity, void* workspace, soc_stream stream);
 
 /* Render-graph raster head (renderer.cpp:965-1021: DepthPrepass, SunShadowDraw, GBufferGeneration): with a
  * scene set, every PRE phase first rasterises the mesh into the frame's G-buffer images (depth, albedo,

@@ -199,7 +199,7 @@ FUNCTIONS = {
     "soc_raster_visibility": (_I, [C.POINTER(Mesh), C.POINTER(C.c_float), C.c_int32, _P, C.c_int32, C.c_int32,
                                    C.c_int32, _P, _P]),
     "soc_raster_depth": (_I, [C.POINTER(Mesh), C.POINTER(C.c_float), C.c_int32, C.c_float, C.c_float, _IMG, _P, _P]),
-    "soc_gbuffer_resolve": (_I, [_G, C.POINTER(Mesh), _P, C.c_int32, _P, _IMG, _IMG, _IMG, _IMG, _IMG, _P]),
+    "soc_gbuffer_resolve": (_I, [_G, C.POINTER(Mesh), _P, C.c_int32, _P, _IMG, _IMG, _IMG, _IMG, _IMG, _P, _P]),
 }
 
 # not in the public header: test hooks

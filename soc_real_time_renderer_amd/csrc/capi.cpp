@@ -542,7 +542,7 @@ void build_raster_passes(soc_renderer* r) {
     add("GBufferGeneration", "Rendering G-Buffer", [r](const soc_globals* g, hipStream_t s) {
         const soc_frame_images& I = r->img;
         return soc_gbuffer_resolve(g, &r->scene.mesh, r->scene.materials, r->scene.material_count, r->scene.visibility,
-                                   I.depth, I.albedo, I.emissive, I.normal, I.velocity, (soc_stream)s);
+                                   I.depth, I.albedo, I.emissive, I.normal, I.velocity, r->scene.workspace, (soc_stream)s);
     });
 }
 

@@ -52,6 +52,7 @@ struct Workspace {
     float4* screen;
     unsigned long long* counter;
     uint2* entries;   // {triangle, first tile index (low 32 bits of the range start)}
+    float4* vdata;    // G-buffer resolve: 4 float4 per vertex (gbuffer_vertex_setup)
 };
 constexpr int ENTRY_SHIFT = 40;
 
@@ -65,7 +66,8 @@ inline Workspace carve(void* ws, int V, int T) {
     w.counter = reinterpret_cast<unsigned long long*>(p + off);
     off += 256;
     w.entries = reinterpret_cast<uint2*>(p + off);
-    (void)T;
+    off = align_up(off + (size_t)T * 8, 256);
+    w.vdata = reinterpret_cast<float4*>(p + off);
     return w;
 }
 
@@ -374,10 +376,50 @@ __device__ __forceinline__ f3 normalize_exact(f3 a) {
     return f3{a.x / l, a.y / l, a.z / l};
 }
 
+// The vertex stage of GBufferGeneration (g_buffer_generation.inl:169-178) for vertex v: the raster's
+// homogeneous screen vertex, normalize(normal_matrix * normal), and the current / previous clip x, y, w.
+// 4 float4 per vertex; computed once per vertex into the workspace (gbuffer_vertex_setup) or inline by
+// the resolve; the same function either way, so both give the same bits.
+struct VtxData { float4 s, n, cc, pc; };
+
+__device__ __forceinline__ VtxData vertex_data(const soc_mesh& mesh, uint32_t v, const ResolveParams& p) {
+#pragma clang fp contract(off)
+    VtxData d;
+    d.s = clip_vertex(mesh.positions, v, p.model, p.vp, p.width, p.height);
+    const float* nr = mesh.normals;
+    const f3 n = normalize_exact(mat3_vec_exact(p.normal3, f3{nr[3 * v], nr[3 * v + 1], nr[3 * v + 2]}));
+    d.n = float4{n.x, n.y, n.z, 0.0f};
+    const float* ps = mesh.positions;
+    const f4 wp = mat_vec_exact(p.model, ps[3 * v], ps[3 * v + 1], ps[3 * v + 2], 1.0f);
+    const f4 c = mat_vec_exact(p.vp, wp.x, wp.y, wp.z, wp.w);
+    const f4 q = mat_vec_exact(p.prev_vp, wp.x, wp.y, wp.z, wp.w);
+    d.cc = float4{c.x, c.y, c.w, 0.0f};
+    d.pc = float4{q.x, q.y, q.w, 0.0f};
+    return d;
+}
+
+__global__ __launch_bounds__(256) void gbuffer_vertex_setup(soc_mesh mesh, float4* __restrict__ vd, ResolveParams p) {
+    const int v = blockIdx.x * 256 + threadIdx.x;
+    if (v >= mesh.vertex_count) return;
+    const VtxData d = vertex_data(mesh, (uint32_t)v, p);
+    vd[4 * v] = d.s;
+    vd[4 * v + 1] = d.n;
+    vd[4 * v + 2] = d.cc;
+    vd[4 * v + 3] = d.pc;
+}
+
+template <bool PRE>
+__device__ __forceinline__ VtxData fetch_vertex(const soc_mesh& mesh, const float4* __restrict__ vd, uint32_t v,
+                                                const ResolveParams& p) {
+    if (!PRE) return vertex_data(mesh, v, p);
+    return VtxData{vd[4 * v], vd[4 * v + 1], vd[4 * v + 2], vd[4 * v + 3]};
+}
+
+template <bool PRE>
 __global__ __launch_bounds__(256) void gbuffer_resolve(soc_mesh mesh, const soc_material* __restrict__ mats,
                                                        const unsigned long long* __restrict__ vis, DImg depth,
                                                        DImg albedo, DImg emissive, DImg normal, DImg velocity,
-                                                       ResolveParams p) {
+                                                       const float4* __restrict__ vd, ResolveParams p) {
 #pragma clang fp contract(off)
     __shared__ float lut[256];
     lut[threadIdx.y * 64 + threadIdx.x] = srgb_to_linear(unorm8(threadIdx.y * 64 + threadIdx.x));
@@ -396,9 +438,9 @@ __global__ __launch_bounds__(256) void gbuffer_resolve(soc_mesh mesh, const soc_
     }
     const int id = (int)(0xFFFFFFFEu - low);
     const uint32_t ia = mesh.indices[3 * id], ib = mesh.indices[3 * id + 1], ic = mesh.indices[3 * id + 2];
-    const float4 A = clip_vertex(mesh.positions, ia, p.model, p.vp, p.width, p.height);
-    const float4 B = clip_vertex(mesh.positions, ib, p.model, p.vp, p.width, p.height);
-    const float4 C = clip_vertex(mesh.positions, ic, p.model, p.vp, p.width, p.height);
+    const VtxData VA = fetch_vertex<PRE>(mesh, vd, ia, p), VB = fetch_vertex<PRE>(mesh, vd, ib, p),
+                  VC = fetch_vertex<PRE>(mesh, vd, ic, p);
+    const float4 A = VA.s, B = VB.s, C = VC.s;
     // perspective-correct barycentrics b_i = E_i / sum E from the raster's edge functions
     const f3 v0{A.x, A.y, A.w}, v1{B.x, B.y, B.w}, v2{C.x, C.y, C.w};
     f3 r0 = cross_exact(v1, v2), r1 = cross_exact(v2, v0), r2 = cross_exact(v0, v1);
@@ -409,14 +451,11 @@ __global__ __launch_bounds__(256) void gbuffer_resolve(soc_mesh mesh, const soc_
     const float es = e0 + e1 + e2;
     const float b1 = e1 / es, b2 = e2 / es, b0 = 1.0f - b1 - b2;
 
-    // vertex stage (g_buffer_generation.inl:169-178): uv, normal_matrix * normal, current/previous clip
+    // interpolated vertex outputs (g_buffer_generation.inl:169-178)
     const float* uv = mesh.uvs;
     const float u = b0 * uv[2 * ia] + b1 * uv[2 * ib] + b2 * uv[2 * ic];
     const float v = b0 * uv[2 * ia + 1] + b1 * uv[2 * ib + 1] + b2 * uv[2 * ic + 1];
-    const float* nr = mesh.normals;
-    const f3 na = normalize_exact(mat3_vec_exact(p.normal3, f3{nr[3 * ia], nr[3 * ia + 1], nr[3 * ia + 2]}));
-    const f3 nb = normalize_exact(mat3_vec_exact(p.normal3, f3{nr[3 * ib], nr[3 * ib + 1], nr[3 * ib + 2]}));
-    const f3 nc = normalize_exact(mat3_vec_exact(p.normal3, f3{nr[3 * ic], nr[3 * ic + 1], nr[3 * ic + 2]}));
+    const float4 na = VA.n, nb = VB.n, nc = VC.n;
     const f3 n = normalize_exact(f3{b0 * na.x + b1 * nb.x + b2 * nc.x, b0 * na.y + b1 * nb.y + b2 * nc.y,
                                     b0 * na.z + b1 * nb.z + b2 * nc.z});
     const uint32_t mi = mesh.materials ? min(mesh.materials[id], (uint32_t)(p.material_count - 1)) : 0u;
@@ -429,18 +468,11 @@ __global__ __launch_bounds__(256) void gbuffer_resolve(soc_mesh mesh, const soc_
     const f4 al = sample_texture(m.albedo, u, v, lut);
     f4 vel = f4{0.0f, 0.0f, 0.0f, 0.0f};
     if (!(m.flags & SOC_MATERIAL_ZERO_VELOCITY)) {
-        const float* ps = mesh.positions;
-        f4 cc[3], pc[3];
-        const uint32_t vi[3] = {ia, ib, ic};
-        for (int k = 0; k < 3; ++k) {
-            const f4 wp = mat_vec_exact(p.model, ps[3 * vi[k]], ps[3 * vi[k] + 1], ps[3 * vi[k] + 2], 1.0f);
-            cc[k] = mat_vec_exact(p.vp, wp.x, wp.y, wp.z, wp.w);
-            pc[k] = mat_vec_exact(p.prev_vp, wp.x, wp.y, wp.z, wp.w);
-        }
-        const float cx = b0 * cc[0].x + b1 * cc[1].x + b2 * cc[2].x, cy = b0 * cc[0].y + b1 * cc[1].y + b2 * cc[2].y;
-        const float cw = b0 * cc[0].w + b1 * cc[1].w + b2 * cc[2].w;
-        const float px = b0 * pc[0].x + b1 * pc[1].x + b2 * pc[2].x, py = b0 * pc[0].y + b1 * pc[1].y + b2 * pc[2].y;
-        const float pw = b0 * pc[0].w + b1 * pc[1].w + b2 * pc[2].w;
+        const float4 ca = VA.cc, cb = VB.cc, cd = VC.cc, pa = VA.pc, pb = VB.pc, pd = VC.pc;
+        const float cx = b0 * ca.x + b1 * cb.x + b2 * cd.x, cy = b0 * ca.y + b1 * cb.y + b2 * cd.y;
+        const float cw = b0 * ca.z + b1 * cb.z + b2 * cd.z;
+        const float px = b0 * pa.x + b1 * pb.x + b2 * pd.x, py = b0 * pa.y + b1 * pb.y + b2 * pd.y;
+        const float pw = b0 * pa.z + b1 * pb.z + b2 * pd.z;
         vel = f4{((cx / cw) * 0.5f + 0.5f) - ((px / pw) * 0.5f + 0.5f), ((cy / cw) * 0.5f + 0.5f) - ((py / pw) * 0.5f + 0.5f),
                  0.0f, 1.0f};
     }
@@ -495,7 +527,8 @@ using namespace soc;
 
 extern "C" size_t soc_raster_workspace_size(int32_t vertex_count, int32_t triangle_count) {
     if (vertex_count < 0 || triangle_count < 0) return 0;
-    return align_up((size_t)vertex_count * 16, 256) + 256 + (size_t)triangle_count * 8;
+    return align_up(align_up((size_t)vertex_count * 16, 256) + 256 + (size_t)triangle_count * 8, 256) +
+           (size_t)vertex_count * 64;
 }
 
 extern "C" int soc_raster_visibility(const soc_mesh* mesh, const float view_projection[16], int32_t cull,
@@ -535,7 +568,8 @@ extern "C" int soc_raster_depth(const soc_mesh* mesh, const float view_projectio
 
 extern "C" int soc_gbuffer_resolve(const soc_globals* g, const soc_mesh* mesh, const soc_material* d_materials,
                                    int32_t material_count, const uint64_t* visibility, soc_img depth, soc_img albedo,
-                                   soc_img emissive, soc_img normal, soc_img velocity, soc_stream stream) {
+                                   soc_img emissive, soc_img normal, soc_img velocity, void* workspace,
+                                   soc_stream stream) {
     int rc = check_mesh(mesh, "soc_gbuffer_resolve", true);
     if (!rc) rc = check_img(depth, SOC_FMT_D32F, "soc_gbuffer_resolve", "depth");
     if (!rc) rc = check_img(albedo, SOC_FMT_RGBA16F, "soc_gbuffer_resolve", "albedo");
@@ -561,7 +595,16 @@ extern "C" int soc_gbuffer_resolve(const soc_globals* g, const soc_mesh* mesh, c
     p.triangle_count = mesh->triangle_count;
     p.material_count = material_count;
     dim3 blk(64, 4), grd(ceil_div(W, 64), ceil_div(H, 4));
-    gbuffer_resolve<<<grd, blk, 0, hs(stream)>>>(*mesh, d_materials, reinterpret_cast<const unsigned long long*>(visibility),
-                                                 dimg(depth), dimg(albedo), dimg(emissive), dimg(normal), dimg(velocity), p);
+    const unsigned long long* vis = reinterpret_cast<const unsigned long long*>(visibility);
+    if (workspace) {   // per-vertex outputs once, then the per-pixel resolve reads them
+        const Workspace ws = carve(workspace, mesh->vertex_count, mesh->triangle_count);
+        if (mesh->vertex_count > 0)
+            gbuffer_vertex_setup<<<ceil_div(mesh->vertex_count, 256), 256, 0, hs(stream)>>>(*mesh, ws.vdata, p);
+        gbuffer_resolve<true><<<grd, blk, 0, hs(stream)>>>(*mesh, d_materials, vis, dimg(depth), dimg(albedo),
+                                                           dimg(emissive), dimg(normal), dimg(velocity), ws.vdata, p);
+    } else {
+        gbuffer_resolve<false><<<grd, blk, 0, hs(stream)>>>(*mesh, d_materials, vis, dimg(depth), dimg(albedo),
+                                                            dimg(emissive), dimg(normal), dimg(velocity), nullptr, p);
+    }
     return check_launch("gbuffer_resolve");
 }

@@ -121,10 +121,11 @@ def raster_depth(mesh: MeshBuffers, view_projection, cull, depth: torch.Tensor, 
 
 
 def gbuffer_resolve(g, mesh: MeshBuffers, d_materials: torch.Tensor, material_count: int, visibility: torch.Tensor,
-                    depth, albedo, emissive, normal, velocity, stream=None):
+                    depth, albedo, emissive, normal, velocity, workspace=None, stream=None):
+    """workspace (MeshBuffers.workspace()): vertex stage once per vertex; None: per pixel (same bits)."""
     _check(lib().soc_gbuffer_resolve(_gp(g), C.byref(mesh.struct), _ptr(d_materials), int(material_count),
                                      _ptr(visibility), img(depth), img(albedo), img(emissive), img(normal), img(velocity),
-                                     _stream(stream)), "gbuffer_resolve")
+                                     _ptr(workspace), _stream(stream)), "gbuffer_resolve")
 
 
 def visibility_triangles(vis) -> np.ndarray:

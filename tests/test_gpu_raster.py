@@ -140,6 +140,12 @@ def test_gbuffer_resolve(soc, oracle, scene_id, camera, W, H):
     assert np.array_equal(host(out["depth"]), ref["depth"])
     for k in ("albedo", "emissive", "normal", "velocity"):
         assert f16_close(host(out[k]), ref[k]).all(), k
+    # the vertex stage precomputed once per vertex (workspace) gives the per-pixel path's bits
+    out2 = {k: torch.zeros_like(v) for k, v in out.items()}
+    raster.gbuffer_resolve(g, dm, dmat, len(dmats), dvis, out2["depth"], out2["albedo"], out2["emissive"],
+                           out2["normal"], out2["velocity"], workspace=dm.workspace())
+    for k in out:
+        assert torch.equal(out[k], out2[k]), k
 
 
 @pytest.mark.parametrize("scene_id,camera", [(scene.SPONZA_PROXY, SPONZA_CAMERA), (scene.TERRAIN, TERRAIN_CAMERA)])
