@@ -3,7 +3,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 rm -rf gpurun_out/ktq
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/ktq -o run -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --profile-frames 2 --no-sky-lane > gpurun_out/ktq.log 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/ktq -o run -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --profile-frames 2 --no-sky-lane ${KT_ARGS:-} > gpurun_out/ktq.log 2>&1 || exit 1
 python - <<'PY'
 import csv, glob
 f = glob.glob('gpurun_out/ktq/**/*kernel_stats.csv', recursive=True)[0]
