@@ -5,7 +5,7 @@ set -o pipefail
 export TMPDIR=/tmp
 OUT=$1; shift
 mkdir -p $OUT
-ARGS="--steps 3 --warmup 1 --no-cpu-baseline --profile-frames 1"
+ARGS="--steps 3 --warmup 1 --no-cpu-baseline --profile-frames 1 ${BENCH_ARGS:-}"
 i=0
 for pass in "$@"; do
   i=$((i+1))
