@@ -455,6 +455,10 @@ int soc_gbuffer_resolve(const soc_globals* g, const soc_mesh* mesh, const soc_ma
                         int32_t material_count, const uint64_t* visibility, soc_img depth, soc_img albedo,
                         soc_img emissive, soc_img normal, soc_img velocity, void* workspace, soc_stream stream);
 
+/* HeightToNormalTask (height_to_normal.inl:52-83): RGBA8 heightmap (.r) -> RGBA16F normal map of the same
+ * extent; run once at terrain load (renderer.cpp:158-190). */
+int soc_height_to_normal(soc_img heightmap, soc_img normal_target, soc_stream stream);
+
 /* Render-graph raster head (renderer.cpp:965-1021: DepthPrepass, SunShadowDraw, GBufferGeneration): with a
  * scene set, every PRE phase first rasterises the mesh into the frame's G-buffer images (depth, albedo,
  * emissive, normal, velocity) and, with `shadow`, the sun shadow map into images.shadow, on the caller's

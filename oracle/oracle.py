@@ -38,6 +38,7 @@ _FUNCS = {
                                           _IMG]),
     "soc_oracle_gbuffer_resolve": (C.c_int, [_G, C.POINTER(_abi.Mesh), C.POINTER(_abi.Material), C.c_int32, C.c_void_p,
                                              _IMG, _IMG, _IMG, _IMG, _IMG]),
+    "soc_oracle_height_to_normal": (C.c_int, [_IMG, _IMG]),
     "soc_oracle_luminance_bin": (C.c_uint32, [C.c_float] * 5),
     "soc_oracle_log2": (C.c_float, [C.c_float]),
     "soc_oracle_f32_to_f16": (C.c_uint16, [C.c_float]),
@@ -153,6 +154,10 @@ def gbuffer_resolve(g, mesh, materials, vis, depth, albedo, emissive, normal, ve
     _rc(lib().soc_oracle_gbuffer_resolve(C.byref(g), C.byref(mesh.struct), arr, len(materials), vis.ctypes.data,
                                          _img(depth), _img(albedo), _img(emissive), _img(normal), _img(velocity)),
         "gbuffer_resolve")
+
+
+def height_to_normal(heightmap, target):
+    _rc(lib().soc_oracle_height_to_normal(_img(heightmap), _img(target)), "height_to_normal")
 
 
 def luminance_bin(r, g, b, log_min, log_max) -> int:

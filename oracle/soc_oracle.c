@@ -1270,3 +1270,28 @@ int soc_oracle_gbuffer_resolve(const soc_globals* g, const soc_mesh* mesh, const
         }
     return SOC_OK;
 }
+
+/* ------------------------------------------------------------------------------------------------ */
+/* HeightToNormalTask, height_to_normal.inl:52-83                                                     */
+/* ------------------------------------------------------------------------------------------------ */
+int soc_oracle_height_to_normal(soc_img heightmap, soc_img target) {
+    if (!valid(&heightmap) || !valid(&target) || heightmap.width != target.width || heightmap.height != target.height)
+        return SOC_E_INVALID_ARG;
+    const int W = heightmap.width, H = heightmap.height;
+#pragma omp parallel for schedule(static)
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+            /* clamp(pos + offset, 0, size - 1), :57-60 */
+            int yu = y + 1 < H - 1 ? y + 1 : H - 1, yd = y - 1 > 0 ? y - 1 : 0;
+            int xr = x + 1 < W - 1 ? x + 1 : W - 1, xl = x - 1 > 0 ? x - 1 : 0;
+            float su = fetch(&heightmap, x, yu).x, sd = fetch(&heightmap, x, yd).x;
+            float sr = fetch(&heightmap, xr, y).x, sl = fetch(&heightmap, xl, y).x;
+            float fw = (float)W, fh = (float)H;
+            v3 pu = V3((float)x / fw, su, (float)yu / fh), pd = V3((float)x / fw, sd, (float)yd / fh);
+            v3 pr = V3((float)xr / fw, sr, (float)y / fh), pl = V3((float)xl / fw, sl, (float)y / fh);
+            v3 vd = rs_normalize(sub3(pu, pd)), hd = rs_normalize(sub3(pr, pl));
+            v3 n = rs_normalize(cross3(vd, hd));
+            store(&target, x, y, V4(n.x, n.y, n.z, 1.0f));
+        }
+    return SOC_OK;
+}

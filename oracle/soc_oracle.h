@@ -46,6 +46,8 @@ int soc_oracle_gbuffer_resolve(const soc_globals* g, const soc_mesh* mesh, const
                                int32_t material_count, const uint64_t* visibility, soc_img depth, soc_img albedo,
                                soc_img emissive, soc_img normal, soc_img velocity);
 
+int soc_oracle_height_to_normal(soc_img heightmap, soc_img target);
+
 /* Scalar helpers exposed for known-answer tests. */
 uint32_t soc_oracle_luminance_bin(float r, float g, float b, float log_min, float log_max);
 float soc_oracle_log2(float x);

@@ -148,3 +148,8 @@ def scene_setup(g, scene_id: int, tex_size: int = 512, device="cuda") -> dict:
             for i in range(len(tex))]
     return {"mesh": mesh, "textures": dtex, "materials": materials_device(mats, device), "material_count": len(mats),
             "host_mesh": m, "host_textures": tex, "emissive": em, "workspace": mesh.workspace(device)}
+
+
+def height_to_normal(heightmap, normal_target, stream=None):
+    """HeightToNormalTask (height_to_normal.inl:52-83): (H, W, 4) uint8 heightmap -> (H, W, 4) f16 normals."""
+    _check(lib().soc_height_to_normal(img(heightmap), img(normal_target), _stream(stream)), "height_to_normal")

@@ -43,6 +43,7 @@ def lib():
             "soc_scene_mesh_counts": (C.c_int, [C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
             "soc_scene_mesh": (C.c_int, [C.c_int, G] + [C.c_void_p] * 5),
             "soc_scene_material_count": (C.c_int, [C.c_int]),
+            "soc_scene_terrain_heightmap": (C.c_int, [C.c_int, C.c_void_p]),
             "soc_scene_material_textures": (C.c_int, [C.c_int, G, C.c_int, C.c_void_p, C.c_void_p]),
         })
         _LIB = l
@@ -91,6 +92,14 @@ def material_textures(g: Globals, size: int, scene_id: int = SPONZA_PROXY):
     if lib().soc_scene_material_textures(scene_id, C.byref(g), size, tex.ctypes.data, em.ctypes.data):
         raise RuntimeError("soc_scene_material_textures failed")
     return tex, em
+
+
+def terrain_heightmap(size: int = 1024) -> np.ndarray:
+    """(size, size, 4) uint8 heightmap of the C4 terrain (R8G8B8A8_UNORM as renderer.cpp:155 loads it)."""
+    out = np.zeros((size, size, 4), np.uint8)
+    if lib().soc_scene_terrain_heightmap(size, out.ctypes.data):
+        raise RuntimeError("soc_scene_terrain_heightmap failed")
+    return out
 
 
 def noise_texture() -> np.ndarray:

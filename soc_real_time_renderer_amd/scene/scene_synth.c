@@ -646,3 +646,19 @@ int soc_scene_material_textures(int scene_id, const soc_globals* g, int size, ui
     }
     return 0;
 }
+
+/* Terrain heightmap as the reference loads it (R8G8B8A8_UNORM, renderer.cpp:155): terrain_height at
+   texel centres, 8-bit in r = g = b, a = 255 (input of HeightToNormalTask). */
+int soc_scene_terrain_heightmap(int size, uint8_t* rgba) {
+    if (size <= 0 || !rgba) return -1;
+#pragma omp parallel for schedule(static)
+    for (int y = 0; y < size; ++y)
+        for (int x = 0; x < size; ++x) {
+            const float h = terrain_height(((float)x + 0.5f) / (float)size, ((float)y + 0.5f) / (float)size);
+            const uint8_t v = (uint8_t)lrintf((h < 0.0f ? 0.0f : (h > 1.0f ? 1.0f : h)) * 255.0f);
+            uint8_t* o = rgba + 4 * ((size_t)y * size + x);
+            o[0] = o[1] = o[2] = v;
+            o[3] = 255;
+        }
+    return 0;
+}
