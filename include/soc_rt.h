@@ -459,6 +459,13 @@ int soc_gbuffer_resolve(const soc_globals* g, const soc_mesh* mesh, const soc_ma
  * extent; run once at terrain load (renderer.cpp:158-190). */
 int soc_height_to_normal(soc_img heightmap, soc_img normal_target, soc_stream stream);
 
+/* GenerateMinHIZTask / GenerateMaxHIZTask (generate_min_hiz.inl:23-95, generate_hiz.glsl:17-98): single-pass
+ * min (op_max = 0) or max depth pyramid. mips[i] is D32 of (W/2 >> i) x (H/2 >> i) (at least 1), i <
+ * mip_count <= 12 (the reference uses ceil(log2(max(W, H) / 2)) levels); `counter` is one device u32 of
+ * scratch (reset by the call). Computed but unused by the reference graph (quirk Q12). */
+int soc_generate_hiz(const soc_globals* g, soc_img depth, const soc_img* mips, int32_t mip_count, int32_t op_max,
+                     uint32_t* counter, soc_stream stream);
+
 /* Render-graph raster head (renderer.cpp:965-1021: DepthPrepass, SunShadowDraw, GBufferGeneration): with a
  * scene set, every PRE phase first rasterises the mesh into the frame's G-buffer images (depth, albedo,
  * emissive, normal, velocity) and, with `shadow`, the sun shadow map into images.shadow, on the caller's

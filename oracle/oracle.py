@@ -39,6 +39,7 @@ _FUNCS = {
     "soc_oracle_gbuffer_resolve": (C.c_int, [_G, C.POINTER(_abi.Mesh), C.POINTER(_abi.Material), C.c_int32, C.c_void_p,
                                              _IMG, _IMG, _IMG, _IMG, _IMG]),
     "soc_oracle_height_to_normal": (C.c_int, [_IMG, _IMG]),
+    "soc_oracle_generate_hiz": (C.c_int, [_G, _IMG, C.POINTER(_IMG), C.c_int32, C.c_int32]),
     "soc_oracle_luminance_bin": (C.c_uint32, [C.c_float] * 5),
     "soc_oracle_log2": (C.c_float, [C.c_float]),
     "soc_oracle_f32_to_f16": (C.c_uint16, [C.c_float]),
@@ -158,6 +159,11 @@ def gbuffer_resolve(g, mesh, materials, vis, depth, albedo, emissive, normal, ve
 
 def height_to_normal(heightmap, target):
     _rc(lib().soc_oracle_height_to_normal(_img(heightmap), _img(target)), "height_to_normal")
+
+
+def generate_hiz(g, depth, mips, op_max=False):
+    arr = (_IMG * len(mips))(*[_img(m) for m in mips])
+    _rc(lib().soc_oracle_generate_hiz(C.byref(g), _img(depth), arr, len(mips), int(bool(op_max))), "generate_hiz")
 
 
 def luminance_bin(r, g, b, log_min, log_max) -> int:

@@ -1295,3 +1295,58 @@ int soc_oracle_height_to_normal(soc_img heightmap, soc_img target) {
         }
     return SOC_OK;
 }
+
+/* ------------------------------------------------------------------------------------------------ */
+/* GenerateMin/MaxHIZTask, generate_hiz.glsl:17-98: the same 64x64-window reduction, serially. Every   */
+/* window value is an exact min / max, so a per-window restatement over "virtual" mips (texels beyond  */
+/* a mip's extent included, as the shader's LDS keeps them) gives the shader's results.               */
+/* ------------------------------------------------------------------------------------------------ */
+static inline float hz_op(int mx, float a, float b) { return mx ? fmaxf(a, b) : fminf(a, b); }
+
+static void hz_store(const soc_img* mips, int count, int level, int x, int y, float v) {
+    if (level >= count) return;
+    const soc_img* d = &mips[level];
+    if (x < d->width && y < d->height) ((float*)((char*)d->data + (size_t)y * d->pitch_bytes))[x] = v;
+}
+
+static float hz_load(const soc_img* im, int x, int y, int w, int h) {
+    x = x < w - 1 ? x : w - 1;
+    y = y < h - 1 ? y : h - 1;
+    return ((const float*)((const char*)im->data + (size_t)y * im->pitch_bytes))[x];
+}
+
+/* one workgroup: window (gx, gy) of `src` (clamped to w x h) -> levels src_level+1 .. src_level+levels */
+static void hz_window(const soc_img* src, int w, int h, int gx, int gy, int src_level, int levels, const soc_img* mips,
+                      int count, int mx) {
+    float a[32][32], b[32][32];   /* virtual level src_level+1 (32x32) and the following ones */
+    for (int y = 0; y < 32; ++y)
+        for (int x = 0; x < 32; ++x) {
+            int ix = (gx * 32 + x) * 2, iy = (gy * 32 + y) * 2;
+            float m = hz_op(mx, hz_op(mx, hz_load(src, ix, iy, w, h), hz_load(src, ix, iy + 1, w, h)),
+                            hz_op(mx, hz_load(src, ix + 1, iy, w, h), hz_load(src, ix + 1, iy + 1, w, h)));
+            a[y][x] = m;
+            hz_store(mips, count, src_level + 1, gx * 32 + x, gy * 32 + y, m);
+        }
+    int n = 32;
+    for (int i = 1; i < (levels > 2 ? levels : 2); ++i) {   /* the shader always writes the second level */
+        n /= 2;
+        for (int y = 0; y < n; ++y)
+            for (int x = 0; x < n; ++x) {
+                float m = hz_op(mx, hz_op(mx, a[2 * y][2 * x], a[2 * y][2 * x + 1]), hz_op(mx, a[2 * y + 1][2 * x], a[2 * y + 1][2 * x + 1]));
+                b[y][x] = m;
+                hz_store(mips, count, src_level + 1 + i, (gx * 32 >> i) + x, (gy * 32 >> i) + y, m);
+            }
+        memcpy(a, b, sizeof a);
+        if (n == 1) break;
+    }
+}
+
+int soc_oracle_generate_hiz(const soc_globals* g, soc_img depth, const soc_img* mips, int32_t mip_count, int32_t op_max) {
+    if (!g || !mips || mip_count <= 0 || mip_count > 12 || !valid(&depth)) return SOC_E_INVALID_ARG;
+    const int W = g->resolution[0], H = g->resolution[1];
+    const int dx = (W + 63) / 64, dy = (H + 63) / 64;
+    for (int gy = 0; gy < dy; ++gy)
+        for (int gx = 0; gx < dx; ++gx) hz_window(&depth, depth.width, depth.height, gx, gy, -1, 6, mips, mip_count, op_max);
+    if (mip_count > 5) hz_window(&mips[5], W >> 6, H >> 6, 0, 0, 5, mip_count - 6, mips, mip_count, op_max);
+    return SOC_OK;
+}

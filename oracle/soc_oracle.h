@@ -47,6 +47,7 @@ int soc_oracle_gbuffer_resolve(const soc_globals* g, const soc_mesh* mesh, const
                                soc_img emissive, soc_img normal, soc_img velocity);
 
 int soc_oracle_height_to_normal(soc_img heightmap, soc_img target);
+int soc_oracle_generate_hiz(const soc_globals* g, soc_img depth, const soc_img* mips, int32_t mip_count, int32_t op_max);
 
 /* Scalar helpers exposed for known-answer tests. */
 uint32_t soc_oracle_luminance_bin(float r, float g, float b, float log_min, float log_max);

@@ -194,6 +194,7 @@ FUNCTIONS = {
     "soc_raster_workspace_size": (C.c_size_t, [C.c_int32, C.c_int32]),
     "soc_renderer_set_raster_scene": (_I, [_P, C.POINTER(RasterScene)]),
     "soc_height_to_normal": (_I, [_IMG, _IMG, _P]),
+    "soc_generate_hiz": (_I, [_G, _IMG, C.POINTER(SocImg), C.c_int32, C.c_int32, _P, _P]),
     "soc_renderer_metrics_json": (C.c_int64, [_P, C.c_uint64, C.c_char_p, C.c_size_t]),
     "soc_read_image": (_I, [_IMG, _P, C.c_int32, _P]),
     "soc_write_png": (_I, [C.c_char_p, _P, C.c_int32, C.c_int32, C.c_int32]),

@@ -153,3 +153,18 @@ def scene_setup(g, scene_id: int, tex_size: int = 512, device="cuda") -> dict:
 def height_to_normal(heightmap, normal_target, stream=None):
     """HeightToNormalTask (height_to_normal.inl:52-83): (H, W, 4) uint8 heightmap -> (H, W, 4) f16 normals."""
     _check(lib().soc_height_to_normal(img(heightmap), img(normal_target), _stream(stream)), "height_to_normal")
+
+
+def hiz_mip_count(width: int, height: int) -> int:
+    """ceil(log2(max(W/2, H/2))) levels (generate_min_hiz.inl:36-37)."""
+    import math
+    return int(math.ceil(math.log2(max(width // 2, height // 2))))
+
+
+def generate_hiz(g, depth, mips, op_max=False, counter=None, stream=None):
+    """Min (or max) Hi-Z pyramid of a D32 depth into `mips` (list of (H/2>>i, W/2>>i) f32 tensors)."""
+    if counter is None:
+        counter = torch.zeros(1, dtype=torch.int32, device=depth.device)
+    arr = (_abi.SocImg * len(mips))(*[img(m) for m in mips])
+    _check(lib().soc_generate_hiz(_gp(g), img(depth), arr, len(mips), int(bool(op_max)), _ptr(counter), _stream(stream)),
+           "generate_hiz")
