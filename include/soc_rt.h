@@ -428,8 +428,10 @@ typedef struct soc_material {
     int32_t flags;                     /* SOC_MATERIAL_* */
     int32_t has_emissive;              /* 0: emissive = 0 (has_emissive_image) */
     int32_t pad[2];
+    soc_img normal_map;                /* RGBA16F, used with SOC_MATERIAL_NORMAL_MAP */
 } soc_material;
 #define SOC_MATERIAL_ZERO_VELOCITY 1   /* write velocity 0 (the terrain draw, draw_terrain.inl:221) */
+#define SOC_MATERIAL_NORMAL_MAP 2      /* normal = normalize(bilinear normal_map(uv).xyz) (draw_terrain.inl:206-219) */
 
 #define SOC_CULL_NONE 0
 #define SOC_CULL_FRONT 1               /* depth prepass / G-buffer (depth_prepass.inl:45) */

@@ -1233,11 +1233,17 @@ int soc_oracle_gbuffer_resolve(const soc_globals* g, const soc_mesh* mesh, const
             const v3 na = rs_normalize(mat3_mul_v3(n3, V3(nr[3 * ia], nr[3 * ia + 1], nr[3 * ia + 2])));
             const v3 nb = rs_normalize(mat3_mul_v3(n3, V3(nr[3 * ib], nr[3 * ib + 1], nr[3 * ib + 2])));
             const v3 nc = rs_normalize(mat3_mul_v3(n3, V3(nr[3 * ic], nr[3 * ic + 1], nr[3 * ic + 2])));
-            const v3 n = rs_normalize(V3(b0 * na.x + b1 * nb.x + b2 * nc.x, b0 * na.y + b1 * nb.y + b2 * nc.y,
-                                         b0 * na.z + b1 * nb.z + b2 * nc.z));
             uint32_t mi = mesh->materials ? mesh->materials[id] : 0u;
             if (mi > (uint32_t)(material_count - 1)) mi = (uint32_t)(material_count - 1);
             const soc_material* m = &materials[mi];
+            v3 n;
+            if ((m->flags & SOC_MATERIAL_NORMAL_MAP) && m->normal_map.data) {   /* draw_terrain.inl:206-219 */
+                v4 t = sample_clamp(&m->normal_map, u, v);
+                n = rs_normalize(V3(t.x, t.y, t.z));
+            } else {
+                n = rs_normalize(V3(b0 * na.x + b1 * nb.x + b2 * nc.x, b0 * na.y + b1 * nb.y + b2 * nc.y,
+                                    b0 * na.z + b1 * nb.z + b2 * nc.z));
+            }
             v3 em = V3(0, 0, 0);
             if (m->has_emissive) {
                 v4 e = rs_sample_texture(&m->emissive, u, v);

@@ -455,11 +455,18 @@ __global__ __launch_bounds__(256) void gbuffer_resolve(soc_mesh mesh, const soc_
     const float* uv = mesh.uvs;
     const float u = b0 * uv[2 * ia] + b1 * uv[2 * ib] + b2 * uv[2 * ic];
     const float v = b0 * uv[2 * ia + 1] + b1 * uv[2 * ib + 1] + b2 * uv[2 * ic + 1];
-    const float4 na = VA.n, nb = VB.n, nc = VC.n;
-    const f3 n = normalize_exact(f3{b0 * na.x + b1 * nb.x + b2 * nc.x, b0 * na.y + b1 * nb.y + b2 * nc.y,
-                                    b0 * na.z + b1 * nb.z + b2 * nc.z});
     const uint32_t mi = mesh.materials ? min(mesh.materials[id], (uint32_t)(p.material_count - 1)) : 0u;
     const soc_material& m = mats[mi];
+    f3 n;
+    if ((m.flags & SOC_MATERIAL_NORMAL_MAP) && m.normal_map.data) {   // draw_terrain.inl:206-219
+        const DImg nm{static_cast<char*>(m.normal_map.data), m.normal_map.width, m.normal_map.height, m.normal_map.pitch_bytes};
+        const f4 t = sample_h4(nm, u, v);
+        n = normalize_exact(f3{t.x, t.y, t.z});
+    } else {
+        const float4 na = VA.n, nb = VB.n, nc = VC.n;
+        n = normalize_exact(f3{b0 * na.x + b1 * nb.x + b2 * nc.x, b0 * na.y + b1 * nb.y + b2 * nc.y,
+                               b0 * na.z + b1 * nb.z + b2 * nc.z});
+    }
     f3 em = f3{0.0f, 0.0f, 0.0f};
     if (m.has_emissive) {
         const f4 e = sample_texture(m.emissive, u, v, lut);

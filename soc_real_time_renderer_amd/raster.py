@@ -16,7 +16,8 @@ import numpy as np
 import torch
 
 from . import _abi, _check, _gp, _ptr, _stream, img, lib
-from ._abi import CULL_BACK, CULL_FRONT, CULL_NONE, FMT_RGBA8_SRGB, MATERIAL_ZERO_VELOCITY, Material, Mesh
+from ._abi import (CULL_BACK, CULL_FRONT, CULL_NONE, FMT_RGBA8_SRGB, MATERIAL_NORMAL_MAP, MATERIAL_ZERO_VELOCITY,
+                   Material, Mesh)
 
 __all__ = ["CULL_NONE", "CULL_FRONT", "CULL_BACK", "MATERIAL_ZERO_VELOCITY", "MeshBuffers", "material",
            "normal_matrix", "materials_device", "raster_visibility", "raster_depth", "gbuffer_resolve",
@@ -82,7 +83,7 @@ class MeshBuffers:
 
 
 def material(albedo=None, emissive=None, albedo_factor=(1.0, 1.0, 1.0, 1.0), emissive_factor=(1.0, 1.0, 1.0, 1.0),
-             flags=0, has_emissive: Optional[bool] = None, srgb=True) -> Material:
+             flags=0, has_emissive: Optional[bool] = None, srgb=True, normal_map=None) -> Material:
     """soc_material: albedo / emissive RGBA8 textures ((H, W, 4) uint8 tensors or arrays; sRGB like the
     reference's baseColor/emissive images, model.cpp:52-71) or None (white / no emissive)."""
     m = Material()
@@ -93,6 +94,9 @@ def material(albedo=None, emissive=None, albedo_factor=(1.0, 1.0, 1.0, 1.0), emi
     m.emissive_factor[:] = [float(v) for v in emissive_factor]
     m.flags = int(flags)
     m.has_emissive = int(emissive is not None if has_emissive is None else has_emissive)
+    m.normal_map = img(normal_map) if normal_map is not None else img(None)
+    if normal_map is not None:
+        m.flags |= MATERIAL_NORMAL_MAP
     return m
 
 
@@ -143,11 +147,18 @@ def scene_setup(g, scene_id: int, tex_size: int = 512, device="cuda") -> dict:
     tex, em = _scene.material_textures(g, tex_size, scene_id)
     terrain = scene_id == _scene.TERRAIN
     dtex = [torch.from_numpy(tex[i]).to(device) for i in range(len(tex))]
+    nmap = None
+    if terrain:   # the terrain's normal map from its heightmap (HeightToNormalTask, renderer.cpp:158-190)
+        hm = torch.from_numpy(_scene.terrain_heightmap(tex_size)).to(device)
+        nmap = torch.empty((tex_size, tex_size, 4), dtype=torch.float16, device=device)
+        height_to_normal(hm, nmap)
     mats = [material(albedo=dtex[i], emissive_factor=tuple(float(v) for v in em[i]) + (1.0,),
-                     has_emissive=bool(em[i].any()), flags=MATERIAL_ZERO_VELOCITY if terrain else 0, srgb=not terrain)
+                     has_emissive=bool(em[i].any()), flags=MATERIAL_ZERO_VELOCITY if terrain else 0, srgb=not terrain,
+                     normal_map=nmap)
             for i in range(len(tex))]
-    return {"mesh": mesh, "textures": dtex, "materials": materials_device(mats, device), "material_count": len(mats),
-            "host_mesh": m, "host_textures": tex, "emissive": em, "workspace": mesh.workspace(device)}
+    return {"mesh": mesh, "textures": dtex, "normal_map": nmap, "materials": materials_device(mats, device),
+            "material_count": len(mats), "host_mesh": m, "host_textures": tex, "emissive": em,
+            "workspace": mesh.workspace(device)}
 
 
 def height_to_normal(heightmap, normal_target, stream=None):

@@ -119,11 +119,17 @@ def test_gbuffer_resolve(soc, oracle, scene_id, camera, W, H):
     tex, em = scene.material_textures(g, 128, scene_id)
     srgb = scene_id == scene.SPONZA_PROXY   # exercise both texture formats
     flags = raster.MATERIAL_ZERO_VELOCITY if scene_id == scene.TERRAIN else 0
+    hn = dn = None
+    if scene_id == scene.TERRAIN:   # draw_terrain.inl's normal = the heightmap's normal map texel
+        heights = scene.terrain_heightmap(128)
+        hn = np.zeros((128, 128, 4), np.float16)
+        oracle.height_to_normal(heights, hn)
+        dn = torch.from_numpy(hn).to(DEV)
     hmats = [raster.material(albedo=tex[i], emissive_factor=tuple(em[i]) + (1.0,), has_emissive=bool(em[i].any()),
-                             flags=flags, srgb=srgb) for i in range(len(tex))]
+                             flags=flags, srgb=srgb, normal_map=hn) for i in range(len(tex))]
     dtex = [torch.from_numpy(tex[i]).to(DEV) for i in range(len(tex))]
     dmats = [raster.material(albedo=dtex[i], emissive_factor=tuple(em[i]) + (1.0,), has_emissive=bool(em[i].any()),
-                             flags=flags, srgb=srgb) for i in range(len(tex))]
+                             flags=flags, srgb=srgb, normal_map=dn) for i in range(len(tex))]
     dmat = raster.materials_device(dmats)
     vis = np.zeros((H, W), np.uint64)
     oracle.raster_visibility(hm, vp, raster.CULL_FRONT, vis)
