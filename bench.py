@@ -220,7 +220,10 @@ def main():
     ns_bytes = algo[comp] + algo["SSAOGeneration"]
     ns_us = (comp_ms + ssao_ms) * 1e3
     pass_gbs = {n: round(algo[n] / (ms * 1e-3) / 1e9, 1) for n, _, ms, _ in stats if ms > 0 and n in algo}
-    traffic, traffic_src = pmc_traffic("composition_pair<true, false, 0>" if comp != "Composition" else "composition_pair<false, false, 3>", W, H)
+    # the committed PMC table comes from the default command (C3, G-buffer resident): other workloads get null
+    traffic, traffic_src = (pmc_traffic("composition_pair<true, false, 0>" if comp != "Composition"
+                                        else "composition_pair<false, false, 3>", W, H)
+                            if args.config == "c3" and not args.raster else (None, None))
 
     if world > 1:
         dist.barrier()
