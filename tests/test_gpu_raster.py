@@ -46,7 +46,8 @@ def soup_mesh(n, seed, big):
 @pytest.mark.parametrize("scene_id,camera,W,H", [(scene.TERRAIN, TERRAIN_CAMERA, 512, 288),
                                                  (scene.SPONZA_PROXY, SPONZA_CAMERA, 512, 288),
                                                  (scene.TERRAIN, TERRAIN_CAMERA, 1920, 1080),
-                                                 (scene.SPONZA_PROXY, SPONZA_CAMERA, 97, 55)])
+                                                 (scene.SPONZA_PROXY, SPONZA_CAMERA, 97, 55),
+                                                 (scene.SPONZA_PROXY, SPONZA_CAMERA, 3840, 2160)])
 @pytest.mark.parametrize("cull", [raster.CULL_FRONT, raster.CULL_NONE])
 def test_visibility_bit_exact(soc, oracle, scene_id, camera, W, H, cull):
     g = globals_for(W, H, camera=camera)
@@ -94,7 +95,8 @@ def test_visibility_accumulates_without_clear(soc, oracle):
     assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("scene_id,S", [(scene.TERRAIN, 1024), (scene.SPONZA_PROXY, 1024), (scene.TERRAIN, 2048)])
+@pytest.mark.parametrize("scene_id,S", [(scene.TERRAIN, 1024), (scene.SPONZA_PROXY, 1024), (scene.TERRAIN, 2048),
+                                        (scene.SPONZA_PROXY, 4096)])
 def test_shadow_depth_bit_exact(soc, oracle, scene_id, S):
     """The sun shadow map (SunShadowDrawTask: cull BACK, bias 1.25 / 1.75) is bit-exact."""
     g = globals_for(256, 144, camera=TERRAIN_CAMERA if scene_id == scene.TERRAIN else SPONZA_CAMERA)
