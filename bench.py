@@ -133,9 +133,12 @@ def main():
     args = ap.parse_args()
 
     rank, world, local_rank = multi_gpu.env()
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
-    multi_gpu.init(device)
+    # rehearsal of the N-rank path on a 1-GPU box: SOC_BENCH_SHARE_DEVICE=1 puts every rank on device 0
+    # and SOC_DIST_BACKEND=gloo replaces RCCL (which refuses two ranks on one device)
+    dev_index = 0 if os.environ.get("SOC_BENCH_SHARE_DEVICE") == "1" else local_rank
+    torch.cuda.set_device(dev_index)
+    device = torch.device("cuda", dev_index)
+    multi_gpu.init(device, backend=os.environ.get("SOC_DIST_BACKEND", "nccl"))
     W, H = args.width, args.height
 
     # ---- inputs (synthetic Sponza-proxy or terrain G-buffer + 4096^2 sun shadow map), resident in HBM ----
