@@ -47,7 +47,8 @@ inline Mat4 mat4(const float* m) {
 
 inline hipStream_t hs(soc_stream s) { return reinterpret_cast<hipStream_t>(s); }
 
-// Integer tuning knob from the environment (read once per name; `dflt` when unset).
+// Integer tuning knob from the environment (`dflt` when unset). Read at every launch (a getenv scan,
+// ~0.1 us), so A/B runs and the variant-identity tests can switch it between calls.
 int tuning_knob(const char* name, int dflt);
 
 // Checks the launch that was just issued.

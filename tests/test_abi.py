@@ -4,6 +4,7 @@ import ctypes as C
 import os
 import re
 
+import numpy as np
 import pytest
 
 from conftest import ROOT
@@ -81,3 +82,27 @@ def test_library_is_a_gfx950_code_object():
     data = open(so, "rb").read()
     assert b"gfx950" in data
     assert b"__hip_fatbin" in data or b"HIP_FATBIN" in data or b".hip_fatbin" in data
+
+
+def test_raster_and_output_argument_errors_without_gpu(soc):
+    """The raster / Hi-Z / height-to-normal / output entry points validate before any HIP call."""
+    from soc_real_time_renderer_amd import _abi
+    lib = soc.lib()
+    g = soc.globals_defaults(64, 36)
+    vp = (C.c_float * 16)()
+    bad = soc.SocImg(None, 0, 0, 0, 0)
+    E_ARG, E_SHAPE = _abi.SOC_E_INVALID_ARG, _abi.SOC_E_SHAPE
+    assert lib.soc_raster_visibility(None, vp, 1, None, 64, 36, 1, None, None) == E_ARG
+    mesh = _abi.Mesh()
+    assert lib.soc_raster_visibility(C.byref(mesh), vp, 1, None, 64, 36, 1, None, None) == E_ARG
+    assert b"soc_raster_visibility" in lib.soc_last_error_string()
+    assert lib.soc_raster_depth(C.byref(mesh), vp, 2, 1.25, 1.75, bad, None, None) == E_ARG
+    assert lib.soc_gbuffer_resolve(C.byref(g), C.byref(mesh), None, 1, None, bad, bad, bad, bad, bad, None, None) == E_ARG
+    assert lib.soc_generate_hiz(C.byref(g), bad, None, 13, 0, None, None) == E_ARG
+    h = np.zeros((8, 8, 4), np.uint8)
+    n = np.zeros((8, 4, 4), np.float16)
+    assert lib.soc_height_to_normal(soc.img(h), soc.img(n), None) == E_SHAPE
+    assert lib.soc_write_png(b"/tmp/x.png", None, 4, 4, 16) == E_ARG
+    assert lib.soc_read_image(bad, None, 0, None) == E_ARG
+    assert lib.soc_renderer_set_raster_scene(None, None) == E_ARG
+    assert lib.soc_raster_workspace_size(-1, 0) == 0
