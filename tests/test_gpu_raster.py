@@ -191,3 +191,55 @@ def test_render_graph_raster_head(soc, scene_id, camera):
     for k in outs[0]:
         assert torch.equal(outs[0][k], outs[1][k]), k
     assert (outs[0]["depth"] < 1.0).float().mean() > 0.3
+
+
+@pytest.mark.parametrize("scene_id,camera", [(scene.SPONZA_PROXY, SPONZA_CAMERA), (scene.TERRAIN, TERRAIN_CAMERA)])
+def test_end_to_end_frames_vs_oracle(soc, oracle, scene_id, camera):
+    """Whole frames from the mesh: the render graph with its raster head (GPU) against the oracle's raster,
+    G-buffer resolve, shadow map and full pass chain (CPU), 2 frames, the frame tolerances of
+    test_render_graph_frames."""
+    from helpers import host_frame
+    W, H, S = 480, 270, 1024
+    g = globals_for(W, H, camera=camera, elapsed=10.0)
+    sc = raster.scene_setup(g, scene_id, tex_size=128)
+    terrain = scene_id == scene.TERRAIN
+    hmesh = raster.MeshBuffers(*(sc["host_mesh"][k] for k in ("positions", "normals", "uvs", "indices", "materials")))
+    hn = None
+    if terrain:
+        hn = np.zeros((128, 128, 4), np.float16)
+        oracle.height_to_normal(scene.terrain_heightmap(128), hn)
+    em = sc["emissive"]
+    hmats = [raster.material(albedo=sc["host_textures"][i], emissive_factor=tuple(float(v) for v in em[i]) + (1.0,),
+                             has_emissive=bool(em[i].any()), flags=raster.MATERIAL_ZERO_VELOCITY if terrain else 0,
+                             srgb=not terrain, normal_map=hn) for i in range(sc["material_count"])]
+    fr = soc.alloc_frame(W, H, DEV)
+    fr["noise"].copy_(torch.from_numpy(scene.noise_texture()))
+    fr["shadow"] = torch.zeros((S, S), dtype=torch.float32, device=DEV)
+    vis = torch.zeros((H, W), dtype=torch.int64, device=DEV)
+    r = soc.Renderer(fr)
+    r.set_raster_scene(sc["mesh"], sc["materials"], sc["material_count"], vis, sc["workspace"], shadow=True)
+    gb0 = {k: np.zeros((H, W, 4), np.float16) for k in ("albedo", "emissive", "normal", "velocity")}
+    gb0["depth"] = np.zeros((H, W), np.float32)
+    gb0["shadow"] = np.zeros((S, S), np.float32)
+    gb0["noise"] = scene.noise_texture()
+    hf = host_frame(W, H, gb0)
+    ae = soc.AutoExposure()
+    hist = 0
+    hvis = np.zeros((H, W), np.uint64)
+    for f in range(2):
+        r.execute(g)
+        oracle.raster_visibility(hmesh, np.ctypeslib.as_array(g.camera_projection_view_matrix), raster.CULL_FRONT, hvis)
+        oracle.raster_depth(hmesh, np.ctypeslib.as_array(g.sun_info.projection_view_matrix), raster.CULL_BACK,
+                            hf["shadow"], raster.SHADOW_BIAS_CONSTANT, raster.SHADOW_BIAS_SLOPE)
+        oracle.gbuffer_resolve(g, hmesh, hmats, hvis, hf["depth"], hf["albedo"], hf["emissive"], hf["normal"],
+                               hf["velocity"])
+        hist = oracle.frame(g, hf, ae, hist=hist)
+        torch.cuda.synchronize()
+        assert np.array_equal(host(vis).view(np.uint64), hvis)
+        assert np.array_equal(host(fr["shadow"]), hf["shadow"])
+        ok = f16_close(host(fr["color"]), hf["color"], atol=4e-3, rtol=8e-3)
+        assert ok.mean() >= 0.999, (f, ok.mean())
+        d = np.abs(host(fr["output"]).astype(np.int32) - hf["output"].astype(np.int32))
+        assert (d <= 2).mean() >= 0.995, (f, (d <= 2).mean())
+        assert abs(soc.exposure_of(fr["auto_exposure"]) - ae.exposure) <= 1e-4
+    r.close()
