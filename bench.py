@@ -118,10 +118,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", choices=("c3", "c4"), default="c3",
-                    help="c3: Sponza-proxy full chain (the metric's config); c4: terrain + atmosphere/clouds")
-    ap.add_argument("--width", type=int, default=3840)
-    ap.add_argument("--height", type=int, default=2160)
+    ap.add_argument("--config", choices=("c2", "c3", "c4"), default="c3",
+                    help="c3: Sponza-proxy full chain at 4K (the metric's config); c2: the same scene at 1920x1080 "
+                         "(with --raster: deferred lighting + sun shadow map rendered per frame); c4: terrain + "
+                         "atmosphere/clouds")
+    ap.add_argument("--width", type=int, default=None, help="default 3840 (1920 for c2)")
+    ap.add_argument("--height", type=int, default=None, help="default 2160 (1080 for c2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-frames", type=int, default=20)
     ap.add_argument("--no-sky-lane", action="store_true", help="run CloudRendering on the frame stream too")
@@ -139,7 +141,8 @@ def main():
     torch.cuda.set_device(dev_index)
     device = torch.device("cuda", dev_index)
     multi_gpu.init(device, backend=os.environ.get("SOC_DIST_BACKEND", "nccl"))
-    W, H = args.width, args.height
+    W = args.width or (1920 if args.config == "c2" else 3840)
+    H = args.height or (1080 if args.config == "c2" else 2160)
 
     # ---- inputs (synthetic Sponza-proxy or terrain G-buffer + 4096^2 sun shadow map), resident in HBM ----
     terrain = args.config == "c4"
