@@ -99,11 +99,27 @@ __device__ __forceinline__ float aff(const Aff& a, float kx, float ky, float kz)
 // The bilinear depth tap follows the contract's clamp-to-edge / 8-bit sub-texel quantisation with t
 // clamped to [0, n-1-1/256] (right-edge taps keep 1/256 of the inner texel). This regroups the
 // reference's fp32 roundings; the result stays within the SSAO tolerance of DESIGN.md §5.
-template <bool TABLE, bool SPARSE_IP, bool FULL>
+// HALO > 0 (profiling variant, SOC_SSAO_HALO): the workgroup (32x8 outputs, 64x16 depth texels) stages
+// its depth tile plus HALO texels per side in LDS. Every tap reads both an LDS pair (clamped index) and a
+// buffer pair whose offset is pushed out of range for in-tile taps (the hardware returns 0 without a
+// memory access), then selects: branch-free, and the global gathers shrink to the out-of-tile lanes.
+template <bool TABLE, bool SPARSE_IP, bool FULL, int HALO = 0>
 __global__ __launch_bounds__(256) void ssao_kernel(DImg depth, DImg normal, DImg target, const float2* __restrict__ table,
                                                    SsaoParams p) {
+    constexpr int RW = 64 + 2 * HALO, RH = 16 + 2 * HALO;
+    __shared__ float tile[HALO ? RW * RH : 1];
     int bx, by;
     xcd_tile(p.swz, bx, by);
+    const int rx0 = bx * 64 - HALO, ry0 = by * 16 - HALO;
+    if (HALO) {
+        const int tid = threadIdx.y * 16 + threadIdx.x;
+        for (int i = tid; i < RW * RH; i += 256) {
+            const int ry = i / RW, rx = i - ry * RW;
+            const int gx = min(max(rx0 + rx, 0), depth.w - 1), gy = min(max(ry0 + ry, 0), depth.h - 1);
+            tile[i] = row_ptr<float>(depth, gy)[gx];
+        }
+        __syncthreads();
+    }
     int lx = threadIdx.x, ly = threadIdx.y;
     if (p.shape) {
         const int tid = threadIdx.y * 16 + threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -111,7 +127,7 @@ __global__ __launch_bounds__(256) void ssao_kernel(DImg depth, DImg normal, DImg
         else { lx = wave * 4 + (lane & 3); ly = lane >> 2; }
     }
     int x = bx * 16 + lx, y = by * 16 + ly;
-    if (p.shape == 3) {   // 32x8 tiles, waves of 32x2
+    if (HALO || p.shape == 3) {   // 32x8 tiles, waves of 32x2
         const int tid = threadIdx.y * 16 + threadIdx.x;
         x = bx * 32 + (tid & 31);
         y = by * 8 + (tid >> 5);
@@ -167,9 +183,22 @@ __global__ __launch_bounds__(256) void ssao_kernel(DImg depth, DImg normal, DImg
             const int fx = (int)__builtin_fmaf(tx, 256.0f, 0.5f);
             const int fy = (int)__builtin_fmaf(ty, 256.0f, 0.5f);
             const float wx = (float)(fx & 255) * (1.0f / 256.0f), wy = (float)(fy & 255) * (1.0f / 256.0f);
-            const int off = __mul24(fy >> 8, pitch) + (fx >> 8) * 4;
-            const f2a4 r0 = __builtin_bit_cast(f2a4, __builtin_amdgcn_raw_buffer_load_b64(rsrc, off, 0, 0));
-            const f2a4 r1 = __builtin_bit_cast(f2a4, __builtin_amdgcn_raw_buffer_load_b64(rsrc, off, pitch, 0));
+            int off = __mul24(fy >> 8, pitch) + (fx >> 8) * 4;
+            f2a4 r0, r1;
+            if (HALO) {
+                const int tlx = (fx >> 8) - rx0, tly = (fy >> 8) - ry0;
+                const bool in = (unsigned)tlx < (unsigned)(RW - 1) && (unsigned)tly < (unsigned)(RH - 1);
+                const int li = in ? tly * RW + tlx : 0;
+                const f2a4 l0 = f2a4{tile[li], tile[li + 1]}, l1 = f2a4{tile[li + RW], tile[li + RW + 1]};
+                off = in ? 0x7ffffff0 : off;   // out of range: no memory access, returns 0
+                const f2a4 g0 = __builtin_bit_cast(f2a4, __builtin_amdgcn_raw_buffer_load_b64(rsrc, off, 0, 0));
+                const f2a4 g1 = __builtin_bit_cast(f2a4, __builtin_amdgcn_raw_buffer_load_b64(rsrc, off, pitch, 0));
+                r0 = in ? l0 : g0;
+                r1 = in ? l1 : g1;
+            } else {
+                r0 = __builtin_bit_cast(f2a4, __builtin_amdgcn_raw_buffer_load_b64(rsrc, off, 0, 0));
+                r1 = __builtin_bit_cast(f2a4, __builtin_amdgcn_raw_buffer_load_b64(rsrc, off, pitch, 0));
+            }
             const float top = __builtin_fmaf(wx, r0.y - r0.x, r0.x);
             const float bot = __builtin_fmaf(wx, r1.y - r1.x, r1.x);
             const float dd = __builtin_fmaf(wy, bot - top, top);
@@ -272,7 +301,13 @@ extern "C" int soc_ssao_generation(const soc_globals* g, soc_img depth, soc_img 
     DImg dd = dimg(depth), dn = dimg(normal), dt = dimg(target);
 #define SOC_SSAO_LAUNCH(T, B, F) ssao_kernel<T, B, F><<<grd, blk, 0, st>>>(dd, dn, dt, tb, p)
     const bool full = p.ksize == SOC_SSAO_MAX_KERNEL;
-    if (noise_table && sip && full) SOC_SSAO_LAUNCH(true, true, true);
+    const int halo = tuning_knob("SOC_SSAO_HALO", 0);
+    if (halo && noise_table && sip && full) {
+        const dim3 g3(ceil_div(target.width, 32), ceil_div(target.height, 8));
+        if (halo == 8) ssao_kernel<true, true, true, 8><<<g3, blk, 0, st>>>(dd, dn, dt, tb, p);
+        else if (halo == 16) ssao_kernel<true, true, true, 16><<<g3, blk, 0, st>>>(dd, dn, dt, tb, p);
+        else ssao_kernel<true, true, true, 32><<<g3, blk, 0, st>>>(dd, dn, dt, tb, p);
+    } else if (noise_table && sip && full) SOC_SSAO_LAUNCH(true, true, true);
     else if (noise_table && sip) SOC_SSAO_LAUNCH(true, true, false);
     else if (noise_table) SOC_SSAO_LAUNCH(true, false, false);
     else if (sip && full) SOC_SSAO_LAUNCH(false, true, true);
