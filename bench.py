@@ -127,6 +127,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-frames", type=int, default=20)
     ap.add_argument("--no-sky-lane", action="store_true", help="run CloudRendering on the frame stream too")
+    ap.add_argument("--unfused-histogram", action="store_true",
+                    help="Composition and the luminance histogram as two launches (SOC_RENDERER_UNFUSED_HISTOGRAM)")
     ap.add_argument("--write-frame", default="", help="write the last frame's tone-mapped framebuffer (PNG)")
     ap.add_argument("--metrics-jsonl", default="", help="one GPU-metric JSON line per profiled frame")
     ap.add_argument("--raster", action="store_true",
@@ -157,7 +159,7 @@ def main():
         fr[k].copy_(torch.from_numpy(gb[k]))
     fr["shadow"].copy_(torch.from_numpy(shadow))
     fr["noise"].copy_(torch.from_numpy(noise))
-    r = soc.Renderer(fr, sky_lane=not args.no_sky_lane)
+    r = soc.Renderer(fr, sky_lane=not args.no_sky_lane, fused_histogram=not args.unfused_histogram)
     if args.raster:
         sc = raster.scene_setup(g, scene_id, tex_size=1024, device=device)
         vis = torch.empty((H, W), dtype=torch.int64, device=device)
@@ -227,7 +229,7 @@ def main():
     ns_us = (comp_ms + ssao_ms) * 1e3
     pass_gbs = {n: round(algo[n] / (ms * 1e-3) / 1e9, 1) for n, _, ms, _ in stats if ms > 0 and n in algo}
     # the committed PMC table comes from the default command (C3, G-buffer resident): other workloads get null
-    traffic, traffic_src = (pmc_traffic("composition_pair<true, false, 0>" if comp != "Composition"
+    traffic, traffic_src = (pmc_traffic("composition_pair<true, false, 3>" if comp != "Composition"
                                         else "composition_pair<false, false, 3>", W, H)
                             if args.config == "c3" and not args.raster else (None, None))
 

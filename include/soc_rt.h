@@ -365,8 +365,10 @@ typedef struct soc_renderer soc_renderer;
 #define SOC_RENDERER_UNFUSED_BLOOM 2  /* bloom downsweep as the reference's 4 passes, not 2 fused stages */
 #define SOC_RENDERER_SERIAL 4      /* every pass on the caller's stream (no concurrent sky lane) */
 #define SOC_RENDERER_UNFUSED_TONEMAP 8  /* TAA and tone mapping as two passes (default: one launch for RGBA8) */
-#define SOC_RENDERER_FUSED_HISTOGRAM 16  /* composition + luminance histogram in one launch */
+#define SOC_RENDERER_FUSED_HISTOGRAM 16  /* composition + luminance histogram in one launch (the default; kept
+                                            for callers that set it) */
 #define SOC_RENDERER_EXACT_BLOOM 32       /* bit-exact bloom chain instead of the weighted form (bloom_w.hip) */
+#define SOC_RENDERER_UNFUSED_HISTOGRAM 64 /* composition and luminance histogram as two passes */
 
 soc_renderer* soc_renderer_create(const soc_frame_images* images, uint32_t flags);
 void soc_renderer_destroy(soc_renderer* r);

@@ -322,7 +322,7 @@ class Renderer:
     """Host render graph (C++ soc_renderer): the live passes of Renderer::rebuild_task_graph in order."""
 
     def __init__(self, frame: dict, timing: bool = False, stream=None, fused_bloom: bool = True, sky_lane: bool = True,
-                 fused_tonemap: bool = True, fused_histogram: bool = False,
+                 fused_tonemap: bool = True, fused_histogram: bool = True,
                  exact_bloom: bool = False):
         self.frame = frame
         fi = FrameImages()
@@ -343,7 +343,7 @@ class Renderer:
         self._fi = fi
         flags = ((_abi.RENDERER_TIMING if timing else 0) | (0 if fused_bloom else _abi.RENDERER_UNFUSED_BLOOM)
                  | (0 if sky_lane else _abi.RENDERER_SERIAL) | (0 if fused_tonemap else _abi.RENDERER_UNFUSED_TONEMAP)
-                 | (_abi.RENDERER_FUSED_HISTOGRAM if fused_histogram else 0)
+                 | (0 if fused_histogram else _abi.RENDERER_UNFUSED_HISTOGRAM)
                  | (_abi.RENDERER_EXACT_BLOOM if exact_bloom else 0))
         h = lib().soc_renderer_create(C.byref(fi), flags)
         if not h:

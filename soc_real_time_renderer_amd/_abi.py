@@ -37,6 +37,7 @@ RENDERER_SERIAL = 4
 RENDERER_UNFUSED_TONEMAP = 8
 RENDERER_FUSED_HISTOGRAM = 16
 RENDERER_EXACT_BLOOM = 32
+RENDERER_UNFUSED_HISTOGRAM = 64
 HISTOGRAM_SCRATCH_WORDS = 2048
 
 Mat4 = C.c_float * 16

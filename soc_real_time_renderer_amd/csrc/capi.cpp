@@ -614,20 +614,26 @@ void build_passes_tail(soc_renderer* r) {
         return soc_cloud_rendering(g, r->img.depth, r->img.noise, r->img.clouds, r->img.clouds_workspace, (soc_stream)s);
     });
     r->passes.back().lane = 1;
-    // renderer.cpp:1103-1117 (composition) and 1155-1162 (histogram): two launches by default, one
-    // with SOC_RENDERER_FUSED_HISTOGRAM (trade-off measured in composition.hip)
-    if (r->flags & SOC_RENDERER_FUSED_HISTOGRAM) {
+    // renderer.cpp:1103-1117 (composition) and 1155-1162 (histogram): one launch by default (the colour
+    // is binned as it is written), two with SOC_RENDERER_UNFUSED_HISTOGRAM (measured in composition.hip)
+    if (!(r->flags & SOC_RENDERER_UNFUSED_HISTOGRAM)) {
         add("Composition+GenerateLuminanceHistogram", "Composition", SOC_PHASE_PRE_EXPOSURE,
             [r](const soc_globals* g, hipStream_t s) {
                 const auto& I = r->img;
                 const soc_img& em = I.bloom_output.data ? I.bloom_output : I.emissive;
                 int rc = ensure_hist_scratch(r);
                 if (rc) return rc;
-                return soc_composition_luminance_histogram(g, I.d_globals, I.color, I.albedo, em, I.normal, I.depth,
-                                                           I.ssao_blur, I.shadow, I.clouds, I.auto_exposure, r->hist_scratch,
-                                                           (soc_stream)s);
+                return soc::composition_luminance_histogram(g, I.d_globals, I.color, I.albedo, em, I.normal, I.depth,
+                                                            I.ssao_blur, I.shadow, I.clouds, I.auto_exposure,
+                                                            r->hist_scratch, false, (soc_stream)s);
             });
         r->passes.back().join = true;
+        // the 8 partial histograms of the fused launch into the AutoExposure bins (its own pass, so the
+        // Composition pass times the composition kernel alone)
+        add("LuminanceHistogramFold", "Auto Exposure", SOC_PHASE_PRE_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
+            (void)g;
+            return soc::histogram_fold_launch(r->hist_scratch, r->img.auto_exposure, (soc_stream)s);
+        });
     } else {
         add("Composition", "Composition", SOC_PHASE_PRE_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
             const auto& I = r->img;

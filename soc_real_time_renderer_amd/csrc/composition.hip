@@ -29,6 +29,7 @@ struct CompParams {
     int swz;   // XCD-aware tile order (fast path)
     uint32_t* bins;        // fused histogram: 8 x 256 scratch copies (composition_pair<true>)
     float lmin, lrange;    // log_min_luminance, log_max - log_min
+    BinFast bf;            // lum_bin_fast parameters
     const soc_globals* __restrict__ dg;  // device globals (lights), may be null when npl == nsl == 0
 };
 
@@ -115,15 +116,16 @@ constexpr int BX = 64, BY = 4;
 
 // Fast path: all full-res images share the target extent, width even, rows 16-B aligned.
 // HIST: GenerateLuminanceHistogramTask fused in (generate_luminance_histogram.inl:59-78): the bins of the
-// two stored RGBA16F pixels (the exact values the histogram pass would read back) are added per wave
-// into an LDS histogram (wave_bin_pair), which the workgroup flushes with one device atomic per
+// two stored RGBA16F pixels (the exact values the histogram pass would read back; lum_bin_fast with the
+// exact fallback) are added per wave into the wave's LDS histogram (wave_bin_pair), which the workgroup flushes with one device atomic per
 // non-zero bin (~3.6 distinct bins per 32x16 tile at 4K), saving the 8 B/px re-read of the colour.
 // The flush goes to one of 8 scratch copies chosen by linear block id mod 8 (the XCD under round-robin
 // dispatch): a single copy serialises the ~5k atomics of the hottest bin (measured 172 us vs 77 us),
 // 8 copies cut that 8x. histogram_fold adds the copies into the AutoExposure bins and re-zeroes them.
-// Measured at 4K: 94 us + a 4 us fold against 77 + 33 us for the two passes. The render graph keeps
-// the two passes by default (SOC_RENDERER_FUSED_HISTOGRAM opts in): the ~12 us (1.5 % of the frame)
-// costs the composition stream its HBM rate (4.4 -> 3.6 TB/s), the north-star measure.
+// Measured at 4K (kernel trace): 68.4 us + a 4 us fold against 66-68 + 27.7 us for the two passes; frame
+// 0.679 -> 0.660 ms. The render graph fuses by default (SOC_RENDERER_UNFUSED_HISTOGRAM: two passes).
+// (An in-kernel fold by the last-arriving workgroup instead of the fold launch costs one same-address
+// device atomic per workgroup: 16,200 of them serialise across the XCDs, 68 -> 207 us.)
 // LIGHTS = false: no point / spot lights this frame (the reference default): the light loops are not
 // compiled in, which keeps the kernel at a fraction of the registers (more waves, more loads in flight).
 template <bool HIST, bool LIGHTS, int NT = 0>
@@ -132,12 +134,11 @@ __global__ __launch_bounds__(256) void composition_pair(DImg target, DImg albedo
     // a wave covers 16x8 pixels (8 lanes x 2 pixels per row, 8 rows): every row segment is one
     // 128-B line of each G-buffer image, and the wave's shadow-map taps form a compact 2D patch
     // (a 128x1 strip maps to a line across the 4096^2 map and touches a new line per tap)
-    __shared__ uint32_t sh[HIST ? kBins : 1];
+    // HIST: one 256-bin LDS histogram per wave, zeroed by its own wave (LDS operations of a wave are
+    // ordered), so no barrier stands in front of the G-buffer loads
+    __shared__ uint32_t sh[HIST ? 4 * kBins : 1];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (HIST) {
-        sh[threadIdx.x] = 0u;
-        __syncthreads();
-    }
+    if (HIST) reinterpret_cast<uint4*>(sh + wave * kBins)[lane] = uint4{0u, 0u, 0u, 0u};
     int bx, by;
     xcd_tile(p.swz, bx, by);
     const int x = bx * 32 + (wave & 1) * 16 + (lane & 7) * 2;
@@ -186,11 +187,13 @@ __global__ __launch_bounds__(256) void composition_pair(DImg target, DImg albedo
     }
     if (HIST) {
         const f4 c0 = unpack_h4(outp[0]), c1 = unpack_h4(outp[1]);
-        const uint32_t b0 = lum_bin(c0.x, c0.y, c0.z, p.lmin, p.lrange);
-        const uint32_t b1 = lum_bin(c1.x, c1.y, c1.z, p.lmin, p.lrange);
-        wave_bin_pair(sh, b0, b1, inside);
+        uint32_t b0 = lum_bin_fast(c0.x, c0.y, c0.z, p.bf);
+        uint32_t b1 = lum_bin_fast(c1.x, c1.y, c1.z, p.bf);
+        if (b0 == kBinExact) b0 = lum_bin(c0.x, c0.y, c0.z, p.lmin, p.lrange);
+        if (b1 == kBinExact) b1 = lum_bin(c1.x, c1.y, c1.z, p.lmin, p.lrange);
+        wave_bin_pair(sh + wave * kBins, b0, b1, inside);
         __syncthreads();
-        const uint32_t n = sh[threadIdx.x];
+        const uint32_t n = sh[threadIdx.x] + sh[kBins + threadIdx.x] + sh[2 * kBins + threadIdx.x] + sh[3 * kBins + threadIdx.x];
         if (n) atomicAdd(&p.bins[((blockIdx.y * gridDim.x + blockIdx.x) & 7u) * kBins + threadIdx.x], n);
     }
 }
@@ -239,7 +242,7 @@ namespace {
 // (returns 1 otherwise, having launched nothing)
 int composition_launch(const soc_globals* g, const soc_globals* d_globals, soc_img target, soc_img albedo, soc_img emissive,
                        soc_img normal, soc_img depth, soc_img ssao, soc_img shadow, soc_img clouds, uint32_t* bins,
-                       uint32_t* scratch, soc_stream stream) {
+                       uint32_t* scratch, soc_stream stream, bool fold = true) {
     static const char* P = "soc_composition";
     if (!g) return set_error(SOC_E_INVALID_ARG, "%s: null globals", P);
     int rc = check_img(target, SOC_FMT_RGBA16F, P, "target");
@@ -292,9 +295,13 @@ int composition_launch(const soc_globals* g, const soc_globals* d_globals, soc_i
             p.bins = scratch;
             p.lmin = g->log_min_luminance;
             p.lrange = g->log_max_luminance - g->log_min_luminance;
+            p.bf = bin_fast_params(p.lmin, p.lrange);
             if (lights) SOC_COMP_PAIR(true, true);
+            else if (tuning_knob("SOC_COMP_NT", 3) == 3)
+                composition_pair<true, false, 3><<<grd, 256, 0, hs(stream)>>>(dimg(target), dimg(albedo), dimg(emissive),
+                    dimg(normal), dimg(depth), dimg(ssao), dimg(shadow), dimg(clouds), p);
             else SOC_COMP_PAIR(true, false);
-            histogram_fold<<<1, kBins, 0, hs(stream)>>>(scratch, bins);
+            if (fold) histogram_fold<<<1, kBins, 0, hs(stream)>>>(scratch, bins);
         } else if (tuning_knob("SOC_COMP_NT", 3) == 3 && !lights) {
             // non-temporal G-buffer loads and colour store (measured at 4K: 71.5 -> 68 us; TAA, the next
             // reader of depth, +3 us: the frame is unchanged). SOC_COMP_NT=0: default cache policy.
@@ -321,18 +328,32 @@ extern "C" int soc_composition(const soc_globals* g, const soc_globals* d_global
                               stream);
 }
 
-extern "C" int soc_composition_luminance_histogram(const soc_globals* g, const soc_globals* d_globals, soc_img target,
-                                                   soc_img albedo, soc_img emissive, soc_img normal, soc_img depth,
-                                                   soc_img ssao, soc_img shadow, soc_img clouds, soc_auto_exposure* ae,
-                                                   uint32_t* scratch, soc_stream stream) {
+int soc::composition_luminance_histogram(const soc_globals* g, const soc_globals* d_globals, soc_img target,
+                                         soc_img albedo, soc_img emissive, soc_img normal, soc_img depth, soc_img ssao,
+                                         soc_img shadow, soc_img clouds, soc_auto_exposure* ae, uint32_t* scratch,
+                                         bool fold, soc_stream stream) {
     if (!g || !ae || !scratch)
         return set_error(SOC_E_INVALID_ARG, "soc_composition_luminance_histogram: null globals / auto exposure / scratch");
     int rc = composition_launch(g, d_globals, target, albedo, emissive, normal, depth, ssao, shadow, clouds,
-                                ae->histogram_buckets, scratch, stream);
+                                ae->histogram_buckets, scratch, stream, fold);
     if (rc <= 0) return rc;   // launched (or failed validation)
     // not fusable: the two passes back to back (same results)
     rc = composition_launch(g, d_globals, target, albedo, emissive, normal, depth, ssao, shadow, clouds, nullptr, nullptr,
                             stream);
     if (rc) return rc;
     return soc_generate_luminance_histogram(g, target, ae, stream);
+}
+
+int soc::histogram_fold_launch(uint32_t* scratch, soc_auto_exposure* ae, soc_stream stream) {
+    if (!scratch || !ae) return set_error(SOC_E_INVALID_ARG, "histogram fold: null scratch / auto exposure");
+    histogram_fold<<<1, kBins, 0, hs(stream)>>>(scratch, ae->histogram_buckets);
+    return check_launch("luminance_histogram_fold");
+}
+
+extern "C" int soc_composition_luminance_histogram(const soc_globals* g, const soc_globals* d_globals, soc_img target,
+                                                   soc_img albedo, soc_img emissive, soc_img normal, soc_img depth,
+                                                   soc_img ssao, soc_img shadow, soc_img clouds, soc_auto_exposure* ae,
+                                                   uint32_t* scratch, soc_stream stream) {
+    return composition_luminance_histogram(g, d_globals, target, albedo, emissive, normal, depth, ssao, shadow, clouds, ae,
+                                           scratch, true, stream);
 }

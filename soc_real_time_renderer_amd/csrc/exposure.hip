@@ -7,7 +7,8 @@
 // (neighbouring pixels usually share a bin) before one LDS atomic per run into its wave's private
 // 256-bin copy; the block then folds the 4 copies and issues one device atomic per NON-ZERO bin.
 // The bin function is the bit-exact contract of DESIGN.md §3.4 (explicit-FMA luminance and remap,
-// deterministic log2), identical to the oracle's.
+// deterministic log2), identical to the oracle's; the fast path evaluates it with the hardware log2 and
+// falls back to the exact form for pixels near a bin boundary (lum_bin_fast, luminance.hpp).
 #include <type_traits>
 #include <algorithm>
 
@@ -23,7 +24,7 @@ constexpr int kThreads = 256, kWaves = kThreads / 64, kPix = 8;
 
 // Fast path: W % 8 == 0, rows 16-B aligned. One "chunk" = 8 consecutive pixels of a row.
 __global__ __launch_bounds__(kThreads) void histogram_chunks(DImg hdr, int W, int H, float lmin, float lrange,
-                                                             uint32_t* __restrict__ bins) {
+                                                             BinFast bf, uint32_t* __restrict__ bins) {
     __shared__ uint32_t sh[kWaves][kBins];
     const int tid = threadIdx.x, wave = tid >> 6;
     for (int i = tid; i < kWaves * kBins; i += kThreads) (&sh[0][0])[i] = 0u;
@@ -46,13 +47,35 @@ __global__ __launch_bounds__(kThreads) void histogram_chunks(DImg hdr, int W, in
 #pragma unroll
         for (int k = 0; k < kPix / 2; ++k) q[k] = nxt[k];
         if (c + stride < total) fetch(c + stride, nxt);
-        uint32_t cur = 0xffffffffu, run = 0;
+        // fast bins (hardware log2) for the 8 pixels, then lum_bin for the few near a bin boundary
+        uint32_t bq[kPix], need = 0;
 #pragma unroll
         for (int k = 0; k < kPix / 2; ++k) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const f4 c4 = unpack_h4(h ? uint2{q[k].z, q[k].w} : uint2{q[k].x, q[k].y});
-                const uint32_t b = lum_bin(c4.x, c4.y, c4.z, lmin, lrange);
+                bq[2 * k + h] = lum_bin_fast(c4.x, c4.y, c4.z, bf);
+                need |= (bq[2 * k + h] == kBinExact ? 1u : 0u) << (2 * k + h);
+            }
+        }
+        if (need) {
+#pragma unroll
+            for (int k = 0; k < kPix / 2; ++k) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    if ((need >> (2 * k + h)) & 1u) {
+                        const f4 c4 = unpack_h4(h ? uint2{q[k].z, q[k].w} : uint2{q[k].x, q[k].y});
+                        bq[2 * k + h] = lum_bin(c4.x, c4.y, c4.z, lmin, lrange);
+                    }
+                }
+            }
+        }
+        uint32_t cur = 0xffffffffu, run = 0;
+#pragma unroll
+        for (int k = 0; k < kPix / 2; ++k) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const uint32_t b = bq[2 * k + h];
                 if (b == cur) {
                     ++run;
                 } else {
@@ -152,7 +175,7 @@ extern "C" int soc_generate_luminance_histogram(const soc_globals* g, soc_img hd
     if (grid < 1) grid = 1;
     uint32_t* bins = ae->histogram_buckets;
     if (chunks)
-        histogram_chunks<<<grid, kThreads, 0, hs(stream)>>>(dimg(hdr), W, H, lmin, lrange, bins);
+        histogram_chunks<<<grid, kThreads, 0, hs(stream)>>>(dimg(hdr), W, H, lmin, lrange, bin_fast_params(lmin, lrange), bins);
     else
         histogram_pixels<<<grid, kThreads, 0, hs(stream)>>>(dimg(hdr), W, H, lmin, lrange, bins);
     return check_launch("generate_luminance_histogram");

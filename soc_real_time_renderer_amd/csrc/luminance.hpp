@@ -5,12 +5,15 @@
 // histogram pass (composition.hip).
 #pragma once
 
+#include <cmath>
+
 #include "../../include/soc_rt.h"
 #include "soc_device.hpp"
 
 namespace soc {
 
 constexpr int kBins = SOC_AUTO_EXPOSURE_BIN_COUNT;
+
 
 __device__ __forceinline__ float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
 __device__ __forceinline__ uint32_t f2u(float f) { return __builtin_bit_cast(uint32_t, f); }
@@ -49,6 +52,47 @@ __device__ __forceinline__ uint32_t lum_bin(float r, float g, float b, float lmi
     if (mapped >= 255.0f) return 255u;
     if (mapped > 0.0f) return (uint32_t)(int32_t)mapped;
     return 0u;
+}
+
+// Fast bin with an exact fallback. lum_bin spends most of its ~70 VALU ops in det_log2's two IEEE
+// divisions and polynomial; the bin only depends on which integer interval `mapped` falls in. The fast
+// form uses the hardware log2 (v_log_f32) and a reciprocal multiply; over the luminances that reach it
+// (finite, >= 1e-3, < 2^17 from RGBA16F inputs, so |log2| < 17) it differs from lum_bin's `mapped` by
+// at most |dlog2| * 254/|lrange| + the rounding of the remap: |dlog2| <= a few ulp(16) ~ 5e-6 (both
+// log2 forms are within 2-3 ulp of the true value). BinFast::eps is that bound with a 6x margin
+// (host: bin_fast_params). A `mapped` farther than eps from every bin boundary (the integers 1..255)
+// truncates to the same bin in both forms; anything closer, and any non-finite value, returns
+// kBinExact and the caller recomputes that pixel with lum_bin, so the result is lum_bin's bit for bit.
+// With the reference's range (|lrange| = 30) eps = 3.5e-4: ~0.07 % of pixels take the exact path.
+struct BinFast {
+    float lmin, rlr, eps;   // log_min, 1 / (log_max - log_min), fallback margin in `mapped` units
+    uint32_t zero;          // lum_bin of a luminance < 1e-3 (log2(0) = -inf through the remap)
+};
+constexpr uint32_t kBinExact = 0xffffffffu;
+
+// Host: the BinFast parameters of a frame. `zero` follows lum_bin for lum = 0 (det_log2(0) = -inf,
+// then the same IEEE remap and clamp).
+inline BinFast bin_fast_params(float lmin, float lrange) {
+    BinFast f;
+    f.lmin = lmin;
+    f.rlr = 1.0f / lrange;
+    f.eps = 3.0e-5f * ((float)(kBins - 1) - 1.0f) / std::fabs(lrange) + 1.0e-4f;
+    if (!(f.eps < 0.25f)) f.eps = 0.25f;   // degenerate range (or NaN): the `> eps` test sends nearly all to lum_bin
+    const float q = (-INFINITY - lmin) / lrange;
+    const float mapped = std::fmaf(q, (float)(kBins - 1) - 1.0f, 1.0f);
+    f.zero = mapped >= 255.0f ? 255u : (mapped > 0.0f ? (uint32_t)(int32_t)mapped : 0u);
+    return f;
+}
+
+__device__ __forceinline__ uint32_t lum_bin_fast(float r, float g, float b, const BinFast& f) {
+#pragma clang fp contract(off)
+    const float lum = __builtin_fmaf(b, 0.0722f, __builtin_fmaf(g, 0.7152f, r * 0.2126f));   // as lum_bin
+    if (lum < 1e-3f) return f.zero;
+    const float mapped = __builtin_fmaf((__builtin_amdgcn_logf(lum) - f.lmin) * f.rlr, (float)(kBins - 1) - 1.0f, 1.0f);
+    if (mapped < 1.0f - f.eps) return 0u;
+    if (mapped >= 255.0f + f.eps) return 255u;
+    if (!(__builtin_fabsf(mapped - __builtin_rintf(mapped)) > f.eps)) return kBinExact;   // near a boundary, or NaN
+    return (uint32_t)(int32_t)mapped;
 }
 
 // Adds the bins of two pixels per lane into an LDS histogram with one LDS atomic per distinct bin of

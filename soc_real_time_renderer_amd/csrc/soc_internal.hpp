@@ -67,4 +67,11 @@ int launch_bloom_fused(const soc_img& emissive, const soc_img* mips, const soc_i
 // Weighted-form bloom chain (bloom_w.hip): same applicability as the fused chain.
 int launch_bloom_weighted(const soc_img& emissive, const soc_img* mips, const soc_img& output, hipStream_t s, int stage);
 
+// soc_composition_luminance_histogram with the fold of the 8 partial histograms optionally left to a
+// separate histogram_fold_launch (the render graph times the fold as a pass of its own).
+int composition_luminance_histogram(const soc_globals* g, const soc_globals* d_globals, soc_img target, soc_img albedo,
+                                    soc_img emissive, soc_img normal, soc_img depth, soc_img ssao, soc_img shadow,
+                                    soc_img clouds, soc_auto_exposure* ae, uint32_t* scratch, bool fold, soc_stream stream);
+int histogram_fold_launch(uint32_t* scratch, soc_auto_exposure* ae, soc_stream stream);
+
 }  // namespace soc

@@ -322,6 +322,46 @@ def test_histogram_bit_exact(soc, oracle, W, H):
     assert np.array_equal(got, ref)
 
 
+def _boundary_colours(g, n, rng):
+    """RGBA16F colours whose luminance maps within ~1e-3 of a bin boundary (the integers 1..255 of the
+    remap of generate_luminance_histogram.inl:64-69), half of them within the fast path's fallback margin:
+    the pixels where lum_bin_fast must hand over to the exact lum_bin."""
+    lmin, lmax = float(g.log_min_luminance), float(g.log_max_luminance)
+    out = []
+    while sum(len(o) for o in out) < n:
+        k = rng.integers(1, 256, 200_000)
+        t = (k - 1 + rng.uniform(-2e-3, 2e-3, k.size)) / 254.0       # target mapped - 1, over 254
+        lum = np.exp2(lmin + t * (lmax - lmin))
+        ok = (lum > 1.5e-3) & (lum < 6.0e4)
+        w = rng.dirichlet((1.0, 1.0, 1.0), k.size)[ok]               # random channel split of the luminance
+        lum = lum[ok]
+        rgb = w * (lum / (w @ np.array([0.2126, 0.7152, 0.0722])))[:, None]
+        rgb = rgb[(rgb < 6.0e4).all(axis=1)].astype(np.float16).astype(np.float64)
+        m = 1.0 + 254.0 * (np.log2(np.maximum(rgb @ np.array([0.2126, 0.7152, 0.0722]), 1e-30)) - lmin) / (lmax - lmin)
+        keep = np.abs(m - np.rint(m)) < 1e-3
+        out.append(rgb[keep])
+    rgb = np.concatenate(out)[:n]
+    return np.concatenate([rgb, np.ones((n, 1))], axis=1).astype(np.float16)
+
+
+@pytest.mark.parametrize("W,H", [(512, 256), (1920, 1080)])
+def test_histogram_bin_boundaries_bit_exact(soc, oracle, W, H):
+    """Every pixel near a bin boundary (the fast bin's exact fallback), mixed with ordinary pixels."""
+    g = globals_for(W, H)
+    rng = np.random.default_rng(H)
+    img = np.exp(rng.normal(-1.0, 3.0, (H, W, 4))).astype(np.float16)
+    sel = rng.uniform(size=(H, W)) < 0.5
+    img[sel] = _boundary_colours(g, int(sel.sum()), rng)
+    ae = soc.AutoExposure()
+    oracle.generate_luminance_histogram(g, img, ae)
+    ref = np.array(ae.histogram_buckets, np.int64)
+    buf = soc.auto_exposure_buffer()
+    soc.generate_luminance_histogram(g, dev(img), buf)
+    got = host(buf)[1:].astype(np.int64)
+    assert got.sum() == W * H
+    assert np.array_equal(got, ref)
+
+
 @pytest.mark.parametrize("wide", [False, True])
 def test_resolve(soc, oracle, wide):
     g = globals_for(640, 360)
