@@ -223,13 +223,28 @@ struct TmOut {
     TmParams p;
 };
 
-template <bool TM>
+// Lane i's left neighbour column (x0 - 1) is lane i-1's second pixel and its right one (x0 + 2) lane
+// i+1's first: with NBR the neighbourhood's side columns come from the adjacent lanes through DPP wave
+// shifts (VALU) instead of two more colour and two more depth loads per row, and only the lanes at a
+// block-row edge (threadIdx.x == 0 / blockDim.x - 1) or at the image border load them. The texture path
+// is the bound of this kernel (TA / TD ~83 % busy, profiles/r01_l1_counters.json).
+__device__ __forceinline__ uint32_t from_left(uint32_t v) {   // lane i <- lane i-1 (wave_shr:1)
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t from_right(uint32_t v) {  // lane i <- lane i+1 (wave_shl:1)
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, false);
+}
+
+template <bool TM, bool NBR = true>
 __global__ __launch_bounds__(256) void taa_pair2(DImg target, DImg cur, DImg prev, DImg vel, DImg pvel, DImg depth,
                                                  DImg vel_out, TaaParams p, TmOut tm) {
     int tbx, tby;
     xcd_tile(p.swz, tbx, tby);
     const int x0 = (tbx * (int)blockDim.x + threadIdx.x) * 2, y = tby * (int)blockDim.y + threadIdx.y;
-    if (x0 >= target.w || y >= target.h) return;
+    // NBR: every lane stays for the lane shifts (the grid covers whole rows of lanes; W is even, so a lane
+    // is either wholly inside or wholly outside the image)
+    if ((!NBR && x0 >= target.w) || y >= target.h) return;
+    const bool inside_x = x0 < target.w;
     const float exposure = TM ? tm.ae->exposure : 0.0f;
     const int W = target.w, H = target.h;
     const int xl = max(x0 - 1, 0), xr = min(x0 + 2, W - 1);
@@ -243,9 +258,24 @@ __global__ __launch_bounds__(256) void taa_pair2(DImg target, DImg cur, DImg pre
         rows[r] = sy;
         const uint2* crow = row_ptr<uint2>(cur, sy);
         const float* drow = row_ptr<float>(depth, sy);
-        const uint4 mid = *reinterpret_cast<const uint4*>(crow + x0);
-        const float2 dmid = *reinterpret_cast<const float2*>(drow + x0);
-        const uint2 L = crow[xl], R = crow[xr];
+        const int xm = NBR ? min(x0, W - 2) : x0;
+        const uint4 mid = *reinterpret_cast<const uint4*>(crow + xm);
+        const float2 dmid = *reinterpret_cast<const float2*>(drow + xm);
+        uint2 L, R;
+        float dl, dr;
+        if (NBR) {
+            L = uint2{from_left(mid.z), from_left(mid.w)};
+            R = uint2{from_right(mid.x), from_right(mid.y)};
+            dl = __builtin_bit_cast(float, from_left(__builtin_bit_cast(uint32_t, dmid.y)));
+            dr = __builtin_bit_cast(float, from_right(__builtin_bit_cast(uint32_t, dmid.x)));
+            if (threadIdx.x == 0) { L = crow[xl]; dl = drow[xl]; }
+            if (threadIdx.x == blockDim.x - 1 || x0 + 2 >= W) { R = crow[xr]; dr = drow[xr]; }
+        } else {
+            L = crow[xl];
+            R = crow[xr];
+            dl = drow[xl];
+            dr = drow[xr];
+        }
         Cxy[r][0] = as_h2(L.x);
         Czw[r][0] = as_h2(L.y);
         Cxy[r][1] = as_h2(mid.x);
@@ -254,11 +284,12 @@ __global__ __launch_bounds__(256) void taa_pair2(DImg target, DImg cur, DImg pre
         Czw[r][2] = as_h2(mid.w);
         Cxy[r][3] = as_h2(R.x);
         Czw[r][3] = as_h2(R.y);
-        D[r][0] = drow[xl];
+        D[r][0] = dl;
         D[r][1] = dmid.x;
         D[r][2] = dmid.y;
-        D[r][3] = drow[xr];
+        D[r][3] = dr;
     }
+    if (NBR && !inside_x) return;   // past the image: only fed its neighbours' shifts
     // column min / max (packed f16) and Gaussian column sums (fp32)
     h2 nxy[4], nzw[4], xxy[4], xzw[4];
     v2f sxy[4], szw[4];
@@ -426,7 +457,10 @@ int taa_launch(const soc_globals* g, soc_img target, soc_img current_color, soc_
         // 32 x 8 lanes (64 x 8 pixels): the 3-row neighbourhood reloads 10 rows per 8 instead of 6 per 4
         const int by = tuning_knob("SOC_TAA_BY", 8), bxl = 256 / by;
         dim3 blk(bxl, by), g2(ceil_div(W / 2, bxl), ceil_div(H, by));
-        if (tm)
+        if (tm && tuning_knob("SOC_TAA_NBR", 1) == 0)   // side columns loaded by every lane (A/B, identity test)
+            taa_pair2<true, false><<<g2, blk, 0, hs(stream)>>>(dimg(target), dimg(current_color), dimg(previous_color),
+                                                       dimg(current_velocity), dimg(previous_velocity), dimg(depth), vo, p, *tm);
+        else if (tm)
             taa_pair2<true><<<g2, blk, 0, hs(stream)>>>(dimg(target), dimg(current_color), dimg(previous_color),
                                                        dimg(current_velocity), dimg(previous_velocity), dimg(depth), vo, p, *tm);
         else

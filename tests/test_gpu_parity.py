@@ -397,6 +397,34 @@ def test_taa(soc, oracle, W, H):
     assert np.array_equal(host(vout).view(np.uint16), gb["velocity"].view(np.uint16))
 
 
+@pytest.mark.parametrize("W,H", [(100, 40), (1920, 1080)])
+def test_taa_lane_shift_neighbours_identical(soc, oracle, monkeypatch, W, H):
+    """Side columns of the 3x3 neighbourhood from the adjacent lanes (DPP wave shifts, default) give the
+    bits of the per-lane loads (SOC_TAA_NBR=0). 100 px: the second block row of 32 lanes has 18 lanes
+    inside the image and 14 past it."""
+    g, gb = sponza_inputs(W, H)
+    cur = dev(random_rgba16(H, W, seed=3, hi=3.0))
+    prev = dev(random_rgba16(H, W, seed=4, hi=3.0))
+    pvel = gb["velocity"].copy()
+    pvel[..., :2] += np.float16(0.0015)
+    vel, pvel, depth = dev(gb["velocity"]), dev(pvel), dev(gb["depth"])
+    ae = soc.auto_exposure_buffer(exposure=0.37)
+    outs = []
+    for nbr in ("1", "0"):
+        monkeypatch.setenv("SOC_TAA_NBR", nbr)
+        t = torch.zeros(H, W, 4, dtype=torch.float16, device=DEV)
+        o = torch.zeros(H, W, 4, dtype=torch.uint8, device=DEV)
+        soc.temporal_antialiasing_tone_mapping(g, t, cur, prev, vel, pvel, depth, ae, o)
+        outs.append((t, o))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+    ref = np.zeros((H, W, 4), np.float16)
+    oracle.temporal_antialiasing(g, ref, host(cur), host(prev), gb["velocity"], host(pvel), gb["depth"])
+    ok = f16_close(host(outs[0][0]), ref)
+    assert ok.all(), ok.mean()
+
+
 @pytest.mark.parametrize("W,H", [(64, 36), (97, 55), (1920, 1080)])
 def test_taa_tone_mapping_fused_equals_two_passes(soc, W, H):
     """The fused TAA + tone-map launch gives the TAA pass's bits and the tone-map pass's bits (97x55:
