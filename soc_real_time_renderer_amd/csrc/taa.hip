@@ -235,16 +235,21 @@ __device__ __forceinline__ uint32_t from_right(uint32_t v) {  // lane i <- lane 
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, false);
 }
 
-template <bool TM, bool NBR = true>
+// NBR = 2 (default): 64-lane block rows whose first and last lanes only load the halo pairs for their
+// neighbours (62 output pairs per wave), so no lane issues a side-column load at all: the kernel is bound
+// by texture-path instructions, not bytes.
+template <bool TM, int NBR = 2>
 __global__ __launch_bounds__(256) void taa_pair2(DImg target, DImg cur, DImg prev, DImg vel, DImg pvel, DImg depth,
                                                  DImg vel_out, TaaParams p, TmOut tm) {
     int tbx, tby;
     xcd_tile(p.swz, tbx, tby);
-    const int x0 = (tbx * (int)blockDim.x + threadIdx.x) * 2, y = tby * (int)blockDim.y + threadIdx.y;
+    const int x0 = NBR == 2 ? (tbx * 62 + (int)threadIdx.x - 1) * 2 : (tbx * (int)blockDim.x + threadIdx.x) * 2;
+    const int y = tby * (int)blockDim.y + threadIdx.y;
+    const bool halo = NBR == 2 && (threadIdx.x == 0 || threadIdx.x == 63);
     // NBR: every lane stays for the lane shifts (the grid covers whole rows of lanes; W is even, so a lane
     // is either wholly inside or wholly outside the image)
     if ((!NBR && x0 >= target.w) || y >= target.h) return;
-    const bool inside_x = x0 < target.w;
+    const bool inside_x = !halo && x0 < target.w;
     const float exposure = TM ? tm.ae->exposure : 0.0f;
     const int W = target.w, H = target.h;
     const int xl = max(x0 - 1, 0), xr = min(x0 + 2, W - 1);
@@ -258,7 +263,7 @@ __global__ __launch_bounds__(256) void taa_pair2(DImg target, DImg cur, DImg pre
         rows[r] = sy;
         const uint2* crow = row_ptr<uint2>(cur, sy);
         const float* drow = row_ptr<float>(depth, sy);
-        const int xm = NBR ? min(x0, W - 2) : x0;
+        const int xm = NBR ? min(max(x0, 0), W - 2) : x0;
         const uint4 mid = *reinterpret_cast<const uint4*>(crow + xm);
         const float2 dmid = *reinterpret_cast<const float2*>(drow + xm);
         uint2 L, R;
@@ -268,8 +273,13 @@ __global__ __launch_bounds__(256) void taa_pair2(DImg target, DImg cur, DImg pre
             R = uint2{from_right(mid.x), from_right(mid.y)};
             dl = __builtin_bit_cast(float, from_left(__builtin_bit_cast(uint32_t, dmid.y)));
             dr = __builtin_bit_cast(float, from_right(__builtin_bit_cast(uint32_t, dmid.x)));
-            if (threadIdx.x == 0) { L = crow[xl]; dl = drow[xl]; }
-            if (threadIdx.x == blockDim.x - 1 || x0 + 2 >= W) { R = crow[xr]; dr = drow[xr]; }
+            if (NBR == 2) {   // image borders: the clamped side column is the pair's own pixel
+                if (x0 == 0) { L = uint2{mid.x, mid.y}; dl = dmid.x; }
+                if (x0 + 2 >= W) { R = uint2{mid.z, mid.w}; dr = dmid.y; }
+            } else {
+                if (threadIdx.x == 0) { L = crow[xl]; dl = drow[xl]; }
+                if (threadIdx.x == blockDim.x - 1 || x0 + 2 >= W) { R = crow[xr]; dr = drow[xr]; }
+            }
         } else {
             L = crow[xl];
             R = crow[xr];
@@ -457,14 +467,20 @@ int taa_launch(const soc_globals* g, soc_img target, soc_img current_color, soc_
         // 32 x 8 lanes (64 x 8 pixels): the 3-row neighbourhood reloads 10 rows per 8 instead of 6 per 4
         const int by = tuning_knob("SOC_TAA_BY", 8), bxl = 256 / by;
         dim3 blk(bxl, by), g2(ceil_div(W / 2, bxl), ceil_div(H, by));
-        if (tm && tuning_knob("SOC_TAA_NBR", 1) == 0)   // side columns loaded by every lane (A/B, identity test)
-            taa_pair2<true, false><<<g2, blk, 0, hs(stream)>>>(dimg(target), dimg(current_color), dimg(previous_color),
+        // side columns: 2 = halo lanes (default), 1 = lane shifts + edge-lane loads, 0 = every lane loads them
+        const int nbr = tuning_knob("SOC_TAA_NBR", 2);
+        const dim3 blk_h(64, 4), g2_h(ceil_div(W / 2, 62), ceil_div(H, 4));
+        if (tm && nbr == 2)
+            taa_pair2<true, 2><<<g2_h, blk_h, 0, hs(stream)>>>(dimg(target), dimg(current_color), dimg(previous_color),
+                                                       dimg(current_velocity), dimg(previous_velocity), dimg(depth), vo, p, *tm);
+        else if (tm && nbr == 0)
+            taa_pair2<true, 0><<<g2, blk, 0, hs(stream)>>>(dimg(target), dimg(current_color), dimg(previous_color),
                                                        dimg(current_velocity), dimg(previous_velocity), dimg(depth), vo, p, *tm);
         else if (tm)
-            taa_pair2<true><<<g2, blk, 0, hs(stream)>>>(dimg(target), dimg(current_color), dimg(previous_color),
+            taa_pair2<true, 1><<<g2, blk, 0, hs(stream)>>>(dimg(target), dimg(current_color), dimg(previous_color),
                                                        dimg(current_velocity), dimg(previous_velocity), dimg(depth), vo, p, *tm);
         else
-            taa_pair2<false><<<g2, blk, 0, hs(stream)>>>(dimg(target), dimg(current_color), dimg(previous_color),
+            taa_pair2<false, 2><<<g2_h, blk_h, 0, hs(stream)>>>(dimg(target), dimg(current_color), dimg(previous_color),
                                                         dimg(current_velocity), dimg(previous_velocity), dimg(depth), vo, p,
                                                         TmOut{});
     } else if (fast)

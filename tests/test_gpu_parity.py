@@ -399,9 +399,10 @@ def test_taa(soc, oracle, W, H):
 
 @pytest.mark.parametrize("W,H", [(100, 40), (1920, 1080)])
 def test_taa_lane_shift_neighbours_identical(soc, oracle, monkeypatch, W, H):
-    """Side columns of the 3x3 neighbourhood from the adjacent lanes (DPP wave shifts, default) give the
-    bits of the per-lane loads (SOC_TAA_NBR=0). 100 px: the second block row of 32 lanes has 18 lanes
-    inside the image and 14 past it."""
+    """Side columns of the 3x3 neighbourhood from the adjacent lanes (DPP wave shifts) give the bits of
+    the per-lane loads (SOC_TAA_NBR=0): with halo-only first / last lanes (2, default) and with edge-lane
+    loads (1). 100 px: 50 pairs in a 62-pair wave row (12 lanes past the image), 32-lane block rows of
+    which the second has 18 lanes inside; 1920 px: 15.5 wave rows."""
     g, gb = sponza_inputs(W, H)
     cur = dev(random_rgba16(H, W, seed=3, hi=3.0))
     prev = dev(random_rgba16(H, W, seed=4, hi=3.0))
@@ -410,15 +411,16 @@ def test_taa_lane_shift_neighbours_identical(soc, oracle, monkeypatch, W, H):
     vel, pvel, depth = dev(gb["velocity"]), dev(pvel), dev(gb["depth"])
     ae = soc.auto_exposure_buffer(exposure=0.37)
     outs = []
-    for nbr in ("1", "0"):
+    for nbr in ("2", "1", "0"):
         monkeypatch.setenv("SOC_TAA_NBR", nbr)
         t = torch.zeros(H, W, 4, dtype=torch.float16, device=DEV)
         o = torch.zeros(H, W, 4, dtype=torch.uint8, device=DEV)
         soc.temporal_antialiasing_tone_mapping(g, t, cur, prev, vel, pvel, depth, ae, o)
         outs.append((t, o))
     torch.cuda.synchronize()
-    assert torch.equal(outs[0][0], outs[1][0])
-    assert torch.equal(outs[0][1], outs[1][1])
+    for t, o in outs[1:]:
+        assert torch.equal(outs[0][0], t)
+        assert torch.equal(outs[0][1], o)
     ref = np.zeros((H, W, 4), np.float16)
     oracle.temporal_antialiasing(g, ref, host(cur), host(prev), gb["velocity"], host(pvel), gb["depth"])
     ok = f16_close(host(outs[0][0]), ref)
