@@ -497,6 +497,8 @@ struct soc_renderer {
     hipEvent_t fork_ev = nullptr, join_ev = nullptr;
     // 8 partial luminance histograms of the fused composition + histogram pass (renderer-owned, 8 KiB)
     uint32_t* hist_scratch = nullptr;
+    // this execute call runs both phases: the resolve folds the partial histograms itself (no fold launch)
+    bool fold_in_resolve = false;
 };
 
 namespace {
@@ -630,8 +632,11 @@ void build_passes_tail(soc_renderer* r) {
         r->passes.back().join = true;
         // the 8 partial histograms of the fused launch into the AutoExposure bins (its own pass, so the
         // Composition pass times the composition kernel alone)
+        // Before a multi-GPU exchange (PRE and POST in separate calls) the fold must precede it; in a one-call
+        // frame the resolve does it instead and this pass launches nothing.
         add("LuminanceHistogramFold", "Auto Exposure", SOC_PHASE_PRE_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
             (void)g;
+            if (r->fold_in_resolve) return (int)SOC_OK;
             return soc::histogram_fold_launch(r->hist_scratch, r->img.auto_exposure, (soc_stream)s);
         });
     } else {
@@ -647,7 +652,8 @@ void build_passes_tail(soc_renderer* r) {
         });
     }
     add("ResolveLuminanceHistogram", "Auto Exposure", SOC_PHASE_POST_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
-        return soc_resolve_luminance_histogram(g, r->img.auto_exposure, r->total_pixels, r->wide, (soc_stream)s);
+        return soc::resolve_luminance_histogram(g, r->img.auto_exposure, r->total_pixels, r->wide,
+                                                r->fold_in_resolve ? r->hist_scratch : nullptr, (soc_stream)s);
     });
     // renderer.cpp:1170-1198: TAA + both history copies (ping-pong + fused velocity history), and
     // renderer.cpp:1210-1217: tone mapping, fused into the TAA launch for an RGBA8_UNORM framebuffer
@@ -773,6 +779,7 @@ static int ensure_side_lane(soc_renderer* r) {
 extern "C" int soc_renderer_execute(soc_renderer* r, const soc_globals* g, int32_t phase, soc_stream stream) {
     if (!r || !g) return set_error(SOC_E_INVALID_ARG, "soc_renderer_execute: null argument");
     hipStream_t s = hs(stream);
+    r->fold_in_resolve = (phase & SOC_PHASE_ALL) == SOC_PHASE_ALL && !(r->flags & SOC_RENDERER_UNFUSED_HISTOGRAM);
     if ((phase & SOC_PHASE_PRE_EXPOSURE) && (g->point_light_count || g->spot_light_count)) {
         int rc = upload_lights(r, g, s);
         if (rc) return rc;

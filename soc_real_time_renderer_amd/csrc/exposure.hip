@@ -115,13 +115,23 @@ __global__ __launch_bounds__(kThreads) void histogram_pixels(DImg hdr, int W, in
 
 // resolve_luminance_histogram.inl:56-80, one workgroup of 256 lanes (quirk Q9: the reference's extra
 // 255 workgroups only index out of bounds).
+// scratch != null: the 8 partial histograms of the fused composition pass are folded in here (u32 adds,
+// the same bins histogram_fold would leave) and re-zeroed, saving that launch in a single-GPU frame.
 template <bool WIDE>
 __global__ __launch_bounds__(kBins) void resolve_kernel(soc_auto_exposure* __restrict__ ae, float pixels, float lmin,
-                                                        float lmax, float target_lum, float dt, float speed) {
+                                                        float lmax, float target_lum, float dt, float speed,
+                                                        uint32_t* __restrict__ scratch) {
     typedef typename std::conditional<WIDE, unsigned long long, uint32_t>::type acc_t;
     __shared__ acc_t sh[kBins];
     const uint32_t i = threadIdx.x;
-    const uint32_t count = ae->histogram_buckets[i];
+    uint32_t count = ae->histogram_buckets[i];
+    if (scratch) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            count += scratch[k * kBins + i];
+            scratch[k * kBins + i] = 0u;
+        }
+    }
     sh[i] = (acc_t)count * (acc_t)i;
     ae->histogram_buckets[i] = 0u;
     __syncthreads();
@@ -181,16 +191,21 @@ extern "C" int soc_generate_luminance_histogram(const soc_globals* g, soc_img hd
     return check_launch("generate_luminance_histogram");
 }
 
-extern "C" int soc_resolve_luminance_histogram(const soc_globals* g, soc_auto_exposure* ae, uint64_t total_pixels,
-                                               int32_t wide_accumulator, soc_stream stream) {
+int soc::resolve_luminance_histogram(const soc_globals* g, soc_auto_exposure* ae, uint64_t total_pixels,
+                                     int32_t wide_accumulator, uint32_t* scratch, soc_stream stream) {
     if (!g || !ae) return set_error(SOC_E_INVALID_ARG, "soc_resolve_luminance_histogram: null argument");
     float pixels = total_pixels ? (float)total_pixels
                                 : (float)(int32_t)((uint32_t)g->resolution[0] * (uint32_t)g->resolution[1]);
     if (wide_accumulator)
         resolve_kernel<true><<<1, kBins, 0, hs(stream)>>>(ae, pixels, g->log_min_luminance, g->log_max_luminance,
-                                                          g->target_luminance, g->delta_time, g->adjustment_speed);
+                                                          g->target_luminance, g->delta_time, g->adjustment_speed, scratch);
     else
         resolve_kernel<false><<<1, kBins, 0, hs(stream)>>>(ae, pixels, g->log_min_luminance, g->log_max_luminance,
-                                                           g->target_luminance, g->delta_time, g->adjustment_speed);
+                                                           g->target_luminance, g->delta_time, g->adjustment_speed, scratch);
     return check_launch("resolve_luminance_histogram");
+}
+
+extern "C" int soc_resolve_luminance_histogram(const soc_globals* g, soc_auto_exposure* ae, uint64_t total_pixels,
+                                               int32_t wide_accumulator, soc_stream stream) {
+    return resolve_luminance_histogram(g, ae, total_pixels, wide_accumulator, nullptr, stream);
 }

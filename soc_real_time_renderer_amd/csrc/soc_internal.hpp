@@ -73,5 +73,8 @@ int composition_luminance_histogram(const soc_globals* g, const soc_globals* d_g
                                     soc_img emissive, soc_img normal, soc_img depth, soc_img ssao, soc_img shadow,
                                     soc_img clouds, soc_auto_exposure* ae, uint32_t* scratch, bool fold, soc_stream stream);
 int histogram_fold_launch(uint32_t* scratch, soc_auto_exposure* ae, soc_stream stream);
+// soc_resolve_luminance_histogram that first folds the 8 partial histograms (null: none).
+int resolve_luminance_histogram(const soc_globals* g, soc_auto_exposure* ae, uint64_t total_pixels, int32_t wide_accumulator,
+                                uint32_t* scratch, soc_stream stream);
 
 }  // namespace soc

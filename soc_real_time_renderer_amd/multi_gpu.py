@@ -75,8 +75,12 @@ def max_over_ranks(x: float, device=None) -> float:
 
 
 def render_frame(renderer, g, bins: torch.Tensor, group=None) -> None:
-    """One frame of the sharded path: PRE phase, histogram exchange, POST phase (all on the frame stream)."""
-    from . import PHASE_POST_EXPOSURE, PHASE_PRE_EXPOSURE
+    """One frame of the sharded path: PRE phase, histogram exchange, POST phase (all on the frame stream).
+    Without peers the frame is one call (the resolve then folds the fused pass's partial histograms)."""
+    from . import PHASE_ALL, PHASE_POST_EXPOSURE, PHASE_PRE_EXPOSURE
+    if not (dist.is_initialized() and dist.get_world_size(group) > 1):
+        renderer.execute(g, PHASE_ALL)
+        return
     renderer.execute(g, PHASE_PRE_EXPOSURE)
     exchange_histogram(bins, group)
     renderer.execute(g, PHASE_POST_EXPOSURE)
