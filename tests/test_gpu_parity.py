@@ -594,3 +594,31 @@ def test_render_graph_sky_lane_bit_identical(soc):
         r.close()
     for k in outs[0]:
         assert torch.equal(outs[0][k], outs[1][k]), k
+
+
+def test_render_graph_split_phases_bit_identical(soc):
+    """A multi-GPU frame runs PRE and POST in separate calls (the fused pass's partial histograms folded by
+    the LuminanceHistogramFold launch before the exchange); a one-call frame folds them in the resolve.
+    Without an exchange both give the same bits, over 3 frames, and leave the scratch zeroed."""
+    W, H = 1920, 1080
+    g, gb = sponza_inputs(W, H, elapsed=10.0)
+    outs = []
+    for split in (False, True):
+        fr = soc.alloc_frame(W, H, DEV, bloom_output=True)
+        for k in ("albedo", "emissive", "normal", "velocity", "depth"):
+            fr[k].copy_(torch.from_numpy(gb[k]))
+        fr["shadow"] = dev(gb["shadow"])
+        fr["noise"].copy_(torch.from_numpy(gb["noise"]))
+        r = soc.Renderer(fr)
+        for _ in range(3):
+            if split:
+                r.execute(g, soc.PHASE_PRE_EXPOSURE)
+                r.execute(g, soc.PHASE_POST_EXPOSURE)
+            else:
+                r.execute(g)
+        torch.cuda.synchronize()
+        outs.append({k: fr[k].clone() for k in ("color", "output", "auto_exposure")})
+        r.close()
+    for k in outs[0]:
+        assert torch.equal(outs[0][k], outs[1][k]), k
+    assert int(outs[0]["auto_exposure"][1:].abs().sum()) == 0   # bins consumed by the resolve
