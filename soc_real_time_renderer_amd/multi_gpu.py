@@ -74,13 +74,36 @@ def max_over_ranks(x: float, device=None) -> float:
     return float(t.item())
 
 
-def render_frame(renderer, g, bins: torch.Tensor, group=None) -> None:
+def render_frame(renderer, g, bins: torch.Tensor, group=None, exchange_events=None) -> None:
     """One frame of the sharded path: PRE phase, histogram exchange, POST phase (all on the frame stream).
-    Without peers the frame is one call (the resolve then folds the fused pass's partial histograms)."""
+    Without peers the frame is one call (the resolve then folds the fused pass's partial histograms).
+    `exchange_events` = (start, end) CUDA events recorded on the current stream around the exchange."""
     from . import PHASE_ALL, PHASE_POST_EXPOSURE, PHASE_PRE_EXPOSURE
     if not (dist.is_initialized() and dist.get_world_size(group) > 1):
         renderer.execute(g, PHASE_ALL)
         return
     renderer.execute(g, PHASE_PRE_EXPOSURE)
+    if exchange_events is not None:
+        exchange_events[0].record()
     exchange_histogram(bins, group)
+    if exchange_events is not None:
+        exchange_events[1].record()
     renderer.execute(g, PHASE_POST_EXPOSURE)
+
+
+def rank_inventory(device) -> dict:
+    """What this rank runs on: the device the collective backend sees (index, name, PCI bus id)."""
+    props = torch.cuda.get_device_properties(device)
+    bus = getattr(props, "pci_bus_id", None)
+    return {"device_index": device.index, "name": props.name,
+            "pci": (f"{getattr(props, 'pci_domain_id', 0):04x}:{bus:02x}:{getattr(props, 'pci_device_id', 0):02x}"
+                    if bus is not None else None)}
+
+
+def gather_objects(obj):
+    """all_gather_object over the world (a list of one object without peers)."""
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return [obj]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out

@@ -1,0 +1,87 @@
+"""Frame-per-GPU path with a real peer, on the GPU.
+
+Two ranks (torch.distributed.run, gloo, both on device 0) each render their own camera through the HIP
+render graph: PRE_EXPOSURE -> histogram all-reduce -> POST_EXPOSURE (wide resolve over 2*W*H pixels).
+Checks, per frame:
+  * each rank's local bins are the oracle's histogram of that rank's own GPU colour image (bit-exact);
+  * the exchanged bins are the sum of the local ones on every rank;
+  * every rank's exposure equals the oracle's wide resolve of the summed bins (|d| <= 1e-5), frame after
+    frame (the exposure carries over: resolve_luminance_histogram.inl:75-79).
+And `bench.py --gpus 2` (self-launching its ranks) prints one line with n_gpus == 2.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _env(**kw):
+    env = dict(os.environ)
+    env.update(SOC_BENCH_SHARE_DEVICE="1", SOC_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0",
+               OMP_NUM_THREADS="2", **kw)
+    return env
+
+
+def test_two_rank_frames_exchange_vs_oracle(tmp_path, soc, oracle):
+    from helpers import globals_for
+    from soc_real_time_renderer_amd import multi_gpu
+    out = tmp_path / "dist.npz"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "tests", "dist_frame_worker.py")]
+    p = subprocess.run(cmd, env=_env(SOC_DIST_OUT=str(out)), capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    d = np.load(out)
+    world, W, H = int(d["world"]), int(d["W"]), int(d["H"])
+    assert world == 2
+    local, reduced, exposure, color = d["local"], d["reduced"], d["exposure"], d["color"]
+    frames = local.shape[1]
+    g = globals_for(W, H, elapsed=10.0, frame_counter=2)
+    ae = soc.AutoExposure()   # exposure 0 at start, like the renderer's buffer
+    for f in range(frames):
+        for r in range(world):
+            ref = soc.AutoExposure()
+            oracle.generate_luminance_histogram(g, color[r, f], ref)
+            assert np.array_equal(np.array(ref.histogram_buckets, np.uint32), local[r, f]), (r, f)
+            assert int(local[r, f].astype(np.int64).sum()) == W * H
+        summed = local[:, f].astype(np.uint64).sum(axis=0)
+        for r in range(world):
+            assert np.array_equal(reduced[r, f].astype(np.uint64), summed), (r, f)
+        ae.histogram_buckets[:] = [int(v) for v in summed]
+        total, wide = multi_gpu.exposure_pixels(world, W, H)
+        oracle.resolve_luminance_histogram(g, ae, total, wide)
+        for r in range(world):
+            assert abs(float(exposure[r, f]) - ae.exposure) <= 1e-5, (r, f, float(exposure[r, f]), ae.exposure)
+        assert exposure[0, f] == exposure[1, f]
+    # the two ranks rendered different cameras
+    assert not np.array_equal(local[0, 0], local[1, 0])
+
+
+def test_bench_gpus2_self_launch():
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "1",
+           "--width", "320", "--height", "180", "--no-cpu-baseline", "--profile-frames", "2"]
+    p = subprocess.run(cmd, env=_env(), capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2
+    assert out["config"]["histogram_allreduce"] is True
+    assert [x["rank"] for x in out["ranks"]] == [0, 1]
+    assert out["allreduce_us_per_frame"] is not None and out["allreduce_us_per_frame"] > 0
+    assert out["value"] > 0
