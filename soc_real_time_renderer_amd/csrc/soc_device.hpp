@@ -182,6 +182,25 @@ __device__ __forceinline__ void xcd_tile(int swz, int& tx, int& ty) {
     tx = id - ty * gx;
 }
 
+// XCD-aware order with a compact footprint. The tiles are enumerated band by band (8 horizontal bands
+// of ceil(gy / 8) tile rows), each band in column strips of `strip` tiles, each strip row by row; XCD k
+// (workgroup id mod 8) takes the k-th contiguous eighth of that sequence. The workgroups in flight on
+// one XCD then cover a near-square region, so its L2 holds their gather footprint. A bijection.
+__device__ __forceinline__ void xcd_tile_strips(int strip, int& tx, int& ty) {
+    const int gx = (int)gridDim.x, gy = (int)gridDim.y, n = gx * gy;
+    const int id = (int)(blockIdx.y * gridDim.x + blockIdx.x);
+    const int q = n >> 3, r = n & 7, k = id & 7;
+    const int i = k * q + min(k, r) + (id >> 3);   // position in the band/strip sequence
+    const int B = (gy + 7) >> 3;
+    const int band = i / (B * gx), off = i - band * B * gx;
+    const int rows = min(B, gy - band * B);
+    const int s = off / (strip * rows), in = off - s * strip * rows;
+    const int w = min(strip, gx - s * strip);
+    const int ly = in / w;
+    tx = s * strip + (in - ly * w);
+    ty = band * B + ly;
+}
+
 // Pixel-centre uv exactly as the oracle computes it: (x + 0.5) / n, correctly rounded.
 __device__ __forceinline__ float centre_uv(int x, int n) { return ((float)x + 0.5f) / (float)n; }
 

@@ -109,7 +109,8 @@ __global__ __launch_bounds__(256) void ssao_kernel(DImg depth, DImg normal, DImg
     constexpr int RW = 64 + 2 * HALO, RH = 16 + 2 * HALO;
     __shared__ float tile[HALO ? RW * RH : 1];
     int bx, by;
-    xcd_tile(p.swz, bx, by);
+    if (p.swz >= 2) xcd_tile_strips(p.swz, bx, by);   // SOC_SWZ_SSAO >= 2: strip width in tiles
+    else xcd_tile(p.swz, bx, by);
     const int rx0 = bx * 64 - HALO, ry0 = by * 16 - HALO;
     if (HALO) {
         const int tid = threadIdx.y * 16 + threadIdx.x;
