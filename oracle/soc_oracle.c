@@ -4,7 +4,8 @@
  * TEST INFRASTRUCTURE ONLY: used by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
  * leg, never by the product path. Parity vs the reference itself is UNPINNED (the Vulkan/Daxa
  * reference cannot run here and holds no golden vectors); this file is pinned by
- * hand-derived known-answer tests and by an independent numpy restatement (tools/np_oracle.py).
+ * hand-derived known-answer tests and cross-checked against a second, independent restatement of
+ * the GLSL in numpy (oracle/np_oracle.py, float64, textbook filter) by tests/test_np_oracle.py.
  *
  * Every pass follows the GLSL of the reference line by line; the file:line of each restated shader
  * is cited at the function. Numerics: IEEE fp32, compiled with -ffp-contract=off (no implicit FMA),

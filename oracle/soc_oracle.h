@@ -8,8 +8,8 @@
  * Parity status: the reference (Vulkan/GLSL via Daxa) cannot be built or run here
  * and ships no tests, golden vectors or fixtures. The restatement is therefore
  * pinned by hand-derived known-answer tests of the reference formulas (tests/test_oracle_kat.py)
- * and by an independent numpy restatement (tools/np_oracle.py) — "parity unpinned" against a run
- * of the reference itself.
+ * and cross-checked against an independent numpy restatement of the GLSL (oracle/np_oracle.py,
+ * tests/test_np_oracle.py) — "parity unpinned" against a run of the reference itself.
  *
  * Functions take the same arguments as the C ABI in include/soc_rt.h, with HOST pointers.
  */
