@@ -397,6 +397,57 @@ int32_t soc_renderer_current_history(const soc_renderer* r);
  * Composition, so it overlaps bloom and SSAO. Results are identical either way. */
 int soc_renderer_set_async(soc_renderer* r, int32_t enable);
 
+/* --- Pass declaration (the Daxa task-uses block + TaskGraph::add_task, e.g. composition.inl:10-21 and
+ * renderer.cpp:1103-1117) ------------------------------------------------------------------------
+ * Every pass of the graph, built-in or added, declares the frame resources it reads and writes. The graph
+ * keeps the registration order (the reference executes tasks in add_task order) and derives from the
+ * declared uses what Daxa derives barriers from: each pass's dependencies (read-after-write,
+ * write-after-read, write-after-write on the latest earlier user of a resource) and the placement of
+ * SOC_PASS_ASYNC passes on the renderer's second lane: such a pass waits only for the passes it depends
+ * on, and a later pass on the caller's stream waits for it only if it depends on it. */
+enum soc_resource {
+    SOC_RES_ALBEDO = 0, SOC_RES_EMISSIVE, SOC_RES_NORMAL, SOC_RES_DEPTH, SOC_RES_VELOCITY,
+    SOC_RES_SUN_SHADOW, SOC_RES_NOISE,
+    SOC_RES_BLOOM_MIP0, SOC_RES_BLOOM_MIP1, SOC_RES_BLOOM_MIP2, SOC_RES_BLOOM_MIP3,
+    SOC_RES_BLOOM_OUTPUT,        /* images.bloom_output (aliases EMISSIVE when that image is absent) */
+    SOC_RES_SSAO, SOC_RES_SSAO_BLUR, SOC_RES_CLOUDS, SOC_RES_COLOR,
+    SOC_RES_PREVIOUS_COLOR, SOC_RES_RESOLVED,          /* TAA history pair, renderer.cpp:1170-1198 */
+    SOC_RES_PREVIOUS_VELOCITY,
+    SOC_RES_AUTO_EXPOSURE,       /* AutoExposure buffer (histogram bins + exposure) */
+    SOC_RES_OUTPUT,              /* tone-mapped framebuffer (the reference's swapchain image) */
+    SOC_RES_VISIBILITY,          /* raster visibility buffer (raster head) */
+    SOC_RES_HISTOGRAM_PARTIALS,  /* the fused composition + histogram pass's partial bins */
+    SOC_RES_USER0 = 32,          /* SOC_RES_USER0 .. SOC_RES_USER0 + 31: caller-defined resources */
+    SOC_RES_COUNT = 64
+};
+#define SOC_PASS_MAX_USES 16
+#define SOC_PASS_ASYNC 1          /* may run on the second lane (the reference's unused async-compute queue) */
+typedef struct soc_pass_desc {
+    const char* name;             /* task name, unique in the graph */
+    const char* group;            /* GPU-metric group (renderer.cpp:577-588) or any label */
+    int32_t phase;                /* SOC_PHASE_PRE_EXPOSURE or SOC_PHASE_POST_EXPOSURE */
+    uint32_t flags;               /* SOC_PASS_ASYNC */
+    int32_t read_count, write_count;
+    int32_t reads[SOC_PASS_MAX_USES];    /* enum soc_resource */
+    int32_t writes[SOC_PASS_MAX_USES];
+} soc_pass_desc;
+/* The callback of a caller pass: record its work on `stream`, return 0 (or a negative code, which aborts the
+ * frame with that code). `images` is the renderer's frame, with history_color[0] / history_velocity[0] the
+ * PREVIOUS and [1] the RESOLVED slots of this frame. */
+typedef int32_t (*soc_pass_callback)(void* user, const soc_globals* g, const soc_frame_images* images, soc_stream stream);
+/* Add a caller pass. before = name of the pass it precedes, or NULL to append at the end of its phase.
+ * Caller passes survive soc_renderer_set_raster_scene. Errors: duplicate name, unknown `before` or a `before`
+ * in another phase, bad resource id, more than SOC_PASS_MAX_USES uses. */
+int soc_renderer_add_pass(soc_renderer* r, const soc_pass_desc* desc, soc_pass_callback fn, void* user,
+                          const char* before);
+/* Declared uses of pass `index` as resource bitmasks (bit = enum soc_resource). */
+int soc_renderer_pass_uses(const soc_renderer* r, int32_t index, uint64_t* reads, uint64_t* writes);
+/* Derived dependencies of pass `index`: the indices of the earlier passes it must follow (ascending).
+ * Returns their count (at most cap are written) or a negative error. */
+int32_t soc_renderer_pass_dependencies(const soc_renderer* r, int32_t index, int32_t* out, int32_t cap);
+/* Derived lane of pass `index` with the second lane enabled: 0 = the caller's stream, 1 = the second lane. */
+int32_t soc_renderer_pass_lane(const soc_renderer* r, int32_t index);
+
 /* --- Rasterisation: depth prepass, G-buffer and sun shadow map ---------------
  * Replaces the raster producers upstream of the hot path: DepthPrepassTask (depth_prepass.inl:26-120),
  * GBufferGenerationTask (g_buffer_generation.inl:33-230) and SunShadowDrawTask (sun_shadow_draw.inl:27-91).

@@ -413,8 +413,58 @@ class Renderer:
             out.append((n, gname, (tot.value / cnt.value) if cnt.value else float("nan"), cnt.value))
         return out
 
+    def add_pass(self, name: str, fn, reads=(), writes=(), phase: int = PHASE_PRE_EXPOSURE, group: str = "",
+                 before: Optional[str] = None, async_compute: bool = False) -> None:
+        """Register a caller pass (soc_renderer_add_pass): `fn(globals_ptr, frame_images_ptr, stream_handle)` records
+        its work on the stream and returns 0. reads / writes are resource names ("SSAO_BLUR", ...) or ids; the
+        pass runs before `before` (a pass name) or at the end of its phase."""
+        def ids(xs):
+            return [(_abi.RES[x] if isinstance(x, str) else int(x)) for x in xs]
+        d = _abi.PassDesc()
+        d.name, d.group, d.phase = name.encode(), group.encode(), int(phase)
+        d.flags = _abi.PASS_ASYNC if async_compute else 0
+        r_, w_ = ids(reads), ids(writes)
+        d.read_count, d.write_count = len(r_), len(w_)
+        for i, x in enumerate(r_):
+            d.reads[i] = x
+        for i, x in enumerate(w_):
+            d.writes[i] = x
+
+        def tramp(user, g, images, stream):
+            try:
+                rc = fn(g, images, stream if stream is not None else 0)   # NULL = the null stream
+                return int(rc or 0)
+            except Exception:   # an exception must not cross the C ABI
+                return -1
+        cb = _abi.PASS_CALLBACK(tramp)
+        _check(lib().soc_renderer_add_pass(self.handle, C.byref(d), cb, None, before.encode() if before else None),
+               "soc_renderer_add_pass")
+        self._callbacks = getattr(self, "_callbacks", []) + [cb]    # keep the trampolines alive
+
+    def pass_uses(self, index: int):
+        """(reads, writes) of pass `index` as sets of resource names (ids >= 32 as 'USER<k>')."""
+        rd, wr = C.c_uint64(0), C.c_uint64(0)
+        _check(lib().soc_renderer_pass_uses(self.handle, index, C.byref(rd), C.byref(wr)), "soc_renderer_pass_uses")
+
+        def names(m):
+            return {(_abi.RESOURCES[b] if b < len(_abi.RESOURCES) else f"USER{b - _abi.RES_USER0}")
+                    for b in range(_abi.RES_COUNT) if (m >> b) & 1}
+        return names(rd.value), names(wr.value)
+
+    def pass_dependencies(self, index: int):
+        """Indices of the earlier passes pass `index` depends on (derived from the declared uses)."""
+        buf = (C.c_int32 * 64)()
+        n = lib().soc_renderer_pass_dependencies(self.handle, index, buf, 64)
+        if n < 0:
+            _check(int(n), "soc_renderer_pass_dependencies")
+        return [int(buf[i]) for i in range(min(n, 64))]
+
+    def pass_lane(self, index: int) -> int:
+        return int(lib().soc_renderer_pass_lane(self.handle, index))
+
     def set_async(self, enable: bool) -> None:
-        """Sky lane: CloudRendering on a concurrent renderer-owned stream (identical results)."""
+        """Second lane: SOC_PASS_ASYNC passes (CloudRendering) on a concurrent renderer-owned stream (identical
+        results)."""
         _check(lib().soc_renderer_set_async(self.handle, int(bool(enable))), "soc_renderer_set_async")
 
     def current_history(self) -> int:

@@ -133,6 +133,26 @@ class RasterScene(C.Structure):
                 ("visibility", C.c_void_p), ("workspace", C.c_void_p)]
 
 
+# enum soc_resource (include/soc_rt.h): the frame resources a pass declares it reads / writes
+RESOURCES = ["ALBEDO", "EMISSIVE", "NORMAL", "DEPTH", "VELOCITY", "SUN_SHADOW", "NOISE", "BLOOM_MIP0", "BLOOM_MIP1",
+             "BLOOM_MIP2", "BLOOM_MIP3", "BLOOM_OUTPUT", "SSAO", "SSAO_BLUR", "CLOUDS", "COLOR", "PREVIOUS_COLOR",
+             "RESOLVED", "PREVIOUS_VELOCITY", "AUTO_EXPOSURE", "OUTPUT", "VISIBILITY", "HISTOGRAM_PARTIALS"]
+RES = {n: i for i, n in enumerate(RESOURCES)}
+RES_USER0 = 32
+RES_COUNT = 64
+PASS_MAX_USES = 16
+PASS_ASYNC = 1
+
+
+class PassDesc(C.Structure):
+    _fields_ = [("name", C.c_char_p), ("group", C.c_char_p), ("phase", C.c_int32), ("flags", C.c_uint32),
+                ("read_count", C.c_int32), ("write_count", C.c_int32), ("reads", C.c_int32 * PASS_MAX_USES),
+                ("writes", C.c_int32 * PASS_MAX_USES)]
+
+
+# int32_t (*soc_pass_callback)(void* user, const soc_globals*, const soc_frame_images*, soc_stream)
+PASS_CALLBACK = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.POINTER(Globals), C.POINTER(FrameImages), C.c_void_p)
+
 CULL_NONE, CULL_FRONT, CULL_BACK = 0, 1, 2
 MATERIAL_ZERO_VELOCITY = 1
 MATERIAL_NORMAL_MAP = 2
@@ -140,7 +160,7 @@ MATERIAL_NORMAL_MAP = 2
 STRUCTS = {"soc_img": SocImg, "soc_globals": Globals, "soc_sun_info": SunInfo, "soc_point_light": PointLight,
            "soc_spot_light": SpotLight, "soc_auto_exposure": AutoExposure, "soc_camera": Camera,
            "soc_frame_images": FrameImages, "soc_mesh": Mesh, "soc_material": Material,
-           "soc_raster_scene": RasterScene}
+           "soc_raster_scene": RasterScene, "soc_pass_desc": PassDesc}
 
 _I = C.c_int
 _P = C.c_void_p
@@ -190,6 +210,10 @@ FUNCTIONS = {
     "soc_renderer_pass_ms": (C.c_float, [_P, C.c_int32]),
     "soc_renderer_current_history": (C.c_int32, [_P]),
     "soc_renderer_set_async": (C.c_int, [_P, C.c_int32]),
+    "soc_renderer_add_pass": (_I, [_P, C.POINTER(PassDesc), PASS_CALLBACK, _P, C.c_char_p]),
+    "soc_renderer_pass_uses": (_I, [_P, C.c_int32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "soc_renderer_pass_dependencies": (C.c_int32, [_P, C.c_int32, C.POINTER(C.c_int32), C.c_int32]),
+    "soc_renderer_pass_lane": (C.c_int32, [_P, C.c_int32]),
     "soc_renderer_set_pass_timing": (_I, [_P, C.c_int32, C.c_int32]),
     "soc_renderer_reset_timing": (_I, [_P]),
     "soc_renderer_pass_stats": (_I, [_P, C.c_int32, C.POINTER(C.c_float), C.POINTER(C.c_int32)]),

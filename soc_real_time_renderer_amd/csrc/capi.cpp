@@ -171,6 +171,8 @@ const FieldInfo kFields[] = {
     F(soc_material, flags), F(soc_material, has_emissive), F(soc_material, pad), F(soc_material, normal_map),
     F(soc_raster_scene, mesh), F(soc_raster_scene, materials), F(soc_raster_scene, material_count),
     F(soc_raster_scene, shadow), F(soc_raster_scene, visibility), F(soc_raster_scene, workspace),
+    F(soc_pass_desc, name), F(soc_pass_desc, group), F(soc_pass_desc, phase), F(soc_pass_desc, flags),
+    F(soc_pass_desc, read_count), F(soc_pass_desc, write_count), F(soc_pass_desc, reads), F(soc_pass_desc, writes),
 };
 #undef F
 }  // namespace
@@ -191,6 +193,7 @@ extern "C" size_t soc_abi_sizeof(const char* t) {
     if (s == "soc_mesh") return sizeof(soc_mesh);
     if (s == "soc_material") return sizeof(soc_material);
     if (s == "soc_raster_scene") return sizeof(soc_raster_scene);
+    if (s == "soc_pass_desc") return sizeof(soc_pass_desc);
     return 0;
 }
 
@@ -463,23 +466,41 @@ extern "C" int soc_upload_globals(const soc_globals* g, soc_globals* d_globals, 
 
 // =================================================================================================
 // Render graph (renderer.cpp:929-1235, live passes only; SSR / Hi-Z / DOF are dead or disabled)
+//
+// Every pass declares the frame resources it reads and writes (the Daxa task-uses block,
+// e.g. composition.inl:10-21). The graph keeps the registration order, which is the reference's
+// add_task order, and derives from the uses what Daxa derives its barriers from: each pass's
+// dependencies on earlier passes (RAW, WAR, WAW). On one HIP stream stream order already satisfies
+// them; they matter for SOC_PASS_ASYNC passes, which run on a second stream of the renderer
+// (the async-compute queue the reference leaves unused): such a pass waits only for the passes it
+// depends on, and a pass on the caller's stream waits for it only if it depends on it.
 // =================================================================================================
 struct soc_renderer {
+    using PassFn = std::function<int(const soc_globals*, hipStream_t)>;
     struct Pass {
         std::string name, group;
-        int phase;
-        std::function<int(const soc_globals*, hipStream_t)> run;
-        int lane = 0;        // 1 = the sky lane: runs on the renderer's side stream, concurrently with lane 0
-        bool join = false;   // lane-0 pass that consumes the sky lane's output (waits on its join event)
-        bool head = false;   // raster head: runs on the caller's stream before the sky lane forks
+        int phase = SOC_PHASE_PRE_EXPOSURE;
+        uint64_t reads = 0, writes = 0;
+        uint32_t flags = 0;
+        PassFn run;
+        std::function<bool()> skip;   // true: the pass has no work this call (no launch, no timing)
+        std::vector<int> deps;        // derived: earlier passes this one must follow
         bool timed = false;
-        std::vector<hipEvent_t> ev0, ev1;  // ring of SOC_RENDERER_TIMING_RING frames
+        std::vector<hipEvent_t> ev0, ev1;  // timing ring of SOC_RENDERER_TIMING_RING frames
         int next = 0, count = 0, last = -1;
+        hipEvent_t done = nullptr;    // cross-lane completion event (created on first use)
+    };
+    struct UserPass {
+        soc_pass_desc desc;
+        std::string name, group, before;
+        soc_pass_callback fn;
+        void* user;
     };
     soc_frame_images img{};
     soc_raster_scene scene{};
     bool has_scene = false;
     std::vector<Pass> passes;
+    std::vector<UserPass> user_passes;
     uint32_t flags = 0;
     int hist = 0;               // history slot read as "previous" this frame
     uint64_t total_pixels = 0;  // 0 = this frame
@@ -488,9 +509,8 @@ struct soc_renderer {
     soc_globals* staging = nullptr;
     hipEvent_t staging_ev[4] = {nullptr, nullptr, nullptr, nullptr};
     int staging_slot = 0;
-    // sky lane: CloudRendering is VALU-bound and depends on depth only, so it overlaps the memory-bound
-    // bloom / SSAO passes on a second stream (fork at the frame start, join before Composition) -- the
-    // HIP counterpart of the async-compute queue the reference leaves unused (renderer.cpp:1094-1117)
+    // second lane (SOC_PASS_ASYNC passes: CloudRendering is VALU-bound and reads only depth and noise, so
+    // it overlaps the memory-bound bloom / SSAO passes)
     bool async = true;
     int side_device = -1;
     hipStream_t side = nullptr;
@@ -502,15 +522,26 @@ struct soc_renderer {
 };
 
 namespace {
-using PassFn = std::function<int(const soc_globals*, hipStream_t)>;
+using PassFn = soc_renderer::PassFn;
 
-void add_pass(soc_renderer* r, std::string name, std::string group, int phase, PassFn fn) {
+uint64_t res_mask(std::initializer_list<int> ids) {
+    uint64_t m = 0;
+    for (int i : ids) m |= 1ull << i;
+    return m;
+}
+
+soc_renderer::Pass& add_pass(soc_renderer* r, std::string name, std::string group, int phase, uint64_t reads,
+                             uint64_t writes, PassFn fn, uint32_t flags = 0) {
     soc_renderer::Pass p;
     p.name = std::move(name);
     p.group = std::move(group);
     p.phase = phase;
+    p.reads = reads;
+    p.writes = writes;
+    p.flags = flags;
     p.run = std::move(fn);
     r->passes.push_back(std::move(p));
+    return r->passes.back();
 }
 
 int ensure_hist_scratch(soc_renderer* r) {
@@ -527,159 +558,279 @@ int ensure_hist_scratch(soc_renderer* r) {
 // Raster head of the graph (renderer.cpp:965-1021): depth prepass, sun shadow, G-buffer.
 void build_raster_passes(soc_renderer* r) {
     if (!r->has_scene) return;
-    auto add = [r](std::string name, std::string group, PassFn fn) {
-        add_pass(r, std::move(name), std::move(group), SOC_PHASE_PRE_EXPOSURE, std::move(fn));
-        r->passes.back().head = true;
-    };
-    add("DepthPrepass", "Depth Prepass", [r](const soc_globals* g, hipStream_t s) {
-        const soc_img& d = r->img.depth;
-        return soc_raster_visibility(&r->scene.mesh, g->camera_projection_view_matrix, SOC_CULL_FRONT,
-                                     r->scene.visibility, d.width, d.height, 1, r->scene.workspace, (soc_stream)s);
-    });
+    const int pre = SOC_PHASE_PRE_EXPOSURE;
+    // DepthPrepassTask writes depth (depth_prepass.inl); here the visibility buffer it becomes
+    add_pass(r, "DepthPrepass", "Depth Prepass", pre, 0, res_mask({SOC_RES_VISIBILITY}),
+             [r](const soc_globals* g, hipStream_t s) {
+                 const soc_img& d = r->img.depth;
+                 return soc_raster_visibility(&r->scene.mesh, g->camera_projection_view_matrix, SOC_CULL_FRONT,
+                                              r->scene.visibility, d.width, d.height, 1, r->scene.workspace, (soc_stream)s);
+             });
     if (r->scene.shadow)
-        add("SunShadowDraw", "Shadows", [r](const soc_globals* g, hipStream_t s) {
-            return soc_raster_depth(&r->scene.mesh, g->sun_info.projection_view_matrix, SOC_CULL_BACK, 1.25f, 1.75f,
-                                    r->img.shadow, r->scene.workspace, (soc_stream)s);
-        });
-    add("GBufferGeneration", "Rendering G-Buffer", [r](const soc_globals* g, hipStream_t s) {
-        const soc_frame_images& I = r->img;
-        return soc_gbuffer_resolve(g, &r->scene.mesh, r->scene.materials, r->scene.material_count, r->scene.visibility,
-                                   I.depth, I.albedo, I.emissive, I.normal, I.velocity, r->scene.workspace, (soc_stream)s);
-    });
+        add_pass(r, "SunShadowDraw", "Shadows", pre, 0, res_mask({SOC_RES_SUN_SHADOW}),
+                 [r](const soc_globals* g, hipStream_t s) {
+                     return soc_raster_depth(&r->scene.mesh, g->sun_info.projection_view_matrix, SOC_CULL_BACK, 1.25f,
+                                             1.75f, r->img.shadow, r->scene.workspace, (soc_stream)s);
+                 });
+    // GBufferGenerationTask uses (renderer.cpp:993-1005): albedo, emissive, normal, velocity, depth
+    add_pass(r, "GBufferGeneration", "Rendering G-Buffer", pre, res_mask({SOC_RES_VISIBILITY}),
+             res_mask({SOC_RES_ALBEDO, SOC_RES_EMISSIVE, SOC_RES_NORMAL, SOC_RES_VELOCITY, SOC_RES_DEPTH}),
+             [r](const soc_globals* g, hipStream_t s) {
+                 const soc_frame_images& I = r->img;
+                 return soc_gbuffer_resolve(g, &r->scene.mesh, r->scene.materials, r->scene.material_count,
+                                            r->scene.visibility, I.depth, I.albedo, I.emissive, I.normal, I.velocity,
+                                            r->scene.workspace, (soc_stream)s);
+             });
 }
 
 // Bloom passes of the graph (renderer.cpp:1024-1062); build_passes_tail adds the rest.
 void build_passes(soc_renderer* r) {
     auto& I = r->img;
-    auto add = [r](std::string name, std::string group, int phase, PassFn fn) {
-        add_pass(r, std::move(name), std::move(group), phase, std::move(fn));
-    };
+    const int pre = SOC_PHASE_PRE_EXPOSURE;
     const int nm = 4;
-    // renderer.cpp:1024-1062
     const soc_img& bloom_dst = I.bloom_output.data ? I.bloom_output : I.emissive;
+    const int dst_res = I.bloom_output.data ? SOC_RES_BLOOM_OUTPUT : SOC_RES_EMISSIVE;
+    const int mip[4] = {SOC_RES_BLOOM_MIP0, SOC_RES_BLOOM_MIP1, SOC_RES_BLOOM_MIP2, SOC_RES_BLOOM_MIP3};
     const bool chain_ok = bloom_fused_applicable(I.emissive, I.bloom_mips, nm, bloom_dst);
     if (chain_ok && !(r->flags & (SOC_RENDERER_EXACT_BLOOM | SOC_RENDERER_UNFUSED_BLOOM))) {
         // weighted form (bloom_w.hip): 4 launches, mip0 / mip2 only in LDS, within the RGBA16F tolerance
         static const char* names[4] = {"BloomDownsample - 0+1", "BloomDownsample - 2+3", "BloomUpsample - 3+2",
                                        "BloomUpsample - 1+0"};
+        const uint64_t rd[4] = {res_mask({SOC_RES_EMISSIVE}), res_mask({mip[1]}), res_mask({mip[3]}), res_mask({mip[1]})};
+        const uint64_t wr[4] = {res_mask({mip[1]}), res_mask({mip[3]}), res_mask({mip[1]}), res_mask({dst_res})};
         for (int st = 1; st <= 4; ++st)
-            add(names[st - 1], "Bloom", SOC_PHASE_PRE_EXPOSURE, [r, st](const soc_globals* g, hipStream_t s) {
+            add_pass(r, names[st - 1], "Bloom", pre, rd[st - 1], wr[st - 1], [r, st](const soc_globals* g, hipStream_t s) {
                 const soc_img& dst = r->img.bloom_output.data ? r->img.bloom_output : r->img.emissive;
                 return soc_bloom_weighted_stage(g, r->img.emissive, r->img.bloom_mips, 4, dst, st, (soc_stream)s);
             });
         return;
-
     }
     const bool fused = !(r->flags & SOC_RENDERER_UNFUSED_BLOOM) && chain_ok;
     if (fused) {
         // bit-exact: downsweep as 2 fused stages (mip0 / mip2 of the downsweep stay in LDS;
         // bloom_fused.hip), the upsweep as the reference's 4 passes. Every mip and the output end up
         // with exactly the 8-pass chain's bits.
-        add("BloomDownsample - 0+1", "Bloom", SOC_PHASE_PRE_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
-            return soc_bloom_fused_stage(g, r->img.emissive, r->img.bloom_mips, 4, r->img.emissive, 1, (soc_stream)s);
-        });
-        add("BloomDownsample - 2+3", "Bloom", SOC_PHASE_PRE_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
-            return soc_bloom_fused_stage(g, r->img.emissive, r->img.bloom_mips, 4, r->img.emissive, 2, (soc_stream)s);
-        });
+        add_pass(r, "BloomDownsample - 0+1", "Bloom", pre, res_mask({SOC_RES_EMISSIVE}), res_mask({mip[0], mip[1]}),
+                 [r](const soc_globals* g, hipStream_t s) {
+                     return soc_bloom_fused_stage(g, r->img.emissive, r->img.bloom_mips, 4, r->img.emissive, 1, (soc_stream)s);
+                 });
+        add_pass(r, "BloomDownsample - 2+3", "Bloom", pre, res_mask({mip[1]}), res_mask({mip[2], mip[3]}),
+                 [r](const soc_globals* g, hipStream_t s) {
+                     return soc_bloom_fused_stage(g, r->img.emissive, r->img.bloom_mips, 4, r->img.emissive, 2, (soc_stream)s);
+                 });
     } else {
-        add("BloomDownsample - 0", "Bloom", SOC_PHASE_PRE_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
-            return soc_bloom_downsample(g, r->img.emissive, r->img.bloom_mips[0], (soc_stream)s);
-        });
+        // renderer.cpp:1024-1042
+        add_pass(r, "BloomDownsample - 0", "Bloom", pre, res_mask({SOC_RES_EMISSIVE}), res_mask({mip[0]}),
+                 [r](const soc_globals* g, hipStream_t s) {
+                     return soc_bloom_downsample(g, r->img.emissive, r->img.bloom_mips[0], (soc_stream)s);
+                 });
         for (int i = 0; i < nm - 1; ++i)
-            add("BloomDownsample - " + std::to_string(i + 1), "Bloom", SOC_PHASE_PRE_EXPOSURE, [r, i](const soc_globals* g, hipStream_t s) {
-                return soc_bloom_downsample(g, r->img.bloom_mips[i], r->img.bloom_mips[i + 1], (soc_stream)s);
-            });
+            add_pass(r, "BloomDownsample - " + std::to_string(i + 1), "Bloom", pre, res_mask({mip[i]}),
+                     res_mask({mip[i + 1]}), [r, i](const soc_globals* g, hipStream_t s) {
+                         return soc_bloom_downsample(g, r->img.bloom_mips[i], r->img.bloom_mips[i + 1], (soc_stream)s);
+                     });
     }
+    // renderer.cpp:1044-1062 (load_op CLEAR: the upsample overwrites its target, quirk Q5)
     for (int i = nm - 1; i > 0; --i)
-        add("BloomUpsample - " + std::to_string(i), "Bloom", SOC_PHASE_PRE_EXPOSURE, [r, i](const soc_globals* g, hipStream_t s) {
-            return soc_bloom_upsample(g, r->img.bloom_mips[i], r->img.bloom_mips[i - 1], (soc_stream)s);
-        });
-    add("BloomUpsample - 0", "Bloom", SOC_PHASE_PRE_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
-        const soc_img& dst = r->img.bloom_output.data ? r->img.bloom_output : r->img.emissive;
-        return soc_bloom_upsample(g, r->img.bloom_mips[0], dst, (soc_stream)s);
-    });
+        add_pass(r, "BloomUpsample - " + std::to_string(i), "Bloom", pre, res_mask({mip[i]}), res_mask({mip[i - 1]}),
+                 [r, i](const soc_globals* g, hipStream_t s) {
+                     return soc_bloom_upsample(g, r->img.bloom_mips[i], r->img.bloom_mips[i - 1], (soc_stream)s);
+                 });
+    add_pass(r, "BloomUpsample - 0", "Bloom", pre, res_mask({mip[0]}), res_mask({dst_res}),
+             [r](const soc_globals* g, hipStream_t s) {
+                 const soc_img& dst = r->img.bloom_output.data ? r->img.bloom_output : r->img.emissive;
+                 return soc_bloom_upsample(g, r->img.bloom_mips[0], dst, (soc_stream)s);
+             });
 }
 
 void build_passes_tail(soc_renderer* r) {
-    auto add = [r](std::string name, std::string group, int phase, PassFn fn) {
-        add_pass(r, std::move(name), std::move(group), phase, std::move(fn));
-    };
     auto& I = r->img;
+    const int pre = SOC_PHASE_PRE_EXPOSURE, post = SOC_PHASE_POST_EXPOSURE;
+    const int em_res = I.bloom_output.data ? SOC_RES_BLOOM_OUTPUT : SOC_RES_EMISSIVE;
     // renderer.cpp:1064-1079
-    add("SSAOGeneration", "Ambient Occlusion", SOC_PHASE_PRE_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
-        return soc_ssao_generation(g, r->img.depth, r->img.normal, r->img.ssao, r->img.ssao_noise_table, (soc_stream)s);
-    });
-    add("SSAOBlur", "Ambient Occlusion", SOC_PHASE_PRE_EXPOSURE,
-        [r](const soc_globals* g, hipStream_t s) { return soc_ssao_blur(g, r->img.ssao, r->img.ssao_blur, (soc_stream)s); });
+    add_pass(r, "SSAOGeneration", "Ambient Occlusion", pre, res_mask({SOC_RES_DEPTH, SOC_RES_NORMAL}),
+             res_mask({SOC_RES_SSAO}), [r](const soc_globals* g, hipStream_t s) {
+                 return soc_ssao_generation(g, r->img.depth, r->img.normal, r->img.ssao, r->img.ssao_noise_table,
+                                            (soc_stream)s);
+             });
+    add_pass(r, "SSAOBlur", "Ambient Occlusion", pre, res_mask({SOC_RES_SSAO}), res_mask({SOC_RES_SSAO_BLUR}),
+             [r](const soc_globals* g, hipStream_t s) { return soc_ssao_blur(g, r->img.ssao, r->img.ssao_blur, (soc_stream)s); });
     // renderer.cpp:1094-1101
-    add("CloudRendering", "Sky Rendering", SOC_PHASE_PRE_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
-        return soc_cloud_rendering(g, r->img.depth, r->img.noise, r->img.clouds, r->img.clouds_workspace, (soc_stream)s);
-    });
-    r->passes.back().lane = 1;
-    // renderer.cpp:1103-1117 (composition) and 1155-1162 (histogram): one launch by default (the colour
+    add_pass(r, "CloudRendering", "Sky Rendering", pre, res_mask({SOC_RES_DEPTH, SOC_RES_NOISE}),
+             res_mask({SOC_RES_CLOUDS}), [r](const soc_globals* g, hipStream_t s) {
+                 return soc_cloud_rendering(g, r->img.depth, r->img.noise, r->img.clouds, r->img.clouds_workspace,
+                                            (soc_stream)s);
+             }, SOC_PASS_ASYNC);
+    // renderer.cpp:1103-1117 (composition uses) and 1155-1162 (histogram): one launch by default (the colour
     // is binned as it is written), two with SOC_RENDERER_UNFUSED_HISTOGRAM (measured in composition.hip)
+    const uint64_t comp_reads = res_mask({SOC_RES_ALBEDO, em_res, SOC_RES_NORMAL, SOC_RES_DEPTH, SOC_RES_SSAO_BLUR,
+                                          SOC_RES_SUN_SHADOW, SOC_RES_CLOUDS});
     if (!(r->flags & SOC_RENDERER_UNFUSED_HISTOGRAM)) {
-        add("Composition+GenerateLuminanceHistogram", "Composition", SOC_PHASE_PRE_EXPOSURE,
-            [r](const soc_globals* g, hipStream_t s) {
-                const auto& I = r->img;
-                const soc_img& em = I.bloom_output.data ? I.bloom_output : I.emissive;
-                int rc = ensure_hist_scratch(r);
-                if (rc) return rc;
-                return soc::composition_luminance_histogram(g, I.d_globals, I.color, I.albedo, em, I.normal, I.depth,
-                                                            I.ssao_blur, I.shadow, I.clouds, I.auto_exposure,
-                                                            r->hist_scratch, false, (soc_stream)s);
-            });
-        r->passes.back().join = true;
-        // the 8 partial histograms of the fused launch into the AutoExposure bins (its own pass, so the
-        // Composition pass times the composition kernel alone)
-        // Before a multi-GPU exchange (PRE and POST in separate calls) the fold must precede it; in a one-call
-        // frame the resolve does it instead and this pass launches nothing.
-        add("LuminanceHistogramFold", "Auto Exposure", SOC_PHASE_PRE_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
-            (void)g;
-            if (r->fold_in_resolve) return (int)SOC_OK;
-            return soc::histogram_fold_launch(r->hist_scratch, r->img.auto_exposure, (soc_stream)s);
-        });
+        add_pass(r, "Composition+GenerateLuminanceHistogram", "Composition", pre, comp_reads,
+                 res_mask({SOC_RES_COLOR, SOC_RES_HISTOGRAM_PARTIALS}), [r](const soc_globals* g, hipStream_t s) {
+                     const auto& I = r->img;
+                     const soc_img& em = I.bloom_output.data ? I.bloom_output : I.emissive;
+                     int rc = ensure_hist_scratch(r);
+                     if (rc) return rc;
+                     return soc::composition_luminance_histogram(g, I.d_globals, I.color, I.albedo, em, I.normal, I.depth,
+                                                                 I.ssao_blur, I.shadow, I.clouds, I.auto_exposure,
+                                                                 r->hist_scratch, false, (soc_stream)s);
+                 });
+        // the 8 partial histograms of the fused launch into the AutoExposure bins. Before a multi-GPU exchange
+        // (PRE and POST in separate calls) the fold must precede it; in a one-call frame the resolve folds them
+        // itself and this pass has no work (it is then neither launched nor timed).
+        auto& fold = add_pass(r, "LuminanceHistogramFold", "Auto Exposure", pre, res_mask({SOC_RES_HISTOGRAM_PARTIALS}),
+                              res_mask({SOC_RES_AUTO_EXPOSURE, SOC_RES_HISTOGRAM_PARTIALS}),
+                              [r](const soc_globals* g, hipStream_t s) {
+                                  (void)g;
+                                  return soc::histogram_fold_launch(r->hist_scratch, r->img.auto_exposure, (soc_stream)s);
+                              });
+        fold.skip = [r] { return r->fold_in_resolve; };
     } else {
-        add("Composition", "Composition", SOC_PHASE_PRE_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
-            const auto& I = r->img;
-            const soc_img& em = I.bloom_output.data ? I.bloom_output : I.emissive;
-            return soc_composition(g, I.d_globals, I.color, I.albedo, em, I.normal, I.depth, I.ssao_blur, I.shadow, I.clouds,
-                                   (soc_stream)s);
-        });
-        r->passes.back().join = true;
-        add("GenerateLuminanceHistogram", "Auto Exposure", SOC_PHASE_PRE_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
-            return soc_generate_luminance_histogram(g, r->img.color, r->img.auto_exposure, (soc_stream)s);
-        });
+        add_pass(r, "Composition", "Composition", pre, comp_reads, res_mask({SOC_RES_COLOR}),
+                 [r](const soc_globals* g, hipStream_t s) {
+                     const auto& I = r->img;
+                     const soc_img& em = I.bloom_output.data ? I.bloom_output : I.emissive;
+                     return soc_composition(g, I.d_globals, I.color, I.albedo, em, I.normal, I.depth, I.ssao_blur,
+                                            I.shadow, I.clouds, (soc_stream)s);
+                 });
+        add_pass(r, "GenerateLuminanceHistogram", "Auto Exposure", pre, res_mask({SOC_RES_COLOR}),
+                 res_mask({SOC_RES_AUTO_EXPOSURE}), [r](const soc_globals* g, hipStream_t s) {
+                     return soc_generate_luminance_histogram(g, r->img.color, r->img.auto_exposure, (soc_stream)s);
+                 });
     }
-    add("ResolveLuminanceHistogram", "Auto Exposure", SOC_PHASE_POST_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
-        return soc::resolve_luminance_histogram(g, r->img.auto_exposure, r->total_pixels, r->wide,
-                                                r->fold_in_resolve ? r->hist_scratch : nullptr, (soc_stream)s);
-    });
+    // renderer.cpp:1164-1168
+    add_pass(r, "ResolveLuminanceHistogram", "Auto Exposure", post,
+             res_mask({SOC_RES_AUTO_EXPOSURE, SOC_RES_HISTOGRAM_PARTIALS}),
+             res_mask({SOC_RES_AUTO_EXPOSURE, SOC_RES_HISTOGRAM_PARTIALS}), [r](const soc_globals* g, hipStream_t s) {
+                 return soc::resolve_luminance_histogram(g, r->img.auto_exposure, r->total_pixels, r->wide,
+                                                         r->fold_in_resolve ? r->hist_scratch : nullptr, (soc_stream)s);
+             });
     // renderer.cpp:1170-1198: TAA + both history copies (ping-pong + fused velocity history), and
     // renderer.cpp:1210-1217: tone mapping, fused into the TAA launch for an RGBA8_UNORM framebuffer
+    const uint64_t taa_reads = res_mask({SOC_RES_COLOR, SOC_RES_PREVIOUS_COLOR, SOC_RES_VELOCITY,
+                                         SOC_RES_PREVIOUS_VELOCITY, SOC_RES_DEPTH});
+    const uint64_t taa_writes = res_mask({SOC_RES_RESOLVED, SOC_RES_PREVIOUS_VELOCITY});
     const bool fuse_tm = !(r->flags & SOC_RENDERER_UNFUSED_TONEMAP) && I.output.format == SOC_FMT_RGBA8_UNORM;
     if (fuse_tm) {
-        add("TemporalAntiAliasing+ToneMapping", "Temporal Anti-Aliasing", SOC_PHASE_POST_EXPOSURE,
-            [r](const soc_globals* g, hipStream_t s) {
-                const auto& I = r->img;
-                const int p = r->hist, q = 1 - r->hist;
-                return soc_temporal_antialiasing_tone_mapping(g, I.history_color[q], I.color, I.history_color[p], I.velocity,
-                                                              I.history_velocity[p], I.depth, I.history_velocity[q],
-                                                              I.auto_exposure, I.output, (soc_stream)s);
-            });
+        add_pass(r, "TemporalAntiAliasing+ToneMapping", "Temporal Anti-Aliasing", post,
+                 taa_reads | res_mask({SOC_RES_AUTO_EXPOSURE}), taa_writes | res_mask({SOC_RES_OUTPUT}),
+                 [r](const soc_globals* g, hipStream_t s) {
+                     const auto& I = r->img;
+                     const int p = r->hist, q = 1 - r->hist;
+                     return soc_temporal_antialiasing_tone_mapping(g, I.history_color[q], I.color, I.history_color[p],
+                                                                   I.velocity, I.history_velocity[p], I.depth,
+                                                                   I.history_velocity[q], I.auto_exposure, I.output,
+                                                                   (soc_stream)s);
+                 });
     } else {
-        add("TemporalAntiAliasing", "Temporal Anti-Aliasing", SOC_PHASE_POST_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
-            const auto& I = r->img;
-            const int p = r->hist, q = 1 - r->hist;
-            return soc_temporal_antialiasing(g, I.history_color[q], I.color, I.history_color[p], I.velocity,
-                                             I.history_velocity[p], I.depth, I.history_velocity[q], (soc_stream)s);
-        });
-        add("ToneMapping", "Tone Mapping", SOC_PHASE_POST_EXPOSURE, [r](const soc_globals* g, hipStream_t s) {
-            const auto& I = r->img;
-            return soc_tone_mapping(g, I.history_color[1 - r->hist], I.auto_exposure, I.output, (soc_stream)s);
-        });
+        add_pass(r, "TemporalAntiAliasing", "Temporal Anti-Aliasing", post, taa_reads, taa_writes,
+                 [r](const soc_globals* g, hipStream_t s) {
+                     const auto& I = r->img;
+                     const int p = r->hist, q = 1 - r->hist;
+                     return soc_temporal_antialiasing(g, I.history_color[q], I.color, I.history_color[p], I.velocity,
+                                                      I.history_velocity[p], I.depth, I.history_velocity[q], (soc_stream)s);
+                 });
+        add_pass(r, "ToneMapping", "Tone Mapping", post, res_mask({SOC_RES_RESOLVED, SOC_RES_AUTO_EXPOSURE}),
+                 res_mask({SOC_RES_OUTPUT}), [r](const soc_globals* g, hipStream_t s) {
+                     const auto& I = r->img;
+                     return soc_tone_mapping(g, I.history_color[1 - r->hist], I.auto_exposure, I.output, (soc_stream)s);
+                 });
     }
-    (void)I;
+}
+
+// The frame as a caller pass sees it: history slot 0 = PREVIOUS, 1 = RESOLVED of this frame.
+soc_frame_images callback_view(const soc_renderer* r) {
+    soc_frame_images v = r->img;
+    const int p = r->hist, q = 1 - r->hist;
+    v.history_color[0] = r->img.history_color[p];
+    v.history_color[1] = r->img.history_color[q];
+    v.history_velocity[0] = r->img.history_velocity[p];
+    v.history_velocity[1] = r->img.history_velocity[q];
+    return v;
+}
+
+uint64_t desc_mask(const int32_t* ids, int32_t n) {
+    uint64_t m = 0;
+    for (int i = 0; i < n; ++i) m |= 1ull << ids[i];
+    return m;
+}
+
+// Insert the caller passes: before their anchor, or at the end of their phase. Returns an error for an
+// unknown or cross-phase anchor.
+int insert_user_passes(soc_renderer* r) {
+    for (auto& up : r->user_passes) {
+        soc_renderer::Pass p;
+        p.name = up.name;
+        p.group = up.group;
+        p.phase = up.desc.phase;
+        p.reads = desc_mask(up.desc.reads, up.desc.read_count);
+        p.writes = desc_mask(up.desc.writes, up.desc.write_count);
+        p.flags = up.desc.flags;
+        const soc_pass_callback fn = up.fn;
+        void* user = up.user;
+        p.run = [r, fn, user](const soc_globals* g, hipStream_t s) {
+            const soc_frame_images v = callback_view(r);
+            const int32_t rc = fn(user, g, &v, (soc_stream)s);
+            return rc ? set_error(rc, "caller pass failed with %d", (int)rc) : (int)SOC_OK;
+        };
+        size_t at = r->passes.size();
+        if (!up.before.empty()) {
+            at = r->passes.size() + 1;
+            for (size_t i = 0; i < r->passes.size(); ++i)
+                if (r->passes[i].name == up.before) { at = i; break; }
+            if (at > r->passes.size())
+                return set_error(SOC_E_INVALID_ARG, "soc_renderer_add_pass: no pass named \"%s\"", up.before.c_str());
+            if (r->passes[at].phase != p.phase)
+                return set_error(SOC_E_INVALID_ARG, "soc_renderer_add_pass: \"%s\" is in another phase", up.before.c_str());
+        } else {
+            for (size_t i = 0; i < r->passes.size(); ++i)
+                if (r->passes[i].phase > p.phase) { at = i; break; }
+        }
+        r->passes.insert(r->passes.begin() + (long)at, std::move(p));
+    }
+    return SOC_OK;
+}
+
+// Dependencies from the declared uses: for every resource a pass reads, the latest earlier writer (RAW);
+// for every resource it writes, the latest earlier writer (WAW) and the readers since then (WAR).
+void derive_dependencies(soc_renderer* r) {
+    const int n = (int)r->passes.size();
+    for (int i = 0; i < n; ++i) {
+        auto& p = r->passes[i];
+        p.deps.clear();
+        std::vector<char> dep(n, 0);
+        for (int b = 0; b < SOC_RES_COUNT; ++b) {
+            const uint64_t bit = 1ull << b;
+            if (!((p.reads | p.writes) & bit)) continue;
+            for (int j = i - 1; j >= 0; --j) {
+                const auto& q = r->passes[j];
+                if (q.writes & bit) { dep[j] = 1; break; }              // RAW / WAW: the latest writer
+                if ((p.writes & bit) && (q.reads & bit)) dep[j] = 1;    // WAR: readers since that writer
+            }
+        }
+        for (int j = 0; j < i; ++j)
+            if (dep[j]) p.deps.push_back(j);
+    }
+}
+
+void destroy_pass_events(soc_renderer* r) {
+    for (auto& p : r->passes) {
+        for (auto e : p.ev0) (void)hipEventDestroy(e);
+        for (auto e : p.ev1) (void)hipEventDestroy(e);
+        if (p.done) (void)hipEventDestroy(p.done);
+    }
+}
+
+int build_graph(soc_renderer* r) {
+    destroy_pass_events(r);
+    r->passes.clear();
+    build_raster_passes(r);
+    build_passes(r);
+    build_passes_tail(r);
+    int rc = insert_user_passes(r);
+    derive_dependencies(r);
+    return rc;
 }
 }  // namespace
 
@@ -696,9 +847,7 @@ extern "C" soc_renderer* soc_renderer_create(const soc_frame_images* images, uin
     r->img = *images;
     r->flags = flags;
     r->async = !(flags & SOC_RENDERER_SERIAL);
-    build_raster_passes(r);
-    build_passes(r);
-    build_passes_tail(r);
+    (void)build_graph(r);
     if ((flags & SOC_RENDERER_TIMING) && soc_renderer_set_pass_timing(r, -1, 1) != SOC_OK) {
         soc_renderer_destroy(r);
         return nullptr;
@@ -708,10 +857,7 @@ extern "C" soc_renderer* soc_renderer_create(const soc_frame_images* images, uin
 
 extern "C" void soc_renderer_destroy(soc_renderer* r) {
     if (!r) return;
-    for (auto& p : r->passes) {
-        for (auto e : p.ev0) (void)hipEventDestroy(e);
-        for (auto e : p.ev1) (void)hipEventDestroy(e);
-    }
+    destroy_pass_events(r);
     for (auto& e : r->staging_ev)
         if (e) (void)hipEventDestroy(e);
     if (r->staging) (void)hipHostFree(r->staging);
@@ -759,19 +905,19 @@ static int ensure_side_lane(soc_renderer* r) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return set_error(SOC_E_HIP, "soc_renderer_execute: hipGetDevice failed");
     if (r->side && r->side_device == dev) return SOC_OK;
-    if (r->side) {   // the caller moved to another device: rebuild the lane there
+    if (r->side) {   // the caller moved to another device: rebuild the lane (and its events) there
         (void)hipStreamDestroy(r->side);
         (void)hipEventDestroy(r->fork_ev);
         (void)hipEventDestroy(r->join_ev);
+        for (auto& p : r->passes)
+            if (p.done) { (void)hipEventDestroy(p.done); p.done = nullptr; }
         r->side = nullptr;
         r->fork_ev = r->join_ev = nullptr;
     }
-    const char* pe = getenv("SOC_SKY_PRIORITY");   // tuning knob: HIP stream priority of the sky lane
-    if ((pe ? hipStreamCreateWithPriority(&r->side, hipStreamNonBlocking, atoi(pe))
-            : hipStreamCreateWithFlags(&r->side, hipStreamNonBlocking)) != hipSuccess ||
+    if (hipStreamCreateWithFlags(&r->side, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&r->fork_ev, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&r->join_ev, hipEventDisableTiming) != hipSuccess)
-        return set_error(SOC_E_HIP, "soc_renderer_execute: sky lane stream/event creation failed");
+        return set_error(SOC_E_HIP, "soc_renderer_execute: second lane stream/event creation failed");
     r->side_device = dev;
     return SOC_OK;
 }
@@ -784,42 +930,48 @@ extern "C" int soc_renderer_execute(soc_renderer* r, const soc_globals* g, int32
         int rc = upload_lights(r, g, s);
         if (rc) return rc;
     }
-    if (phase & SOC_PHASE_PRE_EXPOSURE)
-        for (auto& p : r->passes) {
-            if (!p.head) continue;
-            int rc = run_pass(p, g, s);
-            if (rc) return rc;
-        }
-    // lane-1 passes run on the side stream, ordered after everything already on `s` (fork) and
-    // before the first lane-0 pass marked `join`; every pass still reads and writes the same images
-    const bool lanes = r->async && (phase & SOC_PHASE_PRE_EXPOSURE);
+    const int n = (int)r->passes.size();
+    // lane of every pass run by this call (-1: not run)
+    std::vector<int> lane(n, -1);
+    bool lanes = false;
+    for (int i = 0; i < n; ++i) {
+        const auto& p = r->passes[i];
+        if (!(p.phase & phase) || (p.skip && p.skip())) continue;
+        lane[i] = (r->async && (p.flags & SOC_PASS_ASYNC)) ? 1 : 0;
+        lanes |= lane[i] == 1;
+    }
+    // a pass records its completion event when a pass of the other lane depends on it
+    std::vector<char> signal(n, 0);
+    for (int i = 0; i < n; ++i)
+        if (lane[i] >= 0)
+            for (int j : r->passes[i].deps)
+                if (lane[j] >= 0 && lane[j] != lane[i]) signal[j] = 1;
     if (lanes) {
         int rc = ensure_side_lane(r);
         if (rc) return rc;
+        // fork: the second lane starts after everything the caller queued before this call
         if (hipEventRecord(r->fork_ev, s) != hipSuccess || hipStreamWaitEvent(r->side, r->fork_ev, 0) != hipSuccess)
-            return set_error(SOC_E_HIP, "soc_renderer_execute: sky lane fork failed");
-        for (auto& p : r->passes) {
-            if (p.lane != 1 || !(p.phase & phase)) continue;
-            rc = run_pass(p, g, r->side);
-            if (rc) return rc;
-        }
-        if (hipEventRecord(r->join_ev, r->side) != hipSuccess)
-            return set_error(SOC_E_HIP, "soc_renderer_execute: sky lane join failed");
+            return set_error(SOC_E_HIP, "soc_renderer_execute: second lane fork failed");
     }
-    bool joined = !lanes;
-    for (auto& p : r->passes) {
-        if (!(p.phase & phase) || p.head) continue;
-        if (lanes && p.lane == 1) continue;
-        if (p.join && !joined) {
-            if (hipStreamWaitEvent(s, r->join_ev, 0) != hipSuccess)
-                return set_error(SOC_E_HIP, "soc_renderer_execute: sky lane join failed");
-            joined = true;
-        }
-        int rc = run_pass(p, g, s);
+    for (int i = 0; i < n; ++i) {
+        if (lane[i] < 0) continue;
+        auto& p = r->passes[i];
+        hipStream_t ls = lane[i] ? r->side : s;
+        for (int j : p.deps)
+            if (lane[j] >= 0 && lane[j] != lane[i] && hipStreamWaitEvent(ls, r->passes[j].done, 0) != hipSuccess)
+                return set_error(SOC_E_HIP, "soc_renderer_execute: %s: cross-lane wait failed", p.name.c_str());
+        int rc = run_pass(p, g, ls);
         if (rc) return rc;
+        if (signal[i]) {
+            if (!p.done && hipEventCreateWithFlags(&p.done, hipEventDisableTiming) != hipSuccess)
+                return set_error(SOC_E_HIP, "soc_renderer_execute: hipEventCreate failed");
+            if (hipEventRecord(p.done, ls) != hipSuccess)
+                return set_error(SOC_E_HIP, "soc_renderer_execute: %s: event record failed", p.name.c_str());
+        }
     }
-    if (!joined && hipStreamWaitEvent(s, r->join_ev, 0) != hipSuccess)   // no consumer this phase: still join
-        return set_error(SOC_E_HIP, "soc_renderer_execute: sky lane join failed");
+    // join: everything of this call is ordered before whatever the caller queues next on `stream`
+    if (lanes && (hipEventRecord(r->join_ev, r->side) != hipSuccess || hipStreamWaitEvent(s, r->join_ev, 0) != hipSuccess))
+        return set_error(SOC_E_HIP, "soc_renderer_execute: second lane join failed");
     if (phase & SOC_PHASE_POST_EXPOSURE) r->hist = 1 - r->hist;   // ping-pong the TAA history
     return SOC_OK;
 }
@@ -833,18 +985,68 @@ extern "C" int soc_renderer_set_raster_scene(soc_renderer* r, const soc_raster_s
         if (scene->shadow && !r->img.shadow.data)
             return set_error(SOC_E_INVALID_ARG, "soc_renderer_set_raster_scene: shadow pass needs images.shadow");
     }
-    for (auto& p : r->passes) {
-        for (auto e : p.ev0) (void)hipEventDestroy(e);
-        for (auto e : p.ev1) (void)hipEventDestroy(e);
-    }
-    r->passes.clear();
     r->has_scene = scene != nullptr;
     if (scene) r->scene = *scene;
-    build_raster_passes(r);
-    build_passes(r);
-    build_passes_tail(r);
+    int rc = build_graph(r);
+    if (rc) return rc;
     if (r->flags & SOC_RENDERER_TIMING) return soc_renderer_set_pass_timing(r, -1, 1);
     return SOC_OK;
+}
+
+extern "C" int soc_renderer_add_pass(soc_renderer* r, const soc_pass_desc* d, soc_pass_callback fn, void* user,
+                                     const char* before) {
+    if (!r || !d || !fn || !d->name || !d->name[0])
+        return set_error(SOC_E_INVALID_ARG, "soc_renderer_add_pass: null renderer, descriptor, callback or name");
+    if (d->phase != SOC_PHASE_PRE_EXPOSURE && d->phase != SOC_PHASE_POST_EXPOSURE)
+        return set_error(SOC_E_INVALID_ARG, "soc_renderer_add_pass: %s: phase must be PRE or POST", d->name);
+    if (d->read_count < 0 || d->read_count > SOC_PASS_MAX_USES || d->write_count < 0 || d->write_count > SOC_PASS_MAX_USES)
+        return set_error(SOC_E_INVALID_ARG, "soc_renderer_add_pass: %s: at most %d reads / writes", d->name, SOC_PASS_MAX_USES);
+    for (int i = 0; i < d->read_count + d->write_count; ++i) {
+        const int id = i < d->read_count ? d->reads[i] : d->writes[i - d->read_count];
+        if (id < 0 || id >= SOC_RES_COUNT)
+            return set_error(SOC_E_INVALID_ARG, "soc_renderer_add_pass: %s: bad resource id %d", d->name, id);
+    }
+    for (const auto& p : r->passes)
+        if (p.name == d->name) return set_error(SOC_E_INVALID_ARG, "soc_renderer_add_pass: duplicate pass name \"%s\"", d->name);
+    soc_renderer::UserPass up;
+    up.desc = *d;
+    up.name = d->name;
+    up.group = d->group ? d->group : "";
+    up.before = before ? before : "";
+    up.fn = fn;
+    up.user = user;
+    up.desc.name = nullptr;
+    up.desc.group = nullptr;
+    r->user_passes.push_back(up);
+    int rc = build_graph(r);
+    if (rc) {   // roll back
+        r->user_passes.pop_back();
+        (void)build_graph(r);
+        return rc;
+    }
+    if (r->flags & SOC_RENDERER_TIMING) return soc_renderer_set_pass_timing(r, -1, 1);
+    return SOC_OK;
+}
+
+extern "C" int soc_renderer_pass_uses(const soc_renderer* r, int32_t i, uint64_t* reads, uint64_t* writes) {
+    if (!r || i < 0 || i >= (int32_t)r->passes.size() || !reads || !writes)
+        return set_error(SOC_E_INVALID_ARG, "soc_renderer_pass_uses: bad arguments");
+    *reads = r->passes[i].reads;
+    *writes = r->passes[i].writes;
+    return SOC_OK;
+}
+
+extern "C" int32_t soc_renderer_pass_dependencies(const soc_renderer* r, int32_t i, int32_t* out, int32_t cap) {
+    if (!r || i < 0 || i >= (int32_t)r->passes.size() || cap < 0 || (cap > 0 && !out))
+        return set_error(SOC_E_INVALID_ARG, "soc_renderer_pass_dependencies: bad arguments");
+    const auto& d = r->passes[i].deps;
+    for (int k = 0; k < (int)d.size() && k < cap; ++k) out[k] = d[k];
+    return (int32_t)d.size();
+}
+
+extern "C" int32_t soc_renderer_pass_lane(const soc_renderer* r, int32_t i) {
+    if (!r || i < 0 || i >= (int32_t)r->passes.size()) return set_error(SOC_E_INVALID_ARG, "soc_renderer_pass_lane: bad index");
+    return (r->passes[i].flags & SOC_PASS_ASYNC) ? 1 : 0;
 }
 
 extern "C" int soc_renderer_set_async(soc_renderer* r, int32_t enable) {

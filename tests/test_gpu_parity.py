@@ -538,8 +538,10 @@ def test_render_graph_frames(soc, oracle, W, H, frames, inputs):
         d = np.abs(host(fr["output"]).astype(np.int32) - hf["output"].astype(np.int32))
         assert (d <= 2).mean() >= 0.995, (f, (d <= 2).mean())
         assert abs(soc.exposure_of(fr["auto_exposure"]) - ae.exposure) <= 1e-4
-    ms = r.pass_ms()
-    assert all(m >= 0 for m in ms) and len(ms) == len(r.pass_names())
+    ms = dict(zip(r.pass_names(), r.pass_ms()))
+    # a one-call frame folds the partial histograms in the resolve: the fold pass is neither launched nor timed
+    assert ms.pop("LuminanceHistogramFold") < 0
+    assert all(m >= 0 for m in ms.values())
     r.close()
 
 
