@@ -255,6 +255,7 @@ def main():
     if args.write_frame and rank == 0:   # headless present: the RGBA8 framebuffer to a host image
         soc.write_png(args.write_frame, soc.read_image(fr["output"]))
     r.set_async(not args.no_sky_lane)
+    stats = [st for st in stats if st[3]]     # passes with no work this frame (the folded fold pass) have no record
     ms_pass = {n: round(ms, 4) for n, _, ms, _ in stats}
     ms_group = {}
     for n, gname, ms, _ in stats:

@@ -482,9 +482,15 @@ typedef struct soc_material {
     int32_t has_emissive;              /* 0: emissive = 0 (has_emissive_image) */
     int32_t pad[2];
     soc_img normal_map;                /* RGBA16F, used with SOC_MATERIAL_NORMAL_MAP */
+    soc_img normal_image;              /* RGBA8_UNORM tangent-space normal texture, with SOC_MATERIAL_NORMAL_TEXTURE */
 } soc_material;
 #define SOC_MATERIAL_ZERO_VELOCITY 1   /* write velocity 0 (the terrain draw, draw_terrain.inl:221) */
 #define SOC_MATERIAL_NORMAL_MAP 2      /* normal = normalize(bilinear normal_map(uv).xyz) (draw_terrain.inl:206-219) */
+/* has_normal_image (g_buffer_generation.inl:197-211): n = normalize(TBN * (sample(normal_image).xyz * 2 - 1)) with
+ * T = normalize(Q1 * st2.t - Q2 * st1.t), B = normalize(cross(N, T)); Q1/Q2 and st1/st2 are dFdx/dFdy of the world
+ * position and uv, taken as FINE derivatives: the same triangle's perspective-correct attributes at the two pixel
+ * centres of the pixel's 2x2 quad in that direction (what helper invocations evaluate). */
+#define SOC_MATERIAL_NORMAL_TEXTURE 4
 
 #define SOC_CULL_NONE 0
 #define SOC_CULL_FRONT 1               /* depth prepass / G-buffer (depth_prepass.inl:45) */

@@ -44,7 +44,8 @@ def test_framebuffer_and_metrics(soc, tmp_path):
     torch.cuda.synchronize()
     rec = json.loads(r.metrics_json(7))
     assert rec["frame"] == 7 and list(rec["groups"]) == GROUPS
-    assert set(rec["passes"]) == set(r.pass_names())
+    # a one-call frame folds the partial histograms in the resolve: the fold pass has no work, no record
+    assert set(rec["passes"]) == set(r.pass_names()) - {"LuminanceHistogramFold"}
     assert rec["total_gpu_ms"] == pytest.approx(sum(rec["passes"].values()), rel=1e-4)
     assert rec["groups"]["Rendering G-Buffer"] > 0 and rec["groups"]["Screen Space Reflections"] == 0
     host = soc.read_image(fr["output"])
