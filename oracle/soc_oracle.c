@@ -1187,7 +1187,8 @@ static v3 rs_normalize(v3 a) {
 }
 
 /* GBufferGeneration from the visibility buffer: vertex stage g_buffer_generation.inl:169-178, fragment
-   stage :189-225 (normal map and metallic/roughness not modelled: composition reads neither). */
+   stage :189-225 incl. the normal-image TBN of :197-211 (metallic/roughness not modelled: composition does
+   not read it). */
 int soc_oracle_gbuffer_resolve(const soc_globals* g, const soc_mesh* mesh, const soc_material* materials,
                                int32_t material_count, const uint64_t* visibility, soc_img depth, soc_img albedo,
                                soc_img emissive, soc_img normal, soc_img velocity) {
@@ -1244,6 +1245,37 @@ int soc_oracle_gbuffer_resolve(const soc_globals* g, const soc_mesh* mesh, const
             } else {
                 n = rs_normalize(V3(b0 * na.x + b1 * nb.x + b2 * nc.x, b0 * na.y + b1 * nb.y + b2 * nc.y,
                                     b0 * na.z + b1 * nb.z + b2 * nc.z));
+            }
+            if ((m->flags & SOC_MATERIAL_NORMAL_TEXTURE) && m->normal_image.data) {   /* g_buffer_generation.inl:197-211 */
+                const v4 t = rs_sample_texture(&m->normal_image, u, v);
+                const v3 tn = V3(t.x * 2.0f - 1.0f, t.y * 2.0f - 1.0f, t.z * 2.0f - 1.0f);
+                v4 wp[3];
+                const uint32_t vi[3] = {ia, ib, ic};
+                for (int k = 0; k < 3; ++k) {
+                    const float* p = mesh->positions + 3 * (size_t)vi[k];
+                    wp[k] = mat_vec4(M, p[0], p[1], p[2], 1.0f);
+                }
+                /* fine dFdx / dFdy: the same triangle's attributes at the two centres of the 2x2 quad per direction */
+                const float qx = (float)(x & ~1) + 0.5f, qy = (float)(y & ~1) + 0.5f;
+                const float sxs[4] = {qx, qx + 1.0f, fx, fx}, sys[4] = {fy, fy, qy, qy + 1.0f};
+                v3 P[4];
+                float tv[4];
+                for (int k = 0; k < 4; ++k) {
+                    const float a0 = rs_edge(r0, sxs[k], sys[k]), a1 = rs_edge(r1, sxs[k], sys[k]), a2 = rs_edge(r2, sxs[k], sys[k]);
+                    const float as = a0 + a1 + a2;
+                    const float c1 = a1 / as, c2 = a2 / as, c0 = 1.0f - c1 - c2;
+                    P[k] = V3(c0 * wp[0].x + c1 * wp[1].x + c2 * wp[2].x, c0 * wp[0].y + c1 * wp[1].y + c2 * wp[2].y,
+                              c0 * wp[0].z + c1 * wp[1].z + c2 * wp[2].z);
+                    tv[k] = c0 * uv[2 * ia + 1] + c1 * uv[2 * ib + 1] + c2 * uv[2 * ic + 1];
+                }
+                const v3 Q1 = V3(P[1].x - P[0].x, P[1].y - P[0].y, P[1].z - P[0].z);
+                const v3 Q2 = V3(P[3].x - P[2].x, P[3].y - P[2].y, P[3].z - P[2].z);
+                const float st1t = tv[1] - tv[0], st2t = tv[3] - tv[2];
+                const v3 N = rs_normalize(n);
+                const v3 T = rs_normalize(V3(Q1.x * st2t - Q2.x * st1t, Q1.y * st2t - Q2.y * st1t, Q1.z * st2t - Q2.z * st1t));
+                const v3 B = rs_normalize(cross3(N, T));
+                n = rs_normalize(V3(T.x * tn.x + B.x * tn.y + N.x * tn.z, T.y * tn.x + B.y * tn.y + N.y * tn.z,
+                                    T.z * tn.x + B.z * tn.y + N.z * tn.z));
             }
             v3 em = V3(0, 0, 0);
             if (m->has_emissive) {

@@ -125,7 +125,7 @@ class Mesh(C.Structure):
 class Material(C.Structure):
     _fields_ = [("albedo", SocImg), ("emissive", SocImg), ("albedo_factor", C.c_float * 4),
                 ("emissive_factor", C.c_float * 4), ("flags", C.c_int32), ("has_emissive", C.c_int32),
-                ("pad", C.c_int32 * 2), ("normal_map", SocImg)]
+                ("pad", C.c_int32 * 2), ("normal_map", SocImg), ("normal_image", SocImg)]
 
 
 class RasterScene(C.Structure):
@@ -156,6 +156,7 @@ PASS_CALLBACK = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.POINTER(Globals), C.POINTER
 CULL_NONE, CULL_FRONT, CULL_BACK = 0, 1, 2
 MATERIAL_ZERO_VELOCITY = 1
 MATERIAL_NORMAL_MAP = 2
+MATERIAL_NORMAL_TEXTURE = 4
 
 STRUCTS = {"soc_img": SocImg, "soc_globals": Globals, "soc_sun_info": SunInfo, "soc_point_light": PointLight,
            "soc_spot_light": SpotLight, "soc_auto_exposure": AutoExposure, "soc_camera": Camera,

@@ -467,6 +467,39 @@ __global__ __launch_bounds__(256) void gbuffer_resolve(soc_mesh mesh, const soc_
         n = normalize_exact(f3{b0 * na.x + b1 * nb.x + b2 * nc.x, b0 * na.y + b1 * nb.y + b2 * nc.y,
                                b0 * na.z + b1 * nb.z + b2 * nc.z});
     }
+    if ((m.flags & SOC_MATERIAL_NORMAL_TEXTURE) && m.normal_image.data) {   // g_buffer_generation.inl:197-211
+        const f4 t = sample_texture(m.normal_image, u, v, lut);
+        const f3 tn{t.x * 2.0f - 1.0f, t.y * 2.0f - 1.0f, t.z * 2.0f - 1.0f};
+        // world positions of the triangle's vertices (vertex stage out_position, :171-172)
+        const float* ps = mesh.positions;
+        const f4 wa = mat_vec_exact(p.model, ps[3 * ia], ps[3 * ia + 1], ps[3 * ia + 2], 1.0f);
+        const f4 wb = mat_vec_exact(p.model, ps[3 * ib], ps[3 * ib + 1], ps[3 * ib + 2], 1.0f);
+        const f4 wc = mat_vec_exact(p.model, ps[3 * ic], ps[3 * ic + 1], ps[3 * ic + 2], 1.0f);
+        // fine dFdx / dFdy: this triangle's attributes at the two centres of the pixel's 2x2 quad per direction
+        auto attr = [&](float sx, float sy, f3& P, float& su, float& sv) {
+            const float a0 = edge(r0, sx, sy), a1 = edge(r1, sx, sy), a2 = edge(r2, sx, sy);
+            const float as = a0 + a1 + a2;
+            const float c1 = a1 / as, c2 = a2 / as, c0 = 1.0f - c1 - c2;
+            P = f3{c0 * wa.x + c1 * wb.x + c2 * wc.x, c0 * wa.y + c1 * wb.y + c2 * wc.y, c0 * wa.z + c1 * wb.z + c2 * wc.z};
+            su = c0 * uv[2 * ia] + c1 * uv[2 * ib] + c2 * uv[2 * ic];
+            sv = c0 * uv[2 * ia + 1] + c1 * uv[2 * ib + 1] + c2 * uv[2 * ic + 1];
+        };
+        const float qx = (float)(x & ~1) + 0.5f, qy = (float)(y & ~1) + 0.5f;
+        f3 px0, px1, py0, py1;
+        float ux0, vx0, ux1, vx1, uy0, vy0, uy1, vy1;
+        attr(qx, fy, px0, ux0, vx0);
+        attr(qx + 1.0f, fy, px1, ux1, vx1);
+        attr(fx, qy, py0, uy0, vy0);
+        attr(fx, qy + 1.0f, py1, uy1, vy1);
+        const f3 Q1{px1.x - px0.x, px1.y - px0.y, px1.z - px0.z}, Q2{py1.x - py0.x, py1.y - py0.y, py1.z - py0.z};
+        const float st1t = vx1 - vx0, st2t = vy1 - vy0;
+        (void)ux0; (void)ux1; (void)uy0; (void)uy1;
+        const f3 N = normalize_exact(n);
+        const f3 T = normalize_exact(f3{Q1.x * st2t - Q2.x * st1t, Q1.y * st2t - Q2.y * st1t, Q1.z * st2t - Q2.z * st1t});
+        const f3 B = normalize_exact(cross_exact(N, T));
+        n = normalize_exact(f3{T.x * tn.x + B.x * tn.y + N.x * tn.z, T.y * tn.x + B.y * tn.y + N.y * tn.z,
+                               T.z * tn.x + B.z * tn.y + N.z * tn.z});
+    }
     f3 em = f3{0.0f, 0.0f, 0.0f};
     if (m.has_emissive) {
         const f4 e = sample_texture(m.emissive, u, v, lut);

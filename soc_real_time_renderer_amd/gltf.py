@@ -97,10 +97,12 @@ def load(path: str, max_texture: Optional[int] = None, images: Optional[dict] = 
         materials.append({
             "albedo": tex(pbr["baseColorTexture"]["index"]) if "baseColorTexture" in pbr else None,
             "emissive": tex(m["emissiveTexture"]["index"]) if "emissiveTexture" in m else None,
+            # normalTexture: UNORM (model.cpp:52-71 makes only baseColor / emissive images sRGB), :217-224
+            "normal": tex(m["normalTexture"]["index"]) if "normalTexture" in m else None,
             "albedo_srgb": True, "emissive_srgb": True,
         })
     if not materials:
-        materials.append({"albedo": None, "emissive": None, "albedo_srgb": True, "emissive_srgb": True})
+        materials.append({"albedo": None, "emissive": None, "normal": None, "albedo_srgb": True, "emissive_srgb": True})
     return {"positions": np.ascontiguousarray(np.concatenate(pos)), "normals": np.ascontiguousarray(np.concatenate(nrm)),
             "uvs": np.ascontiguousarray(np.concatenate(uv)), "indices": np.ascontiguousarray(np.concatenate(idx)),
             "materials": np.ascontiguousarray(np.concatenate(mat)), "material_list": materials, "vertex_count": total}

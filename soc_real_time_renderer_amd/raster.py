@@ -16,7 +16,8 @@ import numpy as np
 import torch
 
 from . import _abi, _check, _gp, _ptr, _stream, img, lib
-from ._abi import (CULL_BACK, CULL_FRONT, CULL_NONE, FMT_RGBA8_SRGB, MATERIAL_NORMAL_MAP, MATERIAL_ZERO_VELOCITY,
+from ._abi import (CULL_BACK, CULL_FRONT, CULL_NONE, FMT_RGBA8_SRGB, FMT_RGBA8_UNORM, MATERIAL_NORMAL_MAP,
+                   MATERIAL_NORMAL_TEXTURE, MATERIAL_ZERO_VELOCITY,
                    Material, Mesh)
 
 __all__ = ["CULL_NONE", "CULL_FRONT", "CULL_BACK", "MATERIAL_ZERO_VELOCITY", "MeshBuffers", "material",
@@ -83,9 +84,10 @@ class MeshBuffers:
 
 
 def material(albedo=None, emissive=None, albedo_factor=(1.0, 1.0, 1.0, 1.0), emissive_factor=(1.0, 1.0, 1.0, 1.0),
-             flags=0, has_emissive: Optional[bool] = None, srgb=True, normal_map=None) -> Material:
+             flags=0, has_emissive: Optional[bool] = None, srgb=True, normal_map=None, normal_texture=None) -> Material:
     """soc_material: albedo / emissive RGBA8 textures ((H, W, 4) uint8 tensors or arrays; sRGB like the
-    reference's baseColor/emissive images, model.cpp:52-71) or None (white / no emissive)."""
+    reference's baseColor/emissive images, model.cpp:52-71) or None (white / no emissive); normal_texture: the
+    glTF tangent-space normal image (RGBA8 UNORM, has_normal_image, g_buffer_generation.inl:197-211)."""
     m = Material()
     fmt = FMT_RGBA8_SRGB if srgb else None
     m.albedo = img(albedo, fmt) if albedo is not None else img(None)
@@ -97,6 +99,9 @@ def material(albedo=None, emissive=None, albedo_factor=(1.0, 1.0, 1.0, 1.0), emi
     m.normal_map = img(normal_map) if normal_map is not None else img(None)
     if normal_map is not None:
         m.flags |= MATERIAL_NORMAL_MAP
+    m.normal_image = img(normal_texture, FMT_RGBA8_UNORM) if normal_texture is not None else img(None)
+    if normal_texture is not None:
+        m.flags |= MATERIAL_NORMAL_TEXTURE
     return m
 
 

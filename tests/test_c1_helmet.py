@@ -2,7 +2,8 @@
 
 The reference's asset (glTF + .bin, baseColor / emissive JPEGs box-downsampled to 256^2; fixture made by
 tools/make_helmet_fixture.py) goes through the glTF ingest (model.cpp restated, quirk Q4: node transform
-ignored), the rasteriser (depth prepass, G-buffer, 2048^2 sun shadow map) and Composition with AO = 1
+ignored), the rasteriser (depth prepass, G-buffer with the normal texture's TBN of g_buffer_generation.inl:197-211,
+2048^2 sun shadow map) and Composition with AO = 1
 (no SSAO pass) and no clouds. The CPU run is the oracle path (the reference's "CPU-runnable case"); the
 GPU run must match it: visibility and shadow map bit-exact, G-buffer / lit colour within the RGBA16F
 tolerance |d| <= 1e-3 + 2e-3|ref|.
@@ -34,7 +35,8 @@ def c1_globals():
 
 def oracle_frame(oracle, g, m):
     mb = raster.MeshBuffers(m["positions"], m["normals"], m["uvs"], m["indices"], m["materials"])
-    mats = [raster.material(albedo=x["albedo"], emissive=x["emissive"]) for x in m["material_list"]]
+    mats = [raster.material(albedo=x["albedo"], emissive=x["emissive"], normal_texture=x["normal"])
+            for x in m["material_list"]]
     vis = np.zeros((H, W), np.uint64)
     oracle.raster_visibility(mb, np.ctypeslib.as_array(g.camera_projection_view_matrix), raster.CULL_FRONT, vis)
     shadow = np.zeros((SHADOW, SHADOW), np.float32)
@@ -60,6 +62,7 @@ def test_gltf_ingest_matches_the_accessors():
     assert np.allclose(np.linalg.norm(m["normals"], axis=1), 1.0, atol=1e-3)
     mat = m["material_list"][0]
     assert mat["albedo"].shape == (256, 256, 4) and mat["emissive"].shape == (256, 256, 4)
+    assert mat["normal"].shape == (256, 256, 4) and mat["normal"][..., 2].mean() > 200   # tangent space: +z
     # glTF faces are counter-clockwise seen from outside: the winding agrees with the vertex normals
     P, I = m["positions"], m["indices"]
     fn = np.cross(P[I[:, 1]] - P[I[:, 0]], P[I[:, 2]] - P[I[:, 0]])
@@ -81,6 +84,14 @@ def test_c1_cpu_frame(oracle):
     # the reference sun (ortho +-16 around y = 40, RH_NO: renderer.cpp:109-133) does not reach the origin:
     # the shadow map stays at its clear value, as in the reference
     assert (shadow == 1.0).all()
+    # the normal texture perturbs the interpolated normals (g_buffer_generation.inl:197-211); unit length
+    n = gb["normal"][cov][:, :3].astype(np.float64)
+    assert np.abs(np.linalg.norm(n, axis=1) - 1.0).max() < 4e-3
+    m = helmet()
+    m["material_list"][0]["normal"] = None
+    _, _, gb_flat, _ = oracle_frame(oracle, g, m)
+    moved = np.abs(gb["normal"][cov][:, :3].astype(np.float64) - gb_flat["normal"][cov][:, :3]).max(axis=1) > 0.05
+    assert 0.1 < moved.mean() < 1.0   # 19 % of the helmet pixels tilt by more than 0.05
 
 
 @pytest.mark.gpu
@@ -91,9 +102,10 @@ def test_c1_gpu_matches_cpu(soc, oracle):
     vis_ref, shadow_ref, gb_ref, color_ref = oracle_frame(oracle, g, m)
     dev = "cuda"
     mb = raster.MeshBuffers.from_numpy(m["positions"], m["normals"], m["uvs"], m["indices"], m["materials"])
-    texs = [{k: (torch.from_numpy(x[k]).to(dev) if x[k] is not None else None) for k in ("albedo", "emissive")}
+    texs = [{k: (torch.from_numpy(x[k]).to(dev) if x[k] is not None else None) for k in ("albedo", "emissive", "normal")}
             for x in m["material_list"]]
-    dmats = raster.materials_device([raster.material(albedo=t["albedo"], emissive=t["emissive"]) for t in texs])
+    dmats = raster.materials_device([raster.material(albedo=t["albedo"], emissive=t["emissive"],
+                                                     normal_texture=t["normal"]) for t in texs])
     ws = mb.workspace()
     vis = torch.zeros((H, W), dtype=torch.int64, device=dev)
     raster.raster_visibility(mb, np.ctypeslib.as_array(g.camera_projection_view_matrix), raster.CULL_FRONT, vis, ws)

@@ -209,6 +209,39 @@ def test_resolve_perspective_correct_attributes(oracle):
     assert np.abs(got - c)[cov].max() < 1.5 / 256 + 2e-3   # 8-bit sub-texel weights + f16 storage
 
 
+def test_resolve_normal_texture_tbn(oracle):
+    """has_normal_image (g_buffer_generation.inl:197-211) on the receding plane y = 0 with uv = (x, z) / 2s: dP/du
+    is +x and dP/dv is +z, so T = normalize(Q1 st2.t - Q2 st1.t) = s x (s = the sign of the screen-space uv
+    Jacobian), B = normalize(cross(N, T)) = -s z, N = +y. A constant tangent normal tn then gives
+    normalize(s tn.x x - s tn.y z + tn.z y) at every covered pixel, whatever the derivatives' magnitudes."""
+    W, H = 64, 48
+    g = globals_for(W, H, camera=((0.0, 2.0, 0.0), (0.0, -0.5, 0.0)), frames=2, move=0.02)
+    vp = np.ctypeslib.as_array(g.camera_projection_view_matrix)
+    s_ = 50.0
+    pos = np.float32([(-s_, 0, -s_), (s_, 0, -s_), (s_, 0, s_), (-s_, 0, s_)])
+    uvs = (pos[:, [0, 2]] + s_) / (2 * s_)
+    m = mesh_np(pos, [(0, 3, 2), (0, 2, 1)], uvs=uvs, normals=np.tile(np.float32([0, 1, 0]), (4, 1)))
+    vis = np.zeros((H, W), np.uint64)
+    oracle.raster_visibility(m, vp, raster.CULL_FRONT, vis)
+    cov = raster.visibility_triangles(vis) >= 0
+    got = {}
+    for name, texel in (("x", (255, 128, 128)), ("y", (128, 255, 128)), ("z", (128, 128, 255)), ("mix", (200, 60, 180))):
+        tex = np.zeros((4, 4, 4), np.uint8)
+        tex[..., :3] = texel
+        tex[..., 3] = 255
+        out = {k: np.zeros((H, W, 4), np.float16) for k in ("albedo", "emissive", "normal", "velocity")}
+        oracle.gbuffer_resolve(g, m, [raster.material(normal_texture=tex)], vis, np.zeros((H, W), np.float32),
+                               out["albedo"], out["emissive"], out["normal"], out["velocity"])
+        got[name] = (out["normal"][cov][:, :3].astype(np.float64), np.float64(texel) / 255.0 * 2 - 1)
+    sign = np.sign(got["x"][0][:, 0])
+    assert (sign == sign[0]).all() and sign[0] != 0
+    sg = sign[0]
+    for name, (n, tn) in got.items():
+        want = np.array([sg * tn[0], tn[2], -sg * tn[1]])
+        want /= np.linalg.norm(want)
+        assert np.abs(n - want).max() < 4e-3, (name, np.abs(n - want).max())
+
+
 @pytest.mark.parametrize("scene_id,camera,cull", [(scene.SPONZA_PROXY, SPONZA_CAMERA, raster.CULL_FRONT),
                                                   (scene.TERRAIN, TERRAIN_CAMERA, raster.CULL_FRONT)])
 def test_raster_matches_the_scene_generator(oracle, scene_id, camera, cull):

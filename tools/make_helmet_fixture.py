@@ -1,5 +1,5 @@
 """Config C1 fixture: the reference's DamagedHelmet asset (assets/DamagedHelmet/glTF, data files) copied as
-glTF JSON + .bin, and its baseColor / emissive JPEGs decoded with Pillow and box-downsampled to 256^2
+glTF JSON + .bin, and its baseColor / emissive / normal JPEGs decoded with Pillow and box-downsampled to 256^2
 RGBA8 (tests/golden/damaged_helmet/textures_256.npz). Run in the container that has /root/reference."""
 import os
 import shutil
@@ -17,5 +17,5 @@ os.makedirs(DST, exist_ok=True)
 for f in ("DamagedHelmet.gltf", "DamagedHelmet.bin"):
     shutil.copyfile(os.path.join(SRC, f), os.path.join(DST, f))
 np.savez_compressed(os.path.join(DST, "textures_256.npz"),
-                    **{name: load_image(os.path.join(SRC, name), 256) for name in ("Default_albedo.jpg", "Default_emissive.jpg")})
+                    **{name: load_image(os.path.join(SRC, name), 256) for name in ("Default_albedo.jpg", "Default_emissive.jpg", "Default_normal.jpg")})
 print("wrote", sorted(os.listdir(DST)))
