@@ -70,6 +70,15 @@ def make_globals(W, H, camera):
     return g
 
 
+def point_lights_c3b(n=128, seed=0x3B):
+    """C3b: 128 point-light entities (PointLightComponent defaults, components.hpp:55-58) scattered
+    through the Sponza-proxy atrium, seeded; fed through Scene::update (soc_scene_update)."""
+    rng = np.random.default_rng(seed)
+    return [soc.entity(position=(rng.uniform(-15.0, 12.0), rng.uniform(0.3, 7.0), rng.uniform(-4.5, 4.5)),
+                       point_light=True, color=rng.uniform(0.3, 1.0, 3), intensity=float(rng.uniform(0.5, 4.0)))
+            for _ in range(n)]
+
+
 def algorithmic_bytes(W, H, f_sky):
     """Bytes each pass must move at the reference formats, per launch."""
     P = W * H
@@ -144,8 +153,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", choices=("c2", "c3", "c4"), default="c3",
-                    help="c3: Sponza-proxy full chain at 4K (the metric's config); c2: the same scene at 1920x1080 "
+    ap.add_argument("--config", choices=("c2", "c3", "c3b", "c4"), default="c3",
+                    help="c3: Sponza-proxy full chain at 4K (the metric's config); c3b: C3 with 128 point lights fed "
+                         "through the ECS scene feed (SURVEY.md §8d); c2: the same scene at 1920x1080 "
                          "(with --raster: deferred lighting + sun shadow map rendered per frame); c4: terrain + "
                          "atmosphere/clouds")
     ap.add_argument("--width", type=int, default=None, help="default 3840 (1920 for c2)")
@@ -178,6 +188,8 @@ def main():
     terrain = args.config == "c4"
     scene_id = scene.TERRAIN if terrain else scene.SPONZA_PROXY
     g = make_globals(W, H, (multi_gpu.terrain_camera_for_rank if terrain else multi_gpu.camera_for_rank)(rank))
+    if args.config == "c3b":
+        soc.scene_update(g, point_lights_c3b())
     gb = scene.gbuffer(g, W, H, scene_id=scene_id)
     shadow = scene.shadow_map(g, 4096, scene_id=scene_id)
     noise = scene.noise_texture()
@@ -297,7 +309,8 @@ def main():
         "data": f"synthetic ({'fBm terrain (seed 0x7E44)' if terrain else 'Sponza-proxy'} G-buffer + 4096^2 sun "
                 f"shadow map, scene_synth.c)",
         "config": {"workload": f"{'Terrain' if terrain else 'Sponza-proxy'} {W}x{H} full screen-space chain "
-                               f"({args.config.upper()}): bloom x8, SSAO+blur, clouds, composition, auto-exposure, "
+                               f"({args.config.upper()}): bloom x8, SSAO+blur, clouds, composition"
+                               f"{' with 128 point lights' if args.config == 'c3b' else ''}, auto-exposure, "
                                f"TAA, AgX tone map",
                    "resolution": [W, H], "f_sky": round(f_sky, 4), "parallelism": f"frame-per-gpu x{world}",
                    "histogram_allreduce": world > 1,

@@ -202,6 +202,29 @@ typedef struct soc_camera {
 int soc_globals_frame_update(soc_globals* g, const soc_camera* cam, int32_t width, int32_t height,
                              float delta_time, uint32_t* jitter_index);
 
+/* ECS scene feed: Scene::update (src/ecs/scene.cpp:47-118). An entity carries a TransformComponent (position,
+ * rotation in degrees, scale; components.hpp) and optionally a PointLightComponent or SpotLightComponent
+ * (color, intensity, cut_off / outer_cut_off in degrees; defaults components.hpp:55-66). soc_scene_update
+ * clears the light counts, then walks the entities in order: every transform gets model = translate(position) *
+ * toMat4(quat(radians(rotation))) * scale(scale) and normal = transpose(inverse(model)) (:64-68); a point light
+ * appends {position, color, intensity}; a spot light appends {position, dir = rotateZ(rotateY(rotateX((0,-1,0),
+ * rx), ry), rz), color, intensity, cos(radians(cut_off)), cos(radians(outer_cut_off))} (:87-116). More than
+ * SOC_MAX_POINT_LIGHTS / SOC_MAX_SPOT_LIGHTS lights (an out-of-bounds write in the reference) is an error. */
+#define SOC_ENTITY_POINT_LIGHT 1
+#define SOC_ENTITY_SPOT_LIGHT 2
+typedef struct soc_entity {
+    float position[3];
+    float rotation[3];       /* degrees */
+    float scale[3];
+    int32_t components;      /* SOC_ENTITY_* (a transform is always present) */
+    float color[3];
+    float intensity;
+    float cut_off, outer_cut_off;   /* degrees (spot lights) */
+} soc_entity;
+/* model_matrices / normal_matrices: optional outputs, count x float[16] (column-major), or NULL. */
+int soc_scene_update(soc_globals* g, const soc_entity* entities, int32_t count, float* model_matrices,
+                     float* normal_matrices);
+
 /* glm restatements used by the feed (exported for tests): column-major float[16]. */
 void soc_mat4_perspective_rh_no(float out[16], float fovy_radians, float aspect, float znear, float zfar);
 void soc_mat4_ortho_rh_no(float out[16], float l, float r, float b, float t, float znear, float zfar);

@@ -139,6 +139,32 @@ def frame_update(g: Globals, camera: Camera, width: int, height: int, delta_time
            "soc_globals_frame_update")
 
 
+def entity(position=(0.0, 0.0, 0.0), rotation=(0.0, 0.0, 0.0), scale=(1.0, 1.0, 1.0), point_light=False,
+           spot_light=False, color=(1.0, 1.0, 1.0), intensity=16.0, cut_off=20.0, outer_cut_off=30.0) -> "_abi.Entity":
+    """soc_entity with the reference component defaults (src/ecs/components.hpp:55-66)."""
+    e = _abi.Entity()
+    e.position[:] = [float(v) for v in position]
+    e.rotation[:] = [float(v) for v in rotation]
+    e.scale[:] = [float(v) for v in scale]
+    e.components = (_abi.ENTITY_POINT_LIGHT if point_light else 0) | (_abi.ENTITY_SPOT_LIGHT if spot_light else 0)
+    e.color[:] = [float(v) for v in color]
+    e.intensity, e.cut_off, e.outer_cut_off = float(intensity), float(cut_off), float(outer_cut_off)
+    return e
+
+
+def scene_update(g: Globals, entities):
+    """Scene::update (scene.cpp:47-118): fills g's light lists; returns the (N, 4, 4) model and normal matrices
+    (row index = glm column, i.e. m[c][r] like glm)."""
+    n = len(entities)
+    arr = (_abi.Entity * max(n, 1))(*entities)
+    models = np.zeros((max(n, 1), 16), np.float32)
+    normals = np.zeros((max(n, 1), 16), np.float32)
+    fp = C.POINTER(C.c_float)
+    _check(lib().soc_scene_update(C.byref(g), arr, n, models.ctypes.data_as(fp), normals.ctypes.data_as(fp)),
+           "soc_scene_update")
+    return models[:n].reshape(n, 4, 4), normals[:n].reshape(n, 4, 4)
+
+
 def auto_exposure_buffer(device="cuda", exposure: float = 0.0) -> torch.Tensor:
     """Device AutoExposure block (shared.inl:39-45) as 257 int32 words: [exposure f32 bits, 256 bins]."""
     t = torch.zeros(1 + _abi.BIN_COUNT, dtype=torch.int32, device=device)

@@ -133,6 +133,15 @@ class RasterScene(C.Structure):
                 ("visibility", C.c_void_p), ("workspace", C.c_void_p)]
 
 
+ENTITY_POINT_LIGHT, ENTITY_SPOT_LIGHT = 1, 2
+
+
+class Entity(C.Structure):
+    """soc_entity: TransformComponent + optional Point/SpotLightComponent (src/ecs/components.hpp)."""
+    _fields_ = [("position", Vec3), ("rotation", Vec3), ("scale", Vec3), ("components", C.c_int32), ("color", Vec3),
+                ("intensity", C.c_float), ("cut_off", C.c_float), ("outer_cut_off", C.c_float)]
+
+
 # enum soc_resource (include/soc_rt.h): the frame resources a pass declares it reads / writes
 RESOURCES = ["ALBEDO", "EMISSIVE", "NORMAL", "DEPTH", "VELOCITY", "SUN_SHADOW", "NOISE", "BLOOM_MIP0", "BLOOM_MIP1",
              "BLOOM_MIP2", "BLOOM_MIP3", "BLOOM_OUTPUT", "SSAO", "SSAO_BLUR", "CLOUDS", "COLOR", "PREVIOUS_COLOR",
@@ -161,7 +170,7 @@ MATERIAL_NORMAL_TEXTURE = 4
 STRUCTS = {"soc_img": SocImg, "soc_globals": Globals, "soc_sun_info": SunInfo, "soc_point_light": PointLight,
            "soc_spot_light": SpotLight, "soc_auto_exposure": AutoExposure, "soc_camera": Camera,
            "soc_frame_images": FrameImages, "soc_mesh": Mesh, "soc_material": Material,
-           "soc_raster_scene": RasterScene, "soc_pass_desc": PassDesc}
+           "soc_raster_scene": RasterScene, "soc_pass_desc": PassDesc, "soc_entity": Entity}
 
 _I = C.c_int
 _P = C.c_void_p
@@ -211,6 +220,8 @@ FUNCTIONS = {
     "soc_renderer_pass_ms": (C.c_float, [_P, C.c_int32]),
     "soc_renderer_current_history": (C.c_int32, [_P]),
     "soc_renderer_set_async": (C.c_int, [_P, C.c_int32]),
+    "soc_scene_update": (_I, [C.POINTER(Globals), C.POINTER(Entity), C.c_int32, C.POINTER(C.c_float),
+                              C.POINTER(C.c_float)]),
     "soc_renderer_add_pass": (_I, [_P, C.POINTER(PassDesc), PASS_CALLBACK, _P, C.c_char_p]),
     "soc_renderer_pass_uses": (_I, [_P, C.c_int32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "soc_renderer_pass_dependencies": (C.c_int32, [_P, C.c_int32, C.POINTER(C.c_int32), C.c_int32]),

@@ -172,6 +172,8 @@ const FieldInfo kFields[] = {
     F(soc_material, normal_image),
     F(soc_raster_scene, mesh), F(soc_raster_scene, materials), F(soc_raster_scene, material_count),
     F(soc_raster_scene, shadow), F(soc_raster_scene, visibility), F(soc_raster_scene, workspace),
+    F(soc_entity, position), F(soc_entity, rotation), F(soc_entity, scale), F(soc_entity, components),
+    F(soc_entity, color), F(soc_entity, intensity), F(soc_entity, cut_off), F(soc_entity, outer_cut_off),
     F(soc_pass_desc, name), F(soc_pass_desc, group), F(soc_pass_desc, phase), F(soc_pass_desc, flags),
     F(soc_pass_desc, read_count), F(soc_pass_desc, write_count), F(soc_pass_desc, reads), F(soc_pass_desc, writes),
 };
@@ -195,6 +197,7 @@ extern "C" size_t soc_abi_sizeof(const char* t) {
     if (s == "soc_material") return sizeof(soc_material);
     if (s == "soc_raster_scene") return sizeof(soc_raster_scene);
     if (s == "soc_pass_desc") return sizeof(soc_pass_desc);
+    if (s == "soc_entity") return sizeof(soc_entity);
     return 0;
 }
 
@@ -455,6 +458,95 @@ extern "C" int soc_globals_frame_update(soc_globals* g, const soc_camera* cam, i
     g->delta_time = delta_time;
     g->elapsed_time += delta_time;
     g->frame_counter++;
+    return SOC_OK;
+}
+
+// Scene::update (src/ecs/scene.cpp:47-118): transforms (glm translate * toMat4(quat(euler)) * scale, and
+// transpose(inverse(model))) and the light lists.
+static void quat_euler_to_mat4(float out[16], const float euler_rad[3]) {
+    // glm::qua(vec3 eulerAngle) (gtc/quaternion.inl) then mat3_cast / toMat4 (gtx/quaternion.inl)
+    const float cx = std::cos(euler_rad[0] * 0.5f), cy = std::cos(euler_rad[1] * 0.5f), cz = std::cos(euler_rad[2] * 0.5f);
+    const float sx = std::sin(euler_rad[0] * 0.5f), sy = std::sin(euler_rad[1] * 0.5f), sz = std::sin(euler_rad[2] * 0.5f);
+    const float w = cx * cy * cz + sx * sy * sz;
+    const float x = sx * cy * cz - cx * sy * sz;
+    const float y = cx * sy * cz + sx * cy * sz;
+    const float z = cx * cy * sz - sx * sy * cz;
+    const float qxx = x * x, qyy = y * y, qzz = z * z, qxz = x * z, qxy = x * y, qyz = y * z, qwx = w * x, qwy = w * y,
+                qwz = w * z;
+    ident(out);
+    out[0 * 4 + 0] = 1.0f - 2.0f * (qyy + qzz);
+    out[0 * 4 + 1] = 2.0f * (qxy + qwz);
+    out[0 * 4 + 2] = 2.0f * (qxz - qwy);
+    out[1 * 4 + 0] = 2.0f * (qxy - qwz);
+    out[1 * 4 + 1] = 1.0f - 2.0f * (qxx + qzz);
+    out[1 * 4 + 2] = 2.0f * (qyz + qwx);
+    out[2 * 4 + 0] = 2.0f * (qxz + qwy);
+    out[2 * 4 + 1] = 2.0f * (qyz - qwx);
+    out[2 * 4 + 2] = 1.0f - 2.0f * (qxx + qyy);
+}
+
+extern "C" int soc_scene_update(soc_globals* g, const soc_entity* e, int32_t count, float* model_matrices,
+                                float* normal_matrices) {
+    if (!g || count < 0 || (count > 0 && !e)) return set_error(SOC_E_INVALID_ARG, "soc_scene_update: bad arguments");
+    int np = 0, ns = 0;
+    for (int i = 0; i < count; ++i) {
+        np += (e[i].components & SOC_ENTITY_POINT_LIGHT) ? 1 : 0;
+        ns += (e[i].components & SOC_ENTITY_SPOT_LIGHT) ? 1 : 0;
+    }
+    if (np > SOC_MAX_POINT_LIGHTS || ns > SOC_MAX_SPOT_LIGHTS)
+        return set_error(SOC_E_SHAPE, "soc_scene_update: %d point / %d spot lights exceed %d / %d", np, ns,
+                         SOC_MAX_POINT_LIGHTS, SOC_MAX_SPOT_LIGHTS);
+    g->point_light_count = 0;
+    g->spot_light_count = 0;
+    for (int i = 0; i < count; ++i) {
+        const soc_entity& t = e[i];
+        if (model_matrices || normal_matrices) {   // scene.cpp:64-68
+            float T[16], R[16], S[16], TR[16], M[16], inv[16];
+            ident(T);
+            T[12] = t.position[0];
+            T[13] = t.position[1];
+            T[14] = t.position[2];
+            const float eul[3] = {radians(t.rotation[0]), radians(t.rotation[1]), radians(t.rotation[2])};
+            quat_euler_to_mat4(R, eul);
+            ident(S);
+            S[0] = t.scale[0];
+            S[5] = t.scale[1];
+            S[10] = t.scale[2];
+            mat4_mul_host(TR, T, R);
+            mat4_mul_host(M, TR, S);
+            if (model_matrices) std::memcpy(model_matrices + 16 * i, M, sizeof M);
+            if (normal_matrices) {
+                soc_mat4_inverse(inv, M);
+                for (int c = 0; c < 4; ++c)
+                    for (int r = 0; r < 4; ++r) normal_matrices[16 * i + c * 4 + r] = inv[r * 4 + c];
+            }
+        }
+        if (t.components & SOC_ENTITY_POINT_LIGHT) {   // scene.cpp:87-96
+            soc_point_light& L = g->point_lights[g->point_light_count++];
+            for (int k = 0; k < 3; ++k) {
+                L.position[k] = t.position[k];
+                L.color[k] = t.color[k];
+            }
+            L.intensity = t.intensity;
+        }
+        if (t.components & SOC_ENTITY_SPOT_LIGHT) {    // scene.cpp:98-116
+            V3h dir{0.0f, -1.0f, 0.0f};
+            dir = rotate_x(dir, radians(t.rotation[0]));
+            dir = rotate_y(dir, radians(t.rotation[1]));
+            dir = rotate_z(dir, radians(t.rotation[2]));
+            soc_spot_light& L = g->spot_lights[g->spot_light_count++];
+            for (int k = 0; k < 3; ++k) {
+                L.position[k] = t.position[k];
+                L.color[k] = t.color[k];
+            }
+            L.direction[0] = dir.x;
+            L.direction[1] = dir.y;
+            L.direction[2] = dir.z;
+            L.intensity = t.intensity;
+            L.cut_off = std::cos(radians(t.cut_off));
+            L.outer_cut_off = std::cos(radians(t.outer_cut_off));
+        }
+    }
     return SOC_OK;
 }
 

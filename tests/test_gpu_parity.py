@@ -624,3 +624,27 @@ def test_render_graph_split_phases_bit_identical(soc):
     for k in outs[0]:
         assert torch.equal(outs[0][k], outs[1][k]), k
     assert int(outs[0]["auto_exposure"][1:].abs().sum()) == 0   # bins consumed by the resolve
+
+
+def test_render_graph_c3b_lights(soc, oracle):
+    """Config C3b: 128 point lights from the ECS scene feed (soc_scene_update, scene.cpp:47-118) through the render
+    graph (per-frame globals upload, composition light loops) against the oracle's composition."""
+    import bench
+    W, H = 320, 180
+    g, gb = sponza_inputs(W, H, elapsed=10.0)
+    soc.scene_update(g, bench.point_lights_c3b())
+    assert g.point_light_count == 128
+    fr = soc.alloc_frame(W, H, DEV, bloom_output=True)
+    for k in ("albedo", "emissive", "normal", "velocity", "depth"):
+        fr[k].copy_(torch.from_numpy(gb[k]))
+    fr["shadow"] = dev(gb["shadow"])
+    fr["noise"].copy_(torch.from_numpy(gb["noise"]))
+    r = soc.Renderer(fr)
+    r.execute(g)
+    torch.cuda.synchronize()
+    ref = np.zeros((H, W, 4), np.float16)
+    oracle.composition(g, ref, gb["albedo"], host(fr["bloom_output"]), gb["normal"], gb["depth"], host(fr["ssao_blur"]),
+                       gb["shadow"], host(fr["clouds"]))
+    ok = f16_close(host(fr["color"]), ref)
+    assert ok.mean() >= 0.9995, ok.mean()
+    r.close()
