@@ -38,39 +38,62 @@ __device__ __forceinline__ float fast_pow(float x, float y) {
     return __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x));
 }
 
-// composition.inl:124-139
-__device__ f3 point_light(const soc_point_light& L, f3 frag_color, f3 normal, f3 pos, f3 cam) {
-    f3 lp = mk3(L.position[0], L.position[1], L.position[2]);
-    f3 light_dir = normalize3(lp - pos);
-    float distance = length3(lp - pos);
-    float attenuation = 1.0f / (distance * distance);
-    f3 view_dir = normalize3(cam - pos);
-    f3 halfway = normalize3(light_dir + view_dir);
-    float diffuse = fmaxf(dot3(normal, light_dir), 0.0f);
-    float nh = acosf(dot3(halfway, normal));
-    float ex = nh * 1.0f;
-    ex = -(ex * ex);
-    f3 lc = mk3(L.color[0], L.color[1], L.color[2]);
-    return frag_color * lc * (diffuse + expf(ex)) * attenuation * L.intensity;
+// acos on the native units: Abramowitz & Stegun 4.4.46, acos(a) = sqrt(1 - a) * P7(a) for a in [0, 1]
+// (|error| <= 2e-8 rad), acos(x) = pi - acos(-x) below 0. Outside [-1, 1] the sqrt gives NaN, as acos does.
+__device__ __forceinline__ float acos_fast(float x) {
+    const float a = fabsf(x);
+    float r = -0.0012624911f;
+    r = __builtin_fmaf(r, a, 0.0066700901f);
+    r = __builtin_fmaf(r, a, -0.0170881256f);
+    r = __builtin_fmaf(r, a, 0.0308918810f);
+    r = __builtin_fmaf(r, a, -0.0501743046f);
+    r = __builtin_fmaf(r, a, 0.0889789874f);
+    r = __builtin_fmaf(r, a, -0.2145988016f);
+    r = __builtin_fmaf(r, a, 1.5707963050f);
+    r *= __builtin_amdgcn_sqrtf(1.0f - a);
+    return x < 0.0f ? 3.14159265358979f - r : r;
 }
 
-// composition.inl:141-160
-__device__ f3 spot_light(const soc_spot_light& L, f3 frag_color, f3 normal, f3 pos, f3 cam) {
-    f3 lp = mk3(L.position[0], L.position[1], L.position[2]);
-    f3 light_dir = normalize3(lp - pos);
-    float theta = dot3(light_dir, normalize3(-mk3(L.direction[0], L.direction[1], L.direction[2])));
-    float epsilon = L.cut_off - L.outer_cut_off;
-    float intensity = clampf((theta - L.outer_cut_off) / epsilon, 0.0f, 1.0f);
-    float distance = length3(lp - pos);
-    float attenuation = 1.0f / (distance * distance);
-    f3 view_dir = normalize3(cam - pos);
-    f3 halfway = normalize3(light_dir + view_dir);
-    float diffuse = fmaxf(dot3(normal, light_dir), 0.0f);
-    float nh = acosf(dot3(halfway, normal));
-    float ex = nh / 1.0f;
-    ex = -(ex * ex);
-    f3 lc = mk3(L.color[0], L.color[1], L.color[2]);
-    return frag_color * lc * (diffuse + expf(ex)) * attenuation * L.intensity * intensity;
+// The light loops of composition.inl:124-160, per light: L = light - pos, one rsqrt gives light_dir and the
+// attenuation 1 / distance^2; dot(normalize(light_dir + view_dir), n) with one more rsqrt; acos on the native
+// units (acos_fast) and exp(-x^2) as a native exp2. The pixel's view_dir is hoisted out of the loop and the
+// frag_color (albedo) factor out of the sum. Within the RGBA16F tolerance of the oracle's libm restatement.
+// Light records are wave-uniform (scalar loads from the device globals).
+__device__ __forceinline__ f3 light_sum(const soc_globals* __restrict__ dg, uint32_t npl, uint32_t nsl, f3 n, f3 pos,
+                                        f3 cam) {
+    const f3 vd0 = cam - pos;
+    const f3 view_dir = vd0 * __builtin_amdgcn_rsqf(dot3(vd0, vd0));
+    f3 acc = f3{0.0f, 0.0f, 0.0f};
+    constexpr float kLog2e = 1.44269504088896f;
+#pragma unroll 4
+    for (uint32_t i = 0; i < npl; ++i) {            // calculate_point_light, :124-139
+        const soc_point_light& L = dg->point_lights[i];
+        const f3 l = mk3(L.position[0], L.position[1], L.position[2]) - pos;
+        const float inv = __builtin_amdgcn_rsqf(dot3(l, l));
+        const f3 ld = l * inv;
+        const f3 h = ld + view_dir;
+        const float nh = acos_fast(dot3(h, n) * __builtin_amdgcn_rsqf(dot3(h, h)));
+        const float diffuse = fmaxf(dot3(n, ld), 0.0f);
+        const float s = (diffuse + __builtin_amdgcn_exp2f(-(nh * nh) * kLog2e)) * (inv * inv) * L.intensity;
+        acc = acc + mk3(L.color[0], L.color[1], L.color[2]) * s;
+    }
+#pragma unroll 2
+    for (uint32_t i = 0; i < nsl; ++i) {            // calculate_spot_light, :141-160
+        const soc_spot_light& L = dg->spot_lights[i];
+        const f3 l = mk3(L.position[0], L.position[1], L.position[2]) - pos;
+        const float inv = __builtin_amdgcn_rsqf(dot3(l, l));
+        const f3 ld = l * inv;
+        const f3 sd = -mk3(L.direction[0], L.direction[1], L.direction[2]);
+        const float theta = dot3(ld, sd) * __builtin_amdgcn_rsqf(dot3(sd, sd));
+        const float intensity = clampf((theta - L.outer_cut_off) / (L.cut_off - L.outer_cut_off), 0.0f, 1.0f);
+        const f3 h = ld + view_dir;
+        const float nh = acos_fast(dot3(h, n) * __builtin_amdgcn_rsqf(dot3(h, h)));
+        const float diffuse = fmaxf(dot3(n, ld), 0.0f);
+        const float s =
+            (diffuse + __builtin_amdgcn_exp2f(-(nh * nh) * kLog2e)) * (inv * inv) * L.intensity * intensity;
+        acc = acc + mk3(L.color[0], L.color[1], L.color[2]) * s;
+    }
+    return acc;
 }
 
 // Shading of one pixel given its G-buffer values (composition.inl:164-224).
@@ -105,8 +128,7 @@ __device__ __forceinline__ f4 shade(const CompParams& p, float u, float v, float
         const f4 ws = mul(p.inv_view, vs);
         const f3 wp = f3{ws.x, ws.y, ws.z};
         const f3 cam = mk3(p.cam[0], p.cam[1], p.cam[2]);
-        for (uint32_t i = 0; i < p.npl; ++i) direct = direct + point_light(p.dg->point_lights[i], albedo, n, wp, cam);
-        for (uint32_t i = 0; i < p.nsl; ++i) direct = direct + spot_light(p.dg->spot_lights[i], albedo, n, wp, cam);
+        direct = direct + albedo * light_sum(p.dg, p.npl, p.nsl, n, wp, cam);
     }
     const f3 c = (direct + mk3(p.ambient[0], p.ambient[1], p.ambient[2])) * albedo * occl + em;
     return f4{c.x, c.y, c.z, 1.0f};
