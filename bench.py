@@ -104,7 +104,7 @@ def algorithmic_bytes(W, H, f_sky):
     return b
 
 
-def pmc_traffic(kernel, W, H):
+def pmc_traffic(kernel, W, H, scene_name="mesh"):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC table (profiles/, written by
     tools/pmc_summary.py --traffic from a run of this same workload), or None."""
     import glob
@@ -114,7 +114,7 @@ def pmc_traffic(kernel, W, H):
     with open(files[-1]) as fh:
         t = json.load(fh)
     k = t.get("kernels", {}).get(kernel)
-    if not k or list(t.get("resolution", [])) != [W, H]:
+    if not k or list(t.get("resolution", [])) != [W, H] or t.get("scene", "boxes") != scene_name:
         return None, None
     return k["hbm_bytes"], os.path.relpath(files[-1], ROOT)
 
@@ -158,6 +158,9 @@ def main():
                          "through the ECS scene feed (SURVEY.md §8d); c2: the same scene at 1920x1080 "
                          "(with --raster: deferred lighting + sun shadow map rendered per frame); c4: terrain + "
                          "atmosphere/clouds")
+    ap.add_argument("--scene", choices=("mesh", "boxes"), default="mesh",
+                    help="c2/c3/c3b scene: mesh = the Sponza-proxy mesh (~256k triangles, the reference's Sponza "
+                         "textures; rasterised by the HIP rasteriser); boxes = the round-1 analytic box atrium")
     ap.add_argument("--width", type=int, default=None, help="default 3840 (1920 for c2)")
     ap.add_argument("--height", type=int, default=None, help="default 2160 (1080 for c2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -184,14 +187,23 @@ def main():
     W = args.width or (1920 if args.config == "c2" else 3840)
     H = args.height or (1080 if args.config == "c2" else 2160)
 
-    # ---- inputs (synthetic Sponza-proxy or terrain G-buffer + 4096^2 sun shadow map), resident in HBM ----
+    # ---- inputs (Sponza-proxy mesh or terrain G-buffer + 4096^2 sun shadow map), resident in HBM ----
     terrain = args.config == "c4"
-    scene_id = scene.TERRAIN if terrain else scene.SPONZA_PROXY
+    scene_id = scene.TERRAIN if terrain else (scene.SPONZA_PROXY if args.scene == "boxes" else scene.SPONZA_MESH)
     g = make_globals(W, H, (multi_gpu.terrain_camera_for_rank if terrain else multi_gpu.camera_for_rank)(rank))
     if args.config == "c3b":
         soc.scene_update(g, point_lights_c3b())
-    gb = scene.gbuffer(g, W, H, scene_id=scene_id)
-    shadow = scene.shadow_map(g, 4096, scene_id=scene_id)
+    sc = None
+    if scene_id == scene.SPONZA_MESH:
+        # rasterised once by the HIP rasteriser (DepthPrepass + GBufferGeneration + SunShadowDraw), not timed
+        sc = raster.scene_setup(g, scene_id, tex_size=256, device=device)
+        gbd = raster.render_gbuffer(g, sc, W, H, 4096, device)
+        torch.cuda.synchronize()
+        gb = {k: gbd[k].cpu().numpy() for k in ("albedo", "emissive", "normal", "velocity", "depth")}
+        shadow = gbd["shadow"].cpu().numpy()
+    else:
+        gb = scene.gbuffer(g, W, H, scene_id=scene_id)
+        shadow = scene.shadow_map(g, 4096, scene_id=scene_id)
     noise = scene.noise_texture()
     f_sky = float((gb["depth"] == 1.0).mean())
     fr = soc.alloc_frame(W, H, device, bloom_output=True)
@@ -201,7 +213,8 @@ def main():
     fr["noise"].copy_(torch.from_numpy(noise))
     r = soc.Renderer(fr, sky_lane=not args.no_sky_lane, fused_histogram=not args.unfused_histogram)
     if args.raster:
-        sc = raster.scene_setup(g, scene_id, tex_size=1024, device=device)
+        if sc is None:
+            sc = raster.scene_setup(g, scene_id, tex_size=1024, device=device)
         vis = torch.empty((H, W), dtype=torch.int64, device=device)
         r.set_raster_scene(sc["mesh"], sc["materials"], sc["material_count"], vis, sc["workspace"], shadow=True)
     r.set_exposure_pixels(*multi_gpu.exposure_pixels(world, W, H))
@@ -283,8 +296,8 @@ def main():
     # the committed PMC table comes from the default command (C3, G-buffer resident): other workloads get null
     pmc_ok = args.config == "c3" and not args.raster
     comp_kernel = "composition_pair<true, false, 3>" if comp != "Composition" else "composition_pair<false, false, 3>"
-    traffic, traffic_src = pmc_traffic(comp_kernel, W, H) if pmc_ok else (None, None)
-    ssao_traffic, _ = pmc_traffic(SSAO_KERNEL, W, H) if pmc_ok else (None, None)
+    traffic, traffic_src = pmc_traffic(comp_kernel, W, H, args.scene) if pmc_ok else (None, None)
+    ssao_traffic, _ = pmc_traffic(SSAO_KERNEL, W, H, args.scene) if pmc_ok else (None, None)
     pair_traffic = traffic + ssao_traffic if traffic is not None and ssao_traffic is not None else None
     pair_achieved = ns_bytes / (ns_us * 1e-6) / 1e9
 
@@ -306,8 +319,9 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32 (fp16/unorm8/d32 storage)",
-        "data": f"synthetic ({'fBm terrain (seed 0x7E44)' if terrain else 'Sponza-proxy'} G-buffer + 4096^2 sun "
-                f"shadow map, scene_synth.c)",
+        "data": (f"synthetic: fBm terrain (seed 0x7E44) G-buffer + 4096^2 sun shadow map (scene_synth.c)" if terrain else
+                 f"synthetic: Sponza-proxy {'box atrium (scene_synth.c)' if sc is None else 'mesh (procedural atrium, ' + str(int(sc['mesh'].struct.triangle_count)) + ' triangles, the reference Sponza baseColor/normal textures at 256^2, seed 0x5050)'}; "
+                 f"G-buffer + 4096^2 sun shadow map {'ray-cast on the host' if sc is None else 'rasterised once by the HIP rasteriser'}"),
         "config": {"workload": f"{'Terrain' if terrain else 'Sponza-proxy'} {W}x{H} full screen-space chain "
                                f"({args.config.upper()}): bloom x8, SSAO+blur, clouds, composition"
                                f"{' with 128 point lights' if args.config == 'c3b' else ''}, auto-exposure, "

@@ -143,10 +143,37 @@ def visibility_triangles(vis) -> np.ndarray:
     return np.where(low == 0xFFFFFFFF, -1, 0xFFFFFFFE - low)
 
 
+def sponza_mesh_materials(tex_size: Optional[int] = None, device=None):
+    """The 25 Sponza materials of the mesh proxy: baseColor (sRGB) and normal (UNORM) textures from the fixture;
+    no emissive image (Sponza has none); albedo factor 1 (GBufferGeneration ignores baseColorFactor,
+    g_buffer_generation.inl:189-194). Returns (materials, textures kept alive)."""
+    from .scene import sponza_mesh
+    tex = sponza_mesh.load_textures(tex_size)
+    keep, mats = [], []
+    for i in range(len(sponza_mesh.GLTF_TRIANGLES)):
+        t = tex.get(i, {})
+        a, n = t.get("albedo"), t.get("normal")
+        if device is not None:
+            a = torch.from_numpy(a).to(device) if a is not None else None
+            n = torch.from_numpy(n).to(device) if n is not None else None
+        keep += [a, n]
+        mats.append(material(albedo=a, normal_texture=n))
+    return mats, keep
+
+
 def scene_setup(g, scene_id: int, tex_size: int = 512, device="cuda") -> dict:
-    """Device mesh, textures and material array of a synthetic scene (scene_synth.c): the Sponza-proxy
-    (sRGB tiled textures, emissive lamps) or the terrain (UNORM albedo, velocity 0 as draw_terrain.inl:221)."""
+    """Device mesh, textures and material array of a synthetic scene: the Sponza-proxy mesh (sponza_mesh.py, the
+    reference's Sponza textures), the box atrium (scene_synth.c: sRGB tiled textures, emissive lamps) or the terrain
+    (UNORM albedo, velocity 0 as draw_terrain.inl:221)."""
     from . import scene as _scene
+    if scene_id == _scene.SPONZA_MESH:
+        from .scene import sponza_mesh
+        m = sponza_mesh.build()
+        mesh = MeshBuffers.from_numpy(m["positions"], m["normals"], m["uvs"], m["indices"], m["materials"],
+                                      device=device)
+        mats, keep = sponza_mesh_materials(tex_size, device)
+        return {"mesh": mesh, "textures": keep, "normal_map": None, "materials": materials_device(mats, device),
+                "material_count": len(mats), "host_mesh": m, "workspace": mesh.workspace(device)}
     m = _scene.mesh(g, scene_id)
     mesh = MeshBuffers.from_numpy(m["positions"], m["normals"], m["uvs"], m["indices"], m["materials"], device=device)
     tex, em = _scene.material_textures(g, tex_size, scene_id)
@@ -164,6 +191,23 @@ def scene_setup(g, scene_id: int, tex_size: int = 512, device="cuda") -> dict:
     return {"mesh": mesh, "textures": dtex, "normal_map": nmap, "materials": materials_device(mats, device),
             "material_count": len(mats), "host_mesh": m, "host_textures": tex, "emissive": em,
             "workspace": mesh.workspace(device)}
+
+
+def render_gbuffer(g, sc: dict, width: int, height: int, shadow_size: int = 4096, device="cuda") -> dict:
+    """The G-buffer (depth prepass + GBufferGeneration) and the sun shadow map (SunShadowDraw) of a scene_setup()
+    scene, rendered once by the HIP rasteriser into device images (the inputs of the screen-space chain)."""
+    f16 = dict(dtype=torch.float16, device=device)
+    out = {k: torch.zeros((height, width, 4), **f16) for k in ("albedo", "emissive", "normal", "velocity")}
+    out["depth"] = torch.ones((height, width), dtype=torch.float32, device=device)
+    out["shadow"] = torch.ones((shadow_size, shadow_size), dtype=torch.float32, device=device)
+    vis = torch.empty((height, width), dtype=torch.int64, device=device)
+    raster_visibility(sc["mesh"], np.ctypeslib.as_array(g.camera_projection_view_matrix), CULL_FRONT, vis,
+                      sc["workspace"])
+    gbuffer_resolve(g, sc["mesh"], sc["materials"], sc["material_count"], vis, out["depth"], out["albedo"],
+                    out["emissive"], out["normal"], out["velocity"], sc["workspace"])
+    raster_depth(sc["mesh"], np.ctypeslib.as_array(g.sun_info.projection_view_matrix), CULL_BACK, out["shadow"],
+                 sc["workspace"], SHADOW_BIAS_CONSTANT, SHADOW_BIAS_SLOPE)
+    return out
 
 
 def height_to_normal(heightmap, normal_target, stream=None):

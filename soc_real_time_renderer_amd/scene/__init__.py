@@ -16,8 +16,9 @@ from .._abi import Globals
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(HERE), "lib", "libsoc_scene.so")
 NOISE_PATH = os.path.join(os.path.dirname(HERE), "data", "clouds_noise_64x64.u8")
-SPONZA_PROXY = 0
+SPONZA_PROXY = 0     # the analytic box atrium (ray-cast on the host): unit tests
 TERRAIN = 1          # config C4: fBm terrain grid (seed 0x7E44) rasterised on the host
+SPONZA_MESH = 2      # configs C2/C3/C5: the ~256k-triangle procedural atrium with the Sponza textures (sponza_mesh.py)
 
 _LIB = None
 

@@ -85,3 +85,26 @@ def host_frame(W, H, gb, output_format=soc.FMT_RGBA8_UNORM):
         fr["output"] = np.zeros((H, W, 4), np.float32)
     fr["output_format"] = output_format
     return fr
+
+
+def sponza_mesh_inputs(W, H, shadow_size=512, tex_size=64, **kw):
+    """Config C2/C3 inputs from the Sponza-proxy mesh (scene/sponza_mesh.py), rasterised by the CPU oracle:
+    G-buffer (with the Sponza baseColor / normal textures) and the sun shadow map."""
+    import oracle
+    from soc_real_time_renderer_amd import raster
+    from soc_real_time_renderer_amd.scene import sponza_mesh
+    g = globals_for(W, H, **kw)
+    m = sponza_mesh.build()
+    mb = raster.MeshBuffers(m["positions"], m["normals"], m["uvs"], m["indices"], m["materials"])
+    mats, _ = raster.sponza_mesh_materials(tex_size)
+    vis = np.zeros((H, W), np.uint64)
+    oracle.raster_visibility(mb, np.ctypeslib.as_array(g.camera_projection_view_matrix), raster.CULL_FRONT, vis)
+    gb = {k: np.zeros((H, W, 4), np.float16) for k in ("albedo", "emissive", "normal", "velocity")}
+    gb["depth"] = np.zeros((H, W), np.float32)
+    oracle.gbuffer_resolve(g, mb, mats, vis, gb["depth"], gb["albedo"], gb["emissive"], gb["normal"], gb["velocity"])
+    gb["shadow"] = np.zeros((shadow_size, shadow_size), np.float32)
+    oracle.raster_depth(mb, np.ctypeslib.as_array(g.sun_info.projection_view_matrix), raster.CULL_BACK, gb["shadow"],
+                        raster.SHADOW_BIAS_CONSTANT, raster.SHADOW_BIAS_SLOPE)
+    gb["noise"] = scene.noise_texture()
+    gb["visibility"] = vis
+    return g, gb

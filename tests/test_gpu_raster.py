@@ -243,3 +243,79 @@ def test_end_to_end_frames_vs_oracle(soc, oracle, scene_id, camera):
         assert (d <= 2).mean() >= 0.995, (f, (d <= 2).mean())
         assert abs(soc.exposure_of(fr["auto_exposure"]) - ae.exposure) <= 1e-4
     r.close()
+
+
+# ------------------------------------------------------------------------------------------------ Sponza-proxy mesh
+def _mesh_scene():
+    from soc_real_time_renderer_amd.scene import sponza_mesh
+    m = sponza_mesh.build()
+    host_mesh = raster.MeshBuffers(m["positions"], m["normals"], m["uvs"], m["indices"], m["materials"])
+    dev_mesh = raster.MeshBuffers.from_numpy(m["positions"], m["normals"], m["uvs"], m["indices"], m["materials"])
+    return host_mesh, dev_mesh
+
+
+@pytest.mark.parametrize("W,H,rank", [(320, 180, 0), (480, 270, 3)])
+def test_sponza_mesh_gbuffer_vs_oracle(soc, oracle, W, H, rank):
+    """The C2/C3 input producer: the ~261k-triangle Sponza-proxy mesh with the Sponza baseColor + normal textures
+    (normal-image TBN): visibility and 1024^2 shadow map bit-exact, G-buffer within the RGBA16F tolerance."""
+    from soc_real_time_renderer_amd import multi_gpu
+    g = globals_for(W, H, camera=multi_gpu.camera_for_rank(rank))
+    hm, dm = _mesh_scene()
+    mats_h, _ = raster.sponza_mesh_materials(64)
+    mats_d, keep = raster.sponza_mesh_materials(64, DEV)
+    dmats = raster.materials_device(mats_d)
+    vp = np.ctypeslib.as_array(g.camera_projection_view_matrix)
+    vis_ref = np.zeros((H, W), np.uint64)
+    oracle.raster_visibility(hm, vp, raster.CULL_FRONT, vis_ref)
+    ref = {k: np.zeros((H, W, 4), np.float16) for k in ("albedo", "emissive", "normal", "velocity")}
+    ref["depth"] = np.zeros((H, W), np.float32)
+    oracle.gbuffer_resolve(g, hm, mats_h, vis_ref, ref["depth"], ref["albedo"], ref["emissive"], ref["normal"],
+                           ref["velocity"])
+    ws = dm.workspace()
+    vis = torch.zeros((H, W), dtype=torch.int64, device=DEV)
+    raster.raster_visibility(dm, vp, raster.CULL_FRONT, vis, ws)
+    out = {k: torch.zeros((H, W, 4), dtype=torch.float16, device=DEV) for k in ("albedo", "emissive", "normal", "velocity")}
+    out["depth"] = torch.zeros((H, W), dtype=torch.float32, device=DEV)
+    raster.gbuffer_resolve(g, dm, dmats, len(mats_d), vis, out["depth"], out["albedo"], out["emissive"], out["normal"],
+                           out["velocity"], ws)
+    assert np.array_equal(host(vis).view(np.uint64), vis_ref)
+    assert np.array_equal(host(out["depth"]), ref["depth"])
+    for k in ("albedo", "emissive", "normal", "velocity"):
+        ok = f16_close(host(out[k]), ref[k])
+        assert ok.mean() >= 0.9999, (k, ok.mean())
+    S = 1024
+    sh_ref = np.zeros((S, S), np.float32)
+    oracle.raster_depth(hm, np.ctypeslib.as_array(g.sun_info.projection_view_matrix), raster.CULL_BACK, sh_ref,
+                        raster.SHADOW_BIAS_CONSTANT, raster.SHADOW_BIAS_SLOPE)
+    sh = torch.zeros((S, S), dtype=torch.float32, device=DEV)
+    raster.raster_depth(dm, np.ctypeslib.as_array(g.sun_info.projection_view_matrix), raster.CULL_BACK, sh, ws,
+                        raster.SHADOW_BIAS_CONSTANT, raster.SHADOW_BIAS_SLOPE)
+    assert np.array_equal(host(sh), sh_ref)
+    assert (sh_ref < 1.0).mean() > 0.001       # the canopy and the atrium top cast into the map
+
+
+def test_sponza_mesh_frames_vs_oracle(soc, oracle):
+    """Two render-graph frames on the Sponza-proxy mesh G-buffer (the C3 scene at 320x180) against the oracle."""
+    from helpers import host_frame, sponza_mesh_inputs
+    W, H = 320, 180
+    g, gb = sponza_mesh_inputs(W, H, shadow_size=512, elapsed=10.0)
+    fr = soc.alloc_frame(W, H, DEV)
+    for k in ("albedo", "emissive", "normal", "velocity", "depth"):
+        fr[k].copy_(torch.from_numpy(gb[k]))
+    fr["shadow"] = torch.from_numpy(gb["shadow"]).to(DEV)
+    fr["noise"].copy_(torch.from_numpy(gb["noise"]))
+    r = soc.Renderer(fr)
+    hf = host_frame(W, H, gb)
+    ae = soc.AutoExposure()
+    hist = 0
+    for f in range(2):
+        fr["emissive"].copy_(torch.from_numpy(gb["emissive"]))
+        hf["emissive"][...] = gb["emissive"]
+        r.execute(g)
+        hist = oracle.frame(g, hf, ae, hist=hist)
+        ok = f16_close(host(fr["color"]), hf["color"], atol=4e-3, rtol=8e-3)
+        assert ok.mean() >= 0.999, (f, ok.mean())
+        d = np.abs(host(fr["output"]).astype(np.int32) - hf["output"].astype(np.int32))
+        assert (d <= 2).mean() >= 0.995, (f, (d <= 2).mean())
+        assert abs(soc.exposure_of(fr["auto_exposure"]) - ae.exposure) <= 1e-4
+    r.close()

@@ -1,0 +1,68 @@
+"""The Sponza-proxy mesh (soc_real_time_renderer_amd/scene/sponza_mesh.py) and its texture fixture. No GPU.
+
+SURVEY.md §8d: an atrium of ~262k triangles (Sponza's 262,267, from Sponza.gltf's index counts) textured with
+the real Sponza images, f_sky ~ 0.1 at the C3 camera."""
+import json
+import os
+
+import numpy as np
+
+from soc_real_time_renderer_amd.scene import sponza_mesh as sm
+
+
+def test_mesh_counts_bounds_and_materials():
+    d = sm.build()
+    T = len(d["indices"])
+    assert sum(sm.GLTF_TRIANGLES.values()) == 262267
+    assert abs(T - 262267) / 262267 < 0.03, T
+    assert d["indices"].max() < d["vertex_count"] == len(d["positions"])
+    lo, hi = d["positions"].min(0), d["positions"].max(0)
+    assert lo[0] >= sm.X0 - 1e-3 and hi[0] <= sm.X1 + 1e-3 and lo[2] >= sm.Z0 - 1e-3 and hi[2] <= sm.Z1 + 1e-3
+    assert set(np.unique(d["materials"])) == set(range(25))
+    assert np.allclose(np.linalg.norm(d["normals"], axis=1), 1.0, atol=1e-4)
+    # every material within 40 % of its glTF triangle count
+    counts = np.bincount(d["materials"], minlength=25)
+    for mid, want in sm.GLTF_TRIANGLES.items():
+        if want >= 500:
+            assert 0.6 * want <= counts[mid] <= 1.4 * want, (mid, counts[mid], want)
+
+
+def test_winding_agrees_with_normals():
+    """Triangles are counter-clockwise seen from the side their vertex normals point to (glTF convention)."""
+    d = sm.build()
+    P, I, N = d["positions"].astype(np.float64), d["indices"], d["normals"]
+    fn = np.cross(P[I[:, 1]] - P[I[:, 0]], P[I[:, 2]] - P[I[:, 0]])
+    ok = (fn * N[I].sum(1)).sum(1) >= 0
+    assert ok.mean() > 0.99, ok.mean()
+
+
+def test_deterministic():
+    a, b = sm.build(), sm.build()
+    for k in ("positions", "normals", "uvs", "indices", "materials"):
+        assert np.array_equal(a[k], b[k])
+
+
+def test_texture_fixture():
+    idx = sm.texture_index()
+    assert sorted(idx) == list(range(25))
+    assert sum(1 for v in idx.values() if v.get("albedo")) == 25
+    assert sum(1 for v in idx.values() if v.get("normal")) == 24
+    tex = sm.load_textures()
+    for mid, t in tex.items():
+        for k, a in t.items():
+            if a is not None:
+                assert a.dtype == np.uint8 and a.shape[2] == 4 and a.shape[0] == a.shape[1] <= 256
+    # tangent-space normal images: blue (z) dominant
+    assert np.mean([t["normal"][..., 2].mean() for t in tex.values() if t["normal"] is not None and
+                    t["normal"].shape[0] > 8]) > 180
+
+
+def test_c3_view_sky_fraction(oracle):
+    """At the C3 camera (multi_gpu.SPONZA_CAMERA) about a tenth of the frame is sky through the open court."""
+    from helpers import sponza_mesh_inputs
+    g, gb = sponza_mesh_inputs(192, 108, shadow_size=256)
+    f_sky = float((gb["depth"] == 1.0).mean())
+    assert 0.06 <= f_sky <= 0.14, f_sky
+    # the normal textures perturb the geometric normals over most of the visible surfaces
+    cov = gb["depth"] < 1.0
+    assert np.abs(np.linalg.norm(gb["normal"][cov][:, :3].astype(np.float64), axis=1) - 1).max() < 5e-3

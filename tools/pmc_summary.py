@@ -36,7 +36,8 @@ if "--traffic" in sys.argv:
     meta = {"source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes, --kernel-trace only) "
                       "over `bench.py --steps 3 --warmup 1 --profile-frames 1`; per-dispatch means",
             "formula": "hbm_bytes = 2*FETCH_SIZE + WRITE_SIZE (KiB -> bytes; gfx950 FETCH_SIZE halving correction)",
-            "resolution": [3840, 2160], "kernels": kernels}
+            "resolution": [3840, 2160], "kernels": kernels,
+            "scene": (sys.argv[sys.argv.index("--scene") + 1] if "--scene" in sys.argv else "mesh")}
     with open(dst, "w") as fh:
         json.dump(meta, fh, indent=1, sort_keys=True)
 json.dump(res, sys.stdout, indent=1, sort_keys=True)
