@@ -1054,10 +1054,12 @@ static rs_tri rs_setup(rs_vtx A, rs_vtx B, rs_vtx C, int cull, int W, int H, int
         float ax = A.x / A.w, ay = A.y / A.w, bx = B.x / B.w, by = B.y / B.w, cx = C.x / C.w, cy = C.y / C.w;
         float minx = fminf(ax, fminf(bx, cx)), maxx = fmaxf(ax, fmaxf(bx, cx));
         float miny = fminf(ay, fminf(by, cy)), maxy = fmaxf(ay, fmaxf(by, cy));
-        t.px0 = (int)floorf(fminf(fmaxf(minx - 0.5f, -1.0f), (float)W)); if (t.px0 < 0) t.px0 = 0;
-        t.px1 = (int)ceilf(fminf(fmaxf(maxx - 0.5f, -1.0f), (float)W)); if (t.px1 > W - 1) t.px1 = W - 1;
-        t.py0 = (int)floorf(fminf(fmaxf(miny - 0.5f, -1.0f), (float)H)); if (t.py0 < 0) t.py0 = 0;
-        t.py1 = (int)ceilf(fminf(fmaxf(maxy - 0.5f, -1.0f), (float)H)); if (t.py1 > H - 1) t.py1 = H - 1;
+        /* one pixel of margin: the projected vertices are rounded, and coverage is decided by the edge
+           functions alone (a centre on an edge may lie a rounding error outside the rounded box) */
+        t.px0 = (int)floorf(fminf(fmaxf(minx - 1.5f, -1.0f), (float)W)); if (t.px0 < 0) t.px0 = 0;
+        t.px1 = (int)ceilf(fminf(fmaxf(maxx + 0.5f, -1.0f), (float)W)); if (t.px1 > W - 1) t.px1 = W - 1;
+        t.py0 = (int)floorf(fminf(fmaxf(miny - 1.5f, -1.0f), (float)H)); if (t.py0 < 0) t.py0 = 0;
+        t.py1 = (int)ceilf(fminf(fmaxf(maxy + 0.5f, -1.0f), (float)H)); if (t.py1 > H - 1) t.py1 = H - 1;
     } else {                                           /* a vertex at or behind the eye: whole image */
         t.px0 = 0; t.px1 = W - 1; t.py0 = 0; t.py1 = H - 1;
     }

@@ -256,7 +256,7 @@ def build(seed: int = SEED) -> Dict:
             panel(m, (lathe_x, 1.0, z - 0.7), (0, 0, 1.4), (0, 1.6, 0), (n, 0, 0), GLTF_TRIANGLES[23] // 4, 23,
                   tile=1.4, relief=0.12, freq=(3.0, 2.0), rng=rng)
     # a canopy frame above the west end (inside the sun frustum: it casts a shadow into the map)
-    panel(m, (-19.0, 27.0, 6.0), (3.5, 0, 0), (0, 0, -12.0), (0, -1, 0), 600, 24, tile=2.0)   # behind the C3 camera
+    panel(m, (-19.0, 27.0, 6.0), (3.5, 0, 0), (0, 0, -12.0), (0, 1, 0), 600, 24, tile=2.0)   # behind the C3 camera, facing the sun
     P, N, UV, I, M = m.arrays()
     return {"positions": P, "normals": N, "uvs": UV, "indices": I, "materials": M, "vertex_count": len(P)}
 
