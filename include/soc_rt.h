@@ -392,6 +392,7 @@ typedef struct soc_renderer soc_renderer;
                                             for callers that set it) */
 #define SOC_RENDERER_EXACT_BLOOM 32       /* bit-exact bloom chain instead of the weighted form (bloom_w.hip) */
 #define SOC_RENDERER_UNFUSED_HISTOGRAM 64 /* composition and luminance histogram as two passes */
+#define SOC_RENDERER_NO_SKY_SPLIT 128     /* Composition writes the sky pixels itself (waits for the clouds) */
 
 soc_renderer* soc_renderer_create(const soc_frame_images* images, uint32_t flags);
 void soc_renderer_destroy(soc_renderer* r);
@@ -440,6 +441,8 @@ enum soc_resource {
     SOC_RES_OUTPUT,              /* tone-mapped framebuffer (the reference's swapchain image) */
     SOC_RES_VISIBILITY,          /* raster visibility buffer (raster head) */
     SOC_RES_HISTOGRAM_PARTIALS,  /* the fused composition + histogram pass's partial bins */
+    SOC_RES_SKY_COLOR,           /* the colour image's sky pixels, when the second lane writes them (see below) */
+    SOC_RES_SKY_HISTOGRAM_PARTIALS,  /* their partial bins */
     SOC_RES_USER0 = 32,          /* SOC_RES_USER0 .. SOC_RES_USER0 + 31: caller-defined resources */
     SOC_RES_COUNT = 64
 };
@@ -454,6 +457,11 @@ typedef struct soc_pass_desc {
     int32_t reads[SOC_PASS_MAX_USES];    /* enum soc_resource */
     int32_t writes[SOC_PASS_MAX_USES];
 } soc_pass_desc;
+/* Sky split (the default with the fused histogram and the pair path): Composition's sky pixels (depth == 1 ->
+ * the clouds texel, composition.inl:220-222) are written and binned on the second lane right after
+ * CloudRendering, so Composition does not wait for the clouds. COLOR is then the non-sky pixels and SKY_COLOR the
+ * sky pixels of the same image: a caller pass that needs the whole colour image declares both.
+ * SOC_RENDERER_NO_SKY_SPLIT turns it off (same bits either way). */
 /* The callback of a caller pass: record its work on `stream`, return 0 (or a negative code, which aborts the
  * frame with that code). `images` is the renderer's frame, with history_color[0] / history_velocity[0] the
  * PREVIOUS and [1] the RESOLVED slots of this frame. */

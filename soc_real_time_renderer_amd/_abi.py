@@ -38,6 +38,7 @@ RENDERER_UNFUSED_TONEMAP = 8
 RENDERER_FUSED_HISTOGRAM = 16
 RENDERER_EXACT_BLOOM = 32
 RENDERER_UNFUSED_HISTOGRAM = 64
+RENDERER_NO_SKY_SPLIT = 128
 HISTOGRAM_SCRATCH_WORDS = 2048
 
 Mat4 = C.c_float * 16
@@ -145,7 +146,8 @@ class Entity(C.Structure):
 # enum soc_resource (include/soc_rt.h): the frame resources a pass declares it reads / writes
 RESOURCES = ["ALBEDO", "EMISSIVE", "NORMAL", "DEPTH", "VELOCITY", "SUN_SHADOW", "NOISE", "BLOOM_MIP0", "BLOOM_MIP1",
              "BLOOM_MIP2", "BLOOM_MIP3", "BLOOM_OUTPUT", "SSAO", "SSAO_BLUR", "CLOUDS", "COLOR", "PREVIOUS_COLOR",
-             "RESOLVED", "PREVIOUS_VELOCITY", "AUTO_EXPOSURE", "OUTPUT", "VISIBILITY", "HISTOGRAM_PARTIALS"]
+             "RESOLVED", "PREVIOUS_VELOCITY", "AUTO_EXPOSURE", "OUTPUT", "VISIBILITY", "HISTOGRAM_PARTIALS",
+             "SKY_COLOR", "SKY_HISTOGRAM_PARTIALS"]
 RES = {n: i for i, n in enumerate(RESOURCES)}
 RES_USER0 = 32
 RES_COUNT = 64

@@ -612,6 +612,8 @@ struct soc_renderer {
     uint32_t* hist_scratch = nullptr;
     // this execute call runs both phases: the resolve folds the partial histograms itself (no fold launch)
     bool fold_in_resolve = false;
+    // sky split configured (graph) / active this frame (the pair path applies at the globals' resolution)
+    bool sky_split = false, sky_split_active = false;
 };
 
 namespace {
@@ -748,17 +750,33 @@ void build_passes_tail(soc_renderer* r) {
              });
     add_pass(r, "SSAOBlur", "Ambient Occlusion", pre, res_mask({SOC_RES_SSAO}), res_mask({SOC_RES_SSAO_BLUR}),
              [r](const soc_globals* g, hipStream_t s) { return soc_ssao_blur(g, r->img.ssao, r->img.ssao_blur, (soc_stream)s); });
+    // Sky split: with the fused histogram on the pair path, the clouds lane also writes and bins the colour
+    // image's sky pixels (sky_compose_launch), and Composition skips them, so it does not wait for the clouds.
+    const bool fused_hist = !(r->flags & SOC_RENDERER_UNFUSED_HISTOGRAM);
+    const soc_img& em_img = I.bloom_output.data ? I.bloom_output : I.emissive;
+    soc_globals gres{};
+    gres.resolution[0] = I.color.width;
+    gres.resolution[1] = I.color.height;
+    r->sky_split = fused_hist && !(r->flags & SOC_RENDERER_NO_SKY_SPLIT) &&
+                   soc::composition_pair_applicable(&gres, I.color, I.albedo, em_img, I.normal, I.depth, I.clouds);
+    const uint64_t sky_w = r->sky_split ? res_mask({SOC_RES_SKY_COLOR, SOC_RES_SKY_HISTOGRAM_PARTIALS}) : 0;
+    const uint64_t parts = res_mask({SOC_RES_HISTOGRAM_PARTIALS}) | (r->sky_split ? res_mask({SOC_RES_SKY_HISTOGRAM_PARTIALS}) : 0);
     // renderer.cpp:1094-1101
     add_pass(r, "CloudRendering", "Sky Rendering", pre, res_mask({SOC_RES_DEPTH, SOC_RES_NOISE}),
-             res_mask({SOC_RES_CLOUDS}), [r](const soc_globals* g, hipStream_t s) {
-                 return soc_cloud_rendering(g, r->img.depth, r->img.noise, r->img.clouds, r->img.clouds_workspace,
-                                            (soc_stream)s);
+             res_mask({SOC_RES_CLOUDS}) | sky_w, [r](const soc_globals* g, hipStream_t s) {
+                 int rc = soc_cloud_rendering(g, r->img.depth, r->img.noise, r->img.clouds, r->img.clouds_workspace,
+                                              (soc_stream)s);
+                 if (rc || !r->sky_split_active) return rc;
+                 rc = ensure_hist_scratch(r);
+                 if (rc) return rc;
+                 return soc::sky_compose_launch(g, r->img.color, r->img.depth, r->img.clouds, r->hist_scratch,
+                                                (soc_stream)s);
              }, SOC_PASS_ASYNC);
     // renderer.cpp:1103-1117 (composition uses) and 1155-1162 (histogram): one launch by default (the colour
     // is binned as it is written), two with SOC_RENDERER_UNFUSED_HISTOGRAM (measured in composition.hip)
     const uint64_t comp_reads = res_mask({SOC_RES_ALBEDO, em_res, SOC_RES_NORMAL, SOC_RES_DEPTH, SOC_RES_SSAO_BLUR,
-                                          SOC_RES_SUN_SHADOW, SOC_RES_CLOUDS});
-    if (!(r->flags & SOC_RENDERER_UNFUSED_HISTOGRAM)) {
+                                          SOC_RES_SUN_SHADOW}) | (r->sky_split ? 0 : res_mask({SOC_RES_CLOUDS}));
+    if (fused_hist) {
         add_pass(r, "Composition+GenerateLuminanceHistogram", "Composition", pre, comp_reads,
                  res_mask({SOC_RES_COLOR, SOC_RES_HISTOGRAM_PARTIALS}), [r](const soc_globals* g, hipStream_t s) {
                      const auto& I = r->img;
@@ -767,13 +785,14 @@ void build_passes_tail(soc_renderer* r) {
                      if (rc) return rc;
                      return soc::composition_luminance_histogram(g, I.d_globals, I.color, I.albedo, em, I.normal, I.depth,
                                                                  I.ssao_blur, I.shadow, I.clouds, I.auto_exposure,
-                                                                 r->hist_scratch, false, (soc_stream)s);
+                                                                 r->hist_scratch, false, (soc_stream)s,
+                                                                 r->sky_split_active);
                  });
         // the 8 partial histograms of the fused launch into the AutoExposure bins. Before a multi-GPU exchange
         // (PRE and POST in separate calls) the fold must precede it; in a one-call frame the resolve folds them
         // itself and this pass has no work (it is then neither launched nor timed).
-        auto& fold = add_pass(r, "LuminanceHistogramFold", "Auto Exposure", pre, res_mask({SOC_RES_HISTOGRAM_PARTIALS}),
-                              res_mask({SOC_RES_AUTO_EXPOSURE, SOC_RES_HISTOGRAM_PARTIALS}),
+        auto& fold = add_pass(r, "LuminanceHistogramFold", "Auto Exposure", pre, parts,
+                              res_mask({SOC_RES_AUTO_EXPOSURE}) | parts,
                               [r](const soc_globals* g, hipStream_t s) {
                                   (void)g;
                                   return soc::histogram_fold_launch(r->hist_scratch, r->img.auto_exposure, (soc_stream)s);
@@ -793,16 +812,16 @@ void build_passes_tail(soc_renderer* r) {
                  });
     }
     // renderer.cpp:1164-1168
-    add_pass(r, "ResolveLuminanceHistogram", "Auto Exposure", post,
-             res_mask({SOC_RES_AUTO_EXPOSURE, SOC_RES_HISTOGRAM_PARTIALS}),
-             res_mask({SOC_RES_AUTO_EXPOSURE, SOC_RES_HISTOGRAM_PARTIALS}), [r](const soc_globals* g, hipStream_t s) {
+    add_pass(r, "ResolveLuminanceHistogram", "Auto Exposure", post, res_mask({SOC_RES_AUTO_EXPOSURE}) | parts,
+             res_mask({SOC_RES_AUTO_EXPOSURE}) | parts, [r](const soc_globals* g, hipStream_t s) {
                  return soc::resolve_luminance_histogram(g, r->img.auto_exposure, r->total_pixels, r->wide,
                                                          r->fold_in_resolve ? r->hist_scratch : nullptr, (soc_stream)s);
              });
     // renderer.cpp:1170-1198: TAA + both history copies (ping-pong + fused velocity history), and
     // renderer.cpp:1210-1217: tone mapping, fused into the TAA launch for an RGBA8_UNORM framebuffer
     const uint64_t taa_reads = res_mask({SOC_RES_COLOR, SOC_RES_PREVIOUS_COLOR, SOC_RES_VELOCITY,
-                                         SOC_RES_PREVIOUS_VELOCITY, SOC_RES_DEPTH});
+                                         SOC_RES_PREVIOUS_VELOCITY, SOC_RES_DEPTH}) |
+                               (r->sky_split ? res_mask({SOC_RES_SKY_COLOR}) : 0);
     const uint64_t taa_writes = res_mask({SOC_RES_RESOLVED, SOC_RES_PREVIOUS_VELOCITY});
     const bool fuse_tm = !(r->flags & SOC_RENDERER_UNFUSED_TONEMAP) && I.output.format == SOC_FMT_RGBA8_UNORM;
     if (fuse_tm) {
@@ -1019,6 +1038,15 @@ extern "C" int soc_renderer_execute(soc_renderer* r, const soc_globals* g, int32
     if (!r || !g) return set_error(SOC_E_INVALID_ARG, "soc_renderer_execute: null argument");
     hipStream_t s = hs(stream);
     r->fold_in_resolve = (phase & SOC_PHASE_ALL) == SOC_PHASE_ALL && !(r->flags & SOC_RENDERER_UNFUSED_HISTOGRAM);
+    if (phase & SOC_PHASE_PRE_EXPOSURE) {
+        const soc_img& em = r->img.bloom_output.data ? r->img.bloom_output : r->img.emissive;
+        r->sky_split_active = r->sky_split && soc::composition_pair_applicable(g, r->img.color, r->img.albedo, em,
+                                                                               r->img.normal, r->img.depth, r->img.clouds);
+        // the graph was derived with Composition independent of the clouds: it cannot fall back to reading them
+        if (r->sky_split && !r->sky_split_active)
+            return set_error(SOC_E_SHAPE, "soc_renderer_execute: globals resolution %dx%d differs from the frame images %dx%d",
+                             g->resolution[0], g->resolution[1], r->img.color.width, r->img.color.height);
+    }
     if ((phase & SOC_PHASE_PRE_EXPOSURE) && (g->point_light_count || g->spot_light_count)) {
         int rc = upload_lights(r, g, s);
         if (rc) return rc;

@@ -31,6 +31,7 @@ struct CompParams {
     float lmin, lrange;    // log_min_luminance, log_max - log_min
     BinFast bf;            // lum_bin_fast parameters
     const soc_globals* __restrict__ dg;  // device globals (lights), may be null when npl == nsl == 0
+    int sky_external;      // 1: sky pixels (depth == 1) are written and binned by sky_compose_pair (second lane)
 };
 
 __device__ __forceinline__ float fast_pow(float x, float y) {
@@ -168,6 +169,7 @@ __global__ __launch_bounds__(256) void composition_pair(DImg target, DImg albedo
     const bool inside = x < target.w && y < target.h;
     if (!HIST && !inside) return;
     uint2 outp[2] = {uint2{0u, 0u}, uint2{0u, 0u}};
+    uint32_t own = 3u;   // bit k: this kernel writes (and bins) pixel k of the pair
     if (inside) {
         const float v = centre_uv(y, target.h);
         float2 d2;
@@ -193,6 +195,10 @@ __global__ __launch_bounds__(256) void composition_pair(DImg target, DImg albedo
             const f4 em = unpack_h4(k ? uint2{e4.z, e4.w} : uint2{e4.x, e4.y});
             const f4 nn = unpack_h4(k ? uint2{n4.z, n4.w} : uint2{n4.x, n4.y});
             f4 c;
+            if (d == 1.0f && p.sky_external) {   // the second lane writes it (sky_compose_pair)
+                own &= ~(1u << k);
+                continue;
+            }
             if (d == 1.0f) {
                 const f4 cl = fetch_rgba8(clouds, x + k, y);
                 c = f4{cl.x, cl.y, cl.z, 1.0f};
@@ -204,8 +210,13 @@ __global__ __launch_bounds__(256) void composition_pair(DImg target, DImg albedo
         }
         const uint4 o = uint4{outp[0].x, outp[0].y, outp[1].x, outp[1].y};
         typedef uint32_t v4w __attribute__((ext_vector_type(4)));
-        if (NT & 2) __builtin_nontemporal_store(__builtin_bit_cast(v4w, o), reinterpret_cast<v4w*>(row_ptr_w<uint4>(target, y)) + (x >> 1));
-        else row_ptr_w<uint4>(target, y)[x >> 1] = o;
+        if (own == 3u) {
+            if (NT & 2) __builtin_nontemporal_store(__builtin_bit_cast(v4w, o), reinterpret_cast<v4w*>(row_ptr_w<uint4>(target, y)) + (x >> 1));
+            else row_ptr_w<uint4>(target, y)[x >> 1] = o;
+        } else {   // a sky pixel in the pair belongs to the second lane: 8-B stores of ours only
+            if (own & 1u) row_ptr_w<uint2>(target, y)[x] = outp[0];
+            if (own & 2u) row_ptr_w<uint2>(target, y)[x + 1] = outp[1];
+        }
     }
     if (HIST) {
         const f4 c0 = unpack_h4(outp[0]), c1 = unpack_h4(outp[1]);
@@ -213,11 +224,47 @@ __global__ __launch_bounds__(256) void composition_pair(DImg target, DImg albedo
         uint32_t b1 = lum_bin_fast(c1.x, c1.y, c1.z, p.bf);
         if (b0 == kBinExact) b0 = lum_bin(c0.x, c0.y, c0.z, p.lmin, p.lrange);
         if (b1 == kBinExact) b1 = lum_bin(c1.x, c1.y, c1.z, p.lmin, p.lrange);
-        wave_bin_pair(sh + wave * kBins, b0, b1, inside);
+        wave_bin_pair_mask(sh + wave * kBins, b0, b1, inside ? own : 0u);
         __syncthreads();
         const uint32_t n = sh[threadIdx.x] + sh[kBins + threadIdx.x] + sh[2 * kBins + threadIdx.x] + sh[3 * kBins + threadIdx.x];
         if (n) atomicAdd(&p.bins[((blockIdx.y * gridDim.x + blockIdx.x) & 7u) * kBins + threadIdx.x], n);
     }
+}
+
+// The sky pixels of the colour image (composition.inl:220-222: depth == 1 -> color = clouds texel), written and
+// binned on the renderer's second lane right after CloudRendering, so Composition (sky_external) does not wait
+// for the clouds: the same tiling, texel fetch, f16 packing and bins as composition_pair's sky branch, hence
+// the same bits. 8-B stores of the sky pixels only (Composition writes the others concurrently).
+__global__ __launch_bounds__(256) void sky_compose_pair(DImg target, DImg depth, DImg clouds, CompParams p) {
+    __shared__ uint32_t sh[4 * kBins];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    reinterpret_cast<uint4*>(sh + wave * kBins)[lane] = uint4{0u, 0u, 0u, 0u};
+    const int bx = blockIdx.x, by = blockIdx.y;
+    const int x = bx * 32 + (wave & 1) * 16 + (lane & 7) * 2;
+    const int y = by * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const bool inside = x < target.w && y < target.h;
+    uint32_t mine = 0u;
+    uint2 outp[2] = {uint2{0u, 0u}, uint2{0u, 0u}};
+    if (inside) {
+        const float2 d2 = row_ptr<float2>(depth, y)[x >> 1];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            if ((k ? d2.y : d2.x) != 1.0f) continue;
+            const f4 cl = fetch_rgba8(clouds, x + k, y);
+            outp[k] = pack_h4(f4{cl.x, cl.y, cl.z, 1.0f});
+            row_ptr_w<uint2>(target, y)[x + k] = outp[k];
+            mine |= 1u << k;
+        }
+    }
+    const f4 c0 = unpack_h4(outp[0]), c1 = unpack_h4(outp[1]);
+    uint32_t b0 = lum_bin_fast(c0.x, c0.y, c0.z, p.bf);
+    uint32_t b1 = lum_bin_fast(c1.x, c1.y, c1.z, p.bf);
+    if (b0 == kBinExact) b0 = lum_bin(c0.x, c0.y, c0.z, p.lmin, p.lrange);
+    if (b1 == kBinExact) b1 = lum_bin(c1.x, c1.y, c1.z, p.lmin, p.lrange);
+    wave_bin_pair_mask(sh + wave * kBins, b0, b1, mine);
+    __syncthreads();
+    const uint32_t n = sh[threadIdx.x] + sh[kBins + threadIdx.x] + sh[2 * kBins + threadIdx.x] + sh[3 * kBins + threadIdx.x];
+    if (n) atomicAdd(&p.bins[((blockIdx.y * gridDim.x + blockIdx.x) & 7u) * kBins + threadIdx.x], n);
 }
 
 __global__ __launch_bounds__(256) void histogram_fold(uint32_t* __restrict__ scratch, uint32_t* __restrict__ bins) {
@@ -264,7 +311,7 @@ namespace {
 // (returns 1 otherwise, having launched nothing)
 int composition_launch(const soc_globals* g, const soc_globals* d_globals, soc_img target, soc_img albedo, soc_img emissive,
                        soc_img normal, soc_img depth, soc_img ssao, soc_img shadow, soc_img clouds, uint32_t* bins,
-                       uint32_t* scratch, soc_stream stream, bool fold = true) {
+                       uint32_t* scratch, soc_stream stream, bool fold = true, bool sky_external = false) {
     static const char* P = "soc_composition";
     if (!g) return set_error(SOC_E_INVALID_ARG, "%s: null globals", P);
     int rc = check_img(target, SOC_FMT_RGBA16F, P, "target");
@@ -299,6 +346,7 @@ int composition_launch(const soc_globals* g, const soc_globals* d_globals, soc_i
     p.dg = d_globals;
     p.swz = tuning_knob("SOC_SWZ_COMP", 0);
     p.bins = nullptr;
+    p.sky_external = 0;
     if ((p.npl || p.nsl) && !d_globals)
         return set_error(SOC_E_INVALID_ARG, "%s: frame has lights but no device globals (soc_upload_globals)", P);
 
@@ -308,6 +356,7 @@ int composition_launch(const soc_globals* g, const soc_globals* d_globals, soc_i
                       W <= 8192 && H <= 8192 && aligned16(target) && aligned16(albedo) && aligned16(emissive) &&
                       aligned16(normal) && (reinterpret_cast<uintptr_t>(depth.data) & 7u) == 0 && (depth.pitch_bytes & 7) == 0;
     if (bins && !(fast && W == g->resolution[0] && H == g->resolution[1])) return 1;
+    if (sky_external && !bins) return set_error(SOC_E_INVALID_ARG, "%s: sky_external needs the fused histogram", P);
     if (fast) {
         dim3 grd(ceil_div(W, 32), ceil_div(H, 16));
         const bool lights = (p.npl | p.nsl) != 0;
@@ -315,6 +364,7 @@ int composition_launch(const soc_globals* g, const soc_globals* d_globals, soc_i
             dimg(emissive), dimg(normal), dimg(depth), dimg(ssao), dimg(shadow), dimg(clouds), p)
         if (bins) {
             p.bins = scratch;
+            p.sky_external = sky_external ? 1 : 0;
             p.lmin = g->log_min_luminance;
             p.lrange = g->log_max_luminance - g->log_min_luminance;
             p.bf = bin_fast_params(p.lmin, p.lrange);
@@ -343,6 +393,34 @@ int composition_launch(const soc_globals* g, const soc_globals* d_globals, soc_i
 }
 }  // namespace
 
+bool soc::composition_pair_applicable(const soc_globals* g, const soc_img& target, const soc_img& albedo,
+                                      const soc_img& emissive, const soc_img& normal, const soc_img& depth,
+                                      const soc_img& clouds) {
+    const int W = target.width, H = target.height;
+    auto same = [&](const soc_img& im) { return im.width == W && im.height == H; };
+    return g && same(albedo) && same(emissive) && same(normal) && same(depth) && same(clouds) && (W % 2 == 0) &&
+           W <= 8192 && H <= 8192 && aligned16(target) && aligned16(albedo) && aligned16(emissive) &&
+           aligned16(normal) && (reinterpret_cast<uintptr_t>(depth.data) & 7u) == 0 && (depth.pitch_bytes & 7) == 0 &&
+           W == g->resolution[0] && H == g->resolution[1];
+}
+
+int soc::sky_compose_launch(const soc_globals* g, soc_img target, soc_img depth, soc_img clouds, uint32_t* scratch,
+                            soc_stream stream) {
+    if (!g || !scratch) return set_error(SOC_E_INVALID_ARG, "sky compose: null globals / scratch");
+    int rc = check_img(target, SOC_FMT_RGBA16F, "sky compose", "target");
+    if (!rc) rc = check_img(depth, SOC_FMT_D32F, "sky compose", "depth");
+    if (!rc) rc = check_img(clouds, SOC_FMT_RGBA8_UNORM, "sky compose", "clouds");
+    if (rc) return rc;
+    CompParams p{};
+    p.bins = scratch;
+    p.lmin = g->log_min_luminance;
+    p.lrange = g->log_max_luminance - g->log_min_luminance;
+    p.bf = bin_fast_params(p.lmin, p.lrange);
+    const dim3 grd(ceil_div(target.width, 32), ceil_div(target.height, 16));
+    sky_compose_pair<<<grd, 256, 0, hs(stream)>>>(dimg(target), dimg(depth), dimg(clouds), p);
+    return check_launch("sky_compose");
+}
+
 extern "C" int soc_composition(const soc_globals* g, const soc_globals* d_globals, soc_img target, soc_img albedo,
                                soc_img emissive, soc_img normal, soc_img depth, soc_img ssao, soc_img shadow,
                                soc_img clouds, soc_stream stream) {
@@ -353,12 +431,13 @@ extern "C" int soc_composition(const soc_globals* g, const soc_globals* d_global
 int soc::composition_luminance_histogram(const soc_globals* g, const soc_globals* d_globals, soc_img target,
                                          soc_img albedo, soc_img emissive, soc_img normal, soc_img depth, soc_img ssao,
                                          soc_img shadow, soc_img clouds, soc_auto_exposure* ae, uint32_t* scratch,
-                                         bool fold, soc_stream stream) {
+                                         bool fold, soc_stream stream, bool sky_external) {
     if (!g || !ae || !scratch)
         return set_error(SOC_E_INVALID_ARG, "soc_composition_luminance_histogram: null globals / auto exposure / scratch");
     int rc = composition_launch(g, d_globals, target, albedo, emissive, normal, depth, ssao, shadow, clouds,
-                                ae->histogram_buckets, scratch, stream, fold);
+                                ae->histogram_buckets, scratch, stream, fold, sky_external);
     if (rc <= 0) return rc;   // launched (or failed validation)
+    if (sky_external) return set_error(SOC_E_INVALID_ARG, "composition: sky_external needs the pair path");
     // not fusable: the two passes back to back (same results)
     rc = composition_launch(g, d_globals, target, albedo, emissive, normal, depth, ssao, shadow, clouds, nullptr, nullptr,
                             stream);

@@ -99,8 +99,9 @@ __device__ __forceinline__ uint32_t lum_bin_fast(float r, float g, float b, cons
 // the wave (a ballot loop: neighbouring pixels mostly share a bin, so 2-3 rounds per 16x8 block).
 // Lanes with valid == false contribute nothing; every lane of the wave must call it. (Device atomics per
 // wave instead of the LDS copy measured 186 us at 4K: the hot bins serialise.)
-__device__ __forceinline__ void wave_bin_pair(uint32_t* sh, uint32_t b0, uint32_t b1, bool valid) {
-    uint32_t pend = valid ? 3u : 0u;   // bit 0: pixel 0 pending, bit 1: pixel 1
+// mask bit 0: pixel 0 is binned, bit 1: pixel 1
+__device__ __forceinline__ void wave_bin_pair_mask(uint32_t* sh, uint32_t b0, uint32_t b1, uint32_t mask) {
+    uint32_t pend = mask & 3u;   // bit 0: pixel 0 pending, bit 1: pixel 1
     const uint32_t lane = __lane_id();
     unsigned long long act = __ballot(pend != 0u);
     while (act) {
@@ -117,6 +118,10 @@ __device__ __forceinline__ void wave_bin_pair(uint32_t* sh, uint32_t b0, uint32_
         if (lane == (uint32_t)leader) atomicAdd(&sh[B], total);
         act = __ballot(pend != 0u);
     }
+}
+
+__device__ __forceinline__ void wave_bin_pair(uint32_t* sh, uint32_t b0, uint32_t b1, bool valid) {
+    wave_bin_pair_mask(sh, b0, b1, valid ? 3u : 0u);
 }
 
 }  // namespace soc

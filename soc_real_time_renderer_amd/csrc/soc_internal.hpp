@@ -71,7 +71,16 @@ int launch_bloom_weighted(const soc_img& emissive, const soc_img* mips, const so
 // separate histogram_fold_launch (the render graph times the fold as a pass of its own).
 int composition_luminance_histogram(const soc_globals* g, const soc_globals* d_globals, soc_img target, soc_img albedo,
                                     soc_img emissive, soc_img normal, soc_img depth, soc_img ssao, soc_img shadow,
-                                    soc_img clouds, soc_auto_exposure* ae, uint32_t* scratch, bool fold, soc_stream stream);
+                                    soc_img clouds, soc_auto_exposure* ae, uint32_t* scratch, bool fold, soc_stream stream,
+                                    bool sky_external = false);
+// The fused pair path applies to these images at the globals' resolution (composition.hip).
+bool composition_pair_applicable(const soc_globals* g, const soc_img& target, const soc_img& albedo,
+                                 const soc_img& emissive, const soc_img& normal, const soc_img& depth,
+                                 const soc_img& clouds);
+// The sky pixels of the colour image (depth == 1 -> clouds texel) and their bins into the 8 partial histograms:
+// the second-lane half of a Composition run with sky_external.
+int sky_compose_launch(const soc_globals* g, soc_img target, soc_img depth, soc_img clouds, uint32_t* scratch,
+                       soc_stream stream);
 int histogram_fold_launch(uint32_t* scratch, soc_auto_exposure* ae, soc_stream stream);
 // soc_resolve_luminance_histogram that first folds the 8 partial histograms (null: none).
 int resolve_luminance_histogram(const soc_globals* g, soc_auto_exposure* ae, uint64_t total_pixels, int32_t wide_accumulator,

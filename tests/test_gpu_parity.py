@@ -648,3 +648,33 @@ def test_render_graph_c3b_lights(soc, oracle):
     ok = f16_close(host(fr["color"]), ref)
     assert ok.mean() >= 0.9995, ok.mean()
     r.close()
+
+
+@pytest.mark.parametrize("phases", ["one-call", "split"])
+def test_render_graph_sky_split_bit_identical(soc, phases):
+    """Sky split: the second lane writes and bins the colour image's sky pixels after the clouds, Composition skips
+    them and does not wait. Against Composition writing them itself: the same bits over 3 frames (colour, output,
+    exposure, resolved history), for one-call frames and PRE / POST frames (the multi-GPU shape)."""
+    W, H = 1920, 1080
+    g, gb = sponza_inputs(W, H, elapsed=10.0, camera=((-14.0, 2.2, 0.3), (0.0, -0.9, 0.0)))   # looking up: more sky
+    assert (gb["depth"] == 1.0).mean() > 0.1
+    outs = []
+    for split in (True, False):
+        fr = soc.alloc_frame(W, H, DEV, bloom_output=True)
+        for k in ("albedo", "emissive", "normal", "velocity", "depth"):
+            fr[k].copy_(torch.from_numpy(gb[k]))
+        fr["shadow"] = dev(gb["shadow"])
+        fr["noise"].copy_(torch.from_numpy(gb["noise"]))
+        r = soc.Renderer(fr, sky_split=split)
+        for _ in range(3):
+            if phases == "split":
+                r.execute(g, soc.PHASE_PRE_EXPOSURE)
+                r.execute(g, soc.PHASE_POST_EXPOSURE)
+            else:
+                r.execute(g)
+        torch.cuda.synchronize()
+        outs.append({k: fr[k].clone() for k in ("clouds", "color", "output", "auto_exposure")})
+        outs[-1]["resolved"] = r.resolved().clone()
+        r.close()
+    for k in outs[0]:
+        assert torch.equal(outs[0][k], outs[1][k]), k

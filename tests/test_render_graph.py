@@ -91,8 +91,15 @@ def test_second_lane_is_derived(soc):
     names = r.pass_names()
     lanes = {n: r.pass_lane(i) for i, n in enumerate(names)}
     assert [n for n, l in lanes.items() if l == 1] == ["CloudRendering"]
-    # only the composition waits for it
+    # sky split (default): the second lane also writes and bins the colour's sky pixels, so Composition does not
+    # wait for it; the histogram fold (its partial bins) and TAA (the sky pixels) do
+    assert r.pass_uses(names.index("CloudRendering"))[1] == {"CLOUDS", "SKY_COLOR", "SKY_HISTOGRAM_PARTIALS"}
+    assert "CLOUDS" not in r.pass_uses(names.index("Composition+GenerateLuminanceHistogram"))[0]
     waiters = [n for n, d in _deps(r).items() if "CloudRendering" in d]
+    assert waiters == ["LuminanceHistogramFold", "TemporalAntiAliasing+ToneMapping"]
+    # without the split only the composition waits for it
+    r2 = _renderer(soc, sky_split=False)
+    waiters = [n for n, d in _deps(r2).items() if "CloudRendering" in d]
     assert waiters == ["Composition+GenerateLuminanceHistogram"]
 
 
