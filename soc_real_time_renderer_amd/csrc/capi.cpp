@@ -1061,12 +1061,23 @@ extern "C" int soc_renderer_execute(soc_renderer* r, const soc_globals* g, int32
         lane[i] = (r->async && (p.flags & SOC_PASS_ASYNC)) ? 1 : 0;
         lanes |= lane[i] == 1;
     }
+    // dependencies among the passes run by this call; a skipped pass (no work this call) hands its own
+    // dependencies on to its dependents
+    std::vector<std::vector<int>> deps(n);
+    for (int i = 0; i < n; ++i) {
+        const auto& p = r->passes[i];
+        if (lane[i] < 0 && !(p.phase & phase)) continue;
+        for (int j : p.deps) {
+            if (lane[j] >= 0) deps[i].push_back(j);
+            else if (r->passes[j].phase & phase) deps[i].insert(deps[i].end(), deps[j].begin(), deps[j].end());
+        }
+    }
     // a pass records its completion event when a pass of the other lane depends on it
     std::vector<char> signal(n, 0);
     for (int i = 0; i < n; ++i)
         if (lane[i] >= 0)
-            for (int j : r->passes[i].deps)
-                if (lane[j] >= 0 && lane[j] != lane[i]) signal[j] = 1;
+            for (int j : deps[i])
+                if (lane[j] != lane[i]) signal[j] = 1;
     if (lanes) {
         int rc = ensure_side_lane(r);
         if (rc) return rc;
@@ -1078,8 +1089,8 @@ extern "C" int soc_renderer_execute(soc_renderer* r, const soc_globals* g, int32
         if (lane[i] < 0) continue;
         auto& p = r->passes[i];
         hipStream_t ls = lane[i] ? r->side : s;
-        for (int j : p.deps)
-            if (lane[j] >= 0 && lane[j] != lane[i] && hipStreamWaitEvent(ls, r->passes[j].done, 0) != hipSuccess)
+        for (int j : deps[i])
+            if (lane[j] != lane[i] && hipStreamWaitEvent(ls, r->passes[j].done, 0) != hipSuccess)
                 return set_error(SOC_E_HIP, "soc_renderer_execute: %s: cross-lane wait failed", p.name.c_str());
         int rc = run_pass(p, g, ls);
         if (rc) return rc;

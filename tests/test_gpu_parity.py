@@ -657,7 +657,7 @@ def test_render_graph_sky_split_bit_identical(soc, phases):
     exposure, resolved history), for one-call frames and PRE / POST frames (the multi-GPU shape)."""
     W, H = 1920, 1080
     g, gb = sponza_inputs(W, H, elapsed=10.0, camera=((-14.0, 2.2, 0.3), (0.0, -0.9, 0.0)))   # looking up: more sky
-    assert (gb["depth"] == 1.0).mean() > 0.1
+    assert (gb["depth"] == 1.0).mean() > 0.05
     outs = []
     for split in (True, False):
         fr = soc.alloc_frame(W, H, DEV, bloom_output=True)
