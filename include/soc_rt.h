@@ -505,7 +505,10 @@ typedef struct soc_mesh {              /* device pointers (Vertex, shared.inl:15
 /* Material (shared.inl:159-170, as GBufferGeneration's fragment shader reads it, g_buffer_generation.inl:
  * 189-225): albedo = sample(albedo).rgb * albedo_factor + emissive; emissive = sample(emissive).rgb *
  * emissive_factor (zero without an emissive image). Textures are RGBA8 (SRGB decoded to linear per
- * texel), bilinear, REPEAT, level 0 (no mip selection); data == NULL samples white (model.cpp:188). */
+ * texel), bilinear, REPEAT; data == NULL samples white (model.cpp:188). Without SOC_MATERIAL_MIPMAPPED only
+ * level 0 is read; with it every RGBA8 texture of the material carries its packed mip chain
+ * (soc_generate_mips) and is sampled trilinear + anisotropic (the reference's sampler, texture.cpp:121-136):
+ * see SOC_MATERIAL_MIPMAPPED. */
 typedef struct soc_material {
     soc_img albedo, emissive;
     float albedo_factor[4], emissive_factor[4];
@@ -514,6 +517,8 @@ typedef struct soc_material {
     int32_t pad[2];
     soc_img normal_map;                /* RGBA16F, used with SOC_MATERIAL_NORMAL_MAP */
     soc_img normal_image;              /* RGBA8_UNORM tangent-space normal texture, with SOC_MATERIAL_NORMAL_TEXTURE */
+    float max_anisotropy;              /* with SOC_MATERIAL_MIPMAPPED: 16 in the reference (texture.cpp:129-130) */
+    int32_t pad2[3];
 } soc_material;
 #define SOC_MATERIAL_ZERO_VELOCITY 1   /* write velocity 0 (the terrain draw, draw_terrain.inl:221) */
 #define SOC_MATERIAL_NORMAL_MAP 2      /* normal = normalize(bilinear normal_map(uv).xyz) (draw_terrain.inl:206-219) */
@@ -522,6 +527,15 @@ typedef struct soc_material {
  * position and uv, taken as FINE derivatives: the same triangle's perspective-correct attributes at the two pixel
  * centres of the pixel's 2x2 quad in that direction (what helper invocations evaluate). */
 #define SOC_MATERIAL_NORMAL_TEXTURE 4
+/* Mip-mapped sampling (texture.cpp:108-136: LINEAR min/mag/mip, REPEAT, anisotropy max_anisotropy, lod in
+ * [0, levels]). Per texture, from the FINE uv derivatives of the pixel's quad (as the TBN above), in level-0
+ * texels: Px = |(du/dx W, dv/dx H)|, Py = |(du/dy W, dv/dy H)|, N = min(ceil(Pmax / Pmin), floor(max_anisotropy))
+ * (1 when max_anisotropy <= 1, Pmax is 0 or not finite; floor(max_anisotropy) when Pmin is 0),
+ * lod = log2(Pmax / N) (the deterministic log2 of the histogram contract) rounded to 1/256 and clamped to
+ * [0, levels - 1]; result = (1/N) sum_{i=1..N} trilinear(uv + (i / (N + 1) - 1/2) d_major) with d_major the uv
+ * derivative of the longer axis (EXT_texture_filter_anisotropic's reference filter; N = 1 samples uv itself);
+ * trilinear = lerp of the bilinear REPEAT samples of levels floor(lod) and floor(lod) + 1. */
+#define SOC_MATERIAL_MIPMAPPED 8
 
 #define SOC_CULL_NONE 0
 #define SOC_CULL_FRONT 1               /* depth prepass / G-buffer (depth_prepass.inl:45) */
@@ -546,6 +560,19 @@ int soc_raster_depth(const soc_mesh* mesh, const float view_projection[16], int3
 int soc_gbuffer_resolve(const soc_globals* g, const soc_mesh* mesh, const soc_material* d_materials,
                         int32_t material_count, const uint64_t* visibility, soc_img depth, soc_img albedo,
                         soc_img emissive, soc_img normal, soc_img velocity, void* workspace, soc_stream stream);
+
+/* Texture mip chains (texture.cpp:108, 184-246): floor(log2(max(W, H))) + 1 levels, level k of max(1, W >> k) x
+ * max(1, H >> k) texels. Packed chain layout: level 0 is the soc_img itself (any pitch); level k >= 1 follows at
+ * data + pitch_bytes * H + sum_{1 <= j < k} 4 w_j h_j with tight rows. soc_mip_chain_bytes is the size of the
+ * whole allocation (level 0 included). */
+int32_t soc_mip_level_count(int32_t width, int32_t height);
+size_t soc_mip_chain_bytes(int32_t width, int32_t height, int32_t pitch_bytes);
+/* The load-time blit chain (texture.cpp:190-246): level k from level k-1 by a LINEAR blit (vkCmdBlitImage):
+ * destination texel (x, y) samples the source at ((x + 0.5) Ws / Wd, (y + 0.5) Hs / Hd) bilinearly, clamp to
+ * edge, 8-bit sub-texel weights; RGBA8_SRGB filters in linear space (per-texel decode, re-encoded to the
+ * nearest sRGB code: the largest k with linear >= the midpoint of codes k-1 and k), RGBA8_UNORM and alpha
+ * round to nearest. Runs once per texture at load (upload), one launch per level on `stream`. */
+int soc_generate_mips(soc_img texture, soc_stream stream);
 
 /* HeightToNormalTask (height_to_normal.inl:52-83): RGBA8 heightmap (.r) -> RGBA16F normal map of the same
  * extent; run once at terrain load (renderer.cpp:158-190). */

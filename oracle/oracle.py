@@ -39,6 +39,7 @@ _FUNCS = {
     "soc_oracle_gbuffer_resolve": (C.c_int, [_G, C.POINTER(_abi.Mesh), C.POINTER(_abi.Material), C.c_int32, C.c_void_p,
                                              _IMG, _IMG, _IMG, _IMG, _IMG]),
     "soc_oracle_height_to_normal": (C.c_int, [_IMG, _IMG]),
+    "soc_oracle_generate_mips": (C.c_int, [_IMG]),
     "soc_oracle_generate_hiz": (C.c_int, [_G, _IMG, C.POINTER(_IMG), C.c_int32, C.c_int32]),
     "soc_oracle_luminance_bin": (C.c_uint32, [C.c_float] * 5),
     "soc_oracle_log2": (C.c_float, [C.c_float]),
@@ -155,6 +156,11 @@ def gbuffer_resolve(g, mesh, materials, vis, depth, albedo, emissive, normal, ve
     _rc(lib().soc_oracle_gbuffer_resolve(C.byref(g), C.byref(mesh.struct), arr, len(materials), vis.ctypes.data,
                                          _img(depth), _img(albedo), _img(emissive), _img(normal), _img(velocity)),
         "gbuffer_resolve")
+
+
+def generate_mips(tex):
+    """Levels 1.. of a host MipTexture (raster.MipTexture over a numpy buffer), in place."""
+    _rc(lib().soc_oracle_generate_mips(tex.img()), "generate_mips")
 
 
 def height_to_normal(heightmap, target):

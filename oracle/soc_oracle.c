@@ -1183,6 +1183,143 @@ static v4 rs_sample_texture(const soc_img* tex, float u, float v) {
     return sample_repeat(tex, u, v);
 }
 
+/* ---- texture mip chains (texture.cpp:108, 184-246; soc_rt.h soc_generate_mips) ---- */
+static int mip_levels(int w, int h) {
+    int m = w > h ? w : h, n = 0;
+    while (m > 0) { ++n; m >>= 1; }
+    return n;
+}
+/* packed layout: level 0 = the image (any pitch), level k >= 1 tight, after the previous level */
+static size_t mip_offset(int w, int h, int pitch, int k, int* wk, int* hk) {
+    size_t off = 0;
+    *wk = w;
+    *hk = h;
+    for (int j = 1; j <= k; ++j) {
+        off += j == 1 ? (size_t)pitch * h : (size_t)4 * *wk * *hk;
+        *wk = *wk > 1 ? *wk >> 1 : 1;
+        *hk = *hk > 1 ? *hk >> 1 : 1;
+    }
+    return off;
+}
+static soc_img mip_level(const soc_img* tex, int k) {
+    int wk, hk;
+    size_t off = mip_offset(tex->width, tex->height, tex->pitch_bytes, k, &wk, &hk);
+    soc_img im = {(char*)tex->data + off, wk, hk, k ? 4 * wk : tex->pitch_bytes, tex->format};
+    return im;
+}
+
+/* vkCmdBlitImage LINEAR sample axis: destination texel x -> source coordinate (x + 0.5) n_src / n_dst, clamp to
+   edge, the sampling contract's 8-bit weights */
+static void blit_axis(int x, int n_src, int n_dst, int* i0, int* i1, float* w) {
+    const float t = ((float)(2 * x + 1) * (float)n_src) / (float)(2 * n_dst) - 0.5f;
+    const int fx = (int)floorf(t * 256.0f + 0.5f);
+    int i = fx >> 8;
+    float ww = (float)(fx & 255) * (1.0f / 256.0f);
+    if (i < 0) { i = 0; ww = 0.0f; }
+    else if (i >= n_src - 1) { i = n_src - 2; ww = 1.0f; }
+    if (n_src == 1) { i = 0; ww = 0.0f; }
+    *i0 = i;
+    *i1 = i + 1 < n_src - 1 ? i + 1 : n_src - 1;
+    *w = ww;
+}
+
+int soc_oracle_generate_mips(soc_img tex) {
+    if (!tex.data || tex.width <= 0 || tex.height <= 0 || tex.pitch_bytes < tex.width * 4 ||
+        (tex.format != SOC_FMT_RGBA8_UNORM && tex.format != SOC_FMT_RGBA8_SRGB))
+        return SOC_E_INVALID_ARG;
+    /* sRGB tables in double precision: decode per code, re-encode to the nearest code (midpoints) */
+    float dec[256], mid[256];
+    double prev = 0.0;
+    for (int k = 0; k < 256; ++k) {
+        const double c = k / 255.0;
+        const double d = c <= 0.04045 ? c / 12.92 : pow((c + 0.055) / 1.055, 2.4);
+        dec[k] = (float)d;
+        mid[k] = k ? (float)(0.5 * (prev + d)) : 0.0f;
+        prev = d;
+    }
+    const int srgb = tex.format == SOC_FMT_RGBA8_SRGB, L = mip_levels(tex.width, tex.height);
+    for (int k = 1; k < L; ++k) {
+        const soc_img src = mip_level(&tex, k - 1), dst = mip_level(&tex, k);
+        for (int y = 0; y < dst.height; ++y)
+            for (int x = 0; x < dst.width; ++x) {
+                int x0, x1, y0, y1;
+                float wx, wy;
+                blit_axis(x, src.width, dst.width, &x0, &x1, &wx);
+                blit_axis(y, src.height, dst.height, &y0, &y1, &wy);
+                const uint8_t* r0 = (const uint8_t*)src.data + (size_t)y0 * src.pitch_bytes;
+                const uint8_t* r1 = (const uint8_t*)src.data + (size_t)y1 * src.pitch_bytes;
+                uint8_t* o = (uint8_t*)dst.data + (size_t)y * dst.pitch_bytes + 4 * (size_t)x;
+                for (int c = 0; c < 4; ++c) {
+                    const uint8_t b[4] = {r0[4 * x0 + c], r0[4 * x1 + c], r1[4 * x0 + c], r1[4 * x1 + c]};
+                    float v[4];
+                    for (int q = 0; q < 4; ++q) v[q] = (srgb && c < 3) ? dec[b[q]] : unorm8(b[q]);
+                    const float f = lerp_w(lerp_w(v[0], v[1], wx), lerp_w(v[2], v[3], wx), wy);
+                    if (srgb && c < 3) {
+                        int code = 0;
+                        while (code < 255 && f >= mid[code + 1]) ++code;
+                        o[c] = (uint8_t)code;
+                    } else {
+                        o[c] = to_unorm8(f);
+                    }
+                }
+            }
+    }
+    return SOC_OK;
+}
+
+/* bilinear REPEAT sample of one chain level */
+static v4 rs_sample_level(const soc_img* tex, int k, float u, float v) {
+    const soc_img im = mip_level(tex, k);
+    return sample_repeat(&im, u, v);
+}
+
+/* SOC_MATERIAL_MIPMAPPED sampling (soc_rt.h): trilinear + EXT_texture_filter_anisotropic's reference filter
+   over the fine uv derivatives (texture.cpp:121-136: LINEAR/LINEAR/LINEAR, REPEAT, anisotropy 16) */
+static v4 rs_sample_texture_mip(const soc_img* tex, float u, float v, float dudx, float dvdx, float dudy, float dvdy,
+                                float max_aniso) {
+    if (!tex->data) return V4(1.0f, 1.0f, 1.0f, 1.0f);
+    const int L = mip_levels(tex->width, tex->height);
+    const float W = (float)tex->width, H = (float)tex->height;
+    const float ax = dudx * W, ay = dvdx * H, bx = dudy * W, by = dvdy * H;
+    const float px = sqrtf(ax * ax + ay * ay), py = sqrtf(bx * bx + by * by);
+    const float pmax = fmaxf(px, py), pmin = fminf(px, py);
+    int n = 1;
+    if (max_aniso > 1.0f && pmax > 0.0f && pmax <= 3.4e38f) {
+        const float cap = floorf(max_aniso);
+        n = (int)(pmin > 0.0f ? fminf(ceilf(pmax / pmin), cap) : cap);
+    }
+    int lq = 0;
+    const float rho = pmax / (float)n;
+    if (rho > 0.0f && rho <= 3.4e38f) {
+        const float lam = fminf(fmaxf(soc_oracle_log2(rho), -64.0f), 64.0f);
+        lq = (int)floorf(lam * 256.0f + 0.5f);
+        if (lq < 0) lq = 0;
+        if (lq > (L - 1) * 256) lq = (L - 1) * 256;
+    }
+    const int l0 = lq >> 8;
+    const float f = (float)(lq & 255) * (1.0f / 256.0f);
+    const int xmajor = px >= py;
+    const float du = xmajor ? dudx : dudy, dv = xmajor ? dvdx : dvdy;
+    v4 acc = V4(0.0f, 0.0f, 0.0f, 0.0f);
+    for (int i = 1; i <= n; ++i) {
+        float su = u, sv = v;
+        if (n > 1) {
+            const float t = (float)i / (float)(n + 1) - 0.5f;
+            su = u + t * du;
+            sv = v + t * dv;
+        }
+        v4 s0 = rs_sample_level(tex, l0, su, sv);
+        if (lq & 255) {
+            const v4 s1 = rs_sample_level(tex, l0 + 1, su, sv);
+            s0 = V4(lerp_w(s0.x, s1.x, f), lerp_w(s0.y, s1.y, f), lerp_w(s0.z, s1.z, f), lerp_w(s0.w, s1.w, f));
+        }
+        acc = V4(acc.x + s0.x, acc.y + s0.y, acc.z + s0.z, acc.w + s0.w);
+    }
+    if (n == 1) return acc;
+    const float fn = (float)n;
+    return V4(acc.x / fn, acc.y / fn, acc.z / fn, acc.w / fn);
+}
+
 static v3 rs_normalize(v3 a) {
     float l = sqrtf(a.x * a.x + a.y * a.y + a.z * a.z);
     return V3(a.x / l, a.y / l, a.z / l);
@@ -1248,31 +1385,42 @@ int soc_oracle_gbuffer_resolve(const soc_globals* g, const soc_mesh* mesh, const
                 n = rs_normalize(V3(b0 * na.x + b1 * nb.x + b2 * nc.x, b0 * na.y + b1 * nb.y + b2 * nc.y,
                                     b0 * na.z + b1 * nb.z + b2 * nc.z));
             }
-            if ((m->flags & SOC_MATERIAL_NORMAL_TEXTURE) && m->normal_image.data) {   /* g_buffer_generation.inl:197-211 */
-                const v4 t = rs_sample_texture(&m->normal_image, u, v);
-                const v3 tn = V3(t.x * 2.0f - 1.0f, t.y * 2.0f - 1.0f, t.z * 2.0f - 1.0f);
-                v4 wp[3];
+            const int tbn = (m->flags & SOC_MATERIAL_NORMAL_TEXTURE) && m->normal_image.data;
+            const int mipped = (m->flags & SOC_MATERIAL_MIPMAPPED) != 0;
+            /* fine dFdx / dFdy: the same triangle's attributes at the two centres of the 2x2 quad per direction */
+            v3 Q1 = V3(0, 0, 0), Q2 = V3(0, 0, 0);
+            float gd[4] = {0.0f, 0.0f, 0.0f, 0.0f};   /* du/dx, dv/dx, du/dy, dv/dy */
+            if (tbn || mipped) {
+                v4 wp[3] = {V4(0, 0, 0, 0), V4(0, 0, 0, 0), V4(0, 0, 0, 0)};
                 const uint32_t vi[3] = {ia, ib, ic};
-                for (int k = 0; k < 3; ++k) {
-                    const float* p = mesh->positions + 3 * (size_t)vi[k];
-                    wp[k] = mat_vec4(M, p[0], p[1], p[2], 1.0f);
-                }
-                /* fine dFdx / dFdy: the same triangle's attributes at the two centres of the 2x2 quad per direction */
+                if (tbn)
+                    for (int k = 0; k < 3; ++k) {
+                        const float* p = mesh->positions + 3 * (size_t)vi[k];
+                        wp[k] = mat_vec4(M, p[0], p[1], p[2], 1.0f);
+                    }
                 const float qx = (float)(x & ~1) + 0.5f, qy = (float)(y & ~1) + 0.5f;
                 const float sxs[4] = {qx, qx + 1.0f, fx, fx}, sys[4] = {fy, fy, qy, qy + 1.0f};
                 v3 P[4];
-                float tv[4];
+                float tu[4], tv[4];
                 for (int k = 0; k < 4; ++k) {
                     const float a0 = rs_edge(r0, sxs[k], sys[k]), a1 = rs_edge(r1, sxs[k], sys[k]), a2 = rs_edge(r2, sxs[k], sys[k]);
                     const float as = a0 + a1 + a2;
                     const float c1 = a1 / as, c2 = a2 / as, c0 = 1.0f - c1 - c2;
                     P[k] = V3(c0 * wp[0].x + c1 * wp[1].x + c2 * wp[2].x, c0 * wp[0].y + c1 * wp[1].y + c2 * wp[2].y,
                               c0 * wp[0].z + c1 * wp[1].z + c2 * wp[2].z);
+                    tu[k] = c0 * uv[2 * ia] + c1 * uv[2 * ib] + c2 * uv[2 * ic];
                     tv[k] = c0 * uv[2 * ia + 1] + c1 * uv[2 * ib + 1] + c2 * uv[2 * ic + 1];
                 }
-                const v3 Q1 = V3(P[1].x - P[0].x, P[1].y - P[0].y, P[1].z - P[0].z);
-                const v3 Q2 = V3(P[3].x - P[2].x, P[3].y - P[2].y, P[3].z - P[2].z);
-                const float st1t = tv[1] - tv[0], st2t = tv[3] - tv[2];
+                Q1 = V3(P[1].x - P[0].x, P[1].y - P[0].y, P[1].z - P[0].z);
+                Q2 = V3(P[3].x - P[2].x, P[3].y - P[2].y, P[3].z - P[2].z);
+                gd[0] = tu[1] - tu[0]; gd[1] = tv[1] - tv[0]; gd[2] = tu[3] - tu[2]; gd[3] = tv[3] - tv[2];
+            }
+#define RS_TEX(img) (mipped ? rs_sample_texture_mip(&(img), u, v, gd[0], gd[1], gd[2], gd[3], m->max_anisotropy) \
+                            : rs_sample_texture(&(img), u, v))
+            if (tbn) {   /* g_buffer_generation.inl:197-211 */
+                const v4 t = RS_TEX(m->normal_image);
+                const v3 tn = V3(t.x * 2.0f - 1.0f, t.y * 2.0f - 1.0f, t.z * 2.0f - 1.0f);
+                const float st1t = gd[1], st2t = gd[3];
                 const v3 N = rs_normalize(n);
                 const v3 T = rs_normalize(V3(Q1.x * st2t - Q2.x * st1t, Q1.y * st2t - Q2.y * st1t, Q1.z * st2t - Q2.z * st1t));
                 const v3 B = rs_normalize(cross3(N, T));
@@ -1281,10 +1429,11 @@ int soc_oracle_gbuffer_resolve(const soc_globals* g, const soc_mesh* mesh, const
             }
             v3 em = V3(0, 0, 0);
             if (m->has_emissive) {
-                v4 e = rs_sample_texture(&m->emissive, u, v);
+                v4 e = RS_TEX(m->emissive);
                 em = V3(e.x * m->emissive_factor[0], e.y * m->emissive_factor[1], e.z * m->emissive_factor[2]);
             }
-            const v4 al = rs_sample_texture(&m->albedo, u, v);
+            const v4 al = RS_TEX(m->albedo);
+#undef RS_TEX
             v4 vel = V4(0, 0, 0, 0);
             if (!(m->flags & SOC_MATERIAL_ZERO_VELOCITY)) {
                 v4 cc[3], pc[3];

@@ -46,6 +46,8 @@ int soc_oracle_gbuffer_resolve(const soc_globals* g, const soc_mesh* mesh, const
                                int32_t material_count, const uint64_t* visibility, soc_img depth, soc_img albedo,
                                soc_img emissive, soc_img normal, soc_img velocity);
 
+/* soc_generate_mips (texture.cpp:184-246): levels 1.. of a packed RGBA8 chain from level 0, in place. */
+int soc_oracle_generate_mips(soc_img texture);
 int soc_oracle_height_to_normal(soc_img heightmap, soc_img target);
 int soc_oracle_generate_hiz(const soc_globals* g, soc_img depth, const soc_img* mips, int32_t mip_count, int32_t op_max);
 

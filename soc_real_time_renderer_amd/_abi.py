@@ -126,7 +126,8 @@ class Mesh(C.Structure):
 class Material(C.Structure):
     _fields_ = [("albedo", SocImg), ("emissive", SocImg), ("albedo_factor", C.c_float * 4),
                 ("emissive_factor", C.c_float * 4), ("flags", C.c_int32), ("has_emissive", C.c_int32),
-                ("pad", C.c_int32 * 2), ("normal_map", SocImg), ("normal_image", SocImg)]
+                ("pad", C.c_int32 * 2), ("normal_map", SocImg), ("normal_image", SocImg),
+                ("max_anisotropy", C.c_float), ("pad2", C.c_int32 * 3)]
 
 
 class RasterScene(C.Structure):
@@ -168,6 +169,7 @@ CULL_NONE, CULL_FRONT, CULL_BACK = 0, 1, 2
 MATERIAL_ZERO_VELOCITY = 1
 MATERIAL_NORMAL_MAP = 2
 MATERIAL_NORMAL_TEXTURE = 4
+MATERIAL_MIPMAPPED = 8
 
 STRUCTS = {"soc_img": SocImg, "soc_globals": Globals, "soc_sun_info": SunInfo, "soc_point_light": PointLight,
            "soc_spot_light": SpotLight, "soc_auto_exposure": AutoExposure, "soc_camera": Camera,
@@ -234,6 +236,9 @@ FUNCTIONS = {
     "soc_raster_workspace_size": (C.c_size_t, [C.c_int32, C.c_int32]),
     "soc_renderer_set_raster_scene": (_I, [_P, C.POINTER(RasterScene)]),
     "soc_height_to_normal": (_I, [_IMG, _IMG, _P]),
+    "soc_mip_level_count": (_I, [_I, _I]),
+    "soc_mip_chain_bytes": (C.c_size_t, [_I, _I, _I]),
+    "soc_generate_mips": (_I, [_IMG, _P]),
     "soc_generate_hiz": (_I, [_G, _IMG, C.POINTER(SocImg), C.c_int32, C.c_int32, _P, _P]),
     "soc_renderer_metrics_json": (C.c_int64, [_P, C.c_uint64, C.c_char_p, C.c_size_t]),
     "soc_read_image": (_I, [_IMG, _P, C.c_int32, _P]),

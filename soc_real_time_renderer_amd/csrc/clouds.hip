@@ -571,8 +571,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void c
     }
 }
 
-template <bool NOISE_R8>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void clouds_sunvis(
+// 512-lane workgroups: the 26 KiB noise table per workgroup caps residency at 6 workgroups per CU, so 256 lanes
+// give 6 waves per SIMD and 512 lanes give the full 8 (one table per 8 waves).
+template <bool NOISE_R8, uint32_t kSunvisThreads>
+__global__ __launch_bounds__(kSunvisThreads) __attribute__((amdgpu_waves_per_eu(kSunvisThreads == 512 ? 8 : 6))) void clouds_sunvis(
     DImg noise, CloudParams p, const uint32_t* __restrict__ list, PairBufs pb) {
     __shared__ uint32_t quads[kTable];
     __shared__ uint32_t pre[kShards + 1];
@@ -587,8 +589,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void c
     }
     __syncthreads();
     const uint32_t total = pre[kShards];
-    if (blockIdx.x * 256u >= total) return;
-    stage_noise<NOISE_R8>(noise, quads, tid, 256);
+    if (blockIdx.x * kSunvisThreads >= total) return;
+    stage_noise<NOISE_R8>(noise, quads, tid, kSunvisThreads);
     __syncthreads();
     Ctx cx;
     cx.quads = quads;
@@ -596,7 +598,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void c
     cx.cam_z = p.cam[2];
     cx.time = -1.0f * 0.02f * p.elapsed;
     const f3 sun = f3{p.sun[0], p.sun[1], p.sun[2]};
-    for (uint32_t v = blockIdx.x * 256u + tid; v < total; v += gridDim.x * 256u) {
+    for (uint32_t v = blockIdx.x * kSunvisThreads + tid; v < total; v += gridDim.x * kSunvisThreads) {
         int k = 0;
         while (k + 1 < kShards && v >= pre[k + 1]) ++k;
         const uint32_t phys = (uint32_t)k * pb.cap + (v - pre[k]);
@@ -685,14 +687,14 @@ __global__ __launch_bounds__(256) void clouds_resolve(DImg noise, DImg target, C
     }
 }
 
-// Lanes resident on the device for a 256-thread kernel (grid of one full wave set).
+// Workgroups resident on the device for a kernel of `threads` lanes per workgroup (grid of one full wave set).
 template <typename K>
-int resident_blocks(K kernel) {
+int resident_blocks(K kernel, int threads = 256) {
     int dev = 0, cus = 256, per_cu = 0;
     (void)hipGetDevice(&dev);
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0) cus = prop.multiProcessorCount;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || per_cu < 1) per_cu = 4;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0) != hipSuccess || per_cu < 1) per_cu = 2;
     return per_cu * cus;
 }
 
@@ -790,14 +792,13 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
     // One resident wave set per kernel, grid-stride over the list / pairs: the long per-item work is
     // balanced over all SIMDs instead of running as a second, partially filled round.
     static int res_atmos = 0, res_density = 0, res_sunvis = 0, res_resolve = 0;
+    static bool sunvis512 = true;
     if (!res_atmos) {
-        const char* ev = getenv("SOC_SKY_SHARE");   // tuning knob: fraction of the resident wave set
-        const double share = ev ? atof(ev) : 1.0;
-        auto scaled = [&](int res) { return std::max(1, (int)(res * share)); };
-        res_atmos = scaled(resident_blocks(clouds_atmosphere));
-        res_density = scaled(resident_blocks(clouds_density<false>));
-        res_sunvis = scaled(resident_blocks(clouds_sunvis<false>));
-        res_resolve = scaled(resident_blocks(clouds_resolve<false>));
+        res_atmos = resident_blocks(clouds_atmosphere);
+        res_density = resident_blocks(clouds_density<false>);
+        sunvis512 = tuning_knob("SOC_SUNVIS_THREADS", 512) == 512;
+        res_sunvis = sunvis512 ? resident_blocks(clouds_sunvis<false, 512>, 512) : resident_blocks(clouds_sunvis<false, 256>, 256);
+        res_resolve = resident_blocks(clouds_resolve<false>);
     }
     const long long blocks = ((long long)W * H + 255) / 256;
     if (SOC_CLOUDS_PROFILE >= 4) return check_launch("cloud_rendering");
@@ -806,11 +807,13 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
     const DImg nz = dimg(noise), tg = dimg(target);
     if (r8) {
         clouds_density<true><<<grid(res_density, blocks), 256, 0, s>>>(nz, p, counter, list, ws.pb);
-        clouds_sunvis<true><<<grid(res_sunvis, 2 * blocks), 256, 0, s>>>(nz, p, list, ws.pb);
+        if (sunvis512) clouds_sunvis<true, 512><<<grid(res_sunvis, blocks), 512, 0, s>>>(nz, p, list, ws.pb);
+        else clouds_sunvis<true, 256><<<grid(res_sunvis, 2 * blocks), 256, 0, s>>>(nz, p, list, ws.pb);
         clouds_resolve<true><<<grid(res_resolve, blocks), 256, 0, s>>>(nz, tg, p, counter, list, ws.atmos, ws.pb);
     } else {
         clouds_density<false><<<grid(res_density, blocks), 256, 0, s>>>(nz, p, counter, list, ws.pb);
-        clouds_sunvis<false><<<grid(res_sunvis, 2 * blocks), 256, 0, s>>>(nz, p, list, ws.pb);
+        if (sunvis512) clouds_sunvis<false, 512><<<grid(res_sunvis, blocks), 512, 0, s>>>(nz, p, list, ws.pb);
+        else clouds_sunvis<false, 256><<<grid(res_sunvis, 2 * blocks), 256, 0, s>>>(nz, p, list, ws.pb);
         clouds_resolve<false><<<grid(res_resolve, blocks), 256, 0, s>>>(nz, tg, p, counter, list, ws.atmos, ws.pb);
     }
     return check_launch("cloud_rendering");

@@ -21,6 +21,7 @@
 // The coverage, depth and barycentric arithmetic is written without FMA contraction and matches the
 // oracle's (oracle/soc_oracle.c, soc_oracle_raster_*) operation for operation, so the visibility buffer
 // and the depth images are bit-exact against it.
+#include "luminance.hpp"
 #include "soc_internal.hpp"
 
 namespace soc {
@@ -364,6 +365,65 @@ __device__ __forceinline__ f4 sample_texture(const soc_img& tex, float u, float 
     return bilerp4(a, b, c, d, ax.w, ay.w);
 }
 
+// Bilinear REPEAT sample of level k of a packed mip chain (soc_generate_mips layout).
+__device__ __forceinline__ f4 sample_level(const soc_img& tex, int k, float u, float v, bool srgb, const float* lut) {
+    int wk, hk;
+    const size_t off = mip_offset(tex.width, tex.height, tex.pitch_bytes, k, wk, hk);
+    const DImg im{static_cast<char*>(tex.data) + off, wk, hk, k ? 4 * wk : tex.pitch_bytes};
+    const Axis ax = axis_repeat_any(u, wk), ay = axis_repeat_any(v, hk);
+    const f4 a = texel_rgba8(im, ax.i0, ay.i0, srgb, lut), b = texel_rgba8(im, ax.i1, ay.i0, srgb, lut);
+    const f4 c = texel_rgba8(im, ax.i0, ay.i1, srgb, lut), d = texel_rgba8(im, ax.i1, ay.i1, srgb, lut);
+    return bilerp4(a, b, c, d, ax.w, ay.w);
+}
+
+// Fine uv derivatives of the pixel's quad.
+struct UVGrad { float dudx, dvdx, dudy, dvdy; };
+
+// Trilinear + anisotropic REPEAT sample of a mip-chained texture (soc_rt.h SOC_MATERIAL_MIPMAPPED).
+__device__ f4 sample_texture_mip(const soc_img& tex, float u, float v, const UVGrad& gr, float max_aniso, const float* lut) {
+#pragma clang fp contract(off)
+    if (!tex.data) return f4{1.0f, 1.0f, 1.0f, 1.0f};
+    const bool srgb = tex.format == SOC_FMT_RGBA8_SRGB;
+    const int L = mip_levels(tex.width, tex.height);
+    const float W = (float)tex.width, H = (float)tex.height;
+    const float ax = gr.dudx * W, ay = gr.dvdx * H, bx = gr.dudy * W, by = gr.dvdy * H;
+    const float px = sqrtf(ax * ax + ay * ay), py = sqrtf(bx * bx + by * by);
+    const float pmax = fmaxf(px, py), pmin = fminf(px, py);
+    int n = 1;
+    if (max_aniso > 1.0f && pmax > 0.0f && pmax <= 3.4e38f) {
+        const float cap = floorf(max_aniso);
+        n = (int)(pmin > 0.0f ? fminf(ceilf(pmax / pmin), cap) : cap);
+    }
+    int lq = 0;   // lod in 1/256 steps, clamped to [0, (L - 1) 256]
+    const float rho = pmax / (float)n;
+    if (rho > 0.0f && rho <= 3.4e38f) {
+        const float lam = fminf(fmaxf(det_log2(rho), -64.0f), 64.0f);
+        lq = min(max((int)floorf(lam * 256.0f + 0.5f), 0), (L - 1) * 256);
+    }
+    const int l0 = lq >> 8;
+    const float f = (float)(lq & 255) * (1.0f / 256.0f);
+    const bool xmajor = px >= py;
+    const float du = xmajor ? gr.dudx : gr.dudy, dv = xmajor ? gr.dvdx : gr.dvdy;
+    f4 acc = f4{0.0f, 0.0f, 0.0f, 0.0f};
+    for (int i = 1; i <= n; ++i) {
+        float su = u, sv = v;
+        if (n > 1) {
+            const float t = (float)i / (float)(n + 1) - 0.5f;
+            su = u + t * du;
+            sv = v + t * dv;
+        }
+        f4 s0 = sample_level(tex, l0, su, sv, srgb, lut);
+        if (lq & 255) {
+            const f4 s1 = sample_level(tex, l0 + 1, su, sv, srgb, lut);
+            s0 = f4{lerp_w(s0.x, s1.x, f), lerp_w(s0.y, s1.y, f), lerp_w(s0.z, s1.z, f), lerp_w(s0.w, s1.w, f)};
+        }
+        acc = f4{acc.x + s0.x, acc.y + s0.y, acc.z + s0.z, acc.w + s0.w};
+    }
+    if (n == 1) return acc;
+    const float fn = (float)n;
+    return f4{acc.x / fn, acc.y / fn, acc.z / fn, acc.w / fn};
+}
+
 __device__ __forceinline__ f3 mat3_vec_exact(const Mat3& M, f3 v) {
 #pragma clang fp contract(off)
     const float* m = M.m;
@@ -467,15 +527,20 @@ __global__ __launch_bounds__(256) void gbuffer_resolve(soc_mesh mesh, const soc_
         n = normalize_exact(f3{b0 * na.x + b1 * nb.x + b2 * nc.x, b0 * na.y + b1 * nb.y + b2 * nc.y,
                                b0 * na.z + b1 * nb.z + b2 * nc.z});
     }
-    if ((m.flags & SOC_MATERIAL_NORMAL_TEXTURE) && m.normal_image.data) {   // g_buffer_generation.inl:197-211
-        const f4 t = sample_texture(m.normal_image, u, v, lut);
-        const f3 tn{t.x * 2.0f - 1.0f, t.y * 2.0f - 1.0f, t.z * 2.0f - 1.0f};
-        // world positions of the triangle's vertices (vertex stage out_position, :171-172)
+    const bool tbn = (m.flags & SOC_MATERIAL_NORMAL_TEXTURE) && m.normal_image.data;
+    const bool mipped = m.flags & SOC_MATERIAL_MIPMAPPED;
+    // fine dFdx / dFdy: this triangle's attributes at the two centres of the pixel's 2x2 quad per direction
+    // (what helper invocations evaluate); world positions only for the TBN
+    f3 Q1{0.0f, 0.0f, 0.0f}, Q2{0.0f, 0.0f, 0.0f};
+    UVGrad gr{0.0f, 0.0f, 0.0f, 0.0f};
+    if (tbn || mipped) {
         const float* ps = mesh.positions;
-        const f4 wa = mat_vec_exact(p.model, ps[3 * ia], ps[3 * ia + 1], ps[3 * ia + 2], 1.0f);
-        const f4 wb = mat_vec_exact(p.model, ps[3 * ib], ps[3 * ib + 1], ps[3 * ib + 2], 1.0f);
-        const f4 wc = mat_vec_exact(p.model, ps[3 * ic], ps[3 * ic + 1], ps[3 * ic + 2], 1.0f);
-        // fine dFdx / dFdy: this triangle's attributes at the two centres of the pixel's 2x2 quad per direction
+        f4 wa{0.0f, 0.0f, 0.0f, 0.0f}, wb = wa, wc = wa;
+        if (tbn) {   // vertex stage out_position (:171-172)
+            wa = mat_vec_exact(p.model, ps[3 * ia], ps[3 * ia + 1], ps[3 * ia + 2], 1.0f);
+            wb = mat_vec_exact(p.model, ps[3 * ib], ps[3 * ib + 1], ps[3 * ib + 2], 1.0f);
+            wc = mat_vec_exact(p.model, ps[3 * ic], ps[3 * ic + 1], ps[3 * ic + 2], 1.0f);
+        }
         auto attr = [&](float sx, float sy, f3& P, float& su, float& sv) {
             const float a0 = edge(r0, sx, sy), a1 = edge(r1, sx, sy), a2 = edge(r2, sx, sy);
             const float as = a0 + a1 + a2;
@@ -491,9 +556,17 @@ __global__ __launch_bounds__(256) void gbuffer_resolve(soc_mesh mesh, const soc_
         attr(qx + 1.0f, fy, px1, ux1, vx1);
         attr(fx, qy, py0, uy0, vy0);
         attr(fx, qy + 1.0f, py1, uy1, vy1);
-        const f3 Q1{px1.x - px0.x, px1.y - px0.y, px1.z - px0.z}, Q2{py1.x - py0.x, py1.y - py0.y, py1.z - py0.z};
-        const float st1t = vx1 - vx0, st2t = vy1 - vy0;
-        (void)ux0; (void)ux1; (void)uy0; (void)uy1;
+        Q1 = f3{px1.x - px0.x, px1.y - px0.y, px1.z - px0.z};
+        Q2 = f3{py1.x - py0.x, py1.y - py0.y, py1.z - py0.z};
+        gr = UVGrad{ux1 - ux0, vx1 - vx0, uy1 - uy0, vy1 - vy0};
+    }
+    auto tex = [&](const soc_img& t) {
+        return mipped ? sample_texture_mip(t, u, v, gr, m.max_anisotropy, lut) : sample_texture(t, u, v, lut);
+    };
+    if (tbn) {   // g_buffer_generation.inl:197-211
+        const f4 t = tex(m.normal_image);
+        const f3 tn{t.x * 2.0f - 1.0f, t.y * 2.0f - 1.0f, t.z * 2.0f - 1.0f};
+        const float st1t = gr.dvdx, st2t = gr.dvdy;
         const f3 N = normalize_exact(n);
         const f3 T = normalize_exact(f3{Q1.x * st2t - Q2.x * st1t, Q1.y * st2t - Q2.y * st1t, Q1.z * st2t - Q2.z * st1t});
         const f3 B = normalize_exact(cross_exact(N, T));
@@ -502,10 +575,10 @@ __global__ __launch_bounds__(256) void gbuffer_resolve(soc_mesh mesh, const soc_
     }
     f3 em = f3{0.0f, 0.0f, 0.0f};
     if (m.has_emissive) {
-        const f4 e = sample_texture(m.emissive, u, v, lut);
+        const f4 e = tex(m.emissive);
         em = f3{e.x * m.emissive_factor[0], e.y * m.emissive_factor[1], e.z * m.emissive_factor[2]};
     }
-    const f4 al = sample_texture(m.albedo, u, v, lut);
+    const f4 al = tex(m.albedo);
     f4 vel = f4{0.0f, 0.0f, 0.0f, 0.0f};
     if (!(m.flags & SOC_MATERIAL_ZERO_VELOCITY)) {
         const float4 ca = VA.cc, cb = VB.cc, cd = VC.cc, pa = VA.pc, pb = VB.pc, pd = VC.pc;

@@ -149,6 +149,24 @@ __device__ __forceinline__ f4 sample_rgba8(const DImg& im, float u, float v) {
                    fetch_rgba8(im, ax.i1, ay.i1), ax.w, ay.w);
 }
 
+// Packed mip chain (soc_rt.h soc_generate_mips): level count and the byte offset / extent of level k.
+__host__ __device__ __forceinline__ int mip_levels(int w, int h) {
+    int m = w > h ? w : h, n = 0;
+    while (m > 0) { ++n; m >>= 1; }
+    return n;
+}
+__host__ __device__ __forceinline__ size_t mip_offset(int w, int h, int pitch, int k, int& wk, int& hk) {
+    size_t off = 0;
+    wk = w;
+    hk = h;
+    for (int j = 1; j <= k; ++j) {
+        off += j == 1 ? (size_t)pitch * h : (size_t)4 * wk * hk;
+        wk = wk > 1 ? wk >> 1 : 1;
+        hk = hk > 1 ? hk >> 1 : 1;
+    }
+    return off;
+}
+
 // GLSL mat4 * vec4 on a column-major float[16] (kernel-argument copy).
 struct Mat4 { float m[16]; };
 struct Mat3 { float m[9]; };

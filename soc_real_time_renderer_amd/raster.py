@@ -16,11 +16,10 @@ import numpy as np
 import torch
 
 from . import _abi, _check, _gp, _ptr, _stream, img, lib
-from ._abi import (CULL_BACK, CULL_FRONT, CULL_NONE, FMT_RGBA8_SRGB, FMT_RGBA8_UNORM, MATERIAL_NORMAL_MAP,
-                   MATERIAL_NORMAL_TEXTURE, MATERIAL_ZERO_VELOCITY,
-                   Material, Mesh)
+from ._abi import (CULL_BACK, CULL_FRONT, CULL_NONE, FMT_RGBA8_SRGB, FMT_RGBA8_UNORM, MATERIAL_MIPMAPPED,
+                   MATERIAL_NORMAL_MAP, MATERIAL_NORMAL_TEXTURE, MATERIAL_ZERO_VELOCITY, Material, Mesh, SocImg)
 
-__all__ = ["CULL_NONE", "CULL_FRONT", "CULL_BACK", "MATERIAL_ZERO_VELOCITY", "MeshBuffers", "material",
+__all__ = ["CULL_NONE", "CULL_FRONT", "CULL_BACK", "MATERIAL_ZERO_VELOCITY", "MeshBuffers", "MipTexture", "material",
            "normal_matrix", "materials_device", "raster_visibility", "raster_depth", "gbuffer_resolve",
            "SHADOW_BIAS_CONSTANT", "SHADOW_BIAS_SLOPE"]
 
@@ -83,23 +82,82 @@ class MeshBuffers:
         return torch.empty(n, dtype=torch.uint8, device=device)
 
 
+def mip_level_count(width: int, height: int) -> int:
+    """floor(log2(max(W, H))) + 1 (texture.cpp:108)."""
+    return int(lib().soc_mip_level_count(int(width), int(height)))
+
+
+def mip_level_shapes(width: int, height: int):
+    """(h, w) of every level of a chain: max(1, W >> k) x max(1, H >> k)."""
+    return [(max(1, height >> k), max(1, width >> k)) for k in range(mip_level_count(width, height))]
+
+
+class MipTexture:
+    """An RGBA8 texture with its packed mip chain (include/soc_rt.h soc_generate_mips): `buf` is one flat uint8
+    buffer (device tensor or host array) holding level 0 (tight rows) followed by levels 1.. . The reference
+    builds the chain at upload (texture.cpp:184-246); build() does the same on the GPU."""
+
+    def __init__(self, buf, width: int, height: int, srgb: bool = True):
+        self.buf, self.width, self.height = buf, int(width), int(height)
+        self.format = FMT_RGBA8_SRGB if srgb else FMT_RGBA8_UNORM
+
+    @staticmethod
+    def chain_bytes(width: int, height: int) -> int:
+        return int(lib().soc_mip_chain_bytes(int(width), int(height), int(width) * 4))
+
+    @classmethod
+    def build(cls, level0, srgb: bool = True, device="cuda", stream=None) -> "MipTexture":
+        """Upload an (H, W, 4) uint8 level 0 and generate levels 1.. with soc_generate_mips."""
+        t = level0 if isinstance(level0, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(level0, np.uint8))
+        H, W = int(t.shape[0]), int(t.shape[1])
+        buf = torch.empty(cls.chain_bytes(W, H), dtype=torch.uint8, device=device)
+        buf[:H * W * 4].copy_(t.reshape(-1))
+        tex = cls(buf, W, H, srgb)
+        _check(lib().soc_generate_mips(tex.img(), _stream(stream)), "generate_mips")
+        return tex
+
+    def img(self) -> SocImg:
+        ptr = self.buf.data_ptr() if isinstance(self.buf, torch.Tensor) else self.buf.ctypes.data
+        return SocImg(ptr, self.width, self.height, self.width * 4, self.format)
+
+    def levels(self):
+        """Host copies of every level, (h, w, 4) uint8."""
+        raw = self.buf.cpu().numpy() if isinstance(self.buf, torch.Tensor) else np.asarray(self.buf)
+        out, off = [], 0
+        for h, w in mip_level_shapes(self.width, self.height):
+            out.append(raw[off:off + h * w * 4].reshape(h, w, 4))
+            off += h * w * 4
+        return out
+
+
 def material(albedo=None, emissive=None, albedo_factor=(1.0, 1.0, 1.0, 1.0), emissive_factor=(1.0, 1.0, 1.0, 1.0),
-             flags=0, has_emissive: Optional[bool] = None, srgb=True, normal_map=None, normal_texture=None) -> Material:
+             flags=0, has_emissive: Optional[bool] = None, srgb=True, normal_map=None, normal_texture=None,
+             max_anisotropy: float = 16.0) -> Material:
     """soc_material: albedo / emissive RGBA8 textures ((H, W, 4) uint8 tensors or arrays; sRGB like the
     reference's baseColor/emissive images, model.cpp:52-71) or None (white / no emissive); normal_texture: the
-    glTF tangent-space normal image (RGBA8 UNORM, has_normal_image, g_buffer_generation.inl:197-211)."""
+    glTF tangent-space normal image (RGBA8 UNORM, has_normal_image, g_buffer_generation.inl:197-211).
+    MipTexture arguments make the material mip-mapped (SOC_MATERIAL_MIPMAPPED: trilinear, anisotropy up to
+    max_anisotropy as the reference's sampler, texture.cpp:121-136); then every texture given must be one."""
     m = Material()
     fmt = FMT_RGBA8_SRGB if srgb else None
-    m.albedo = img(albedo, fmt) if albedo is not None else img(None)
-    m.emissive = img(emissive, fmt) if emissive is not None else img(None)
+    given = [t for t in (albedo, emissive, normal_texture) if t is not None]
+    mipped = any(isinstance(t, MipTexture) for t in given)
+    if mipped and not all(isinstance(t, MipTexture) for t in given):
+        raise ValueError("a mip-mapped material needs every RGBA8 texture as a MipTexture")
+    tex_img = lambda t, f: t.img() if isinstance(t, MipTexture) else img(t, f)
+    m.albedo = tex_img(albedo, fmt) if albedo is not None else img(None)
+    m.emissive = tex_img(emissive, fmt) if emissive is not None else img(None)
+    if mipped:
+        m.flags |= MATERIAL_MIPMAPPED
+        m.max_anisotropy = float(max_anisotropy)
     m.albedo_factor[:] = [float(v) for v in albedo_factor]
     m.emissive_factor[:] = [float(v) for v in emissive_factor]
-    m.flags = int(flags)
+    m.flags |= int(flags)
     m.has_emissive = int(emissive is not None if has_emissive is None else has_emissive)
     m.normal_map = img(normal_map) if normal_map is not None else img(None)
     if normal_map is not None:
         m.flags |= MATERIAL_NORMAL_MAP
-    m.normal_image = img(normal_texture, FMT_RGBA8_UNORM) if normal_texture is not None else img(None)
+    m.normal_image = tex_img(normal_texture, FMT_RGBA8_UNORM) if normal_texture is not None else img(None)
     if normal_texture is not None:
         m.flags |= MATERIAL_NORMAL_TEXTURE
     return m
@@ -143,25 +201,41 @@ def visibility_triangles(vis) -> np.ndarray:
     return np.where(low == 0xFFFFFFFF, -1, 0xFFFFFFFE - low)
 
 
-def sponza_mesh_materials(tex_size: Optional[int] = None, device=None):
+def sponza_mesh_materials(tex_size: Optional[int] = None, device=None, mips: bool = False, host_mip_generator=None):
     """The 25 Sponza materials of the mesh proxy: baseColor (sRGB) and normal (UNORM) textures from the fixture;
     no emissive image (Sponza has none); albedo factor 1 (GBufferGeneration ignores baseColorFactor,
-    g_buffer_generation.inl:189-194). Returns (materials, textures kept alive)."""
+    g_buffer_generation.inl:189-194). mips=True gives every texture its mip chain (the reference's upload,
+    texture.cpp:184-246) and the anisotropic sampler: built on `device` by soc_generate_mips, or for host
+    materials (device None) by `host_mip_generator(MipTexture)`. Returns (materials, textures kept alive)."""
     from .scene import sponza_mesh
     tex = sponza_mesh.load_textures(tex_size)
     keep, mats = [], []
+
+    def prep(a, srgb):
+        if a is None:
+            return None
+        if mips:
+            if device is not None:
+                return MipTexture.build(a, srgb, device)
+            H, W = a.shape[:2]
+            buf = np.zeros(MipTexture.chain_bytes(W, H), np.uint8)
+            buf[:H * W * 4] = np.ascontiguousarray(a).reshape(-1)
+            t = MipTexture(buf, W, H, srgb)
+            if host_mip_generator is None:
+                raise ValueError("host mip-mapped materials need a host_mip_generator")
+            host_mip_generator(t)
+            return t
+        return torch.from_numpy(a).to(device) if device is not None else a
+
     for i in range(len(sponza_mesh.GLTF_TRIANGLES)):
         t = tex.get(i, {})
-        a, n = t.get("albedo"), t.get("normal")
-        if device is not None:
-            a = torch.from_numpy(a).to(device) if a is not None else None
-            n = torch.from_numpy(n).to(device) if n is not None else None
+        a, n = prep(t.get("albedo"), True), prep(t.get("normal"), False)
         keep += [a, n]
         mats.append(material(albedo=a, normal_texture=n))
     return mats, keep
 
 
-def scene_setup(g, scene_id: int, tex_size: int = 512, device="cuda") -> dict:
+def scene_setup(g, scene_id: int, tex_size: int = 512, device="cuda", mips: bool = True) -> dict:
     """Device mesh, textures and material array of a synthetic scene: the Sponza-proxy mesh (sponza_mesh.py, the
     reference's Sponza textures), the box atrium (scene_synth.c: sRGB tiled textures, emissive lamps) or the terrain
     (UNORM albedo, velocity 0 as draw_terrain.inl:221)."""
@@ -171,7 +245,7 @@ def scene_setup(g, scene_id: int, tex_size: int = 512, device="cuda") -> dict:
         m = sponza_mesh.build()
         mesh = MeshBuffers.from_numpy(m["positions"], m["normals"], m["uvs"], m["indices"], m["materials"],
                                       device=device)
-        mats, keep = sponza_mesh_materials(tex_size, device)
+        mats, keep = sponza_mesh_materials(tex_size, device, mips=mips)
         return {"mesh": mesh, "textures": keep, "normal_map": None, "materials": materials_device(mats, device),
                 "material_count": len(mats), "host_mesh": m, "workspace": mesh.workspace(device)}
     m = _scene.mesh(g, scene_id)

@@ -3,9 +3,9 @@
 # Usage: tools/sq_pass.sh <tag> "<up to 8 SQ counters>"
 set -o pipefail
 export TMPDIR=/tmp
-T=$1
+T=$1; C=$2; shift 2
 rm -rf gpurun_out/$T
-timeout -s KILL 120 rocprofv3 --pmc $2 --kernel-trace --output-format csv -d gpurun_out/$T/p1 -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --profile-frames 1 --no-sky-lane > gpurun_out/$T.log 2>&1 || { echo "pmc failed"; tail -5 gpurun_out/$T.log; exit 1; }
+timeout -s KILL 120 rocprofv3 --pmc $C --kernel-trace --output-format csv -d gpurun_out/$T/p1 -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --profile-frames 1 --no-sky-lane "$@" > gpurun_out/$T.log 2>&1 || { echo "pmc failed"; tail -5 gpurun_out/$T.log; exit 1; }
 python tools/pmc_summary.py gpurun_out/$T > gpurun_out/$T.json
 python - "$T" <<'PY'
 import json, sys
