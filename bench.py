@@ -168,7 +168,7 @@ def main():
     ap.add_argument("--no-sky-lane", action="store_true", help="run CloudRendering on the frame stream too")
     ap.add_argument("--unfused-histogram", action="store_true",
                     help="Composition and the luminance histogram as two launches (SOC_RENDERER_UNFUSED_HISTOGRAM)")
-    ap.add_argument("--write-frame", default="", help="write the last frame's tone-mapped framebuffer (PNG)")
+    ap.add_argument("--write-frame", default="", help="write the last frame: tone-mapped framebuffer (.png) or HDR composition colour (.exr, f16)")
     ap.add_argument("--metrics-jsonl", default="", help="one GPU-metric JSON line per profiled frame")
     ap.add_argument("--raster", action="store_true",
                     help="end-to-end frame: rasterise the scene mesh into the G-buffer and the 4096^2 sun shadow "
@@ -277,8 +277,11 @@ def main():
     if args.metrics_jsonl and rank == 0:
         with open(args.metrics_jsonl, "w") as f:
             f.write("\n".join(metrics_lines) + "\n")
-    if args.write_frame and rank == 0:   # headless present: the RGBA8 framebuffer to a host image
-        soc.write_png(args.write_frame, soc.read_image(fr["output"]))
+    if args.write_frame and rank == 0:   # headless present: the RGBA8 framebuffer (PNG) or the HDR colour (EXR f16)
+        if args.write_frame.endswith(".exr"):
+            soc.write_exr(args.write_frame, soc.read_image(fr["color"]))
+        else:
+            soc.write_png(args.write_frame, soc.read_image(fr["output"]))
     r.set_async(not args.no_sky_lane)
     stats = [st for st in stats if st[3]]     # passes with no work this frame (the folded fold pass) have no record
     ms_pass = {n: round(ms, 4) for n, _, ms, _ in stats}

@@ -610,6 +610,9 @@ int64_t soc_renderer_metrics_json(soc_renderer* r, uint64_t frame, char* buf, si
 int soc_read_image(soc_img image, void* host, int32_t host_pitch_bytes, soc_stream stream);
 /* 8-bit RGBA host image -> PNG file (uncompressed deflate; no external library). */
 int soc_write_png(const char* path, const void* rgba8, int32_t width, int32_t height, int32_t pitch_bytes);
+/* RGBA16F host image (e.g. the HDR composition / TAA colour) -> OpenEXR 2 scanline file, uncompressed HALF
+ * channels (the f16 framebuffer dump; the reference reads EXR through tinyexr, texture.cpp:300-412). */
+int soc_write_exr(const char* path, const void* rgba16f, int32_t width, int32_t height, int32_t pitch_bytes);
 
 #ifdef __cplusplus
 }

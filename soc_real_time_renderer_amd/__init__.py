@@ -29,7 +29,7 @@ __all__ = ["SocError", "lib", "img", "Globals", "Camera", "AutoExposure", "globa
            "bloom_downsample", "bloom_upsample", "bloom_chain", "ssao_prepare_noise", "ssao_generation",
            "ssao_blur", "cloud_rendering", "composition", "generate_luminance_histogram",
            "resolve_luminance_histogram", "temporal_antialiasing", "copy_image", "tone_mapping", "upload_globals",
-           "Renderer", "read_image", "write_png", "FMT_RGBA16F", "FMT_D32F", "FMT_R8_UNORM", "FMT_RGBA8_UNORM", "FMT_RGBA8_SRGB",
+           "Renderer", "read_image", "write_png", "write_exr", "FMT_RGBA16F", "FMT_D32F", "FMT_R8_UNORM", "FMT_RGBA8_UNORM", "FMT_RGBA8_SRGB",
            "FMT_RGBA32F", "PHASE_PRE_EXPOSURE", "PHASE_POST_EXPOSURE", "PHASE_ALL"]
 
 
@@ -220,6 +220,15 @@ def write_png(path: str, rgba8: np.ndarray) -> None:
     a = np.ascontiguousarray(rgba8, np.uint8)
     _check(lib().soc_write_png(path.encode(), a.ctypes.data, int(a.shape[1]), int(a.shape[0]), int(a.strides[0])),
            "soc_write_png")
+
+
+def write_exr(path: str, rgba16f: np.ndarray) -> None:
+    """(H, W, 4) float16 host image -> OpenEXR, uncompressed HALF (soc_write_exr)."""
+    a = np.ascontiguousarray(rgba16f, np.float16)
+    if a.ndim != 3 or a.shape[2] != 4:
+        raise ValueError("write_exr needs an (H, W, 4) float16 image")
+    _check(lib().soc_write_exr(path.encode(), a.ctypes.data, int(a.shape[1]), int(a.shape[0]), int(a.strides[0])),
+           "soc_write_exr")
 
 
 def ssao_prepare_noise(normal, target, table, stream=None):

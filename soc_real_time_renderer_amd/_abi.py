@@ -243,6 +243,7 @@ FUNCTIONS = {
     "soc_renderer_metrics_json": (C.c_int64, [_P, C.c_uint64, C.c_char_p, C.c_size_t]),
     "soc_read_image": (_I, [_IMG, _P, C.c_int32, _P]),
     "soc_write_png": (_I, [C.c_char_p, _P, C.c_int32, C.c_int32, C.c_int32]),
+    "soc_write_exr": (_I, [C.c_char_p, _P, C.c_int32, C.c_int32, C.c_int32]),
     "soc_raster_visibility": (_I, [C.POINTER(Mesh), C.POINTER(C.c_float), C.c_int32, _P, C.c_int32, C.c_int32,
                                    C.c_int32, _P, _P]),
     "soc_raster_depth": (_I, [C.POINTER(Mesh), C.POINTER(C.c_float), C.c_int32, C.c_float, C.c_float, _IMG, _P, _P]),

@@ -92,6 +92,86 @@ extern "C" int soc_write_png(const char* path, const void* rgba8, int32_t width,
     return SOC_OK;
 }
 
+// OpenEXR 2 single-part scanline file, NO_COMPRESSION, HALF channels A, B, G, R (the channel list is sorted by
+// name; each scanline block is one row: y, byte count, then every channel's row of halves).
+namespace {
+void put_le32(std::vector<uint8_t>& v, uint32_t x) {
+    for (int i = 0; i < 4; ++i) v.push_back((uint8_t)(x >> (8 * i)));
+}
+void put_le64(std::vector<uint8_t>& v, uint64_t x) {
+    for (int i = 0; i < 8; ++i) v.push_back((uint8_t)(x >> (8 * i)));
+}
+void attr(std::vector<uint8_t>& h, const char* name, const char* type, const std::vector<uint8_t>& value) {
+    h.insert(h.end(), name, name + std::strlen(name) + 1);
+    h.insert(h.end(), type, type + std::strlen(type) + 1);
+    put_le32(h, (uint32_t)value.size());
+    h.insert(h.end(), value.begin(), value.end());
+}
+}  // namespace
+
+extern "C" int soc_write_exr(const char* path, const void* rgba16f, int32_t width, int32_t height, int32_t pitch_bytes) {
+    if (!path || !rgba16f || width <= 0 || height <= 0 || pitch_bytes < width * 8)
+        return set_error(SOC_E_INVALID_ARG, "soc_write_exr: bad arguments");
+    std::vector<uint8_t> out;
+    put_le32(out, 20000630u);   // magic 0x762f3101
+    put_le32(out, 2u);          // version 2, single-part scanline
+    std::vector<uint8_t> v;
+    for (const char* ch : {"A", "B", "G", "R"}) {
+        v.push_back((uint8_t)ch[0]);
+        v.push_back(0);
+        put_le32(v, 1u);                  // HALF
+        v.push_back(0); v.push_back(0); v.push_back(0); v.push_back(0);   // pLinear + reserved
+        put_le32(v, 1u);
+        put_le32(v, 1u);                  // x / y sampling
+    }
+    v.push_back(0);
+    attr(out, "channels", "chlist", v);
+    attr(out, "compression", "compression", {0});
+    v.clear();
+    put_le32(v, 0); put_le32(v, 0); put_le32(v, (uint32_t)(width - 1)); put_le32(v, (uint32_t)(height - 1));
+    attr(out, "dataWindow", "box2i", v);
+    attr(out, "displayWindow", "box2i", v);
+    attr(out, "lineOrder", "lineOrder", {0});   // INCREASING_Y
+    const float one = 1.0f, zero = 0.0f;
+    uint32_t bits;
+    v.clear();
+    std::memcpy(&bits, &one, 4);
+    put_le32(v, bits);
+    attr(out, "pixelAspectRatio", "float", v);
+    v.clear();
+    std::memcpy(&bits, &zero, 4);
+    put_le32(v, bits);
+    put_le32(v, bits);
+    attr(out, "screenWindowCenter", "v2f", v);
+    v.clear();
+    std::memcpy(&bits, &one, 4);
+    put_le32(v, bits);
+    attr(out, "screenWindowWidth", "float", v);
+    out.push_back(0);   // end of header
+    const size_t row_bytes = (size_t)width * 8, block = 8 + row_bytes;
+    const size_t table = out.size(), first = table + (size_t)height * 8;
+    for (int y = 0; y < height; ++y) put_le64(out, first + (size_t)y * block);
+    out.reserve(first + (size_t)height * block);
+    static const int order[4] = {3, 2, 1, 0};   // A, B, G, R from RGBA
+    for (int y = 0; y < height; ++y) {
+        put_le32(out, (uint32_t)y);
+        put_le32(out, (uint32_t)row_bytes);
+        const uint16_t* row = reinterpret_cast<const uint16_t*>(static_cast<const uint8_t*>(rgba16f) + (size_t)y * pitch_bytes);
+        for (int c : order)
+            for (int x = 0; x < width; ++x) {
+                const uint16_t h = row[4 * x + c];
+                out.push_back((uint8_t)h);
+                out.push_back((uint8_t)(h >> 8));
+            }
+    }
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return set_error(SOC_E_INVALID_ARG, "soc_write_exr: cannot open %s", path);
+    const size_t w = std::fwrite(out.data(), 1, out.size(), f);
+    std::fclose(f);
+    if (w != out.size()) return set_error(SOC_E_INVALID_ARG, "soc_write_exr: short write to %s", path);
+    return SOC_OK;
+}
+
 // Device image -> host rows (stream-ordered; the caller synchronises before reading `host`).
 extern "C" int soc_read_image(soc_img image, void* host, int32_t host_pitch_bytes, soc_stream stream) {
     int rc = check_img(image, 0, "soc_read_image", "image");
