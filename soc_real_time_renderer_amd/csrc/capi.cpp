@@ -1026,7 +1026,12 @@ static int ensure_side_lane(soc_renderer* r) {
         r->side = nullptr;
         r->fork_ev = r->join_ev = nullptr;
     }
-    if (hipStreamCreateWithFlags(&r->side, hipStreamNonBlocking) != hipSuccess ||
+    // tuning knob: priority of the second lane (-1 high, 1 low, 0 the default priority)
+    const int prio_knob = tuning_knob("SOC_SIDE_PRIORITY", 0);
+    int least = 0, greatest = 0;
+    (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
+    const int prio = prio_knob < 0 ? greatest : prio_knob > 0 ? least : 0;
+    if (hipStreamCreateWithPriority(&r->side, hipStreamNonBlocking, prio) != hipSuccess ||
         hipEventCreateWithFlags(&r->fork_ev, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&r->join_ev, hipEventDisableTiming) != hipSuccess)
         return set_error(SOC_E_HIP, "soc_renderer_execute: second lane stream/event creation failed");

@@ -468,6 +468,8 @@ struct PairBufs {
     float2* odvis;        // [kShards * cap] (od, vis)
     uint32_t* pix_mask;   // [W*H] per list entry: dense-step mask | kInline
     uint32_t* batch_base; // [W*H/256] per 256-entry batch: physical index of its first pair | kInline
+    float4* geom;         // [W*H] x 2 per list entry: (start, dither), (inc, stepLength) of its march (density
+                          // writes it for upward rays; sunvis and resolve read it instead of re-deriving it)
     uint32_t cap;         // pairs per shard
 };
 
@@ -533,6 +535,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void c
             if (SOC_CLOUDS_PROFILE != 1 && !(dir.y < 0.0f)) {
                 const MarchGeom mg = march_geometry(dir);
                 const float dither = bayer16((float)x, (float)y);
+                pb.geom[2 * i] = float4{mg.start.x, mg.start.y, mg.start.z, dither};
+                pb.geom[2 * i + 1] = float4{mg.inc.x, mg.inc.y, mg.inc.z, mg.stepLength};
                 for (int s = 0; s < 24; s++)
                     if (!(get_clouds(cx, step_position(mg, dither, s)) * mg.stepLength <= 0.0f)) mask |= 1u << s;
             }
@@ -605,10 +609,9 @@ __global__ __launch_bounds__(kSunvisThreads) __attribute__((amdgpu_waves_per_eu(
         const uint32_t pr = pb.pairs[phys];
         if (pr == 0xffffffffu) continue;   // slot of an overflowed batch
         const uint32_t i = pr >> 5, step = pr & 31u;
-        const uint32_t e = list[i];
-        const int x = (int)(e & 0xffffu), y = (int)(e >> 16);
-        const MarchGeom mg = march_geometry(sky_dir(p, x, y));
-        const f3 cp = step_position(mg, bayer16((float)x, (float)y), (int)step);
+        const float4 g0 = pb.geom[2 * i], g1 = pb.geom[2 * i + 1];   // the pixel's march, from clouds_density
+        const MarchGeom mg{f3{g0.x, g0.y, g0.z}, f3{g1.x, g1.y, g1.z}, g1.w};
+        const f3 cp = step_position(mg, g0.w, (int)step);
         const float od = get_clouds(cx, cp) * mg.stepLength;
         const float vis = SOC_CLOUDS_PROFILE == 3 ? 1.0f : sun_visibility(cx, cp, sun);
         pb.odvis[phys] = float2{od, vis};
@@ -664,7 +667,8 @@ __global__ __launch_bounds__(256) void clouds_resolve(DImg noise, DImg target, C
             MarchGeom mg{};
             MarchShade ms{};
             if (march) {
-                mg = march_geometry(dir);
+                const float4 g0 = pb.geom[2 * i], g1 = pb.geom[2 * i + 1];
+                mg = MarchGeom{f3{g0.x, g0.y, g0.z}, f3{g1.x, g1.y, g1.z}, g1.w};
                 ms = march_shade(dir, sun);
             }
             f3 scattering = f3{0.0f, 0.0f, 0.0f};
@@ -705,7 +709,7 @@ using namespace soc;
 
 namespace {
 // Workspace: counters (256 B: [0] sky pixels, [8..15] pair counts per shard) | sky list (u32) |
-// atmosphere (float4) | per-pixel dense mask (u32) | per-batch first pair (u32) | pairs (u32) |
+// atmosphere (float4) | per-pixel dense mask (u32) | per-batch first pair (u32) | march geometry (2 float4) | pairs (u32) |
 // (od, vis) per pair (float2). Pair capacity 2 per pixel of the image (8 shards).
 // Per 256-entry batch of the list: the physical index of its first pair (or kInline).
 struct CloudWs {
@@ -730,6 +734,8 @@ CloudWs cloud_ws_layout(void* base, size_t n) {
     off = al(off + n * 4);
     w.pb.batch_base = reinterpret_cast<uint32_t*>(b + off);
     off = al(off + (n / 256 + 1) * 4);
+    w.pb.geom = reinterpret_cast<float4*>(b + off);
+    off = al(off + n * 32);
     w.pb.cap = (uint32_t)((2 * n + kShards - 1) / kShards);
     w.pb.pairs = reinterpret_cast<uint32_t*>(b + off);
     off = al(off + (size_t)kShards * w.pb.cap * 4);
@@ -794,11 +800,15 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
     static int res_atmos = 0, res_density = 0, res_sunvis = 0, res_resolve = 0;
     static bool sunvis512 = true;
     if (!res_atmos) {
-        res_atmos = resident_blocks(clouds_atmosphere);
-        res_density = resident_blocks(clouds_density<false>);
+        // tuning knob: percent of the resident set each persistent kernel takes (the rest of the CU slots stay
+        // free for the frame lane's kernels running beside the sky lane)
+        const int pct = std::max(1, tuning_knob("SOC_SKY_SHARE_PCT", 100));
+        auto share = [&](int res) { return std::max(1, res * pct / 100); };
+        res_atmos = share(resident_blocks(clouds_atmosphere));
+        res_density = share(resident_blocks(clouds_density<false>));
         sunvis512 = tuning_knob("SOC_SUNVIS_THREADS", 512) == 512;
-        res_sunvis = sunvis512 ? resident_blocks(clouds_sunvis<false, 512>, 512) : resident_blocks(clouds_sunvis<false, 256>, 256);
-        res_resolve = resident_blocks(clouds_resolve<false>);
+        res_sunvis = share(sunvis512 ? resident_blocks(clouds_sunvis<false, 512>, 512) : resident_blocks(clouds_sunvis<false, 256>, 256));
+        res_resolve = share(resident_blocks(clouds_resolve<false>));
     }
     const long long blocks = ((long long)W * H + 255) / 256;
     if (SOC_CLOUDS_PROFILE >= 4) return check_launch("cloud_rendering");
