@@ -170,6 +170,8 @@ def main():
                     help="Composition and the luminance histogram as two launches (SOC_RENDERER_UNFUSED_HISTOGRAM)")
     ap.add_argument("--write-frame", default="", help="write the last frame: tone-mapped framebuffer (.png) or HDR composition colour (.exr, f16)")
     ap.add_argument("--metrics-jsonl", default="", help="one GPU-metric JSON line per profiled frame")
+    ap.add_argument("--no-mips", action="store_true",
+                    help="mesh scene: level-0 bilinear textures instead of the reference's mip chains + 16x anisotropic sampler")
     ap.add_argument("--raster", action="store_true",
                     help="end-to-end frame: rasterise the scene mesh into the G-buffer and the 4096^2 sun shadow "
                          "map every frame (DepthPrepass / SunShadowDraw / GBufferGeneration in the graph)")
@@ -196,7 +198,7 @@ def main():
     sc = None
     if scene_id == scene.SPONZA_MESH:
         # rasterised once by the HIP rasteriser (DepthPrepass + GBufferGeneration + SunShadowDraw), not timed
-        sc = raster.scene_setup(g, scene_id, tex_size=256, device=device)
+        sc = raster.scene_setup(g, scene_id, tex_size=256, device=device, mips=not args.no_mips)
         gbd = raster.render_gbuffer(g, sc, W, H, 4096, device)
         torch.cuda.synchronize()
         gb = {k: gbd[k].cpu().numpy() for k in ("albedo", "emissive", "normal", "velocity", "depth")}

@@ -355,25 +355,34 @@ __device__ __forceinline__ Axis axis_repeat_any(float u, int n) {
     return a;
 }
 
+// REPEAT axis of extent n: the power-of-two mask when n is one (every texture of the reference's assets),
+// else the general modulo; same taps and weight either way.
+__device__ __forceinline__ Axis axis_repeat_level(float u, int n) {
+    return (n & (n - 1)) ? axis_repeat_any(u, n) : axis_repeat_pow2(u, n, n - 1);
+}
+
 __device__ __forceinline__ f4 sample_texture(const soc_img& tex, float u, float v, const float* lut) {
     if (!tex.data) return f4{1.0f, 1.0f, 1.0f, 1.0f};
     const DImg im{static_cast<char*>(tex.data), tex.width, tex.height, tex.pitch_bytes};
     const bool srgb = tex.format == SOC_FMT_RGBA8_SRGB;
-    const Axis ax = axis_repeat_any(u, tex.width), ay = axis_repeat_any(v, tex.height);
+    const Axis ax = axis_repeat_level(u, tex.width), ay = axis_repeat_level(v, tex.height);
     const f4 a = texel_rgba8(im, ax.i0, ay.i0, srgb, lut), b = texel_rgba8(im, ax.i1, ay.i0, srgb, lut);
     const f4 c = texel_rgba8(im, ax.i0, ay.i1, srgb, lut), d = texel_rgba8(im, ax.i1, ay.i1, srgb, lut);
     return bilerp4(a, b, c, d, ax.w, ay.w);
 }
 
-// Bilinear REPEAT sample of level k of a packed mip chain (soc_generate_mips layout).
-__device__ __forceinline__ f4 sample_level(const soc_img& tex, int k, float u, float v, bool srgb, const float* lut) {
-    int wk, hk;
-    const size_t off = mip_offset(tex.width, tex.height, tex.pitch_bytes, k, wk, hk);
-    const DImg im{static_cast<char*>(tex.data) + off, wk, hk, k ? 4 * wk : tex.pitch_bytes};
-    const Axis ax = axis_repeat_any(u, wk), ay = axis_repeat_any(v, hk);
+
+// Bilinear REPEAT sample of one level (its image view already resolved) of a packed mip chain.
+__device__ __forceinline__ f4 sample_level(const DImg& im, float u, float v, bool srgb, const float* lut) {
+    const Axis ax = axis_repeat_level(u, im.w), ay = axis_repeat_level(v, im.h);
     const f4 a = texel_rgba8(im, ax.i0, ay.i0, srgb, lut), b = texel_rgba8(im, ax.i1, ay.i0, srgb, lut);
     const f4 c = texel_rgba8(im, ax.i0, ay.i1, srgb, lut), d = texel_rgba8(im, ax.i1, ay.i1, srgb, lut);
     return bilerp4(a, b, c, d, ax.w, ay.w);
+}
+__device__ __forceinline__ DImg level_view(const soc_img& tex, int k) {
+    int wk, hk;
+    const size_t off = mip_offset(tex.width, tex.height, tex.pitch_bytes, k, wk, hk);
+    return DImg{static_cast<char*>(tex.data) + off, wk, hk, k ? 4 * wk : tex.pitch_bytes};
 }
 
 // Fine uv derivatives of the pixel's quad.
@@ -402,6 +411,7 @@ __device__ f4 sample_texture_mip(const soc_img& tex, float u, float v, const UVG
     }
     const int l0 = lq >> 8;
     const float f = (float)(lq & 255) * (1.0f / 256.0f);
+    const DImg im0 = level_view(tex, l0), im1 = level_view(tex, min(l0 + 1, L - 1));
     const bool xmajor = px >= py;
     const float du = xmajor ? gr.dudx : gr.dudy, dv = xmajor ? gr.dvdx : gr.dvdy;
     f4 acc = f4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -412,9 +422,9 @@ __device__ f4 sample_texture_mip(const soc_img& tex, float u, float v, const UVG
             su = u + t * du;
             sv = v + t * dv;
         }
-        f4 s0 = sample_level(tex, l0, su, sv, srgb, lut);
+        f4 s0 = sample_level(im0, su, sv, srgb, lut);
         if (lq & 255) {
-            const f4 s1 = sample_level(tex, l0 + 1, su, sv, srgb, lut);
+            const f4 s1 = sample_level(im1, su, sv, srgb, lut);
             s0 = f4{lerp_w(s0.x, s1.x, f), lerp_w(s0.y, s1.y, f), lerp_w(s0.z, s1.z, f), lerp_w(s0.w, s1.w, f)};
         }
         acc = f4{acc.x + s0.x, acc.y + s0.y, acc.z + s0.z, acc.w + s0.w};
