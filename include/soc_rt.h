@@ -561,6 +561,18 @@ int soc_gbuffer_resolve(const soc_globals* g, const soc_mesh* mesh, const soc_ma
                         int32_t material_count, const uint64_t* visibility, soc_img depth, soc_img albedo,
                         soc_img emissive, soc_img normal, soc_img velocity, void* workspace, soc_stream stream);
 
+/* DrawTerrain / SunShadowDrawTerrain patch tessellation (renderer.cpp:194-220 builds a grid_size^2 uv control
+ * grid, 100 in the reference, of 4-point quad patches; draw_terrain.inl:144-191 tessellates each at
+ * terrain_max_tess_level (3) with fractional_odd_spacing and displaces it by (heightmap(uv).r -
+ * terrain_midpoint) * terrain_height_scale). Odd integer levels only (n equal segments). Output: the
+ * ((grid - 1) n + 1)^2 shared vertices in world space (x = u scale.x - offset.x, y = offset.y + height,
+ * z = v scale.y - offset.z; the TES's clip-space point before the linear clip transform), up normals (the
+ * G-buffer normal comes from the terrain normal map), uvs, and 2 triangles per tessellated quad,
+ * counter-clockwise seen from above. Heightmap: RGBA8_UNORM, bilinear clamp-to-edge (.r). */
+int soc_terrain_tess_counts(int32_t grid_size, int32_t tess_level, int32_t* vertices, int32_t* triangles);
+int soc_terrain_tessellate(const soc_globals* g, soc_img heightmap, int32_t grid_size, int32_t tess_level,
+                           float* positions, float* normals, float* uvs, uint32_t* indices, soc_stream stream);
+
 /* Texture mip chains (texture.cpp:108, 184-246): floor(log2(max(W, H))) + 1 levels, level k of max(1, W >> k) x
  * max(1, H >> k) texels. Packed chain layout: level 0 is the soc_img itself (any pitch); level k >= 1 follows at
  * data + pitch_bytes * H + sum_{1 <= j < k} 4 w_j h_j with tight rows. soc_mip_chain_bytes is the size of the

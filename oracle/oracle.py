@@ -40,6 +40,7 @@ _FUNCS = {
                                              _IMG, _IMG, _IMG, _IMG, _IMG]),
     "soc_oracle_height_to_normal": (C.c_int, [_IMG, _IMG]),
     "soc_oracle_generate_mips": (C.c_int, [_IMG]),
+    "soc_oracle_terrain_tessellate": (C.c_int, [_G, _IMG, C.c_int32, C.c_int32] + [C.c_void_p] * 4),
     "soc_oracle_generate_hiz": (C.c_int, [_G, _IMG, C.POINTER(_IMG), C.c_int32, C.c_int32]),
     "soc_oracle_luminance_bin": (C.c_uint32, [C.c_float] * 5),
     "soc_oracle_log2": (C.c_float, [C.c_float]),
@@ -161,6 +162,16 @@ def gbuffer_resolve(g, mesh, materials, vis, depth, albedo, emissive, normal, ve
 def generate_mips(tex):
     """Levels 1.. of a host MipTexture (raster.MipTexture over a numpy buffer), in place."""
     _rc(lib().soc_oracle_generate_mips(tex.img()), "generate_mips")
+
+
+def terrain_tessellate(g, heightmap, grid_size, tess_level, V, T):
+    """Host restatement of soc_terrain_tessellate: dict of positions / normals (V,3), uvs (V,2), indices (T,3)."""
+    out = {"positions": np.zeros((V, 3), np.float32), "normals": np.zeros((V, 3), np.float32),
+           "uvs": np.zeros((V, 2), np.float32), "indices": np.zeros((T, 3), np.uint32)}
+    _rc(lib().soc_oracle_terrain_tessellate(C.byref(g), _img(heightmap), int(grid_size), int(tess_level),
+                                            *(out[k].ctypes.data for k in ("positions", "normals", "uvs", "indices"))),
+        "terrain_tessellate")
+    return out
 
 
 def height_to_normal(heightmap, target):

@@ -1183,6 +1183,47 @@ static v4 rs_sample_texture(const soc_img* tex, float u, float v) {
     return sample_repeat(tex, u, v);
 }
 
+/* DrawTerrain patch tessellation (renderer.cpp:194-220, draw_terrain.inl:138-191; soc_rt.h
+   soc_terrain_tessellate): the TES's uv bilinear in its operation order, the heightmap's .r bilinear clamp,
+   the world point of the displaced vertex; shared vertices evaluated by the lowest patch holding them. */
+int soc_oracle_terrain_tessellate(const soc_globals* g, soc_img heightmap, int32_t grid_size, int32_t tess_level,
+                                  float* positions, float* normals, float* uvs, uint32_t* indices) {
+    if (!g || !valid(&heightmap) || heightmap.format != SOC_FMT_RGBA8_UNORM || grid_size < 2 || tess_level < 1 ||
+        !(tess_level & 1) || !positions || !normals || !uvs || !indices)
+        return SOC_E_INVALID_ARG;
+    const int n = tess_level, nv = (grid_size - 1) * n + 1;
+    const float fn = (float)n, side = (float)(grid_size - 1);
+    for (int gz = 0; gz < nv; ++gz)
+        for (int gx = 0; gx < nv; ++gx) {
+            const int k = gz * nv + gx;
+            int pi = gx / n, pj = gz / n;
+            if (pi > grid_size - 2) pi = grid_size - 2;
+            if (pj > grid_size - 2) pj = grid_size - 2;
+            const float tu = (float)(gz - pj * n) / fn, tv = (float)(gx - pi * n) / fn;
+            const float i0 = (float)pi / side, i1 = (float)(pi + 1) / side, j0 = (float)pj / side, j1 = (float)(pj + 1) / side;
+            const float u0x = (i0 - i0) * tu + i0, u0y = (j1 - j0) * tu + j0;
+            const float u1x = (i1 - i1) * tu + i1, u1y = (j1 - j0) * tu + j0;
+            const float ux = (u1x - u0x) * tv + u0x, uy = (u1y - u0y) * tv + u0y;
+            const float h = sample_clamp(&heightmap, ux, uy).x;
+            const float adj = (h - g->terrain_midpoint) * g->terrain_height_scale;
+            positions[3 * k] = ux * g->terrain_scale[0] - g->terrain_offset[0];
+            positions[3 * k + 1] = g->terrain_offset[1] + adj;
+            positions[3 * k + 2] = uy * g->terrain_scale[1] - g->terrain_offset[2];
+            normals[3 * k] = 0.0f; normals[3 * k + 1] = 1.0f; normals[3 * k + 2] = 0.0f;
+            uvs[2 * k] = ux;
+            uvs[2 * k + 1] = uy;
+        }
+    const int segs = nv - 1;
+    for (int id = 0; id < 2 * segs * segs; ++id) {
+        const int q = id >> 1, qi = q % segs, qj = q / segs;
+        const uint32_t v00 = (uint32_t)(qj * nv + qi), v10 = v00 + 1, v01 = v00 + (uint32_t)nv, v11 = v01 + 1;
+        indices[3 * id] = v00;
+        indices[3 * id + 1] = (id & 1) ? v01 : v11;
+        indices[3 * id + 2] = (id & 1) ? v11 : v10;
+    }
+    return SOC_OK;
+}
+
 /* ---- texture mip chains (texture.cpp:108, 184-246; soc_rt.h soc_generate_mips) ---- */
 static int mip_levels(int w, int h) {
     int m = w > h ? w : h, n = 0;

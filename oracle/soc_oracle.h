@@ -49,6 +49,9 @@ int soc_oracle_gbuffer_resolve(const soc_globals* g, const soc_mesh* mesh, const
 /* soc_generate_mips (texture.cpp:184-246): levels 1.. of a packed RGBA8 chain from level 0, in place. */
 int soc_oracle_generate_mips(soc_img texture);
 int soc_oracle_height_to_normal(soc_img heightmap, soc_img target);
+/* soc_terrain_tessellate (draw_terrain.inl:138-191): the tessellated terrain vertices / indices. */
+int soc_oracle_terrain_tessellate(const soc_globals* g, soc_img heightmap, int32_t grid_size, int32_t tess_level,
+                                  float* positions, float* normals, float* uvs, uint32_t* indices);
 int soc_oracle_generate_hiz(const soc_globals* g, soc_img depth, const soc_img* mips, int32_t mip_count, int32_t op_max);
 
 /* Scalar helpers exposed for known-answer tests. */

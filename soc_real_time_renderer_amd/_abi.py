@@ -236,6 +236,8 @@ FUNCTIONS = {
     "soc_raster_workspace_size": (C.c_size_t, [C.c_int32, C.c_int32]),
     "soc_renderer_set_raster_scene": (_I, [_P, C.POINTER(RasterScene)]),
     "soc_height_to_normal": (_I, [_IMG, _IMG, _P]),
+    "soc_terrain_tess_counts": (_I, [_I, _I, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "soc_terrain_tessellate": (_I, [_G, _IMG, _I, _I, _P, _P, _P, _P, _P]),
     "soc_mip_level_count": (_I, [_I, _I]),
     "soc_mip_chain_bytes": (C.c_size_t, [_I, _I, _I]),
     "soc_generate_mips": (_I, [_IMG, _P]),

@@ -238,7 +238,7 @@ def sponza_mesh_materials(tex_size: Optional[int] = None, device=None, mips: boo
 def scene_setup(g, scene_id: int, tex_size: int = 512, device="cuda", mips: bool = True) -> dict:
     """Device mesh, textures and material array of a synthetic scene: the Sponza-proxy mesh (sponza_mesh.py, the
     reference's Sponza textures), the box atrium (scene_synth.c: sRGB tiled textures, emissive lamps) or the terrain
-    (UNORM albedo, velocity 0 as draw_terrain.inl:221)."""
+    (the GPU-tessellated patch grid over a tex_size^2 heightmap, UNORM albedo, velocity 0 as draw_terrain.inl:221)."""
     from . import scene as _scene
     if scene_id == _scene.SPONZA_MESH:
         from .scene import sponza_mesh
@@ -248,16 +248,25 @@ def scene_setup(g, scene_id: int, tex_size: int = 512, device="cuda", mips: bool
         mats, keep = sponza_mesh_materials(tex_size, device, mips=mips)
         return {"mesh": mesh, "textures": keep, "normal_map": None, "materials": materials_device(mats, device),
                 "material_count": len(mats), "host_mesh": m, "workspace": mesh.workspace(device)}
-    m = _scene.mesh(g, scene_id)
-    mesh = MeshBuffers.from_numpy(m["positions"], m["normals"], m["uvs"], m["indices"], m["materials"], device=device)
     tex, em = _scene.material_textures(g, tex_size, scene_id)
     terrain = scene_id == _scene.TERRAIN
     dtex = [torch.from_numpy(tex[i]).to(device) for i in range(len(tex))]
     nmap = None
-    if terrain:   # the terrain's normal map from its heightmap (HeightToNormalTask, renderer.cpp:158-190)
+    if terrain:
+        # the terrain's normal map from its heightmap (HeightToNormalTask, renderer.cpp:158-190), and its mesh:
+        # the patch grid tessellated on the GPU with heights from the same heightmap (draw_terrain.inl:138-191)
         hm = torch.from_numpy(_scene.terrain_heightmap(tex_size)).to(device)
         nmap = torch.empty((tex_size, tex_size, 4), dtype=torch.float16, device=device)
         height_to_normal(hm, nmap)
+        mesh = terrain_tessellate(g, hm, device=device)
+        torch.cuda.synchronize()
+        m = {"positions": mesh.positions.cpu().numpy(), "normals": mesh.normals.cpu().numpy(),
+             "uvs": mesh.uvs.cpu().numpy(), "indices": mesh.indices.cpu().numpy().view(np.uint32),
+             "materials": mesh.materials.cpu().numpy().view(np.uint32)}
+    else:
+        m = _scene.mesh(g, scene_id)
+        mesh = MeshBuffers.from_numpy(m["positions"], m["normals"], m["uvs"], m["indices"], m["materials"],
+                                      device=device)
     mats = [material(albedo=dtex[i], emissive_factor=tuple(float(v) for v in em[i]) + (1.0,),
                      has_emissive=bool(em[i].any()), flags=MATERIAL_ZERO_VELOCITY if terrain else 0, srgb=not terrain,
                      normal_map=nmap)
@@ -282,6 +291,30 @@ def render_gbuffer(g, sc: dict, width: int, height: int, shadow_size: int = 4096
     raster_depth(sc["mesh"], np.ctypeslib.as_array(g.sun_info.projection_view_matrix), CULL_BACK, out["shadow"],
                  sc["workspace"], SHADOW_BIAS_CONSTANT, SHADOW_BIAS_SLOPE)
     return out
+
+
+TERRAIN_GRID = 100   # renderer.cpp:197
+
+
+def terrain_tess_counts(grid_size: int = TERRAIN_GRID, tess_level: int = 3):
+    v, t = C.c_int32(), C.c_int32()
+    _check(lib().soc_terrain_tess_counts(int(grid_size), int(tess_level), C.byref(v), C.byref(t)), "terrain_tess_counts")
+    return v.value, t.value
+
+
+def terrain_tessellate(g, heightmap, grid_size: int = TERRAIN_GRID, tess_level: Optional[int] = None, device="cuda",
+                       stream=None) -> MeshBuffers:
+    """DrawTerrain's patch grid tessellated on the GPU (soc_terrain_tessellate): the terrain as a MeshBuffers
+    whose heights come from `heightmap` ((H, W, 4) uint8 device tensor); level = globals' terrain_max_tess_level."""
+    n = int(g.terrain_max_tess_level if tess_level is None else tess_level)
+    V, T = terrain_tess_counts(grid_size, n)
+    f32 = dict(dtype=torch.float32, device=device)
+    pos, nrm, uv = torch.empty((V, 3), **f32), torch.empty((V, 3), **f32), torch.empty((V, 2), **f32)
+    idx = torch.empty((T, 3), dtype=torch.int32, device=device)
+    _check(lib().soc_terrain_tessellate(_gp(g), img(heightmap), int(grid_size), n, _ptr(pos), _ptr(nrm), _ptr(uv),
+                                        _ptr(idx), _stream(stream)), "terrain_tessellate")
+    mats = torch.zeros(T, dtype=torch.int32, device=device)
+    return MeshBuffers(pos, nrm, uv, idx, mats)
 
 
 def height_to_normal(heightmap, normal_target, stream=None):

@@ -376,3 +376,20 @@ def test_sponza_mesh_mipmapped_gbuffer_vs_oracle(soc, oracle):
         assert ok.mean() >= 0.9999, (k, ok.mean())
     moved = ~f16_close(ref["albedo"], ref_l0["albedo"])
     assert moved.any(axis=-1).mean() > 0.05
+
+
+@pytest.mark.parametrize("size,grid,level", [(1024, 100, 3), (128, 100, 3), (64, 17, 5), (32, 2, 1)])
+def test_terrain_tessellate_bit_exact(soc, oracle, size, grid, level):
+    """soc_terrain_tessellate (draw_terrain.inl:138-191 on the renderer.cpp:194-220 patch grid) against the oracle:
+    positions, normals, uvs and indices bit-exact (same fp32 operation order, same heightmap sampling contract)."""
+    g = globals_for(320, 180, camera=TERRAIN_CAMERA)
+    hm = scene.terrain_heightmap(size)
+    dm = raster.terrain_tessellate(g, torch.from_numpy(hm).to(DEV), grid, level)
+    V, T = raster.terrain_tess_counts(grid, level)
+    ref = oracle.terrain_tessellate(g, hm, grid, level, V, T)
+    torch.cuda.synchronize()
+    for k, t in (("positions", dm.positions), ("normals", dm.normals), ("uvs", dm.uvs)):
+        assert np.array_equal(t.cpu().numpy().view(np.uint32), ref[k].view(np.uint32)), k
+    assert np.array_equal(dm.indices.cpu().numpy().view(np.uint32), ref["indices"])
+    y = ref["positions"][:, 1]
+    assert y.max() - y.min() > 5.0     # the heightmap's relief reaches the mesh
