@@ -20,8 +20,7 @@ struct SsaoParams {
     float radius, bias, kernel_size_f;
     int ksize;     // loop bound, min(kernel_size, 26)
     int noise_w;   // textureSize(u_normal_image).x
-    int swz;       // XCD-aware tile order
-    int shape;     // wave shape: 3 = 32x2 in 32x8 tiles (default); 0 = 16x4, 1 = 8x8, 2 = 4x16 in 16x16; 4 = 64x1
+    int swz;       // XCD-aware tile order (tuning knob SOC_SWZ_SSAO; 0 = row-major)
 };
 
 // ssao_generation.inl:139-141 (no FMA contraction: keeps the sin argument as the oracle's)
@@ -99,44 +98,15 @@ __device__ __forceinline__ float aff(const Aff& a, float kx, float ky, float kz)
 // The bilinear depth tap follows the contract's clamp-to-edge / 8-bit sub-texel quantisation with t
 // clamped to [0, n-1-1/256] (right-edge taps keep 1/256 of the inner texel). This regroups the
 // reference's fp32 roundings; the result stays within the SSAO tolerance of DESIGN.md §5.
-// HALO > 0 (profiling variant, SOC_SSAO_HALO): the workgroup (32x8 outputs, 64x16 depth texels) stages
-// its depth tile plus HALO texels per side in LDS. Every tap reads both an LDS pair (clamped index) and a
-// buffer pair whose offset is pushed out of range for in-tile taps (the hardware returns 0 without a
-// memory access), then selects: branch-free, and the global gathers shrink to the out-of-tile lanes.
-template <bool TABLE, bool SPARSE_IP, bool FULL, int HALO = 0>
+// 32x8-pixel workgroups of 32x2-pixel waves (each tap row of a wave spans two 128-B depth lines).
+template <bool TABLE, bool SPARSE_IP, bool FULL>
 __global__ __launch_bounds__(256) void ssao_kernel(DImg depth, DImg normal, DImg target, const float2* __restrict__ table,
                                                    SsaoParams p) {
-    constexpr int RW = 64 + 2 * HALO, RH = 16 + 2 * HALO;
-    __shared__ float tile[HALO ? RW * RH : 1];
     int bx, by;
     if (p.swz >= 2) xcd_tile_strips(p.swz, bx, by);   // SOC_SWZ_SSAO >= 2: strip width in tiles
     else xcd_tile(p.swz, bx, by);
-    const int rx0 = bx * 64 - HALO, ry0 = by * 16 - HALO;
-    if (HALO) {
-        const int tid = threadIdx.y * 16 + threadIdx.x;
-        for (int i = tid; i < RW * RH; i += 256) {
-            const int ry = i / RW, rx = i - ry * RW;
-            const int gx = min(max(rx0 + rx, 0), depth.w - 1), gy = min(max(ry0 + ry, 0), depth.h - 1);
-            tile[i] = row_ptr<float>(depth, gy)[gx];
-        }
-        __syncthreads();
-    }
-    int lx = threadIdx.x, ly = threadIdx.y;
-    if (p.shape) {
-        const int tid = threadIdx.y * 16 + threadIdx.x, wave = tid >> 6, lane = tid & 63;
-        if (p.shape == 1) { lx = (wave & 1) * 8 + (lane & 7); ly = (wave >> 1) * 8 + (lane >> 3); }
-        else { lx = wave * 4 + (lane & 3); ly = lane >> 2; }
-    }
-    int x = bx * 16 + lx, y = by * 16 + ly;
-    if (HALO || p.shape == 3) {   // 32x8 tiles, waves of 32x2
-        const int tid = threadIdx.y * 16 + threadIdx.x;
-        x = bx * 32 + (tid & 31);
-        y = by * 8 + (tid >> 5);
-    } else if (p.shape == 4) {   // 64x4 tiles, waves of 64x1
-        const int tid = threadIdx.y * 16 + threadIdx.x;
-        x = bx * 64 + (tid & 63);
-        y = by * 4 + (tid >> 6);
-    }
+    const int tid = threadIdx.x;
+    const int x = bx * 32 + (tid & 31), y = by * 8 + (tid >> 5);
     if (x >= target.w || y >= target.h) return;
     const float u = centre_uv(x, target.w), v = centre_uv(y, target.h);
 
@@ -184,22 +154,9 @@ __global__ __launch_bounds__(256) void ssao_kernel(DImg depth, DImg normal, DImg
             const int fx = (int)__builtin_fmaf(tx, 256.0f, 0.5f);
             const int fy = (int)__builtin_fmaf(ty, 256.0f, 0.5f);
             const float wx = (float)(fx & 255) * (1.0f / 256.0f), wy = (float)(fy & 255) * (1.0f / 256.0f);
-            int off = __mul24(fy >> 8, pitch) + (fx >> 8) * 4;
-            f2a4 r0, r1;
-            if (HALO) {
-                const int tlx = (fx >> 8) - rx0, tly = (fy >> 8) - ry0;
-                const bool in = (unsigned)tlx < (unsigned)(RW - 1) && (unsigned)tly < (unsigned)(RH - 1);
-                const int li = in ? tly * RW + tlx : 0;
-                const f2a4 l0 = f2a4{tile[li], tile[li + 1]}, l1 = f2a4{tile[li + RW], tile[li + RW + 1]};
-                off = in ? 0x7ffffff0 : off;   // out of range: no memory access, returns 0
-                const f2a4 g0 = __builtin_bit_cast(f2a4, __builtin_amdgcn_raw_buffer_load_b64(rsrc, off, 0, 0));
-                const f2a4 g1 = __builtin_bit_cast(f2a4, __builtin_amdgcn_raw_buffer_load_b64(rsrc, off, pitch, 0));
-                r0 = in ? l0 : g0;
-                r1 = in ? l1 : g1;
-            } else {
-                r0 = __builtin_bit_cast(f2a4, __builtin_amdgcn_raw_buffer_load_b64(rsrc, off, 0, 0));
-                r1 = __builtin_bit_cast(f2a4, __builtin_amdgcn_raw_buffer_load_b64(rsrc, off, pitch, 0));
-            }
+            const int off = __mul24(fy >> 8, pitch) + (fx >> 8) * 4;
+            const f2a4 r0 = __builtin_bit_cast(f2a4, __builtin_amdgcn_raw_buffer_load_b64(rsrc, off, 0, 0));
+            const f2a4 r1 = __builtin_bit_cast(f2a4, __builtin_amdgcn_raw_buffer_load_b64(rsrc, off, pitch, 0));
             const float top = __builtin_fmaf(wx, r0.y - r0.x, r0.x);
             const float bot = __builtin_fmaf(wx, r1.y - r1.x, r1.x);
             const float dd = __builtin_fmaf(wy, bot - top, top);
@@ -261,7 +218,6 @@ SsaoParams make_params(const soc_globals* g, const soc_img& normal) {
     p.ksize = g->ssao_kernel_size < SOC_SSAO_MAX_KERNEL ? g->ssao_kernel_size : SOC_SSAO_MAX_KERNEL;
     p.noise_w = normal.width;
     p.swz = tuning_knob("SOC_SWZ_SSAO", 0);
-    p.shape = tuning_knob("SOC_SSAO_SHAPE", 3);
     return p;
 }
 
@@ -294,21 +250,13 @@ extern "C" int soc_ssao_generation(const soc_globals* g, soc_img depth, soc_img 
     SsaoParams p = make_params(g, normal);
     const float* IP = g->camera_inverse_projection_matrix;
     const bool sip = IP[2] == 0.0f && IP[3] == 0.0f && IP[6] == 0.0f && IP[7] == 0.0f;
-    dim3 blk(16, 16), grd(ceil_div(target.width, 16), ceil_div(target.height, 16));
-    if (p.shape == 3) grd = dim3(ceil_div(target.width, 32), ceil_div(target.height, 8));
-    if (p.shape == 4) grd = dim3(ceil_div(target.width, 64), ceil_div(target.height, 4));
+    const dim3 blk(256), grd(ceil_div(target.width, 32), ceil_div(target.height, 8));
     const float2* tb = reinterpret_cast<const float2*>(noise_table);
     hipStream_t st = hs(stream);
     DImg dd = dimg(depth), dn = dimg(normal), dt = dimg(target);
 #define SOC_SSAO_LAUNCH(T, B, F) ssao_kernel<T, B, F><<<grd, blk, 0, st>>>(dd, dn, dt, tb, p)
     const bool full = p.ksize == SOC_SSAO_MAX_KERNEL;
-    const int halo = tuning_knob("SOC_SSAO_HALO", 0);
-    if (halo && noise_table && sip && full) {
-        const dim3 g3(ceil_div(target.width, 32), ceil_div(target.height, 8));
-        if (halo == 8) ssao_kernel<true, true, true, 8><<<g3, blk, 0, st>>>(dd, dn, dt, tb, p);
-        else if (halo == 16) ssao_kernel<true, true, true, 16><<<g3, blk, 0, st>>>(dd, dn, dt, tb, p);
-        else ssao_kernel<true, true, true, 32><<<g3, blk, 0, st>>>(dd, dn, dt, tb, p);
-    } else if (noise_table && sip && full) SOC_SSAO_LAUNCH(true, true, true);
+    if (noise_table && sip && full) SOC_SSAO_LAUNCH(true, true, true);
     else if (noise_table && sip) SOC_SSAO_LAUNCH(true, true, false);
     else if (noise_table) SOC_SSAO_LAUNCH(true, false, false);
     else if (sip && full) SOC_SSAO_LAUNCH(false, true, true);

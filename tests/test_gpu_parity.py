@@ -193,14 +193,13 @@ def test_ssao_noise_table_is_bit_identical(soc):
 
 
 @pytest.mark.parametrize("W,H", [(97, 55), (1920, 1080)])
-def test_ssao_wave_shapes_bit_identical(soc, monkeypatch, W, H):
-    """Every wave shape (SOC_SSAO_SHAPE) and LDS-halo variant (SOC_SSAO_HALO) computes each pixel the same way."""
+def test_ssao_tile_orders_bit_identical(soc, monkeypatch, W, H):
+    """Every workgroup order (row-major, XCD-aware, XCD band/strip: SOC_SWZ_SSAO) computes each pixel the same way."""
     g, gb = sponza_inputs(W, H)
     depth, normal = dev(gb["depth"]), dev(gb["normal"])
     outs = []
-    for shape, halo in (("3", "0"), ("0", "0"), ("1", "0"), ("2", "0"), ("4", "0"), ("3", "8"), ("3", "16"), ("3", "32")):
-        monkeypatch.setenv("SOC_SSAO_SHAPE", shape)
-        monkeypatch.setenv("SOC_SSAO_HALO", halo)   # LDS depth tile + out-of-range buffer fallback
+    for swz in ("0", "1", "4", "16"):
+        monkeypatch.setenv("SOC_SWZ_SSAO", swz)
         out = torch.zeros(H // 2, W // 2, dtype=torch.uint8, device=DEV)
         soc.ssao_generation(g, depth, normal, out)
         outs.append(host(out))
