@@ -120,6 +120,18 @@ __device__ __forceinline__ void wave_bin_pair_mask(uint32_t* sh, uint32_t b0, ui
     }
 }
 
+// The same counts as wave_bin_pair_mask with one LDS atomic per lane (two when its pixels' bins differ) and no
+// ballot loop: same-address atomics of a wave serialise in the LDS unit, off the VALU issue path.
+__device__ __forceinline__ void lane_bin_pair_mask(uint32_t* sh, uint32_t b0, uint32_t b1, uint32_t mask) {
+    const bool p0 = mask & 1u, p1 = (mask & 2u) != 0u;
+    if (p0 && p1 && b0 == b1) {
+        atomicAdd(&sh[b0], 2u);
+    } else {
+        if (p0) atomicAdd(&sh[b0], 1u);
+        if (p1) atomicAdd(&sh[b1], 1u);
+    }
+}
+
 __device__ __forceinline__ void wave_bin_pair(uint32_t* sh, uint32_t b0, uint32_t b1, bool valid) {
     wave_bin_pair_mask(sh, b0, b1, valid ? 3u : 0u);
 }

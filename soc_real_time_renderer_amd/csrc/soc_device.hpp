@@ -149,6 +149,42 @@ __device__ __forceinline__ f4 sample_rgba8(const DImg& im, float u, float v) {
                    fetch_rgba8(im, ax.i1, ay.i1), ax.w, ay.w);
 }
 
+// An image as a buffer resource (wave-uniform descriptor) addressed with 32-bit byte offsets: one VALU
+// multiply-add per address instead of the 64-bit pointer arithmetic of row_ptr. Images below 2 GiB
+// (the C ABI checks the extents it launches with).
+struct BufImg {
+    __amdgpu_buffer_rsrc_t r;
+    int pitch, w, h;
+};
+__device__ __forceinline__ BufImg buf_img(const DImg& im) {
+    return BufImg{__builtin_amdgcn_make_buffer_rsrc(im.data, 0, im.pitch * im.h, 0x00020000), im.pitch, im.w, im.h};
+}
+__device__ __forceinline__ int buf_row(const BufImg& b, int y) { return __mul24(y, b.pitch); }
+
+// sample_f32 / sample_r8 on a BufImg: the same taps, weights and arithmetic (same bits).
+__device__ __forceinline__ float sample_f32(const BufImg& b, float u, float v) {
+    typedef float f2u4 __attribute__((ext_vector_type(2))) __attribute__((aligned(4)));
+    const Axis ax = axis_clamp(u, b.w), ay = axis_clamp(v, b.h);
+    if (b.w < 2) {   // i1 == i0: the generic two-load form
+        const float t0 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(b.r, buf_row(b, ay.i0), 0, 0));
+        const float t1 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(b.r, buf_row(b, ay.i1), 0, 0));
+        return bilerp1(t0, t0, t1, t1, ax.w, ay.w);
+    }
+    const int o = ax.i0 * 4;   // i1 == i0 + 1: one 8-B load per row
+    const f2u4 r0 = __builtin_bit_cast(f2u4, __builtin_amdgcn_raw_buffer_load_b64(b.r, buf_row(b, ay.i0) + o, 0, 0));
+    const f2u4 r1 = __builtin_bit_cast(f2u4, __builtin_amdgcn_raw_buffer_load_b64(b.r, buf_row(b, ay.i1) + o, 0, 0));
+    return bilerp1(r0.x, r0.y, r1.x, r1.y, ax.w, ay.w);
+}
+__device__ __forceinline__ float sample_r8(const BufImg& b, float u, float v) {
+    const Axis ax = axis_clamp(u, b.w), ay = axis_clamp(v, b.h);
+    const int o0 = buf_row(b, ay.i0), o1 = buf_row(b, ay.i1);
+    const uint32_t a = __builtin_amdgcn_raw_buffer_load_b8(b.r, o0 + ax.i0, 0, 0);
+    const uint32_t c = __builtin_amdgcn_raw_buffer_load_b8(b.r, o0 + ax.i1, 0, 0);
+    const uint32_t d = __builtin_amdgcn_raw_buffer_load_b8(b.r, o1 + ax.i0, 0, 0);
+    const uint32_t e = __builtin_amdgcn_raw_buffer_load_b8(b.r, o1 + ax.i1, 0, 0);
+    return bilerp1(unorm8(a), unorm8(c), unorm8(d), unorm8(e), ax.w, ay.w);
+}
+
 // Packed mip chain (soc_rt.h soc_generate_mips): level count and the byte offset / extent of level k.
 __host__ __device__ __forceinline__ int mip_levels(int w, int h) {
     int m = w > h ? w : h, n = 0;
