@@ -325,7 +325,7 @@ def main():
         "vs_baseline": None,
         "dtype": "f32 (fp16/unorm8/d32 storage)",
         "data": (f"synthetic: fBm terrain (seed 0x7E44) G-buffer + 4096^2 sun shadow map (scene_synth.c)" if terrain else
-                 f"synthetic: Sponza-proxy {'box atrium (scene_synth.c)' if sc is None else 'mesh (procedural atrium, ' + str(int(sc['mesh'].struct.triangle_count)) + ' triangles, the reference Sponza baseColor/normal textures at 256^2, seed 0x5050)'}; "
+                 f"synthetic: Sponza-proxy {'box atrium (scene_synth.c)' if sc is None else 'mesh (procedural atrium, ' + str(int(sc['mesh'].struct.triangle_count)) + ' triangles, the reference Sponza baseColor/normal textures at 256^2' + ('' if args.no_mips else ' with mip chains + 16x anisotropic sampling') + ', seed 0x5050)'}; "
                  f"G-buffer + 4096^2 sun shadow map {'ray-cast on the host' if sc is None else 'rasterised once by the HIP rasteriser'}"),
         "config": {"workload": f"{'Terrain' if terrain else 'Sponza-proxy'} {W}x{H} full screen-space chain "
                                f"({args.config.upper()}): bloom x8, SSAO+blur, clouds, composition"
