@@ -139,11 +139,13 @@ constexpr int W1_OW = 32, W1_OH = 8;                          // mip1 outputs pe
 constexpr int W1_MW = 2 * W1_OW + 4, W1_MH = 2 * W1_OH + 4;   // mip0 tile 68 x 20, origin (2 X0 - 2, 2 Y0 - 2)
 constexpr int W1_EW = W1_MW + 4, W1_EH = W1_MH + 4;           // emissive tile 72 x 24, origin (2 X0 - 4, 2 Y0 - 4)
 
-__global__ __launch_bounds__(256) void bloomw_down01(DImg E, DImg M1) {
+__global__ __launch_bounds__(256) void bloomw_down01(DImg E, DImg M1, int swz) {
     __shared__ uint2 et[W1_EH][W1_EW];
     __shared__ uint2 mt[W1_MH][W1_MW];
     const int tid = threadIdx.x;
-    const int X0 = blockIdx.x * W1_OW, Y0 = blockIdx.y * W1_OH;
+    int tbx, tby;
+    xcd_tile(swz, tbx, tby);   // swz: XCD-aware order (neighbouring tiles share an XCD's L2 for their halos)
+    const int X0 = tbx * W1_OW, Y0 = tby * W1_OH;
     const int mx0 = 2 * X0 - 2, my0 = 2 * Y0 - 2, ex0 = mx0 - 2, ey0 = my0 - 2;
     load_tile<W1_EW, W1_EH>(E, ex0, ey0, et, tid);
     __syncthreads();
@@ -165,11 +167,13 @@ constexpr int W2_OW = 16, W2_OH = 8;                          // mip3 outputs pe
 constexpr int W2_MW = 2 * W2_OW + 4, W2_MH = 2 * W2_OH + 4;   // mip2 tile 36 x 20
 constexpr int W2_SW = 2 * W2_MW + 4, W2_SH = 2 * W2_MH + 4;   // mip1 tile 76 x 44
 
-__global__ __launch_bounds__(256) void bloomw_down23(DImg S1, DImg M3, int W2, int H2) {
+__global__ __launch_bounds__(256) void bloomw_down23(DImg S1, DImg M3, int W2, int H2, int swz) {
     __shared__ uint2 st[W2_SH][W2_SW];
     __shared__ uint2 mt[W2_MH][W2_MW];
     const int tid = threadIdx.x;
-    const int X0 = blockIdx.x * W2_OW, Y0 = blockIdx.y * W2_OH;
+    int tbx, tby;
+    xcd_tile(swz, tbx, tby);   // swz: XCD-aware order (neighbouring tiles share an XCD's L2 for their halos)
+    const int X0 = tbx * W2_OW, Y0 = tby * W2_OH;
     const int mx0 = 2 * X0 - 2, my0 = 2 * Y0 - 2, sx0 = 2 * mx0 - 2, sy0 = 2 * my0 - 2;
     load_tile<W2_SW, W2_SH>(S1, sx0, sy0, st, tid);
     __syncthreads();
@@ -219,11 +223,13 @@ __device__ __forceinline__ void up12_into(const uint2 (*s)[SW], int sx0, int sy0
     }
 }
 
-__global__ __launch_bounds__(256) void bloomw_up32(DImg S3, DImg M1, int W2, int H2, bool vec) {
+__global__ __launch_bounds__(256) void bloomw_up32(DImg S3, DImg M1, int W2, int H2, bool vec, int swz) {
     __shared__ uint2 st[W3_SH][W3_SW];
     __shared__ uint2 mt[W3_MH][W3_MW];
     const int tid = threadIdx.x;
-    const int X0 = blockIdx.x * U_OW, Y0 = blockIdx.y * U_OH;
+    int tbx, tby;
+    xcd_tile(swz, tbx, tby);   // swz: XCD-aware order (neighbouring tiles share an XCD's L2 for their halos)
+    const int X0 = tbx * U_OW, Y0 = tby * U_OH;
     const int mx0 = X0 / 2 - 2, my0 = Y0 / 2 - 2;       // even
     const int sx0 = mx0 / 2 - 2, sy0 = my0 / 2 - 2;     // mx0 / 2 = floor since mx0 is even
     load_tile<W3_SW, W3_SH>(S3, sx0, sy0, st, tid);
@@ -251,11 +257,13 @@ __global__ __launch_bounds__(256) void bloomw_up32(DImg S3, DImg M1, int W2, int
 constexpr int W4_MW = U_OW + 2, W4_MH = U_OH + 2;             // mip0 tile 66 x 18, origin (X0 - 1, Y0 - 1)
 constexpr int W4_SW = U_OW / 2 + 6, W4_SH = U_OH / 2 + 6;     // mip1 tile 38 x 14, origin (X0/2 - 3, Y0/2 - 3)
 
-__global__ __launch_bounds__(256) void bloomw_up10(DImg S1, DImg O, bool vec) {
+__global__ __launch_bounds__(256) void bloomw_up10(DImg S1, DImg O, bool vec, int swz) {
     __shared__ uint2 st[W4_SH][W4_SW];
     __shared__ uint2 mt[W4_MH][W4_MW + 2];   // +2: the pair loop writes whole pairs
     const int tid = threadIdx.x;
-    const int X0 = blockIdx.x * U_OW, Y0 = blockIdx.y * U_OH;
+    int tbx, tby;
+    xcd_tile(swz, tbx, tby);   // swz: XCD-aware order (neighbouring tiles share an XCD's L2 for their halos)
+    const int X0 = tbx * U_OW, Y0 = tby * U_OH;
     const int mx0 = X0 - 1, my0 = Y0 - 1;
     const int sx0 = X0 / 2 - 3, sy0 = Y0 / 2 - 3;
     const int W0 = O.w, H0 = O.h;   // mip0 extent = output extent
@@ -292,21 +300,22 @@ bool a16(const soc_img& im) { return im.pitch_bytes % 16 == 0 && reinterpret_cas
 
 int launch_bloom_weighted(const soc_img& emissive, const soc_img* mips, const soc_img& output, hipStream_t s, int stage) {
     const DImg E = dimg(emissive), M1 = dimg(mips[1]), M3 = dimg(mips[3]), O = dimg(output);
+    const int swz = tuning_knob("SOC_SWZ_BLOOM", 1);   // XCD-aware order: halo re-reads served by L2 (2.0x -> 1.0x HBM traffic)
     if (stage == 0 || stage == 1) {
         dim3 g(ceil_div(mips[1].width, W1_OW), ceil_div(mips[1].height, W1_OH));
-        bloomw_down01<<<g, 256, 0, s>>>(E, M1);
+        bloomw_down01<<<g, 256, 0, s>>>(E, M1, swz);
     }
     if (stage == 0 || stage == 2) {
         dim3 g(ceil_div(mips[3].width, W2_OW), ceil_div(mips[3].height, W2_OH));
-        bloomw_down23<<<g, 256, 0, s>>>(M1, M3, mips[2].width, mips[2].height);
+        bloomw_down23<<<g, 256, 0, s>>>(M1, M3, mips[2].width, mips[2].height, swz);
     }
     if (stage == 0 || stage == 3) {
         dim3 g(ceil_div(mips[1].width, U_OW), ceil_div(mips[1].height, U_OH));
-        bloomw_up32<<<g, 256, 0, s>>>(M3, M1, mips[2].width, mips[2].height, a16(mips[1]));
+        bloomw_up32<<<g, 256, 0, s>>>(M3, M1, mips[2].width, mips[2].height, a16(mips[1]), swz);
     }
     if (stage == 0 || stage == 4) {
         dim3 g(ceil_div(output.width, U_OW), ceil_div(output.height, U_OH));
-        bloomw_up10<<<g, 256, 0, s>>>(M1, O, a16(output));
+        bloomw_up10<<<g, 256, 0, s>>>(M1, O, a16(output), swz);
     }
     return check_launch("bloom_weighted");
 }
