@@ -8,6 +8,7 @@
 // stage the 64x64 noise texture into LDS as packed 2x2 quads (one ds_read_b32 returns the four texels
 // of a bilinear REPEAT tap), 16 KiB per workgroup.
 #include <cstdlib>
+#include <type_traits>
 
 #include "soc_internal.hpp"
 
@@ -39,10 +40,15 @@ struct CloudParams {
     int res_x, res_y;
 };
 
-struct Ctx {
-    const uint32_t* quads;   // LDS
+// Q = uint32_t: LDS quads of 4 bytes (c0 c1 / c2 c3); Q = uint2: the same quad pre-expanded to 16-bit pairs
+// (c0 | c1 << 16, c2 | c3 << 16), which saves the two byte permutes per bilinear tap (twice the LDS).
+template <typename Q>
+struct CtxT {
+    const Q* quads;   // LDS
     float cam_x, cam_z, time;
 };
+using Ctx = CtxT<uint32_t>;
+using CtxW = CtxT<uint2>;
 
 __device__ __forceinline__ float bayer2(float ax, float ay) {
     ax = floorf(ax);
@@ -80,8 +86,13 @@ __device__ __forceinline__ uint32_t quad_bilerp_u(uint32_t q, uint32_t wxp, uint
     return udot2(top | (bot << 16), wyp);
 }
 
+__device__ __forceinline__ uint32_t quad_bilerp_u(uint2 q, uint32_t wxp, uint32_t wyp) {
+    return udot2(udot2(q.x, wxp) | (udot2(q.y, wxp) << 16), wyp);
+}
+
 // get_3d_noise, :219-233
-__device__ __forceinline__ float noise3(const Ctx& cx, f3 pos) {
+template <typename Q>
+__device__ __forceinline__ float noise3(const CtxT<Q>& cx, f3 pos) {
     const float p = floorf(pos.z);
     const float f = pos.z - p;
     // fixed-point texel coordinate of the first tap: (u 64 - 0.5) 256 + 0.5 with u = pos.x / 64 + p 17/64,
@@ -92,8 +103,8 @@ __device__ __forceinline__ float noise3(const Ctx& cx, f3 pos) {
     const uint32_t wx = (uint32_t)fx & 255u, wy = (uint32_t)fy & 255u;
     const uint32_t wxp = wx * 65535u + 256u, wyp = wy * 65535u + 256u;
     const uint32_t ix = ((uint32_t)fx >> 8) & kNoiseMask, iy = ((uint32_t)fy >> 8) & kNoiseMask;
-    const uint32_t* t = cx.quads + (iy * (uint32_t)kTW + ix);
-    const uint32_t q0 = t[0], q1 = t[kTap2 * kTW + kTap2];
+    const Q* t = cx.quads + (iy * (uint32_t)kTW + ix);
+    const Q q0 = t[0], q1 = t[kTap2 * kTW + kTap2];
     const float a = (float)quad_bilerp_u(q0, wxp, wyp), b = (float)quad_bilerp_u(q1, wxp, wyp);
     return __builtin_fmaf(f, b - a, a) * (1.0f / (255.0f * 65536.0f));
 }
@@ -110,7 +121,8 @@ __device__ __forceinline__ float cloud_height(f3 p) { return hw_length3(f3{p.x, 
 // plus the largest possible remainder stays below the smoothstep's lower edge 0.55 the result is
 // exactly 0 (smoothstep clamps to 0) and the remaining octaves are skipped. The 1e-4 margin covers the
 // fp32 rounding of the remainder, so the early exits never change a result.
-__device__ float clouds_at(const Ctx& cx, f3 p, float h) {
+template <typename C>
+__device__ float clouds_at(const C& cx, f3 p, float h) {
     p = f3{p.x + cx.cam_x, h, p.z + cx.cam_z};
     const f3 mv = f3{cx.time, 0.0f, cx.time};
     const f3 cc = p * 0.001f + mv;
@@ -127,7 +139,8 @@ __device__ float clouds_at(const Ctx& cx, f3 p, float h) {
     return clouds * 0.03f;
 }
 
-__device__ __forceinline__ float get_clouds(const Ctx& cx, f3 p) {
+template <typename C>
+__device__ __forceinline__ float get_clouds(const C& cx, f3 p) {
     const float h = cloud_height(p);
     if (h < kMinH || h > kMaxH) return 0.0f;
     return clouds_at(cx, p, h);
@@ -137,7 +150,8 @@ __device__ __forceinline__ float get_clouds(const Ctx& cx, f3 p) {
 // ((p + R e_y) . sun > 0) the altitude grows monotonically along it (|a + t s|^2 is convex in t), so
 // once a step leaves the top of the layer every later step returns 0, and stopping there leaves tr
 // unchanged (tr + 0 == tr).
-__device__ float sun_visibility(const Ctx& cx, f3 p, f3 sun) {
+template <typename C>
+__device__ float sun_visibility(const C& cx, f3 p, f3 sun) {
     const float rSteps = 500.0f / 10.0f;
     const f3 inc = sun * rSteps;
     f3 pos = inc * 0.5f + p;
@@ -353,6 +367,20 @@ __device__ __forceinline__ void stage_noise(const DImg& noise, uint32_t* quads, 
             return row_ptr<uint32_t>(noise, ty)[tx] & 0xffu;
         };
         quads[i] = texel(nx, nyw) | (texel(nx1, nyw) << 8) | (texel(nx, ny1) << 16) | (texel(nx1, ny1) << 24);
+    }
+}
+
+template <bool NOISE_R8>
+__device__ __forceinline__ void stage_noise_wide(const DImg& noise, uint2* quads, int tid, int nthreads) {
+    for (int i = tid; i < kTable; i += nthreads) {
+        const int ny = i / kTW, nx = (i - ny * kTW) & kNoiseMask;
+        const int nyw = ny & kNoiseMask;
+        const int nx1 = (nx + 1) & kNoiseMask, ny1 = (nyw + 1) & kNoiseMask;
+        auto texel = [&](int tx, int ty) -> uint32_t {
+            if (NOISE_R8) return row_ptr<uint8_t>(noise, ty)[tx];
+            return row_ptr<uint32_t>(noise, ty)[tx] & 0xffu;
+        };
+        quads[i] = uint2{texel(nx, nyw) | (texel(nx1, nyw) << 16), texel(nx, ny1) | (texel(nx1, ny1) << 16)};
     }
 }
 
@@ -577,10 +605,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void c
 
 // 512-lane workgroups: the 26 KiB noise table per workgroup caps residency at 6 workgroups per CU, so 256 lanes
 // give 6 waves per SIMD and 512 lanes give the full 8 (one table per 8 waves).
-template <bool NOISE_R8, uint32_t kSunvisThreads>
-__global__ __launch_bounds__(kSunvisThreads) __attribute__((amdgpu_waves_per_eu(kSunvisThreads == 512 ? 8 : 6))) void clouds_sunvis(
+template <bool NOISE_R8, uint32_t kSunvisThreads, bool WIDE = false>
+__global__ __launch_bounds__(kSunvisThreads) __attribute__((amdgpu_waves_per_eu(kSunvisThreads == 512 && !WIDE ? 8 : 6))) void clouds_sunvis(
     DImg noise, CloudParams p, const uint32_t* __restrict__ list, PairBufs pb) {
-    __shared__ uint32_t quads[kTable];
+    using Q = typename std::conditional<WIDE, uint2, uint32_t>::type;
+    __shared__ Q quads[kTable];
     __shared__ uint32_t pre[kShards + 1];
     const uint32_t tid = threadIdx.x;
     if (tid == 0) {
@@ -594,9 +623,10 @@ __global__ __launch_bounds__(kSunvisThreads) __attribute__((amdgpu_waves_per_eu(
     __syncthreads();
     const uint32_t total = pre[kShards];
     if (blockIdx.x * kSunvisThreads >= total) return;
-    stage_noise<NOISE_R8>(noise, quads, tid, kSunvisThreads);
+    if constexpr (WIDE) stage_noise_wide<NOISE_R8>(noise, quads, tid, kSunvisThreads);
+    else stage_noise<NOISE_R8>(noise, quads, tid, kSunvisThreads);
     __syncthreads();
-    Ctx cx;
+    CtxT<Q> cx;
     cx.quads = quads;
     cx.cam_x = p.cam[0];
     cx.cam_z = p.cam[2];
@@ -798,7 +828,7 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
     // One resident wave set per kernel, grid-stride over the list / pairs: the long per-item work is
     // balanced over all SIMDs instead of running as a second, partially filled round.
     static int res_atmos = 0, res_density = 0, res_sunvis = 0, res_resolve = 0;
-    static bool sunvis512 = true;
+    static bool sunvis512 = true, sunvis_wide = true;
     if (!res_atmos) {
         // tuning knob: percent of the resident set each persistent kernel takes (the rest of the CU slots stay
         // free for the frame lane's kernels running beside the sky lane)
@@ -807,7 +837,9 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
         res_atmos = share(resident_blocks(clouds_atmosphere));
         res_density = share(resident_blocks(clouds_density<false>));
         sunvis512 = tuning_knob("SOC_SUNVIS_THREADS", 512) == 512;
-        res_sunvis = share(sunvis512 ? resident_blocks(clouds_sunvis<false, 512>, 512) : resident_blocks(clouds_sunvis<false, 256>, 256));
+        sunvis_wide = tuning_knob("SOC_SUNVIS_WIDE", 1) != 0;
+        res_sunvis = share(sunvis_wide ? resident_blocks(clouds_sunvis<false, 512, true>, 512)
+                           : sunvis512 ? resident_blocks(clouds_sunvis<false, 512>, 512) : resident_blocks(clouds_sunvis<false, 256>, 256));
         res_resolve = share(resident_blocks(clouds_resolve<false>));
     }
     const long long blocks = ((long long)W * H + 255) / 256;
@@ -817,12 +849,14 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
     const DImg nz = dimg(noise), tg = dimg(target);
     if (r8) {
         clouds_density<true><<<grid(res_density, blocks), 256, 0, s>>>(nz, p, counter, list, ws.pb);
-        if (sunvis512) clouds_sunvis<true, 512><<<grid(res_sunvis, blocks), 512, 0, s>>>(nz, p, list, ws.pb);
+        if (sunvis_wide) clouds_sunvis<true, 512, true><<<grid(res_sunvis, blocks), 512, 0, s>>>(nz, p, list, ws.pb);
+        else if (sunvis512) clouds_sunvis<true, 512><<<grid(res_sunvis, blocks), 512, 0, s>>>(nz, p, list, ws.pb);
         else clouds_sunvis<true, 256><<<grid(res_sunvis, 2 * blocks), 256, 0, s>>>(nz, p, list, ws.pb);
         clouds_resolve<true><<<grid(res_resolve, blocks), 256, 0, s>>>(nz, tg, p, counter, list, ws.atmos, ws.pb);
     } else {
         clouds_density<false><<<grid(res_density, blocks), 256, 0, s>>>(nz, p, counter, list, ws.pb);
-        if (sunvis512) clouds_sunvis<false, 512><<<grid(res_sunvis, blocks), 512, 0, s>>>(nz, p, list, ws.pb);
+        if (sunvis_wide) clouds_sunvis<false, 512, true><<<grid(res_sunvis, blocks), 512, 0, s>>>(nz, p, list, ws.pb);
+        else if (sunvis512) clouds_sunvis<false, 512><<<grid(res_sunvis, blocks), 512, 0, s>>>(nz, p, list, ws.pb);
         else clouds_sunvis<false, 256><<<grid(res_sunvis, 2 * blocks), 256, 0, s>>>(nz, p, list, ws.pb);
         clouds_resolve<false><<<grid(res_resolve, blocks), 256, 0, s>>>(nz, tg, p, counter, list, ws.atmos, ws.pb);
     }
