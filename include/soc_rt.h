@@ -179,6 +179,9 @@ int32_t soc_abi_version(void);
 size_t soc_abi_sizeof(const char* type_name);                        /* "soc_globals", "soc_img", ... */
 int64_t soc_abi_offsetof(const char* type_name, const char* field);  /* -1 if unknown */
 const char* soc_last_error_string(void);
+/* Tuning knobs (SOC_* environment variables of the profiling variants) are read once and cached;
+ * this drops the cache so the current environment applies to the next launches. */
+void soc_tuning_reload(void);
 const char* soc_device_arch(void);                                   /* "gfx950" the kernels were built for */
 
 /* --- Host-side globals feed (native C++, no GPU needed) ----------------------------------------- */

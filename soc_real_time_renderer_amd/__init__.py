@@ -222,6 +222,11 @@ def write_png(path: str, rgba8: np.ndarray) -> None:
            "soc_write_png")
 
 
+def reload_tuning() -> None:
+    """Re-read the SOC_* tuning-knob environment variables on the next launches (soc_tuning_reload)."""
+    lib().soc_tuning_reload()
+
+
 def write_exr(path: str, rgba16f: np.ndarray) -> None:
     """(H, W, 4) float16 host image -> OpenEXR, uncompressed HALF (soc_write_exr)."""
     a = np.ascontiguousarray(rgba16f, np.float16)
@@ -291,7 +296,7 @@ def temporal_antialiasing(g, target, current_color, previous_color, current_velo
 def temporal_antialiasing_tone_mapping(g, target, current_color, previous_color, current_velocity, previous_velocity,
                                        depth, auto_exposure, output, velocity_history_out=None, output_format=None,
                                        stream=None):
-    """TAA followed by AgX tone mapping into `output` (one launch for an RGBA8_UNORM output)."""
+    """TAA followed by AgX tone mapping into `output` (one launch for an RGBA8_UNORM or RGBA8_SRGB output)."""
     _check(lib().soc_temporal_antialiasing_tone_mapping(
         _gp(g), img(target), img(current_color), img(previous_color), img(current_velocity), img(previous_velocity),
         img(depth), img(velocity_history_out), _ptr(auto_exposure), img(output, output_format), _stream(stream)),

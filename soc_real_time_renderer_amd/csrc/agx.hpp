@@ -34,6 +34,13 @@ __device__ __forceinline__ f3 agx(const TmParams& p, f4 c, float expo) {
     return mul(p.Minv, w);
 }
 
+// linear -> sRGB transfer for an RGBA8_SRGB framebuffer (the store of an *_SRGB swapchain image), shared by the
+// tone-mapping pass and the fused TAA + tone map so both write the same codes.
+__device__ __forceinline__ float srgb_encode(float c) {
+    c = clampf(c, 0.0f, 1.0f);
+    return c <= 0.0031308f ? c * 12.92f : 1.055f * powf(c, 1.0f / 2.4f) - 0.055f;
+}
+
 // Host: the uniform DualSection constants of a TmParams whose linear / peak / saturation are set.
 inline void tm_params_finish(TmParams& p) {
     p.S = p.peak * p.linear;

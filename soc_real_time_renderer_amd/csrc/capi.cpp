@@ -13,6 +13,7 @@
 #include <cstring>
 #include <functional>
 #include <string>
+#include <mutex>
 #include <vector>
 
 #include "soc_internal.hpp"
@@ -42,9 +43,21 @@ int check_img(const soc_img& im, int fmt, const char* pass, const char* what) {
     return SOC_OK;
 }
 
+// Tuning knobs: the environment is read once per knob and cached (not per launch);
+// soc_tuning_reload() drops the cache so a changed environment takes effect.
+namespace {
+std::mutex g_knob_mu;
+std::vector<std::pair<std::string, int>> g_knobs;
+}  // namespace
+
 int tuning_knob(const char* name, int dflt) {
+    std::lock_guard<std::mutex> lock(g_knob_mu);
+    for (const auto& k : g_knobs)
+        if (k.first == name) return k.second;
     const char* e = getenv(name);
-    return e ? atoi(e) : dflt;
+    const int v = e ? atoi(e) : dflt;
+    g_knobs.emplace_back(name, v);
+    return v;
 }
 
 int check_launch(const char* pass) {
@@ -327,6 +340,11 @@ static inline float radians(float deg) { return deg * 0.017453292519943295769236
 static V3h rotate_x(V3h v, float a) { float c = std::cos(a), s = std::sin(a); return V3h{v.x, v.y * c - v.z * s, v.y * s + v.z * c}; }
 static V3h rotate_y(V3h v, float a) { float c = std::cos(a), s = std::sin(a); return V3h{v.x * c + v.z * s, v.y, -v.x * s + v.z * c}; }
 static V3h rotate_z(V3h v, float a) { float c = std::cos(a), s = std::sin(a); return V3h{v.x * c - v.y * s, v.x * s + v.y * c, v.z}; }
+
+extern "C" void soc_tuning_reload(void) {
+    std::lock_guard<std::mutex> lock(g_knob_mu);
+    g_knobs.clear();
+}
 
 extern "C" int soc_globals_init_defaults(soc_globals* g, int32_t width, int32_t height) {
     if (!g || width <= 0 || height <= 0) return set_error(SOC_E_INVALID_ARG, "soc_globals_init_defaults: bad args");
@@ -818,12 +836,13 @@ void build_passes_tail(soc_renderer* r) {
                                                          r->fold_in_resolve ? r->hist_scratch : nullptr, (soc_stream)s);
              });
     // renderer.cpp:1170-1198: TAA + both history copies (ping-pong + fused velocity history), and
-    // renderer.cpp:1210-1217: tone mapping, fused into the TAA launch for an RGBA8_UNORM framebuffer
+    // renderer.cpp:1210-1217: tone mapping, fused into the TAA launch for an RGBA8 (UNORM or SRGB) framebuffer
     const uint64_t taa_reads = res_mask({SOC_RES_COLOR, SOC_RES_PREVIOUS_COLOR, SOC_RES_VELOCITY,
                                          SOC_RES_PREVIOUS_VELOCITY, SOC_RES_DEPTH}) |
                                (r->sky_split ? res_mask({SOC_RES_SKY_COLOR}) : 0);
     const uint64_t taa_writes = res_mask({SOC_RES_RESOLVED, SOC_RES_PREVIOUS_VELOCITY});
-    const bool fuse_tm = !(r->flags & SOC_RENDERER_UNFUSED_TONEMAP) && I.output.format == SOC_FMT_RGBA8_UNORM;
+    const bool fuse_tm = !(r->flags & SOC_RENDERER_UNFUSED_TONEMAP) &&
+                         (I.output.format == SOC_FMT_RGBA8_UNORM || I.output.format == SOC_FMT_RGBA8_SRGB);
     if (fuse_tm) {
         add_pass(r, "TemporalAntiAliasing+ToneMapping", "Temporal Anti-Aliasing", post,
                  taa_reads | res_mask({SOC_RES_AUTO_EXPOSURE}), taa_writes | res_mask({SOC_RES_OUTPUT}),

@@ -221,6 +221,7 @@ struct TmOut {
     DImg out;
     const soc_auto_exposure* ae;
     TmParams p;
+    int srgb;   // RGBA8_SRGB framebuffer: sRGB-encode on store
 };
 
 // Lane i's left neighbour column (x0 - 1) is lane i-1's second pixel and its right one (x0 + 2) lane
@@ -368,8 +369,12 @@ __global__ __launch_bounds__(256) void taa_pair2(DImg target, DImg cur, DImg pre
     if (vel_out.data) row_ptr_w<uint4>(vel_out, y)[x0 >> 1] = row_ptr<uint4>(vel, y)[x0 >> 1];
     if (TM) {
         const float expo = exp2f(exposure);   // pow(2.0, exposure)
-        const f3 c0 = agx(tm.p, unpack_h4(outp[0]), expo);
-        const f3 c1 = agx(tm.p, unpack_h4(outp[1]), expo);
+        f3 c0 = agx(tm.p, unpack_h4(outp[0]), expo);
+        f3 c1 = agx(tm.p, unpack_h4(outp[1]), expo);
+        if (tm.srgb) {
+            c0 = f3{srgb_encode(c0.x), srgb_encode(c0.y), srgb_encode(c0.z)};
+            c1 = f3{srgb_encode(c1.x), srgb_encode(c1.y), srgb_encode(c1.z)};
+        }
         row_ptr_w<uint2>(tm.out, y)[x0 >> 1] =
             uint2{pack_unorm8x4(f4{c0.x, c0.y, c0.z, 1.0f}), pack_unorm8x4(f4{c1.x, c1.y, c1.z, 1.0f})};
     }
@@ -510,13 +515,15 @@ extern "C" int soc_temporal_antialiasing_tone_mapping(const soc_globals* g, soc_
     if (!g || !d_auto_exposure) return set_error(SOC_E_INVALID_ARG, "%s: null globals / auto exposure buffer", P);
     int rc = check_img(output, 0, P, "output");
     if (rc) return rc;
-    const bool fusable = output.format == SOC_FMT_RGBA8_UNORM && output.width == target.width &&
+    const bool fusable = (output.format == SOC_FMT_RGBA8_UNORM || output.format == SOC_FMT_RGBA8_SRGB) &&
+                         output.width == target.width &&
                          output.height == target.height && (reinterpret_cast<uintptr_t>(output.data) & 7u) == 0 &&
                          (output.pitch_bytes & 7) == 0 && output.data != target.data;
     if (fusable) {
         TmOut tm;
         tm.out = dimg(output);
         tm.ae = d_auto_exposure;
+        tm.srgb = output.format == SOC_FMT_RGBA8_SRGB;
         agx_matrices(g->compression, tm.p.M.m, tm.p.Minv.m);
         tm.p.linear = g->agxDs_linear_section;
         tm.p.peak = g->peak;

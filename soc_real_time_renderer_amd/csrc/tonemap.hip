@@ -11,11 +11,6 @@
 namespace soc {
 namespace {
 
-__device__ __forceinline__ float srgb_encode(float c) {
-    c = clampf(c, 0.0f, 1.0f);
-    return c <= 0.0031308f ? c * 12.92f : 1.055f * powf(c, 1.0f / 2.4f) - 0.055f;
-}
-
 template <int FMT>
 __device__ __forceinline__ void store_px(const DImg& t, int x, int y, f3 c) {
     if constexpr (FMT == SOC_FMT_RGBA8_UNORM) {

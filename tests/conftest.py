@@ -25,3 +25,15 @@ def oracle():
     import oracle as o
     o.lib()
     return o
+
+
+@pytest.fixture(autouse=True)
+def _tuning_knobs_fresh(monkeypatch):
+    """Tests that set SOC_* tuning knobs (monkeypatch.setenv, then soc.reload_tuning()) leave no cached value
+    behind: the knob cache is dropped after the environment is restored."""
+    yield
+    monkeypatch.undo()
+    if "soc_real_time_renderer_amd" in sys.modules:
+        m = sys.modules["soc_real_time_renderer_amd"]
+        if getattr(m, "_LIB", None) is not None:
+            m.reload_tuning()

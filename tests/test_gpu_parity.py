@@ -200,6 +200,7 @@ def test_ssao_tile_orders_bit_identical(soc, monkeypatch, W, H):
     outs = []
     for swz in ("0", "1", "4", "16"):
         monkeypatch.setenv("SOC_SWZ_SSAO", swz)
+        soc.reload_tuning()
         out = torch.zeros(H // 2, W // 2, dtype=torch.uint8, device=DEV)
         soc.ssao_generation(g, depth, normal, out)
         outs.append(host(out))
@@ -232,6 +233,7 @@ def test_composition_cache_policy_variants_bit_identical(soc, monkeypatch):
     outs = []
     for nt in ("3", "0"):
         monkeypatch.setenv("SOC_COMP_NT", nt)
+        soc.reload_tuning()
         out = torch.zeros(H, W, 4, dtype=torch.float16, device=DEV)
         soc.composition(g, out, *ins, ssao, shadow, clouds)
         outs.append(host(out))
@@ -412,6 +414,7 @@ def test_taa_lane_shift_neighbours_identical(soc, oracle, monkeypatch, W, H):
     outs = []
     for nbr in ("2", "1", "0"):
         monkeypatch.setenv("SOC_TAA_NBR", nbr)
+        soc.reload_tuning()
         t = torch.zeros(H, W, 4, dtype=torch.float16, device=DEV)
         o = torch.zeros(H, W, 4, dtype=torch.uint8, device=DEV)
         soc.temporal_antialiasing_tone_mapping(g, t, cur, prev, vel, pvel, depth, ae, o)
@@ -426,10 +429,12 @@ def test_taa_lane_shift_neighbours_identical(soc, oracle, monkeypatch, W, H):
     assert ok.all(), ok.mean()
 
 
-@pytest.mark.parametrize("W,H", [(64, 36), (97, 55), (1920, 1080)])
-def test_taa_tone_mapping_fused_equals_two_passes(soc, W, H):
+@pytest.mark.parametrize("W,H,srgb", [(64, 36, False), (97, 55, False), (1920, 1080, False), (64, 36, True),
+                                      (1920, 1080, True)])
+def test_taa_tone_mapping_fused_equals_two_passes(soc, W, H, srgb):
     """The fused TAA + tone-map launch gives the TAA pass's bits and the tone-map pass's bits (97x55:
-    odd width, the two-pass fallback)."""
+    odd width, the two-pass fallback), for an RGBA8_UNORM and an RGBA8_SRGB framebuffer (sRGB-encoded store)."""
+    fmt = soc.FMT_RGBA8_SRGB if srgb else None
     g, gb = sponza_inputs(W, H)
     cur = dev(random_rgba16(H, W, seed=1, hi=3.0))
     prev = dev(random_rgba16(H, W, seed=2, hi=3.0))
@@ -440,9 +445,10 @@ def test_taa_tone_mapping_fused_equals_two_passes(soc, W, H):
     t1 = torch.zeros(H, W, 4, dtype=torch.float16, device=DEV)
     o1 = torch.zeros(H, W, 4, dtype=torch.uint8, device=DEV)
     soc.temporal_antialiasing(g, t1, cur, prev, vel, pvel, depth)
-    soc.tone_mapping(g, t1, ae, o1)
+    soc.tone_mapping(g, t1, ae, o1, target_format=fmt)
     t2, o2, v2 = torch.zeros_like(t1), torch.zeros_like(o1), torch.zeros_like(t1)
-    soc.temporal_antialiasing_tone_mapping(g, t2, cur, prev, vel, pvel, depth, ae, o2, velocity_history_out=v2)
+    soc.temporal_antialiasing_tone_mapping(g, t2, cur, prev, vel, pvel, depth, ae, o2, velocity_history_out=v2,
+                                           output_format=fmt)
     torch.cuda.synchronize()
     assert torch.equal(t1, t2)
     assert torch.equal(v2, vel)

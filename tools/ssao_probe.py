@@ -33,6 +33,7 @@ def main():
         env = dict(kv.split("=") for kv in v.split(",") if kv)
         saved = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
+        soc.reload_tuning()
         out = torch.zeros_like(ref)
         for _ in range(5):
             soc.ssao_generation(g, depth, normal, out, table)
