@@ -34,33 +34,6 @@ __global__ __launch_bounds__(256) void bloom_down_generic(DImg src, DImg dst, fl
     store_rgb1(dst, x, y, SOC_DOWN13(a, b, c, d, e, f, g, h, i, j, k, l, m));
 }
 
-// src and dst have the same extent: every tap lands on a texel centre (weights 0/1).
-__global__ __launch_bounds__(256) void bloom_down_same(DImg src, DImg dst) {
-    const int x = blockIdx.x * BX + threadIdx.x, y = blockIdx.y * BY + threadIdx.y;
-    if (x >= dst.w || y >= dst.h) return;
-    // uv.y + 2*texel is the row BELOW (y grows downward in texel space as uv.y grows).
-    f3 a = point(src, x - 2, y + 2), b = point(src, x, y + 2), c = point(src, x + 2, y + 2);
-    f3 d = point(src, x - 2, y), e = point(src, x, y), f = point(src, x + 2, y);
-    f3 g = point(src, x - 2, y - 2), h = point(src, x, y - 2), i = point(src, x + 2, y - 2);
-    f3 j = point(src, x - 1, y + 1), k = point(src, x + 1, y + 1), l = point(src, x - 1, y - 1), m = point(src, x + 1, y - 1);
-    store_rgb1(dst, x, y, SOC_DOWN13(a, b, c, d, e, f, g, h, i, j, k, l, m));
-}
-
-// src is exactly twice dst: every tap is the w = 0.5 blend of a 2x2 block starting at 2x + k.
-__global__ __launch_bounds__(256) void bloom_down_half(DImg src, DImg dst) {
-    const int x = blockIdx.x * BX + threadIdx.x, y = blockIdx.y * BY + threadIdx.y;
-    if (x >= dst.w || y >= dst.h) return;
-    auto AX = [&](int k) { return axis_from_fixed(256 * (2 * x + k) + 128, src.w); };
-    auto AY = [&](int k) { return axis_from_fixed(256 * (2 * y + k) + 128, src.h); };
-    const Axis xm2 = AX(-2), xm1 = AX(-1), x0 = AX(0), xp1 = AX(1), xp2 = AX(2);
-    const Axis ym2 = AY(-2), ym1 = AY(-1), y0 = AY(0), yp1 = AY(1), yp2 = AY(2);
-    f3 a = tap(src, xm2, yp2), b = tap(src, x0, yp2), c = tap(src, xp2, yp2);
-    f3 d = tap(src, xm2, y0), e = tap(src, x0, y0), f = tap(src, xp2, y0);
-    f3 g = tap(src, xm2, ym2), h = tap(src, x0, ym2), i = tap(src, xp2, ym2);
-    f3 j = tap(src, xm1, yp1), k = tap(src, xp1, yp1), l = tap(src, xm1, ym1), m = tap(src, xp1, ym1);
-    store_rgb1(dst, x, y, SOC_DOWN13(a, b, c, d, e, f, g, h, i, j, k, l, m));
-}
-
 // ------------------------------------------------------------------------------------------------
 // upsample (result overwrites the destination: quirk Q5)
 // ------------------------------------------------------------------------------------------------
@@ -74,15 +47,6 @@ __global__ __launch_bounds__(256) void bloom_up_generic(DImg src, DImg dst, floa
     f3 a = S(u - X, v + Y), b = S(u, v + Y), c = S(u + X, v + Y);
     f3 d = S(u - X, v), e = S(u, v), f = S(u + X, v);
     f3 g = S(u - X, v - Y), h = S(u, v - Y), i = S(u + X, v - Y);
-    store_rgb1(dst, x, y, SOC_UP9(a, b, c, d, e, f, g, h, i));
-}
-
-__global__ __launch_bounds__(256) void bloom_up_same(DImg src, DImg dst) {
-    const int x = blockIdx.x * BX + threadIdx.x, y = blockIdx.y * BY + threadIdx.y;
-    if (x >= dst.w || y >= dst.h) return;
-    f3 a = point(src, x - 1, y + 1), b = point(src, x, y + 1), c = point(src, x + 1, y + 1);
-    f3 d = point(src, x - 1, y), e = point(src, x, y), f = point(src, x + 1, y);
-    f3 g = point(src, x - 1, y - 1), h = point(src, x, y - 1), i = point(src, x + 1, y - 1);
     store_rgb1(dst, x, y, SOC_UP9(a, b, c, d, e, f, g, h, i));
 }
 
@@ -103,7 +67,8 @@ __global__ __launch_bounds__(256) void bloom_up_double(DImg src, DImg dst) {
 // register-window kernels: each lane loads the raw RGBA16F texels of its window once (8-B loads, L1
 // shared with its neighbours) and evaluates the taps channel by channel; bilinear taps share their
 // horizontal lerps between taps that use the same row and x-pair. Every tap is computed with exactly
-// the arithmetic of tap()/point() above (same lerps, same order), so results are bit-identical.
+// the arithmetic of tap()/point() above (same lerps, same order) as the oracle's per-tap restatement,
+// so results are bit-identical.
 // ------------------------------------------------------------------------------------------------
 // same-size 13-tap downsample, 2x2 output pixels per lane from a 6x6 texel window
 __global__ __launch_bounds__(256) void bloom_down_same_q(DImg src, DImg dst, bool vec) {

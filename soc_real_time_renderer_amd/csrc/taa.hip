@@ -85,100 +85,6 @@ __global__ __launch_bounds__(256) void taa_fast(DImg target, DImg cur, DImg prev
 
 typedef uint32_t u4a8 __attribute__((ext_vector_type(4))) __attribute__((aligned(8)));
 
-// Bilinear RGBA16F sample whose two taps per row come from one 16-byte load (texels i0 and i0+1 are
-// adjacent: the contract's axis keeps i0 <= n-2). Same arithmetic as sample_h4.
-__device__ __forceinline__ f4 sample_h4_pairs(const DImg& im, float u, float v) {
-    const Axis ax = axis_clamp(u, im.w), ay = axis_clamp(v, im.h);
-    const u4a8 r0 = *reinterpret_cast<const u4a8*>(row_ptr<uint2>(im, ay.i0) + ax.i0);
-    const u4a8 r1 = *reinterpret_cast<const u4a8*>(row_ptr<uint2>(im, ay.i1) + ax.i0);
-    return bilerp4(unpack_h4(uint2{r0.x, r0.y}), unpack_h4(uint2{r0.z, r0.w}), unpack_h4(uint2{r1.x, r1.y}),
-                   unpack_h4(uint2{r1.z, r1.w}), ax.w, ay.w);
-}
-
-__device__ __forceinline__ f4 resolve_pairs(const TaaParams& p, float u, float v, f4 color, f4 mn, f4 mx, f4 blurred,
-                                            float2 vel, const DImg& prev, const DImg& pvel) {
-    float accum = p.accum0;
-    const float vx = u - vel.x, vy = v - vel.y;
-    f4 acc = sample_h4_pairs(prev, vx, vy);
-    if (vx < 0.0f || vy < 0.0f || vx > 1.0f || vy > 1.0f) accum = 1.0f;
-    acc = f4{clampf(acc.x, mn.x, mx.x), clampf(acc.y, mn.y, mx.y), clampf(acc.z, mn.z, mx.z), clampf(acc.w, mn.w, mx.w)};
-    f4 o = f4{color.x * accum + acc.x * (1.0f - accum), color.y * accum + acc.y * (1.0f - accum),
-              color.z * accum + acc.z * (1.0f - accum), color.w * accum + acc.w * (1.0f - accum)};
-    const f4 pv = sample_h4_pairs(pvel, vx, vy);
-    const float dvx = pv.x - vel.x, dvy = pv.y - vel.y;
-    const float vlen = sqrtf(dvx * dvx + dvy * dvy);
-    const float dis = clampf((vlen - 0.001f) * 10.0f, 0.0f, 1.0f);
-    return f4{mixf(o.x, blurred.x, dis), mixf(o.y, blurred.y, dis), mixf(o.z, blurred.z, dis), mixf(o.w, blurred.w, dis)};
-}
-
-// Two horizontally adjacent pixels per lane (x0 even): the 3x4 neighbourhood of colour and depth is
-// loaded once (a 16-B / 8-B pair load for columns x0, x0+1 plus the clamped edge columns), the
-// history taps use 16-B row-pair loads, the velocity history copy is one 16-B load + store.
-// Per-pixel arithmetic is that of taa_fast.
-__global__ __launch_bounds__(256) void taa_pair(DImg target, DImg cur, DImg prev, DImg vel, DImg pvel, DImg depth,
-                                                DImg vel_out, TaaParams p) {
-    const int x0 = (blockIdx.x * BX + threadIdx.x) * 2, y = blockIdx.y * BY + threadIdx.y;
-    if (x0 >= target.w || y >= target.h) return;
-    const int W = target.w, H = target.h;
-    const int xl = max(x0 - 1, 0), xr = min(x0 + 2, W - 1);
-    f4 C[3][4];
-    float D[3][4];
-    int rows[3];
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-        const int sy = min(max(y + 1 - r, 0), H - 1);   // r = 0: oy = +1, r = 1: oy = 0, r = 2: oy = -1
-        rows[r] = sy;
-        const uint2* crow = row_ptr<uint2>(cur, sy);
-        const float* drow = row_ptr<float>(depth, sy);
-        const uint4 mid = *reinterpret_cast<const uint4*>(crow + x0);
-        const float2 dmid = *reinterpret_cast<const float2*>(drow + x0);
-        C[r][0] = unpack_h4(crow[xl]);
-        C[r][1] = unpack_h4(uint2{mid.x, mid.y});
-        C[r][2] = unpack_h4(uint2{mid.z, mid.w});
-        C[r][3] = unpack_h4(crow[xr]);
-        D[r][0] = drow[xl];
-        D[r][1] = dmid.x;
-        D[r][2] = dmid.y;
-        D[r][3] = drow[xr];
-    }
-    const int colx[4] = {xl, x0, x0 + 1, xr};
-    uint2 outp[2];
-    const float v = centre_uv(y, H);
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const int x = x0 + k;
-        const float u = centre_uv(x, W);
-        f4 nb5 = f4{0, 0, 0, 0}, blurred = f4{0, 0, 0, 0};
-        f4 mn = f4{10.0e5f, 10.0e5f, 10.0e5f, 10.0e5f}, mx = f4{-10.0e5f, -10.0e5f, -10.0e5f, -10.0e5f};
-        float closest = 1.0f;
-        int bx = x, by = y;
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-            const int oy = 1 - r;
-#pragma unroll
-            for (int ox = 1; ox > -2; --ox) {
-                const int idx = (oy + 1) * 3 + (ox + 1);
-                const int c = k + 1 + ox;              // column slot of x + ox
-                // pixel x0+1 at the right edge: its +1 neighbour clamps to itself
-                const f4 cc = (k == 1 && ox == 1 && x0 + 2 > W - 1) ? C[r][2] : C[r][c];
-                const float d = (k == 1 && ox == 1 && x0 + 2 > W - 1) ? D[r][2] : D[r][c];
-                const int sx = (k == 1 && ox == 1 && x0 + 2 > W - 1) ? x0 + 1 : colx[c];
-                closest = fminf(d, closest);
-                if (closest == d) { bx = sx; by = rows[r]; }
-                mn = min4(cc, mn);
-                mx = max4(cc, mx);
-                const float gw = gauss_w(idx);
-                blurred = f4{blurred.x + gw * cc.x, blurred.y + gw * cc.y, blurred.z + gw * cc.z, blurred.w + gw * cc.w};
-                if (idx == 5) nb5 = cc;
-            }
-        }
-        const f4 vv = fetch_h4(vel, bx, by);
-        outp[k] = pack_h4(resolve_pairs(p, u, v, nb5, mn, mx, blurred, float2{vv.x, vv.y}, prev, pvel));
-    }
-    row_ptr_w<uint4>(target, y)[x0 >> 1] = uint4{outp[0].x, outp[0].y, outp[1].x, outp[1].y};
-    if (vel_out.data) row_ptr_w<uint4>(vel_out, y)[x0 >> 1] = row_ptr<uint4>(vel, y)[x0 >> 1];
-}
-
 // ---- two pixels per lane, reduced instruction count (the pass is VALU-issue bound on gfx950) ----
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 typedef float v2f __attribute__((ext_vector_type(2)));
