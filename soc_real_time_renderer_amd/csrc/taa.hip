@@ -228,9 +228,9 @@ __global__ __launch_bounds__(256) void taa_pair2(DImg target, DImg cur, DImg pre
         const int x = x0 + k;
         const float u = centre_uv(x, W);
         // closest depth in the reference order (oy = +1..-1, ox = +1..-1), last equal wins
+        // the winning tap as one index r * 4 + c (one select per tap instead of two)
         float closest = 1.0f;
-        int bc = k + 1, br = 1;
-        bool first = true;
+        int bi = 4 + k + 1;
 #pragma unroll
         for (int r = 0; r < 3; ++r)
 #pragma unroll
@@ -238,11 +238,9 @@ __global__ __launch_bounds__(256) void taa_pair2(DImg target, DImg cur, DImg pre
                 const int c = k + 1 + ox;
                 const float d = D[r][c];
                 closest = fminf(d, closest);
-                const bool take = closest == d;
-                if (first) { bc = take ? c : bc; br = take ? r : br; first = false; }
-                else { bc = take ? c : bc; br = take ? r : br; }
+                bi = closest == d ? r * 4 + c : bi;
             }
-        const int bx = colx[bc], by = rows[br];
+        const int bx = colx[bi & 3], by = rows[bi >> 2];
         const h2 mnxy = __builtin_elementwise_min(__builtin_elementwise_min(nxy[k], nxy[k + 1]), nxy[k + 2]);
         const h2 mnzw = __builtin_elementwise_min(__builtin_elementwise_min(nzw[k], nzw[k + 1]), nzw[k + 2]);
         const h2 mxxy = __builtin_elementwise_max(__builtin_elementwise_max(xxy[k], xxy[k + 1]), xxy[k + 2]);
