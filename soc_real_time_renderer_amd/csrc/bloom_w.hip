@@ -144,7 +144,7 @@ __global__ __launch_bounds__(256) void bloomw_down01(DImg E, DImg M1, int swz) {
     __shared__ uint2 mt[W1_MH][W1_MW];
     const int tid = threadIdx.x;
     int tbx, tby;
-    xcd_tile(swz, tbx, tby);   // swz: XCD-aware order (neighbouring tiles share an XCD's L2 for their halos)
+    xcd_order(swz, tbx, tby);   // swz: XCD-aware order (neighbouring tiles share an XCD's L2 for their halos)
     const int X0 = tbx * W1_OW, Y0 = tby * W1_OH;
     const int mx0 = 2 * X0 - 2, my0 = 2 * Y0 - 2, ex0 = mx0 - 2, ey0 = my0 - 2;
     load_tile<W1_EW, W1_EH>(E, ex0, ey0, et, tid);
@@ -172,7 +172,7 @@ __global__ __launch_bounds__(256) void bloomw_down23(DImg S1, DImg M3, int W2, i
     __shared__ uint2 mt[W2_MH][W2_MW];
     const int tid = threadIdx.x;
     int tbx, tby;
-    xcd_tile(swz, tbx, tby);   // swz: XCD-aware order (neighbouring tiles share an XCD's L2 for their halos)
+    xcd_order(swz, tbx, tby);   // swz: XCD-aware order (neighbouring tiles share an XCD's L2 for their halos)
     const int X0 = tbx * W2_OW, Y0 = tby * W2_OH;
     const int mx0 = 2 * X0 - 2, my0 = 2 * Y0 - 2, sx0 = 2 * mx0 - 2, sy0 = 2 * my0 - 2;
     load_tile<W2_SW, W2_SH>(S1, sx0, sy0, st, tid);
@@ -228,7 +228,7 @@ __global__ __launch_bounds__(256) void bloomw_up32(DImg S3, DImg M1, int W2, int
     __shared__ uint2 mt[W3_MH][W3_MW];
     const int tid = threadIdx.x;
     int tbx, tby;
-    xcd_tile(swz, tbx, tby);   // swz: XCD-aware order (neighbouring tiles share an XCD's L2 for their halos)
+    xcd_order(swz, tbx, tby);   // swz: XCD-aware order (neighbouring tiles share an XCD's L2 for their halos)
     const int X0 = tbx * U_OW, Y0 = tby * U_OH;
     const int mx0 = X0 / 2 - 2, my0 = Y0 / 2 - 2;       // even
     const int sx0 = mx0 / 2 - 2, sy0 = my0 / 2 - 2;     // mx0 / 2 = floor since mx0 is even
@@ -262,7 +262,7 @@ __global__ __launch_bounds__(256) void bloomw_up10(DImg S1, DImg O, bool vec, in
     __shared__ uint2 mt[W4_MH][W4_MW + 2];   // +2: the pair loop writes whole pairs
     const int tid = threadIdx.x;
     int tbx, tby;
-    xcd_tile(swz, tbx, tby);   // swz: XCD-aware order (neighbouring tiles share an XCD's L2 for their halos)
+    xcd_order(swz, tbx, tby);   // swz: XCD-aware order (neighbouring tiles share an XCD's L2 for their halos)
     const int X0 = tbx * U_OW, Y0 = tby * U_OH;
     const int mx0 = X0 - 1, my0 = Y0 - 1;
     const int sx0 = X0 / 2 - 3, sy0 = Y0 / 2 - 3;

@@ -165,8 +165,7 @@ __global__ __launch_bounds__(256) void composition_pair(DImg target, DImg albedo
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (HIST) reinterpret_cast<uint4*>(sh + wave * kBins)[lane] = uint4{0u, 0u, 0u, 0u};
     int bx, by;
-    if (p.swz >= 2) xcd_tile_strips(p.swz, bx, by);   // SOC_SWZ_COMP >= 2: XCD band/strip order
-    else xcd_tile(p.swz, bx, by);
+    xcd_order(p.swz, bx, by);
     const int x = bx * 32 + (wave & 1) * 16 + (lane & 7) * 2;
     const int y = by * 16 + (wave >> 1) * 8 + (lane >> 3);
     const bool inside = x < target.w && y < target.h;

@@ -255,6 +255,29 @@ __device__ __forceinline__ void xcd_tile_strips(int strip, int& tx, int& ty) {
     ty = band * B + ly;
 }
 
+// XCD-aware order in vertical bands: the tiles are enumerated in column strips of `strip` tiles over the
+// full image height (left to right, each strip row by row); XCD k takes the k-th contiguous eighth, i.e. a
+// vertical band of about gx / 8 tile columns. Every XCD then sees the same mix of rows (a sky band at the
+// top of the frame no longer idles whole XCDs, as the horizontal bands of xcd_tile_strips do), and its
+// workgroups in flight still cover a compact strip. A bijection.
+__device__ __forceinline__ void xcd_tile_vbands(int strip, int& tx, int& ty) {
+    const int gx = (int)gridDim.x, gy = (int)gridDim.y, n = gx * gy;
+    const int id = (int)(blockIdx.y * gridDim.x + blockIdx.x);
+    const int q = n >> 3, r = n & 7, k = id & 7;
+    const int i = k * q + min(k, r) + (id >> 3);   // position in the strip sequence
+    const int s = i / (strip * gy), in = i - s * strip * gy;
+    const int w = min(strip, gx - s * strip);
+    const int ly = in / w;
+    tx = s * strip + (in - ly * w);
+    ty = ly;
+}
+// swz: 0 row-major, 1 contiguous eighths, >= 2 horizontal bands of `swz`-tile strips, <= -2 vertical bands.
+__device__ __forceinline__ void xcd_order(int swz, int& tx, int& ty) {
+    if (swz >= 2) xcd_tile_strips(swz, tx, ty);
+    else if (swz <= -2) xcd_tile_vbands(-swz, tx, ty);
+    else xcd_tile(swz, tx, ty);
+}
+
 // Pixel-centre uv exactly as the oracle computes it: (x + 0.5) / n, correctly rounded.
 __device__ __forceinline__ float centre_uv(int x, int n) { return ((float)x + 0.5f) / (float)n; }
 

@@ -20,7 +20,7 @@ struct SsaoParams {
     float radius, bias, kernel_size_f;
     int ksize;     // loop bound, min(kernel_size, 26)
     int noise_w;   // textureSize(u_normal_image).x
-    int swz;       // XCD-aware tile order (tuning knob SOC_SWZ_SSAO; 0 = row-major)
+    int swz;       // XCD-aware tile order (tuning knob SOC_SWZ_SSAO, see xcd_order; 0 = row-major)
 };
 
 // ssao_generation.inl:139-141 (no FMA contraction: keeps the sin argument as the oracle's)
@@ -103,8 +103,7 @@ template <bool TABLE, bool SPARSE_IP, bool FULL>
 __global__ __launch_bounds__(256) void ssao_kernel(DImg depth, DImg normal, DImg target, const float2* __restrict__ table,
                                                    SsaoParams p) {
     int bx, by;
-    if (p.swz >= 2) xcd_tile_strips(p.swz, bx, by);   // SOC_SWZ_SSAO >= 2: strip width in tiles
-    else xcd_tile(p.swz, bx, by);
+    xcd_order(p.swz, bx, by);
     const int tid = threadIdx.x;
     const int x = bx * 32 + (tid & 31), y = by * 8 + (tid >> 5);
     if (x >= target.w || y >= target.h) return;
@@ -217,7 +216,7 @@ SsaoParams make_params(const soc_globals* g, const soc_img& normal) {
     p.kernel_size_f = (float)g->ssao_kernel_size;
     p.ksize = g->ssao_kernel_size < SOC_SSAO_MAX_KERNEL ? g->ssao_kernel_size : SOC_SSAO_MAX_KERNEL;
     p.noise_w = normal.width;
-    p.swz = tuning_knob("SOC_SWZ_SSAO", 16);   // XCD band/strip order: HBM traffic 3.3x -> 1.3x algorithmic
+    p.swz = tuning_knob("SOC_SWZ_SSAO", -16);   // XCD vertical bands: HBM traffic 3.3x -> 1.25x algorithmic
     return p;
 }
 

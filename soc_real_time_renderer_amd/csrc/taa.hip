@@ -149,8 +149,7 @@ template <bool TM, int NBR = 2>
 __global__ __launch_bounds__(256) void taa_pair2(DImg target, DImg cur, DImg prev, DImg vel, DImg pvel, DImg depth,
                                                  DImg vel_out, TaaParams p, TmOut tm) {
     int tbx, tby;
-    if (p.swz >= 2) xcd_tile_strips(p.swz, tbx, tby);   // SOC_SWZ_TAA >= 2: XCD band/strip order
-    else xcd_tile(p.swz, tbx, tby);
+    xcd_order(p.swz, tbx, tby);
     const int x0 = NBR == 2 ? (tbx * 62 + (int)threadIdx.x - 1) * 2 : (tbx * (int)blockDim.x + threadIdx.x) * 2;
     const int y = tby * (int)blockDim.y + threadIdx.y;
     const bool halo = NBR == 2 && (threadIdx.x == 0 || threadIdx.x == 63);
@@ -360,7 +359,7 @@ int taa_launch(const soc_globals* g, soc_img target, soc_img current_color, soc_
     p.pox = 1.0f / (float)g->resolution[0];
     p.poy = 1.0f / (float)g->resolution[1];
     p.accum0 = fminf(0.1f, (float)g->frame_counter);
-    p.swz = tuning_knob("SOC_SWZ_TAA", 16);   // XCD band/strip order: HBM traffic 1.39x -> 1.01x algorithmic
+    p.swz = tuning_knob("SOC_SWZ_TAA", -16);   // XCD vertical bands: HBM traffic 1.39x -> 1.01x algorithmic
     const int W = target.width, H = target.height;
     auto same = [&](const soc_img& im) { return im.width == W && im.height == H; };
     const bool fast = W == g->resolution[0] && H == g->resolution[1] && same(current_color) && same(depth) &&
