@@ -194,11 +194,12 @@ def test_ssao_noise_table_is_bit_identical(soc):
 
 @pytest.mark.parametrize("W,H", [(97, 55), (1920, 1080)])
 def test_ssao_tile_orders_bit_identical(soc, monkeypatch, W, H):
-    """Every workgroup order (row-major, XCD-aware, XCD band/strip: SOC_SWZ_SSAO) computes each pixel the same way."""
+    """Every workgroup order (row-major, XCD-aware eighths, horizontal and vertical XCD bands: SOC_SWZ_SSAO) computes
+    each pixel the same way (the orders are bijections, also for ragged grids)."""
     g, gb = sponza_inputs(W, H)
     depth, normal = dev(gb["depth"]), dev(gb["normal"])
     outs = []
-    for swz in ("0", "1", "4", "16"):
+    for swz in ("0", "1", "4", "16", "-16", "-3"):
         monkeypatch.setenv("SOC_SWZ_SSAO", swz)
         soc.reload_tuning()
         out = torch.zeros(H // 2, W // 2, dtype=torch.uint8, device=DEV)
