@@ -109,12 +109,19 @@ __global__ __launch_bounds__(256) void ssao_kernel(DImg depth, DImg normal, DImg
     if (x >= target.w || y >= target.h) return;
     const float u = centre_uv(x, target.w), v = centre_uv(y, target.h);
 
+    // normal = mat3(view) * normalize(texture(normal, uv).rgb), :178
+    const f4 nn = sample_h4(normal, u, v);
+    // A zero normal (the G-buffer's clear value: sky) normalises to NaN; every sample's s.z + bias is then NaN,
+    // no comparison adds occlusion, and the result is 1 - 0 / kernel_size = 255 whatever the taps read. Write
+    // it without the 26 taps (the same bits as the full evaluation).
+    if (nn.x == 0.0f && nn.y == 0.0f && nn.z == 0.0f && p.kernel_size_f != 0.0f) {   // (0 / 0 would be NaN -> 0)
+        row_ptr_w<uint8_t>(target, y)[x] = 255;
+        return;
+    }
     // frag_position = get_view_position_from_depth(in_uv, depth), :177
     const float d = depth_tap(depth, u, v);
     f4 vp = mul(p.inv_proj, f4{u * 2.0f - 1.0f, v * 2.0f - 1.0f, d, 1.0f});
     const f3 frag = f3{vp.x / vp.w, vp.y / vp.w, vp.z / vp.w};
-    // normal = mat3(view) * normalize(texture(normal, uv).rgb), :178
-    f4 nn = sample_h4(normal, u, v);
     const f3 n = mul3of4(p.view, normalize3(f3{nn.x, nn.y, nn.z}));
 
     float2 rv2 = TABLE ? table[(size_t)y * target.w + x] : ssao_random_vec(u, v, p.noise_w);
