@@ -340,16 +340,18 @@ def test_generate_mips_bit_exact(soc, oracle, W, H, srgb):
         assert np.array_equal(a, b), (k, (a != b).mean())
 
 
-def test_sponza_mesh_mipmapped_gbuffer_vs_oracle(soc, oracle):
+@pytest.mark.parametrize("tex", [128, 96])
+def test_sponza_mesh_mipmapped_gbuffer_vs_oracle(soc, oracle, tex):
     """GBufferGeneration with the reference's sampler (mip chains, trilinear, anisotropy 16; texture.cpp:121-136)
     on the Sponza-proxy mesh: G-buffer within the RGBA16F tolerance of the oracle's restatement, and the mip path
-    really engaged (the albedo differs from the level-0 sampling on a share of the pixels)."""
+    really engaged (the albedo differs from the level-0 sampling on a share of the pixels). 96^2 textures take the
+    non-power-of-two REPEAT path and a chain with odd levels (96 48 24 12 6 3 1)."""
     W, H = 320, 180
     g = globals_for(W, H)
     hm, dm = _mesh_scene()
-    mats_h, keep_h = raster.sponza_mesh_materials(128, mips=True, host_mip_generator=oracle.generate_mips)
-    mats_l0, _ = raster.sponza_mesh_materials(128)
-    mats_d, keep_d = raster.sponza_mesh_materials(128, DEV, mips=True)
+    mats_h, keep_h = raster.sponza_mesh_materials(tex, mips=True, host_mip_generator=oracle.generate_mips)
+    mats_l0, _ = raster.sponza_mesh_materials(tex)
+    mats_d, keep_d = raster.sponza_mesh_materials(tex, DEV, mips=True)
     dmats = raster.materials_device(mats_d)
     vp = np.ctypeslib.as_array(g.camera_projection_view_matrix)
     vis_ref = np.zeros((H, W), np.uint64)

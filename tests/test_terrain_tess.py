@@ -54,3 +54,19 @@ def test_ramp_height_monotone_and_winding():
     ny = np.cross(b - a, c - a)[:, 1]
     assert (ny > 0).all()          # counter-clockwise seen from above: the normal points up
     assert tri.max() == nv * nv - 1 and len(np.unique(tri)) == nv * nv
+
+
+def test_offset_and_scale():
+    """terrain_offset / terrain_scale / terrain_height_scale / terrain_midpoint as the vertex shader applies them
+    (draw_terrain.inl:141, 188-190): x = u sx - ox, y = oy + (h - mid) hs, z = v sz - oz."""
+    g = globals_for(64, 64)
+    g.terrain_offset[:] = [10.0, 2.0, -5.0]
+    g.terrain_scale[:] = [50.0, 80.0]
+    g.terrain_height_scale = 30.0
+    g.terrain_midpoint = 0.25
+    hm = np.full((16, 16, 4), 51, np.uint8)   # 0.2
+    m = tess(g, hm, grid=5, n=3)
+    p, uv = m["positions"], m["uvs"]
+    assert np.allclose(p[:, 0], uv[:, 0] * 50.0 - 10.0, atol=1e-5)
+    assert np.allclose(p[:, 2], uv[:, 1] * 80.0 + 5.0, atol=1e-5)
+    assert np.allclose(p[:, 1], 2.0 + (np.float32(51 / 255) - 0.25) * 30.0, atol=1e-5)
