@@ -90,6 +90,14 @@ __device__ __forceinline__ uint32_t quad_bilerp_u(uint2 q, uint32_t wxp, uint32_
     return udot2(udot2(q.x, wxp) | (udot2(q.y, wxp) << 16), wyp);
 }
 
+// (int)floorf(x) as one v_cvt_flr_i32_f32 (the compiler emits v_floor_f32 + v_cvt_i32_f32); the same value for
+// every finite x in the int range, which the noise coordinates (|x| < 2^24) are.
+__device__ __forceinline__ int floor_to_int(float x) {
+    int r;
+    asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+
 // get_3d_noise, :219-233
 template <typename Q>
 __device__ __forceinline__ float noise3(const CtxT<Q>& cx, f3 pos) {
@@ -98,8 +106,8 @@ __device__ __forceinline__ float noise3(const CtxT<Q>& cx, f3 pos) {
     // fixed-point texel coordinate of the first tap: (u 64 - 0.5) 256 + 0.5 with u = pos.x / 64 + p 17/64,
     // i.e. 256 pos.x + 4352 p - 127.5 (one rounding instead of four; within the pass tolerance)
     const float base = __builtin_fmaf(p, 4352.0f, -127.5f);
-    const int fx = (int)floorf(__builtin_fmaf(pos.x, 256.0f, base));
-    const int fy = (int)floorf(__builtin_fmaf(pos.y, 256.0f, base));
+    const int fx = floor_to_int(__builtin_fmaf(pos.x, 256.0f, base));
+    const int fy = floor_to_int(__builtin_fmaf(pos.y, 256.0f, base));
     const uint32_t wx = (uint32_t)fx & 255u, wy = (uint32_t)fy & 255u;
     const uint32_t wxp = wx * 65535u + 256u, wyp = wy * 65535u + 256u;
     const uint32_t ix = ((uint32_t)fx >> 8) & kNoiseMask, iy = ((uint32_t)fy >> 8) & kNoiseMask;
