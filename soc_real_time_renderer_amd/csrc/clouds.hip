@@ -114,8 +114,9 @@ __device__ __forceinline__ float noise3(const CtxT<Q>& cx, f3 pos) {
     const Q* t = cx.quads + (iy * (uint32_t)kTW + ix);
     const Q q0 = t[0], q1 = t[kTap2 * kTW + kTap2];
     const float a = (float)quad_bilerp_u(q0, wxp, wyp), b = (float)quad_bilerp_u(q1, wxp, wyp);
-    return __builtin_fmaf(f, b - a, a) * (1.0f / (255.0f * 65536.0f));
+    return __builtin_fmaf(f, b - a, a);   // x 1 / (255 65536) = the noise value; the caller folds it into the octave weight
 }
+constexpr float kNoiseNorm = 1.0f / (255.0f * 65536.0f);
 
 // |v| with the hardware square root (1 ulp). Every length in this pass is an Earth-scale distance
 // (|v| ~ 6.4e6 m, ulp 0.5 m), far from the denormal range the full-precision sequence guards.
@@ -134,12 +135,16 @@ __device__ float clouds_at(const C& cx, f3 p, float h) {
     p = f3{p.x + cx.cam_x, h, p.z + cx.cam_z};
     const f3 mv = f3{cx.time, 0.0f, cx.time};
     const f3 cc = p * 0.001f + mv;
-    float n = noise3(cx, cc) * 0.5f;
-    n += noise3(cx, cc * 2.0f + mv) * 0.25f;
+    // octave weight x noise normalisation as one constant per octave (powers of two apart: one fma per octave)
+    float n = noise3(cx, cc) * (0.5f * kNoiseNorm);
+    n = __builtin_fmaf(noise3(cx, cc * 2.0f + mv), 0.25f * kNoiseNorm, n);
     if (n < 0.55f - 0.1875f - 1e-4f) return 0.0f;
-    n += noise3(cx, cc * 7.0f - mv) * 0.125f;
+    n = __builtin_fmaf(noise3(cx, cc * 7.0f - mv), 0.125f * kNoiseNorm, n);
     if (n < 0.55f - 0.0625f - 1e-4f) return 0.0f;
-    n += noise3(cx, (cc + mv) * 16.0f) * 0.0625f;
+    // (cc + mv) 16 == fma(cc, 16, 16 mv) exactly: scaling by a power of two commutes with the rounding
+    const f3 c4 = f3{__builtin_fmaf(cc.x, 16.0f, mv.x * 16.0f), __builtin_fmaf(cc.y, 16.0f, mv.y * 16.0f),
+                     __builtin_fmaf(cc.z, 16.0f, mv.z * 16.0f)};
+    n = __builtin_fmaf(noise3(cx, c4), 0.0625f * kNoiseNorm, n);
     const float hh = p.y - kMinH;
     const float th = (1.0f - __expf(-0.01f * hh)) * __expf(-0.004f * hh);
     const float t = clampf((n - 0.55f) * (1.0f / (0.6f - 0.55f)), 0.0f, 1.0f);
