@@ -227,11 +227,13 @@ struct MarchShade {
     float phase;
     f3 skyl;   // sky * 0.25 / pi
 };
-__device__ __forceinline__ MarchShade march_shade(f3 dir, f3 sun) {
+// skyl depends on the sun only: sky_light(sun) once per thread, then march_shade per pixel (same bits).
+__device__ __forceinline__ f3 sky_light(f3 sun) { return scattering_top(sun) * 0.25f * (1.0f / kPi); }
+__device__ __forceinline__ MarchShade march_shade(f3 dir, f3 sun, f3 skyl) {
     const float x = dot3(sun, dir);
     MarchShade m;
     m.phase = mixf(hg_phase(x, -0.5f * 0.8f), hg_phase(x, 0.8f * 0.8f), 0.5f);
-    m.skyl = scattering_top(sun) * 0.25f * (1.0f / kPi);
+    m.skyl = skyl;
     return m;
 }
 
@@ -268,7 +270,7 @@ __device__ __forceinline__ f3 march_finish(const MarchGeom& mg, f3 color, f3 sca
 __device__ f3 volumetric_clouds(const Ctx& cx, f3 dir, f3 sun, f3 color, float dither, f3 sun_color) {
     if (dir.y < 0.0f) return color;
     const MarchGeom mg = march_geometry(dir);
-    const MarchShade ms = march_shade(dir, sun);
+    const MarchShade ms = march_shade(dir, sun, sky_light(sun));
     f3 scattering = f3{0.0f, 0.0f, 0.0f};
     float transmittance = 1.0f;
     for (int i = 0; i < 24; i++) {
@@ -671,6 +673,7 @@ __global__ __launch_bounds__(256) void clouds_resolve(DImg noise, DImg target, C
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (blockIdx.x * 256u >= count) return;
     const f3 sun = f3{p.sun[0], p.sun[1], p.sun[2]}, sun_color = f3{0.8f, 0.8f, 0.8f};
+    const f3 skyl = sky_light(sun);
     uint32_t dummy = 0;
     for (uint32_t first = blockIdx.x * 256u; first < count; first += gridDim.x * 256u) {
         const uint32_t i = first + tid;
@@ -712,7 +715,7 @@ __global__ __launch_bounds__(256) void clouds_resolve(DImg noise, DImg target, C
             if (march) {
                 const float4 g0 = pb.geom[2 * i], g1 = pb.geom[2 * i + 1];
                 mg = MarchGeom{f3{g0.x, g0.y, g0.z}, f3{g1.x, g1.y, g1.z}, g1.w};
-                ms = march_shade(dir, sun);
+                ms = march_shade(dir, sun, skyl);
             }
             f3 scattering = f3{0.0f, 0.0f, 0.0f};
             float transmittance = 1.0f;
