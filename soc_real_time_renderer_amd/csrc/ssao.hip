@@ -140,10 +140,15 @@ __global__ __launch_bounds__(256) void ssao_kernel(DImg depth, DImg normal, DImg
         return Aff{m0 * frag.x + m1 * frag.y + m2 * frag.z + m3, m0 * tr.x + m1 * tr.y + m2 * tr.z,
                    m0 * br.x + m1 * br.y + m2 * br.z, m0 * nr.x + m1 * nr.y + m2 * nr.z};
     };
-    const Aff ax = proj_aff(0, 0.5f * (float)W), ay = proj_aff(1, 0.5f * (float)H), aw = proj_aff(3, 1.0f);
+    // SPARSE_IP: the x / y forms carry the sub-texel scale 256 (exact: a power of two) and the +0.5 of the rounding,
+    // so a tap's fixed-point coordinate is one fma + clamp (the texel coordinate itself is not needed)
+    const float fxs = SPARSE_IP ? 256.0f : 1.0f;
+    const Aff ax = proj_aff(0, 0.5f * (float)W * fxs), ay = proj_aff(1, 0.5f * (float)H * fxs), aw = proj_aff(3, 1.0f);
     const Aff az = Aff{frag.z + p.bias, tr.z, br.z, nr.z};     // s.z + bias
     const float cx0 = 0.5f * (float)(W - 1), cy0 = 0.5f * (float)(H - 1);
     const float tmax_x = (float)(W - 1) - 1.0f / 256.0f, tmax_y = (float)(H - 1) - 1.0f / 256.0f;
+    const float cx0s = cx0 * 256.0f + 0.5f, cy0s = cy0 * 256.0f + 0.5f;
+    const float fmax_x = tmax_x * 256.0f + 0.5f, fmax_y = tmax_y * 256.0f + 0.5f;
     const int pitch = depth.pitch;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(depth.data, 0, pitch * H, 0x00020000);
     float occ = 0.0f;
@@ -152,13 +157,20 @@ __global__ __launch_bounds__(256) void ssao_kernel(DImg depth, DImg normal, DImg
         if (FULL || i < p.ksize) {
             const float kx = kKernel.v[i][0], ky = kKernel.v[i][1], kz = kKernel.v[i][2];
             const float rw = fast_rcp(aff(aw, kx, ky, kz));
-            float tx = __builtin_fmaf(aff(ax, kx, ky, kz), rw, cx0);
-            float ty = __builtin_fmaf(aff(ay, kx, ky, kz), rw, cy0);
-            tx = __builtin_amdgcn_fmed3f(tx, 0.0f, tmax_x);   // clamp: one v_med3, no NaN quieting
-            ty = __builtin_amdgcn_fmed3f(ty, 0.0f, tmax_y);
-            // t >= 0, so truncation is the floor
-            const int fx = (int)__builtin_fmaf(tx, 256.0f, 0.5f);
-            const int fy = (int)__builtin_fmaf(ty, 256.0f, 0.5f);
+            float tx = 0.0f, ty = 0.0f;
+            int fx, fy;
+            if (SPARSE_IP) {   // 256 t + 0.5 directly, clamped to [0.5, 256 tmax + 0.5]; >= 0, so truncation floors
+                fx = (int)__builtin_amdgcn_fmed3f(__builtin_fmaf(aff(ax, kx, ky, kz), rw, cx0s), 0.5f, fmax_x);
+                fy = (int)__builtin_amdgcn_fmed3f(__builtin_fmaf(aff(ay, kx, ky, kz), rw, cy0s), 0.5f, fmax_y);
+            } else {
+                tx = __builtin_fmaf(aff(ax, kx, ky, kz), rw, cx0);
+                ty = __builtin_fmaf(aff(ay, kx, ky, kz), rw, cy0);
+                tx = __builtin_amdgcn_fmed3f(tx, 0.0f, tmax_x);   // clamp: one v_med3, no NaN quieting
+                ty = __builtin_amdgcn_fmed3f(ty, 0.0f, tmax_y);
+                // t >= 0, so truncation is the floor
+                fx = (int)__builtin_fmaf(tx, 256.0f, 0.5f);
+                fy = (int)__builtin_fmaf(ty, 256.0f, 0.5f);
+            }
             const float wx = (float)(fx & 255) * (1.0f / 256.0f), wy = (float)(fy & 255) * (1.0f / 256.0f);
             const int off = __mul24(fy >> 8, pitch) + (fx >> 8) * 4;
             const f2a4 r0 = __builtin_bit_cast(f2a4, __builtin_amdgcn_raw_buffer_load_b64(rsrc, off, 0, 0));
