@@ -35,6 +35,7 @@ struct CloudParams {
     float sun[3];      // -sun_info.direction
     float cam[3];
     float res_x_m1, res_y_m1;  // resolution - 1
+    float r_res_x_m1, r_res_y_m1;  // recip_rn(resolution - 1) for the ray uv x / (W - 1) (div_rn)
     float elapsed;
     float sun_factor;  // max(min(|sun.x|, |sun.z|) + sun.y, 0)
     int res_x, res_y;
@@ -337,7 +338,7 @@ constexpr int TX = 16, TY = 16;
 
 // View ray of pixel (x, y): main(), :445-452 (ray_uv = pixel / (resolution - 1), not texel centres).
 __device__ __forceinline__ f3 sky_dir(const CloudParams& p, int x, int y) {
-    const float ru = (float)x / p.res_x_m1, rv = (float)y / p.res_y_m1;
+    const float ru = div_rn((float)x, p.res_x_m1, p.r_res_x_m1), rv = div_rn((float)y, p.res_y_m1, p.r_res_y_m1);
     const float ndx = ru * 2.0f - 1.0f, ndy = rv * 2.0f - 1.0f;
     const f4 rvs = mul(p.inv_proj, f4{ndx, ndy, -1.0f, 0.0f});
     const f4 rws = mul(p.inv_view, f4{rvs.x, rvs.y, -1.0f, 0.0f});
@@ -400,7 +401,8 @@ __device__ __forceinline__ void stage_noise_wide(const DImg& noise, uint2* quads
 }
 
 __device__ __forceinline__ bool is_sky(const CloudParams& p, const DImg& depth, int x, int y) {
-    return sample_f32(depth, (float)x / p.res_x_m1, (float)y / p.res_y_m1) == 1.0f;   // textureLod(depth, ray_uv, 0), :458
+    return sample_f32(depth, div_rn((float)x, p.res_x_m1, p.r_res_x_m1), div_rn((float)y, p.res_y_m1, p.r_res_y_m1)) ==
+           1.0f;   // textureLod(depth, ray_uv, 0), :458
 }
 
 // Single-kernel path (no workspace): 16x16 tiles, a tile without sky exits after its depth test.
@@ -441,8 +443,9 @@ __global__ __launch_bounds__(256) void clouds_classify(DImg depth, DImg target, 
     if (y < H) {
         // all 16 depth loads issued together (clamped coordinates, no per-pixel branch)
         float d[4];
+        const float ray_v = div_rn((float)y, p.res_y_m1, p.r_res_y_m1);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) d[k] = sample_f32(depth, (float)min(x0 + k, W - 1) / p.res_x_m1, (float)y / p.res_y_m1);
+        for (int k = 0; k < 4; ++k) d[k] = sample_f32(depth, div_rn((float)min(x0 + k, W - 1), p.res_x_m1, p.r_res_x_m1), ray_v);
 #pragma unroll
         for (int k = 0; k < 4; ++k)
             if (x0 + k < W && d[k] == 1.0f) mask |= 1u << k;
@@ -820,6 +823,8 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
     p.res_y = g->resolution[1];
     p.res_x_m1 = (float)g->resolution[0] - 1.0f;
     p.res_y_m1 = (float)g->resolution[1] - 1.0f;
+    p.r_res_x_m1 = recip_rn(g->resolution[0] - 1);
+    p.r_res_y_m1 = recip_rn(g->resolution[1] - 1);
     p.elapsed = g->elapsed_time;
     p.sun_factor = fmaxf(fminf(fabsf(p.sun[0]), fabsf(p.sun[2])) + p.sun[1], 0.0f);
     const int W = std::min(target.width, p.res_x), H = std::min(target.height, p.res_y);

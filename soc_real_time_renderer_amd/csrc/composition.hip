@@ -32,6 +32,7 @@ struct CompParams {
     BinFast bf;            // lum_bin_fast parameters
     const soc_globals* __restrict__ dg;  // device globals (lights), may be null when npl == nsl == 0
     int sky_external;      // 1: sky pixels (depth == 1) are written and binned by sky_compose_pair (second lane)
+    float rw, rh;          // recip_rn(target extent) for the pixel-centre uv (div_rn)
 };
 
 __device__ __forceinline__ float fast_pow(float x, float y) {
@@ -176,7 +177,7 @@ __global__ __launch_bounds__(256) void composition_pair(DImg target, DImg albedo
     const BufImg bd = buf_img(depth), ba = buf_img(albedo), be = buf_img(emissive), bn = buf_img(normal);
     const BufImg bt = buf_img(target), bs = buf_img(shadow), bo = buf_img(ssao);
     if (inside) {
-        const float v = centre_uv(y, target.h);
+        const float v = centre_uv_rn(y, target.h, p.rh);
         // once-read streams non-temporal (NT & 1: keep L2 for the shadow-map / AO gathers); aux bit 1 = nt
         constexpr int ld_aux = (NT & 1) ? 2 : 0;
         const float2 d2 = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(bd.r, buf_row(bd, y) + x * 4, 0, ld_aux));
@@ -185,7 +186,7 @@ __global__ __launch_bounds__(256) void composition_pair(DImg target, DImg albedo
         const uint4 n4 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(bn.r, buf_row(bn, y) + x * 8, 0, ld_aux));
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
-            const float u = centre_uv(x + k, target.w);
+            const float u = centre_uv_rn(x + k, target.w, p.rw);
             const float d = k ? d2.y : d2.x;
             const f4 al = unpack_h4(k ? uint2{a4.z, a4.w} : uint2{a4.x, a4.y});
             const f4 em = unpack_h4(k ? uint2{e4.z, e4.w} : uint2{e4.x, e4.y});
@@ -342,6 +343,8 @@ int composition_launch(const soc_globals* g, const soc_globals* d_globals, soc_i
     p.nsl = g->spot_light_count < SOC_MAX_SPOT_LIGHTS ? g->spot_light_count : SOC_MAX_SPOT_LIGHTS;
     p.dg = d_globals;
     p.swz = tuning_knob("SOC_SWZ_COMP", 0);
+    p.rw = recip_rn(target.width);
+    p.rh = recip_rn(target.height);
     p.bins = nullptr;
     p.sky_external = 0;
     if ((p.npl || p.nsl) && !d_globals)

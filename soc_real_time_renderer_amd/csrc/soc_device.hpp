@@ -281,4 +281,14 @@ __device__ __forceinline__ void xcd_order(int swz, int& tx, int& ty) {
 // Pixel-centre uv exactly as the oracle computes it: (x + 0.5) / n, correctly rounded.
 __device__ __forceinline__ float centre_uv(int x, int n) { return ((float)x + 0.5f) / (float)n; }
 
+// a / n correctly rounded without the IEEE division sequence, given rn = RN(1 / n) (host: recip_rn): one multiply and
+// two fmas (Markstein's correction step). tools/check_div_rn.c verifies it exhaustively against the division for
+// every a = x + 0.5 (x < n) and a = x (x <= n), n <= 16384; for larger n the host passes rn = 0 and the division runs.
+__device__ __forceinline__ float div_rn(float a, float n, float rn) {
+    if (rn == 0.0f) return a / n;   // wave-uniform
+    const float q = a * rn;
+    return __builtin_fmaf(__builtin_fmaf(-q, n, a), rn, q);
+}
+__device__ __forceinline__ float centre_uv_rn(int x, int n, float rn) { return div_rn((float)x + 0.5f, (float)n, rn); }
+
 }  // namespace soc

@@ -50,6 +50,8 @@ inline hipStream_t hs(soc_stream s) { return reinterpret_cast<hipStream_t>(s); }
 // Integer tuning knob from the environment (`dflt` when unset). Read at every launch (a getenv scan,
 // ~0.1 us), so A/B runs and the variant-identity tests can switch it between calls.
 int tuning_knob(const char* name, int dflt);
+// RN(1 / n) for div_rn (soc_device.hpp), or 0 when n is outside the exhaustively checked range (1..16384).
+inline float recip_rn(int n) { return n >= 1 && n <= 16384 ? 1.0f / (float)n : 0.0f; }
 
 // Checks the launch that was just issued.
 int check_launch(const char* pass);

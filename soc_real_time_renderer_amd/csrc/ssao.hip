@@ -21,6 +21,7 @@ struct SsaoParams {
     int ksize;     // loop bound, min(kernel_size, 26)
     int noise_w;   // textureSize(u_normal_image).x
     int swz;       // XCD-aware tile order (tuning knob SOC_SWZ_SSAO, see xcd_order; 0 = row-major)
+    float rw, rh;  // recip_rn(target extent) for the pixel-centre uv (div_rn)
 };
 
 // ssao_generation.inl:139-141 (no FMA contraction: keeps the sin argument as the oracle's)
@@ -107,7 +108,7 @@ __global__ __launch_bounds__(256) void ssao_kernel(DImg depth, DImg normal, DImg
     const int tid = threadIdx.x;
     const int x = bx * 32 + (tid & 31), y = by * 8 + (tid >> 5);
     if (x >= target.w || y >= target.h) return;
-    const float u = centre_uv(x, target.w), v = centre_uv(y, target.h);
+    const float u = centre_uv_rn(x, target.w, p.rw), v = centre_uv_rn(y, target.h, p.rh);
 
     // normal = mat3(view) * normalize(texture(normal, uv).rgb), :178
     const f4 nn = sample_h4(normal, u, v);
@@ -187,10 +188,19 @@ __global__ __launch_bounds__(256) void ssao_kernel(DImg depth, DImg normal, DImg
                 vz = ip[2] * ex + ip[6] * ey + ip[10] * dd + ip[14];
                 vw = ip[3] * ex + ip[7] * ey + ip[11] * dd + ip[15];
             }
-            const float sd = vz * fast_rcp(vw);
-            const float rc = __builtin_amdgcn_fmed3f(r * fast_rcp(fabsf(frag.z - sd)), 0.0f, 1.0f);   // >= 0
-            const float range = rc * rc * (3.0f - 2.0f * rc);   // smoothstep(0, 1, x)
-            occ += (sd >= aff(az, kx, ky, kz)) ? range : 0.0f;
+            if (SPARSE_IP) {
+                // vw > 0 for every stored depth (the host selects this path only then), so with sd = vz / vw:
+                // r / |frag.z - sd| = r vw / |frag.z vw - vz| and sd >= s.z  <=>  s.z vw - vz <= 0 (one
+                // reciprocal per tap instead of two)
+                const float rc = __builtin_amdgcn_fmed3f(r * vw * fast_rcp(fabsf(__builtin_fmaf(frag.z, vw, -vz))), 0.0f, 1.0f);
+                const float range = rc * rc * (3.0f - 2.0f * rc);   // smoothstep(0, 1, x)
+                occ += (__builtin_fmaf(aff(az, kx, ky, kz), vw, -vz) <= 0.0f) ? range : 0.0f;
+            } else {
+                const float sd = vz * fast_rcp(vw);
+                const float rc = __builtin_amdgcn_fmed3f(r * fast_rcp(fabsf(frag.z - sd)), 0.0f, 1.0f);   // >= 0
+                const float range = rc * rc * (3.0f - 2.0f * rc);   // smoothstep(0, 1, x)
+                occ += (sd >= aff(az, kx, ky, kz)) ? range : 0.0f;
+            }
         }
     }
     occ = 1.0f - (occ / p.kernel_size_f);
@@ -266,8 +276,12 @@ extern "C" int soc_ssao_generation(const soc_globals* g, soc_img depth, soc_img 
     if ((long long)depth.pitch_bytes * depth.height >= (1ll << 31) || depth.pitch_bytes >= (1 << 23))
         return set_error(SOC_E_SHAPE, "soc_ssao_generation: depth image exceeds the 2 GiB buffer-offset range");
     SsaoParams p = make_params(g, normal);
+    p.rw = recip_rn(target.width);
+    p.rh = recip_rn(target.height);
     const float* IP = g->camera_inverse_projection_matrix;
-    const bool sip = IP[2] == 0.0f && IP[3] == 0.0f && IP[6] == 0.0f && IP[7] == 0.0f;
+    // sparse inverse projection (the reference's perspective) whose w row stays positive over depths [-1, 1]
+    const bool sip = IP[2] == 0.0f && IP[3] == 0.0f && IP[6] == 0.0f && IP[7] == 0.0f && IP[15] - IP[11] > 0.0f &&
+                     IP[15] + IP[11] > 0.0f;
     const dim3 blk(256), grd(ceil_div(target.width, 32), ceil_div(target.height, 8));
     const float2* tb = reinterpret_cast<const float2*>(noise_table);
     hipStream_t st = hs(stream);

@@ -13,6 +13,7 @@ namespace soc {
 namespace {
 
 struct TaaParams {
+    float rw, rh;       // recip_rn(target extent) for the pixel-centre uv (div_rn)
     float pox, poy;     // 1 / resolution
     float accum0;       // min(0.1, frame_counter)
     int swz;            // XCD-aware tile order (pair path)
@@ -220,12 +221,12 @@ __global__ __launch_bounds__(256) void taa_pair2(DImg target, DImg cur, DImg pre
         szw[c] = gauss_col(Czw[0][c], Czw[1][c], Czw[2][c]);
     }
     const int colx[4] = {xl, x0, x0 + 1, xr};
-    const float v = centre_uv(y, H);
+    const float v = centre_uv_rn(y, H, p.rh);
     uint2 outp[2];
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
         const int x = x0 + k;
-        const float u = centre_uv(x, W);
+        const float u = centre_uv_rn(x, W, p.rw);
         // closest depth in the reference order (oy = +1..-1, ox = +1..-1), last equal wins
         // the winning tap as one index r * 4 + c (one select per tap instead of two)
         float closest = 1.0f;
@@ -356,6 +357,8 @@ int taa_launch(const soc_globals* g, soc_img target, soc_img current_color, soc_
             return set_error(SOC_E_SHAPE, "%s: velocity_history_out extent != current_velocity extent", P);
     }
     TaaParams p;
+    p.rw = recip_rn(target.width);
+    p.rh = recip_rn(target.height);
     p.pox = 1.0f / (float)g->resolution[0];
     p.poy = 1.0f / (float)g->resolution[1];
     p.accum0 = fminf(0.1f, (float)g->frame_counter);
