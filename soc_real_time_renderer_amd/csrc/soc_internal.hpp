@@ -51,7 +51,10 @@ inline hipStream_t hs(soc_stream s) { return reinterpret_cast<hipStream_t>(s); }
 // ~0.1 us), so A/B runs and the variant-identity tests can switch it between calls.
 int tuning_knob(const char* name, int dflt);
 // RN(1 / n) for div_rn (soc_device.hpp), or 0 when n is outside the exhaustively checked range (1..16384).
-inline float recip_rn(int n) { return n >= 1 && n <= 16384 ? 1.0f / (float)n : 0.0f; }
+// (tuning knob SOC_NO_DIV_RN=1: always 0, i.e. the IEEE division, for A/B runs)
+inline float recip_rn(int n) {
+    return n >= 1 && n <= 16384 && !tuning_knob("SOC_NO_DIV_RN", 0) ? 1.0f / (float)n : 0.0f;
+}
 
 // Checks the launch that was just issued.
 int check_launch(const char* pass);
