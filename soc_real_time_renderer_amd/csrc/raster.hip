@@ -324,6 +324,7 @@ struct ResolveParams {
     Mat4 model, vp, prev_vp;
     Mat3 normal3;
     int width, height, triangle_count, material_count;
+    int tex_pairs;   // share the footprint of same-extent normal image + albedo (tuning knob SOC_GB_TEX_PAIRS, default on)
 };
 
 __device__ __forceinline__ float srgb_to_linear(float c) {
@@ -372,12 +373,15 @@ __device__ __forceinline__ f4 sample_texture(const soc_img& tex, float u, float 
 }
 
 
-// Bilinear REPEAT sample of one level (its image view already resolved) of a packed mip chain.
-__device__ __forceinline__ f4 sample_level(const DImg& im, float u, float v, bool srgb, const float* lut) {
-    const Axis ax = axis_repeat_level(u, im.w), ay = axis_repeat_level(v, im.h);
+// Bilinear REPEAT sample of one level (its image view already resolved) of a packed mip chain, from the
+// level's two axes (computed once when two textures of the same extent share them).
+__device__ __forceinline__ f4 sample_level_ax(const DImg& im, const Axis& ax, const Axis& ay, bool srgb, const float* lut) {
     const f4 a = texel_rgba8(im, ax.i0, ay.i0, srgb, lut), b = texel_rgba8(im, ax.i1, ay.i0, srgb, lut);
     const f4 c = texel_rgba8(im, ax.i0, ay.i1, srgb, lut), d = texel_rgba8(im, ax.i1, ay.i1, srgb, lut);
     return bilerp4(a, b, c, d, ax.w, ay.w);
+}
+__device__ __forceinline__ f4 sample_level(const DImg& im, float u, float v, bool srgb, const float* lut) {
+    return sample_level_ax(im, axis_repeat_level(u, im.w), axis_repeat_level(v, im.h), srgb, lut);
 }
 __device__ __forceinline__ DImg level_view(const soc_img& tex, int k) {
     int wk, hk;
@@ -389,7 +393,7 @@ __device__ __forceinline__ DImg level_view(const soc_img& tex, int k) {
 struct UVGrad { float dudx, dvdx, dudy, dvdy; };
 
 // Trilinear + anisotropic REPEAT sample of a mip-chained texture (soc_rt.h SOC_MATERIAL_MIPMAPPED).
-__device__ f4 sample_texture_mip(const soc_img& tex, float u, float v, const UVGrad& gr, float max_aniso, const float* lut) {
+__device__ __forceinline__ f4 sample_texture_mip(const soc_img& tex, float u, float v, const UVGrad& gr, float max_aniso, const float* lut) {
 #pragma clang fp contract(off)
     if (!tex.data) return f4{1.0f, 1.0f, 1.0f, 1.0f};
     const bool srgb = tex.format == SOC_FMT_RGBA8_SRGB;
@@ -432,6 +436,66 @@ __device__ f4 sample_texture_mip(const soc_img& tex, float u, float v, const UVG
     if (n == 1) return acc;
     const float fn = (float)n;
     return f4{acc.x / fn, acc.y / fn, acc.z / fn, acc.w / fn};
+}
+
+// sample_texture_mip of two textures of the same extent at the same uv (the material's normal image and
+// albedo): the footprint, tap count, lod and every tap's level axes depend only on the extent, so they are
+// computed once; each texture's taps, lerps and sums are sample_texture_mip's, in its order (same bits).
+// Precondition: both have data and ta.width == tb.width, ta.height == tb.height.
+__device__ __forceinline__ void sample_texture_mip2(const soc_img& ta, const soc_img& tb, float u, float v, const UVGrad& gr,
+                                    float max_aniso, const float* lut, f4& ra, f4& rb) {
+#pragma clang fp contract(off)
+    const bool sa = ta.format == SOC_FMT_RGBA8_SRGB, sb = tb.format == SOC_FMT_RGBA8_SRGB;
+    const int L = mip_levels(ta.width, ta.height);
+    const float W = (float)ta.width, H = (float)ta.height;
+    const float ax = gr.dudx * W, ay = gr.dvdx * H, bx = gr.dudy * W, by = gr.dvdy * H;
+    const float px = sqrtf(ax * ax + ay * ay), py = sqrtf(bx * bx + by * by);
+    const float pmax = fmaxf(px, py), pmin = fminf(px, py);
+    int n = 1;
+    if (max_aniso > 1.0f && pmax > 0.0f && pmax <= 3.4e38f) {
+        const float cap = floorf(max_aniso);
+        n = (int)(pmin > 0.0f ? fminf(ceilf(pmax / pmin), cap) : cap);
+    }
+    int lq = 0;
+    const float rho = pmax / (float)n;
+    if (rho > 0.0f && rho <= 3.4e38f) {
+        const float lam = fminf(fmaxf(det_log2(rho), -64.0f), 64.0f);
+        lq = min(max((int)floorf(lam * 256.0f + 0.5f), 0), (L - 1) * 256);
+    }
+    const int l0 = lq >> 8, l1 = min(l0 + 1, L - 1);
+    const float f = (float)(lq & 255) * (1.0f / 256.0f);
+    const DImg a0 = level_view(ta, l0), a1 = level_view(ta, l1), b0 = level_view(tb, l0), b1 = level_view(tb, l1);
+    const bool xmajor = px >= py;
+    const float du = xmajor ? gr.dudx : gr.dudy, dv = xmajor ? gr.dvdx : gr.dvdy;
+    f4 acca = f4{0.0f, 0.0f, 0.0f, 0.0f}, accb = acca;
+    auto tri = [&](f4 s0, const f4& s1) {
+        return f4{lerp_w(s0.x, s1.x, f), lerp_w(s0.y, s1.y, f), lerp_w(s0.z, s1.z, f), lerp_w(s0.w, s1.w, f)};
+    };
+    for (int i = 1; i <= n; ++i) {
+        float su = u, sv = v;
+        if (n > 1) {
+            const float t = (float)i / (float)(n + 1) - 0.5f;
+            su = u + t * du;
+            sv = v + t * dv;
+        }
+        const Axis x0 = axis_repeat_level(su, a0.w), y0 = axis_repeat_level(sv, a0.h);
+        f4 pa = sample_level_ax(a0, x0, y0, sa, lut), pb = sample_level_ax(b0, x0, y0, sb, lut);
+        if (lq & 255) {
+            const Axis x1 = axis_repeat_level(su, a1.w), y1 = axis_repeat_level(sv, a1.h);
+            pa = tri(pa, sample_level_ax(a1, x1, y1, sa, lut));
+            pb = tri(pb, sample_level_ax(b1, x1, y1, sb, lut));
+        }
+        acca = f4{acca.x + pa.x, acca.y + pa.y, acca.z + pa.z, acca.w + pa.w};
+        accb = f4{accb.x + pb.x, accb.y + pb.y, accb.z + pb.z, accb.w + pb.w};
+    }
+    if (n == 1) {
+        ra = acca;
+        rb = accb;
+        return;
+    }
+    const float fn = (float)n;
+    ra = f4{acca.x / fn, acca.y / fn, acca.z / fn, acca.w / fn};
+    rb = f4{accb.x / fn, accb.y / fn, accb.z / fn, accb.w / fn};
 }
 
 __device__ __forceinline__ f3 mat3_vec_exact(const Mat3& M, f3 v) {
@@ -573,8 +637,13 @@ __global__ __launch_bounds__(256) void gbuffer_resolve(soc_mesh mesh, const soc_
     auto tex = [&](const soc_img& t) {
         return mipped ? sample_texture_mip(t, u, v, gr, m.max_anisotropy, lut) : sample_texture(t, u, v, lut);
     };
+    // normal image and albedo of one extent on the reference sampler: one footprint for both (same bits)
+    const bool pair = tbn && mipped && p.tex_pairs && m.albedo.data && m.albedo.width == m.normal_image.width &&
+                      m.albedo.height == m.normal_image.height;
+    f4 t_pair{0.0f, 0.0f, 0.0f, 0.0f}, al_pair = t_pair;
+    if (pair) sample_texture_mip2(m.normal_image, m.albedo, u, v, gr, m.max_anisotropy, lut, t_pair, al_pair);
     if (tbn) {   // g_buffer_generation.inl:197-211
-        const f4 t = tex(m.normal_image);
+        const f4 t = pair ? t_pair : tex(m.normal_image);
         const f3 tn{t.x * 2.0f - 1.0f, t.y * 2.0f - 1.0f, t.z * 2.0f - 1.0f};
         const float st1t = gr.dvdx, st2t = gr.dvdy;
         const f3 N = normalize_exact(n);
@@ -588,7 +657,7 @@ __global__ __launch_bounds__(256) void gbuffer_resolve(soc_mesh mesh, const soc_
         const f4 e = tex(m.emissive);
         em = f3{e.x * m.emissive_factor[0], e.y * m.emissive_factor[1], e.z * m.emissive_factor[2]};
     }
-    const f4 al = tex(m.albedo);
+    const f4 al = pair ? al_pair : tex(m.albedo);
     f4 vel = f4{0.0f, 0.0f, 0.0f, 0.0f};
     if (!(m.flags & SOC_MATERIAL_ZERO_VELOCITY)) {
         const float4 ca = VA.cc, cb = VB.cc, cd = VC.cc, pa = VA.pc, pb = VB.pc, pd = VC.pc;
@@ -717,6 +786,7 @@ extern "C" int soc_gbuffer_resolve(const soc_globals* g, const soc_mesh* mesh, c
     p.height = H;
     p.triangle_count = mesh->triangle_count;
     p.material_count = material_count;
+    p.tex_pairs = tuning_knob("SOC_GB_TEX_PAIRS", 1);
     dim3 blk(64, 4), grd(ceil_div(W, 64), ceil_div(H, 4));
     const unsigned long long* vis = reinterpret_cast<const unsigned long long*>(visibility);
     if (workspace) {   // per-vertex outputs once, then the per-pixel resolve reads them

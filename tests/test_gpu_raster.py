@@ -380,6 +380,34 @@ def test_sponza_mesh_mipmapped_gbuffer_vs_oracle(soc, oracle, tex):
     assert moved.any(axis=-1).mean() > 0.05
 
 
+@pytest.mark.parametrize("tex", [128, 96])
+def test_mipmapped_gbuffer_shared_footprint_bit_identical(soc, monkeypatch, tex):
+    """The resolve samples a material's normal image and albedo of one extent with one shared footprint / tap /
+    lod computation (SOC_GB_TEX_PAIRS, default on): the same bits as sampling them one after the other."""
+    W, H = 480, 270
+    g = globals_for(W, H)
+    _, dm = _mesh_scene()
+    mats_d, keep_d = raster.sponza_mesh_materials(tex, DEV, mips=True)
+    dmats = raster.materials_device(mats_d)
+    vp = np.ctypeslib.as_array(g.camera_projection_view_matrix)
+    ws = dm.workspace()
+    vis = torch.zeros((H, W), dtype=torch.int64, device=DEV)
+    raster.raster_visibility(dm, vp, raster.CULL_FRONT, vis, ws)
+    outs = []
+    for pairs in ("1", "0"):
+        monkeypatch.setenv("SOC_GB_TEX_PAIRS", pairs)
+        soc.reload_tuning()
+        out = {k: torch.zeros((H, W, 4), dtype=torch.float16, device=DEV) for k in ("albedo", "emissive", "normal", "velocity")}
+        out["depth"] = torch.zeros((H, W), dtype=torch.float32, device=DEV)
+        raster.gbuffer_resolve(g, dm, dmats, len(mats_d), vis, out["depth"], out["albedo"], out["emissive"], out["normal"],
+                               out["velocity"], ws)
+        outs.append(out)
+    monkeypatch.delenv("SOC_GB_TEX_PAIRS")
+    soc.reload_tuning()
+    for k in outs[0]:
+        assert torch.equal(outs[0][k], outs[1][k]), k
+
+
 @pytest.mark.parametrize("size,grid,level", [(1024, 100, 3), (128, 100, 3), (64, 17, 5), (32, 2, 1)])
 def test_terrain_tessellate_bit_exact(soc, oracle, size, grid, level):
     """soc_terrain_tessellate (draw_terrain.inl:138-191 on the renderer.cpp:194-220 patch grid) against the oracle:
