@@ -123,6 +123,26 @@ def pmc_traffic(kernel, W, H, scene_name="mesh"):
     return k["hbm_bytes"], os.path.relpath(files[-1], ROOT)
 
 
+def ssao_gather_bound(W, H, scene_name, ssao_us):
+    """SSAOGeneration against its texture-path ceiling: the measured wave loads per launch
+    (SQ_INSTS_VMEM_RD, profiles/*ssao_gather.json, same workload) at the microbenchmarked per-CU issue cost of
+    a wave load that touches one 128-B line (coalesced) or >= 4 lines (scattered, L1/L2-resident)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*ssao_gather.json")))
+    if not files:
+        return None
+    with open(files[-1]) as fh:
+        t = json.load(fh)
+    if list(t.get("resolution", [])) != [W, H] or t.get("scene") != scene_name:
+        return None
+    loads, cus = float(t["counters"]["SQ_INSTS_VMEM_RD"]), int(t["cus"])
+    rate = t["gather_rate_ns_per_wave_load_per_cu"]
+    us_c = loads * rate["one_line"] / cus / 1e3
+    us_s = loads * rate["four_or_more_lines_l1"] / cus / 1e3
+    return {"wave_loads_per_launch": int(loads), "us_if_coalesced": round(us_c, 1), "us_if_scattered": round(us_s, 1),
+            "frac_of_scattered_rate": round(us_s / ssao_us, 3), "source": os.path.relpath(files[-1], ROOT)}
+
+
 def cpu_baseline(W, H, host_inputs, g):
     """The oracle (plain-C restatement, OpenMP over rows) timed on this box's host cores."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -357,7 +377,9 @@ def main():
                                             "frac": round(algo["SSAOGeneration"] / (ssao_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                                             "traffic": ssao_traffic,
                                             "algorithmic_bytes_per_launch": int(algo["SSAOGeneration"]),
-                                            "avg_launch_us": round(ssao_ms * 1e3, 2)}}},
+                                            "avg_launch_us": round(ssao_ms * 1e3, 2),
+                                            "gather_bound": (ssao_gather_bound(W, H, args.scene, ssao_ms * 1e3)
+                                                             if args.config == "c3" else None)}}},
         "ranks": per_rank,
         "allreduce_us_per_frame": (round(sum(p["allreduce_us_per_frame"] for p in per_rank) / world, 2)
                                    if world > 1 else None),
