@@ -195,20 +195,33 @@ def num_threads() -> int:
     return int(lib().soc_oracle_num_threads())
 
 
-def frame(g, fr: dict, ae: AutoExposure, total_pixels=0, wide=False, hist=0):
+def frame(g, fr: dict, ae: AutoExposure, total_pixels=0, wide=False, hist=0, times=None):
     """One full hot-path frame on the CPU (renderer.cpp:1024-1217 order), numpy frame dict as
-    soc_real_time_renderer_amd.alloc_frame lays out (host arrays). Returns the history slot written."""
-    bloom_chain(g, fr["emissive"], fr["bloom_mips"])
-    ssao_generation(g, fr["depth"], fr["normal"], fr["ssao"])
-    ssao_blur(g, fr["ssao"], fr["ssao_blur"])
-    cloud_rendering(g, fr["depth"], fr["noise"], fr["clouds"])
-    composition(g, fr["color"], fr["albedo"], fr["emissive"], fr["normal"], fr["depth"], fr["ssao_blur"], fr["shadow"],
-                fr["clouds"])
-    generate_luminance_histogram(g, fr["color"], ae)
-    resolve_luminance_histogram(g, ae, total_pixels, wide)
+    soc_real_time_renderer_amd.alloc_frame lays out (host arrays). Returns the history slot written.
+    times: optional dict, pass name -> list of seconds, appended to per pass (the CPU baseline's per-pass figures)."""
+    import time
     q = 1 - hist
-    temporal_antialiasing(g, fr["history_color"][q], fr["color"], fr["history_color"][hist], fr["velocity"],
-                          fr["history_velocity"][hist], fr["depth"])
-    fr["history_velocity"][q][...] = fr["velocity"]
-    tone_mapping(g, fr["history_color"][q], ae, fr["output"], fr.get("output_format"))
+
+    def taa():
+        temporal_antialiasing(g, fr["history_color"][q], fr["color"], fr["history_color"][hist], fr["velocity"],
+                              fr["history_velocity"][hist], fr["depth"])
+        fr["history_velocity"][q][...] = fr["velocity"]
+
+    steps = (
+        ("Bloom", lambda: bloom_chain(g, fr["emissive"], fr["bloom_mips"])),
+        ("SSAOGeneration", lambda: ssao_generation(g, fr["depth"], fr["normal"], fr["ssao"])),
+        ("SSAOBlur", lambda: ssao_blur(g, fr["ssao"], fr["ssao_blur"])),
+        ("CloudRendering", lambda: cloud_rendering(g, fr["depth"], fr["noise"], fr["clouds"])),
+        ("Composition", lambda: composition(g, fr["color"], fr["albedo"], fr["emissive"], fr["normal"], fr["depth"],
+                                            fr["ssao_blur"], fr["shadow"], fr["clouds"])),
+        ("GenerateLuminanceHistogram", lambda: generate_luminance_histogram(g, fr["color"], ae)),
+        ("ResolveLuminanceHistogram", lambda: resolve_luminance_histogram(g, ae, total_pixels, wide)),
+        ("TemporalAntiAliasing", taa),
+        ("ToneMapping", lambda: tone_mapping(g, fr["history_color"][q], ae, fr["output"], fr.get("output_format"))),
+    )
+    for name, fn in steps:
+        t0 = time.perf_counter()
+        fn()
+        if times is not None:
+            times.setdefault(name, []).append(time.perf_counter() - t0)
     return q

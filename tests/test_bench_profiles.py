@@ -33,3 +33,18 @@ def test_ssao_gather_bound():
     assert 52 * 0.8 * waves < gb["wave_loads_per_launch"] < 60 * waves
     assert abs(gb["frac_of_scattered_rate"] - gb["us_if_scattered"] / 170.0) < 1e-3
     assert bench.ssao_gather_bound(1920, 1080, "mesh", 50.0) is None
+
+
+def test_cpu_baseline_per_pass_medians():
+    """The CPU baseline: the oracle frame timed per frame and per pass (median after a warm-up)."""
+    import bench
+    from helpers import sponza_inputs
+    W, H = 64, 36
+    g, gb = sponza_inputs(W, H, elapsed=10.0, frame_counter=2)
+    host = {k: gb[k] for k in ("albedo", "emissive", "normal", "velocity", "depth", "shadow", "noise")}
+    cb = bench.cpu_baseline(W, H, host, g)
+    assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1
+    assert set(cb["ms_per_pass_median"]) == {"Bloom", "SSAOGeneration", "SSAOBlur", "CloudRendering", "Composition",
+                                            "GenerateLuminanceHistogram", "ResolveLuminanceHistogram",
+                                            "TemporalAntiAliasing", "ToneMapping"}
+    assert sum(cb["ms_per_pass_median"].values()) <= 1.5 * cb["ms_per_frame_median"] + 1.0
