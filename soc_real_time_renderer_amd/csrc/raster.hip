@@ -522,13 +522,14 @@ __device__ __forceinline__ VtxData vertex_data(const soc_mesh& mesh, uint32_t v,
     d.s = clip_vertex(mesh.positions, v, p.model, p.vp, p.width, p.height);
     const float* nr = mesh.normals;
     const f3 n = normalize_exact(mat3_vec_exact(p.normal3, f3{nr[3 * v], nr[3 * v + 1], nr[3 * v + 2]}));
-    d.n = float4{n.x, n.y, n.z, 0.0f};
+    d.n = float4{n.x, n.y, n.z, 0.0f};   // .w of n, cc, pc: the world position (the TBN's out_position)
     const float* ps = mesh.positions;
     const f4 wp = mat_vec_exact(p.model, ps[3 * v], ps[3 * v + 1], ps[3 * v + 2], 1.0f);
     const f4 c = mat_vec_exact(p.vp, wp.x, wp.y, wp.z, wp.w);
     const f4 q = mat_vec_exact(p.prev_vp, wp.x, wp.y, wp.z, wp.w);
-    d.cc = float4{c.x, c.y, c.w, 0.0f};
-    d.pc = float4{q.x, q.y, q.w, 0.0f};
+    d.n.w = wp.x;
+    d.cc = float4{c.x, c.y, c.w, wp.y};
+    d.pc = float4{q.x, q.y, q.w, wp.z};
     return d;
 }
 
@@ -608,12 +609,11 @@ __global__ __launch_bounds__(256) void gbuffer_resolve(soc_mesh mesh, const soc_
     f3 Q1{0.0f, 0.0f, 0.0f}, Q2{0.0f, 0.0f, 0.0f};
     UVGrad gr{0.0f, 0.0f, 0.0f, 0.0f};
     if (tbn || mipped) {
-        const float* ps = mesh.positions;
         f4 wa{0.0f, 0.0f, 0.0f, 0.0f}, wb = wa, wc = wa;
-        if (tbn) {   // vertex stage out_position (:171-172)
-            wa = mat_vec_exact(p.model, ps[3 * ia], ps[3 * ia + 1], ps[3 * ia + 2], 1.0f);
-            wb = mat_vec_exact(p.model, ps[3 * ib], ps[3 * ib + 1], ps[3 * ib + 2], 1.0f);
-            wc = mat_vec_exact(p.model, ps[3 * ic], ps[3 * ic + 1], ps[3 * ic + 2], 1.0f);
+        if (tbn) {   // vertex stage out_position (:171-172), kept by the vertex stage in the .w components
+            wa = f4{VA.n.w, VA.cc.w, VA.pc.w, 1.0f};
+            wb = f4{VB.n.w, VB.cc.w, VB.pc.w, 1.0f};
+            wc = f4{VC.n.w, VC.cc.w, VC.pc.w, 1.0f};
         }
         auto attr = [&](float sx, float sy, f3& P, float& su, float& sv) {
             const float a0 = edge(r0, sx, sy), a1 = edge(r1, sx, sy), a2 = edge(r2, sx, sy);
