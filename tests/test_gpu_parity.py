@@ -517,10 +517,13 @@ def test_clouds_pair_path_equals_single_lane(soc, W, H, pitch, all_sky):
 
 # ------------------------------------------------------------------------------------------------ full frame
 @pytest.mark.parametrize("W,H,frames,inputs", [(256, 144, 3, "sponza"), (1920, 1080, 2, "sponza"),
-                                               (320, 180, 2, "terrain"), (960, 540, 2, "terrain")])
+                                               (320, 180, 2, "terrain"), (960, 540, 2, "terrain"),
+                                               (97, 55, 2, "sponza"), (8200, 18, 2, "sponza"), (18, 1200, 2, "sponza")])
 def test_render_graph_frames(soc, oracle, W, H, frames, inputs):
     """Multi-frame render graph (ping-pong TAA history, fused velocity history) vs the oracle frame, on the
-    Sponza-proxy (C2/C3) and on the terrain (C4: half the frame is sky, so clouds dominate)."""
+    Sponza-proxy (C2/C3) and on the terrain (C4: half the frame is sky, so clouds dominate). Ragged and extreme
+    shapes: an odd extent (no pair paths), a frame wider than the 8192-texel fast paths (TAA falls back to the
+    generic kernel and the tone map runs as its own pass) and a tall narrow one (one-tile-wide grids)."""
     g, gb = (sponza_inputs if inputs == "sponza" else terrain_inputs)(W, H, elapsed=10.0)
     fr = soc.alloc_frame(W, H, DEV)
     for k in ("albedo", "emissive", "normal", "velocity", "depth"):
