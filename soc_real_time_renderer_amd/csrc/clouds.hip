@@ -516,6 +516,9 @@ struct PairBufs {
     uint32_t* batch_base; // [W*H/256] per 256-entry batch: physical index of its first pair | kInline
     float4* geom;         // [W*H] x 2 per list entry: (start, dither), (inc, stepLength) of its march (density
                           // writes it for upward rays; sunvis and resolve read it instead of re-deriving it)
+    float* od;            // [24 * W*H] step-major: od of dense step s of list entry i at od[s * n + i] (density writes
+                          // it, sunvis reads it instead of evaluating the step's clouds again); null: sunvis evaluates
+    uint32_t n;           // list capacity (W*H)
     uint32_t cap;         // pairs per shard
 };
 
@@ -583,8 +586,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void c
                 const float dither = bayer16((float)x, (float)y);
                 pb.geom[2 * i] = float4{mg.start.x, mg.start.y, mg.start.z, dither};
                 pb.geom[2 * i + 1] = float4{mg.inc.x, mg.inc.y, mg.inc.z, mg.stepLength};
-                for (int s = 0; s < 24; s++)
-                    if (!(get_clouds(cx, step_position(mg, dither, s)) * mg.stepLength <= 0.0f)) mask |= 1u << s;
+                for (int s = 0; s < 24; s++) {
+                    const float od = get_clouds(cx, step_position(mg, dither, s)) * mg.stepLength;
+                    if (!(od <= 0.0f)) {
+                        mask |= 1u << s;
+                        if (pb.od) pb.od[(size_t)s * pb.n + i] = od;
+                    }
+                }
             }
         }
         // pairs in step-major order within the batch (lanes of a sunvis wave then share the step and
@@ -660,7 +668,8 @@ __global__ __launch_bounds__(kSunvisThreads) __attribute__((amdgpu_waves_per_eu(
         const float4 g0 = pb.geom[2 * i], g1 = pb.geom[2 * i + 1];   // the pixel's march, from clouds_density
         const MarchGeom mg{f3{g0.x, g0.y, g0.z}, f3{g1.x, g1.y, g1.z}, g1.w};
         const f3 cp = step_position(mg, g0.w, (int)step);
-        const float od = get_clouds(cx, cp) * mg.stepLength;
+        // the dense step's od as clouds_density computed it (the same function of the same stored geometry)
+        const float od = pb.od ? pb.od[(size_t)step * pb.n + i] : get_clouds(cx, cp) * mg.stepLength;
         const float vis = SOC_CLOUDS_PROFILE == 3 ? 1.0f : sun_visibility(cx, cp, sun);
         pb.odvis[phys] = float2{od, vis};
     }
@@ -759,7 +768,8 @@ using namespace soc;
 namespace {
 // Workspace: counters (256 B: [0] sky pixels, [8..15] pair counts per shard) | sky list (u32) |
 // atmosphere (float4) | per-pixel dense mask (u32) | per-batch first pair (u32) | march geometry (2 float4) | pairs (u32) |
-// (od, vis) per pair (float2). Pair capacity 2 per pixel of the image (8 shards).
+// (od, vis) per pair (float2) | od of every dense step (24 float per pixel, step-major). Pair capacity 2 per pixel
+// of the image (8 shards).
 // Per 256-entry batch of the list: the physical index of its first pair (or kInline).
 struct CloudWs {
     uint32_t* counter;
@@ -790,6 +800,9 @@ CloudWs cloud_ws_layout(void* base, size_t n) {
     off = al(off + (size_t)kShards * w.pb.cap * 4);
     w.pb.odvis = reinterpret_cast<float2*>(b + off);
     off = al(off + (size_t)kShards * w.pb.cap * 8);
+    w.pb.od = reinterpret_cast<float*>(b + off);
+    w.pb.n = (uint32_t)n;
+    off = al(off + n * 24 * 4);
     w.bytes = off;
     return w;
 }
@@ -839,7 +852,9 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
         return check_launch("cloud_rendering");
     }
     // the caller sized the workspace for the target extent (soc_cloud_rendering_workspace_size)
-    const CloudWs ws = cloud_ws_layout(workspace, (size_t)target.width * (size_t)target.height);
+    CloudWs ws = cloud_ws_layout(workspace, (size_t)target.width * (size_t)target.height);
+    const bool od_store = tuning_knob("SOC_CLOUDS_OD_STORE", 1) != 0;   // A/B: sunvis re-evaluates the step
+    if (!od_store) ws.pb.od = nullptr;
     uint32_t* counter = ws.counter;
     uint32_t* list = ws.list;
     hipError_t e = hipMemsetAsync(counter, 0, 256, s);
