@@ -1,10 +1,10 @@
 #!/bin/bash
 # A/B of one tuning knob on the default bench line: tests matching $TESTS first (if set), then bench lines
-# alternating KNOB=0 / KNOB=1, twice each.  Usage: KNOB=SOC_X [TESTS="-k expr"] [BENCH_ARGS=...] tools/ab_knob2.sh
+# alternating KNOB=0 / KNOB=1, twice each.  Usage: KNOB=SOC_X [TESTS="pytest -k expression"] [BENCH_ARGS=...] tools/ab_knob2.sh
 set -o pipefail
 mkdir -p gpurun_out
 if [ -n "${TESTS:-}" ]; then
-  timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread $TESTS > gpurun_out/ab2_tests.log 2>&1 || { grep -E "FAIL|Error" gpurun_out/ab2_tests.log | head; tail -20 gpurun_out/ab2_tests.log; exit 1; }
+  timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -k "$TESTS" > gpurun_out/ab2_tests.log 2>&1 || { grep -E "FAIL|Error" gpurun_out/ab2_tests.log | head; tail -20 gpurun_out/ab2_tests.log; exit 1; }
   tail -1 gpurun_out/ab2_tests.log
 fi
 for rep in 1 2; do for v in 0 1; do
