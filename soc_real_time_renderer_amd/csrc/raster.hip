@@ -332,11 +332,28 @@ __device__ __forceinline__ float srgb_to_linear(float c) {
 }
 
 // lut: srgb_to_linear(unorm8(i)) for i in 0..255 (LDS, filled per workgroup)
-__device__ __forceinline__ f4 texel_rgba8(const DImg& im, int x, int y, bool srgb, const float* lut) {
-    const uint32_t u = row_ptr<uint32_t>(im, y)[x];
+__device__ __forceinline__ f4 decode_rgba8(uint32_t u, bool srgb, const float* lut) {
     const float a = unorm8(u >> 24);
     if (!srgb) return f4{unorm8(u & 255u), unorm8((u >> 8) & 255u), unorm8((u >> 16) & 255u), a};
     return f4{lut[u & 255u], lut[(u >> 8) & 255u], lut[(u >> 16) & 255u], a};
+}
+__device__ __forceinline__ f4 texel_rgba8(const DImg& im, int x, int y, bool srgb, const float* lut) {
+    return decode_rgba8(row_ptr<uint32_t>(im, y)[x], srgb, lut);
+}
+
+typedef uint32_t u2a4 __attribute__((ext_vector_type(2))) __attribute__((aligned(4)));
+// The two texels (x0, y), (x1, y) of a bilinear tap's row: one 8-byte load when x1 = x0 + 1 (every tap that does
+// not wrap around the REPEAT edge), else two. The same texels either way.
+__device__ __forceinline__ void texel_row_pair(const DImg& im, int x0, int x1, int y, uint32_t& a, uint32_t& b) {
+    const uint32_t* row = row_ptr<uint32_t>(im, y);
+    if (x1 == x0 + 1) {
+        const u2a4 t = *reinterpret_cast<const u2a4*>(row + x0);
+        a = t.x;
+        b = t.y;
+    } else {
+        a = row[x0];
+        b = row[x1];
+    }
 }
 
 // REPEAT addressing for any extent (the sampling contract's 8-bit sub-texel weights).
@@ -362,24 +379,24 @@ __device__ __forceinline__ Axis axis_repeat_level(float u, int n) {
     return (n & (n - 1)) ? axis_repeat_any(u, n) : axis_repeat_pow2(u, n, n - 1);
 }
 
+// Bilinear REPEAT sample of one level (its image view already resolved) of a packed mip chain, from the
+// level's two axes (computed once when two textures of the same extent share them).
+__device__ __forceinline__ f4 sample_level_ax(const DImg& im, const Axis& ax, const Axis& ay, bool srgb, const float* lut) {
+    uint32_t ua, ub, uc, ud;
+    texel_row_pair(im, ax.i0, ax.i1, ay.i0, ua, ub);
+    texel_row_pair(im, ax.i0, ax.i1, ay.i1, uc, ud);
+    const f4 a = decode_rgba8(ua, srgb, lut), b = decode_rgba8(ub, srgb, lut);
+    const f4 c = decode_rgba8(uc, srgb, lut), d = decode_rgba8(ud, srgb, lut);
+    return bilerp4(a, b, c, d, ax.w, ay.w);
+}
 __device__ __forceinline__ f4 sample_texture(const soc_img& tex, float u, float v, const float* lut) {
     if (!tex.data) return f4{1.0f, 1.0f, 1.0f, 1.0f};
     const DImg im{static_cast<char*>(tex.data), tex.width, tex.height, tex.pitch_bytes};
     const bool srgb = tex.format == SOC_FMT_RGBA8_SRGB;
-    const Axis ax = axis_repeat_level(u, tex.width), ay = axis_repeat_level(v, tex.height);
-    const f4 a = texel_rgba8(im, ax.i0, ay.i0, srgb, lut), b = texel_rgba8(im, ax.i1, ay.i0, srgb, lut);
-    const f4 c = texel_rgba8(im, ax.i0, ay.i1, srgb, lut), d = texel_rgba8(im, ax.i1, ay.i1, srgb, lut);
-    return bilerp4(a, b, c, d, ax.w, ay.w);
+    return sample_level_ax(im, axis_repeat_level(u, tex.width), axis_repeat_level(v, tex.height), srgb, lut);
 }
 
 
-// Bilinear REPEAT sample of one level (its image view already resolved) of a packed mip chain, from the
-// level's two axes (computed once when two textures of the same extent share them).
-__device__ __forceinline__ f4 sample_level_ax(const DImg& im, const Axis& ax, const Axis& ay, bool srgb, const float* lut) {
-    const f4 a = texel_rgba8(im, ax.i0, ay.i0, srgb, lut), b = texel_rgba8(im, ax.i1, ay.i0, srgb, lut);
-    const f4 c = texel_rgba8(im, ax.i0, ay.i1, srgb, lut), d = texel_rgba8(im, ax.i1, ay.i1, srgb, lut);
-    return bilerp4(a, b, c, d, ax.w, ay.w);
-}
 __device__ __forceinline__ f4 sample_level(const DImg& im, float u, float v, bool srgb, const float* lut) {
     return sample_level_ax(im, axis_repeat_level(u, im.w), axis_repeat_level(v, im.h), srgb, lut);
 }
