@@ -663,7 +663,11 @@ int ensure_hist_scratch(soc_renderer* r) {
         r->hist_scratch = nullptr;
         return set_error(SOC_E_HIP, "soc_renderer_execute: histogram scratch allocation failed");
     }
-    if (hipMemset(r->hist_scratch, 0, SOC_HISTOGRAM_SCRATCH_WORDS * sizeof(uint32_t)) != hipSuccess)
+    // hipMemset is queued on the null stream, which does not order the renderer's non-blocking second lane: the
+    // first call comes from the sky lane's pass (sky_compose bins into the scratch), so the clear must have
+    // landed before any lane's kernel runs (one device synchronisation, on the first frame only)
+    if (hipMemset(r->hist_scratch, 0, SOC_HISTOGRAM_SCRATCH_WORDS * sizeof(uint32_t)) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess)
         return set_error(SOC_E_HIP, "soc_renderer_execute: histogram scratch clear failed");
     return SOC_OK;
 }

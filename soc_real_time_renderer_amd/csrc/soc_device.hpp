@@ -125,16 +125,31 @@ __device__ __forceinline__ f4 bilerp4(f4 a, f4 b, f4 c, f4 d, float wx, float wy
               bilerp1(a.z, b.z, c.z, d.z, wx, wy), bilerp1(a.w, b.w, c.w, d.w, wx, wy)};
 }
 
+// With n >= 2 texels across, axis_clamp's taps are i0 and i0 + 1 (i0 <= n - 2): each row's texel pair is one
+// load of twice the texel size (4-byte aligned: the hardware's dword alignment), the same texels.
+typedef uint32_t soc_u4a4 __attribute__((ext_vector_type(4))) __attribute__((aligned(4)));
+typedef float soc_f2a4 __attribute__((ext_vector_type(2))) __attribute__((aligned(4)));
 __device__ __forceinline__ f4 sample_h4(const DImg& im, float u, float v) {
     Axis ax = axis_clamp(u, im.w), ay = axis_clamp(v, im.h);
     const uint2* r0 = row_ptr<uint2>(im, ay.i0);
     const uint2* r1 = row_ptr<uint2>(im, ay.i1);
+    if (im.w >= 2) {
+        const soc_u4a4 p0 = *reinterpret_cast<const soc_u4a4*>(r0 + ax.i0);
+        const soc_u4a4 p1 = *reinterpret_cast<const soc_u4a4*>(r1 + ax.i0);
+        return bilerp4(unpack_h4(uint2{p0.x, p0.y}), unpack_h4(uint2{p0.z, p0.w}), unpack_h4(uint2{p1.x, p1.y}),
+                       unpack_h4(uint2{p1.z, p1.w}), ax.w, ay.w);
+    }
     return bilerp4(unpack_h4(r0[ax.i0]), unpack_h4(r0[ax.i1]), unpack_h4(r1[ax.i0]), unpack_h4(r1[ax.i1]), ax.w, ay.w);
 }
 __device__ __forceinline__ float sample_f32(const DImg& im, float u, float v) {
     Axis ax = axis_clamp(u, im.w), ay = axis_clamp(v, im.h);
     const float* r0 = row_ptr<float>(im, ay.i0);
     const float* r1 = row_ptr<float>(im, ay.i1);
+    if (im.w >= 2) {
+        const soc_f2a4 p0 = *reinterpret_cast<const soc_f2a4*>(r0 + ax.i0);
+        const soc_f2a4 p1 = *reinterpret_cast<const soc_f2a4*>(r1 + ax.i0);
+        return bilerp1(p0.x, p0.y, p1.x, p1.y, ax.w, ay.w);
+    }
     return bilerp1(r0[ax.i0], r0[ax.i1], r1[ax.i0], r1[ax.i1], ax.w, ay.w);
 }
 __device__ __forceinline__ float sample_r8(const DImg& im, float u, float v) {
