@@ -554,6 +554,30 @@ def test_render_graph_frames(soc, oracle, W, H, frames, inputs):
     r.close()
 
 
+@pytest.mark.parametrize("W,H", [(320, 180), (1920, 1080)])
+def test_fresh_renderers_first_frame_exposure(soc, oracle, W, H):
+    """A renderer's first frame on a sky-heavy (terrain) view: the histogram scratch is allocated and cleared on
+    first use, while the sky lane (a non-blocking stream) bins the sky pixels into it; the clear must land first.
+    Several fresh renderers in a row (their frame buffers reuse freed memory), each frame 0 against the oracle."""
+    g, gb = terrain_inputs(W, H, elapsed=10.0)
+    hf0 = host_frame(W, H, gb)
+    ae0 = soc.AutoExposure()
+    oracle.frame(g, hf0, ae0, hist=0)
+    for k in range(6):
+        fr = soc.alloc_frame(W, H, DEV)
+        for key in ("albedo", "emissive", "normal", "velocity", "depth"):
+            fr[key].copy_(torch.from_numpy(gb[key]))
+        fr["shadow"] = dev(gb["shadow"])
+        fr["noise"].copy_(torch.from_numpy(gb["noise"]))
+        r = soc.Renderer(fr)
+        r.execute(g)
+        torch.cuda.synchronize()
+        assert abs(soc.exposure_of(fr["auto_exposure"]) - ae0.exposure) <= 1e-4, (k, soc.exposure_of(fr["auto_exposure"]),
+                                                                                ae0.exposure)
+        r.close()
+        del fr
+
+
 # ------------------------------------------------------------------------------------------------ 4K properties
 def test_4k_properties(soc):
     """Size-independent properties at the benchmark resolution (oracle would take too long)."""
