@@ -1113,7 +1113,25 @@ extern "C" int soc_renderer_execute(soc_renderer* r, const soc_globals* g, int32
         if (hipEventRecord(r->fork_ev, s) != hipSuccess || hipStreamWaitEvent(r->side, r->fork_ev, 0) != hipSuccess)
             return set_error(SOC_E_HIP, "soc_renderer_execute: second lane fork failed");
     }
-    for (int i = 0; i < n; ++i) {
+    // issue order: by default (tuning knob SOC_RENDERER_SSAO_FIRST=1) the AO passes ahead of the
+    // bloom passes they do not depend on, so the gather-bound SSAO overlaps the VALU-bound atmosphere at the start
+    // of the sky lane (same passes, same per-pass results)
+    std::vector<int> order(n);
+    for (int i = 0; i < n; ++i) order[i] = i;
+    if (tuning_knob("SOC_RENDERER_SSAO_FIRST", 1)) {
+        std::vector<int> ao, rest;
+        for (int i = 0; i < n; ++i) (r->passes[i].group == "Ambient Occlusion" ? ao : rest).push_back(i);
+        bool free = !ao.empty();   // the AO passes may move only if none depends on an earlier non-AO pass
+        for (int a : ao)
+            for (int j : deps[a])
+                if (r->passes[j].group != "Ambient Occlusion") free = false;
+        if (free) {   // AO, then everything else in registration order
+            order = ao;
+            order.insert(order.end(), rest.begin(), rest.end());
+        }
+    }
+    for (int oi = 0; oi < n; ++oi) {
+        const int i = order[oi];
         if (lane[i] < 0) continue;
         auto& p = r->passes[i];
         hipStream_t ls = lane[i] ? r->side : s;

@@ -554,6 +554,32 @@ def test_render_graph_frames(soc, oracle, W, H, frames, inputs):
     r.close()
 
 
+def test_render_graph_ao_first_issue_order_bit_identical(soc, monkeypatch):
+    """The default issue order puts SSAOGeneration / SSAOBlur ahead of the bloom passes they do not depend on
+    (SOC_RENDERER_SSAO_FIRST); the registration order gives the same bits over 3 frames."""
+    W, H = 960, 540
+    g, gb = sponza_inputs(W, H, elapsed=10.0)
+    outs = []
+    for first in ("1", "0"):
+        monkeypatch.setenv("SOC_RENDERER_SSAO_FIRST", first)
+        soc.reload_tuning()
+        fr = soc.alloc_frame(W, H, DEV, bloom_output=True)
+        for k in ("albedo", "emissive", "normal", "velocity", "depth"):
+            fr[k].copy_(torch.from_numpy(gb[k]))
+        fr["shadow"] = dev(gb["shadow"])
+        fr["noise"].copy_(torch.from_numpy(gb["noise"]))
+        r = soc.Renderer(fr)
+        for _ in range(3):
+            r.execute(g)
+        torch.cuda.synchronize()
+        outs.append({k: fr[k].clone() for k in ("color", "output", "auto_exposure", "ssao_blur", "bloom_output")})
+        r.close()
+    monkeypatch.delenv("SOC_RENDERER_SSAO_FIRST")
+    soc.reload_tuning()
+    for k in outs[0]:
+        assert torch.equal(outs[0][k], outs[1][k]), k
+
+
 @pytest.mark.parametrize("W,H", [(320, 180), (1920, 1080)])
 def test_fresh_renderers_first_frame_exposure(soc, oracle, W, H):
     """A renderer's first frame on a sky-heavy (terrain) view: the histogram scratch is allocated and cleared on
