@@ -177,6 +177,37 @@ def cpu_baseline(W, H, host_inputs, g):
             "ms_per_pass_median": {k: round(float(np.median(v)) * 1e3, 2) for k, v in times.items()}}
 
 
+def build_inputs(config, scene_name, W, H, rank, device, mips=True):
+    """The frame inputs of a bench configuration (shared with the 4K C3 parity test): globals of rank `rank`'s camera,
+    the G-buffer + 4096^2 sun shadow map (the Sponza-proxy mesh rasterised once by the HIP rasteriser, or the
+    host-synthesised box atrium / terrain), the noise texture, and the device frame images holding them.
+    Returns (g, host G-buffer dict, host shadow, host noise, mesh scene or None, device frame)."""
+    terrain = config == "c4"
+    scene_id = scene.TERRAIN if terrain else (scene.SPONZA_PROXY if scene_name == "boxes" else scene.SPONZA_MESH)
+    g = make_globals(W, H, (multi_gpu.terrain_camera_for_rank if terrain else multi_gpu.camera_for_rank)(rank))
+    if config == "c3b":
+        soc.scene_update(g, point_lights_c3b())
+    sc = None
+    if scene_id == scene.SPONZA_MESH:
+        # rasterised once by the HIP rasteriser (DepthPrepass + GBufferGeneration + SunShadowDraw), not timed
+        sc = raster.scene_setup(g, scene_id, tex_size=256, device=device, mips=mips)
+        gbd = raster.render_gbuffer(g, sc, W, H, 4096, device)
+        torch.cuda.synchronize()
+        gb = {k: gbd[k].cpu().numpy() for k in ("albedo", "emissive", "normal", "velocity", "depth")}
+        shadow = gbd["shadow"].cpu().numpy()
+        del gbd
+    else:
+        gb = scene.gbuffer(g, W, H, scene_id=scene_id)
+        shadow = scene.shadow_map(g, 4096, scene_id=scene_id)
+    noise = scene.noise_texture()
+    fr = soc.alloc_frame(W, H, device, bloom_output=True)
+    for k in ("albedo", "emissive", "normal", "velocity", "depth"):
+        fr[k].copy_(torch.from_numpy(gb[k]))
+    fr["shadow"].copy_(torch.from_numpy(shadow))
+    fr["noise"].copy_(torch.from_numpy(noise))
+    return g, gb, shadow, noise, sc, fr
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -220,28 +251,9 @@ def main():
 
     # ---- inputs (Sponza-proxy mesh or terrain G-buffer + 4096^2 sun shadow map), resident in HBM ----
     terrain = args.config == "c4"
+    g, gb, shadow, noise, sc, fr = build_inputs(args.config, args.scene, W, H, rank, device, mips=not args.no_mips)
     scene_id = scene.TERRAIN if terrain else (scene.SPONZA_PROXY if args.scene == "boxes" else scene.SPONZA_MESH)
-    g = make_globals(W, H, (multi_gpu.terrain_camera_for_rank if terrain else multi_gpu.camera_for_rank)(rank))
-    if args.config == "c3b":
-        soc.scene_update(g, point_lights_c3b())
-    sc = None
-    if scene_id == scene.SPONZA_MESH:
-        # rasterised once by the HIP rasteriser (DepthPrepass + GBufferGeneration + SunShadowDraw), not timed
-        sc = raster.scene_setup(g, scene_id, tex_size=256, device=device, mips=not args.no_mips)
-        gbd = raster.render_gbuffer(g, sc, W, H, 4096, device)
-        torch.cuda.synchronize()
-        gb = {k: gbd[k].cpu().numpy() for k in ("albedo", "emissive", "normal", "velocity", "depth")}
-        shadow = gbd["shadow"].cpu().numpy()
-    else:
-        gb = scene.gbuffer(g, W, H, scene_id=scene_id)
-        shadow = scene.shadow_map(g, 4096, scene_id=scene_id)
-    noise = scene.noise_texture()
     f_sky = float((gb["depth"] == 1.0).mean())
-    fr = soc.alloc_frame(W, H, device, bloom_output=True)
-    for k in ("albedo", "emissive", "normal", "velocity", "depth"):
-        fr[k].copy_(torch.from_numpy(gb[k]))
-    fr["shadow"].copy_(torch.from_numpy(shadow))
-    fr["noise"].copy_(torch.from_numpy(noise))
     r = soc.Renderer(fr, sky_lane=not args.no_sky_lane, fused_histogram=not args.unfused_histogram)
     if args.raster:
         if sc is None:

@@ -479,6 +479,13 @@ int soc_renderer_pass_uses(const soc_renderer* r, int32_t index, uint64_t* reads
 /* Derived dependencies of pass `index`: the indices of the earlier passes it must follow (ascending).
  * Returns their count (at most cap are written) or a negative error. */
 int32_t soc_renderer_pass_dependencies(const soc_renderer* r, int32_t index, int32_t* out, int32_t cap);
+/* Derived cross-frame (ring) dependencies of pass `index`: the passes of the PREVIOUS frame it must follow, for the
+ * resources no earlier pass of its own frame writes (e.g. GBufferGeneration's depth write after the previous
+ * frame's CloudRendering read it; CloudRendering's sky-colour write after the previous frame's TAA read the colour).
+ * Indices ascending; returns their count (at most cap written) or a negative error. Cross-lane ring edges are
+ * enforced by waits on the source pass's completion event; the fork at the start of a call orders the second lane
+ * after everything queued on `stream` before the call. */
+int32_t soc_renderer_pass_carry_dependencies(const soc_renderer* r, int32_t index, int32_t* out, int32_t cap);
 /* Derived lane of pass `index` with the second lane enabled: 0 = the caller's stream, 1 = the second lane. */
 int32_t soc_renderer_pass_lane(const soc_renderer* r, int32_t index);
 

@@ -499,6 +499,14 @@ class Renderer:
             _check(int(n), "soc_renderer_pass_dependencies")
         return [int(buf[i]) for i in range(min(n, 64))]
 
+    def pass_carry_dependencies(self, index: int):
+        """Ring edges: indices of the PREVIOUS frame's passes this pass must follow (soc_renderer_pass_carry_dependencies)."""
+        buf = (C.c_int32 * 64)()
+        n = lib().soc_renderer_pass_carry_dependencies(self.handle, index, buf, 64)
+        if n < 0:
+            _check(int(n), "soc_renderer_pass_carry_dependencies")
+        return [int(buf[k]) for k in range(n)]
+
     def pass_lane(self, index: int) -> int:
         return int(lib().soc_renderer_pass_lane(self.handle, index))
 

@@ -230,6 +230,7 @@ FUNCTIONS = {
     "soc_renderer_add_pass": (_I, [_P, C.POINTER(PassDesc), PASS_CALLBACK, _P, C.c_char_p]),
     "soc_renderer_pass_uses": (_I, [_P, C.c_int32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "soc_renderer_pass_dependencies": (C.c_int32, [_P, C.c_int32, C.POINTER(C.c_int32), C.c_int32]),
+    "soc_renderer_pass_carry_dependencies": (C.c_int32, [_P, C.c_int32, C.POINTER(C.c_int32), C.c_int32]),
     "soc_renderer_pass_lane": (C.c_int32, [_P, C.c_int32]),
     "soc_renderer_set_pass_timing": (_I, [_P, C.c_int32, C.c_int32]),
     "soc_renderer_reset_timing": (_I, [_P]),

@@ -596,10 +596,13 @@ struct soc_renderer {
         PassFn run;
         std::function<bool()> skip;   // true: the pass has no work this call (no launch, no timing)
         std::vector<int> deps;        // derived: earlier passes this one must follow
+        std::vector<int> carry;       // derived: passes of the PREVIOUS frame this one must follow (ring edges)
+        bool signal = false;          // derived: a pass of the other lane depends on this one (records `done`)
         bool timed = false;
         std::vector<hipEvent_t> ev0, ev1;  // timing ring of SOC_RENDERER_TIMING_RING frames
         int next = 0, count = 0, last = -1;
         hipEvent_t done = nullptr;    // cross-lane completion event (created on first use)
+        bool done_recorded = false;   // `done` holds this pass's latest run
     };
     struct UserPass {
         soc_pass_desc desc;
@@ -657,17 +660,18 @@ soc_renderer::Pass& add_pass(soc_renderer* r, std::string name, std::string grou
     return r->passes.back();
 }
 
-int ensure_hist_scratch(soc_renderer* r) {
+// The fused histogram's 8 partial copies: allocated on the first PRE phase and cleared on the caller's stream
+// BEFORE the second lane is forked, so the fork orders the clear ahead of the sky lane's sky_compose bins.
+// (Round 2 cleared it with hipMemset on the null stream from inside the sky lane's pass: a non-blocking stream
+// is not ordered after null-stream work, so a first frame's sky bins could land before the clear and be wiped,
+// or land in stale memory: DESIGN.md §2.2.)
+int ensure_hist_scratch(soc_renderer* r, hipStream_t s) {
     if (r->hist_scratch) return SOC_OK;
     if (hipMalloc((void**)&r->hist_scratch, SOC_HISTOGRAM_SCRATCH_WORDS * sizeof(uint32_t)) != hipSuccess) {
         r->hist_scratch = nullptr;
         return set_error(SOC_E_HIP, "soc_renderer_execute: histogram scratch allocation failed");
     }
-    // hipMemset is queued on the null stream, which does not order the renderer's non-blocking second lane: the
-    // first call comes from the sky lane's pass (sky_compose bins into the scratch), so the clear must have
-    // landed before any lane's kernel runs (one device synchronisation, on the first frame only)
-    if (hipMemset(r->hist_scratch, 0, SOC_HISTOGRAM_SCRATCH_WORDS * sizeof(uint32_t)) != hipSuccess ||
-        hipDeviceSynchronize() != hipSuccess)
+    if (hipMemsetAsync(r->hist_scratch, 0, SOC_HISTOGRAM_SCRATCH_WORDS * sizeof(uint32_t), s) != hipSuccess)
         return set_error(SOC_E_HIP, "soc_renderer_execute: histogram scratch clear failed");
     return SOC_OK;
 }
@@ -789,8 +793,6 @@ void build_passes_tail(soc_renderer* r) {
                  int rc = soc_cloud_rendering(g, r->img.depth, r->img.noise, r->img.clouds, r->img.clouds_workspace,
                                               (soc_stream)s);
                  if (rc || !r->sky_split_active) return rc;
-                 rc = ensure_hist_scratch(r);
-                 if (rc) return rc;
                  return soc::sky_compose_launch(g, r->img.color, r->img.depth, r->img.clouds, r->hist_scratch,
                                                 (soc_stream)s);
              }, SOC_PASS_ASYNC);
@@ -803,8 +805,6 @@ void build_passes_tail(soc_renderer* r) {
                  res_mask({SOC_RES_COLOR, SOC_RES_HISTOGRAM_PARTIALS}), [r](const soc_globals* g, hipStream_t s) {
                      const auto& I = r->img;
                      const soc_img& em = I.bloom_output.data ? I.bloom_output : I.emissive;
-                     int rc = ensure_hist_scratch(r);
-                     if (rc) return rc;
                      return soc::composition_luminance_histogram(g, I.d_globals, I.color, I.albedo, em, I.normal, I.depth,
                                                                  I.ssao_blur, I.shadow, I.clouds, I.auto_exposure,
                                                                  r->hist_scratch, false, (soc_stream)s,
@@ -891,6 +891,16 @@ uint64_t desc_mask(const int32_t* ids, int32_t n) {
     return m;
 }
 
+// Under the sky split COLOR is the non-sky pixels and SKY_COLOR the sky pixels of the same image (and the partial
+// histograms have a sky copy): a caller pass declaring COLOR (or the partials) gets both, so it is ordered against
+// the second lane's sky writes too.
+uint64_t widen_sky(const soc_renderer* r, uint64_t m) {
+    if (!r->sky_split) return m;
+    if (m & (1ull << SOC_RES_COLOR)) m |= 1ull << SOC_RES_SKY_COLOR;
+    if (m & (1ull << SOC_RES_HISTOGRAM_PARTIALS)) m |= 1ull << SOC_RES_SKY_HISTOGRAM_PARTIALS;
+    return m;
+}
+
 // Insert the caller passes: before their anchor, or at the end of their phase. Returns an error for an
 // unknown or cross-phase anchor.
 int insert_user_passes(soc_renderer* r) {
@@ -899,8 +909,8 @@ int insert_user_passes(soc_renderer* r) {
         p.name = up.name;
         p.group = up.group;
         p.phase = up.desc.phase;
-        p.reads = desc_mask(up.desc.reads, up.desc.read_count);
-        p.writes = desc_mask(up.desc.writes, up.desc.write_count);
+        p.reads = widen_sky(r, desc_mask(up.desc.reads, up.desc.read_count));
+        p.writes = widen_sky(r, desc_mask(up.desc.writes, up.desc.write_count));
         p.flags = up.desc.flags;
         const soc_pass_callback fn = up.fn;
         void* user = up.user;
@@ -929,23 +939,47 @@ int insert_user_passes(soc_renderer* r) {
 
 // Dependencies from the declared uses: for every resource a pass reads, the latest earlier writer (RAW);
 // for every resource it writes, the latest earlier writer (WAW) and the readers since then (WAR).
+//
+// Cross-frame (ring) edges: the graph runs frame after frame, so the pass list is a ring. For a resource that no
+// earlier pass of its own frame writes, the walk goes on into the PREVIOUS frame, from the last pass back to the
+// pass itself: the latest writer there (RAW / WAW) and, for a write, the readers since that writer (WAR). The TAA
+// history pair swaps each frame (ping-pong: this frame's PREVIOUS_COLOR is the last frame's RESOLVED), so in the
+// previous frame the walk looks at the swapped resource. Example: GBufferGeneration writes DEPTH, which the
+// previous frame's CloudRendering (second lane) still reads: a WAR ring edge across the lanes.
+int prev_frame_resource(int b) {
+    if (b == SOC_RES_PREVIOUS_COLOR) return SOC_RES_RESOLVED;
+    if (b == SOC_RES_RESOLVED) return SOC_RES_PREVIOUS_COLOR;
+    return b;
+}
+
 void derive_dependencies(soc_renderer* r) {
     const int n = (int)r->passes.size();
     for (int i = 0; i < n; ++i) {
         auto& p = r->passes[i];
         p.deps.clear();
-        std::vector<char> dep(n, 0);
+        p.carry.clear();
+        std::vector<char> dep(n, 0), carry(n, 0);
         for (int b = 0; b < SOC_RES_COUNT; ++b) {
             const uint64_t bit = 1ull << b;
             if (!((p.reads | p.writes) & bit)) continue;
-            for (int j = i - 1; j >= 0; --j) {
+            bool writer = false;
+            for (int j = i - 1; j >= 0 && !writer; --j) {
                 const auto& q = r->passes[j];
-                if (q.writes & bit) { dep[j] = 1; break; }              // RAW / WAW: the latest writer
-                if ((p.writes & bit) && (q.reads & bit)) dep[j] = 1;    // WAR: readers since that writer
+                if (q.writes & bit) { dep[j] = 1; writer = true; }       // RAW / WAW: the latest writer
+                else if ((p.writes & bit) && (q.reads & bit)) dep[j] = 1; // WAR: readers since that writer
+            }
+            if (writer) continue;
+            const uint64_t pbit = 1ull << prev_frame_resource(b);
+            for (int j = n - 1; j >= i; --j) {                           // the previous frame, back to pass i itself
+                const auto& q = r->passes[j];
+                if (q.writes & pbit) { carry[j] = 1; break; }
+                if ((p.writes & bit) && (q.reads & pbit)) carry[j] = 1;
             }
         }
-        for (int j = 0; j < i; ++j)
+        for (int j = 0; j < n; ++j) {
             if (dep[j]) p.deps.push_back(j);
+            if (carry[j]) p.carry.push_back(j);
+        }
     }
 }
 
@@ -957,6 +991,19 @@ void destroy_pass_events(soc_renderer* r) {
     }
 }
 
+// A pass records its completion event when a pass of the other lane depends on it, in its own frame or the next.
+void derive_signals(soc_renderer* r) {
+    const int n = (int)r->passes.size();
+    for (auto& p : r->passes) p.signal = false;
+    for (int i = 0; i < n; ++i) {
+        const bool li = (r->passes[i].flags & SOC_PASS_ASYNC) != 0;
+        for (int j : r->passes[i].deps)
+            if (((r->passes[j].flags & SOC_PASS_ASYNC) != 0) != li) r->passes[j].signal = true;
+        for (int j : r->passes[i].carry)
+            if (((r->passes[j].flags & SOC_PASS_ASYNC) != 0) != li) r->passes[j].signal = true;
+    }
+}
+
 int build_graph(soc_renderer* r) {
     destroy_pass_events(r);
     r->passes.clear();
@@ -965,6 +1012,7 @@ int build_graph(soc_renderer* r) {
     build_passes_tail(r);
     int rc = insert_user_passes(r);
     derive_dependencies(r);
+    derive_signals(r);
     return rc;
 }
 }  // namespace
@@ -1045,7 +1093,7 @@ static int ensure_side_lane(soc_renderer* r) {
         (void)hipEventDestroy(r->fork_ev);
         (void)hipEventDestroy(r->join_ev);
         for (auto& p : r->passes)
-            if (p.done) { (void)hipEventDestroy(p.done); p.done = nullptr; }
+            if (p.done) { (void)hipEventDestroy(p.done); p.done = nullptr; p.done_recorded = false; }
         r->side = nullptr;
         r->fork_ev = r->join_ev = nullptr;
     }
@@ -1062,6 +1110,23 @@ static int ensure_side_lane(soc_renderer* r) {
     return SOC_OK;
 }
 
+// Lane of pass i with the second lane on or off: 0 = the caller's stream, 1 = the renderer's second lane.
+static int static_lane(const soc_renderer* r, int i) {
+    return (r->async && (r->passes[i].flags & SOC_PASS_ASYNC)) ? 1 : 0;
+}
+
+// An aborted frame (a pass or a caller pass returned an error after the fork): join the second lane so nothing of
+// this call is left unordered against the caller's next work, and drop the frame's partial histograms (the resolve
+// that would clear them did not run) so they are not counted into the next frame's exposure. The TAA history is
+// not flipped: the next frame reads the last completed frame's history.
+static int abort_frame(soc_renderer* r, hipStream_t s, bool forked, int rc) {
+    if (forked && r->side && hipEventRecord(r->join_ev, r->side) == hipSuccess) (void)hipStreamWaitEvent(s, r->join_ev, 0);
+    if (r->hist_scratch) (void)hipMemsetAsync(r->hist_scratch, 0, SOC_HISTOGRAM_SCRATCH_WORDS * sizeof(uint32_t), s);
+    if (r->img.auto_exposure)
+        (void)hipMemsetAsync(r->img.auto_exposure->histogram_buckets, 0, sizeof(r->img.auto_exposure->histogram_buckets), s);
+    return rc;
+}
+
 extern "C" int soc_renderer_execute(soc_renderer* r, const soc_globals* g, int32_t phase, soc_stream stream) {
     if (!r || !g) return set_error(SOC_E_INVALID_ARG, "soc_renderer_execute: null argument");
     hipStream_t s = hs(stream);
@@ -1074,6 +1139,10 @@ extern "C" int soc_renderer_execute(soc_renderer* r, const soc_globals* g, int32
         if (r->sky_split && !r->sky_split_active)
             return set_error(SOC_E_SHAPE, "soc_renderer_execute: globals resolution %dx%d differs from the frame images %dx%d",
                              g->resolution[0], g->resolution[1], r->img.color.width, r->img.color.height);
+        if (!(r->flags & SOC_RENDERER_UNFUSED_HISTOGRAM)) {   // the fused histogram's partial copies, cleared on `s`
+            int rc = ensure_hist_scratch(r, s);
+            if (rc) return rc;
+        }
     }
     if ((phase & SOC_PHASE_PRE_EXPOSURE) && (g->point_light_count || g->spot_light_count)) {
         int rc = upload_lights(r, g, s);
@@ -1086,7 +1155,7 @@ extern "C" int soc_renderer_execute(soc_renderer* r, const soc_globals* g, int32
     for (int i = 0; i < n; ++i) {
         const auto& p = r->passes[i];
         if (!(p.phase & phase) || (p.skip && p.skip())) continue;
-        lane[i] = (r->async && (p.flags & SOC_PASS_ASYNC)) ? 1 : 0;
+        lane[i] = static_lane(r, i);
         lanes |= lane[i] == 1;
     }
     // dependencies among the passes run by this call; a skipped pass (no work this call) hands its own
@@ -1100,16 +1169,23 @@ extern "C" int soc_renderer_execute(soc_renderer* r, const soc_globals* g, int32
             else if (r->passes[j].phase & phase) deps[i].insert(deps[i].end(), deps[j].begin(), deps[j].end());
         }
     }
-    // a pass records its completion event when a pass of the other lane depends on it
-    std::vector<char> signal(n, 0);
-    for (int i = 0; i < n; ++i)
-        if (lane[i] >= 0)
-            for (int j : deps[i])
-                if (lane[j] != lane[i]) signal[j] = 1;
+    // Edges whose source is not run by this call, onto the other lane: the ring edges to the previous frame
+    // (pass.carry) and this frame's edges to a pass of another phase's call (PRE -> POST of a multi-GPU frame).
+    // Each waits on the source's latest `done` event; on the same lane stream order covers them.
+    std::vector<std::vector<int>> ext(n);
+    for (int i = 0; i < n; ++i) {
+        if (lane[i] < 0) continue;
+        const auto& p = r->passes[i];
+        for (int j : p.carry)
+            if (static_lane(r, j) != lane[i]) ext[i].push_back(j);
+        for (int j : p.deps)
+            if (lane[j] < 0 && !(r->passes[j].phase & phase) && static_lane(r, j) != lane[i]) ext[i].push_back(j);
+    }
     if (lanes) {
         int rc = ensure_side_lane(r);
         if (rc) return rc;
-        // fork: the second lane starts after everything the caller queued before this call
+        // fork (the frame-inputs edge): the second lane starts after everything the caller queued before this
+        // call (e.g. the depth image it uploaded)
         if (hipEventRecord(r->fork_ev, s) != hipSuccess || hipStreamWaitEvent(r->side, r->fork_ev, 0) != hipSuccess)
             return set_error(SOC_E_HIP, "soc_renderer_execute: second lane fork failed");
     }
@@ -1130,26 +1206,38 @@ extern "C" int soc_renderer_execute(soc_renderer* r, const soc_globals* g, int32
             order.insert(order.end(), rest.begin(), rest.end());
         }
     }
+    int last_side = -1;            // the second lane's last pass of this call
+    bool side_joined = false;      // a later main-lane pass of this call waits on it
     for (int oi = 0; oi < n; ++oi) {
         const int i = order[oi];
         if (lane[i] < 0) continue;
         auto& p = r->passes[i];
         hipStream_t ls = lane[i] ? r->side : s;
         for (int j : deps[i])
-            if (lane[j] != lane[i] && hipStreamWaitEvent(ls, r->passes[j].done, 0) != hipSuccess)
-                return set_error(SOC_E_HIP, "soc_renderer_execute: %s: cross-lane wait failed", p.name.c_str());
+            if (lane[j] != lane[i]) {
+                if (hipStreamWaitEvent(ls, r->passes[j].done, 0) != hipSuccess)
+                    return abort_frame(r, s, lanes, set_error(SOC_E_HIP, "soc_renderer_execute: %s: cross-lane wait failed", p.name.c_str()));
+                if (lane[i] == 0 && j == last_side) side_joined = true;
+            }
+        for (int j : ext[i])
+            if (r->passes[j].done_recorded && hipStreamWaitEvent(ls, r->passes[j].done, 0) != hipSuccess)
+                return abort_frame(r, s, lanes, set_error(SOC_E_HIP, "soc_renderer_execute: %s: ring-edge wait failed", p.name.c_str()));
         int rc = run_pass(p, g, ls);
-        if (rc) return rc;
-        if (signal[i]) {
+        if (rc) return abort_frame(r, s, lanes, rc);
+        if (p.signal) {
             if (!p.done && hipEventCreateWithFlags(&p.done, hipEventDisableTiming) != hipSuccess)
-                return set_error(SOC_E_HIP, "soc_renderer_execute: hipEventCreate failed");
+                return abort_frame(r, s, lanes, set_error(SOC_E_HIP, "soc_renderer_execute: hipEventCreate failed"));
             if (hipEventRecord(p.done, ls) != hipSuccess)
-                return set_error(SOC_E_HIP, "soc_renderer_execute: %s: event record failed", p.name.c_str());
+                return abort_frame(r, s, lanes, set_error(SOC_E_HIP, "soc_renderer_execute: %s: event record failed", p.name.c_str()));
+            p.done_recorded = true;
         }
+        if (lane[i] == 1) { last_side = i; side_joined = false; }
     }
-    // join: everything of this call is ordered before whatever the caller queues next on `stream`
-    if (lanes && (hipEventRecord(r->join_ev, r->side) != hipSuccess || hipStreamWaitEvent(s, r->join_ev, 0) != hipSuccess))
-        return set_error(SOC_E_HIP, "soc_renderer_execute: second lane join failed");
+    // join (the caller's edge, not the graph's): everything of this call is ordered before whatever the caller
+    // queues next on `stream`. Skipped when a main-lane pass already waited on the second lane's last pass.
+    if (lanes && !side_joined &&
+        (hipEventRecord(r->join_ev, r->side) != hipSuccess || hipStreamWaitEvent(s, r->join_ev, 0) != hipSuccess))
+        return abort_frame(r, s, false, set_error(SOC_E_HIP, "soc_renderer_execute: second lane join failed"));
     if (phase & SOC_PHASE_POST_EXPOSURE) r->hist = 1 - r->hist;   // ping-pong the TAA history
     return SOC_OK;
 }
@@ -1218,6 +1306,14 @@ extern "C" int32_t soc_renderer_pass_dependencies(const soc_renderer* r, int32_t
     if (!r || i < 0 || i >= (int32_t)r->passes.size() || cap < 0 || (cap > 0 && !out))
         return set_error(SOC_E_INVALID_ARG, "soc_renderer_pass_dependencies: bad arguments");
     const auto& d = r->passes[i].deps;
+    for (int k = 0; k < (int)d.size() && k < cap; ++k) out[k] = d[k];
+    return (int32_t)d.size();
+}
+
+extern "C" int32_t soc_renderer_pass_carry_dependencies(const soc_renderer* r, int32_t i, int32_t* out, int32_t cap) {
+    if (!r || i < 0 || i >= (int32_t)r->passes.size() || cap < 0 || (cap > 0 && !out))
+        return set_error(SOC_E_INVALID_ARG, "soc_renderer_pass_carry_dependencies: bad arguments");
+    const auto& d = r->passes[i].carry;
     for (int k = 0; k < (int)d.size() && k < cap; ++k) out[k] = d[k];
     return (int32_t)d.size();
 }

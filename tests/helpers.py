@@ -57,12 +57,15 @@ def random_rgba16(H, W, seed, lo=0.0, hi=4.0, alpha=1.0):
     return a.astype(np.float16)
 
 
-def f16_close(a, b, atol=1e-3, rtol=2e-3):
-    """|a-b| <= atol + rtol*|b| on RGBA16F images (float16 arrays); NaNs must match."""
+def f16_close(a, b, atol=1e-3, rtol=2e-3, nan_mismatch=0.0):
+    """|a-b| <= atol + rtol*|b| on RGBA16F images (float16 arrays); NaNs must match (on all but a `nan_mismatch`
+    fraction of the values: for inputs where a NaN comes from an argument rounding across a domain edge, e.g. the
+    reference's acos(dot(h, n)) of a not-renormalised G-buffer normal, composition.inl:133)."""
     a = np.asarray(a, np.float32)
     b = np.asarray(b, np.float32)
     nan = np.isnan(a) | np.isnan(b)
-    assert (np.isnan(a) == np.isnan(b)).all(), "NaN pattern differs"
+    differ = np.isnan(a) != np.isnan(b)
+    assert differ.mean() <= nan_mismatch, f"NaN pattern differs on {differ.mean():.2e} of the values"
     d = np.abs(a - b)
     ok = (d <= atol + rtol * np.abs(b)) | nan
     return ok
@@ -108,3 +111,16 @@ def sponza_mesh_inputs(W, H, shadow_size=512, tex_size=64, **kw):
     gb["noise"] = scene.noise_texture()
     gb["visibility"] = vis
     return g, gb
+
+
+_MESH_CACHE = {}
+
+
+def mesh_inputs(W, H, **kw):
+    """sponza_mesh_inputs, memoised per (W, H, kw) within a test session (the oracle raster of the ~261k-triangle mesh
+    at 1920x1080 takes seconds); every call returns fresh copies of the arrays."""
+    key = (W, H, repr(sorted(kw.items())))
+    if key not in _MESH_CACHE:
+        _MESH_CACHE[key] = sponza_mesh_inputs(W, H, **kw)
+    g, gb = _MESH_CACHE[key]
+    return g, {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in gb.items()}

@@ -1,0 +1,54 @@
+"""The benchmarked configuration at its own size: bench.py's default command (C3) rendered by the render graph at
+3840x2160 and compared with the oracle's frame of the same inputs.
+
+The inputs come from bench.build_inputs, exactly as the bench builds them: the Sponza-proxy mesh rasterised once by
+the HIP rasteriser (mip-mapped anisotropic textures), the 4096^2 sun shadow map, the C3 globals (elapsed 10 s,
+frame counter 2). The renderer runs the bench's graph: the concurrent sky lane, the sky split, the AO-first issue
+order, the fused composition + histogram and the fused TAA + tone map. Two frames (the second one resolves TAA
+against the first one's history). Tolerances: colour |d| <= 4e-3 + 8e-3|ref| on >= 99.9 % of the
+pixels (two frames of TAA), framebuffer within 2 levels on >= 99.5 %, SSAO within 2/255 on >= 99.5 % with mean
+<= 0.5/255, exposure within 1e-4. Reference: renderer.cpp:1024-1217."""
+import numpy as np
+import pytest
+import torch
+
+from helpers import f16_close, host_frame
+
+pytestmark = pytest.mark.gpu
+
+
+def test_c3_bench_frame_4k_vs_oracle(soc, oracle):
+    import bench
+    W, H = 3840, 2160
+    dev = torch.device("cuda", 0)
+    g, gb, shadow, noise, sc, fr = bench.build_inputs("c3", "mesh", W, H, 0, dev)
+    r = soc.Renderer(fr)                               # the bench's renderer flags (defaults)
+    r.set_exposure_pixels(W * H, False)
+    assert r.pass_names() == ["BloomDownsample - 0+1", "BloomDownsample - 2+3", "BloomUpsample - 3+2",
+                              "BloomUpsample - 1+0", "SSAOGeneration", "SSAOBlur", "CloudRendering",
+                              "Composition+GenerateLuminanceHistogram", "LuminanceHistogramFold",
+                              "ResolveLuminanceHistogram", "TemporalAntiAliasing+ToneMapping"]
+    assert r.pass_lane(r.pass_names().index("CloudRendering")) == 1
+    f_sky = float((gb["depth"] == 1.0).mean())
+    assert 0.05 < f_sky < 0.2, f_sky
+    hf = host_frame(W, H, {**gb, "shadow": shadow, "noise": noise})
+    ae = soc.AutoExposure()
+    hist = 0
+    for f in range(2):
+        r.execute(g)
+        hf["emissive"][...] = gb["emissive"]          # the bench writes bloom into bloom_output (emissive kept)
+        hist = oracle.frame(g, hf, ae, hist=hist)
+        torch.cuda.synchronize()
+        assert r.current_history() == hist
+        ssao = fr["ssao"].cpu().numpy()
+        d = np.abs(ssao.astype(np.int32) - hf["ssao"].astype(np.int32))
+        assert (d <= 2).mean() >= 0.995 and d.mean() <= 0.5, (f, (d <= 2).mean(), d.mean())
+        ok = f16_close(fr["color"].cpu().numpy(), hf["color"], atol=4e-3, rtol=8e-3)
+        assert ok.mean() >= 0.999, (f, ok.mean())
+        sky = gb["depth"] == 1.0                       # the sky pixels, written by the second lane
+        assert ok[sky].mean() >= 0.999, (f, ok[sky].mean())
+        d = np.abs(fr["output"].cpu().numpy().astype(np.int32) - hf["output"].astype(np.int32))
+        assert (d <= 2).mean() >= 0.995, (f, (d <= 2).mean())
+        assert abs(soc.exposure_of(fr["auto_exposure"]) - ae.exposure) <= 1e-4, (f, soc.exposure_of(fr["auto_exposure"]),
+                                                                                ae.exposure)
+    r.close()

@@ -9,7 +9,8 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import (f16_close, globals_for, host_frame, random_rgba16, random_shadow, sponza_inputs, terrain_inputs)
+from helpers import (f16_close, globals_for, host_frame, mesh_inputs, random_rgba16, random_shadow, sponza_inputs,
+                     terrain_inputs)
 
 pytestmark = pytest.mark.gpu
 
@@ -167,9 +168,11 @@ def test_bloom_weighted_in_place(soc):
 
 
 # ------------------------------------------------------------------------------------------------ ssao
-@pytest.mark.parametrize("W,H", [(128, 72), (97, 55), (1920, 1080)])
-def test_ssao_generation(soc, oracle, W, H):
-    g, gb = sponza_inputs(W, H)
+@pytest.mark.parametrize("W,H,inputs", [(128, 72, "boxes"), (97, 55, "boxes"), (1920, 1080, "boxes"),
+                                         (1920, 1080, "mesh"), (961, 541, "mesh")])
+def test_ssao_generation(soc, oracle, W, H, inputs):
+    """boxes: the box atrium; mesh: the Sponza-proxy mesh the bench renders (curved, normal-mapped surfaces)."""
+    g, gb = (sponza_inputs if inputs == "boxes" else mesh_inputs)(W, H)
     ref = np.zeros((H // 2, W // 2), np.uint8)
     oracle.ssao_generation(g, gb["depth"], gb["normal"], ref)
     out = torch.zeros(H // 2, W // 2, dtype=torch.uint8, device=DEV)
@@ -241,10 +244,11 @@ def test_composition_cache_policy_variants_bit_identical(soc, monkeypatch):
     assert np.array_equal(outs[0].view(np.uint16), outs[1].view(np.uint16))
 
 
-@pytest.mark.parametrize("W,H", [(64, 36), (97, 55), (512, 288), (1920, 1080)])
+@pytest.mark.parametrize("W,H,inputs", [(64, 36, "boxes"), (97, 55, "boxes"), (512, 288, "boxes"), (1920, 1080, "boxes"),
+                                         (1920, 1080, "mesh")])
 @pytest.mark.parametrize("lights", [0, 3])
-def test_composition(soc, oracle, W, H, lights):
-    g, gb = sponza_inputs(W, H)
+def test_composition(soc, oracle, W, H, inputs, lights):
+    g, gb = (sponza_inputs if inputs == "boxes" else mesh_inputs)(W, H)
     shadow = random_shadow(256, seed=W)
     rng = np.random.default_rng(W + lights)
     ssao = rng.integers(120, 256, (H // 2, W // 2), dtype=np.uint8)
@@ -270,7 +274,15 @@ def test_composition(soc, oracle, W, H, lights):
     soc.composition(g, out, dev(gb["albedo"]), dev(gb["emissive"]), dev(gb["normal"]), dev(gb["depth"]), dev(ssao),
                     dev(shadow), dev(clouds), d_globals=dg)
     got = host(out)
-    ok = f16_close(got, ref)
+    # the mesh's normal-mapped G-buffer normals are not unit length after RGBA16F rounding, and the reference feeds
+    # them to acos(dot(halfway, normal)) unnormalised (composition.inl:133, 154): |dot| > 1 gives NaN on both sides,
+    # but which pixels round across 1 depends on the dot's rounding (0.16 % of the pixels at 1080p, 3 + 3 lights)
+    nan_tol = 5e-3 if (inputs == "mesh" and lights) else 0.0
+    ok = f16_close(got, ref, nan_mismatch=nan_tol)
+    if nan_tol:
+        both = ~(np.isnan(got.astype(np.float32)) | np.isnan(ref.astype(np.float32)))
+        assert abs(np.isnan(got.astype(np.float32)).mean() - np.isnan(ref.astype(np.float32)).mean()) < 1e-3
+        ok = ok | ~both
     assert ok.all(), (ok.mean(), np.argwhere(~ok)[:5])
     sky = gb["depth"] == 1.0
     assert np.array_equal(got[sky].view(np.uint16), ref[sky].view(np.uint16))   # sky = clouds texel, exact
@@ -382,9 +394,9 @@ def test_resolve(soc, oracle, wide):
 
 
 # ------------------------------------------------------------------------------------------------ TAA
-@pytest.mark.parametrize("W,H", [(64, 36), (97, 55), (1920, 1080)])
-def test_taa(soc, oracle, W, H):
-    g, gb = sponza_inputs(W, H)
+@pytest.mark.parametrize("W,H,inputs", [(64, 36, "boxes"), (97, 55, "boxes"), (1920, 1080, "boxes"), (1920, 1080, "mesh")])
+def test_taa(soc, oracle, W, H, inputs):
+    g, gb = (sponza_inputs if inputs == "boxes" else mesh_inputs)(W, H)
     cur = random_rgba16(H, W, seed=1, hi=3.0)
     prev = random_rgba16(H, W, seed=2, hi=3.0)
     pvel = gb["velocity"].copy()
@@ -483,10 +495,14 @@ def test_tone_mapping(soc, oracle, W, H, fmt):
 
 
 # ------------------------------------------------------------------------------------------------ clouds
-@pytest.mark.parametrize("W,H,pitch", [(96, 64, -0.42), (160, 90, -0.9), (480, 270, -0.42), (1920, 1080, -0.6)])
+@pytest.mark.parametrize("W,H,pitch,inputs", [(96, 64, -0.42, "boxes"), (160, 90, -0.9, "boxes"), (480, 270, -0.42, "boxes"),
+                                               (1920, 1080, -0.6, "boxes"), (1920, 1080, -0.42, "mesh")])
 @pytest.mark.parametrize("compact", [False, True])
-def test_clouds(soc, oracle, W, H, pitch, compact):
-    g, gb = sponza_inputs(W, H, camera=((-14.0, 2.2, 0.3), (0.0, pitch, 0.0)), elapsed=10.0)
+def test_clouds(soc, oracle, W, H, pitch, inputs, compact):
+    g, gb = (sponza_inputs if inputs == "boxes" else mesh_inputs)(W, H, camera=((-14.0, 2.2, 0.3), (0.0, pitch, 0.0)),
+                                                                  elapsed=10.0)
+    if inputs == "mesh":
+        assert (gb["depth"] == 1.0).mean() > 0.05
     ref = np.zeros((H, W, 4), np.uint8)
     oracle.cloud_rendering(g, gb["depth"], gb["noise"], ref)
     out = torch.zeros(H, W, 4, dtype=torch.uint8, device=DEV)

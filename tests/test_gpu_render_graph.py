@@ -70,3 +70,53 @@ def test_async_caller_pass_and_its_consumer(soc):
     torch.cuda.synchronize()
     assert torch.equal(seen, fr["depth"])
     r.close()
+
+
+@pytest.mark.parametrize("where", ["post", "pre"])
+def test_aborted_frame_leaves_next_frame_exact(soc, oracle, where):
+    """A caller pass that returns an error aborts its frame after the second lane was forked: the call
+    returns the error, joins the second lane, and drops the frame's partial histograms (the composition's and the
+    sky lane's bins, which the resolve would have folded and cleared). The next frame then equals the oracle's frame
+    that follows the last COMPLETED frame: same colour, framebuffer and exposure, and the TAA history of that frame.
+    post: the failing pass sits before the resolve (every PRE pass ran, bins in the scratch); pre: before the
+    composition (the sky lane's bins only)."""
+    from helpers import host_frame, terrain_inputs
+    W, H = 320, 180
+    g, gb = terrain_inputs(W, H, elapsed=10.0)       # half the frame is sky: the sky lane bins many pixels
+    fr = _frame(soc, W, H, gb)
+    r = soc.Renderer(fr)
+    calls = []
+
+    def flaky(gp, images, stream):
+        calls.append(1)
+        return -7 if len(calls) == 2 else 0
+    if where == "post":
+        r.add_pass("Flaky", flaky, reads=["COLOR"], writes=[soc._abi.RES_USER0], phase=soc.PHASE_POST_EXPOSURE,
+                   before="ResolveLuminanceHistogram")
+    else:
+        r.add_pass("Flaky", flaky, reads=["SSAO_BLUR"], writes=[soc._abi.RES_USER0],
+                   before="Composition+GenerateLuminanceHistogram")
+    hf = host_frame(W, H, gb)
+    ae = soc.AutoExposure()
+    hist = 0
+    for f in range(3):
+        fr["emissive"].copy_(torch.from_numpy(gb["emissive"]))
+        if f == 1:
+            with pytest.raises(soc.SocError, match="-7|caller pass"):
+                r.execute(g)
+            torch.cuda.synchronize()
+            assert int(fr["auto_exposure"][1:].abs().sum()) == 0     # no partial bins left for the next frame
+            continue
+        r.execute(g)
+        hf["emissive"][...] = gb["emissive"]
+        hist = oracle.frame(g, hf, ae, hist=hist)
+        torch.cuda.synchronize()
+        assert r.current_history() == hist
+        ok = f16_close(fr["color"].cpu().numpy(), hf["color"], atol=4e-3, rtol=8e-3)
+        assert ok.mean() >= 0.999, (f, ok.mean())
+        d = np.abs(fr["output"].cpu().numpy().astype(np.int32) - hf["output"].astype(np.int32))
+        assert (d <= 2).mean() >= 0.995, (f, (d <= 2).mean())
+        assert abs(soc.exposure_of(fr["auto_exposure"]) - ae.exposure) <= 1e-4, (f, soc.exposure_of(fr["auto_exposure"]),
+                                                                                ae.exposure)
+    assert len(calls) == 3
+    r.close()

@@ -164,3 +164,77 @@ def test_caller_passes_survive_raster_scene_changes(soc):
     r.add_pass("RawAO", lambda *a: 0, reads=["SSAO"], writes=["SSAO_BLUR"], before="Composition+GenerateLuminanceHistogram")
     assert soc.lib().soc_renderer_set_raster_scene(r.handle, None) == 0
     assert "RawAO" in r.pass_names()
+
+
+def _carry(r):
+    names = r.pass_names()
+    return {names[i]: {names[j] for j in r.pass_carry_dependencies(i)} for i in range(len(names))}
+
+
+def _cross_lane_ring_edges(r):
+    names = r.pass_names()
+    return {(names[i], names[j]) for i in range(len(names)) for j in r.pass_carry_dependencies(i)
+            if r.pass_lane(i) != r.pass_lane(j)}
+
+
+def _raster_renderer(soc, **kw):
+    r = _renderer(soc, **kw)
+    sc = soc._abi.RasterScene()
+    for f in ("positions", "normals", "uvs", "indices"):
+        setattr(sc.mesh, f, 1)
+    sc.mesh.vertex_count, sc.mesh.triangle_count = 3, 1
+    sc.materials, sc.material_count, sc.shadow, sc.visibility, sc.workspace = 1, 1, 1, 1, 1
+    assert soc.lib().soc_renderer_set_raster_scene(r.handle, C.byref(sc)) == 0
+    return r
+
+
+def test_ring_edges(soc):
+    """Cross-frame dependencies: the pass list as a ring (renderer.cpp:1155-1217 run frame after frame)."""
+    r = _renderer(soc)
+    c = _carry(r)
+    # the second lane's sky writes follow the previous frame's readers of the colour's sky pixels (TAA) and the
+    # resolve that folded and cleared the partial bins; CLOUDS is rewritten by the pass itself
+    assert c["CloudRendering"] == {"CloudRendering", "ResolveLuminanceHistogram", "TemporalAntiAliasing+ToneMapping"}
+    # composition's colour write follows the previous frame's TAA read and its own write (same lane); its partials
+    # follow the resolve
+    assert c["Composition+GenerateLuminanceHistogram"] == {"Composition+GenerateLuminanceHistogram",
+                                                           "ResolveLuminanceHistogram", "TemporalAntiAliasing+ToneMapping"}
+    # the TAA history ping-pong: this frame's PREVIOUS_COLOR is the last frame's RESOLVED (and vice versa)
+    assert c["TemporalAntiAliasing+ToneMapping"] == {"TemporalAntiAliasing+ToneMapping"}
+    # the bloom writes follow the previous frame's readers of its mips / output (same lane)
+    assert "Composition+GenerateLuminanceHistogram" in c["BloomUpsample - 1+0"]
+    assert _cross_lane_ring_edges(r) == {("CloudRendering", "ResolveLuminanceHistogram"),
+                                         ("CloudRendering", "TemporalAntiAliasing+ToneMapping")}
+
+
+def test_ring_edges_raster_head(soc):
+    """With a raster head the G-buffer pass rewrites depth every frame: it must follow the previous frame's
+    CloudRendering (second lane), which reads depth: the cross-lane WAR edge the end-of-call join used to cover."""
+    r = _raster_renderer(soc)
+    c = _carry(r)
+    assert "CloudRendering" in c["GBufferGeneration"]
+    assert {"SSAOGeneration", "TemporalAntiAliasing+ToneMapping"} <= c["GBufferGeneration"]
+    assert c["DepthPrepass"] == {"DepthPrepass", "GBufferGeneration"}   # WAW / WAR on the visibility buffer
+    assert _cross_lane_ring_edges(r) == {("CloudRendering", "ResolveLuminanceHistogram"),
+                                         ("CloudRendering", "TemporalAntiAliasing+ToneMapping"),
+                                         ("GBufferGeneration", "CloudRendering")}
+
+
+def test_ring_edges_without_sky_split(soc):
+    r = _renderer(soc, sky_split=False)
+    # CloudRendering rewrites CLOUDS, which the previous frame's composition read (across the lanes)
+    assert _cross_lane_ring_edges(r) == {("CloudRendering", "Composition+GenerateLuminanceHistogram")}
+
+
+def test_caller_colour_use_includes_sky_pixels(soc):
+    """Under the sky split a caller pass declaring COLOR also orders against the second lane's sky writes."""
+    r = _renderer(soc)
+    r.add_pass("ColorProbe", lambda *a: 0, reads=["COLOR"], writes=[soc._abi.RES_USER0], phase=soc.PHASE_POST_EXPOSURE,
+               before="TemporalAntiAliasing+ToneMapping")
+    names = r.pass_names()
+    i = names.index("ColorProbe")
+    assert r.pass_uses(i)[0] == {"COLOR", "SKY_COLOR"}
+    assert "CloudRendering" in _deps(r)["ColorProbe"]
+    r2 = _renderer(soc, sky_split=False)
+    r2.add_pass("ColorProbe", lambda *a: 0, reads=["COLOR"], phase=soc.PHASE_POST_EXPOSURE)
+    assert r2.pass_uses(r2.pass_names().index("ColorProbe"))[0] == {"COLOR"}
