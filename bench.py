@@ -86,10 +86,8 @@ def algorithmic_bytes(W, H, f_sky):
         "BloomDownsample - 0": 16.0 * P, "BloomDownsample - 1": (8.0 + 2.0) * P, "BloomDownsample - 2": (2.0 + 0.5) * P,
         "BloomDownsample - 3": (0.5 + 0.125) * P, "BloomUpsample - 3": (0.125 + 0.5) * P,
         "BloomUpsample - 2": (0.5 + 2.0) * P, "BloomUpsample - 1": (2.0 + 8.0) * P, "BloomUpsample - 0": 16.0 * P,
-        # fused stages (bloom_fused.hip): mip0 / mip2 of the downsweep never leave LDS (stages 3-4
-        # are available through soc_bloom_fused_stage but not scheduled: slower than per-pass)
+        # weighted-form chain (bloom_w.hip): mip0 / mip2 stay in LDS (emissive -> mip1 -> mip3 -> mip1 -> output)
         "BloomDownsample - 0+1": (8.0 + 2.0) * P, "BloomDownsample - 2+3": (2.0 + 0.125) * P,
-        # weighted-form upsweep (bloom_w.hip): mip2 / mip0 stay in LDS (mip3 -> mip1, mip1 -> output)
         "BloomUpsample - 3+2": (0.125 + 2.0) * P, "BloomUpsample - 1+0": (2.0 + 8.0) * P,
         "SSAOGeneration": 12.25 * P, "SSAOBlur": 0.5 * P, "CloudRendering": 8.0 * P,
         "Composition": (40.25 + 4.0 * f_sky) * P, "GenerateLuminanceHistogram": 8.0 * P,

@@ -248,26 +248,17 @@ int soc_bloom_upsample(const soc_globals* g, soc_img lower_mip, soc_img higher_m
 
 /* Whole bloom chain as scheduled by renderer.cpp:1024-1062: down(emissive->mip0), down(mip i ->
  * mip i+1), up(mip i -> mip i-1), up(mip0 -> emissive). `mips` holds mip_count images (4 in the
- * reference, renderer.hpp:51). With 4 exactly halving mips the downsweep runs as fused stages 1-2 of
- * soc_bloom_fused_stage (same bits in every mip and in emissive), otherwise as 4 passes. */
+ * reference, renderer.hpp:51). The reference's 8 passes, bit-exact. */
 int soc_bloom_chain(const soc_globals* g, soc_img emissive, const soc_img* mips, int32_t mip_count,
                     soc_stream stream);
-
-/* One stage of the fused bloom chain (4 mips, each exactly half the previous, mips[0] the size of
- * emissive; SOC_E_UNSUPPORTED otherwise). stage 1: emissive -> mip1 (mip0 stays in LDS);
- * 2: mip1 -> mip3 (mip2 in LDS); 3: mip3 -> mip2 -> mip1; 4: mip1 -> mip0 -> output; 0: all four.
- * `output` is the final upsample's target (emissive itself for the in-place reference graph). After
- * stage 4 every mip and `output` hold exactly what the 8-pass chain leaves there. */
-int soc_bloom_fused_stage(const soc_globals* g, soc_img emissive, const soc_img* mips, int32_t mip_count, soc_img output,
-                          int32_t stage, soc_stream stream);
 
 /* The bloom chain in weighted form (bloom_w.hip): at the chain's fixed ratios every tap of the sampling
  * contract has exact weights on clamp-to-edge texels, so each pass is evaluated as one fixed weighted
  * sum of RGBA16F texels with fp32 FMAs (same weights, different rounding order: within the RGBA16F
  * tolerance, not bit-exact). Stages: 1 emissive -> [mip0] -> mips[1], 2 mips[1] -> [mip2] -> mips[3],
  * 3 mips[3] -> [mip2] -> mips[1], 4 mips[1] -> [mip0] -> output; 0 = all four. mips[0] and mips[2] are
- * scratch (never written: their final contents are unobservable in the reference graph). Same extent
- * rules as soc_bloom_fused_stage; output may be `emissive` (in place, as the reference) but not mips[1]. */
+ * scratch (never written: their final contents are unobservable in the reference graph). Needs 4 mips halving
+ * exactly from the emissive extent (<= 8192); output may be `emissive` (in place, as the reference) but not mips[1]. */
 int soc_bloom_weighted_stage(const soc_globals* g, soc_img emissive, const soc_img* mips, int32_t mip_count, soc_img output,
                              int32_t stage, soc_stream stream);
 
@@ -388,12 +379,12 @@ typedef struct soc_renderer soc_renderer;
 
 /* flags */
 #define SOC_RENDERER_TIMING 1      /* record hipEvents around every pass (GPUMetric, gpu_metric.cpp:18-42) */
-#define SOC_RENDERER_UNFUSED_BLOOM 2  /* bloom downsweep as the reference's 4 passes, not 2 fused stages */
+#define SOC_RENDERER_UNFUSED_BLOOM 2  /* bloom as the reference's 8 bit-exact passes (as EXACT_BLOOM) */
 #define SOC_RENDERER_SERIAL 4      /* every pass on the caller's stream (no concurrent sky lane) */
 #define SOC_RENDERER_UNFUSED_TONEMAP 8  /* TAA and tone mapping as two passes (default: one launch for RGBA8) */
 #define SOC_RENDERER_FUSED_HISTOGRAM 16  /* composition + luminance histogram in one launch (the default; kept
                                             for callers that set it) */
-#define SOC_RENDERER_EXACT_BLOOM 32       /* bit-exact bloom chain instead of the weighted form (bloom_w.hip) */
+#define SOC_RENDERER_EXACT_BLOOM 32       /* bit-exact 8-pass bloom chain instead of the weighted form (bloom_w.hip) */
 #define SOC_RENDERER_UNFUSED_HISTOGRAM 64 /* composition and luminance histogram as two passes */
 #define SOC_RENDERER_NO_SKY_SPLIT 128     /* Composition writes the sky pixels itself (waits for the clouds) */
 

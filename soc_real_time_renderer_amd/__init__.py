@@ -192,13 +192,6 @@ def bloom_chain(g, emissive, mips, stream=None):
     _check(lib().soc_bloom_chain(_gp(g), img(emissive), arr, len(mips), _stream(stream)), "bloom_chain")
 
 
-def bloom_fused_stage(g, emissive, mips, output, stage=0, stream=None):
-    """One stage (1-4, 0 = all) of the fused bloom chain (soc_bloom_fused_stage)."""
-    arr = (SocImg * len(mips))(*[img(m) for m in mips])
-    _check(lib().soc_bloom_fused_stage(_gp(g), img(emissive), arr, len(mips), img(output), int(stage), _stream(stream)),
-           "bloom_fused_stage")
-
-
 def bloom_weighted_stage(g, emissive, mips, output, stage=0, stream=None):
     """One stage (1-4, 0 = all) of the weighted-form bloom chain (soc_bloom_weighted_stage)."""
     arr = (SocImg * len(mips))(*[img(m) for m in mips])

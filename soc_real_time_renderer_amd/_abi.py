@@ -199,7 +199,6 @@ FUNCTIONS = {
     "soc_bloom_downsample": (_I, [_G, _IMG, _IMG, _P]),
     "soc_bloom_upsample": (_I, [_G, _IMG, _IMG, _P]),
     "soc_bloom_chain": (_I, [_G, _IMG, C.POINTER(SocImg), C.c_int32, _P]),
-    "soc_bloom_fused_stage": (_I, [_G, _IMG, C.POINTER(SocImg), C.c_int32, _IMG, C.c_int32, _P]),
     "soc_bloom_weighted_stage": (_I, [_G, _IMG, C.POINTER(SocImg), C.c_int32, _IMG, C.c_int32, _P]),
     "soc_ssao_prepare_noise": (_I, [_IMG, _IMG, _P, _P]),
     "soc_ssao_generation": (_I, [_G, _IMG, _IMG, _IMG, _P, _P]),

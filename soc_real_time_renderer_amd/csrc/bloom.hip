@@ -334,21 +334,6 @@ extern "C" int soc_debug_bloom_generic(int32_t up, soc_img a, soc_img b, soc_str
     return up ? launch_bloom_up(a, b, hs(stream), 1) : launch_bloom_down(a, b, hs(stream), 1);
 }
 
-extern "C" int soc_bloom_fused_stage(const soc_globals* g, soc_img emissive, const soc_img* mips, int32_t mip_count,
-                                     soc_img output, int32_t stage, soc_stream stream) {
-    (void)g;
-    static const char* P = "soc_bloom_fused_stage";
-    if (!mips) return set_error(SOC_E_INVALID_ARG, "%s: null mips", P);
-    if (stage < 0 || stage > 4) return set_error(SOC_E_INVALID_ARG, "%s: stage %d not in 0..4", P, stage);
-    int rc = check_img(emissive, SOC_FMT_RGBA16F, P, "emissive");
-    if (!rc) rc = check_img(output, SOC_FMT_RGBA16F, P, "output");
-    for (int i = 0; !rc && i < mip_count; ++i) rc = check_img(mips[i], SOC_FMT_RGBA16F, P, "mip");
-    if (rc) return rc;
-    if (!bloom_fused_applicable(emissive, mips, mip_count, output))
-        return set_error(SOC_E_UNSUPPORTED, "%s: needs 4 mips halving exactly from the emissive extent (<= 8192)", P);
-    return launch_bloom_fused(emissive, mips, output, hs(stream), stage);
-}
-
 extern "C" int soc_bloom_weighted_stage(const soc_globals* g, soc_img emissive, const soc_img* mips, int32_t mip_count,
                                         soc_img output, int32_t stage, soc_stream stream) {
     (void)g;
@@ -369,15 +354,8 @@ extern "C" int soc_bloom_weighted_stage(const soc_globals* g, soc_img emissive, 
 extern "C" int soc_bloom_chain(const soc_globals* g, soc_img emissive, const soc_img* mips, int32_t mip_count,
                                soc_stream stream) {
     if (!mips || mip_count < 1) return set_error(SOC_E_INVALID_ARG, "soc_bloom_chain: need >= 1 mip");
-    int rc = SOC_OK;
-    if (bloom_fused_applicable(emissive, mips, mip_count, emissive)) {
-        // fused downsweep (stages 1-2), per-pass upsweep: the renderer's default schedule
-        rc = soc_bloom_fused_stage(g, emissive, mips, mip_count, emissive, 1, stream);
-        if (!rc) rc = soc_bloom_fused_stage(g, emissive, mips, mip_count, emissive, 2, stream);
-    } else {
-        rc = soc_bloom_downsample(g, emissive, mips[0], stream);
-        for (int i = 0; !rc && i < mip_count - 1; ++i) rc = soc_bloom_downsample(g, mips[i], mips[i + 1], stream);
-    }
+    int rc = soc_bloom_downsample(g, emissive, mips[0], stream);
+    for (int i = 0; !rc && i < mip_count - 1; ++i) rc = soc_bloom_downsample(g, mips[i], mips[i + 1], stream);
     for (int i = mip_count - 1; !rc && i > 0; --i) rc = soc_bloom_upsample(g, mips[i], mips[i - 1], stream);
     if (!rc) rc = soc_bloom_upsample(g, mips[0], emissive, stream);
     return rc;

@@ -1,5 +1,5 @@
-// bloom_common.hpp — tap arithmetic shared by the per-pass bloom kernels (bloom.hip) and the fused
-// chain kernels (bloom_fused.hip). Every helper reproduces the oracle's rounding exactly.
+// bloom_common.hpp — tap arithmetic of the bit-exact per-pass bloom kernels (bloom.hip). Every helper reproduces the
+// oracle's rounding exactly.
 #pragma once
 
 #include "soc_internal.hpp"

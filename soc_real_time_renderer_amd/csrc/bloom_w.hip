@@ -21,6 +21,21 @@
 #include "soc_internal.hpp"
 
 namespace soc {
+// The chain's fixed-ratio fast paths apply when the four mips halve exactly (the reference's mip chain at even
+// extents, renderer.cpp:492-513) and the extents fit the 8-bit fixed-point tap range.
+bool bloom_fused_applicable(const soc_img& emissive, const soc_img* mips, int mip_count, const soc_img& output) {
+    if (mip_count != 4 || output.width != emissive.width || output.height != emissive.height) return false;
+    if (emissive.width > 8192 || emissive.height > 8192) return false;
+    if (mips[0].width != emissive.width || mips[0].height != emissive.height) return false;
+    for (int i = 1; i < 4; ++i)
+        if (mips[i - 1].width != 2 * mips[i].width || mips[i - 1].height != 2 * mips[i].height || mips[i].width < 2 ||
+            mips[i].height < 2)
+            return false;
+    return true;
+}
+}  // namespace soc
+
+namespace soc {
 namespace {
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return min(max(v, lo), hi); }
@@ -300,7 +315,7 @@ bool a16(const soc_img& im) { return im.pitch_bytes % 16 == 0 && reinterpret_cas
 
 int launch_bloom_weighted(const soc_img& emissive, const soc_img* mips, const soc_img& output, hipStream_t s, int stage) {
     const DImg E = dimg(emissive), M1 = dimg(mips[1]), M3 = dimg(mips[3]), O = dimg(output);
-    const int swz = tuning_knob("SOC_SWZ_BLOOM", 1);   // XCD-aware order: halo re-reads served by L2 (2.0x -> 1.0x HBM traffic)
+    const int swz = 1;   // XCD-aware order: halo re-reads served by L2 (2.0x -> 1.0x HBM traffic)
     if (stage == 0 || stage == 1) {
         dim3 g(ceil_div(mips[1].width, W1_OW), ceil_div(mips[1].height, W1_OH));
         bloomw_down01<<<g, 256, 0, s>>>(E, M1, swz);

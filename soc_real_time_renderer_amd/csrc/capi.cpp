@@ -726,31 +726,17 @@ void build_passes(soc_renderer* r) {
             });
         return;
     }
-    const bool fused = !(r->flags & SOC_RENDERER_UNFUSED_BLOOM) && chain_ok;
-    if (fused) {
-        // bit-exact: downsweep as 2 fused stages (mip0 / mip2 of the downsweep stay in LDS;
-        // bloom_fused.hip), the upsweep as the reference's 4 passes. Every mip and the output end up
-        // with exactly the 8-pass chain's bits.
-        add_pass(r, "BloomDownsample - 0+1", "Bloom", pre, res_mask({SOC_RES_EMISSIVE}), res_mask({mip[0], mip[1]}),
-                 [r](const soc_globals* g, hipStream_t s) {
-                     return soc_bloom_fused_stage(g, r->img.emissive, r->img.bloom_mips, 4, r->img.emissive, 1, (soc_stream)s);
+    // renderer.cpp:1024-1042: the bit-exact per-pass chain (SOC_RENDERER_EXACT_BLOOM / _UNFUSED_BLOOM, or mips that do
+    // not halve exactly)
+    add_pass(r, "BloomDownsample - 0", "Bloom", pre, res_mask({SOC_RES_EMISSIVE}), res_mask({mip[0]}),
+             [r](const soc_globals* g, hipStream_t s) {
+                 return soc_bloom_downsample(g, r->img.emissive, r->img.bloom_mips[0], (soc_stream)s);
+             });
+    for (int i = 0; i < nm - 1; ++i)
+        add_pass(r, "BloomDownsample - " + std::to_string(i + 1), "Bloom", pre, res_mask({mip[i]}),
+                 res_mask({mip[i + 1]}), [r, i](const soc_globals* g, hipStream_t s) {
+                     return soc_bloom_downsample(g, r->img.bloom_mips[i], r->img.bloom_mips[i + 1], (soc_stream)s);
                  });
-        add_pass(r, "BloomDownsample - 2+3", "Bloom", pre, res_mask({mip[1]}), res_mask({mip[2], mip[3]}),
-                 [r](const soc_globals* g, hipStream_t s) {
-                     return soc_bloom_fused_stage(g, r->img.emissive, r->img.bloom_mips, 4, r->img.emissive, 2, (soc_stream)s);
-                 });
-    } else {
-        // renderer.cpp:1024-1042
-        add_pass(r, "BloomDownsample - 0", "Bloom", pre, res_mask({SOC_RES_EMISSIVE}), res_mask({mip[0]}),
-                 [r](const soc_globals* g, hipStream_t s) {
-                     return soc_bloom_downsample(g, r->img.emissive, r->img.bloom_mips[0], (soc_stream)s);
-                 });
-        for (int i = 0; i < nm - 1; ++i)
-            add_pass(r, "BloomDownsample - " + std::to_string(i + 1), "Bloom", pre, res_mask({mip[i]}),
-                     res_mask({mip[i + 1]}), [r, i](const soc_globals* g, hipStream_t s) {
-                         return soc_bloom_downsample(g, r->img.bloom_mips[i], r->img.bloom_mips[i + 1], (soc_stream)s);
-                     });
-    }
     // renderer.cpp:1044-1062 (load_op CLEAR: the upsample overwrites its target, quirk Q5)
     for (int i = nm - 1; i > 0; --i)
         add_pass(r, "BloomUpsample - " + std::to_string(i), "Bloom", pre, res_mask({mip[i]}), res_mask({mip[i - 1]}),
@@ -1097,12 +1083,7 @@ static int ensure_side_lane(soc_renderer* r) {
         r->side = nullptr;
         r->fork_ev = r->join_ev = nullptr;
     }
-    // tuning knob: priority of the second lane (-1 high, 1 low, 0 the default priority)
-    const int prio_knob = tuning_knob("SOC_SIDE_PRIORITY", 0);
-    int least = 0, greatest = 0;
-    (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
-    const int prio = prio_knob < 0 ? greatest : prio_knob > 0 ? least : 0;
-    if (hipStreamCreateWithPriority(&r->side, hipStreamNonBlocking, prio) != hipSuccess ||
+    if (hipStreamCreateWithFlags(&r->side, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&r->fork_ev, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&r->join_ev, hipEventDisableTiming) != hipSuccess)
         return set_error(SOC_E_HIP, "soc_renderer_execute: second lane stream/event creation failed");

@@ -516,8 +516,9 @@ struct PairBufs {
     uint32_t* batch_base; // [W*H/256] per 256-entry batch: physical index of its first pair | kInline
     float4* geom;         // [W*H] x 2 per list entry: (start, dither), (inc, stepLength) of its march (density
                           // writes it for upward rays; sunvis and resolve read it instead of re-deriving it)
-    float* od;            // [24 * W*H] step-major: od of dense step s of list entry i at od[s * n + i] (density writes
-                          // it, sunvis reads it instead of evaluating the step's clouds again); null: sunvis evaluates
+    float* od_tmp;        // [od_blocks][24][256]: per density workgroup, the od of its current batch's dense steps until
+                          // their pair slots are known; density then stores od in odvis[slot].x, and sunvis only adds vis
+    uint32_t od_blocks;   // density workgroups the od scratch holds (the density grid is clamped to it)
     uint32_t n;           // list capacity (W*H)
     uint32_t cap;         // pairs per shard
 };
@@ -573,6 +574,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void c
     cx.cam_z = p.cam[2];
     cx.time = -1.0f * 0.02f * p.elapsed;
     const uint32_t shard = blockIdx.x & (kShards - 1);
+    float* const od_tmp = pb.od_tmp + (size_t)blockIdx.x * (24 * 256) + tid;   // this lane's od of dense step s at [s * 256]
     // workgroup-uniform trip count: every lane reaches the barriers of every round
     for (uint32_t first = blockIdx.x * 256u; first < count; first += gridDim.x * 256u) {
         const uint32_t i = first + tid;
@@ -590,7 +592,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void c
                     const float od = get_clouds(cx, step_position(mg, dither, s)) * mg.stepLength;
                     if (!(od <= 0.0f)) {
                         mask |= 1u << s;
-                        if (pb.od) pb.od[(size_t)s * pb.n + i] = od;
+                        od_tmp[s * 256] = od;
                     }
                 }
             }
@@ -622,7 +624,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void c
             // uniform loop: the ballot of every step sees every lane of the wave
             for (uint32_t st = 0; st < 24; ++st) {
                 const uint32_t rank = mask_ballot_rank(mask, st, lane);
-                if ((mask >> st) & 1u) pb.pairs[slot_base + pair_offset(offs, st, wave, rank)] = (i << 5) | st;
+                if ((mask >> st) & 1u) {
+                    const uint32_t slot = slot_base + pair_offset(offs, st, wave, rank);
+                    pb.pairs[slot] = (i << 5) | st;
+                    reinterpret_cast<float*>(pb.odvis)[2 * (size_t)slot] = od_tmp[st * 256];   // this lane's own write
+                }
             }
         }
         __syncthreads();   // offs / wg_base are reused next round
@@ -668,10 +674,9 @@ __global__ __launch_bounds__(kSunvisThreads) __attribute__((amdgpu_waves_per_eu(
         const float4 g0 = pb.geom[2 * i], g1 = pb.geom[2 * i + 1];   // the pixel's march, from clouds_density
         const MarchGeom mg{f3{g0.x, g0.y, g0.z}, f3{g1.x, g1.y, g1.z}, g1.w};
         const f3 cp = step_position(mg, g0.w, (int)step);
-        // the dense step's od as clouds_density computed it (the same function of the same stored geometry)
-        const float od = pb.od ? pb.od[(size_t)step * pb.n + i] : get_clouds(cx, cp) * mg.stepLength;
+        // od of the step is already in odvis[phys].x (clouds_density)
         const float vis = SOC_CLOUDS_PROFILE == 3 ? 1.0f : sun_visibility(cx, cp, sun);
-        pb.odvis[phys] = float2{od, vis};
+        reinterpret_cast<float*>(pb.odvis)[2 * (size_t)phys + 1] = vis;
     }
 }
 
@@ -768,9 +773,11 @@ using namespace soc;
 namespace {
 // Workspace: counters (256 B: [0] sky pixels, [8..15] pair counts per shard) | sky list (u32) |
 // atmosphere (float4) | per-pixel dense mask (u32) | per-batch first pair (u32) | march geometry (2 float4) | pairs (u32) |
-// (od, vis) per pair (float2) | od of every dense step (24 float per pixel, step-major). Pair capacity 2 per pixel
-// of the image (8 shards).
+// (od, vis) per pair (float2) | od scratch of the density workgroups (24 x 256 float each, at most kDensityBlocks).
+// Pair capacity 2 per pixel of the image (8 shards).
 // Per 256-entry batch of the list: the physical index of its first pair (or kInline).
+// density workgroups the od scratch is sized for (the resident set: 6 per CU on 256 CUs is 1536)
+constexpr size_t kDensityBlocks = 2048;
 struct CloudWs {
     uint32_t* counter;
     uint32_t* list;
@@ -800,9 +807,10 @@ CloudWs cloud_ws_layout(void* base, size_t n) {
     off = al(off + (size_t)kShards * w.pb.cap * 4);
     w.pb.odvis = reinterpret_cast<float2*>(b + off);
     off = al(off + (size_t)kShards * w.pb.cap * 8);
-    w.pb.od = reinterpret_cast<float*>(b + off);
+    w.pb.od_tmp = reinterpret_cast<float*>(b + off);
+    w.pb.od_blocks = (uint32_t)std::min<size_t>(kDensityBlocks, (n + 255) / 256);
     w.pb.n = (uint32_t)n;
-    off = al(off + n * 24 * 4);
+    off = al(off + (size_t)w.pb.od_blocks * 24 * 256 * 4);
     w.bytes = off;
     return w;
 }
@@ -853,8 +861,6 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
     }
     // the caller sized the workspace for the target extent (soc_cloud_rendering_workspace_size)
     CloudWs ws = cloud_ws_layout(workspace, (size_t)target.width * (size_t)target.height);
-    const bool od_store = tuning_knob("SOC_CLOUDS_OD_STORE", 1) != 0;   // A/B: sunvis re-evaluates the step
-    if (!od_store) ws.pb.od = nullptr;
     uint32_t* counter = ws.counter;
     uint32_t* list = ws.list;
     hipError_t e = hipMemsetAsync(counter, 0, 256, s);
@@ -864,36 +870,25 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
     // One resident wave set per kernel, grid-stride over the list / pairs: the long per-item work is
     // balanced over all SIMDs instead of running as a second, partially filled round.
     static int res_atmos = 0, res_density = 0, res_sunvis = 0, res_resolve = 0;
-    static bool sunvis512 = true, sunvis_wide = true;
     if (!res_atmos) {
-        // tuning knob: percent of the resident set each persistent kernel takes (the rest of the CU slots stay
-        // free for the frame lane's kernels running beside the sky lane)
-        const int pct = std::max(1, tuning_knob("SOC_SKY_SHARE_PCT", 100));
-        auto share = [&](int res) { return std::max(1, res * pct / 100); };
-        res_atmos = share(resident_blocks(clouds_atmosphere));
-        res_density = share(resident_blocks(clouds_density<false>));
-        sunvis512 = tuning_knob("SOC_SUNVIS_THREADS", 512) == 512;
-        sunvis_wide = tuning_knob("SOC_SUNVIS_WIDE", 1) != 0;
-        res_sunvis = share(sunvis_wide ? resident_blocks(clouds_sunvis<false, 512, true>, 512)
-                           : sunvis512 ? resident_blocks(clouds_sunvis<false, 512>, 512) : resident_blocks(clouds_sunvis<false, 256>, 256));
-        res_resolve = share(resident_blocks(clouds_resolve<false>));
+        res_atmos = resident_blocks(clouds_atmosphere);
+        res_density = resident_blocks(clouds_density<false>);
+        res_sunvis = resident_blocks(clouds_sunvis<false, 512, true>, 512);
+        res_resolve = resident_blocks(clouds_resolve<false>);
     }
     const long long blocks = ((long long)W * H + 255) / 256;
     if (SOC_CLOUDS_PROFILE >= 4) return check_launch("cloud_rendering");
     auto grid = [&](int res, long long items_blocks) { return (int)std::max(1LL, std::min<long long>(res, items_blocks)); };
     clouds_atmosphere<<<grid(res_atmos, blocks), 256, 0, s>>>(p, counter, list, ws.atmos);
     const DImg nz = dimg(noise), tg = dimg(target);
+    const int density_grid = std::min(grid(res_density, blocks), (int)ws.pb.od_blocks);   // one od scratch per workgroup
     if (r8) {
-        clouds_density<true><<<grid(res_density, blocks), 256, 0, s>>>(nz, p, counter, list, ws.pb);
-        if (sunvis_wide) clouds_sunvis<true, 512, true><<<grid(res_sunvis, blocks), 512, 0, s>>>(nz, p, list, ws.pb);
-        else if (sunvis512) clouds_sunvis<true, 512><<<grid(res_sunvis, blocks), 512, 0, s>>>(nz, p, list, ws.pb);
-        else clouds_sunvis<true, 256><<<grid(res_sunvis, 2 * blocks), 256, 0, s>>>(nz, p, list, ws.pb);
+        clouds_density<true><<<density_grid, 256, 0, s>>>(nz, p, counter, list, ws.pb);
+        clouds_sunvis<true, 512, true><<<grid(res_sunvis, blocks), 512, 0, s>>>(nz, p, list, ws.pb);
         clouds_resolve<true><<<grid(res_resolve, blocks), 256, 0, s>>>(nz, tg, p, counter, list, ws.atmos, ws.pb);
     } else {
-        clouds_density<false><<<grid(res_density, blocks), 256, 0, s>>>(nz, p, counter, list, ws.pb);
-        if (sunvis_wide) clouds_sunvis<false, 512, true><<<grid(res_sunvis, blocks), 512, 0, s>>>(nz, p, list, ws.pb);
-        else if (sunvis512) clouds_sunvis<false, 512><<<grid(res_sunvis, blocks), 512, 0, s>>>(nz, p, list, ws.pb);
-        else clouds_sunvis<false, 256><<<grid(res_sunvis, 2 * blocks), 256, 0, s>>>(nz, p, list, ws.pb);
+        clouds_density<false><<<density_grid, 256, 0, s>>>(nz, p, counter, list, ws.pb);
+        clouds_sunvis<false, 512, true><<<grid(res_sunvis, blocks), 512, 0, s>>>(nz, p, list, ws.pb);
         clouds_resolve<false><<<grid(res_resolve, blocks), 256, 0, s>>>(nz, tg, p, counter, list, ws.atmos, ws.pb);
     }
     return check_launch("cloud_rendering");

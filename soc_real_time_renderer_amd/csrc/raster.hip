@@ -40,9 +40,7 @@ struct RasterParams {
     int cull;
     int depth_only;
     float bias_constant, bias_slope;
-    int precheck;       // load the target before the atomic (skip it when already nearer)
     int small_pixels;   // boxes up to this many pixels are scanned by one lane
-    int probe;          // profiling (SOC_RASTER_PROBE): 1 = skip the atomics, 2 = skip raster_big
 };
 
 // workspace: [float4 clip-space screen vertices[V]] [u64 counter, pad..] [uint2 entries[T]]
@@ -212,18 +210,17 @@ __device__ __forceinline__ void shade(const TriSetup& t, int id, int x, int y, c
                                       size_t pitch) {
     float e0, e1, e2, z;
     if (!cover(t, x, y, e0, e1, e2, z)) return;
-    if (p.probe == 1 && z > -1.0f) return;   // profiling probe: coverage work only, no memory traffic
     // a plain load first: values only decrease, so a stale (larger) value never skips a needed atomic
     if (p.depth_only) {
 #pragma clang fp contract(off)
         const float zb = fminf(fmaxf(z + t.bias, 0.0f), 1.0f);
         uint32_t* d = reinterpret_cast<uint32_t*>(static_cast<char*>(target) + (size_t)y * pitch) + x;
         const uint32_t key = __float_as_uint(zb);
-        if (!p.precheck || key < __builtin_nontemporal_load(d)) atomicMin(d, key);
+        atomicMin(d, key);
     } else {
         const unsigned long long key = ((unsigned long long)__float_as_uint(z) << 32) | (unsigned long long)(0xFFFFFFFEu - (uint32_t)id);
         unsigned long long* d = reinterpret_cast<unsigned long long*>(static_cast<char*>(target) + (size_t)y * pitch) + x;
-        if (!p.precheck || key < __builtin_nontemporal_load(d)) atomicMin(d, key);
+        atomicMin(d, key);
     }
 }
 
@@ -712,9 +709,7 @@ RasterParams make_raster_params(const soc_mesh* mesh, const float* vp, int W, in
     p.vertex_count = mesh->vertex_count;
     p.triangle_count = mesh->triangle_count;
     p.cull = cull;
-    p.precheck = tuning_knob("SOC_RASTER_PRECHECK", 0);
-    p.small_pixels = tuning_knob("SOC_RASTER_SMALL", SMALL_PIXELS);
-    p.probe = tuning_knob("SOC_RASTER_PROBE", 0);
+    p.small_pixels = SMALL_PIXELS;
     return p;
 }
 
@@ -724,7 +719,7 @@ int launch_raster(const soc_mesh* mesh, const RasterParams& p, void* target, siz
     raster_setup<<<ceil_div(max(mesh->vertex_count, 1), 256), 256, 0, s>>>(mesh->positions, ws, p);
     if (mesh->triangle_count > 0) {
         raster_small<<<ceil_div(mesh->triangle_count, 256), 256, 0, s>>>(mesh->indices, ws, p, target, pitch);
-        if (p.probe != 2) raster_big<<<2048, 256, 0, s>>>(mesh->indices, ws, p, target, pitch);
+        raster_big<<<2048, 256, 0, s>>>(mesh->indices, ws, p, target, pitch);
     }
     return check_launch(pass);
 }

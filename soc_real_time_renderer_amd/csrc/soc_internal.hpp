@@ -47,13 +47,13 @@ inline Mat4 mat4(const float* m) {
 
 inline hipStream_t hs(soc_stream s) { return reinterpret_cast<hipStream_t>(s); }
 
-// Integer tuning knob from the environment (`dflt` when unset). Read at every launch (a getenv scan,
-// ~0.1 us), so A/B runs and the variant-identity tests can switch it between calls.
+// Integer tuning knob from the environment (`dflt` when unset), read once and cached until soc_tuning_reload():
+// only the variants the identity tests switch (SOC_SWZ_SSAO, SOC_TAA_NBR, SOC_COMP_NT, SOC_GB_TEX_PAIRS,
+// SOC_RENDERER_SSAO_FIRST) are knobs; measured-and-rejected variants are removed.
 int tuning_knob(const char* name, int dflt);
 // RN(1 / n) for div_rn (soc_device.hpp), or 0 when n is outside the exhaustively checked range (1..16384).
-// (tuning knob SOC_NO_DIV_RN=1: always 0, i.e. the IEEE division, for A/B runs)
 inline float recip_rn(int n) {
-    return n >= 1 && n <= 16384 && !tuning_knob("SOC_NO_DIV_RN", 0) ? 1.0f / (float)n : 0.0f;
+    return n >= 1 && n <= 16384 ? 1.0f / (float)n : 0.0f;
 }
 
 // Checks the launch that was just issued.
@@ -66,9 +66,8 @@ inline unsigned ceil_div(unsigned a, unsigned b) { return (a + b - 1) / b; }
 void agx_matrices(float compression, float M[9], float Minv[9]);
 void mat4_mul_host(float out[16], const float a[16], const float b[16]);
 
-// Fused bloom chain (bloom_fused.hip).
+// The bloom chain's exactly-halving mips (bloom_w.hip).
 bool bloom_fused_applicable(const soc_img& emissive, const soc_img* mips, int mip_count, const soc_img& output);
-int launch_bloom_fused(const soc_img& emissive, const soc_img* mips, const soc_img& output, hipStream_t s, int stage);
 // Weighted-form bloom chain (bloom_w.hip): same applicability as the fused chain.
 int launch_bloom_weighted(const soc_img& emissive, const soc_img* mips, const soc_img& output, hipStream_t s, int stage);
 

@@ -100,67 +100,26 @@ __device__ __forceinline__ float aff(const Aff& a, float kx, float ky, float kz)
 // clamped to [0, n-1-1/256] (right-edge taps keep 1/256 of the inner texel). This regroups the
 // reference's fp32 roundings; the result stays within the SSAO tolerance of DESIGN.md §5.
 // 32x8-pixel workgroups of 32x2-pixel waves (each tap row of a wave spans two 128-B depth lines).
-// Depth layouts the taps can read (experiment; SOC_SSAO_LAYOUT_*): a tap needs texels (x0, y0), (x0+1, y0),
-// (x0, y0+1), (x0+1, y0+1) with x0 <= W-2, y0 <= H-2.
-//   0 D32 row-major: two 8-B row loads
-//   1 row pairs, both parities: rows [0, hp) hold (y=2r, 2r+1) interleaved per column, rows [hp, 2hp) hold (2r+1, 2r+2);
-//     one 16-B load per tap (2x the depth footprint)
-//   2 quads: texel (x, y) holds its 2x2 block; one 16-B load per tap (4x footprint)
-//   3 even row pairs only: one 16-B load for an even y0, two for an odd one (1x footprint)
-enum { LAY_D32 = 0, LAY_PAIRS2 = 1, LAY_QUADS = 2, LAY_PAIRS = 3, LAY_PROBE_LOCAL = 9, LAY_PROBE_ROW = 8 };
-
-__global__ __launch_bounds__(256) void depth_layout_kernel(DImg depth, char* __restrict__ out, int layout, int pitch_out,
-                                                           int rows, int hp) {
-    const int x = blockIdx.x * 64 + threadIdx.x, r = blockIdx.y * 4 + threadIdx.y;
-    if (x >= depth.w || r >= rows) return;
-    const int H = depth.h, W = depth.w;
-    auto d = [&](int xx, int yy) { return row_ptr<float>(depth, min(yy, H - 1))[min(xx, W - 1)]; };
-    if (layout == LAY_QUADS) {
-        float4 q = make_float4(d(x, r), d(x + 1, r), d(x, r + 1), d(x + 1, r + 1));
-        reinterpret_cast<float4*>(out + (size_t)r * pitch_out)[x] = q;
-        return;
-    }
-    int ya, yb;
-    if (r < hp) { ya = 2 * r; yb = 2 * r + 1; }
-    else { ya = 2 * (r - hp) + 1; yb = ya + 1; }
-    reinterpret_cast<float2*>(out + (size_t)r * pitch_out)[x] = make_float2(d(x, ya), d(x, yb));
-}
-
-template <int LAYOUT>
-__device__ __forceinline__ void depth_quad(const __amdgpu_buffer_rsrc_t& rsrc, int x0, int y0, int pitch, int hp, float& t0,
-                                           float& t1, float& b0, float& b1) {
-    if (LAYOUT == LAY_D32 || LAYOUT == LAY_PROBE_LOCAL || LAYOUT == LAY_PROBE_ROW) {
+// D32 texel quad (x0, y0) .. (x0 + 1, y0 + 1) through the buffer descriptor: two 8-byte row loads.
+struct GlobalQuad {
+    __amdgpu_buffer_rsrc_t rsrc;
+    int pitch;
+    __device__ __forceinline__ void operator()(int x0, int y0, float& t0, float& t1, float& b0, float& b1) const {
         const int off = __mul24(y0, pitch) + x0 * 4;
         const f2a4 r0 = __builtin_bit_cast(f2a4, __builtin_amdgcn_raw_buffer_load_b64(rsrc, off, 0, 0));
         const f2a4 r1 = __builtin_bit_cast(f2a4, __builtin_amdgcn_raw_buffer_load_b64(rsrc, off, pitch, 0));
         t0 = r0.x; t1 = r0.y; b0 = r1.x; b1 = r1.y;
-    } else if (LAYOUT == LAY_PAIRS2) {
-        const int row = (y0 >> 1) + ((y0 & 1) ? hp : 0);
-        const auto q = __builtin_amdgcn_raw_buffer_load_b128(rsrc, __mul24(row, pitch) + x0 * 8, 0, 0);
-        t0 = __uint_as_float(q[0]); b0 = __uint_as_float(q[1]); t1 = __uint_as_float(q[2]); b1 = __uint_as_float(q[3]);
-    } else if (LAYOUT == LAY_QUADS) {
-        const auto q = __builtin_amdgcn_raw_buffer_load_b128(rsrc, __mul24(y0, pitch) + x0 * 16, 0, 0);
-        t0 = __uint_as_float(q[0]); t1 = __uint_as_float(q[1]); b0 = __uint_as_float(q[2]); b1 = __uint_as_float(q[3]);
-    } else {
-        const int off = __mul24(y0 >> 1, pitch) + x0 * 8;
-        const auto q = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0);
-        if (y0 & 1) {
-            const auto q2 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, pitch, 0);
-            t0 = __uint_as_float(q[1]); t1 = __uint_as_float(q[3]); b0 = __uint_as_float(q2[0]); b1 = __uint_as_float(q2[2]);
-        } else {
-            t0 = __uint_as_float(q[0]); t1 = __uint_as_float(q[2]); b0 = __uint_as_float(q[1]); b1 = __uint_as_float(q[3]);
-        }
     }
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t depth_rsrc(const DImg& depth) {
+    return __builtin_amdgcn_make_buffer_rsrc(depth.data, 0, depth.pitch * depth.h, 0x00020000);
 }
 
-template <bool TABLE, bool SPARSE_IP, bool FULL, int LAYOUT = LAY_D32>
-__global__ __launch_bounds__(256) void ssao_kernel(DImg depth, DImg normal, DImg target, const float2* __restrict__ table,
-                                                   SsaoParams p, DImg lay = DImg{}) {
-    int bx, by;
-    xcd_order(p.swz, bx, by);
-    const int tid = threadIdx.x;
-    const int x = bx * 32 + (tid & 31), y = by * 8 + (tid >> 5);
-    if (x >= target.w || y >= target.h) return;
+// One half-res pixel of SSAOGenerationTask (:176-214); `quad` fetches a tap's 2x2 D32 texels.
+template <bool TABLE, bool SPARSE_IP, bool FULL, class Quad, int UNROLL = SOC_SSAO_MAX_KERNEL>
+__device__ __forceinline__ void ssao_pixel(int x, int y, const DImg& depth, const DImg& normal, const DImg& target,
+                                           const float2* __restrict__ table, const SsaoParams& p, const Quad& quad) {
     const float u = centre_uv_rn(x, target.w, p.rw), v = centre_uv_rn(y, target.h, p.rh);
 
     // normal = mat3(view) * normalize(texture(normal, uv).rgb), :178
@@ -203,14 +162,8 @@ __global__ __launch_bounds__(256) void ssao_kernel(DImg depth, DImg normal, DImg
     const float tmax_x = (float)(W - 1) - 1.0f / 256.0f, tmax_y = (float)(H - 1) - 1.0f / 256.0f;
     const float cx0s = cx0 * 256.0f + 0.5f, cy0s = cy0 * 256.0f + 0.5f;
     const float fmax_x = tmax_x * 256.0f + 0.5f, fmax_y = tmax_y * 256.0f + 0.5f;
-    const int pitch = depth.pitch;
-    const bool d32 = LAYOUT == LAY_D32 || LAYOUT == LAY_PROBE_LOCAL || LAYOUT == LAY_PROBE_ROW;
-    const int lpitch = d32 ? pitch : lay.pitch, hp = (H + 1) >> 1;
-    const __amdgpu_buffer_rsrc_t rsrc = d32
-        ? __builtin_amdgcn_make_buffer_rsrc(depth.data, 0, pitch * H, 0x00020000)
-        : __builtin_amdgcn_make_buffer_rsrc(lay.data, 0, lay.pitch * lay.h, 0x00020000);
     float occ = 0.0f;
-#pragma unroll
+#pragma unroll UNROLL
     for (int i = 0; i < SOC_SSAO_MAX_KERNEL; ++i) {
         if (FULL || i < p.ksize) {
             const float kx = kKernel.v[i][0], ky = kKernel.v[i][1], kz = kKernel.v[i][2];
@@ -231,12 +184,7 @@ __global__ __launch_bounds__(256) void ssao_kernel(DImg depth, DImg normal, DImg
             }
             const float wx = (float)(fx & 255) * (1.0f / 256.0f), wy = (float)(fy & 255) * (1.0f / 256.0f);
             float t0, t1, b0, b1;
-            if (LAYOUT == LAY_PROBE_LOCAL)      // probe (wrong results): every tap reads the lane's own texel pair rows
-                depth_quad<LAYOUT>(rsrc, min(x * 2, W - 2) + (fx & 1), min(y * 2, H - 2), lpitch, hp, t0, t1, b0, b1);
-            else if (LAYOUT == LAY_PROBE_ROW)   // probe: the tap's own x, the lane's row (each wave load spans 2 rows)
-                depth_quad<LAYOUT>(rsrc, fx >> 8, min(y * 2, H - 2), lpitch, hp, t0, t1, b0, b1);
-            else
-                depth_quad<LAYOUT>(rsrc, fx >> 8, fy >> 8, lpitch, hp, t0, t1, b0, b1);
+            quad(fx >> 8, fy >> 8, t0, t1, b0, b1);
             const float top = __builtin_fmaf(wx, t1 - t0, t0);
             const float bot = __builtin_fmaf(wx, b1 - b0, b0);
             const float dd = __builtin_fmaf(wy, bot - top, top);
@@ -266,6 +214,73 @@ __global__ __launch_bounds__(256) void ssao_kernel(DImg depth, DImg normal, DImg
     }
     occ = 1.0f - (occ / p.kernel_size_f);
     row_ptr_w<uint8_t>(target, y)[x] = (uint8_t)to_unorm8(occ);
+}
+
+template <bool TABLE, bool SPARSE_IP, bool FULL>
+__global__ __launch_bounds__(256) void ssao_kernel(DImg depth, DImg normal, DImg target, const float2* __restrict__ table,
+                                                   SsaoParams p) {
+    int bx, by;
+    xcd_order(p.swz, bx, by);
+    const int tid = threadIdx.x;
+    const int x = bx * 32 + (tid & 31), y = by * 8 + (tid >> 5);
+    if (x >= target.w || y >= target.h) return;
+    ssao_pixel<TABLE, SPARSE_IP, FULL>(x, y, depth, normal, target, table, p, GlobalQuad{depth_rsrc(depth), depth.pitch});
+}
+
+// LDS-tiled taps. A workgroup of TXP x TYP half-res pixels (waves of 32 x 2) first stages the full-res depth tile
+// its pixels cover plus a HALO-texel border in LDS (16-B loads, one pass); every tap whose 2x2 texels lie inside the
+// tile reads them from LDS, the others (near geometry: the screen-space radius exceeds the halo) from the D32 image
+// as before, exec-masked to those lanes. The same texels, so the same bits as ssao_kernel.
+template <int TXP, int TYP, int HALO>
+struct SsaoTile {
+    static constexpr int TW = 2 * TXP + 2 * HALO, TH = 2 * TYP + 2 * HALO, THREADS = TXP * TYP;
+};
+
+template <int TXP, int TYP, int HALO>
+struct LdsQuad {
+    const float* tile;
+    int gx0, gy0;
+    GlobalQuad g;
+    __device__ __forceinline__ void operator()(int x0, int y0, float& t0, float& t1, float& b0, float& b1) const {
+        constexpr int TW = SsaoTile<TXP, TYP, HALO>::TW, TH = SsaoTile<TXP, TYP, HALO>::TH;
+        const int lx = x0 - gx0, ly = y0 - gy0;
+        const bool in = (unsigned)lx < (unsigned)(TW - 1) && (unsigned)ly < (unsigned)(TH - 1);
+        const int i = in ? ly * TW + lx : 0;
+        t0 = tile[i];
+        t1 = tile[i + 1];
+        b0 = tile[i + TW];
+        b1 = tile[i + TW + 1];
+        if (!in) g(x0, y0, t0, t1, b0, b1);
+    }
+};
+
+template <bool TABLE, bool SPARSE_IP, bool FULL, int TXP, int TYP, int HALO, int UNROLL>
+__global__ __attribute__((amdgpu_flat_work_group_size(TXP * TYP, TXP * TYP)))
+__attribute__((amdgpu_waves_per_eu(TXP * TYP >= 1024 ? 8 : TXP * TYP >= 512 ? 4 : 2)))
+void ssao_lds_kernel(DImg depth, DImg normal, DImg target, const float2* __restrict__ table, SsaoParams p) {
+    using T = SsaoTile<TXP, TYP, HALO>;
+    __shared__ float4 tile4[T::TW * T::TH / 4];
+    int bx, by;
+    xcd_order(p.swz, bx, by);
+    const int tid = threadIdx.x;
+    const int gx0 = bx * 2 * TXP - HALO, gy0 = by * 2 * TYP - HALO;
+    const __amdgpu_buffer_rsrc_t rsrc = depth_rsrc(depth);
+    // stage the tile: rows clamped into the image; columns left of the image give a negative (out-of-range) offset,
+    // which the buffer load returns as 0. No tap reads a texel outside the image (taps clamp to [0, n - 2]).
+    constexpr int Q = T::TW / 4;
+    for (int i = tid; i < Q * T::TH; i += T::THREADS) {
+        const int r = i / Q, c = i - r * Q;
+        const int gy = min(max(gy0 + r, 0), depth.h - 1);
+        const int off = __mul24(gy, depth.pitch) + (gx0 + 4 * c) * 4;
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0);
+        tile4[i] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+    }
+    __syncthreads();
+    const int w = tid >> 6, lane = tid & 63;
+    const int x = bx * TXP + (w % (TXP / 32)) * 32 + (lane & 31), y = by * TYP + (w / (TXP / 32)) * 2 + (lane >> 5);
+    if (x >= target.w || y >= target.h) return;
+    const LdsQuad<TXP, TYP, HALO> quad{reinterpret_cast<const float*>(tile4), gx0, gy0, GlobalQuad{rsrc, depth.pitch}};
+    ssao_pixel<TABLE, SPARSE_IP, FULL, LdsQuad<TXP, TYP, HALO>, UNROLL>(x, y, depth, normal, target, table, p, quad);
 }
 
 // ssao_blur.inl:91-106: 4x4 box at offsets -2..+1 (x outer, y inner), all taps on texel centres.
@@ -349,7 +364,21 @@ extern "C" int soc_ssao_generation(const soc_globals* g, soc_img depth, soc_img 
     DImg dd = dimg(depth), dn = dimg(normal), dt = dimg(target);
 #define SOC_SSAO_LAUNCH(T, B, F) ssao_kernel<T, B, F><<<grd, blk, 0, st>>>(dd, dn, dt, tb, p)
     const bool full = p.ksize == SOC_SSAO_MAX_KERNEL;
-    if (noise_table && sip && full) SOC_SSAO_LAUNCH(true, true, true);
+    const int tile = tuning_knob("SOC_SSAO_TILE", 0);
+#define SOC_SSAO_TILED(TX, TY, HALO, U) ssao_lds_kernel<true, true, true, TX, TY, HALO, U> \
+    <<<dim3(ceil_div(target.width, TX), ceil_div(target.height, TY)), TX * TY, 0, st>>>(dd, dn, dt, tb, p)
+    if (noise_table && sip && full && tile) {
+        switch (tile) {
+        case 1: SOC_SSAO_TILED(64, 16, 32, 26); break;
+        case 3: SOC_SSAO_TILED(32, 8, 48, 26); break;
+        case 4: SOC_SSAO_TILED(32, 8, 32, 26); break;
+        case 6: SOC_SSAO_TILED(32, 8, 64, 26); break;
+        case 11: SOC_SSAO_TILED(64, 16, 32, 2); break;
+        case 13: SOC_SSAO_TILED(32, 8, 48, 2); break;
+        case 14: SOC_SSAO_TILED(32, 8, 32, 2); break;
+        default: SOC_SSAO_TILED(32, 8, 64, 2); break;
+        }
+    } else if (noise_table && sip && full) SOC_SSAO_LAUNCH(true, true, true);
     else if (noise_table && sip) SOC_SSAO_LAUNCH(true, true, false);
     else if (noise_table) SOC_SSAO_LAUNCH(true, false, false);
     else if (sip && full) SOC_SSAO_LAUNCH(false, true, true);
@@ -371,47 +400,4 @@ extern "C" int soc_ssao_blur(const soc_globals* g, soc_img ssao, soc_img target,
         ssao_blur_generic<<<grd, blk, 0, hs(stream)>>>(dimg(ssao), dimg(target), 1.0f / (float)ssao.width,
                                                        1.0f / (float)ssao.height);
     return check_launch("ssao_blur");
-}
-
-// Experiment: the tap depth in another layout (see LAY_*); `layout_buf` sized by soc_depth_layout_bytes.
-extern "C" int64_t soc_depth_layout_bytes(int32_t width, int32_t height, int32_t layout) {
-    const int64_t hp = (height + 1) / 2;
-    const int64_t pitch = ((int64_t)width * (layout == LAY_QUADS ? 16 : 8) + 255) / 256 * 256;
-    const int64_t rows = layout == LAY_QUADS ? height : layout == LAY_PAIRS2 ? 2 * hp : hp;
-    return pitch * rows;
-}
-
-extern "C" int soc_depth_layout(soc_img depth, void* layout_buf, int32_t layout, soc_stream stream) {
-    int rc = check_img(depth, SOC_FMT_D32F, "soc_depth_layout", "depth");
-    if (rc) return rc;
-    if (!layout_buf || layout < 1 || layout > 3) return set_error(SOC_E_INVALID_ARG, "soc_depth_layout: bad layout");
-    const int hp = (depth.height + 1) / 2;
-    const int pitch = (int)(((int64_t)depth.width * (layout == LAY_QUADS ? 16 : 8) + 255) / 256 * 256);
-    const int rows = layout == LAY_QUADS ? depth.height : layout == LAY_PAIRS2 ? 2 * hp : hp;
-    dim3 blk(64, 4), grd(ceil_div(depth.width, 64), ceil_div(rows, 4));
-    depth_layout_kernel<<<grd, blk, 0, hs(stream)>>>(dimg(depth), static_cast<char*>(layout_buf), layout, pitch, rows, hp);
-    return check_launch("depth_layout");
-}
-
-extern "C" int soc_ssao_generation_layout(const soc_globals* g, soc_img depth, const void* layout_buf, int32_t layout,
-                                          soc_img normal, soc_img target, const float* noise_table, soc_stream stream) {
-    if (!g || !noise_table || !layout_buf || layout < 1 || (layout > 3 && layout < 8) || layout > 9)
-        return set_error(SOC_E_INVALID_ARG, "soc_ssao_generation_layout: bad arguments");
-    SsaoParams p = make_params(g, normal);
-    p.rw = recip_rn(target.width);
-    p.rh = recip_rn(target.height);
-    const int hp = (depth.height + 1) / 2;
-    const int pitch = (int)(((int64_t)depth.width * (layout == LAY_QUADS ? 16 : 8) + 255) / 256 * 256);
-    const int rows = layout == LAY_QUADS ? depth.height : layout == LAY_PAIRS2 ? 2 * hp : hp;
-    DImg lay{static_cast<char*>(const_cast<void*>(layout_buf)), depth.width, rows, pitch};
-    const dim3 blk(256), grd(ceil_div(target.width, 32), ceil_div(target.height, 8));
-    const float2* tb = reinterpret_cast<const float2*>(noise_table);
-    hipStream_t st = hs(stream);
-    DImg dd = dimg(depth), dn = dimg(normal), dt = dimg(target);
-    if (layout == 1) ssao_kernel<true, true, true, LAY_PAIRS2><<<grd, blk, 0, st>>>(dd, dn, dt, tb, p, lay);
-    else if (layout == 2) ssao_kernel<true, true, true, LAY_QUADS><<<grd, blk, 0, st>>>(dd, dn, dt, tb, p, lay);
-    else if (layout == 3) ssao_kernel<true, true, true, LAY_PAIRS><<<grd, blk, 0, st>>>(dd, dn, dt, tb, p, lay);
-    else if (layout == 8) ssao_kernel<true, true, true, LAY_PROBE_ROW><<<grd, blk, 0, st>>>(dd, dn, dt, tb, p, lay);
-    else ssao_kernel<true, true, true, LAY_PROBE_LOCAL><<<grd, blk, 0, st>>>(dd, dn, dt, tb, p, lay);
-    return check_launch("ssao_generation_layout");
 }

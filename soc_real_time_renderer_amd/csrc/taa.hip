@@ -362,7 +362,7 @@ int taa_launch(const soc_globals* g, soc_img target, soc_img current_color, soc_
     p.pox = 1.0f / (float)g->resolution[0];
     p.poy = 1.0f / (float)g->resolution[1];
     p.accum0 = fminf(0.1f, (float)g->frame_counter);
-    p.swz = tuning_knob("SOC_SWZ_TAA", -16);   // XCD vertical bands: HBM traffic 1.39x -> 1.01x algorithmic
+    p.swz = -16;   // XCD vertical bands of 16-tile strips: HBM traffic 1.39x -> 1.01x algorithmic
     const int W = target.width, H = target.height;
     auto same = [&](const soc_img& im) { return im.width == W && im.height == H; };
     const bool fast = W == g->resolution[0] && H == g->resolution[1] && same(current_color) && same(depth) &&
@@ -377,7 +377,7 @@ int taa_launch(const soc_globals* g, soc_img target, soc_img current_color, soc_
     if (tm && !pair) return 1;
     if (pair) {
         // 32 x 8 lanes (64 x 8 pixels): the 3-row neighbourhood reloads 10 rows per 8 instead of 6 per 4
-        const int by = tuning_knob("SOC_TAA_BY", 8), bxl = 256 / by;
+        const int by = 8, bxl = 256 / by;
         dim3 blk(bxl, by), g2(ceil_div(W / 2, bxl), ceil_div(H, by));
         // side columns: 2 = halo lanes (default), 1 = lane shifts + edge-lane loads, 0 = every lane loads them
         const int nbr = tuning_knob("SOC_TAA_NBR", 2);

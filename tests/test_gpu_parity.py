@@ -89,34 +89,6 @@ def test_bloom_chain_bit_exact(soc, oracle, W, H):
         assert np.array_equal(host(mips_d[i])[..., :3].view(np.uint16), mips_h[i][..., :3].view(np.uint16)), i
 
 
-@pytest.mark.parametrize("W,H", [(200, 136), (968, 552), (3840, 2160)])
-def test_bloom_fused_stages_equal_eight_passes(soc, W, H):
-    """The 4 fused kernels against the reference's 8 separate passes, on the GPU, with a separate
-    bloom output (the emissive input stays untouched) and per stage."""
-    g = globals_for(W, H)
-    em = dev(random_rgba16(H, W, seed=17, hi=16.0))
-    shapes = [(H >> i, W >> i, 4) for i in range(4)]
-    ref_mips = [torch.zeros(s, dtype=torch.float16, device=DEV) for s in shapes]
-    ref_out = torch.zeros_like(em)
-    soc.bloom_downsample(g, em, ref_mips[0])
-    for i in range(3):
-        soc.bloom_downsample(g, ref_mips[i], ref_mips[i + 1])
-    for i in range(3, 0, -1):
-        soc.bloom_upsample(g, ref_mips[i], ref_mips[i - 1])
-    soc.bloom_upsample(g, ref_mips[0], ref_out)
-    mips = [torch.full(s, 7.0, dtype=torch.float16, device=DEV) for s in shapes]
-    out = torch.zeros_like(em)
-    em_before = em.clone()
-    for st in (1, 2, 3, 4):
-        soc.bloom_fused_stage(g, em, mips, out, st)
-    torch.cuda.synchronize()
-    assert torch.equal(em, em_before)
-    assert torch.equal(out[..., :3].view(torch.int16), ref_out[..., :3].view(torch.int16))
-    for i in (1, 2, 3):   # mip0's final state is written by stage 4 as well
-        assert torch.equal(mips[i][..., :3].view(torch.int16), ref_mips[i][..., :3].view(torch.int16)), i
-    assert torch.equal(mips[0][..., :3].view(torch.int16), ref_mips[0][..., :3].view(torch.int16))
-
-
 @pytest.mark.parametrize("W,H", [(64, 40), (200, 136), (968, 552), (1920, 1080), (3840, 2160)])
 def test_bloom_weighted_chain(soc, W, H):
     """The weighted-form chain (bloom_w.hip, 4 kernels) against the reference's 8 separate passes

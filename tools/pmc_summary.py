@@ -1,4 +1,4 @@
-"""Summarise tools/pmc.sh output: per-kernel mean counter values per dispatch -> JSON.
+"""Summarise `tools/gpu.sh pmc|traffic` output: per-kernel mean counter values per dispatch -> JSON.
 
 With --traffic OUT.json also writes the per-launch HBM traffic table bench.py reads for the
 roofline's `traffic` field: hbm_bytes = 2 * FETCH_SIZE + WRITE_SIZE (both reported in KiB). The factor

@@ -1,5 +1,7 @@
-"""SSAO variant probe at 4K on the C3 Sponza-proxy G-buffer: times SSAOGeneration under tuning knobs
-(environment variables read per launch) and checks every variant's output against the default's bits.
+"""SSAO variant probe at 4K on the C3 G-buffer: times SSAOGeneration under tuning knobs (environment variables,
+re-read through soc_tuning_reload) and checks every variant's output against the default's bits.
+PROBE_SCENE=mesh (default): the Sponza-proxy mesh rasterised by the HIP rasteriser, as bench.py renders it;
+PROBE_SCENE=boxes: the round-1 box atrium.
 
 usage: python tools/ssao_probe.py KNOB=V[,KNOB=V...] ...   (each argument is one variant; "" = default)
 """
@@ -12,7 +14,7 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 import soc_real_time_renderer_amd as soc  # noqa: E402
-from soc_real_time_renderer_amd import multi_gpu, scene  # noqa: E402
+from soc_real_time_renderer_amd import multi_gpu, raster, scene  # noqa: E402
 from bench import make_globals  # noqa: E402
 
 
@@ -20,9 +22,14 @@ def main():
     W, H = int(os.environ.get("PROBE_W", 3840)), int(os.environ.get("PROBE_H", 2160))
     dev = torch.device("cuda", 0)
     g = make_globals(W, H, multi_gpu.camera_for_rank(0))
-    gb = scene.gbuffer(g, W, H)
-    depth = torch.from_numpy(gb["depth"]).to(dev)
-    normal = torch.from_numpy(gb["normal"]).to(dev)
+    if os.environ.get("PROBE_SCENE", "mesh") == "mesh":
+        sc = raster.scene_setup(g, scene.SPONZA_MESH, tex_size=256, device=dev)
+        gbd = raster.render_gbuffer(g, sc, W, H, 1024, dev)
+        depth, normal = gbd["depth"], gbd["normal"]
+    else:
+        gb = scene.gbuffer(g, W, H)
+        depth = torch.from_numpy(gb["depth"]).to(dev)
+        normal = torch.from_numpy(gb["normal"]).to(dev)
     table = torch.zeros((H // 2) * (W // 2) * 2, dtype=torch.float32, device=dev)
     ref = torch.zeros(H // 2, W // 2, dtype=torch.uint8, device=dev)
     soc.ssao_prepare_noise(normal, ref, table)

@@ -3,7 +3,7 @@ measured gfx950 issue costs (tools/microbench/valu_mix.hip: 4 cycles per wave64 
 ~9.5 for a transcendental, i.e. +5.5 over a plain op) against its measured duration.
 
 usage: python tools/valu_model.py gpurun_out/sqmix_c4 [more dirs] > profiles/<tag>_valu_model.json
-(each dir: a tools/sq_pass.sh output with SQ_INSTS_VALU and SQ_INSTS_VALU_TRANS_F32 and its kernel trace)
+(each dir: a `tools/gpu.sh pmc` output with SQ_INSTS_VALU and SQ_INSTS_VALU_TRANS_F32 and its kernel trace)
 """
 import collections
 import csv
