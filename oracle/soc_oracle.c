@@ -1578,6 +1578,9 @@ int soc_oracle_generate_hiz(const soc_globals* g, soc_img depth, const soc_img* 
     const int dx = (W + 63) / 64, dy = (H + 63) / 64;
     for (int gy = 0; gy < dy; ++gy)
         for (int gx = 0; gx < dx; ++gx) hz_window(&depth, depth.width, depth.height, gx, gy, -1, 6, mips, mip_count, op_max);
-    if (mip_count > 5) hz_window(&mips[5], W >> 6, H >> 6, 0, 0, 5, mip_count - 6, mips, mip_count, op_max);
+    /* the tail reads mip 5 at min(index, extent - 1) (:29-32): an extent of 0 (a frame under 64 texels across) reads
+     * outside the image, undefined in the reference; the tail levels are then not written (hiz.hip does the same) */
+    if (mip_count > 5 && (W >> 6) > 0 && (H >> 6) > 0)
+        hz_window(&mips[5], W >> 6, H >> 6, 0, 0, 5, mip_count - 6, mips, mip_count, op_max);
     return SOC_OK;
 }

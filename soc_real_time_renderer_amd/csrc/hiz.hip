@@ -75,7 +75,9 @@ __global__ __launch_bounds__(256) void hiz_kernel(DImg depth, HizMips mips, uint
     __syncthreads();
     if (lx == 0 && ly == 0) last = atomicAdd(counter, 1u) + 1u == total;
     __syncthreads();
-    if (last && mips.count > 5) {
+    // the tail reads mip 5 at min(index, extent - 1) (generate_hiz.glsl:29-32): an extent of 0 (a frame under 64 texels
+    // across) would read outside the image, which the reference leaves undefined; the tail levels are then not written
+    if (last && mips.count > 5 && (res_w >> 6) > 0 && (res_h >> 6) > 0) {
         __threadfence();
         // mip 5 of the other workgroups, read back through L2 (the reference's coherent image accesses)
         downsample_64x64<MAX>(sh, lx, ly, 0, 0, mips.m[5], res_w >> 6, res_h >> 6, 5, mips.count - 6, mips);
