@@ -55,7 +55,7 @@ import soc_real_time_renderer_amd as soc  # noqa: E402
 from soc_real_time_renderer_amd import multi_gpu, raster, scene  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
-SSAO_KERNEL = "ssao_kernel<true, true, true>"   # the default SSAOGeneration instantiation (ssao.hip)
+SSAO_KERNEL = "ssao_lds_kernel<true, true, true, 64, 16, 32, 2>"   # the default SSAOGeneration kernel (ssao.hip)
 
 
 def make_globals(W, H, camera):

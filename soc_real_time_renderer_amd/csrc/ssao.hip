@@ -120,6 +120,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t depth_rsrc(const DImg& depth) 
 template <bool TABLE, bool SPARSE_IP, bool FULL, class Quad, int UNROLL = SOC_SSAO_MAX_KERNEL>
 __device__ __forceinline__ void ssao_pixel(int x, int y, const DImg& depth, const DImg& normal, const DImg& target,
                                            const float2* __restrict__ table, const SsaoParams& p, const Quad& quad) {
+    // no implicit contraction: every fused multiply-add below is an explicit fma, so the per-pixel arithmetic does not
+    // depend on how the surrounding kernel is unrolled or scheduled (ssao_kernel and ssao_lds_kernel give the same bits)
+#pragma clang fp contract(off)
     const float u = centre_uv_rn(x, target.w, p.rw), v = centre_uv_rn(y, target.h, p.rh);
 
     // normal = mat3(view) * normalize(texture(normal, uv).rgb), :178
@@ -202,12 +205,12 @@ __device__ __forceinline__ void ssao_pixel(int x, int y, const DImg& depth, cons
                 // r / |frag.z - sd| = r vw / |frag.z vw - vz| and sd >= s.z  <=>  s.z vw - vz <= 0 (one
                 // reciprocal per tap instead of two)
                 const float rc = __builtin_amdgcn_fmed3f(r * vw * fast_rcp(fabsf(__builtin_fmaf(frag.z, vw, -vz))), 0.0f, 1.0f);
-                const float range = rc * rc * (3.0f - 2.0f * rc);   // smoothstep(0, 1, x)
+                const float range = rc * rc * __builtin_fmaf(-2.0f, rc, 3.0f);   // smoothstep(0, 1, x)
                 occ += (__builtin_fmaf(aff(az, kx, ky, kz), vw, -vz) <= 0.0f) ? range : 0.0f;
             } else {
                 const float sd = vz * fast_rcp(vw);
                 const float rc = __builtin_amdgcn_fmed3f(r * fast_rcp(fabsf(frag.z - sd)), 0.0f, 1.0f);   // >= 0
-                const float range = rc * rc * (3.0f - 2.0f * rc);   // smoothstep(0, 1, x)
+                const float range = rc * rc * __builtin_fmaf(-2.0f, rc, 3.0f);   // smoothstep(0, 1, x)
                 occ += (sd >= aff(az, kx, ky, kz)) ? range : 0.0f;
             }
         }
@@ -364,20 +367,14 @@ extern "C" int soc_ssao_generation(const soc_globals* g, soc_img depth, soc_img 
     DImg dd = dimg(depth), dn = dimg(normal), dt = dimg(target);
 #define SOC_SSAO_LAUNCH(T, B, F) ssao_kernel<T, B, F><<<grd, blk, 0, st>>>(dd, dn, dt, tb, p)
     const bool full = p.ksize == SOC_SSAO_MAX_KERNEL;
-    const int tile = tuning_knob("SOC_SSAO_TILE", 0);
-#define SOC_SSAO_TILED(TX, TY, HALO, U) ssao_lds_kernel<true, true, true, TX, TY, HALO, U> \
-    <<<dim3(ceil_div(target.width, TX), ceil_div(target.height, TY)), TX * TY, 0, st>>>(dd, dn, dt, tb, p)
-    if (noise_table && sip && full && tile) {
-        switch (tile) {
-        case 1: SOC_SSAO_TILED(64, 16, 32, 26); break;
-        case 3: SOC_SSAO_TILED(32, 8, 48, 26); break;
-        case 4: SOC_SSAO_TILED(32, 8, 32, 26); break;
-        case 6: SOC_SSAO_TILED(32, 8, 64, 26); break;
-        case 11: SOC_SSAO_TILED(64, 16, 32, 2); break;
-        case 13: SOC_SSAO_TILED(32, 8, 48, 2); break;
-        case 14: SOC_SSAO_TILED(32, 8, 32, 2); break;
-        default: SOC_SSAO_TILED(32, 8, 64, 2); break;
-        }
+    // default: the LDS-tiled kernel (64 x 16 pixels, 32-texel halo) in the contiguous-eighths XCD order; SOC_SSAO_TILE=0
+    // selects the plain gather kernel (the same bits: tests/test_gpu_parity.py)
+    const bool tiled = tuning_knob("SOC_SSAO_TILE", 1) != 0;
+    if (noise_table && sip && full && tiled) {
+        SsaoParams pt = p;
+        pt.swz = 1;
+        ssao_lds_kernel<true, true, true, 64, 16, 32, 2>
+            <<<dim3(ceil_div(target.width, 64), ceil_div(target.height, 16)), 1024, 0, st>>>(dd, dn, dt, tb, pt);
     } else if (noise_table && sip && full) SOC_SSAO_LAUNCH(true, true, true);
     else if (noise_table && sip) SOC_SSAO_LAUNCH(true, true, false);
     else if (noise_table) SOC_SSAO_LAUNCH(true, false, false);

@@ -167,21 +167,42 @@ def test_ssao_noise_table_is_bit_identical(soc):
     assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("W,H", [(97, 55), (1920, 1080)])
-def test_ssao_tile_orders_bit_identical(soc, monkeypatch, W, H):
-    """Every workgroup order (row-major, XCD-aware eighths, horizontal and vertical XCD bands: SOC_SWZ_SSAO) computes
-    each pixel the same way (the orders are bijections, also for ragged grids)."""
-    g, gb = sponza_inputs(W, H)
-    depth, normal = dev(gb["depth"]), dev(gb["normal"])
+@pytest.mark.parametrize("W,H,inputs", [(97, 55, "boxes"), (1920, 1080, "boxes"), (1920, 1080, "mesh"), (3840, 2160, "mesh"),
+                                         (130, 1200, "boxes"), (2000, 34, "boxes")])
+def test_ssao_tile_orders_bit_identical(soc, monkeypatch, W, H, inputs):
+    """The LDS-tiled kernel (default: depth tile + 32-texel halo in LDS, the other taps gathered) and the plain gather
+    kernel (SOC_SSAO_TILE=0) give the same bits, in every workgroup order of the gather kernel (row-major, XCD-aware
+    eighths, horizontal and vertical XCD bands: SOC_SWZ_SSAO; the orders are bijections, also for ragged grids), on the
+    box atrium and on the mesh (near geometry: many taps leave the tile), at odd, tall and wide extents (partial tiles,
+    tiles hanging over every image edge)."""
+    if inputs == "mesh":
+        from soc_real_time_renderer_amd import raster, scene
+        import bench
+        g = bench.make_globals(W, H, bench.multi_gpu.camera_for_rank(0))
+        sc = raster.scene_setup(g, scene.SPONZA_MESH, tex_size=64, device=DEV)
+        gbd = raster.render_gbuffer(g, sc, W, H, 256, DEV)
+        depth, normal = gbd["depth"], gbd["normal"]
+    else:
+        g, gb = sponza_inputs(W, H)
+        depth, normal = dev(gb["depth"]), dev(gb["normal"])
+    table = torch.zeros((H // 2) * (W // 2) * 2, dtype=torch.float32, device=DEV)
     outs = []
-    for swz in ("0", "1", "4", "16", "-16", "-3"):
-        monkeypatch.setenv("SOC_SWZ_SSAO", swz)
+    for tile, swz in (("1", None), ("0", "0"), ("0", "1"), ("0", "4"), ("0", "16"), ("0", "-16"), ("0", "-3")):
+        monkeypatch.setenv("SOC_SSAO_TILE", tile)
+        if swz is None:
+            monkeypatch.delenv("SOC_SWZ_SSAO", raising=False)
+        else:
+            monkeypatch.setenv("SOC_SWZ_SSAO", swz)
         soc.reload_tuning()
         out = torch.zeros(H // 2, W // 2, dtype=torch.uint8, device=DEV)
-        soc.ssao_generation(g, depth, normal, out)
+        soc.ssao_prepare_noise(normal, out, table)
+        soc.ssao_generation(g, depth, normal, out, table)
         outs.append(host(out))
+    monkeypatch.delenv("SOC_SSAO_TILE")
+    monkeypatch.delenv("SOC_SWZ_SSAO", raising=False)
+    soc.reload_tuning()
     for o in outs[1:]:
-        assert np.array_equal(o, outs[0])
+        assert np.array_equal(o, outs[0]), int((o != outs[0]).sum())
 
 
 @pytest.mark.parametrize("W,H", [(64, 36), (97, 55), (1920, 1080)])
