@@ -1083,7 +1083,8 @@ static int ensure_side_lane(soc_renderer* r) {
         r->side = nullptr;
         r->fork_ev = r->join_ev = nullptr;
     }
-    if (hipStreamCreateWithFlags(&r->side, hipStreamNonBlocking) != hipSuccess ||
+    const hipError_t se = hipStreamCreateWithFlags(&r->side, hipStreamNonBlocking);
+    if (se != hipSuccess ||
         hipEventCreateWithFlags(&r->fork_ev, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&r->join_ev, hipEventDisableTiming) != hipSuccess)
         return set_error(SOC_E_HIP, "soc_renderer_execute: second lane stream/event creation failed");
