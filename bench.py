@@ -131,14 +131,32 @@ def ssao_gather_bound(W, H, scene_name, ssao_us):
         return None
     with open(files[-1]) as fh:
         t = json.load(fh)
-    if list(t.get("resolution", [])) != [W, H] or t.get("scene") != scene_name:
-        return None
+    if list(t.get("resolution", [])) != [W, H] or t.get("scene") != scene_name or t.get("kernel") != SSAO_KERNEL:
+        return None   # a table of another workload or of another SSAO kernel (round 2's gather kernel)
     loads, cus = float(t["counters"]["SQ_INSTS_VMEM_RD"]), int(t["cus"])
     rate = t["gather_rate_ns_per_wave_load_per_cu"]
     us_c = loads * rate["one_line"] / cus / 1e3
     us_s = loads * rate["four_or_more_lines_l1"] / cus / 1e3
     return {"wave_loads_per_launch": int(loads), "us_if_coalesced": round(us_c, 1), "us_if_scattered": round(us_s, 1),
             "frac_of_scattered_rate": round(us_s / ssao_us, 3), "source": os.path.relpath(files[-1], ROOT)}
+
+
+def valu_bound(kernel, us):
+    """The kernel's VALU issue time from the committed issue model (profiles/*valu_model.json: SQ_INSTS_VALU and
+    SQ_INSTS_VALU_TRANS_F32 per launch of the same C3 command at 4 cycles per wave64 VALU instruction and +5.5 per
+    transcendental over 1024 SIMDs at 2.4 GHz, tools/valu_model.py) against its measured time `us`, or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*valu_model.json")))
+    if not files:
+        return None
+    with open(files[-1]) as fh:
+        t = json.load(fh)
+    for rows in t.get("runs", {}).values():
+        if kernel in rows:
+            r = rows[kernel]
+            return {"valu_issue_us": r["issue_bound_us"], "frac_of_launch": round(r["issue_bound_us"] / us, 3),
+                    "serial_us": r["us"], "source": os.path.relpath(files[-1], ROOT)}
+    return None
 
 
 def cpu_baseline(W, H, host_inputs, g):
@@ -394,7 +412,9 @@ def main():
                                             "algorithmic_bytes_per_launch": int(algo["SSAOGeneration"]),
                                             "avg_launch_us": round(ssao_ms * 1e3, 2),
                                             "gather_bound": (ssao_gather_bound(W, H, args.scene, ssao_ms * 1e3)
-                                                             if args.config == "c3" else None)}}},
+                                                             if args.config == "c3" else None),
+                                            "valu_bound": (valu_bound(SSAO_KERNEL, ssao_ms * 1e3)
+                                                           if pmc_ok else None)}}},
         "ranks": per_rank,
         "allreduce_us_per_frame": (round(sum(p["allreduce_us_per_frame"] for p in per_rank) / world, 2)
                                    if world > 1 else None),

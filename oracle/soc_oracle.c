@@ -1268,15 +1268,13 @@ int soc_oracle_generate_mips(soc_img tex) {
     if (!tex.data || tex.width <= 0 || tex.height <= 0 || tex.pitch_bytes < tex.width * 4 ||
         (tex.format != SOC_FMT_RGBA8_UNORM && tex.format != SOC_FMT_RGBA8_SRGB))
         return SOC_E_INVALID_ARG;
-    /* sRGB tables in double precision: decode per code, re-encode to the nearest code (midpoints) */
+    /* sRGB tables in double precision: decode per code; re-encode as a LINEAR blit does, encode then round: code k
+     * from the boundary decode((k - 0.5) / 255) up (the decoded codes' midpoints biased near a boundary) */
     float dec[256], mid[256];
-    double prev = 0.0;
     for (int k = 0; k < 256; ++k) {
-        const double c = k / 255.0;
-        const double d = c <= 0.04045 ? c / 12.92 : pow((c + 0.055) / 1.055, 2.4);
-        dec[k] = (float)d;
-        mid[k] = k ? (float)(0.5 * (prev + d)) : 0.0f;
-        prev = d;
+        const double c = k / 255.0, b = (k - 0.5) / 255.0;
+        dec[k] = (float)(c <= 0.04045 ? c / 12.92 : pow((c + 0.055) / 1.055, 2.4));
+        mid[k] = k ? (float)(b <= 0.04045 ? b / 12.92 : pow((b + 0.055) / 1.055, 2.4)) : 0.0f;
     }
     const int srgb = tex.format == SOC_FMT_RGBA8_SRGB, L = mip_levels(tex.width, tex.height);
     for (int k = 1; k < L; ++k) {

@@ -17,7 +17,8 @@ namespace {
 
 struct SrgbTables {
     float dec[256];   // srgb_decode(k / 255)
-    float mid[256];   // mid[k] = midpoint of dec[k-1] and dec[k] (k >= 1); mid[0] unused
+    float mid[256];   // mid[k] = srgb_decode((k - 0.5) / 255) (k >= 1): the linear value whose sRGB encoding rounds up
+                      // to code k, as a LINEAR blit's encode-then-round does; mid[0] unused
 };
 
 double srgb_decode_d(double c) { return c <= 0.04045 ? c / 12.92 : std::pow((c + 0.055) / 1.055, 2.4); }
@@ -25,12 +26,9 @@ double srgb_decode_d(double c) { return c <= 0.04045 ? c / 12.92 : std::pow((c +
 const SrgbTables& srgb_tables() {
     static SrgbTables t = [] {
         SrgbTables r{};
-        double prev = 0.0;
         for (int k = 0; k < 256; ++k) {
-            const double d = srgb_decode_d(k / 255.0);
-            r.dec[k] = (float)d;
-            r.mid[k] = k ? (float)(0.5 * (prev + d)) : 0.0f;
-            prev = d;
+            r.dec[k] = (float)srgb_decode_d(k / 255.0);
+            r.mid[k] = k ? (float)srgb_decode_d((k - 0.5) / 255.0) : 0.0f;
         }
         return r;
     }();
@@ -54,7 +52,7 @@ __device__ __forceinline__ Axis blit_axis(int x, int n_src, int n_dst) {
     return a;
 }
 
-// Nearest sRGB code of a linear value: the number of midpoints <= c (binary search over mid[1..255]).
+// sRGB code of a linear value, round(encode(c) * 255): the number of boundaries mid[1..255] <= c (binary search).
 __device__ __forceinline__ uint32_t srgb_encode_code(float c, const SrgbTables& t) {
     uint32_t k = 0;
 #pragma unroll

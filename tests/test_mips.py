@@ -20,8 +20,9 @@ def srgb_encode(c):
     return np.where(c <= 0.0031308, c * 12.92, 1.055 * c ** (1 / 2.4) - 0.055)
 
 
-def np_blit(src, dw, dh, srgb):
-    """Bilinear sample of src at ((x + .5) sw / dw, (y + .5) sh / dh), clamp to edge, float64."""
+def np_blit(src, dw, dh, srgb, raw=False):
+    """Bilinear sample of src at ((x + .5) sw / dw, (y + .5) sh / dh), clamp to edge, float64; raw: the unrounded code
+    value (encode(f) * 255 for sRGB channels, f * 255 for the others) instead of the rounded code."""
     sh, sw = src.shape[:2]
     lin = src.astype(np.float64) / 255.0
     if srgb:
@@ -40,7 +41,8 @@ def np_blit(src, dw, dh, srgb):
     f = top * (1 - wy)[:, None, None] + bot * wy[:, None, None]
     if srgb:
         f[..., :3] = srgb_encode(f[..., :3])
-    return np.rint(np.clip(f, 0, 1) * 255.0).astype(np.int32)
+    v = np.clip(f, 0, 1) * 255.0
+    return v if raw else np.rint(v).astype(np.int32)
 
 
 def host_chain(level0, srgb):
@@ -70,10 +72,19 @@ def test_oracle_chain_vs_numpy_blit(W, H, srgb):
     assert np.array_equal(levels[0], level0)
     for k in range(1, len(levels)):
         h, w = levels[k].shape[:2]
-        ref = np_blit(levels[k - 1], w, h, srgb)
+        raw = np_blit(levels[k - 1], w, h, srgb, raw=True)
+        ref = np.rint(raw).astype(np.int32)
         d = np.abs(levels[k].astype(np.int32) - ref)
         assert d.max() <= 1, (k, d.max())
-        assert d.size < 256 or (d == 0).mean() > 0.85, k      # the +-1 cases are rounding ties (a 2x2 mean ends in .5 1/4 of the time)
+        # every code equals the float64 blit's (encode-then-round for sRGB, texture.cpp:190-246 LINEAR blits) except at
+        # genuine ties: values within the fp32 filter's rounding of a .5 code boundary (a 2x2 mean ends in .5 often)
+        sh_, sw_ = levels[k - 1].shape[:2]
+        exact = (sw_ == 2 * w or sw_ == w == 1) and (sh_ == 2 * h or sh_ == h == 1)   # weights 1/2 (or 1): no 8-bit quantisation
+        if exact:
+            tie = np.abs(raw - np.floor(raw) - 0.5) < 2e-3
+            assert (tie | (d == 0)).all(), (k, np.argwhere(~(tie | (d == 0)))[:5], raw[~(tie | (d == 0))][:5])
+        else:   # odd extents: the contract's 8-bit sub-texel weights against exact float64 weights
+            assert d.size < 256 or (d == 0).mean() > 0.85, k
 
 
 def test_oracle_chain_constant_and_gradient():

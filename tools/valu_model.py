@@ -2,8 +2,10 @@
 measured gfx950 issue costs (tools/microbench/valu_mix.hip: 4 cycles per wave64 VALU instruction per SIMD,
 ~9.5 for a transcendental, i.e. +5.5 over a plain op) against its measured duration.
 
-usage: python tools/valu_model.py gpurun_out/sqmix_c4 [more dirs] > profiles/<tag>_valu_model.json
-(each dir: a `tools/gpu.sh pmc` output with SQ_INSTS_VALU and SQ_INSTS_VALU_TRANS_F32 and its kernel trace)
+usage: python tools/valu_model.py [--durations KT_DIR] [--calibration VMIX_DIR] PMC_DIR [more dirs] > profiles/<tag>_valu_model.json
+(each PMC_DIR: a `tools/gpu.sh pmc` output with SQ_INSTS_VALU and SQ_INSTS_VALU_TRANS_F32; KT_DIR: a counter-free
+`tools/gpu.sh kt` trace of the same build and command, whose median durations replace the counter runs' own;
+VMIX_DIR: the same counters over tools/microbench/valu_mix, whose instruction counts are known, to check the counter)
 """
 import collections
 import csv
@@ -27,26 +29,54 @@ def load(d):
     return counters, durs
 
 
+def opt(name):
+    if name in sys.argv:
+        i = sys.argv.index(name)
+        v = sys.argv[i + 1]
+        del sys.argv[i:i + 2]
+        return v
+    return None
+
+
 def main():
+    kt_dir, vmix_dir = opt("--durations"), opt("--calibration")
+    kt_durs = load(kt_dir)[1] if kt_dir else None
     out = {"model": {"valu_cycles_per_wave_instr": VALU_CYC, "trans_extra_cycles": TRANS_EXTRA, "simds": SIMDS,
                      "clock_ghz": CLOCK_GHZ, "source": "tools/microbench/valu_mix.hip (8 waves/SIMD, full chip)"},
            "runs": {}}
+    if vmix_dir:   # valu_mix: 2048 blocks x 4 waves x 2048 iterations x 8 chains x per-iteration VALU ops per dispatch
+        counters, _ = load(vmix_dir)
+        per_iter = {"FMA": 1, "EXP": 1, "SQRT": 1, "RCP": 1, "CVT_I32": 1, "CVT_F32": 1, "FLOOR": 1, "DOT2": 1, "PERM": 2,
+                    "MIX_EXP_2FMA": 3, "MIX_SQRT_4FMA": 5}
+        cal = {}
+        for k, c in counters.items():
+            kind = next((n for n in sorted(per_iter, key=len, reverse=True) if f"(Kind){n}" in k or f"<{n}>" in k or f"Kind){list(per_iter).index(n)}" in k), None)
+            mean = {n: sum(v) / len(v) for n, v in c.items()}
+            expected = 2048 * 4 * 2048 * 8 * per_iter[kind] if kind else None
+            cal[k[:80]] = {"SQ_INSTS_VALU": int(mean.get("SQ_INSTS_VALU", 0)), "expected_wave_instr": expected,
+                           "ratio": round(mean.get("SQ_INSTS_VALU", 0) / expected, 4) if expected else None,
+                           "SQ_INSTS_VALU_TRANS_F32": int(mean.get("SQ_INSTS_VALU_TRANS_F32", 0))}
+        out["counter_calibration"] = cal
     for d in sys.argv[1:]:
         counters, durs = load(d)
+        if kt_durs is not None:
+            durs = kt_durs
         rows = {}
         for k, c in counters.items():
-            if "clouds" not in k and "ssao_kernel" not in k and "composition_pair" not in k and "sky_compose" not in k:
+            if not any(t in k for t in ("clouds", "ssao", "composition_pair", "sky_compose", "taa_pair", "bloomw", "tonemap")):
                 continue
             mean = {n: sum(v) / len(v) for n, v in c.items()}
             if "SQ_INSTS_VALU" not in mean or not durs.get(k):
                 continue
+            extra = {n: int(v) for n, v in mean.items() if n in ("SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD", "SQ_WAVES",
+                                                                  "SQ_INSTS_VMEM_WR", "SQ_INSTS_SMEM")}
             us = sorted(durs[k])[len(durs[k]) // 2]
             trans = mean.get("SQ_INSTS_VALU_TRANS_F32", 0.0)
             need_us = (VALU_CYC * mean["SQ_INSTS_VALU"] + TRANS_EXTRA * trans) / SIMDS / (CLOCK_GHZ * 1e3)
             short = k.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0].replace("soc::", "")
             rows[short] = {"us": round(us, 1), "valu_wave_instr": int(mean["SQ_INSTS_VALU"]), "trans": int(trans),
                            "issue_bound_us": round(need_us, 1), "valu_issue_fraction": round(need_us / us, 3),
-                           "mix": {n[14:]: int(v) for n, v in mean.items() if n.startswith("SQ_INSTS_VALU_")}}
+                           "mix": {n[14:]: int(v) for n, v in mean.items() if n.startswith("SQ_INSTS_VALU_")}, **extra}
         out["runs"][os.path.basename(d.rstrip("/"))] = rows
     json.dump(out, sys.stdout, indent=1, sort_keys=True)
 
