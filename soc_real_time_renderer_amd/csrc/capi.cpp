@@ -635,6 +635,8 @@ struct soc_renderer {
     bool fold_in_resolve = false;
     // sky split configured (graph) / active this frame (the pair path applies at the globals' resolution)
     bool sky_split = false, sky_split_active = false;
+    // the caller's stream is ordered after all second-lane work of the previous call (its join or an equivalent wait)
+    bool main_after_side = true;
 };
 
 namespace {
@@ -977,7 +979,10 @@ void destroy_pass_events(soc_renderer* r) {
     }
 }
 
-// A pass records its completion event when a pass of the other lane depends on it, in its own frame or the next.
+// A pass records its completion event when a pass of the other lane may wait on it: an in-frame dependency across
+// the lanes, or a ring edge from a main-lane pass onto a second-lane pass (waited on only when the previous call ended
+// without its join). Ring edges from second-lane passes onto main-lane passes are covered by the fork, so a main-lane
+// pass whose only cross-lane dependents are such edges records nothing (an event record costs its queue a marker).
 void derive_signals(soc_renderer* r) {
     const int n = (int)r->passes.size();
     for (auto& p : r->passes) p.signal = false;
@@ -985,8 +990,9 @@ void derive_signals(soc_renderer* r) {
         const bool li = (r->passes[i].flags & SOC_PASS_ASYNC) != 0;
         for (int j : r->passes[i].deps)
             if (((r->passes[j].flags & SOC_PASS_ASYNC) != 0) != li) r->passes[j].signal = true;
-        for (int j : r->passes[i].carry)
-            if (((r->passes[j].flags & SOC_PASS_ASYNC) != 0) != li) r->passes[j].signal = true;
+        if (!li)
+            for (int j : r->passes[i].carry)
+                if ((r->passes[j].flags & SOC_PASS_ASYNC) != 0) r->passes[j].signal = true;
     }
 }
 
@@ -1102,7 +1108,11 @@ static int static_lane(const soc_renderer* r, int i) {
 // that would clear them did not run) so they are not counted into the next frame's exposure. The TAA history is
 // not flipped: the next frame reads the last completed frame's history.
 static int abort_frame(soc_renderer* r, hipStream_t s, bool forked, int rc) {
-    if (forked && r->side && hipEventRecord(r->join_ev, r->side) == hipSuccess) (void)hipStreamWaitEvent(s, r->join_ev, 0);
+    if (forked && r->side && hipEventRecord(r->join_ev, r->side) == hipSuccess &&
+        hipStreamWaitEvent(s, r->join_ev, 0) == hipSuccess)
+        r->main_after_side = true;
+    else if (forked)
+        r->main_after_side = false;
     if (r->hist_scratch) (void)hipMemsetAsync(r->hist_scratch, 0, SOC_HISTOGRAM_SCRATCH_WORDS * sizeof(uint32_t), s);
     if (r->img.auto_exposure)
         (void)hipMemsetAsync(r->img.auto_exposure->histogram_buckets, 0, sizeof(r->img.auto_exposure->histogram_buckets), s);
@@ -1168,7 +1178,8 @@ extern "C" int soc_renderer_execute(soc_renderer* r, const soc_globals* g, int32
         if (rc) return rc;
         // fork (the frame-inputs edge): the second lane starts after everything the caller queued before this
         // call (e.g. the depth image it uploaded)
-        if (hipEventRecord(r->fork_ev, s) != hipSuccess || hipStreamWaitEvent(r->side, r->fork_ev, 0) != hipSuccess)
+        if (!tuning_knob("SOC_EXP_NO_FORK", 0) &&
+            (hipEventRecord(r->fork_ev, s) != hipSuccess || hipStreamWaitEvent(r->side, r->fork_ev, 0) != hipSuccess))
             return set_error(SOC_E_HIP, "soc_renderer_execute: second lane fork failed");
     }
     // issue order: by default (tuning knob SOC_RENDERER_SSAO_FIRST=1) the AO passes ahead of the
@@ -1188,24 +1199,33 @@ extern "C" int soc_renderer_execute(soc_renderer* r, const soc_globals* g, int32
             order.insert(order.end(), rest.begin(), rest.end());
         }
     }
-    int last_side = -1;            // the second lane's last pass of this call
-    bool side_joined = false;      // a later main-lane pass of this call waits on it
+    // Each lane is one in-order stream, so a wait on the other lane's pass at position k (in this call's issue order on
+    // that lane) also covers every earlier pass of it: waits already covered are not issued again (each costs the
+    // waiting queue a barrier packet, ~10 us of idle measured between dependent kernels).
+    std::vector<int> pos(n, -1);
+    int next_pos[2] = {0, 0}, waited[2] = {-1, -1};
     for (int oi = 0; oi < n; ++oi) {
         const int i = order[oi];
         if (lane[i] < 0) continue;
         auto& p = r->passes[i];
-        hipStream_t ls = lane[i] ? r->side : s;
+        const int L = lane[i];
+        hipStream_t ls = L ? r->side : s;
         for (int j : deps[i])
-            if (lane[j] != lane[i]) {
+            if (lane[j] != L && pos[j] > waited[L]) {
                 if (hipStreamWaitEvent(ls, r->passes[j].done, 0) != hipSuccess)
                     return abort_frame(r, s, lanes, set_error(SOC_E_HIP, "soc_renderer_execute: %s: cross-lane wait failed", p.name.c_str()));
-                if (lane[i] == 0 && j == last_side) side_joined = true;
+                waited[L] = pos[j];
             }
+        // ring edges and edges into another phase's call: sources of an earlier call. The second lane is ordered after
+        // them by this call's fork; the caller's stream by the end of that earlier call (its join, or a main-lane wait
+        // on the second lane's last pass), so a wait is issued only if that call ended without either.
         for (int j : ext[i])
-            if (r->passes[j].done_recorded && hipStreamWaitEvent(ls, r->passes[j].done, 0) != hipSuccess)
+            if (L == 0 && !r->main_after_side && r->passes[j].done_recorded &&
+                hipStreamWaitEvent(ls, r->passes[j].done, 0) != hipSuccess)
                 return abort_frame(r, s, lanes, set_error(SOC_E_HIP, "soc_renderer_execute: %s: ring-edge wait failed", p.name.c_str()));
         int rc = run_pass(p, g, ls);
         if (rc) return abort_frame(r, s, lanes, rc);
+        pos[i] = next_pos[L]++;
         if (p.signal) {
             if (!p.done && hipEventCreateWithFlags(&p.done, hipEventDisableTiming) != hipSuccess)
                 return abort_frame(r, s, lanes, set_error(SOC_E_HIP, "soc_renderer_execute: hipEventCreate failed"));
@@ -1213,13 +1233,14 @@ extern "C" int soc_renderer_execute(soc_renderer* r, const soc_globals* g, int32
                 return abort_frame(r, s, lanes, set_error(SOC_E_HIP, "soc_renderer_execute: %s: event record failed", p.name.c_str()));
             p.done_recorded = true;
         }
-        if (lane[i] == 1) { last_side = i; side_joined = false; }
     }
-    // join (the caller's edge, not the graph's): everything of this call is ordered before whatever the caller
-    // queues next on `stream`. Skipped when a main-lane pass already waited on the second lane's last pass.
+    // join (the caller's edge): everything of this call is ordered before whatever the caller queues next on `stream`.
+    // Not issued when a main-lane pass already waited on the second lane's last pass.
+    const bool side_joined = waited[0] >= next_pos[1] - 1;
     if (lanes && !side_joined &&
         (hipEventRecord(r->join_ev, r->side) != hipSuccess || hipStreamWaitEvent(s, r->join_ev, 0) != hipSuccess))
         return abort_frame(r, s, false, set_error(SOC_E_HIP, "soc_renderer_execute: second lane join failed"));
+    r->main_after_side = true;
     if (phase & SOC_PHASE_POST_EXPOSURE) r->hist = 1 - r->hist;   // ping-pong the TAA history
     return SOC_OK;
 }
