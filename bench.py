@@ -242,6 +242,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-frames", type=int, default=20)
     ap.add_argument("--no-sky-lane", action="store_true", help="run CloudRendering on the frame stream too")
+    ap.add_argument("--no-static-inputs", action="store_true",
+                    help="fork the second lane at every frame start (no cross-frame overlap of the clouds)")
     ap.add_argument("--unfused-histogram", action="store_true",
                     help="Composition and the luminance histogram as two launches (SOC_RENDERER_UNFUSED_HISTOGRAM)")
     ap.add_argument("--write-frame", default="", help="write the last frame: tone-mapped framebuffer (.png) or HDR composition colour (.exr, f16)")
@@ -270,7 +272,10 @@ def main():
     g, gb, shadow, noise, sc, fr = build_inputs(args.config, args.scene, W, H, rank, device, mips=not args.no_mips)
     scene_id = scene.TERRAIN if terrain else (scene.SPONZA_PROXY if args.scene == "boxes" else scene.SPONZA_MESH)
     f_sky = float((gb["depth"] == 1.0).mean())
-    r = soc.Renderer(fr, sky_lane=not args.no_sky_lane, fused_histogram=not args.unfused_histogram)
+    # the G-buffer, shadow map and noise stay resident and unchanged between frames (or come from the raster head):
+    # the second lane may start a frame's clouds before the previous frame's TAA is done (SOC_RENDERER_STATIC_INPUTS)
+    r = soc.Renderer(fr, sky_lane=not args.no_sky_lane, fused_histogram=not args.unfused_histogram,
+                     static_inputs=not args.no_static_inputs)
     if args.raster:
         if sc is None:
             sc = raster.scene_setup(g, scene_id, tex_size=1024, device=device)
@@ -392,7 +397,9 @@ def main():
                    "resolution": [W, H], "f_sky": round(f_sky, 4), "parallelism": f"frame-per-gpu x{world}",
                    "histogram_allreduce": world > 1,
                    "collective_backend": (dist.get_backend() if world > 1 else None),
-                   "sky_lane": "CloudRendering on a concurrent stream, joined before Composition",
+                   "sky_lane": ("CloudRendering + SkyCompose on a concurrent stream; " +
+                                ("the clouds of frame N+1 may start before frame N's TAA (static inputs)"
+                                 if not args.no_static_inputs else "forked at every frame start")),
                    "raster": (f"in-frame: DepthPrepass + SunShadowDraw (4096^2) + GBufferGeneration of the "
                               f"{int(sc['mesh'].struct.triangle_count)}-triangle scene mesh") if args.raster
                    else "off: G-buffer and shadow map are resident inputs"},

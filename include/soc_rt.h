@@ -387,6 +387,11 @@ typedef struct soc_renderer soc_renderer;
 #define SOC_RENDERER_EXACT_BLOOM 32       /* bit-exact 8-pass bloom chain instead of the weighted form (bloom_w.hip) */
 #define SOC_RENDERER_UNFUSED_HISTOGRAM 64 /* composition and luminance histogram as two passes */
 #define SOC_RENDERER_NO_SKY_SPLIT 128     /* Composition writes the sky pixels itself (waits for the clouds) */
+/* The caller does not rewrite the frame's input images (G-buffer, shadow map, noise) between frames, e.g. a resident
+ * G-buffer, or one produced in the graph by the raster head. Second-lane passes whose only cross-frame dependencies are
+ * on the second lane (CloudRendering: it writes only CLOUDS) may then start before the fork, i.e. before the caller's
+ * stream reaches this frame: the clouds of frame N+1 overlap the composition / TAA of frame N. Same results. */
+#define SOC_RENDERER_STATIC_INPUTS 256
 
 soc_renderer* soc_renderer_create(const soc_frame_images* images, uint32_t flags);
 void soc_renderer_destroy(soc_renderer* r);

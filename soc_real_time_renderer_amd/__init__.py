@@ -356,7 +356,7 @@ class Renderer:
 
     def __init__(self, frame: dict, timing: bool = False, stream=None, fused_bloom: bool = True, sky_lane: bool = True,
                  fused_tonemap: bool = True, fused_histogram: bool = True,
-                 exact_bloom: bool = False, sky_split: bool = True):
+                 exact_bloom: bool = False, sky_split: bool = True, static_inputs: bool = False):
         self.frame = frame
         fi = FrameImages()
         for k in ("albedo", "emissive", "normal", "depth", "velocity", "shadow", "noise", "ssao", "ssao_blur", "clouds",
@@ -377,7 +377,8 @@ class Renderer:
         flags = ((_abi.RENDERER_TIMING if timing else 0) | (0 if fused_bloom else _abi.RENDERER_UNFUSED_BLOOM)
                  | (0 if sky_lane else _abi.RENDERER_SERIAL) | (0 if fused_tonemap else _abi.RENDERER_UNFUSED_TONEMAP)
                  | (0 if fused_histogram else _abi.RENDERER_UNFUSED_HISTOGRAM)
-                 | (_abi.RENDERER_EXACT_BLOOM if exact_bloom else 0) | (0 if sky_split else _abi.RENDERER_NO_SKY_SPLIT))
+                 | (_abi.RENDERER_EXACT_BLOOM if exact_bloom else 0) | (0 if sky_split else _abi.RENDERER_NO_SKY_SPLIT)
+                 | (_abi.RENDERER_STATIC_INPUTS if static_inputs else 0))
         h = lib().soc_renderer_create(C.byref(fi), flags)
         if not h:
             raise SocError(-1, lib().soc_last_error_string().decode())

@@ -775,15 +775,20 @@ void build_passes_tail(soc_renderer* r) {
                    soc::composition_pair_applicable(&gres, I.color, I.albedo, em_img, I.normal, I.depth, I.clouds);
     const uint64_t sky_w = r->sky_split ? res_mask({SOC_RES_SKY_COLOR, SOC_RES_SKY_HISTOGRAM_PARTIALS}) : 0;
     const uint64_t parts = res_mask({SOC_RES_HISTOGRAM_PARTIALS}) | (r->sky_split ? res_mask({SOC_RES_SKY_HISTOGRAM_PARTIALS}) : 0);
-    // renderer.cpp:1094-1101
-    add_pass(r, "CloudRendering", "Sky Rendering", pre, res_mask({SOC_RES_DEPTH, SOC_RES_NOISE}),
-             res_mask({SOC_RES_CLOUDS}) | sky_w, [r](const soc_globals* g, hipStream_t s) {
-                 int rc = soc_cloud_rendering(g, r->img.depth, r->img.noise, r->img.clouds, r->img.clouds_workspace,
-                                              (soc_stream)s);
-                 if (rc || !r->sky_split_active) return rc;
-                 return soc::sky_compose_launch(g, r->img.color, r->img.depth, r->img.clouds, r->hist_scratch,
-                                                (soc_stream)s);
+    // renderer.cpp:1094-1101. Under the sky split the second lane then writes and bins the colour's sky pixels
+    // (SkyCompose, composition.inl:220-222): a pass of its own, so CloudRendering itself has no cross-lane ring edge
+    // (it writes only CLOUDS) and, with SOC_RENDERER_STATIC_INPUTS, may start before the fork.
+    add_pass(r, "CloudRendering", "Sky Rendering", pre, res_mask({SOC_RES_DEPTH, SOC_RES_NOISE}), res_mask({SOC_RES_CLOUDS}),
+             [r](const soc_globals* g, hipStream_t s) {
+                 return soc_cloud_rendering(g, r->img.depth, r->img.noise, r->img.clouds, r->img.clouds_workspace,
+                                            (soc_stream)s);
              }, SOC_PASS_ASYNC);
+    if (r->sky_split)
+        add_pass(r, "SkyCompose", "Sky Rendering", pre, res_mask({SOC_RES_CLOUDS, SOC_RES_DEPTH}), sky_w,
+                 [r](const soc_globals* g, hipStream_t s) {
+                     return soc::sky_compose_launch(g, r->img.color, r->img.depth, r->img.clouds, r->hist_scratch,
+                                                    (soc_stream)s);
+                 }, SOC_PASS_ASYNC);
     // renderer.cpp:1103-1117 (composition uses) and 1155-1162 (histogram): one launch by default (the colour
     // is binned as it is written), two with SOC_RENDERER_UNFUSED_HISTOGRAM (measured in composition.hip)
     const uint64_t comp_reads = res_mask({SOC_RES_ALBEDO, em_res, SOC_RES_NORMAL, SOC_RES_DEPTH, SOC_RES_SSAO_BLUR,
@@ -1173,13 +1178,17 @@ extern "C" int soc_renderer_execute(soc_renderer* r, const soc_globals* g, int32
         for (int j : p.deps)
             if (lane[j] < 0 && !(r->passes[j].phase & phase) && static_lane(r, j) != lane[i]) ext[i].push_back(j);
     }
+    // The fork orders the second lane after everything the caller queued on `stream` before this call: the frame
+    // inputs it wrote (e.g. the depth image), and the previous frame's main-lane passes that second-lane passes have
+    // ring edges on (SkyCompose after TAA and the resolve). With SOC_RENDERER_STATIC_INPUTS the caller does not rewrite
+    // the frame inputs between frames, so second-lane passes without such a ring edge (CloudRendering, which writes
+    // only CLOUDS) run before the fork: the second lane starts the frame's clouds as soon as the previous frame's
+    // second-lane work is done, overlapping the previous frame's composition and TAA.
+    bool forked_wait = false;
     if (lanes) {
         int rc = ensure_side_lane(r);
         if (rc) return rc;
-        // fork (the frame-inputs edge): the second lane starts after everything the caller queued before this
-        // call (e.g. the depth image it uploaded)
-        if (!tuning_knob("SOC_EXP_NO_FORK", 0) &&
-            (hipEventRecord(r->fork_ev, s) != hipSuccess || hipStreamWaitEvent(r->side, r->fork_ev, 0) != hipSuccess))
+        if (hipEventRecord(r->fork_ev, s) != hipSuccess)
             return set_error(SOC_E_HIP, "soc_renderer_execute: second lane fork failed");
     }
     // issue order: by default (tuning knob SOC_RENDERER_SSAO_FIRST=1) the AO passes ahead of the
@@ -1199,6 +1208,16 @@ extern "C" int soc_renderer_execute(soc_renderer* r, const soc_globals* g, int32
             order.insert(order.end(), rest.begin(), rest.end());
         }
     }
+    std::vector<char> needs_fork(n, 0);
+    bool pre_fork = true;
+    for (int oi = 0; oi < n; ++oi) {
+        const int i = order[oi];
+        if (lane[i] != 1) continue;
+        bool carry_main = false;
+        for (int j : r->passes[i].carry) carry_main |= static_lane(r, j) == 0;
+        if (!(r->flags & SOC_RENDERER_STATIC_INPUTS) || carry_main) pre_fork = false;
+        needs_fork[i] = !pre_fork;
+    }
     // Each lane is one in-order stream, so a wait on the other lane's pass at position k (in this call's issue order on
     // that lane) also covers every earlier pass of it: waits already covered are not issued again (each costs the
     // waiting queue a barrier packet, ~10 us of idle measured between dependent kernels).
@@ -1210,6 +1229,11 @@ extern "C" int soc_renderer_execute(soc_renderer* r, const soc_globals* g, int32
         auto& p = r->passes[i];
         const int L = lane[i];
         hipStream_t ls = L ? r->side : s;
+        if (L == 1 && needs_fork[i] && !forked_wait) {
+            if (hipStreamWaitEvent(r->side, r->fork_ev, 0) != hipSuccess)
+                return abort_frame(r, s, lanes, set_error(SOC_E_HIP, "soc_renderer_execute: second lane fork failed"));
+            forked_wait = true;
+        }
         for (int j : deps[i])
             if (lane[j] != L && pos[j] > waited[L]) {
                 if (hipStreamWaitEvent(ls, r->passes[j].done, 0) != hipSuccess)

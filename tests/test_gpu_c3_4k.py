@@ -22,11 +22,11 @@ def test_c3_bench_frame_4k_vs_oracle(soc, oracle):
     W, H = 3840, 2160
     dev = torch.device("cuda", 0)
     g, gb, shadow, noise, sc, fr = bench.build_inputs("c3", "mesh", W, H, 0, dev)
-    r = soc.Renderer(fr)                               # the bench's renderer flags (defaults)
+    r = soc.Renderer(fr, static_inputs=True)          # the bench's renderer flags
     r.set_exposure_pixels(W * H, False)
     assert r.pass_names() == ["BloomDownsample - 0+1", "BloomDownsample - 2+3", "BloomUpsample - 3+2",
                               "BloomUpsample - 1+0", "SSAOGeneration", "SSAOBlur", "CloudRendering",
-                              "Composition+GenerateLuminanceHistogram", "LuminanceHistogramFold",
+                              "SkyCompose", "Composition+GenerateLuminanceHistogram", "LuminanceHistogramFold",
                               "ResolveLuminanceHistogram", "TemporalAntiAliasing+ToneMapping"]
     assert r.pass_lane(r.pass_names().index("CloudRendering")) == 1
     f_sky = float((gb["depth"] == 1.0).mean())

@@ -746,3 +746,38 @@ def test_render_graph_sky_split_bit_identical(soc, phases):
         r.close()
     for k in outs[0]:
         assert torch.equal(outs[0][k], outs[1][k]), k
+
+
+@pytest.mark.parametrize("inputs", ["sponza", "terrain"])
+def test_render_graph_static_inputs_bit_identical(soc, inputs):
+    """SOC_RENDERER_STATIC_INPUTS lets the second lane start a frame's CloudRendering before the fork (it has no ring
+    edge onto the main lane), overlapping the previous frame's composition and TAA; SkyCompose still waits for the
+    previous frame's TAA and resolve. Four frames with per-frame globals (camera moving, jitter, time) on one resident
+    G-buffer: the same bits as forking at every frame start, sky-heavy terrain included."""
+    import ctypes as C
+    W, H = 1920, 1080
+    g0, gb = (sponza_inputs if inputs == "sponza" else terrain_inputs)(W, H, elapsed=10.0)
+    outs = []
+    for static in (True, False):
+        fr = soc.alloc_frame(W, H, DEV, bloom_output=True)
+        for k in ("albedo", "emissive", "normal", "velocity", "depth"):
+            fr[k].copy_(torch.from_numpy(gb[k]))
+        fr["shadow"] = dev(gb["shadow"])
+        fr["noise"].copy_(torch.from_numpy(gb["noise"]))
+        r = soc.Renderer(fr, static_inputs=static)
+        cam = soc.make_camera((-14.0, 2.2, 0.3), (0.0, -0.42, 0.0))
+        ji = C.c_uint32(0)
+        g = soc.globals_defaults(W, H)
+        seq = []
+        for f in range(4):
+            soc.frame_update(g, cam, W, H, 0.016, ji)
+            cam.position[0] += 0.05
+            r.execute(g)
+            seq.append({k: fr[k].clone() for k in ("color", "output", "clouds")})
+        torch.cuda.synchronize()
+        seq.append({"auto_exposure": fr["auto_exposure"].clone(), "resolved": r.resolved().clone()})
+        outs.append(seq)
+        r.close()
+    for a, b in zip(*outs):
+        for k in a:
+            assert torch.equal(a[k], b[k]), k

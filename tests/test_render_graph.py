@@ -33,7 +33,7 @@ def test_unfused_graph_is_the_reference_task_list(soc):
 def test_default_graph_order(soc):
     r = _renderer(soc)
     assert r.pass_names() == ["BloomDownsample - 0+1", "BloomDownsample - 2+3", "BloomUpsample - 3+2",
-                              "BloomUpsample - 1+0", "SSAOGeneration", "SSAOBlur", "CloudRendering",
+                              "BloomUpsample - 1+0", "SSAOGeneration", "SSAOBlur", "CloudRendering", "SkyCompose",
                               "Composition+GenerateLuminanceHistogram", "LuminanceHistogramFold",
                               "ResolveLuminanceHistogram", "TemporalAntiAliasing+ToneMapping"]
 
@@ -90,13 +90,15 @@ def test_second_lane_is_derived(soc):
     r = _renderer(soc)
     names = r.pass_names()
     lanes = {n: r.pass_lane(i) for i, n in enumerate(names)}
-    assert [n for n, l in lanes.items() if l == 1] == ["CloudRendering"]
-    # sky split (default): the second lane also writes and bins the colour's sky pixels, so Composition does not
-    # wait for it; the histogram fold (its partial bins) and TAA (the sky pixels) do
-    assert r.pass_uses(names.index("CloudRendering"))[1] == {"CLOUDS", "SKY_COLOR", "SKY_HISTOGRAM_PARTIALS"}
+    assert [n for n, l in lanes.items() if l == 1] == ["CloudRendering", "SkyCompose"]
+    # sky split (default): the second lane also writes and bins the colour's sky pixels (SkyCompose), so Composition
+    # does not wait for it; the histogram fold (its partial bins) and TAA (the sky pixels) do
+    assert r.pass_uses(names.index("CloudRendering"))[1] == {"CLOUDS"}
+    assert r.pass_uses(names.index("SkyCompose")) == ({"CLOUDS", "DEPTH"}, {"SKY_COLOR", "SKY_HISTOGRAM_PARTIALS"})
     assert "CLOUDS" not in r.pass_uses(names.index("Composition+GenerateLuminanceHistogram"))[0]
-    waiters = [n for n, d in _deps(r).items() if "CloudRendering" in d]
+    waiters = [n for n, d in _deps(r).items() if "SkyCompose" in d]
     assert waiters == ["LuminanceHistogramFold", "TemporalAntiAliasing+ToneMapping"]
+    assert [n for n, d in _deps(r).items() if "CloudRendering" in d] == ["SkyCompose"]
     # without the split only the composition waits for it
     r2 = _renderer(soc, sky_split=False)
     waiters = [n for n, d in _deps(r2).items() if "CloudRendering" in d]
@@ -193,8 +195,9 @@ def test_ring_edges(soc):
     r = _renderer(soc)
     c = _carry(r)
     # the second lane's sky writes follow the previous frame's readers of the colour's sky pixels (TAA) and the
-    # resolve that folded and cleared the partial bins; CLOUDS is rewritten by the pass itself
-    assert c["CloudRendering"] == {"CloudRendering", "ResolveLuminanceHistogram", "TemporalAntiAliasing+ToneMapping"}
+    # resolve that folded and cleared the partial bins; CLOUDS is rewritten after the previous frame's SkyCompose read it
+    assert c["SkyCompose"] == {"SkyCompose", "ResolveLuminanceHistogram", "TemporalAntiAliasing+ToneMapping"}
+    assert c["CloudRendering"] == {"CloudRendering", "SkyCompose"}      # no cross-lane ring edge
     # composition's colour write follows the previous frame's TAA read and its own write (same lane); its partials
     # follow the resolve
     assert c["Composition+GenerateLuminanceHistogram"] == {"Composition+GenerateLuminanceHistogram",
@@ -203,8 +206,8 @@ def test_ring_edges(soc):
     assert c["TemporalAntiAliasing+ToneMapping"] == {"TemporalAntiAliasing+ToneMapping"}
     # the bloom writes follow the previous frame's readers of its mips / output (same lane)
     assert "Composition+GenerateLuminanceHistogram" in c["BloomUpsample - 1+0"]
-    assert _cross_lane_ring_edges(r) == {("CloudRendering", "ResolveLuminanceHistogram"),
-                                         ("CloudRendering", "TemporalAntiAliasing+ToneMapping")}
+    assert _cross_lane_ring_edges(r) == {("SkyCompose", "ResolveLuminanceHistogram"),
+                                         ("SkyCompose", "TemporalAntiAliasing+ToneMapping")}
 
 
 def test_ring_edges_raster_head(soc):
@@ -215,9 +218,9 @@ def test_ring_edges_raster_head(soc):
     assert "CloudRendering" in c["GBufferGeneration"]
     assert {"SSAOGeneration", "TemporalAntiAliasing+ToneMapping"} <= c["GBufferGeneration"]
     assert c["DepthPrepass"] == {"DepthPrepass", "GBufferGeneration"}   # WAW / WAR on the visibility buffer
-    assert _cross_lane_ring_edges(r) == {("CloudRendering", "ResolveLuminanceHistogram"),
-                                         ("CloudRendering", "TemporalAntiAliasing+ToneMapping"),
-                                         ("GBufferGeneration", "CloudRendering")}
+    assert _cross_lane_ring_edges(r) == {("SkyCompose", "ResolveLuminanceHistogram"),
+                                         ("SkyCompose", "TemporalAntiAliasing+ToneMapping"),
+                                         ("GBufferGeneration", "CloudRendering"), ("GBufferGeneration", "SkyCompose")}
 
 
 def test_ring_edges_without_sky_split(soc):
@@ -234,7 +237,7 @@ def test_caller_colour_use_includes_sky_pixels(soc):
     names = r.pass_names()
     i = names.index("ColorProbe")
     assert r.pass_uses(i)[0] == {"COLOR", "SKY_COLOR"}
-    assert "CloudRendering" in _deps(r)["ColorProbe"]
+    assert "SkyCompose" in _deps(r)["ColorProbe"]
     r2 = _renderer(soc, sky_split=False)
     r2.add_pass("ColorProbe", lambda *a: 0, reads=["COLOR"], phase=soc.PHASE_POST_EXPOSURE)
     assert r2.pass_uses(r2.pass_names().index("ColorProbe"))[0] == {"COLOR"}
