@@ -390,7 +390,9 @@ typedef struct soc_renderer soc_renderer;
 /* The caller does not rewrite the frame's input images (G-buffer, shadow map, noise) between frames, e.g. a resident
  * G-buffer, or one produced in the graph by the raster head. Second-lane passes whose only cross-frame dependencies are
  * on the second lane (CloudRendering: it writes only CLOUDS) may then start before the fork, i.e. before the caller's
- * stream reaches this frame: the clouds of frame N+1 overlap the composition / TAA of frame N. Same results. */
+ * stream reaches this frame: the clouds of frame N+1 overlap the composition / TAA of frame N. Same results. The
+ * second lane's intermediate CLOUDS image may then already hold the next frame's clouds when work the caller queued
+ * between two calls reads it: a caller that reads CLOUDS between frames leaves the flag off. */
 #define SOC_RENDERER_STATIC_INPUTS 256
 
 soc_renderer* soc_renderer_create(const soc_frame_images* images, uint32_t flags);
