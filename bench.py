@@ -53,6 +53,7 @@ import torch.distributed as dist  # noqa: E402
 
 import soc_real_time_renderer_amd as soc  # noqa: E402
 from soc_real_time_renderer_amd import multi_gpu, raster, scene  # noqa: E402
+from soc_real_time_renderer_amd.scene import sponza_mesh  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 SSAO_KERNEL = "ssao_lds_kernel<true, true, true, 64, 16, 32, 2>"   # the default SSAOGeneration kernel (ssao.hip)
@@ -206,7 +207,11 @@ def build_inputs(config, scene_name, W, H, rank, device, mips=True):
     sc = None
     if scene_id == scene.SPONZA_MESH:
         # rasterised once by the HIP rasteriser (DepthPrepass + GBufferGeneration + SunShadowDraw), not timed
-        sc = raster.scene_setup(g, scene_id, tex_size=256, device=device, mips=mips)
+        # the reference's Sponza images at their own resolution (1024^2) when build() copied them, else the
+        # committed 256^2 fixture
+        native = sponza_mesh.native_available()
+        sc = raster.scene_setup(g, scene_id, tex_size=None if native else 256, device=device, mips=mips, native=native)
+        sc["texture_set"] = "native 1024^2" if native else "256^2 fixture"
         gbd = raster.render_gbuffer(g, sc, W, H, 4096, device)
         torch.cuda.synchronize()
         gb = {k: gbd[k].cpu().numpy() for k in ("albedo", "emissive", "normal", "velocity", "depth")}
@@ -388,7 +393,7 @@ def main():
         "vs_baseline": None,
         "dtype": "f32 (fp16/unorm8/d32 storage)",
         "data": (f"synthetic: fBm terrain (seed 0x7E44) G-buffer + 4096^2 sun shadow map (scene_synth.c)" if terrain else
-                 f"synthetic: Sponza-proxy {'box atrium (scene_synth.c)' if sc is None else 'mesh (procedural atrium, ' + str(int(sc['mesh'].struct.triangle_count)) + ' triangles, the reference Sponza baseColor/normal textures at 256^2' + ('' if args.no_mips else ' with mip chains + 16x anisotropic sampling') + ', seed 0x5050)'}; "
+                 f"synthetic: Sponza-proxy {'box atrium (scene_synth.c)' if sc is None else 'mesh (procedural atrium, ' + str(int(sc['mesh'].struct.triangle_count)) + ' triangles, the reference Sponza baseColor/normal textures (' + sc['texture_set'] + ')' + ('' if args.no_mips else ' with mip chains + 16x anisotropic sampling') + ', seed 0x5050)'}; "
                  f"G-buffer + 4096^2 sun shadow map {'ray-cast on the host' if sc is None else 'rasterised once by the HIP rasteriser'}"),
         "config": {"workload": f"{'Terrain' if terrain else 'Sponza-proxy'} {W}x{H} full screen-space chain "
                                f"({args.config.upper()}): bloom x8, SSAO+blur, clouds, composition"

@@ -201,14 +201,16 @@ def visibility_triangles(vis) -> np.ndarray:
     return np.where(low == 0xFFFFFFFF, -1, 0xFFFFFFFE - low)
 
 
-def sponza_mesh_materials(tex_size: Optional[int] = None, device=None, mips: bool = False, host_mip_generator=None):
-    """The 25 Sponza materials of the mesh proxy: baseColor (sRGB) and normal (UNORM) textures from the fixture;
+def sponza_mesh_materials(tex_size: Optional[int] = None, device=None, mips: bool = False, host_mip_generator=None,
+                          native: bool = False):
+    """The 25 Sponza materials of the mesh proxy: baseColor (sRGB) and normal (UNORM) textures from the 256^2 fixture
+    or (native=True) the reference's images at their own resolution, box-downsampled to tex_size when larger;
     no emissive image (Sponza has none); albedo factor 1 (GBufferGeneration ignores baseColorFactor,
     g_buffer_generation.inl:189-194). mips=True gives every texture its mip chain (the reference's upload,
     texture.cpp:184-246) and the anisotropic sampler: built on `device` by soc_generate_mips, or for host
     materials (device None) by `host_mip_generator(MipTexture)`. Returns (materials, textures kept alive)."""
     from .scene import sponza_mesh
-    tex = sponza_mesh.load_textures(tex_size)
+    tex = sponza_mesh.load_textures(tex_size, native=native)
     keep, mats = [], []
 
     def prep(a, srgb):
@@ -235,17 +237,19 @@ def sponza_mesh_materials(tex_size: Optional[int] = None, device=None, mips: boo
     return mats, keep
 
 
-def scene_setup(g, scene_id: int, tex_size: int = 512, device="cuda", mips: bool = True) -> dict:
+def scene_setup(g, scene_id: int, tex_size: Optional[int] = 512, device="cuda", mips: bool = True,
+                native: bool = False) -> dict:
     """Device mesh, textures and material array of a synthetic scene: the Sponza-proxy mesh (sponza_mesh.py, the
     reference's Sponza textures), the box atrium (scene_synth.c: sRGB tiled textures, emissive lamps) or the terrain
-    (the GPU-tessellated patch grid over a tex_size^2 heightmap, UNORM albedo, velocity 0 as draw_terrain.inl:221)."""
+    (the GPU-tessellated patch grid over a tex_size^2 heightmap, UNORM albedo, velocity 0 as draw_terrain.inl:221).
+    native=True: the mesh proxy samples the native-resolution Sponza images (sponza_mesh.NATIVE)."""
     from . import scene as _scene
     if scene_id == _scene.SPONZA_MESH:
         from .scene import sponza_mesh
         m = sponza_mesh.build()
         mesh = MeshBuffers.from_numpy(m["positions"], m["normals"], m["uvs"], m["indices"], m["materials"],
                                       device=device)
-        mats, keep = sponza_mesh_materials(tex_size, device, mips=mips)
+        mats, keep = sponza_mesh_materials(tex_size, device, mips=mips, native=native)
         return {"mesh": mesh, "textures": keep, "normal_map": None, "materials": materials_device(mats, device),
                 "material_count": len(mats), "host_mesh": m, "workspace": mesh.workspace(device)}
     tex, em = _scene.material_textures(g, tex_size, scene_id)

@@ -10,9 +10,10 @@ triangle count from the glTF (the budgets below sum to 262,267). Shapes are para
 column shafts, arch bands, displaced cloth, lathed vases, leaf cards, tiled panels) wound counter-clockwise
 seen from outside, like glTF, with planar / cylindrical uvs in world metres.
 
-Deterministic (seed 0x5050). No file of the reference is read at run time: the textures come from
-soc_real_time_renderer_amd/data/sponza/ (tools/make_sponza_fixture.py decodes the JPEGs once, in the container
-that has the reference).
+Deterministic (seed 0x5050). No file of the reference is read at run time: the textures come from the committed
+256^2 fixture soc_real_time_renderer_amd/data/sponza/ or from the native-resolution set data/sponza_native/ (the
+reference's 1024^2 image files, copied by __graft_entry__.build() in the container that has the reference; git-ignored,
+shipped to the GPU box with the built libraries); tools/make_sponza_fixture.py makes both.
 """
 from __future__ import annotations
 
@@ -24,6 +25,7 @@ from typing import Dict, List, Optional
 import numpy as np
 
 DATA = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data", "sponza")
+NATIVE = os.path.join(os.path.dirname(DATA), "sponza_native")
 SEED = 0x5050
 
 # Sponza.gltf: triangles per material (sum over its primitives of indices.count / 3)
@@ -261,21 +263,39 @@ def build(seed: int = SEED) -> Dict:
     return {"positions": P, "normals": N, "uvs": UV, "indices": I, "materials": M, "vertex_count": len(P)}
 
 
-def texture_index() -> dict:
-    """{material: {"albedo": file, "normal": file}} of the committed 256^2 texture fixture."""
-    with open(os.path.join(DATA, "materials.json")) as fh:
+def texture_index(native: bool = False) -> dict:
+    """{material: {"albedo": file, "normal": file}} of the committed 256^2 texture fixture, or of the native-resolution
+    set (NATIVE: the reference's own image files, copied by __graft_entry__.build(); not in the history)."""
+    root = NATIVE if native else DATA
+    path = os.path.join(root, "materials.json")
+    if native and not os.path.exists(path):
+        raise FileNotFoundError(f"{path}: the native-resolution Sponza textures are made by __graft_entry__.build() "
+                                "in a container that has the reference (tools/make_sponza_fixture.py --native)")
+    with open(path) as fh:
         return {int(k): v for k, v in json.load(fh).items()}
 
 
-def load_textures(size: Optional[int] = None) -> Dict[int, dict]:
-    """{material: {"albedo": RGBA8 array or None, "normal": RGBA8 array or None}} from the fixture."""
+def native_available() -> bool:
+    """True when the native-resolution texture set is complete (its materials.json is written last)."""
+    try:
+        idx = texture_index(native=True)
+    except FileNotFoundError:
+        return False
+    return all(os.path.exists(os.path.join(NATIVE, f)) for e in idx.values() for f in e.values())
+
+
+def load_textures(size: Optional[int] = None, native: bool = False) -> Dict[int, dict]:
+    """{material: {"albedo": RGBA8 array or None, "normal": RGBA8 array or None}} from the fixture (native=False) or
+    the native-resolution set; `size` box-downsamples larger images (None: as stored). Alpha is forced to 255 for
+    every image (the G-buffer pass reads colour only, g_buffer_generation.inl:189-194)."""
     from PIL import Image
+    root = NATIVE if native else DATA
     out = {}
-    for mid, t in texture_index().items():
+    for mid, t in texture_index(native).items():
         e = {}
         for k in ("albedo", "normal"):
             if t.get(k):
-                im = Image.open(os.path.join(DATA, t[k])).convert("RGBA")
+                im = Image.open(os.path.join(root, t[k])).convert("RGB").convert("RGBA")
                 if size and im.size[0] > size:
                     im = im.resize((size, size), Image.BOX)
                 e[k] = np.ascontiguousarray(np.asarray(im, np.uint8))

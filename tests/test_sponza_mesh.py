@@ -57,6 +57,29 @@ def test_texture_fixture():
                     t["normal"].shape[0] > 8]) > 180
 
 
+def test_native_texture_set(monkeypatch, tmp_path):
+    """The native-resolution set: the same 49 images as the fixture at the reference's own sizes
+    (1024^2; material 2's albedo is 4^2), alpha forced to 255, and a loud error where build() could not make it."""
+    if not sm.native_available():
+        import pytest
+        pytest.skip("native texture set not built here (needs the reference mount at build time)")
+    idx, fix = sm.texture_index(native=True), sm.texture_index()
+    assert {m: sorted(v) for m, v in idx.items()} == {m: sorted(v) for m, v in fix.items()}
+    tex = sm.load_textures(native=True)
+    sizes = sorted(a.shape[0] for t in tex.values() for a in t.values() if a is not None)
+    assert sizes == [4] + [1024] * 48
+    assert all((a[..., 3] == 255).all() for t in tex.values() for a in t.values() if a is not None)
+    # box-downsampled on request, like the fixture
+    assert sm.load_textures(256, native=True)[0]["albedo"].shape == (256, 256, 4)
+    monkeypatch.setattr(sm, "NATIVE", str(tmp_path))
+    assert not sm.native_available()
+    try:
+        sm.load_textures(native=True)
+        raise AssertionError("missing native set must raise")
+    except FileNotFoundError as e:
+        assert "build()" in str(e)
+
+
 def test_c3_view_sky_fraction(oracle):
     """At the C3 camera (multi_gpu.SPONZA_CAMERA) about a tenth of the frame is sky through the open court."""
     from helpers import sponza_mesh_inputs
