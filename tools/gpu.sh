@@ -5,8 +5,9 @@
 #   tools/gpu.sh suite                          full -m gpu suite, smoke(), the default bench line
 #   tools/gpu.sh tests "<pytest -k expr>"       selected GPU tests
 #   tools/gpu.sh bench NAME [bench args]        one bench line -> gpurun_out/NAME.json (fps, ms/step, roofline frac)
-#   tools/gpu.sh ab "K=V,K2=V2" "" ... -- [bench args]
-#                                               the bench line under environment variants ("" = none)
+#   tools/gpu.sh ab "K=V,K2=V2" "" "--flag,K=V" ... -- [bench args]
+#                                               the bench line under variants: K=V items are environment
+#                                               variables, "-..." items extra bench arguments ("" = none)
 #   tools/gpu.sh kt TAG [bench args]            rocprofv3 --kernel-trace --stats of a short bench run (top kernels)
 #   tools/gpu.sh pmc TAG "<counters>" ... [-- bench args]
 #                                               one rocprofv3 --pmc pass per counter group (kernel trace only) + summary
@@ -72,7 +73,10 @@ case $cmd in
     for v in "${vars[@]}"; do
       i=$((i+1))
       echo "[$v]"
-      ( [ -n "$v" ] && export ${v//,/ }; bench_line ab_$i --steps 40 --warmup 10 --no-cpu-baseline "$@" ) || exit 1
+      # a variant is comma-separated: K=V items are exported, items starting with "-" are extra bench arguments
+      ( extra=(); IFS=, read -ra items <<< "$v"
+        for it in "${items[@]}"; do case $it in -*) extra+=("$it") ;; ?*) export "$it" ;; esac; done
+        bench_line ab_$i --steps 40 --warmup 10 --no-cpu-baseline "${extra[@]}" "$@" ) || exit 1
     done ;;
   kt)
     t=${1:?tag}; shift; kernel_trace "$t" "$@" ;;
