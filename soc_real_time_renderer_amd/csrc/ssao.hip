@@ -22,6 +22,11 @@ struct SsaoParams {
     int noise_w;   // textureSize(u_normal_image).x
     int swz;       // XCD-aware tile order (tuning knob SOC_SWZ_SSAO, see xcd_order; 0 = row-major)
     float rw, rh;  // recip_rn(target extent) for the pixel-centre uv (div_rn)
+    // host-folded constants of the tap loop (make_params): the projection rows x, y, w scaled to texel space
+    // (x 256 sub-texel steps on the sparse path), the texel-space centre and clamp bounds, 1 / kernel_size
+    float pa[3][4];
+    float c0x, c0y, tmx, tmy;
+    float inv_ksize;
 };
 
 // ssao_generation.inl:139-141 (no FMA contraction: keeps the sin argument as the oracle's)
@@ -134,37 +139,49 @@ __device__ __forceinline__ void ssao_pixel(int x, int y, const DImg& depth, cons
         row_ptr_w<uint8_t>(target, y)[x] = 255;
         return;
     }
-    // frag_position = get_view_position_from_depth(in_uv, depth), :177
+    // frag_position = get_view_position_from_depth(in_uv, depth), :177: inv_proj (ndc, depth, 1) as fma chains, then
+    // one reciprocal of w for the three divisions (the setup is a quarter of the pass's instructions; within the
+    // SSAO tolerance of DESIGN.md §5)
     const float d = depth_tap(depth, u, v);
-    f4 vp = mul(p.inv_proj, f4{u * 2.0f - 1.0f, v * 2.0f - 1.0f, d, 1.0f});
-    const f3 frag = f3{vp.x / vp.w, vp.y / vp.w, vp.z / vp.w};
-    const f3 n = mul3of4(p.view, normalize3(f3{nn.x, nn.y, nn.z}));
+    const float* IP = p.inv_proj.m;
+    const float ex = u * 2.0f - 1.0f, ey = v * 2.0f - 1.0f;
+    auto ip_row = [&](int r) {
+        return __builtin_fmaf(IP[8 + r], d, __builtin_fmaf(IP[4 + r], ey, __builtin_fmaf(IP[r], ex, IP[12 + r])));
+    };
+    const float iw = fast_rcp(ip_row(3));
+    const f3 frag = f3{ip_row(0) * iw, ip_row(1) * iw, ip_row(2) * iw};
+    // normal = mat3(view) * normalize(n): v_rsq instead of sqrt + three divisions (the zero normal left above)
+    const float* V = p.view.m;
+    const float nk = __builtin_amdgcn_rsqf(__builtin_fmaf(nn.z, nn.z, __builtin_fmaf(nn.y, nn.y, nn.x * nn.x)));
+    const f3 nu = f3{nn.x * nk, nn.y * nk, nn.z * nk};
+    const f3 n = f3{__builtin_fmaf(V[8], nu.z, __builtin_fmaf(V[4], nu.y, V[0] * nu.x)),
+                    __builtin_fmaf(V[9], nu.z, __builtin_fmaf(V[5], nu.y, V[1] * nu.x)),
+                    __builtin_fmaf(V[10], nu.z, __builtin_fmaf(V[6], nu.y, V[2] * nu.x))};
 
     float2 rv2 = TABLE ? table[(size_t)y * target.w + x] : ssao_random_vec(u, v, p.noise_w);
-    const f3 rv = f3{rv2.x, rv2.y, 0.0f};
-    const f3 t = normalize3(rv - n * dot3(rv, n));
+    // tangent = normalize(rv - n dot(rv, n)) with rv.z = 0 (a zero vector gives NaN, as normalize does)
+    const float rn = __builtin_fmaf(rv2.y, n.y, rv2.x * n.x);
+    const f3 tu = f3{__builtin_fmaf(-n.x, rn, rv2.x), __builtin_fmaf(-n.y, rn, rv2.y), -n.z * rn};
+    const float tk = __builtin_amdgcn_rsqf(__builtin_fmaf(tu.z, tu.z, __builtin_fmaf(tu.y, tu.y, tu.x * tu.x)));
+    const f3 t = f3{tu.x * tk, tu.y * tk, tu.z * tk};
     const f3 b = cross3(t, n);
 
-    const float* P = p.proj.m;
     const float* ip = p.inv_proj.m;
-    const int W = depth.w, H = depth.h;
     const float r = p.radius;
     const f3 tr = t * r, br = b * r, nr = n * r;
-    // s(k) = frag + tr kx + br ky + nr kz;  x' = P0 sx + P4 sy + P8 sz + P12, etc.
-    auto proj_aff = [&](int row, float scale) {
-        const float m0 = P[row] * scale, m1 = P[4 + row] * scale, m2 = P[8 + row] * scale, m3 = P[12 + row] * scale;
-        return Aff{m0 * frag.x + m1 * frag.y + m2 * frag.z + m3, m0 * tr.x + m1 * tr.y + m2 * tr.z,
-                   m0 * br.x + m1 * br.y + m2 * br.z, m0 * nr.x + m1 * nr.y + m2 * nr.z};
+    // s(k) = frag + tr kx + br ky + nr kz;  x' = P0 sx + P4 sy + P8 sz + P12, etc. (rows pre-scaled on the host:
+    // SPARSE_IP's x / y forms carry the sub-texel scale 256 and the +0.5 of the rounding, so a tap's fixed-point
+    // coordinate is one fma + clamp)
+    auto proj_aff = [&](const float* m) {
+        return Aff{__builtin_fmaf(m[2], frag.z, __builtin_fmaf(m[1], frag.y, __builtin_fmaf(m[0], frag.x, m[3]))),
+                   __builtin_fmaf(m[2], tr.z, __builtin_fmaf(m[1], tr.y, m[0] * tr.x)),
+                   __builtin_fmaf(m[2], br.z, __builtin_fmaf(m[1], br.y, m[0] * br.x)),
+                   __builtin_fmaf(m[2], nr.z, __builtin_fmaf(m[1], nr.y, m[0] * nr.x))};
     };
-    // SPARSE_IP: the x / y forms carry the sub-texel scale 256 (exact: a power of two) and the +0.5 of the rounding,
-    // so a tap's fixed-point coordinate is one fma + clamp (the texel coordinate itself is not needed)
-    const float fxs = SPARSE_IP ? 256.0f : 1.0f;
-    const Aff ax = proj_aff(0, 0.5f * (float)W * fxs), ay = proj_aff(1, 0.5f * (float)H * fxs), aw = proj_aff(3, 1.0f);
+    const Aff ax = proj_aff(p.pa[0]), ay = proj_aff(p.pa[1]), aw = proj_aff(p.pa[2]);
     const Aff az = Aff{frag.z + p.bias, tr.z, br.z, nr.z};     // s.z + bias
-    const float cx0 = 0.5f * (float)(W - 1), cy0 = 0.5f * (float)(H - 1);
-    const float tmax_x = (float)(W - 1) - 1.0f / 256.0f, tmax_y = (float)(H - 1) - 1.0f / 256.0f;
-    const float cx0s = cx0 * 256.0f + 0.5f, cy0s = cy0 * 256.0f + 0.5f;
-    const float fmax_x = tmax_x * 256.0f + 0.5f, fmax_y = tmax_y * 256.0f + 0.5f;
+    const int W = depth.w, H = depth.h;
+    const float cx0 = p.c0x, cy0 = p.c0y, tmax_x = p.tmx, tmax_y = p.tmy;   // texel (or sub-texel) space
     float occ = 0.0f;
 #pragma unroll UNROLL
     for (int i = 0; i < SOC_SSAO_MAX_KERNEL; ++i) {
@@ -174,8 +191,8 @@ __device__ __forceinline__ void ssao_pixel(int x, int y, const DImg& depth, cons
             float tx = 0.0f, ty = 0.0f;
             int fx, fy;
             if (SPARSE_IP) {   // 256 t + 0.5 directly, clamped to [0.5, 256 tmax + 0.5]; >= 0, so truncation floors
-                fx = (int)__builtin_amdgcn_fmed3f(__builtin_fmaf(aff(ax, kx, ky, kz), rw, cx0s), 0.5f, fmax_x);
-                fy = (int)__builtin_amdgcn_fmed3f(__builtin_fmaf(aff(ay, kx, ky, kz), rw, cy0s), 0.5f, fmax_y);
+                fx = (int)__builtin_amdgcn_fmed3f(__builtin_fmaf(aff(ax, kx, ky, kz), rw, cx0), 0.5f, tmax_x);
+                fy = (int)__builtin_amdgcn_fmed3f(__builtin_fmaf(aff(ay, kx, ky, kz), rw, cy0), 0.5f, tmax_y);
             } else {
                 tx = __builtin_fmaf(aff(ax, kx, ky, kz), rw, cx0);
                 ty = __builtin_fmaf(aff(ay, kx, ky, kz), rw, cy0);
@@ -215,7 +232,7 @@ __device__ __forceinline__ void ssao_pixel(int x, int y, const DImg& depth, cons
             }
         }
     }
-    occ = 1.0f - (occ / p.kernel_size_f);
+    occ = 1.0f - occ * p.inv_ksize;
     row_ptr_w<uint8_t>(target, y)[x] = (uint8_t)to_unorm8(occ);
 }
 
@@ -325,7 +342,24 @@ SsaoParams make_params(const soc_globals* g, const soc_img& normal) {
     p.ksize = g->ssao_kernel_size < SOC_SSAO_MAX_KERNEL ? g->ssao_kernel_size : SOC_SSAO_MAX_KERNEL;
     p.noise_w = normal.width;
     p.swz = tuning_knob("SOC_SWZ_SSAO", -16);   // XCD vertical bands: HBM traffic 3.3x -> 1.25x algorithmic
+    p.inv_ksize = 1.0f / p.kernel_size_f;
     return p;
+}
+
+// The tap loop's uniform constants for a depth image of W x H (sip: the sparse-inverse-projection path, whose x / y
+// forms count 1/256-texel steps with the rounding's +0.5 folded into the centre).
+void fold_tap_constants(SsaoParams& p, int W, int H, bool sip) {
+    const float fxs = sip ? 256.0f : 1.0f;
+    const float scale[3] = {0.5f * (float)W * fxs, 0.5f * (float)H * fxs, 1.0f};
+    const int rows[3] = {0, 1, 3};
+    for (int k = 0; k < 3; ++k)
+        for (int j = 0; j < 4; ++j) p.pa[k][j] = p.proj.m[4 * j + rows[k]] * scale[k];
+    const float cx0 = 0.5f * (float)(W - 1), cy0 = 0.5f * (float)(H - 1);
+    const float tmax_x = (float)(W - 1) - 1.0f / 256.0f, tmax_y = (float)(H - 1) - 1.0f / 256.0f;
+    p.c0x = sip ? cx0 * 256.0f + 0.5f : cx0;
+    p.c0y = sip ? cy0 * 256.0f + 0.5f : cy0;
+    p.tmx = sip ? tmax_x * 256.0f + 0.5f : tmax_x;
+    p.tmy = sip ? tmax_y * 256.0f + 0.5f : tmax_y;
 }
 
 }  // namespace
@@ -361,6 +395,7 @@ extern "C" int soc_ssao_generation(const soc_globals* g, soc_img depth, soc_img 
     // sparse inverse projection (the reference's perspective) whose w row stays positive over depths [-1, 1]
     const bool sip = IP[2] == 0.0f && IP[3] == 0.0f && IP[6] == 0.0f && IP[7] == 0.0f && IP[15] - IP[11] > 0.0f &&
                      IP[15] + IP[11] > 0.0f;
+    fold_tap_constants(p, depth.width, depth.height, sip);
     const dim3 blk(256), grd(ceil_div(target.width, 32), ceil_div(target.height, 8));
     const float2* tb = reinterpret_cast<const float2*>(noise_table);
     hipStream_t st = hs(stream);
