@@ -417,6 +417,10 @@ int soc_renderer_reset_timing(soc_renderer* r);
 int soc_renderer_pass_stats(soc_renderer* r, int32_t index, float* total_ms, int32_t* frames);
 /* Index (0/1) of the history_color slot holding this frame's TAA result (= tone-map input). */
 int32_t soc_renderer_current_history(const soc_renderer* r);
+/* Restore that index when resuming from a checkpoint of the temporal state (SURVEY.md §5 "Checkpoint / resume"; the
+ * reference keeps it only in its TAA history images and AutoExposure, renderer.cpp:1170-1198): the caller writes back
+ * history_color[index] / history_velocity[index] and the AutoExposure block, then sets the index. 0 or 1. */
+int soc_renderer_set_current_history(soc_renderer* r, int32_t index);
 /* Sky lane on/off (default on unless SOC_RENDERER_SERIAL). On: CloudRendering runs on a renderer-owned
  * stream of the current device, forked from `stream` at the start of the PRE phase and joined before
  * Composition, so it overlaps bloom and SSAO. Results are identical either way. */

@@ -515,6 +515,44 @@ class Renderer:
     def resolved(self) -> torch.Tensor:
         return self.frame["history_color"][self.current_history()]
 
+    STATE_VERSION = 1
+
+    def save_state(self, path: Optional[str] = None) -> dict:
+        """Checkpoint of the frame's temporal state (SURVEY.md §5 "Checkpoint / resume"; the reference keeps it in its TAA
+        history images and AutoExposure, renderer.cpp:1170-1198): the previous frame's resolved colour and velocity,
+        the AutoExposure block (exposure + bins) and the history slot index. Synchronises the device. With `path`,
+        also written with numpy.savez (plain arrays, loadable without pickle)."""
+        torch.cuda.synchronize()
+        h = self.current_history()
+        st = {"version": np.int32(self.STATE_VERSION), "history_index": np.int32(h),
+              "history_color": self.frame["history_color"][h].cpu().numpy(),
+              "history_velocity": self.frame["history_velocity"][h].cpu().numpy(),
+              "auto_exposure": self.frame["auto_exposure"].cpu().numpy()}
+        if path:
+            np.savez(path, **st)
+        return st
+
+    def load_state(self, state) -> None:
+        """Resume from save_state()'s dict or file: writes the history images and the AutoExposure block back into this
+        renderer's frame and restores the history slot (soc_renderer_set_current_history). The frame's extents and
+        formats must match the checkpoint's."""
+        st = dict(np.load(state, allow_pickle=False)) if isinstance(state, (str, os.PathLike)) else state
+        if int(st["version"]) != self.STATE_VERSION:
+            raise ValueError(f"load_state: checkpoint version {int(st['version'])}, expected {self.STATE_VERSION}")
+        h = int(st["history_index"])
+        for key in ("history_color", "history_velocity"):
+            dst = self.frame[key][h]
+            src = np.asarray(st[key])
+            if tuple(src.shape) != tuple(dst.shape) or src.dtype != np.float16:
+                raise ValueError(f"load_state: {key} {src.shape} {src.dtype} does not match the frame's {tuple(dst.shape)}")
+            dst.copy_(torch.from_numpy(np.ascontiguousarray(src)))
+        ae = np.asarray(st["auto_exposure"])
+        if ae.shape != tuple(self.frame["auto_exposure"].shape):
+            raise ValueError("load_state: AutoExposure block size differs")
+        self.frame["auto_exposure"].copy_(torch.from_numpy(np.ascontiguousarray(ae)))
+        _check(lib().soc_renderer_set_current_history(self.handle, h), "soc_renderer_set_current_history")
+        torch.cuda.synchronize()
+
     def close(self):
         if getattr(self, "handle", None):
             lib().soc_renderer_destroy(self.handle)

@@ -224,6 +224,7 @@ FUNCTIONS = {
     "soc_renderer_pass_group": (C.c_char_p, [_P, C.c_int32]),
     "soc_renderer_pass_ms": (C.c_float, [_P, C.c_int32]),
     "soc_renderer_current_history": (C.c_int32, [_P]),
+    "soc_renderer_set_current_history": (C.c_int, [_P, C.c_int32]),
     "soc_renderer_set_async": (C.c_int, [_P, C.c_int32]),
     "soc_scene_update": (_I, [C.POINTER(Globals), C.POINTER(Entity), C.c_int32, C.POINTER(C.c_float),
                               C.POINTER(C.c_float)]),

@@ -1463,3 +1463,13 @@ extern "C" int soc_renderer_pass_stats(soc_renderer* r, int32_t i, float* total_
 }
 
 extern "C" int32_t soc_renderer_current_history(const soc_renderer* r) { return r ? r->hist : -1; }
+
+// Resume from a checkpoint (SURVEY.md §5 "Checkpoint / resume"): the slot whose history_color / history_velocity hold
+// the previous frame's TAA result and velocity. The images and the AutoExposure block are caller-owned and restored by
+// the caller; this is the renderer's one piece of temporal state.
+extern "C" int soc_renderer_set_current_history(soc_renderer* r, int32_t index) {
+    if (!r) return set_error(SOC_E_INVALID_ARG, "soc_renderer_set_current_history: null renderer");
+    if (index != 0 && index != 1) return set_error(SOC_E_INVALID_ARG, "soc_renderer_set_current_history: index %d", index);
+    r->hist = index;
+    return SOC_OK;
+}

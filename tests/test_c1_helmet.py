@@ -24,9 +24,29 @@ CAMERA = ((0.0, 0.0, 2.5), (-math.pi / 2, 0.0, 0.0))   # forw
 SHADOW = 2048
 
 
-def helmet():
+NATIVE = os.path.join(FIX, "native")   # the 2048^2 JPEGs, copied by __graft_entry__.build() (not in the history)
+IMAGES = ("Default_albedo.jpg", "Default_emissive.jpg", "Default_normal.jpg")
+
+
+def native_available():
+    return all(os.path.exists(os.path.join(NATIVE, n)) for n in IMAGES)
+
+
+def helmet(native=False):
+    if native:
+        return gltf.load(os.path.join(FIX, "DamagedHelmet.gltf"),
+                         images={n: gltf.load_image(os.path.join(NATIVE, n)) for n in IMAGES})
     tx = np.load(os.path.join(FIX, "textures_256.npz"))
     return gltf.load(os.path.join(FIX, "DamagedHelmet.gltf"), images={k: tx[k] for k in tx.files})
+
+
+def test_native_images():
+    """The reference's own 2048^2 images (texture.cpp:422 loads them at full size), when build() could copy them."""
+    if not native_available():
+        pytest.skip("native helmet images not built here")
+    mat = helmet(native=True)["material_list"][0]
+    for k in ("albedo", "emissive", "normal"):
+        assert mat[k].shape == (2048, 2048, 4), k
 
 
 def c1_globals():
@@ -95,10 +115,14 @@ def test_c1_cpu_frame(oracle):
 
 
 @pytest.mark.gpu
-def test_c1_gpu_matches_cpu(soc, oracle):
+@pytest.mark.parametrize("textures", ["256", "native"])
+def test_c1_gpu_matches_cpu(soc, oracle, textures):
+    """textures="native": the reference's 2048^2 images (VERDICT r2 #9) instead of the 256^2 fixture."""
     import torch
+    if textures == "native" and not native_available():
+        pytest.skip("native helmet images not shipped")
     g = c1_globals()
-    m = helmet()
+    m = helmet(native=textures == "native")
     vis_ref, shadow_ref, gb_ref, color_ref = oracle_frame(oracle, g, m)
     dev = "cuda"
     mb = raster.MeshBuffers.from_numpy(m["positions"], m["normals"], m["uvs"], m["indices"], m["materials"])
