@@ -12,7 +12,7 @@
 #   tools/gpu.sh pmc TAG "<counters>" ... [-- bench args]
 #                                               one rocprofv3 --pmc pass per counter group (kernel trace only) + summary
 #   tools/gpu.sh traffic TAG [bench args]       FETCH_SIZE / WRITE_SIZE passes -> per-kernel HBM traffic table
-#   tools/gpu.sh round TAG                      the round-end measurement set (bench lines C3/C2/C3b/C4/raster, frame PNG,
+#   tools/gpu.sh round TAG                      the round-end measurement set (bench lines C3/C2/C3b/C4/raster C2/C3/C4, frame PNG,
 #                                               kernel trace + traffic of the default command)
 set -o pipefail
 export TMPDIR=/tmp
@@ -92,6 +92,7 @@ case $cmd in
     bench_line ${t}_bench_c2 --config c2 --no-cpu-baseline
     bench_line ${t}_bench_c3b --config c3b --no-cpu-baseline
     bench_line ${t}_bench_c4 --config c4 --no-cpu-baseline
+    bench_line ${t}_bench_raster_c2 --config c2 --raster --no-cpu-baseline
     bench_line ${t}_bench_raster_c3 --raster --no-cpu-baseline
     bench_line ${t}_bench_raster_c4 --config c4 --raster --no-cpu-baseline
     bench_line ${t}_frame_c3_960 --raster --no-cpu-baseline --width 960 --height 540 --steps 5 --warmup 2 --write-frame gpurun_out/${t}_frame_raster_c3_960x540.png
