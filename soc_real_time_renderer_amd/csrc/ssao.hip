@@ -27,6 +27,7 @@ struct SsaoParams {
     float pa[3][4];
     float c0x, c0y, tmx, tmy;
     float inv_ksize;
+    float inv_radius;   // 1 / radius (the sparse path requires radius > 0)
 };
 
 // ssao_generation.inl:139-141 (no FMA contraction: keeps the sin argument as the oracle's)
@@ -180,6 +181,12 @@ __device__ __forceinline__ void ssao_pixel(int x, int y, const DImg& depth, cons
     };
     const Aff ax = proj_aff(p.pa[0]), ay = proj_aff(p.pa[1]), aw = proj_aff(p.pa[2]);
     const Aff az = Aff{frag.z + p.bias, tr.z, br.z, nr.z};     // s.z + bias
+    // SPARSE_IP range test in units of the radius (r > 0, host-checked): with vw = ip11 d + ip15, vz = ip10 d + ip14,
+    // D1 = frag.z vw - vz = d A + B and D2 = s.z vw - vz = D1 + (s.z - frag.z) vw; r vw / |D1| = vw / |D1 / r| and
+    // sign(D2) = sign(D2 / r), so the tap needs vw, D1 / r (one fma each) and the per-pixel form (s.z - frag.z) / r
+    const float ir = p.inv_radius;
+    const float A1 = (frag.z * ip[11] - ip[10]) * ir, B1 = (frag.z * ip[15] - ip[14]) * ir;
+    const Aff dzr = Aff{p.bias * ir, t.z, b.z, n.z};
     const int W = depth.w, H = depth.h;
     const float cx0 = p.c0x, cy0 = p.c0y, tmax_x = p.tmx, tmax_y = p.tmy;   // texel (or sub-texel) space
     float occ = 0.0f;
@@ -208,9 +215,8 @@ __device__ __forceinline__ void ssao_pixel(int x, int y, const DImg& depth, cons
             const float top = __builtin_fmaf(wx, t1 - t0, t0);
             const float bot = __builtin_fmaf(wx, b1 - b0, b0);
             const float dd = __builtin_fmaf(wy, bot - top, top);
-            float vz, vw;   // get_view_position_from_depth(offset.xy, depth).z
+            float vz = 0.0f, vw;   // get_view_position_from_depth(offset.xy, depth).z
             if (SPARSE_IP) {
-                vz = __builtin_fmaf(ip[10], dd, ip[14]);
                 vw = __builtin_fmaf(ip[11], dd, ip[15]);
             } else {
                 const float ex = (tx + 0.5f) * (2.0f / (float)W) - 1.0f, ey = (ty + 0.5f) * (2.0f / (float)H) - 1.0f;
@@ -220,10 +226,11 @@ __device__ __forceinline__ void ssao_pixel(int x, int y, const DImg& depth, cons
             if (SPARSE_IP) {
                 // vw > 0 for every stored depth (the host selects this path only then), so with sd = vz / vw:
                 // r / |frag.z - sd| = r vw / |frag.z vw - vz| and sd >= s.z  <=>  s.z vw - vz <= 0 (one
-                // reciprocal per tap instead of two)
-                const float rc = __builtin_amdgcn_fmed3f(r * vw * fast_rcp(fabsf(__builtin_fmaf(frag.z, vw, -vz))), 0.0f, 1.0f);
+                // reciprocal per tap instead of two), both scaled by 1 / r (above)
+                const float d1 = __builtin_fmaf(dd, A1, B1);
+                const float rc = __builtin_amdgcn_fmed3f(vw * fast_rcp(fabsf(d1)), 0.0f, 1.0f);
                 const float range = rc * rc * __builtin_fmaf(-2.0f, rc, 3.0f);   // smoothstep(0, 1, x)
-                occ += (__builtin_fmaf(aff(az, kx, ky, kz), vw, -vz) <= 0.0f) ? range : 0.0f;
+                occ += (__builtin_fmaf(aff(dzr, kx, ky, kz), vw, d1) <= 0.0f) ? range : 0.0f;
             } else {
                 const float sd = vz * fast_rcp(vw);
                 const float rc = __builtin_amdgcn_fmed3f(r * fast_rcp(fabsf(frag.z - sd)), 0.0f, 1.0f);   // >= 0
@@ -265,7 +272,10 @@ struct LdsQuad {
         constexpr int TW = SsaoTile<TXP, TYP, HALO>::TW, TH = SsaoTile<TXP, TYP, HALO>::TH;
         const int lx = x0 - gx0, ly = y0 - gy0;
         const bool in = (unsigned)lx < (unsigned)(TW - 1) && (unsigned)ly < (unsigned)(TH - 1);
-        const int i = in ? ly * TW + lx : 0;
+        // ly * TW + lx as one full-rate v_mad_u32_u24 (the compiler otherwise selects v_mad_u64_u32 for it)
+        uint32_t i;
+        asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(i) : "v"(ly), "s"((uint32_t)TW), "v"(lx));
+        i = in ? i : 0u;
         t0 = tile[i];
         t1 = tile[i + 1];
         b0 = tile[i + TW];
@@ -343,6 +353,7 @@ SsaoParams make_params(const soc_globals* g, const soc_img& normal) {
     p.noise_w = normal.width;
     p.swz = tuning_knob("SOC_SWZ_SSAO", -16);   // XCD vertical bands: HBM traffic 3.3x -> 1.25x algorithmic
     p.inv_ksize = 1.0f / p.kernel_size_f;
+    p.inv_radius = 1.0f / p.radius;
     return p;
 }
 
@@ -394,7 +405,7 @@ extern "C" int soc_ssao_generation(const soc_globals* g, soc_img depth, soc_img 
     const float* IP = g->camera_inverse_projection_matrix;
     // sparse inverse projection (the reference's perspective) whose w row stays positive over depths [-1, 1]
     const bool sip = IP[2] == 0.0f && IP[3] == 0.0f && IP[6] == 0.0f && IP[7] == 0.0f && IP[15] - IP[11] > 0.0f &&
-                     IP[15] + IP[11] > 0.0f;
+                     IP[15] + IP[11] > 0.0f && p.radius > 0.0f && std::isfinite(p.inv_radius);
     fold_tap_constants(p, depth.width, depth.height, sip);
     const dim3 blk(256), grd(ceil_div(target.width, 32), ceil_div(target.height, 8));
     const float2* tb = reinterpret_cast<const float2*>(noise_table);
