@@ -93,22 +93,40 @@ typedef float v2f __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ h2 as_h2(uint32_t u) { return __builtin_bit_cast(h2, u); }
 __device__ __forceinline__ v2f h2f2(h2 h) { return v2f{(float)h.x, (float)h.y}; }
 
-// Bilinear sample with the contract's taps; the lerps are fma(w, b - a, a) (within the RGBA16F
-// tolerance of the pass; the texel selection is exactly the contract's). 16-B row-pair loads. The
-// axes are computed once by the caller for the history colour and velocity (same extent).
-__device__ __forceinline__ void sample_pair_rows(const DImg& im, const Axis& ax, const Axis& ay, v2f& xy, v2f& zw,
-                                                 bool need_zw) {
+// Bilinear samples with the contract's taps; the lerps are fma(w, b - a, a) (within the RGBA16F tolerance of the
+// pass; the texel selection is exactly the contract's). 16-B row-pair loads. The axes are computed once by the
+// caller for the history colour and velocity (same extent).
+// The f16 half HI of a packed word, as fp32 (the conversion is exact).
+template <int HI>
+__device__ __forceinline__ float half_f(uint32_t u) {
+    return (float)__builtin_bit_cast(_Float16, (uint16_t)(HI ? u >> 16 : u & 0xffffu));
+}
+// b - a of the f16 halves HI of two words as one v_fma_mix_f32 (b * 1.0 - a, rounded once: the bits of
+// (float)b - (float)a; the compiler would convert both halves and subtract, three instructions)
+template <int HI>
+__device__ __forceinline__ float sub_h(uint32_t b, uint32_t a) {
+    float r;
+    if (HI) asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel:[1,0,1] op_sel_hi:[1,0,1]" : "=v"(r) : "v"(b), "v"(a));
+    else asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(b), "v"(a));
+    return r;
+}
+// Bilinear of the f16 channel HI of the words a, b (top row) and c, d (bottom row): fma(w, b - a, a) per lerp, the
+// horizontal ones straight from the halves (two v_fma_mix_f32 each), the vertical one in fp32
+template <int HI>
+__device__ __forceinline__ float bilerp_h(uint32_t a, uint32_t b, uint32_t c, uint32_t d, float wx, float wy) {
+    const float top = __builtin_fmaf(wx, sub_h<HI>(b, a), half_f<HI>(a));
+    const float bot = __builtin_fmaf(wx, sub_h<HI>(d, c), half_f<HI>(c));
+    return __builtin_fmaf(wy, bot - top, top);
+}
+// The history taps of one pixel: 16-B row-pair loads (texels i0, i0 + 1 of rows i0, i1), channels x y (and z w).
+__device__ __forceinline__ void sample_rows_mix(const DImg& im, const Axis& ax, const Axis& ay, float (&c)[4], bool need_zw) {
     const u4a8 r0 = *reinterpret_cast<const u4a8*>(row_ptr<uint2>(im, ay.i0) + ax.i0);
     const u4a8 r1 = *reinterpret_cast<const u4a8*>(row_ptr<uint2>(im, ay.i1) + ax.i0);
-    const v2f wx = v2f{ax.w, ax.w}, wy = v2f{ay.w, ay.w};
-    auto lerp2 = [](v2f a, v2f b, v2f w) { return __builtin_elementwise_fma(w, b - a, a); };
-    {
-        const v2f a = h2f2(as_h2(r0.x)), b = h2f2(as_h2(r0.z)), c = h2f2(as_h2(r1.x)), d = h2f2(as_h2(r1.z));
-        xy = lerp2(lerp2(a, b, wx), lerp2(c, d, wx), wy);
-    }
+    c[0] = bilerp_h<0>(r0.x, r0.z, r1.x, r1.z, ax.w, ay.w);
+    c[1] = bilerp_h<1>(r0.x, r0.z, r1.x, r1.z, ax.w, ay.w);
     if (need_zw) {
-        const v2f a = h2f2(as_h2(r0.y)), b = h2f2(as_h2(r0.w)), c = h2f2(as_h2(r1.y)), d = h2f2(as_h2(r1.w));
-        zw = lerp2(lerp2(a, b, wx), lerp2(c, d, wx), wy);
+        c[2] = bilerp_h<0>(r0.y, r0.w, r1.y, r1.w, ax.w, ay.w);
+        c[3] = bilerp_h<1>(r0.y, r0.w, r1.y, r1.w, ax.w, ay.w);
     }
 }
 
@@ -248,22 +266,29 @@ __global__ __launch_bounds__(256) void taa_pair2(DImg target, DImg cur, DImg pre
         const v2f q = v2f{0.25f, 0.25f}, hlf = v2f{0.5f, 0.5f};
         const v2f bxy = __builtin_elementwise_fma(sxy[k + 2], q, __builtin_elementwise_fma(sxy[k + 1], hlf, sxy[k] * q));
         const v2f bzw = __builtin_elementwise_fma(szw[k + 2], q, __builtin_elementwise_fma(szw[k + 1], hlf, szw[k] * q));
-        const v2f cxy = h2f2(Cxy[1][k + 2]), czw = h2f2(Czw[1][k + 2]);   // quirk Q7: the (+1, 0) neighbour
-        const h2 vv = as_h2(row_ptr<uint32_t>(vel, by)[2 * bx]);
-        const float velx = (float)vv.x, vely = (float)vv.y;
+        const uint32_t cxy = __builtin_bit_cast(uint32_t, Cxy[1][k + 2]), czw = __builtin_bit_cast(uint32_t, Czw[1][k + 2]);
+        // quirk Q7: the (+1, 0) neighbour is "the" colour
+        const uint32_t vv = row_ptr<uint32_t>(vel, by)[2 * bx];
+        const float velx = half_f<0>(vv), vely = half_f<1>(vv);
         // resolve (:172-189)
         float accum = p.accum0;
         const float vx = u - velx, vy = v - vely;
-        v2f axy, azw, pxy, unused;
         const Axis hax = axis_clamp(vx, prev.w), hay = axis_clamp(vy, prev.h);   // prev and pvel: same extent
-        sample_pair_rows(prev, hax, hay, axy, azw, true);
+        float a4[4], pv[4];
+        sample_rows_mix(prev, hax, hay, a4, true);
         if (vx < 0.0f || vy < 0.0f || vx > 1.0f || vy > 1.0f) accum = 1.0f;
-        axy = __builtin_elementwise_min(__builtin_elementwise_max(axy, h2f2(mnxy)), h2f2(mxxy));
-        azw = __builtin_elementwise_min(__builtin_elementwise_max(azw, h2f2(mnzw)), h2f2(mxzw));
-        const v2f ac = v2f{accum, accum}, ic = v2f{1.0f - accum, 1.0f - accum};
-        const v2f oxy = __builtin_elementwise_fma(cxy, ac, axy * ic), ozw = __builtin_elementwise_fma(czw, ac, azw * ic);
-        sample_pair_rows(pvel, hax, hay, pxy, unused, false);
-        const float dvx = pxy.x - velx, dvy = pxy.y - vely;
+        // clamp to the neighbourhood's [min, max] (min <= max: one v_med3 per channel)
+        const uint32_t mn[2] = {__builtin_bit_cast(uint32_t, mnxy), __builtin_bit_cast(uint32_t, mnzw)};
+        const uint32_t mx[2] = {__builtin_bit_cast(uint32_t, mxxy), __builtin_bit_cast(uint32_t, mxzw)};
+        a4[0] = __builtin_amdgcn_fmed3f(a4[0], half_f<0>(mn[0]), half_f<0>(mx[0]));
+        a4[1] = __builtin_amdgcn_fmed3f(a4[1], half_f<1>(mn[0]), half_f<1>(mx[0]));
+        a4[2] = __builtin_amdgcn_fmed3f(a4[2], half_f<0>(mn[1]), half_f<0>(mx[1]));
+        a4[3] = __builtin_amdgcn_fmed3f(a4[3], half_f<1>(mn[1]), half_f<1>(mx[1]));
+        const float ic = 1.0f - accum;
+        const v2f oxy = v2f{__builtin_fmaf(half_f<0>(cxy), accum, a4[0] * ic), __builtin_fmaf(half_f<1>(cxy), accum, a4[1] * ic)};
+        const v2f ozw = v2f{__builtin_fmaf(half_f<0>(czw), accum, a4[2] * ic), __builtin_fmaf(half_f<1>(czw), accum, a4[3] * ic)};
+        sample_rows_mix(pvel, hax, hay, pv, false);
+        const float dvx = pv[0] - velx, dvy = pv[1] - vely;
         const float vlen = __builtin_amdgcn_sqrtf(__builtin_fmaf(dvx, dvx, dvy * dvy));
         const float dis = clampf((vlen - 0.001f) * 10.0f, 0.0f, 1.0f);
         const v2f dd = v2f{dis, dis};
