@@ -97,6 +97,7 @@ case $cmd in
     bench_line ${t}_bench_raster_c4 --config c4 --raster --no-cpu-baseline
     bench_line ${t}_frame_c3_960 --raster --no-cpu-baseline --width 960 --height 540 --steps 5 --warmup 2 --write-frame gpurun_out/${t}_frame_raster_c3_960x540.png
     kernel_trace $t
+    python tools/roofline_check.py gpurun_out/${t}_bench.json gpurun_out/${t}_kt > gpurun_out/${t}_roofline_check.json
     pmc_passes $t FETCH_SIZE WRITE_SIZE
     python tools/pmc_summary.py gpurun_out/${t}_pmc --traffic gpurun_out/${t}_pmc_traffic.json --scene mesh > gpurun_out/${t}_pmc_summary.json ;;
   *)

@@ -1,0 +1,52 @@
+"""Agreement of the bench line's roofline durations with rocprofv3: the bench measures the north-star kernels with HIP
+events on their stream over its timed frames (lanes concurrent); this takes a `tools/gpu.sh kt` kernel trace of the
+same configuration (`bench.py --steps K --warmup W`: W warm-up frames, K timed frames, then the serial per-pass
+profile frames) and averages each kernel over its timed launches only, so both numbers describe the same kind of
+launch. The kernel trace's own `--stats` average mixes the three segments.
+
+usage: python tools/roofline_check.py BENCH_JSON KT_DIR [--warmup 5] [--steps 20] > profiles/<tag>_roofline_check.json
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+KERNELS = {"SSAOGeneration": "ssao_lds_kernel", "Composition+GenerateLuminanceHistogram": "composition_pair<true"}
+
+
+def main():
+    args = sys.argv[1:]
+    warmup, steps = 5, 20
+    if "--warmup" in args:
+        i = args.index("--warmup")
+        warmup = int(args[i + 1])
+        del args[i:i + 2]
+    if "--steps" in args:
+        i = args.index("--steps")
+        steps = int(args[i + 1])
+        del args[i:i + 2]
+    bench_json, kt_dir = args
+    line = json.load(open(bench_json))
+    trace = glob.glob(os.path.join(kt_dir, "**", "*kernel_trace.csv"), recursive=True)[0]
+    rows = sorted(csv.DictReader(open(trace)), key=lambda r: int(r["Start_Timestamp"]))
+    out = {"bench_line": bench_json, "kernel_trace": trace, "warmup": warmup, "timed": steps, "kernels": {}}
+    pair_events = pair_rocprof = 0.0
+    for name, key in KERNELS.items():
+        d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows if key in r["Kernel_Name"]]
+        timed = d[warmup:warmup + steps]
+        ev = line["roofline"]["per_kernel"][name]["avg_launch_us"]
+        rp = sum(timed) / len(timed)
+        out["kernels"][name] = {"bench_events_us": ev, "rocprof_timed_us": round(rp, 2),
+                                "rocprof_profile_frames_us": round(sum(d[warmup + steps:]) / max(1, len(d[warmup + steps:])), 2),
+                                "ratio": round(ev / rp, 3)}
+        pair_events += ev
+        pair_rocprof += rp
+    out["pair"] = {"bench_events_us": round(pair_events, 2), "rocprof_timed_us": round(pair_rocprof, 2),
+                   "ratio": round(pair_events / pair_rocprof, 3)}
+    json.dump(out, sys.stdout, indent=1)
+    print()
+
+
+if __name__ == "__main__":
+    main()
