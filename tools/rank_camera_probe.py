@@ -35,7 +35,17 @@ def main():
             r.execute(g)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        print(f"{config} rank {rank}: f_sky {f_sky:.3f}, {n / dt:.1f} frames/sec ({dt / n * 1e3:.3f} ms)", flush=True)
+        # per pass, lanes serialised, every pass evented (as bench.py's ms_per_pass)
+        r.set_async(False)
+        r.set_pass_timing(-1, True)
+        r.reset_timing()
+        for _ in range(10):
+            r.execute(g)
+        torch.cuda.synchronize()
+        per = {name: round(ms * 1e3, 1) for name, _, ms, cnt in r.pass_stats() if cnt}
+        big = {k: v for k, v in per.items() if v >= 20.0}
+        print(f"{config} rank {rank}: f_sky {f_sky:.3f}, {n / dt:.1f} frames/sec ({dt / n * 1e3:.3f} ms); passes us {big}",
+              flush=True)
         r.close()
         del fr, sc
         torch.cuda.empty_cache()
