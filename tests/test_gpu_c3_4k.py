@@ -1,5 +1,6 @@
-"""The benchmarked configuration at its own size: bench.py's default command (C3) rendered by the render graph at
-3840x2160 and compared with the oracle's frame of the same inputs.
+"""The benchmarked configurations at their own size: bench.py's default command (C3) and its sky-heavy terrain line
+(C4, f_sky ~0.5: CloudRendering dominates) rendered by the render graph at 3840x2160 and compared with the oracle's
+frame of the same inputs.
 
 The inputs come from bench.build_inputs, exactly as the bench builds them: the Sponza-proxy mesh rasterised once by
 the HIP rasteriser (mip-mapped anisotropic textures), the 4096^2 sun shadow map, the C3 globals (elapsed 10 s,
@@ -17,11 +18,12 @@ from helpers import f16_close, host_frame
 pytestmark = pytest.mark.gpu
 
 
-def test_c3_bench_frame_4k_vs_oracle(soc, oracle):
+@pytest.mark.parametrize("config,sky_range", [("c3", (0.05, 0.2)), ("c4", (0.4, 0.65))])
+def test_bench_frame_4k_vs_oracle(soc, oracle, config, sky_range):
     import bench
     W, H = 3840, 2160
     dev = torch.device("cuda", 0)
-    g, gb, shadow, noise, sc, fr = bench.build_inputs("c3", "mesh", W, H, 0, dev)
+    g, gb, shadow, noise, sc, fr = bench.build_inputs(config, "mesh", W, H, 0, dev)
     r = soc.Renderer(fr, static_inputs=True)          # the bench's renderer flags
     r.set_exposure_pixels(W * H, False)
     assert r.pass_names() == ["BloomDownsample - 0+1", "BloomDownsample - 2+3", "BloomUpsample - 3+2",
@@ -30,7 +32,7 @@ def test_c3_bench_frame_4k_vs_oracle(soc, oracle):
                               "ResolveLuminanceHistogram", "TemporalAntiAliasing+ToneMapping"]
     assert r.pass_lane(r.pass_names().index("CloudRendering")) == 1
     f_sky = float((gb["depth"] == 1.0).mean())
-    assert 0.05 < f_sky < 0.2, f_sky
+    assert sky_range[0] < f_sky < sky_range[1], f_sky
     hf = host_frame(W, H, {**gb, "shadow": shadow, "noise": noise})
     ae = soc.AutoExposure()
     hist = 0
