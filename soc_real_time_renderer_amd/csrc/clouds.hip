@@ -99,6 +99,10 @@ __device__ __forceinline__ int floor_to_int(float x) {
     return r;
 }
 
+// Packed f32 pairs (v_pk_fma_f32 / v_pk_add_f32, tools/microbench/pk_rate.hip): element-wise the scalar operations.
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v pfma(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
+
 // get_3d_noise, :219-233
 template <typename Q>
 __device__ __forceinline__ float noise3(const CtxT<Q>& cx, f3 pos) {
@@ -316,13 +320,20 @@ __device__ f3 atmosphere(f3 r, f3 r0, f3 pSun, float iTime) {
         const float jStep = (delta < 0.0f ? -1.0f : -PoD + __builtin_amdgcn_sqrtf(delta)) / 8.0f;
         const float B = 2.0f * PoD, half = jStep * 0.5f;
         float jTime = 0.0f, jOdR = 0.0f, jOdM = 0.0f;
-#pragma unroll 4
-        for (int j = 0; j < 8; j++) {
-            const float t = jTime + half;
-            const float jLen = __builtin_amdgcn_sqrtf(__builtin_fmaf(t, __builtin_fmaf(t, C2, B), A));
-            jOdR = __builtin_fmaf(__builtin_amdgcn_exp2f(__builtin_fmaf(jLen, kR, cR)), jStep, jOdR);
-            jOdM = __builtin_fmaf(__builtin_amdgcn_exp2f(__builtin_fmaf(jLen, kM, cM)), jStep, jOdM);
-            jTime += jStep;
+        // two secondary steps per packed instruction (v_pk_fma_f32 / v_pk_add_f32), element-wise the same
+        // operations, and the same sequential jTime and accumulation chains: the same bits
+#pragma unroll 2
+        for (int j = 0; j < 8; j += 2) {
+            const float jT1 = jTime + jStep;
+            const f2v t = f2v{jTime, jT1} + f2v{half, half};
+            const f2v q = pfma(t, pfma(t, f2v{C2, C2}, f2v{B, B}), f2v{A, A});
+            const f2v len = {__builtin_amdgcn_sqrtf(q.x), __builtin_amdgcn_sqrtf(q.y)};
+            const f2v eR = pfma(len, f2v{kR, kR}, f2v{cR, cR}), eM = pfma(len, f2v{kM, kM}, f2v{cM, cM});
+            jOdR = __builtin_fmaf(__builtin_amdgcn_exp2f(eR.x), jStep, jOdR);
+            jOdM = __builtin_fmaf(__builtin_amdgcn_exp2f(eM.x), jStep, jOdM);
+            jOdR = __builtin_fmaf(__builtin_amdgcn_exp2f(eR.y), jStep, jOdR);
+            jOdM = __builtin_fmaf(__builtin_amdgcn_exp2f(eM.y), jStep, jOdM);
+            jTime = jT1 + jStep;
         }
         const float fm = kMie * (iOdMie + jOdM);
         const float fr = iOdRlh + jOdR;

@@ -122,8 +122,19 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t depth_rsrc(const DImg& depth) 
     return __builtin_amdgcn_make_buffer_rsrc(depth.data, 0, depth.pitch * depth.h, 0x00020000);
 }
 
+// Packed f32 pairs (v_pk_fma_f32 / v_pk_mul_f32: two lanes' worth of f32 work per issue slot on gfx950,
+// tools/microbench/pk_rate.hip); element-wise the same IEEE operations as the scalar forms, so the same bits.
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v pfma(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2v bc2(float x) { return f2v{x, x}; }
+__device__ __forceinline__ f2v aff2(const Aff& a, f2v kx, f2v ky, f2v kz) {
+    return pfma(bc2(a.a3), kz, pfma(bc2(a.a2), ky, pfma(bc2(a.a1), kx, bc2(a.a0))));
+}
+
 // One half-res pixel of SSAOGenerationTask (:176-214); `quad` fetches a tap's 2x2 D32 texels.
-template <bool TABLE, bool SPARSE_IP, bool FULL, class Quad, int UNROLL = SOC_SSAO_MAX_KERNEL>
+// PK (sparse inverse projection, full kernel only): the taps in pairs, the affine forms, weights, range test and
+// smoothstep of both taps as packed f32 operations; per tap the same operations in the same order (bit-identical).
+template <bool TABLE, bool SPARSE_IP, bool FULL, class Quad, int UNROLL = SOC_SSAO_MAX_KERNEL, bool PK = false>
 __device__ __forceinline__ void ssao_pixel(int x, int y, const DImg& depth, const DImg& normal, const DImg& target,
                                            const float2* __restrict__ table, const SsaoParams& p, const Quad& quad) {
     // no implicit contraction: every fused multiply-add below is an explicit fma, so the per-pixel arithmetic does not
@@ -190,6 +201,36 @@ __device__ __forceinline__ void ssao_pixel(int x, int y, const DImg& depth, cons
     const int W = depth.w, H = depth.h;
     const float cx0 = p.c0x, cy0 = p.c0y, tmax_x = p.tmx, tmax_y = p.tmy;   // texel (or sub-texel) space
     float occ = 0.0f;
+    if constexpr (PK && SPARSE_IP && FULL) {
+        static_assert(SOC_SSAO_MAX_KERNEL % 2 == 0, "taps are paired");
+        // the same per-tap operations as the scalar loop below, two taps per packed instruction
+#pragma unroll 1
+        for (int i = 0; i < SOC_SSAO_MAX_KERNEL; i += 2) {
+            const f2v kx = {kKernel.v[i][0], kKernel.v[i + 1][0]}, ky = {kKernel.v[i][1], kKernel.v[i + 1][1]},
+                      kz = {kKernel.v[i][2], kKernel.v[i + 1][2]};
+            const f2v ww = aff2(aw, kx, ky, kz);
+            const f2v rw = {fast_rcp(ww.x), fast_rcp(ww.y)};
+            const f2v X = pfma(aff2(ax, kx, ky, kz), rw, bc2(cx0)), Y = pfma(aff2(ay, kx, ky, kz), rw, bc2(cy0));
+            const int fx0 = (int)__builtin_amdgcn_fmed3f(X.x, 0.5f, tmax_x), fx1 = (int)__builtin_amdgcn_fmed3f(X.y, 0.5f, tmax_x);
+            const int fy0 = (int)__builtin_amdgcn_fmed3f(Y.x, 0.5f, tmax_y), fy1 = (int)__builtin_amdgcn_fmed3f(Y.y, 0.5f, tmax_y);
+            const f2v wx = f2v{(float)(fx0 & 255), (float)(fx1 & 255)} * bc2(1.0f / 256.0f);
+            const f2v wy = f2v{(float)(fy0 & 255), (float)(fy1 & 255)} * bc2(1.0f / 256.0f);
+            float a0, a1, a2, a3, b0, b1, b2, b3;
+            quad(fx0 >> 8, fy0 >> 8, a0, a1, a2, a3);
+            quad(fx1 >> 8, fy1 >> 8, b0, b1, b2, b3);
+            const float atop = __builtin_fmaf(wx.x, a1 - a0, a0), abot = __builtin_fmaf(wx.x, a3 - a2, a2);
+            const float btop = __builtin_fmaf(wx.y, b1 - b0, b0), bbot = __builtin_fmaf(wx.y, b3 - b2, b2);
+            const f2v dd = {__builtin_fmaf(wy.x, abot - atop, atop), __builtin_fmaf(wy.y, bbot - btop, btop)};
+            const f2v vw = pfma(bc2(ip[11]), dd, bc2(ip[15]));
+            const f2v d1 = pfma(dd, bc2(A1), bc2(B1));
+            const f2v q = vw * f2v{fast_rcp(fabsf(d1.x)), fast_rcp(fabsf(d1.y))};
+            const f2v rc = {__builtin_amdgcn_fmed3f(q.x, 0.0f, 1.0f), __builtin_amdgcn_fmed3f(q.y, 0.0f, 1.0f)};
+            const f2v range = rc * rc * pfma(bc2(-2.0f), rc, bc2(3.0f));   // smoothstep(0, 1, x)
+            const f2v d2 = pfma(aff2(dzr, kx, ky, kz), vw, d1);
+            occ += (d2.x <= 0.0f) ? range.x : 0.0f;
+            occ += (d2.y <= 0.0f) ? range.y : 0.0f;
+        }
+    } else {
 #pragma unroll UNROLL
     for (int i = 0; i < SOC_SSAO_MAX_KERNEL; ++i) {
         if (FULL || i < p.ksize) {
@@ -239,6 +280,7 @@ __device__ __forceinline__ void ssao_pixel(int x, int y, const DImg& depth, cons
             }
         }
     }
+    }
     occ = 1.0f - occ * p.inv_ksize;
     row_ptr_w<uint8_t>(target, y)[x] = (uint8_t)to_unorm8(occ);
 }
@@ -284,7 +326,7 @@ struct LdsQuad {
     }
 };
 
-template <bool TABLE, bool SPARSE_IP, bool FULL, int TXP, int TYP, int HALO, int UNROLL>
+template <bool TABLE, bool SPARSE_IP, bool FULL, int TXP, int TYP, int HALO, int UNROLL, bool PK = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(TXP * TYP, TXP * TYP)))
 __attribute__((amdgpu_waves_per_eu(TXP * TYP >= 1024 ? 8 : TXP * TYP >= 512 ? 4 : 2)))
 void ssao_lds_kernel(DImg depth, DImg normal, DImg target, const float2* __restrict__ table, SsaoParams p) {
@@ -310,7 +352,7 @@ void ssao_lds_kernel(DImg depth, DImg normal, DImg target, const float2* __restr
     const int x = bx * TXP + (w % (TXP / 32)) * 32 + (lane & 31), y = by * TYP + (w / (TXP / 32)) * 2 + (lane >> 5);
     if (x >= target.w || y >= target.h) return;
     const LdsQuad<TXP, TYP, HALO> quad{reinterpret_cast<const float*>(tile4), gx0, gy0, GlobalQuad{rsrc, depth.pitch}};
-    ssao_pixel<TABLE, SPARSE_IP, FULL, LdsQuad<TXP, TYP, HALO>, UNROLL>(x, y, depth, normal, target, table, p, quad);
+    ssao_pixel<TABLE, SPARSE_IP, FULL, LdsQuad<TXP, TYP, HALO>, UNROLL, PK>(x, y, depth, normal, target, table, p, quad);
 }
 
 // ssao_blur.inl:91-106: 4x4 box at offsets -2..+1 (x outer, y inner), all taps on texel centres.
@@ -419,8 +461,8 @@ extern "C" int soc_ssao_generation(const soc_globals* g, soc_img depth, soc_img 
     if (noise_table && sip && full && tiled) {
         SsaoParams pt = p;
         pt.swz = 1;
-        ssao_lds_kernel<true, true, true, 64, 16, 32, 2>
-            <<<dim3(ceil_div(target.width, 64), ceil_div(target.height, 16)), 1024, 0, st>>>(dd, dn, dt, tb, pt);
+        const dim3 g(ceil_div(target.width, 64), ceil_div(target.height, 16));
+        ssao_lds_kernel<true, true, true, 64, 16, 32, 2, true><<<g, 1024, 0, st>>>(dd, dn, dt, tb, pt);
     } else if (noise_table && sip && full) SOC_SSAO_LAUNCH(true, true, true);
     else if (noise_table && sip) SOC_SSAO_LAUNCH(true, true, false);
     else if (noise_table) SOC_SSAO_LAUNCH(true, false, false);
