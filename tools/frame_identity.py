@@ -3,8 +3,11 @@ variants and checks that every frame output (colour, framebuffer, SSAO, clouds, 
 the default variant's, frame after frame. An A/B tool for variants that claim the same bits (e.g. packed-f32 forms).
 
 usage: python tools/frame_identity.py [--config c3|c4] [--frames N] KNOB=V[,KNOB=V...] ...
+       python tools/frame_identity.py --hash [--config c3|c4]      (one digest per output and frame: compare two builds,
+                                                                   e.g. SOC_RT_LIB_VARIANT=libsoc_rt_base.so)
 """
 import argparse
+import hashlib
 import os
 import sys
 
@@ -49,9 +52,17 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c3")
     ap.add_argument("--frames", type=int, default=3)
-    ap.add_argument("variants", nargs="+")
+    ap.add_argument("--hash", action="store_true")
+    ap.add_argument("variants", nargs="*")
     a = ap.parse_args()
     ref = render(a.config, a.frames, {})
+    if a.hash:
+        d = hashlib.sha256()
+        for f in ref:
+            for k in sorted(f):
+                d.update(f[k].cpu().numpy().tobytes())
+        print(f"{a.config} {os.environ.get('SOC_RT_LIB_VARIANT', 'libsoc_rt.so')} frames {a.frames} digest {d.hexdigest()[:16]}",
+              flush=True)
     for v in a.variants:
         env = dict(kv.split("=") for kv in v.split(",") if kv)
         got = render(a.config, a.frames, env)
