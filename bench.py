@@ -56,7 +56,7 @@ from soc_real_time_renderer_amd import multi_gpu, raster, scene  # noqa: E402
 from soc_real_time_renderer_amd.scene import sponza_mesh  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
-SSAO_KERNEL = "ssao_lds_kernel<true, true, true, 64, 16, 32, 2>"   # the default SSAOGeneration kernel (ssao.hip)
+SSAO_KERNEL = "ssao_lds_kernel<true, true, true, 64, 16, 32, 2, true>"   # the default SSAOGeneration kernel (ssao.hip)
 
 
 def make_globals(W, H, camera):
@@ -374,6 +374,13 @@ def main():
     pair_traffic = traffic + ssao_traffic if traffic is not None and ssao_traffic is not None else None
     pair_achieved = ns_bytes / (ns_us * 1e-6) / 1e9
 
+    def serial_fields(n):
+        # the same kernel with the lanes serialised (the per-pass loop above: nothing shares the CUs with it); the
+        # in-frame figure above also carries the concurrent second lane's share of the CUs
+        us = ms_pass.get(n)
+        return {"serial_us": round(us * 1e3, 2), "serial_frac": round(algo[n] / (us * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)} \
+            if us else {}
+
     if world > 1:
         dist.barrier()
     if rank != 0:
@@ -417,12 +424,12 @@ def main():
                      "per_kernel": {
                          comp: {"achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
                                 "traffic": traffic, "algorithmic_bytes_per_launch": int(algo[comp]),
-                                "avg_launch_us": round(comp_ms * 1e3, 2)},
+                                "avg_launch_us": round(comp_ms * 1e3, 2), **serial_fields(comp)},
                          "SSAOGeneration": {"achieved": round(algo["SSAOGeneration"] / (ssao_ms * 1e-3) / 1e9, 1),
                                             "frac": round(algo["SSAOGeneration"] / (ssao_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                                             "traffic": ssao_traffic,
                                             "algorithmic_bytes_per_launch": int(algo["SSAOGeneration"]),
-                                            "avg_launch_us": round(ssao_ms * 1e3, 2),
+                                            "avg_launch_us": round(ssao_ms * 1e3, 2), **serial_fields("SSAOGeneration"),
                                             "gather_bound": (ssao_gather_bound(W, H, args.scene, ssao_ms * 1e3)
                                                              if args.config == "c3" else None),
                                             "valu_bound": (valu_bound(SSAO_KERNEL, ssao_ms * 1e3)

@@ -149,6 +149,101 @@ struct TmOut {
     int srgb;   // RGBA8_SRGB framebuffer: sRGB-encode on store
 };
 
+// The part of the pair kernels after the neighbourhood is loaded (:156-189 and the fused tone map): column min / max,
+// Gaussian column sums, the closest-depth texel, the history resolve and the stores. Cxy / Czw / D: the 3 x 4
+// neighbourhood (rows y+1, y, y-1; columns xl, x0, x0+1, xr); vel_at(x, y): the RG word of the current velocity texel;
+// own_vel(): the lane's own velocity pair (the fused velocity-history copy).
+template <bool TM, class VelAt, class OwnVel>
+__device__ __forceinline__ void taa_pair_tail(const DImg& target, const DImg& prev, const DImg& pvel, const DImg& vel_out,
+                                              const TaaParams& p, const TmOut& tm, int x0, int y, int xl, int xr,
+                                              const int (&rows)[3], const h2 (&Cxy)[3][4], const h2 (&Czw)[3][4],
+                                              const float (&D)[3][4], float exposure, const VelAt& vel_at,
+                                              const OwnVel& own_vel) {
+    const int W = target.w, H = target.h;
+    // column min / max (packed f16) and Gaussian column sums (fp32)
+    h2 nxy[4], nzw[4], xxy[4], xzw[4];
+    v2f sxy[4], szw[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        nxy[c] = __builtin_elementwise_min(__builtin_elementwise_min(Cxy[0][c], Cxy[1][c]), Cxy[2][c]);
+        nzw[c] = __builtin_elementwise_min(__builtin_elementwise_min(Czw[0][c], Czw[1][c]), Czw[2][c]);
+        xxy[c] = __builtin_elementwise_max(__builtin_elementwise_max(Cxy[0][c], Cxy[1][c]), Cxy[2][c]);
+        xzw[c] = __builtin_elementwise_max(__builtin_elementwise_max(Czw[0][c], Czw[1][c]), Czw[2][c]);
+        sxy[c] = gauss_col(Cxy[0][c], Cxy[1][c], Cxy[2][c]);
+        szw[c] = gauss_col(Czw[0][c], Czw[1][c], Czw[2][c]);
+    }
+    const int colx[4] = {xl, x0, x0 + 1, xr};
+    const float v = centre_uv_rn(y, H, p.rh);
+    uint2 outp[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int x = x0 + k;
+        const float u = centre_uv_rn(x, W, p.rw);
+        // closest depth in the reference order (oy = +1..-1, ox = +1..-1), last equal wins
+        // the winning tap as one index r * 4 + c (one select per tap instead of two)
+        float closest = 1.0f;
+        int bi = 4 + k + 1;
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int ox = 1; ox > -2; --ox) {
+                const int c = k + 1 + ox;
+                const float d = D[r][c];
+                closest = fminf(d, closest);
+                bi = closest == d ? r * 4 + c : bi;
+            }
+        const int bx = colx[bi & 3], by = rows[bi >> 2];
+        const h2 mnxy = __builtin_elementwise_min(__builtin_elementwise_min(nxy[k], nxy[k + 1]), nxy[k + 2]);
+        const h2 mnzw = __builtin_elementwise_min(__builtin_elementwise_min(nzw[k], nzw[k + 1]), nzw[k + 2]);
+        const h2 mxxy = __builtin_elementwise_max(__builtin_elementwise_max(xxy[k], xxy[k + 1]), xxy[k + 2]);
+        const h2 mxzw = __builtin_elementwise_max(__builtin_elementwise_max(xzw[k], xzw[k + 1]), xzw[k + 2]);
+        const v2f q = v2f{0.25f, 0.25f}, hlf = v2f{0.5f, 0.5f};
+        const v2f bxy = __builtin_elementwise_fma(sxy[k + 2], q, __builtin_elementwise_fma(sxy[k + 1], hlf, sxy[k] * q));
+        const v2f bzw = __builtin_elementwise_fma(szw[k + 2], q, __builtin_elementwise_fma(szw[k + 1], hlf, szw[k] * q));
+        const uint32_t cxy = __builtin_bit_cast(uint32_t, Cxy[1][k + 2]), czw = __builtin_bit_cast(uint32_t, Czw[1][k + 2]);
+        // quirk Q7: the (+1, 0) neighbour is "the" colour
+        const uint32_t vv = vel_at(bx, by);
+        const float velx = half_f<0>(vv), vely = half_f<1>(vv);
+        // resolve (:172-189)
+        float accum = p.accum0;
+        const float vx = u - velx, vy = v - vely;
+        const Axis hax = axis_clamp(vx, prev.w), hay = axis_clamp(vy, prev.h);   // prev and pvel: same extent
+        float a4[4], pv[4];
+        sample_rows_mix(prev, hax, hay, a4, true);
+        if (vx < 0.0f || vy < 0.0f || vx > 1.0f || vy > 1.0f) accum = 1.0f;
+        // clamp to the neighbourhood's [min, max] (min <= max: one v_med3 per channel)
+        const uint32_t mn[2] = {__builtin_bit_cast(uint32_t, mnxy), __builtin_bit_cast(uint32_t, mnzw)};
+        const uint32_t mx[2] = {__builtin_bit_cast(uint32_t, mxxy), __builtin_bit_cast(uint32_t, mxzw)};
+        a4[0] = __builtin_amdgcn_fmed3f(a4[0], half_f<0>(mn[0]), half_f<0>(mx[0]));
+        a4[1] = __builtin_amdgcn_fmed3f(a4[1], half_f<1>(mn[0]), half_f<1>(mx[0]));
+        a4[2] = __builtin_amdgcn_fmed3f(a4[2], half_f<0>(mn[1]), half_f<0>(mx[1]));
+        a4[3] = __builtin_amdgcn_fmed3f(a4[3], half_f<1>(mn[1]), half_f<1>(mx[1]));
+        const float ic = 1.0f - accum;
+        const v2f oxy = v2f{__builtin_fmaf(half_f<0>(cxy), accum, a4[0] * ic), __builtin_fmaf(half_f<1>(cxy), accum, a4[1] * ic)};
+        const v2f ozw = v2f{__builtin_fmaf(half_f<0>(czw), accum, a4[2] * ic), __builtin_fmaf(half_f<1>(czw), accum, a4[3] * ic)};
+        sample_rows_mix(pvel, hax, hay, pv, false);
+        const float dvx = pv[0] - velx, dvy = pv[1] - vely;
+        const float vlen = __builtin_amdgcn_sqrtf(__builtin_fmaf(dvx, dvx, dvy * dvy));
+        const float dis = clampf((vlen - 0.001f) * 10.0f, 0.0f, 1.0f);
+        const v2f dd = v2f{dis, dis};
+        const v2f rxy = __builtin_elementwise_fma(bxy - oxy, dd, oxy), rzw = __builtin_elementwise_fma(bzw - ozw, dd, ozw);
+        outp[k] = pack_h4(f4{rxy.x, rxy.y, rzw.x, rzw.y});
+    }
+    row_ptr_w<uint4>(target, y)[x0 >> 1] = uint4{outp[0].x, outp[0].y, outp[1].x, outp[1].y};
+    if (vel_out.data) row_ptr_w<uint4>(vel_out, y)[x0 >> 1] = own_vel();
+    if (TM) {
+        const float expo = exp2f(exposure);   // pow(2.0, exposure)
+        f3 c0 = agx(tm.p, unpack_h4(outp[0]), expo);
+        f3 c1 = agx(tm.p, unpack_h4(outp[1]), expo);
+        if (tm.srgb) {
+            c0 = f3{srgb_encode(c0.x), srgb_encode(c0.y), srgb_encode(c0.z)};
+            c1 = f3{srgb_encode(c1.x), srgb_encode(c1.y), srgb_encode(c1.z)};
+        }
+        row_ptr_w<uint2>(tm.out, y)[x0 >> 1] =
+            uint2{pack_unorm8x4(f4{c0.x, c0.y, c0.z, 1.0f}), pack_unorm8x4(f4{c1.x, c1.y, c1.z, 1.0f})};
+    }
+}
+
 // Lane i's left neighbour column (x0 - 1) is lane i-1's second pixel and its right one (x0 + 2) lane
 // i+1's first: with NBR the neighbourhood's side columns come from the adjacent lanes through DPP wave
 // shifts (VALU) instead of two more colour and two more depth loads per row, and only the lanes at a
@@ -226,88 +321,91 @@ __global__ __launch_bounds__(256) void taa_pair2(DImg target, DImg cur, DImg pre
         D[r][3] = dr;
     }
     if (NBR && !inside_x) return;   // past the image: only fed its neighbours' shifts
-    // column min / max (packed f16) and Gaussian column sums (fp32)
-    h2 nxy[4], nzw[4], xxy[4], xzw[4];
-    v2f sxy[4], szw[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        nxy[c] = __builtin_elementwise_min(__builtin_elementwise_min(Cxy[0][c], Cxy[1][c]), Cxy[2][c]);
-        nzw[c] = __builtin_elementwise_min(__builtin_elementwise_min(Czw[0][c], Czw[1][c]), Czw[2][c]);
-        xxy[c] = __builtin_elementwise_max(__builtin_elementwise_max(Cxy[0][c], Cxy[1][c]), Cxy[2][c]);
-        xzw[c] = __builtin_elementwise_max(__builtin_elementwise_max(Czw[0][c], Czw[1][c]), Czw[2][c]);
-        sxy[c] = gauss_col(Cxy[0][c], Cxy[1][c], Cxy[2][c]);
-        szw[c] = gauss_col(Czw[0][c], Czw[1][c], Czw[2][c]);
+    taa_pair_tail<TM>(target, prev, pvel, vel_out, p, tm, x0, y, xl, xr, rows, Cxy, Czw, D, exposure,
+                      [&](int bx, int by) { return row_ptr<uint32_t>(vel, by)[2 * bx]; },
+                      [&]() { return row_ptr<uint4>(vel, y)[x0 >> 1]; });
+}
+
+// LDS-staged neighbourhood: a workgroup of 64 x 4 lanes (128 x 4 output pixels, a pixel pair per lane) stages the
+// colour and velocity pairs and the depth quads of its 6 rows (y0 - 1 .. y0 + 4, clamped) and 2 + 128 + 2 columns with
+// 16-B loads, once; every lane then reads its 3 x 4 neighbourhood, its closest-depth velocity texel and its own
+// velocity pair (the fused history copy) from LDS. Per lane about 4 staging loads instead of 9 neighbourhood, velocity
+// and copy loads (the texture path is the kernel's bound), and the velocity gather no longer waits on a load level.
+// The same values reach the same arithmetic (taa_pair_tail) as taa_pair2: the same bits.
+constexpr int kTaaPairs = 64;                                     // output pairs per workgroup row
+constexpr int kTaaTP = kTaaPairs + 2;                             // staged pairs (pair p0 - 1 .. p0 + 64)
+constexpr int kTaaTQ = kTaaPairs / 2 + 2;                         // staged depth quads (quad q0 - 1 .. q0 + 32)
+
+template <bool TM, int kTaaRows = 4>   // rows per workgroup: 4 measured against 2 and 8 (profiles/r03_ab_taa_lds.txt)
+__global__ __launch_bounds__(64 * kTaaRows) void taa_lds(DImg target, DImg cur, DImg prev, DImg vel, DImg pvel, DImg depth,
+                                                         DImg vel_out, TaaParams p, TmOut tm) {
+    constexpr int kTaaTR = kTaaRows + 2, NT = 64 * kTaaRows;   // staged rows y0 - 1 .. y0 + kTaaRows
+    __shared__ uint4 ct[kTaaTR][kTaaTP];   // colour pairs
+    __shared__ uint4 vt[kTaaTR][kTaaTP];   // velocity pairs
+    __shared__ float4 dt[kTaaTR][kTaaTQ];  // depth quads
+    int tbx, tby;
+    xcd_order(p.swz, tbx, tby);
+    const int W = target.w, H = target.h;
+    const int tid = threadIdx.x + threadIdx.y * 64;
+    const int p0 = tbx * kTaaPairs, y0 = tby * kTaaRows, q0 = tbx * (kTaaPairs / 2);
+    const int npairs = W >> 1, nquads = (W + 3) >> 2;
+    // staging: rows clamped into the image, pairs / quads clamped into the row (the clamped copies are never read:
+    // the border columns come from the lane's own pixels, as in taa_pair2)
+    for (int i = tid; i < kTaaTR * kTaaTP; i += NT) {
+        const int r = i / kTaaTP, c = i - r * kTaaTP;
+        const int sy = min(max(y0 - 1 + r, 0), H - 1), sp = min(max(p0 - 1 + c, 0), npairs - 1);
+        ct[r][c] = row_ptr<uint4>(cur, sy)[sp];
+        vt[r][c] = row_ptr<uint4>(vel, sy)[sp];
     }
-    const int colx[4] = {xl, x0, x0 + 1, xr};
-    const float v = centre_uv_rn(y, H, p.rh);
-    uint2 outp[2];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const int x = x0 + k;
-        const float u = centre_uv_rn(x, W, p.rw);
-        // closest depth in the reference order (oy = +1..-1, ox = +1..-1), last equal wins
-        // the winning tap as one index r * 4 + c (one select per tap instead of two)
-        float closest = 1.0f;
-        int bi = 4 + k + 1;
-#pragma unroll
-        for (int r = 0; r < 3; ++r)
-#pragma unroll
-            for (int ox = 1; ox > -2; --ox) {
-                const int c = k + 1 + ox;
-                const float d = D[r][c];
-                closest = fminf(d, closest);
-                bi = closest == d ? r * 4 + c : bi;
-            }
-        const int bx = colx[bi & 3], by = rows[bi >> 2];
-        const h2 mnxy = __builtin_elementwise_min(__builtin_elementwise_min(nxy[k], nxy[k + 1]), nxy[k + 2]);
-        const h2 mnzw = __builtin_elementwise_min(__builtin_elementwise_min(nzw[k], nzw[k + 1]), nzw[k + 2]);
-        const h2 mxxy = __builtin_elementwise_max(__builtin_elementwise_max(xxy[k], xxy[k + 1]), xxy[k + 2]);
-        const h2 mxzw = __builtin_elementwise_max(__builtin_elementwise_max(xzw[k], xzw[k + 1]), xzw[k + 2]);
-        const v2f q = v2f{0.25f, 0.25f}, hlf = v2f{0.5f, 0.5f};
-        const v2f bxy = __builtin_elementwise_fma(sxy[k + 2], q, __builtin_elementwise_fma(sxy[k + 1], hlf, sxy[k] * q));
-        const v2f bzw = __builtin_elementwise_fma(szw[k + 2], q, __builtin_elementwise_fma(szw[k + 1], hlf, szw[k] * q));
-        const uint32_t cxy = __builtin_bit_cast(uint32_t, Cxy[1][k + 2]), czw = __builtin_bit_cast(uint32_t, Czw[1][k + 2]);
-        // quirk Q7: the (+1, 0) neighbour is "the" colour
-        const uint32_t vv = row_ptr<uint32_t>(vel, by)[2 * bx];
-        const float velx = half_f<0>(vv), vely = half_f<1>(vv);
-        // resolve (:172-189)
-        float accum = p.accum0;
-        const float vx = u - velx, vy = v - vely;
-        const Axis hax = axis_clamp(vx, prev.w), hay = axis_clamp(vy, prev.h);   // prev and pvel: same extent
-        float a4[4], pv[4];
-        sample_rows_mix(prev, hax, hay, a4, true);
-        if (vx < 0.0f || vy < 0.0f || vx > 1.0f || vy > 1.0f) accum = 1.0f;
-        // clamp to the neighbourhood's [min, max] (min <= max: one v_med3 per channel)
-        const uint32_t mn[2] = {__builtin_bit_cast(uint32_t, mnxy), __builtin_bit_cast(uint32_t, mnzw)};
-        const uint32_t mx[2] = {__builtin_bit_cast(uint32_t, mxxy), __builtin_bit_cast(uint32_t, mxzw)};
-        a4[0] = __builtin_amdgcn_fmed3f(a4[0], half_f<0>(mn[0]), half_f<0>(mx[0]));
-        a4[1] = __builtin_amdgcn_fmed3f(a4[1], half_f<1>(mn[0]), half_f<1>(mx[0]));
-        a4[2] = __builtin_amdgcn_fmed3f(a4[2], half_f<0>(mn[1]), half_f<0>(mx[1]));
-        a4[3] = __builtin_amdgcn_fmed3f(a4[3], half_f<1>(mn[1]), half_f<1>(mx[1]));
-        const float ic = 1.0f - accum;
-        const v2f oxy = v2f{__builtin_fmaf(half_f<0>(cxy), accum, a4[0] * ic), __builtin_fmaf(half_f<1>(cxy), accum, a4[1] * ic)};
-        const v2f ozw = v2f{__builtin_fmaf(half_f<0>(czw), accum, a4[2] * ic), __builtin_fmaf(half_f<1>(czw), accum, a4[3] * ic)};
-        sample_rows_mix(pvel, hax, hay, pv, false);
-        const float dvx = pv[0] - velx, dvy = pv[1] - vely;
-        const float vlen = __builtin_amdgcn_sqrtf(__builtin_fmaf(dvx, dvx, dvy * dvy));
-        const float dis = clampf((vlen - 0.001f) * 10.0f, 0.0f, 1.0f);
-        const v2f dd = v2f{dis, dis};
-        const v2f rxy = __builtin_elementwise_fma(bxy - oxy, dd, oxy), rzw = __builtin_elementwise_fma(bzw - ozw, dd, ozw);
-        outp[k] = pack_h4(f4{rxy.x, rxy.y, rzw.x, rzw.y});
+    for (int i = tid; i < kTaaTR * kTaaTQ; i += NT) {
+        const int r = i / kTaaTQ, c = i - r * kTaaTQ;
+        const int sy = min(max(y0 - 1 + r, 0), H - 1), sq = min(max(q0 - 1 + c, 0), nquads - 1);
+        const float* drow = row_ptr<float>(depth, sy);
+        if (4 * sq + 3 < W) dt[r][c] = *reinterpret_cast<const float4*>(drow + 4 * sq);
+        else dt[r][c] = float4{drow[4 * sq], drow[min(4 * sq + 1, W - 1)], drow[min(4 * sq + 2, W - 1)], drow[min(4 * sq + 3, W - 1)]};
     }
-    row_ptr_w<uint4>(target, y)[x0 >> 1] = uint4{outp[0].x, outp[0].y, outp[1].x, outp[1].y};
-    if (vel_out.data) row_ptr_w<uint4>(vel_out, y)[x0 >> 1] = row_ptr<uint4>(vel, y)[x0 >> 1];
-    if (TM) {
-        const float expo = exp2f(exposure);   // pow(2.0, exposure)
-        f3 c0 = agx(tm.p, unpack_h4(outp[0]), expo);
-        f3 c1 = agx(tm.p, unpack_h4(outp[1]), expo);
-        if (tm.srgb) {
-            c0 = f3{srgb_encode(c0.x), srgb_encode(c0.y), srgb_encode(c0.z)};
-            c1 = f3{srgb_encode(c1.x), srgb_encode(c1.y), srgb_encode(c1.z)};
-        }
-        row_ptr_w<uint2>(tm.out, y)[x0 >> 1] =
-            uint2{pack_unorm8x4(f4{c0.x, c0.y, c0.z, 1.0f}), pack_unorm8x4(f4{c1.x, c1.y, c1.z, 1.0f})};
+    __syncthreads();
+    const int pl = threadIdx.x, ty = threadIdx.y;
+    const int x0 = 2 * (p0 + pl), y = y0 + ty;
+    if (x0 >= W || y >= H) return;
+    const int xl = max(x0 - 1, 0), xr = min(x0 + 2, W - 1);
+    const float* dtf = reinterpret_cast<const float*>(dt);
+    const int dbase = 4 * (q0 - 1);   // image column of dtf[r * 4 * kTaaTQ + 0]
+    h2 Cxy[3][4], Czw[3][4];
+    float D[3][4];
+    int rows[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        const int tr = ty + 2 - r;   // tile row of image row y + 1 - r
+        rows[r] = min(max(y + 1 - r, 0), H - 1);
+        const uint4 mid = ct[tr][pl + 1];
+        uint2 L = uint2{ct[tr][pl].z, ct[tr][pl].w}, R = uint2{ct[tr][pl + 2].x, ct[tr][pl + 2].y};
+        const float* drow = dtf + tr * 4 * kTaaTQ - dbase;
+        const float2 dmid = *reinterpret_cast<const float2*>(drow + x0);
+        float dl = drow[x0 - 1], dr = drow[x0 + 2];
+        if (x0 == 0) { L = uint2{mid.x, mid.y}; dl = dmid.x; }           // image borders: the clamped side column is the
+        if (x0 + 2 >= W) { R = uint2{mid.z, mid.w}; dr = dmid.y; }      // pair's own pixel
+        Cxy[r][0] = as_h2(L.x);
+        Czw[r][0] = as_h2(L.y);
+        Cxy[r][1] = as_h2(mid.x);
+        Czw[r][1] = as_h2(mid.y);
+        Cxy[r][2] = as_h2(mid.z);
+        Czw[r][2] = as_h2(mid.w);
+        Cxy[r][3] = as_h2(R.x);
+        Czw[r][3] = as_h2(R.y);
+        D[r][0] = dl;
+        D[r][1] = dmid.x;
+        D[r][2] = dmid.y;
+        D[r][3] = dr;
     }
+    const float exposure = TM ? tm.ae->exposure : 0.0f;
+    const uint32_t* vtw = reinterpret_cast<const uint32_t*>(vt);
+    taa_pair_tail<TM>(target, prev, pvel, vel_out, p, tm, x0, y, xl, xr, rows, Cxy, Czw, D, exposure,
+                      [&](int bx, int by) {   // the RG word of texel (bx, by): pair bx / 2, word 2 (bx & 1)
+                          const int tr = by - (y0 - 1), c = (bx >> 1) - (p0 - 1);
+                          return vtw[(tr * kTaaTP + c) * 4 + 2 * (bx & 1)];
+                      },
+                      [&]() { return vt[ty + 1][pl + 1]; });
 }
 
 __global__ __launch_bounds__(256) void taa_generic(DImg target, DImg cur, DImg prev, DImg vel, DImg pvel, DImg depth,
@@ -404,10 +502,20 @@ int taa_launch(const soc_globals* g, soc_img target, soc_img current_color, soc_
         // 32 x 8 lanes (64 x 8 pixels): the 3-row neighbourhood reloads 10 rows per 8 instead of 6 per 4
         const int by = 8, bxl = 256 / by;
         dim3 blk(bxl, by), g2(ceil_div(W / 2, bxl), ceil_div(H, by));
-        // side columns: 2 = halo lanes (default), 1 = lane shifts + edge-lane loads, 0 = every lane loads them
-        const int nbr = tuning_knob("SOC_TAA_NBR", 2);
+        // neighbourhood source: 3 = LDS-staged tiles (default; needs a 16-B aligned depth image), 2 = halo lanes, 1 = lane
+        // shifts + edge-lane loads, 0 = every lane loads its side columns (the same bits, tests/test_gpu_parity.py)
+        const int nbr = tuning_knob("SOC_TAA_NBR", 3);
         const dim3 blk_h(64, 4), g2_h(ceil_div(W / 2, 62), ceil_div(H, 4));
-        if (tm && nbr == 2)
+        if (nbr == 3 && a16(depth)) {
+            const dim3 gl(ceil_div(W / 2, kTaaPairs), ceil_div(H, 4));
+            if (tm)
+                taa_lds<true><<<gl, blk_h, 0, hs(stream)>>>(dimg(target), dimg(current_color), dimg(previous_color),
+                                                          dimg(current_velocity), dimg(previous_velocity), dimg(depth), vo, p, *tm);
+            else
+                taa_lds<false><<<gl, blk_h, 0, hs(stream)>>>(dimg(target), dimg(current_color), dimg(previous_color),
+                                                           dimg(current_velocity), dimg(previous_velocity), dimg(depth), vo, p,
+                                                           TmOut{});
+        } else if (tm && nbr >= 2)
             taa_pair2<true, 2><<<g2_h, blk_h, 0, hs(stream)>>>(dimg(target), dimg(current_color), dimg(previous_color),
                                                        dimg(current_velocity), dimg(previous_velocity), dimg(depth), vo, p, *tm);
         else if (tm && nbr == 0)

@@ -404,21 +404,27 @@ def test_taa(soc, oracle, W, H, inputs):
     assert np.array_equal(host(vout).view(np.uint16), gb["velocity"].view(np.uint16))
 
 
-@pytest.mark.parametrize("W,H", [(100, 40), (1920, 1080)])
+@pytest.mark.parametrize("W,H", [(100, 40), (102, 42), (1920, 1080)])
 def test_taa_lane_shift_neighbours_identical(soc, oracle, monkeypatch, W, H):
-    """Side columns of the 3x3 neighbourhood from the adjacent lanes (DPP wave shifts) give the bits of
-    the per-lane loads (SOC_TAA_NBR=0): with halo-only first / last lanes (2, default) and with edge-lane
-    loads (1). 100 px: 50 pairs in a 62-pair wave row (12 lanes past the image), 32-lane block rows of
-    which the second has 18 lanes inside; 1920 px: 15.5 wave rows."""
+    """Every neighbourhood source gives the bits of the per-lane loads (SOC_TAA_NBR=0): the LDS-staged tiles (3,
+    default), the side columns from the adjacent lanes (DPP wave shifts) with halo-only first / last lanes (2) and
+    with edge-lane loads (1). 100 px: 50 pairs in one 64-pair LDS tile row (14 lanes past the image) / a 62-pair
+    wave row (12 lanes past), 32-lane block rows of which the second has 18 lanes inside; 102 x 42: a partial last
+    depth quad (W % 4 == 2) and a last tile row with 2 of its 4 rows inside (H % 4 == 2); 1920 px: 15 LDS tiles,
+    15.5 wave rows."""
     g, gb = sponza_inputs(W, H)
     cur = dev(random_rgba16(H, W, seed=3, hi=3.0))
     prev = dev(random_rgba16(H, W, seed=4, hi=3.0))
     pvel = gb["velocity"].copy()
     pvel[..., :2] += np.float16(0.0015)
     vel, pvel, depth = dev(gb["velocity"]), dev(pvel), dev(gb["depth"])
+    if (W * 4) % 16:   # the LDS tiles stage 16-B depth quads: a row pitch padded to 16 B (rows may be padded)
+        dp = torch.zeros(H, W + 2, dtype=torch.float32, device=DEV)
+        dp[:, :W] = depth
+        depth = dp[:, :W]
     ae = soc.auto_exposure_buffer(exposure=0.37)
     outs = []
-    for nbr in ("2", "1", "0"):
+    for nbr in ("3", "2", "1", "0"):
         monkeypatch.setenv("SOC_TAA_NBR", nbr)
         soc.reload_tuning()
         t = torch.zeros(H, W, 4, dtype=torch.float16, device=DEV)
