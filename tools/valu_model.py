@@ -42,7 +42,10 @@ def main():
     kt_dir, vmix_dir = opt("--durations"), opt("--calibration")
     kt_durs = load(kt_dir)[1] if kt_dir else None
     out = {"model": {"valu_cycles_per_wave_instr": VALU_CYC, "trans_extra_cycles": TRANS_EXTRA, "simds": SIMDS,
-                     "clock_ghz": CLOCK_GHZ, "source": "tools/microbench/valu_mix.hip (8 waves/SIMD, full chip)"},
+                     "clock_ghz": CLOCK_GHZ, "source": "tools/microbench/valu_mix.hip (8 waves/SIMD, full chip)",
+                     "caveat": "a packed f32 op (v_pk_*_f32) counts as one instruction (~1.1x the issue time of v_fma_f32, "
+                               "tools/microbench/pk_rate.hip); integer / convert ops interleaved with f32 FMAs co-issue, so "
+                               "the 4-cycle cost is an average, not a hard bound (DESIGN.md 5.2)"},
            "runs": {}}
     if vmix_dir:   # valu_mix: 2048 blocks x 4 waves x 2048 iterations x 8 chains x per-iteration VALU ops per dispatch
         counters, _ = load(vmix_dir)
@@ -63,7 +66,7 @@ def main():
             durs = kt_durs
         rows = {}
         for k, c in counters.items():
-            if not any(t in k for t in ("clouds", "ssao", "composition_pair", "sky_compose", "taa_pair", "bloomw", "tonemap")):
+            if not any(t in k for t in ("clouds", "ssao", "composition_pair", "sky_compose", "taa_pair", "taa_lds", "bloomw", "tonemap")):
                 continue
             mean = {n: sum(v) / len(v) for n, v in c.items()}
             if "SQ_INSTS_VALU" not in mean or not durs.get(k):
