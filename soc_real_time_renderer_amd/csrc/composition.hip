@@ -40,20 +40,53 @@ __device__ __forceinline__ float fast_pow(float x, float y) {
     return __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x));
 }
 
+// The light loops are written once over a lane type T: float (one pixel) or f2v (the lane's two pixels as packed
+// f32 pairs, v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32), with the same operations in the same order, so both
+// forms give the same bits per pixel. The light records are wave-uniform scalars, broadcast into both halves.
+typedef float f2v __attribute__((ext_vector_type(2)));
+template <class T> struct V3 { T x, y, z; };
+__device__ __forceinline__ float bcv(float s, float) { return s; }
+__device__ __forceinline__ f2v bcv(float s, f2v) { return f2v{s, s}; }
+__device__ __forceinline__ float vfma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+__device__ __forceinline__ f2v vfma(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ float vrsq(float x) { return __builtin_amdgcn_rsqf(x); }
+__device__ __forceinline__ f2v vrsq(f2v x) { return f2v{__builtin_amdgcn_rsqf(x.x), __builtin_amdgcn_rsqf(x.y)}; }
+__device__ __forceinline__ float vsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+__device__ __forceinline__ f2v vsqrt(f2v x) { return f2v{__builtin_amdgcn_sqrtf(x.x), __builtin_amdgcn_sqrtf(x.y)}; }
+__device__ __forceinline__ float vexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ f2v vexp2(f2v x) { return f2v{__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)}; }
+__device__ __forceinline__ float vabs(float x) { return fabsf(x); }
+__device__ __forceinline__ f2v vabs(f2v x) { return f2v{fabsf(x.x), fabsf(x.y)}; }
+__device__ __forceinline__ float vmax0(float x) { return fmaxf(x, 0.0f); }
+__device__ __forceinline__ f2v vmax0(f2v x) { return f2v{fmaxf(x.x, 0.0f), fmaxf(x.y, 0.0f)}; }
+__device__ __forceinline__ float vclamp01(float x) { return clampf(x, 0.0f, 1.0f); }
+__device__ __forceinline__ f2v vclamp01(f2v x) { return f2v{clampf(x.x, 0.0f, 1.0f), clampf(x.y, 0.0f, 1.0f)}; }
+__device__ __forceinline__ float vneg_pi(float x, float r) { return x < 0.0f ? 3.14159265358979f - r : r; }
+__device__ __forceinline__ f2v vneg_pi(f2v x, f2v r) {
+    const f2v q = f2v{3.14159265358979f, 3.14159265358979f} - r;
+    return f2v{x.x < 0.0f ? q.x : r.x, x.y < 0.0f ? q.y : r.y};
+}
+__device__ __forceinline__ float vdiv(float a, float b) { return a / b; }
+__device__ __forceinline__ f2v vdiv(f2v a, float b) { return f2v{a.x / b, a.y / b}; }
+template <class T> __device__ __forceinline__ T vdot(const V3<T>& a, const V3<T>& b) {
+    return vfma(a.z, b.z, vfma(a.y, b.y, a.x * b.x));
+}
+
 // acos on the native units: Abramowitz & Stegun 4.4.46, acos(a) = sqrt(1 - a) * P7(a) for a in [0, 1]
 // (|error| <= 2e-8 rad), acos(x) = pi - acos(-x) below 0. Outside [-1, 1] the sqrt gives NaN, as acos does.
-__device__ __forceinline__ float acos_fast(float x) {
-    const float a = fabsf(x);
-    float r = -0.0012624911f;
-    r = __builtin_fmaf(r, a, 0.0066700901f);
-    r = __builtin_fmaf(r, a, -0.0170881256f);
-    r = __builtin_fmaf(r, a, 0.0308918810f);
-    r = __builtin_fmaf(r, a, -0.0501743046f);
-    r = __builtin_fmaf(r, a, 0.0889789874f);
-    r = __builtin_fmaf(r, a, -0.2145988016f);
-    r = __builtin_fmaf(r, a, 1.5707963050f);
-    r *= __builtin_amdgcn_sqrtf(1.0f - a);
-    return x < 0.0f ? 3.14159265358979f - r : r;
+template <class T>
+__device__ __forceinline__ T acos_fast(T x) {
+    const T a = vabs(x);
+    T r = bcv(-0.0012624911f, x);
+    r = vfma(r, a, bcv(0.0066700901f, x));
+    r = vfma(r, a, bcv(-0.0170881256f, x));
+    r = vfma(r, a, bcv(0.0308918810f, x));
+    r = vfma(r, a, bcv(-0.0501743046f, x));
+    r = vfma(r, a, bcv(0.0889789874f, x));
+    r = vfma(r, a, bcv(-0.2145988016f, x));
+    r = vfma(r, a, bcv(1.5707963050f, x));
+    r = r * vsqrt(bcv(1.0f, x) - a);
+    return vneg_pi(x, r);
 }
 
 // The light loops of composition.inl:124-160, per light: L = light - pos, one rsqrt gives light_dir and the
@@ -61,51 +94,64 @@ __device__ __forceinline__ float acos_fast(float x) {
 // units (acos_fast) and exp(-x^2) as a native exp2. The pixel's view_dir is hoisted out of the loop and the
 // frag_color (albedo) factor out of the sum. Within the RGBA16F tolerance of the oracle's libm restatement.
 // Light records are wave-uniform (scalar loads from the device globals).
-__device__ __forceinline__ f3 light_sum(const soc_globals* __restrict__ dg, uint32_t npl, uint32_t nsl, f3 n, f3 pos,
-                                        f3 cam) {
-    const f3 vd0 = cam - pos;
-    const f3 view_dir = vd0 * __builtin_amdgcn_rsqf(dot3(vd0, vd0));
-    f3 acc = f3{0.0f, 0.0f, 0.0f};
-    constexpr float kLog2e = 1.44269504088896f;
+template <class T>
+__device__ __forceinline__ V3<T> light_sum(const soc_globals* __restrict__ dg, uint32_t npl, uint32_t nsl, const V3<T>& n,
+                                           const V3<T>& pos, f3 cam) {
+    const T z = pos.x;   // lane-type witness for the broadcasts
+    const V3<T> vd0 = {bcv(cam.x, z) - pos.x, bcv(cam.y, z) - pos.y, bcv(cam.z, z) - pos.z};
+    const T vk = vrsq(vdot(vd0, vd0));
+    const V3<T> view_dir = {vd0.x * vk, vd0.y * vk, vd0.z * vk};
+    V3<T> acc = {bcv(0.0f, z), bcv(0.0f, z), bcv(0.0f, z)};
+    const T nlog2e = bcv(-1.44269504088896f, z);
+    auto shade_light = [&](const float* lp, T& inv, V3<T>& ld) {
+        const V3<T> l = {bcv(lp[0], z) - pos.x, bcv(lp[1], z) - pos.y, bcv(lp[2], z) - pos.z};
+        inv = vrsq(vdot(l, l));
+        ld = V3<T>{l.x * inv, l.y * inv, l.z * inv};
+        const V3<T> h = {ld.x + view_dir.x, ld.y + view_dir.y, ld.z + view_dir.z};
+        const T nh = acos_fast(vdot(h, n) * vrsq(vdot(h, h)));
+        const T diffuse = vmax0(vdot(n, ld));
+        return (diffuse + vexp2((nh * nh) * nlog2e)) * (inv * inv);
+    };
+    auto add = [&](const float* col, T s) {
+        acc = V3<T>{vfma(bcv(col[0], z), s, acc.x), vfma(bcv(col[1], z), s, acc.y), vfma(bcv(col[2], z), s, acc.z)};
+    };
 #pragma unroll 4
     for (uint32_t i = 0; i < npl; ++i) {            // calculate_point_light, :124-139
         const soc_point_light& L = dg->point_lights[i];
-        const f3 l = mk3(L.position[0], L.position[1], L.position[2]) - pos;
-        const float inv = __builtin_amdgcn_rsqf(dot3(l, l));
-        const f3 ld = l * inv;
-        const f3 h = ld + view_dir;
-        const float nh = acos_fast(dot3(h, n) * __builtin_amdgcn_rsqf(dot3(h, h)));
-        const float diffuse = fmaxf(dot3(n, ld), 0.0f);
-        const float s = (diffuse + __builtin_amdgcn_exp2f(-(nh * nh) * kLog2e)) * (inv * inv) * L.intensity;
-        acc = acc + mk3(L.color[0], L.color[1], L.color[2]) * s;
+        T inv;
+        V3<T> ld;
+        const T s = shade_light(L.position, inv, ld) * bcv(L.intensity, z);
+        add(L.color, s);
     }
 #pragma unroll 2
     for (uint32_t i = 0; i < nsl; ++i) {            // calculate_spot_light, :141-160
         const soc_spot_light& L = dg->spot_lights[i];
-        const f3 l = mk3(L.position[0], L.position[1], L.position[2]) - pos;
-        const float inv = __builtin_amdgcn_rsqf(dot3(l, l));
-        const f3 ld = l * inv;
-        const f3 sd = -mk3(L.direction[0], L.direction[1], L.direction[2]);
-        const float theta = dot3(ld, sd) * __builtin_amdgcn_rsqf(dot3(sd, sd));
-        const float intensity = clampf((theta - L.outer_cut_off) / (L.cut_off - L.outer_cut_off), 0.0f, 1.0f);
-        const f3 h = ld + view_dir;
-        const float nh = acos_fast(dot3(h, n) * __builtin_amdgcn_rsqf(dot3(h, h)));
-        const float diffuse = fmaxf(dot3(n, ld), 0.0f);
-        const float s =
-            (diffuse + __builtin_amdgcn_exp2f(-(nh * nh) * kLog2e)) * (inv * inv) * L.intensity * intensity;
-        acc = acc + mk3(L.color[0], L.color[1], L.color[2]) * s;
+        T inv;
+        V3<T> ld;
+        const T b = shade_light(L.position, inv, ld);
+        const float sdx = -L.direction[0], sdy = -L.direction[1], sdz = -L.direction[2];
+        const float sk = __builtin_amdgcn_rsqf(__builtin_fmaf(sdz, sdz, __builtin_fmaf(sdy, sdy, sdx * sdx)));
+        const T theta = vfma(ld.z, bcv(sdz, z), vfma(ld.y, bcv(sdy, z), ld.x * bcv(sdx, z))) * bcv(sk, z);
+        const T intensity = vclamp01(vdiv(theta - bcv(L.outer_cut_off, z), L.cut_off - L.outer_cut_off));
+        add(L.color, b * bcv(L.intensity, z) * intensity);
     }
     return acc;
 }
 
-// Shading of one pixel given its G-buffer values (composition.inl:164-224).
+// Shading of one pixel given its G-buffer values (composition.inl:164-224), in two parts around the light sum:
+// shade_pre (sun ESM shadow, emissive, AO) and shade_post (lights, ambient, albedo, AO, emissive).
 // The sun-space position is one projective transform of the NDC point: vs = inv_proj * ndc,
 // ws = inv_view * (vs / vs.w), sp = sun_pv * ws, and pc = sp.xyz / sp.w, so the vs.w division cancels
 // and sun_clip = sun_pv * inv_view * inv_proj (host fp32) gives pc directly (one rcp; within the
 // RGBA16F tolerance). The world position itself is only formed for the light loops.
-template <bool LIGHTS = true, typename ShadowImg = DImg>
-__device__ __forceinline__ f4 shade(const CompParams& p, float u, float v, float d, f3 albedo, f3 emissive, f3 n,
-                                    float ssao, const ShadowImg& shadow) {
+struct ShadePre {
+    float direct;   // the sun term dot(n, -sun) * shadow (grey)
+    float occl;
+    f3 em;
+};
+template <typename ShadowImg = DImg>
+__device__ __forceinline__ ShadePre shade_pre(const CompParams& p, float u, float v, float d, f3 emissive, f3 n, float ssao,
+                                              const ShadowImg& shadow) {
     const f4 ndc = f4{u * 2.0f - 1.0f, v * 2.0f - 1.0f, d, 1.0f};
     // sun ESM shadow, :166-173
     const f4 sp = mul(p.sun_clip, ndc);
@@ -117,23 +163,41 @@ __device__ __forceinline__ f4 shade(const CompParams& p, float u, float v, float
     float e = __expf(p.ef * (pcz - sd));
     if (p.df != 1.0f) e = fast_pow(e, p.df);   // pow(x, 1.0) == x exactly
     const float sun_shadow = clampf(e, 0.0f, 1.0f);
-
-    const f3 em = emissive * p.emissive_strength;
-    const float occl = fast_pow(ssao, p.ao_strength);
-    const float dd = fmaxf(0.0f, dot3(n, -mk3(p.sun_dir[0], p.sun_dir[1], p.sun_dir[2]))) * sun_shadow;
-    f3 direct = f3{dd, dd, dd};
-    if (LIGHTS && (p.npl | p.nsl)) {
-        // get_world_position_from_depth, :114-122
-        f4 vs = mul(p.inv_proj, ndc);
-        const float rw = __builtin_amdgcn_rcpf(vs.w);
-        vs = f4{vs.x * rw, vs.y * rw, vs.z * rw, 1.0f};
-        const f4 ws = mul(p.inv_view, vs);
-        const f3 wp = f3{ws.x, ws.y, ws.z};
-        const f3 cam = mk3(p.cam[0], p.cam[1], p.cam[2]);
-        direct = direct + albedo * light_sum(p.dg, p.npl, p.nsl, n, wp, cam);
-    }
-    const f3 c = (direct + mk3(p.ambient[0], p.ambient[1], p.ambient[2])) * albedo * occl + em;
+    ShadePre s;
+    s.em = emissive * p.emissive_strength;
+    s.occl = fast_pow(ssao, p.ao_strength);
+    s.direct = fmaxf(0.0f, dot3(n, -mk3(p.sun_dir[0], p.sun_dir[1], p.sun_dir[2]))) * sun_shadow;
+    return s;
+}
+// get_world_position_from_depth, :114-122
+__device__ __forceinline__ f3 world_pos(const CompParams& p, float u, float v, float d) {
+    const f4 ndc = f4{u * 2.0f - 1.0f, v * 2.0f - 1.0f, d, 1.0f};
+    f4 vs = mul(p.inv_proj, ndc);
+    const float rw = __builtin_amdgcn_rcpf(vs.w);
+    vs = f4{vs.x * rw, vs.y * rw, vs.z * rw, 1.0f};
+    const f4 ws = mul(p.inv_view, vs);
+    return f3{ws.x, ws.y, ws.z};
+}
+__device__ __forceinline__ f4 shade_post(const CompParams& p, const ShadePre& s, f3 albedo, const f3* lights) {
+    f3 direct = f3{s.direct, s.direct, s.direct};
+    if (lights)
+        direct = f3{__builtin_fmaf(albedo.x, lights->x, direct.x), __builtin_fmaf(albedo.y, lights->y, direct.y),
+                    __builtin_fmaf(albedo.z, lights->z, direct.z)};
+    const f3 c = (direct + mk3(p.ambient[0], p.ambient[1], p.ambient[2])) * albedo * s.occl + s.em;
     return f4{c.x, c.y, c.z, 1.0f};
+}
+template <bool LIGHTS = true, typename ShadowImg = DImg>
+__device__ __forceinline__ f4 shade(const CompParams& p, float u, float v, float d, f3 albedo, f3 emissive, f3 n,
+                                    float ssao, const ShadowImg& shadow) {
+    const ShadePre s = shade_pre(p, u, v, d, emissive, n, ssao, shadow);
+    if (LIGHTS && (p.npl | p.nsl)) {
+        const f3 wp = world_pos(p, u, v, d);
+        const V3<float> ls = light_sum(p.dg, p.npl, p.nsl, V3<float>{n.x, n.y, n.z}, V3<float>{wp.x, wp.y, wp.z},
+                                       mk3(p.cam[0], p.cam[1], p.cam[2]));
+        const f3 l3 = f3{ls.x, ls.y, ls.z};
+        return shade_post(p, s, albedo, &l3);
+    }
+    return shade_post(p, s, albedo, nullptr);
 }
 
 constexpr int BX = 64, BY = 4;
@@ -184,6 +248,11 @@ __global__ __launch_bounds__(256) void composition_pair(DImg target, DImg albedo
         const uint4 a4 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ba.r, buf_row(ba, y) + x * 8, 0, ld_aux));
         const uint4 e4 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(be.r, buf_row(be, y) + x * 8, 0, ld_aux));
         const uint4 n4 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(bn.r, buf_row(bn, y) + x * 8, 0, ld_aux));
+        // LIGHTS: the light sum of the lane's two pixels runs once, as packed pairs (light_sum<f2v>, the same bits per
+        // pixel as light_sum<float>); a sky pixel of the pair rides along in the other half and is discarded
+        ShadePre pre[2];
+        f3 alb[2], nrm[2], wps[2];
+        uint32_t lit = 0u;
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
             const float u = centre_uv_rn(x + k, target.w, p.rw);
@@ -192,6 +261,10 @@ __global__ __launch_bounds__(256) void composition_pair(DImg target, DImg albedo
             const f4 em = unpack_h4(k ? uint2{e4.z, e4.w} : uint2{e4.x, e4.y});
             const f4 nn = unpack_h4(k ? uint2{n4.z, n4.w} : uint2{n4.x, n4.y});
             f4 c;
+            if (LIGHTS) {   // the same pixel values for a sky pixel's discarded half
+                nrm[k] = f3{nn.x, nn.y, nn.z};
+                wps[k] = world_pos(p, u, v, d);
+            }
             if (d == 1.0f && p.sky_external) {   // the second lane writes it (sky_compose_pair)
                 own &= ~(1u << k);
                 continue;
@@ -201,9 +274,26 @@ __global__ __launch_bounds__(256) void composition_pair(DImg target, DImg albedo
                 c = f4{cl.x, cl.y, cl.z, 1.0f};
             } else {
                 const float ao = (SOC_COMP_PROFILE & 2) ? u : sample_r8(bo, u, v);
-                c = shade<LIGHTS>(p, u, v, d, f3{al.x, al.y, al.z}, f3{em.x, em.y, em.z}, f3{nn.x, nn.y, nn.z}, ao, bs);
+                if (LIGHTS) {
+                    pre[k] = shade_pre(p, u, v, d, f3{em.x, em.y, em.z}, f3{nn.x, nn.y, nn.z}, ao, bs);
+                    alb[k] = f3{al.x, al.y, al.z};
+                    lit |= 1u << k;
+                    continue;
+                }
+                c = shade<false>(p, u, v, d, f3{al.x, al.y, al.z}, f3{em.x, em.y, em.z}, f3{nn.x, nn.y, nn.z}, ao, bs);
             }
             outp[k] = pack_h4(c);
+        }
+        if (LIGHTS && lit) {
+            const V3<f2v> n2 = {f2v{nrm[0].x, nrm[1].x}, f2v{nrm[0].y, nrm[1].y}, f2v{nrm[0].z, nrm[1].z}};
+            const V3<f2v> w2 = {f2v{wps[0].x, wps[1].x}, f2v{wps[0].y, wps[1].y}, f2v{wps[0].z, wps[1].z}};
+            const V3<f2v> ls = light_sum(p.dg, p.npl, p.nsl, n2, w2, mk3(p.cam[0], p.cam[1], p.cam[2]));
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+                if (lit & (1u << k)) {
+                    const f3 l3 = k ? f3{ls.x.y, ls.y.y, ls.z.y} : f3{ls.x.x, ls.y.x, ls.z.x};
+                    outp[k] = pack_h4(shade_post(p, pre[k], alb[k], &l3));
+                }
         }
         const uint4 o = uint4{outp[0].x, outp[0].y, outp[1].x, outp[1].y};
         typedef uint32_t v4w __attribute__((ext_vector_type(4)));
