@@ -298,7 +298,7 @@ __device__ f3 atmosphere(f3 r, f3 r0, f3 pSun, float iTime) {
     p.y = fminf(p.y, rsi(r0, r, rPlanet).x);
     const float iStep = (p.y - p.x) / 16.0f;
     f3 totalRlh = f3{0, 0, 0}, totalMie = f3{0, 0, 0};
-    float iOdRlh = 0.0f, iOdMie = 0.0f;
+    f2v iOd = {0.0f, 0.0f};   // (Rayleigh, Mie) optical depth of the primary ray, one packed pair
     const float mu = dot3(r, pSun), mumu = mu * mu, gg = g0 * g0;
     const float pRlh = 3.0f / (16.0f * PI) * (1.0f + mumu);
     const float pMie = 3.0f / (8.0f * PI) * ((1.0f - gg) * (mumu + 1.0f)) / (powf(1.0f + gg - 2.0f * mu * g0, 1.5f) * (2.0f + gg));
@@ -311,15 +311,17 @@ __device__ f3 atmosphere(f3 r, f3 r0, f3 pSun, float iTime) {
         const f3 iPos = r0 + r * (iTime + iStep * 0.5f);
         const float A = dot3(iPos, iPos), PoD = dot3(iPos, pSun);
         const float iLen = __builtin_amdgcn_sqrtf(A);
-        const float odR = __builtin_amdgcn_exp2f(__builtin_fmaf(iLen, kR, cR)) * iStep;
-        const float odM = __builtin_amdgcn_exp2f(__builtin_fmaf(iLen, kM, cM)) * iStep;
-        iOdRlh += odR;
-        iOdMie += odM;
+        // (odR, odM) and the accumulators as packed pairs: element-wise the scalar operations (the same bits)
+        const f2v ea = pfma(f2v{iLen, iLen}, f2v{kR, kM}, f2v{cR, cM});
+        const f2v od = f2v{__builtin_amdgcn_exp2f(ea.x), __builtin_amdgcn_exp2f(ea.y)} * f2v{iStep, iStep};
+        const float odR = od.x, odM = od.y;
+        iOd = iOd + od;
         // rsi(iPos, pSun, rAtmos).y (:97-106); the secondary ray starts inside the atmosphere
         float delta = PoD * PoD + rAtmos * rAtmos - A;
         const float jStep = (delta < 0.0f ? -1.0f : -PoD + __builtin_amdgcn_sqrtf(delta)) / 8.0f;
         const float B = 2.0f * PoD, half = jStep * 0.5f;
-        float jTime = 0.0f, jOdR = 0.0f, jOdM = 0.0f;
+        float jTime = 0.0f;
+        f2v jOd = {0.0f, 0.0f};   // (Rayleigh, Mie) optical depth of the secondary ray
         // two secondary steps per packed instruction (v_pk_fma_f32 / v_pk_add_f32), element-wise the same
         // operations, and the same sequential jTime and accumulation chains: the same bits
 #pragma unroll 2
@@ -329,14 +331,13 @@ __device__ f3 atmosphere(f3 r, f3 r0, f3 pSun, float iTime) {
             const f2v q = pfma(t, pfma(t, f2v{C2, C2}, f2v{B, B}), f2v{A, A});
             const f2v len = {__builtin_amdgcn_sqrtf(q.x), __builtin_amdgcn_sqrtf(q.y)};
             const f2v eR = pfma(len, f2v{kR, kR}, f2v{cR, cR}), eM = pfma(len, f2v{kM, kM}, f2v{cM, cM});
-            jOdR = __builtin_fmaf(__builtin_amdgcn_exp2f(eR.x), jStep, jOdR);
-            jOdM = __builtin_fmaf(__builtin_amdgcn_exp2f(eM.x), jStep, jOdM);
-            jOdR = __builtin_fmaf(__builtin_amdgcn_exp2f(eR.y), jStep, jOdR);
-            jOdM = __builtin_fmaf(__builtin_amdgcn_exp2f(eM.y), jStep, jOdM);
+            jOd = pfma(f2v{__builtin_amdgcn_exp2f(eR.x), __builtin_amdgcn_exp2f(eM.x)}, f2v{jStep, jStep}, jOd);
+            jOd = pfma(f2v{__builtin_amdgcn_exp2f(eR.y), __builtin_amdgcn_exp2f(eM.y)}, f2v{jStep, jStep}, jOd);
             jTime = jT1 + jStep;
         }
-        const float fm = kMie * (iOdMie + jOdM);
-        const float fr = iOdRlh + jOdR;
+        const f2v od_sum = iOd + jOd;
+        const float fm = kMie * od_sum.y;
+        const float fr = od_sum.x;
         const f3 attn = f3{__expf(-(fm + kRlh.x * fr)), __expf(-(fm + kRlh.y * fr)), __expf(-(fm + kRlh.z * fr))};
         totalRlh = totalRlh + attn * odR;
         totalMie = totalMie + attn * odM;

@@ -2,7 +2,8 @@
 
   python tools/timeline.py <run_kernel_trace.csv>           one frame (start/end us relative to the frame's first bloom
                                                              kernel, queue id)
-  python tools/timeline.py --lanes <run_kernel_trace.csv>   the timed frames (the longest run of frame periods < 1 ms):
+  python tools/timeline.py --lanes <run_kernel_trace.csv>   the timed frames (the longest run of frame periods within 1.5x of the
+                                                             lower-quartile period):
                                                              per queue, busy time, the gaps between consecutive kernels
                                                              and each kernel's time, per frame
 """
@@ -30,10 +31,11 @@ def lanes(rows):
     idx = [i for i, r in enumerate(rows) if "bloomw_down01" in r["Kernel_Name"]]
     st = [int(rows[i]["Start_Timestamp"]) for i in idx]
     d = [(b - a) / 1e3 for a, b in zip(st, st[1:])]
+    lim = 1.5 * sorted(d)[len(d) // 4]   # the timed loop's periods sit near the short end; warm-up / profile frames do not
     best, i = (0, 0), 0
     while i < len(d):
         j = i
-        while j < len(d) and d[j] < 1000:
+        while j < len(d) and d[j] < lim:
             j += 1
         if j - i > best[1] - best[0]:
             best = (i, j)
