@@ -692,15 +692,11 @@ __global__ __launch_bounds__(kSunvisThreads) __attribute__((amdgpu_waves_per_eu(
     }
 }
 
-// INLINE = false: the batches whose dense steps went through the pair lists (all of them unless a batch overflowed the
-// pair capacity), without the noise table in LDS and with the registers of the accumulation only (more resident waves
-// for this latency-bound pass); INLINE = true: the overflowed batches' single-lane march (a second launch that skips
-// every other batch). The two launches write disjoint pixels.
-template <bool NOISE_R8, bool INLINE>
+template <bool NOISE_R8>
 __global__ __launch_bounds__(256) void clouds_resolve(DImg noise, DImg target, CloudParams p, const uint32_t* __restrict__ counter,
                                                       const uint32_t* __restrict__ list, const float4* __restrict__ atmos,
                                                       PairBufs pb) {
-    __shared__ uint32_t quads[INLINE ? kTable : 1];
+    __shared__ uint32_t quads[kTable];
     __shared__ uint32_t offs[25][4];
     const uint32_t count = *counter;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -708,21 +704,17 @@ __global__ __launch_bounds__(256) void clouds_resolve(DImg noise, DImg target, C
     const f3 sun = f3{p.sun[0], p.sun[1], p.sun[2]}, sun_color = f3{0.8f, 0.8f, 0.8f};
     const f3 skyl = sky_light(sun);
     uint32_t dummy = 0;
-    bool staged = false;
     for (uint32_t first = blockIdx.x * 256u; first < count; first += gridDim.x * 256u) {
-        const uint32_t base = pb.batch_base[first >> 8];   // workgroup-uniform
-        const bool inl = (base & kInline) != 0u;
-        if (inl != INLINE) continue;
         const uint32_t i = first + tid;
         const bool valid = i < count;
         const uint32_t flagged = valid ? pb.pix_mask[i] : 0u;
         const uint32_t mask = flagged & ~kInline;
-        if (INLINE) {   // the single-lane march of an overflowed batch needs the noise in LDS
-            if (!staged) {
-                stage_noise<NOISE_R8>(noise, quads, tid, 256);
-                __syncthreads();
-                staged = true;
-            }
+        const uint32_t base = pb.batch_base[first >> 8];   // workgroup-uniform
+        const bool inl = (base & kInline) != 0u;
+        // the single-lane march of an overflowed batch needs the noise in LDS
+        if (inl) {
+            stage_noise<NOISE_R8>(noise, quads, tid, 256);
+            __syncthreads();
         } else {
             batch_slots(mask, lane, wave, offs, dummy, tid);   // the slot layout of clouds_density
         }
@@ -736,7 +728,7 @@ __global__ __launch_bounds__(256) void clouds_resolve(DImg noise, DImg target, C
         }
         const int x = (int)(e & 0xffffu), y = (int)(e >> 16);
         if (SOC_CLOUDS_PROFILE == 1) {
-        } else if (INLINE) {
+        } else if (inl) {
             if (valid) {
                 Ctx cx;
                 cx.quads = quads;
@@ -770,7 +762,7 @@ __global__ __launch_bounds__(256) void clouds_resolve(DImg noise, DImg target, C
             color = color * p.sun_factor;
             row_ptr_w<uint32_t>(target, y)[x] = pack_unorm8x4(f4{color.x, color.y, color.z, 1.0f});
         }
-        if (!INLINE) __syncthreads();   // offs is reused next round
+        __syncthreads();   // offs / quads are reused next round
     }
 }
 
@@ -889,13 +881,12 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
     clouds_classify<<<dim3(ceil_div(W, 64), ceil_div(H, 16)), 256, 0, s>>>(dimg(depth), dimg(target), p, vec_store, counter, list);
     // One resident wave set per kernel, grid-stride over the list / pairs: the long per-item work is
     // balanced over all SIMDs instead of running as a second, partially filled round.
-    static int res_atmos = 0, res_density = 0, res_sunvis = 0, res_resolve = 0, res_resolve_inl = 0;
+    static int res_atmos = 0, res_density = 0, res_sunvis = 0, res_resolve = 0;
     if (!res_atmos) {
         res_atmos = resident_blocks(clouds_atmosphere);
         res_density = resident_blocks(clouds_density<false>);
         res_sunvis = resident_blocks(clouds_sunvis<false, 512, true>, 512);
-        res_resolve = resident_blocks(clouds_resolve<false, false>);
-        res_resolve_inl = resident_blocks(clouds_resolve<false, true>);
+        res_resolve = resident_blocks(clouds_resolve<false>);
     }
     const long long blocks = ((long long)W * H + 255) / 256;
     if (SOC_CLOUDS_PROFILE >= 4) return check_launch("cloud_rendering");
@@ -906,13 +897,11 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
     if (r8) {
         clouds_density<true><<<density_grid, 256, 0, s>>>(nz, p, counter, list, ws.pb);
         clouds_sunvis<true, 512, true><<<grid(res_sunvis, blocks), 512, 0, s>>>(nz, p, list, ws.pb);
-        clouds_resolve<true, false><<<grid(res_resolve, blocks), 256, 0, s>>>(nz, tg, p, counter, list, ws.atmos, ws.pb);
-        clouds_resolve<true, true><<<grid(res_resolve_inl, blocks), 256, 0, s>>>(nz, tg, p, counter, list, ws.atmos, ws.pb);
+        clouds_resolve<true><<<grid(res_resolve, blocks), 256, 0, s>>>(nz, tg, p, counter, list, ws.atmos, ws.pb);
     } else {
         clouds_density<false><<<density_grid, 256, 0, s>>>(nz, p, counter, list, ws.pb);
         clouds_sunvis<false, 512, true><<<grid(res_sunvis, blocks), 512, 0, s>>>(nz, p, list, ws.pb);
-        clouds_resolve<false, false><<<grid(res_resolve, blocks), 256, 0, s>>>(nz, tg, p, counter, list, ws.atmos, ws.pb);
-        clouds_resolve<false, true><<<grid(res_resolve_inl, blocks), 256, 0, s>>>(nz, tg, p, counter, list, ws.atmos, ws.pb);
+        clouds_resolve<false><<<grid(res_resolve, blocks), 256, 0, s>>>(nz, tg, p, counter, list, ws.atmos, ws.pb);
     }
     return check_launch("cloud_rendering");
 }
