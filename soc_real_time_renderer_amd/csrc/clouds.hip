@@ -891,16 +891,27 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
     const long long blocks = ((long long)W * H + 255) / 256;
     if (SOC_CLOUDS_PROFILE >= 4) return check_launch("cloud_rendering");
     auto grid = [&](int res, long long items_blocks) { return (int)std::max(1LL, std::min<long long>(res, items_blocks)); };
-    clouds_atmosphere<<<grid(res_atmos, blocks), 256, 0, s>>>(p, counter, list, ws.atmos);
+    // Position of the atmosphere kernel in the lane (it feeds only the resolve): before the density march (0), before
+    // the sun visibility (1) or after it (2). Default: after it above 1440p (C3 +0.7 %, C4 +5 % at 3840x2160: the
+    // atmosphere's long transcendental run then overlaps the frame's TAA instead of its SSAO), first otherwise (C2
+    // 1920x1080 -5 % after it); the same bits in every position (profiles/r03_ab_atmos_pos.txt, GPU identity test).
+    const int apos_knob = tuning_knob("SOC_CLOUDS_ATMOS_POS", -1);
+    const int apos = apos_knob >= 0 ? apos_knob : ((long long)W * H > 2560LL * 1440LL ? 2 : 0);
+    auto atmos = [&]() { clouds_atmosphere<<<grid(res_atmos, blocks), 256, 0, s>>>(p, counter, list, ws.atmos); };
+    if (apos == 0) atmos();
     const DImg nz = dimg(noise), tg = dimg(target);
     const int density_grid = std::min(grid(res_density, blocks), (int)ws.pb.od_blocks);   // one od scratch per workgroup
     if (r8) {
         clouds_density<true><<<density_grid, 256, 0, s>>>(nz, p, counter, list, ws.pb);
+        if (apos == 1) atmos();
         clouds_sunvis<true, 512, true><<<grid(res_sunvis, blocks), 512, 0, s>>>(nz, p, list, ws.pb);
+        if (apos == 2) atmos();
         clouds_resolve<true><<<grid(res_resolve, blocks), 256, 0, s>>>(nz, tg, p, counter, list, ws.atmos, ws.pb);
     } else {
         clouds_density<false><<<density_grid, 256, 0, s>>>(nz, p, counter, list, ws.pb);
+        if (apos == 1) atmos();
         clouds_sunvis<false, 512, true><<<grid(res_sunvis, blocks), 512, 0, s>>>(nz, p, list, ws.pb);
+        if (apos == 2) atmos();
         clouds_resolve<false><<<grid(res_resolve, blocks), 256, 0, s>>>(nz, tg, p, counter, list, ws.atmos, ws.pb);
     }
     return check_launch("cloud_rendering");

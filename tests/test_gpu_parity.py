@@ -514,20 +514,26 @@ def test_clouds(soc, oracle, W, H, pitch, inputs, compact):
 
 
 @pytest.mark.parametrize("W,H,pitch,all_sky", [(320, 180, 0.35, False), (1920, 1080, 0.35, False), (256, 144, 0.9, True)])
-def test_clouds_pair_path_equals_single_lane(soc, W, H, pitch, all_sky):
+def test_clouds_pair_path_equals_single_lane(soc, monkeypatch, W, H, pitch, all_sky):
     """The workspace path (classify, atmosphere, density / sunvis / resolve over dense-step pairs) gives
     the single-lane kernel's bits: od and vis are evaluated at the same positions with the same
-    additions and accumulated in the same order. An all-sky frame overflows the pair lists (2 pairs per
-    image pixel) and exercises the per-batch single-lane fallback."""
+    additions and accumulated in the same order, with the atmosphere kernel in any of its positions in the lane
+    (SOC_CLOUDS_ATMOS_POS 0 / 1 / 2). An all-sky frame overflows the pair lists (2 pairs per image pixel) and
+    exercises the per-batch single-lane fallback."""
     g, gb = sponza_inputs(W, H, camera=((-14.0, 2.2, 0.3), (0.0, pitch, 0.0)), elapsed=10.0)
     depth = np.ones_like(gb["depth"]) if all_sky else gb["depth"]
     a = torch.zeros(H, W, 4, dtype=torch.uint8, device=DEV)
-    b = torch.zeros_like(a)
     ws = soc.cloud_rendering_workspace(W, H)
     soc.cloud_rendering(g, dev(depth), dev(gb["noise"]), a, None)
-    soc.cloud_rendering(g, dev(depth), dev(gb["noise"]), b, ws)
-    torch.cuda.synchronize()
-    assert torch.equal(a, b), (a != b).float().mean().item()
+    for pos in ("0", "1", "2"):
+        monkeypatch.setenv("SOC_CLOUDS_ATMOS_POS", pos)
+        soc.reload_tuning()
+        b = torch.zeros_like(a)
+        soc.cloud_rendering(g, dev(depth), dev(gb["noise"]), b, ws)
+        torch.cuda.synchronize()
+        assert torch.equal(a, b), (pos, (a != b).float().mean().item())
+    monkeypatch.delenv("SOC_CLOUDS_ATMOS_POS")
+    soc.reload_tuning()
 
 
 # ------------------------------------------------------------------------------------------------ full frame
