@@ -381,6 +381,14 @@ def main():
         return {"serial_us": round(us * 1e3, 2), "serial_frac": round(algo[n] / (us * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)} \
             if us else {}
 
+    def pair_serial():
+        # the pair with each kernel alone on the GPU (the serial per-pass loop), beside the in-frame figure above
+        us = [ms_pass.get(n) for n in (comp, "SSAOGeneration")]
+        if not all(us):
+            return {}
+        t = sum(us) * 1e3
+        return {"serial_us": round(t, 2), "serial_frac": round(ns_bytes / (t * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+
     if world > 1:
         dist.barrier()
     if rank != 0:
@@ -421,6 +429,7 @@ def main():
                      "traffic": pair_traffic, "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": int(ns_bytes), "avg_launch_us": round(ns_us, 2),
                      "target_us_at_60pct": round(ns_bytes / (0.6 * HBM_PEAK_GBS * 1e9) * 1e6, 2),
+                     **pair_serial(),
                      "per_kernel": {
                          comp: {"achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
                                 "traffic": traffic, "algorithmic_bytes_per_launch": int(algo[comp]),
