@@ -232,8 +232,8 @@ def build_inputs(config, scene_name, W, H, rank, device, mips=True):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--config", choices=("c2", "c3", "c3b", "c4"), default="c3",
                     help="c3: Sponza-proxy full chain at 4K (the metric's config); c3b: C3 with 128 point lights fed "
                          "through the ECS scene feed (SURVEY.md §8d); c2: the same scene at 1920x1080 "
