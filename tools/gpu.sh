@@ -8,7 +8,7 @@
 #   tools/gpu.sh ab "K=V,K2=V2" "" "--flag,K=V" ... -- [bench args]
 #                                               the bench line under variants: K=V items are environment
 #                                               variables, "-..." items extra bench arguments ("" = none)
-#   tools/gpu.sh kt TAG [bench args]            rocprofv3 --kernel-trace --stats of a short bench run (top kernels)
+#   tools/gpu.sh kt TAG [bench args]            rocprofv3 --kernel-trace --stats of the default bench run (top kernels)
 #   tools/gpu.sh pmc TAG "<counters>" ... [-- bench args]
 #                                               one rocprofv3 --pmc pass per counter group (kernel trace only) + summary
 #   tools/gpu.sh traffic TAG [bench args]       FETCH_SIZE / WRITE_SIZE passes -> per-kernel HBM traffic table
@@ -29,7 +29,7 @@ bench_line() {   # name, bench args...
 kernel_trace() {   # tag, bench args...
   local t=$1; shift
   rm -rf gpurun_out/${t}_kt
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${t}_kt -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline "$@" > gpurun_out/${t}_kt.log 2>&1 || { echo "kernel trace failed"; tail -5 gpurun_out/${t}_kt.log; exit 1; }
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${t}_kt -o run -- python bench.py --no-cpu-baseline "$@" > gpurun_out/${t}_kt.log 2>&1 || { echo "kernel trace failed"; tail -5 gpurun_out/${t}_kt.log; exit 1; }
   local f; f=$(find gpurun_out/${t}_kt -name "*kernel_stats.csv" | head -1); cp "$f" gpurun_out/${t}_kernel_stats.csv
   python - "$t" <<'PY'
 import csv, sys

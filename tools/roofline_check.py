@@ -4,7 +4,8 @@ same configuration (`bench.py --steps K --warmup W`: W warm-up frames, K timed f
 profile frames) and averages each kernel over its timed launches only, so both numbers describe the same kind of
 launch. The kernel trace's own `--stats` average mixes the three segments.
 
-usage: python tools/roofline_check.py BENCH_JSON KT_DIR [--warmup 5] [--steps 20] > profiles/<tag>_roofline_check.json
+usage: python tools/roofline_check.py BENCH_JSON KT_DIR [--warmup W] [--steps K] > profiles/<tag>_roofline_check.json
+(W and K default to the bench line's own, i.e. a kernel trace of the same command)
 """
 import csv
 import glob
@@ -17,7 +18,7 @@ KERNELS = {"SSAOGeneration": "ssao_lds_kernel", "Composition+GenerateLuminanceHi
 
 def main():
     args = sys.argv[1:]
-    warmup, steps = 5, 20
+    warmup = steps = None
     if "--warmup" in args:
         i = args.index("--warmup")
         warmup = int(args[i + 1])
@@ -28,6 +29,8 @@ def main():
         del args[i:i + 2]
     bench_json, kt_dir = args
     line = json.load(open(bench_json))
+    warmup = line["warmup"] if warmup is None else warmup
+    steps = line["steps"] if steps is None else steps
     trace = glob.glob(os.path.join(kt_dir, "**", "*kernel_trace.csv"), recursive=True)[0]
     rows = sorted(csv.DictReader(open(trace)), key=lambda r: int(r["Start_Timestamp"]))
     out = {"bench_line": bench_json, "kernel_trace": trace, "warmup": warmup, "timed": steps, "kernels": {}}
