@@ -183,6 +183,11 @@ const char* soc_last_error_string(void);
  * this drops the cache so the current environment applies to the next launches. */
 void soc_tuning_reload(void);
 const char* soc_device_arch(void);                                   /* "gfx950" the kernels were built for */
+/* Launch geometry (no GPU needed): SOC_OK when a block of bx x by x bz lanes fits a kernel whose flat work-group bound
+ * (__launch_bounds__) is `bound`, else SOC_E_INVALID_ARG with the reason. Every launcher in the library applies the
+ * same check with its kernel's own bound before the launch, so a block over the bound is never issued (it would fail
+ * on the device as an "unspecified launch failure"). */
+int soc_check_block_shape(int32_t bound, int32_t bx, int32_t by, int32_t bz);
 
 /* --- Host-side globals feed (native C++, no GPU needed) ----------------------------------------- */
 /* Renderer defaults: renderer.cpp:72-133 (terrain, ssao, composition, dof, auto exposure incl. the

@@ -25,6 +25,7 @@ _FUNCS = {
     "soc_oracle_bloom_downsample": (C.c_int, [_G, _IMG, _IMG]),
     "soc_oracle_bloom_upsample": (C.c_int, [_G, _IMG, _IMG]),
     "soc_oracle_ssao_generation": (C.c_int, [_G, _IMG, _IMG, _IMG]),
+    "soc_oracle_ssao_generation_rv": (C.c_int, [_G, _IMG, _IMG, C.c_void_p, _IMG]),
     "soc_oracle_ssao_blur": (C.c_int, [_G, _IMG, _IMG]),
     "soc_oracle_cloud_rendering": (C.c_int, [_G, _IMG, _IMG, _IMG]),
     "soc_oracle_composition": (C.c_int, [_G] + [_IMG] * 8),
@@ -99,6 +100,15 @@ def ssao_generation(g, depth, normal, target):
     _rc(lib().soc_oracle_ssao_generation(C.byref(g), _img(depth), _img(normal), _img(target)), "ssao_generation")
 
 
+def ssao_generation_rv(g, depth, normal, rv_table, target):
+    """ssao_generation with the per-pixel random vectors of `rv_table` ((H/2, W/2, 2) or flat float32) instead of the
+    Q8 hash."""
+    t = np.ascontiguousarray(np.asarray(rv_table, np.float32))
+    assert t.size == 2 * target.shape[0] * target.shape[1]
+    _rc(lib().soc_oracle_ssao_generation_rv(C.byref(g), _img(depth), _img(normal), t.ctypes.data, _img(target)),
+        "ssao_generation_rv")
+
+
 def ssao_blur(g, ssao, target):
     _rc(lib().soc_oracle_ssao_blur(C.byref(g), _img(ssao), _img(target)), "ssao_blur")
 
@@ -107,10 +117,15 @@ def cloud_rendering(g, depth, noise, target):
     _rc(lib().soc_oracle_cloud_rendering(C.byref(g), _img(depth), _img(noise), _img(target)), "cloud_rendering")
 
 
+CLOUD_COUNTERS = ("sky_pixels", "dense_steps", "get_clouds", "noise_taps", "get_clouds_full", "atmosphere_full",
+                  "cloud_marches", "pixels")
+
+
 def clouds_counters():
-    a = (C.c_uint64 * 4)()
+    """Tallies of the last cloud_rendering call, as a dict (names: CLOUD_COUNTERS; soc_oracle.h)."""
+    a = (C.c_uint64 * len(CLOUD_COUNTERS))()
     lib().soc_oracle_clouds_counters(a)
-    return [int(v) for v in a]
+    return dict(zip(CLOUD_COUNTERS, (int(v) for v in a)))
 
 
 def composition(g, target, albedo, emissive, normal, depth, ssao, shadow, clouds):

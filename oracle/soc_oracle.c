@@ -440,7 +440,9 @@ static inline v3 view_position_from_depth(const float* inv_proj, v2 uv, float de
     return V3(v.x / v.w, v.y / v.w, v.z / v.w);
 }
 
-int soc_oracle_ssao_generation(const soc_globals* g, soc_img depth, soc_img normal, soc_img target) {
+/* rv_table: NULL (the reference's random vector, :184-188) or a (target.width x target.height) table of (x, y) random
+   vectors to use instead (the conditional parity check: the GPU's table, i.e. the oracle's taps given the GPU's Q8 hash). */
+static int ssao_generation(const soc_globals* g, soc_img depth, soc_img normal, soc_img target, const float* rv_table) {
     if (!g || !valid(&depth) || !valid(&normal) || !valid(&target) || depth.format != SOC_FMT_D32F ||
         normal.format != SOC_FMT_RGBA16F || target.format != SOC_FMT_R8_UNORM)
         return SOC_E_INVALID_ARG;
@@ -459,10 +461,16 @@ int soc_oracle_ssao_generation(const soc_globals* g, soc_img depth, soc_img norm
             v4 nn = sample_clamp(&normal, uv.x, uv.y);
             v3 n = mat3of4_mul_v3(V, normalize3(V3(nn.x, nn.y, nn.z)));
             /* random_vec, :184-188 */
-            float n1 = ssao_noise(uv, (float)(ndx * 2));
-            v2 puv = V2(powf(uv.x, 1.1f), powf(uv.y, 1.1f));
-            float n2 = ssao_noise(puv, powf((float)ndx * 4.2f, 1.5f + uv.x / 10.0f));
-            v3 rv = normalize3(V3(n1, n2, 0.0f));
+            v3 rv;
+            if (rv_table) {
+                const float* e = rv_table + 2 * ((size_t)y * (size_t)target.width + (size_t)x);
+                rv = V3(e[0], e[1], 0.0f);
+            } else {
+                float n1 = ssao_noise(uv, (float)(ndx * 2));
+                v2 puv = V2(powf(uv.x, 1.1f), powf(uv.y, 1.1f));
+                float n2 = ssao_noise(puv, powf((float)ndx * 4.2f, 1.5f + uv.x / 10.0f));
+                rv = normalize3(V3(n1, n2, 0.0f));
+            }
             v3 t = normalize3(sub3(rv, muls3(n, dot3(rv, n))));
             v3 b = cross3(t, n);
             float occ = 0.0f;
@@ -483,6 +491,16 @@ int soc_oracle_ssao_generation(const soc_globals* g, soc_img depth, soc_img norm
         }
     }
     return SOC_OK;
+}
+
+int soc_oracle_ssao_generation(const soc_globals* g, soc_img depth, soc_img normal, soc_img target) {
+    return ssao_generation(g, depth, normal, target, NULL);
+}
+
+int soc_oracle_ssao_generation_rv(const soc_globals* g, soc_img depth, soc_img normal, const float* rv_table,
+                                  soc_img target) {
+    if (!rv_table) return SOC_E_INVALID_ARG;
+    return ssao_generation(g, depth, normal, target, rv_table);
 }
 
 int soc_oracle_ssao_blur(const soc_globals* g, soc_img ssao, soc_img target) {
@@ -776,7 +794,9 @@ int soc_oracle_tone_mapping(const soc_globals* g, soc_img color, const soc_auto_
 typedef struct {
     const soc_img* noise;
     const soc_globals* g;
-    uint64_t* counters; /* per-thread: [0] sky px, [1] dense steps, [2] get_clouds, [3] noise taps */
+    uint64_t* counters; /* per-thread tallies (tools/clouds_flops.py): [0] sky px, [1] dense steps, [2] get_clouds,
+                           [3] noise taps, [4] get_clouds past the altitude test, [5] full atmosphere evaluations (not
+                           the early exit of :359), [6] cloud marches (ray_direction.y >= 0, :311) */
 } cloud_ctx;
 
 static inline float bayer2(v2 a) {
@@ -814,6 +834,7 @@ static float get_clouds(cloud_ctx* cx, v3 p) {
     p.x += cx->g->camera_position[0];
     p.z += cx->g->camera_position[2];
     if (p.y < CL_MIN_H || p.y > CL_MAX_H) return 0.0f;
+    cx->counters[4]++;
     float time = -1.0f * 0.02f * cx->g->elapsed_time;
     v3 mv = V3(time, 0.0f, time);
     v3 cc = add3(muls3(p, 0.001f), mv);
@@ -874,6 +895,7 @@ static v3 volumetric_clouds(cloud_ctx* cx, v3 dir, v3 sun, v3 color, float dithe
     const int steps = 24;
     const float iSteps = 1.0f / (float)steps;
     if (dir.y < 0.0f) return color;
+    cx->counters[6]++;
     const float pi = acosf(-1.0f), rPi = 1.0f / pi, hPi = pi * 0.5f, rLOG2 = 1.0f / logf(2.0f);
     v3 c0 = muls3(V3(0.0f, 1.0f, 0.0f), CL_EARTH_RADIUS);
     float bottom = rsi(c0, dir, CL_EARTH_RADIUS + CL_MIN_H).y;
@@ -907,12 +929,13 @@ static v3 volumetric_clouds(cloud_ctx* cx, v3 dir, v3 sun, v3 color, float dithe
     return mix3(lit, color, clampf(length3(start) * 0.00001f * 2.5f, 0.0f, 1.0f));
 }
 
-static v3 atmosphere(const soc_globals* g, v3 r, v3 r0, v3 pSun, float iSun, float rPlanet, float rAtmos, v3 kRlh,
+static v3 atmosphere(cloud_ctx* cx, const soc_globals* g, v3 r, v3 r0, v3 pSun, float iSun, float rPlanet, float rAtmos, v3 kRlh,
                      float kMie, float shRlh, float shMie, float gg0) {
     const float PI = 3.141592f;
     r = normalize3(r);
     v2 p = rsi(r0, r, rAtmos);
     if (p.x > p.y) return V3(0, 0, 0);
+    cx->counters[5]++;
     p.y = fminf(p.y, rsi(r0, r, rPlanet).x);
     float iStepSize = (p.y - p.x) / 16.0f;
     float iTime = g->elapsed_time; /* quirk Q10 */
@@ -951,9 +974,11 @@ static v3 atmosphere(const soc_globals* g, v3 r, v3 r0, v3 pSun, float iSun, flo
     return muls3(add3(a, b), iSun);
 }
 
-static uint64_t g_cloud_counters[4];
+static uint64_t g_cloud_counters[SOC_ORACLE_CLOUD_COUNTERS];
 
-void soc_oracle_clouds_counters(uint64_t out[4]) { memcpy(out, g_cloud_counters, sizeof g_cloud_counters); }
+void soc_oracle_clouds_counters(uint64_t out[SOC_ORACLE_CLOUD_COUNTERS]) {
+    memcpy(out, g_cloud_counters, sizeof g_cloud_counters);
+}
 
 int soc_oracle_cloud_rendering(const soc_globals* g, soc_img depth, soc_img noise, soc_img target) {
     if (!g || !valid(&depth) || !valid(&noise) || !valid(&target)) return SOC_E_INVALID_ARG;
@@ -962,10 +987,10 @@ int soc_oracle_cloud_rendering(const soc_globals* g, soc_img depth, soc_img nois
     const v3 sun = V3(-g->sun_info.direction[0], -g->sun_info.direction[1], -g->sun_info.direction[2]);
     const v3 r0 = V3(0.0f + g->camera_position[0], 6372e3f + g->camera_position[1], 0.0f + g->camera_position[2]);
     const float sun_factor = fmaxf(fminf(fabsf(sun.x), fabsf(sun.z)) + sun.y, 0.0f);
-    uint64_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
-#pragma omp parallel for schedule(dynamic, 2) reduction(+ : c0, c1, c2, c3)
+    uint64_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, c4 = 0, c5 = 0, c6 = 0;
+#pragma omp parallel for schedule(dynamic, 2) reduction(+ : c0, c1, c2, c3, c4, c5, c6)
     for (int y = 0; y < H; ++y) {
-        uint64_t cnt[4] = {0, 0, 0, 0};
+        uint64_t cnt[SOC_ORACLE_CLOUD_COUNTERS] = {0};
         cloud_ctx cx = {&noise, g, cnt};
         for (int x = 0; x < W; ++x) {
             v2 ruv = V2((float)x / ((float)g->resolution[0] - 1.0f), (float)y / ((float)g->resolution[1] - 1.0f));
@@ -978,16 +1003,17 @@ int soc_oracle_cloud_rendering(const soc_globals* g, soc_img depth, soc_img nois
             if (d == 1.0f) {
                 cnt[0]++;
                 float dither = bayer16(V2((float)x, (float)y));
-                color = atmosphere(g, dir, r0, sun, 22.0f, 6371e3f, 6471e3f, V3(5.5e-6f, 13.0e-6f, 22.4e-6f), 21e-6f, 8e3f,
+                color = atmosphere(&cx, g, dir, r0, sun, 22.0f, 6371e3f, 6471e3f, V3(5.5e-6f, 13.0e-6f, 22.4e-6f), 21e-6f, 8e3f,
                                    1.2e3f, 0.758f);
                 color = volumetric_clouds(&cx, dir, sun, color, dither, V3(0.8f, 0.8f, 0.8f));
                 color = muls3(color, sun_factor);
             }
             store(&target, x, y, V4(color.x, color.y, color.z, 1.0f));
         }
-        c0 += cnt[0]; c1 += cnt[1]; c2 += cnt[2]; c3 += cnt[3];
+        c0 += cnt[0]; c1 += cnt[1]; c2 += cnt[2]; c3 += cnt[3]; c4 += cnt[4]; c5 += cnt[5]; c6 += cnt[6];
     }
-    g_cloud_counters[0] = c0; g_cloud_counters[1] = c1; g_cloud_counters[2] = c2; g_cloud_counters[3] = c3;
+    const uint64_t all[SOC_ORACLE_CLOUD_COUNTERS] = {c0, c1, c2, c3, c4, c5, c6, (uint64_t)W * (uint64_t)H};
+    memcpy(g_cloud_counters, all, sizeof all);
     return SOC_OK;
 }
 

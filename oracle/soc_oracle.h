@@ -25,6 +25,10 @@ extern "C" {
 int soc_oracle_bloom_downsample(const soc_globals* g, soc_img higher_mip, soc_img lower_mip);
 int soc_oracle_bloom_upsample(const soc_globals* g, soc_img lower_mip, soc_img higher_mip);
 int soc_oracle_ssao_generation(const soc_globals* g, soc_img depth, soc_img normal, soc_img target);
+/* The same taps with the random vectors given per target pixel (x, y pairs), e.g. the GPU's table: isolates the tap
+   arithmetic from the Q8 hash's sinf precision in the parity checks. */
+int soc_oracle_ssao_generation_rv(const soc_globals* g, soc_img depth, soc_img normal, const float* rv_table,
+                                  soc_img target);
 int soc_oracle_ssao_blur(const soc_globals* g, soc_img ssao, soc_img target);
 int soc_oracle_cloud_rendering(const soc_globals* g, soc_img depth, soc_img noise, soc_img target);
 int soc_oracle_composition(const soc_globals* g, soc_img target, soc_img albedo, soc_img emissive,
@@ -62,7 +66,11 @@ float soc_oracle_f16_to_f32(uint16_t h);
 /* Per-sky-pixel operation tallies of the clouds pass (filled by the last soc_oracle_cloud_rendering
  * call with counting enabled): [0]=sky pixels, [1]=cloud-march steps with density, [2]=get_clouds
  * evaluations, [3]=noise taps. */
-void soc_oracle_clouds_counters(uint64_t out[4]);
+/* Tallies of the last soc_oracle_cloud_rendering call (tools/clouds_flops.py): sky pixels, dense cloud steps,
+   get_clouds calls, noise taps, get_clouds calls past the altitude test, full atmosphere evaluations, cloud marches,
+   pixels. */
+#define SOC_ORACLE_CLOUD_COUNTERS 8
+void soc_oracle_clouds_counters(uint64_t out[SOC_ORACLE_CLOUD_COUNTERS]);
 int soc_oracle_num_threads(void);
 
 #ifdef __cplusplus

@@ -535,20 +535,29 @@ class Renderer:
     def load_state(self, state) -> None:
         """Resume from save_state()'s dict or file: writes the history images and the AutoExposure block back into this
         renderer's frame and restores the history slot (soc_renderer_set_current_history). The frame's extents and
-        formats must match the checkpoint's."""
+        formats must match the checkpoint's; every check runs before anything is written. The checkpoint does not hold
+        the globals: the caller restores its frame_counter (TAA's accumulation factor) and its jitter index (the
+        projection jitter) in the globals of the resumed frames, as the application's update() state."""
         st = dict(np.load(state, allow_pickle=False)) if isinstance(state, (str, os.PathLike)) else state
         if int(st["version"]) != self.STATE_VERSION:
             raise ValueError(f"load_state: checkpoint version {int(st['version'])}, expected {self.STATE_VERSION}")
         h = int(st["history_index"])
+        if h not in (0, 1):
+            raise ValueError(f"load_state: history_index {h} is not 0 or 1")
+        srcs = {}
         for key in ("history_color", "history_velocity"):
             dst = self.frame[key][h]
             src = np.asarray(st[key])
             if tuple(src.shape) != tuple(dst.shape) or src.dtype != np.float16:
                 raise ValueError(f"load_state: {key} {src.shape} {src.dtype} does not match the frame's {tuple(dst.shape)}")
-            dst.copy_(torch.from_numpy(np.ascontiguousarray(src)))
+            srcs[key] = src
         ae = np.asarray(st["auto_exposure"])
-        if ae.shape != tuple(self.frame["auto_exposure"].shape):
-            raise ValueError("load_state: AutoExposure block size differs")
+        if ae.shape != tuple(self.frame["auto_exposure"].shape) or ae.dtype != np.int32:
+            raise ValueError(f"load_state: AutoExposure block {ae.shape} {ae.dtype} does not match the frame's "
+                             f"{tuple(self.frame['auto_exposure'].shape)} int32")
+        # every check passed: nothing of the frame is written before this point
+        for key, src in srcs.items():
+            self.frame[key][h].copy_(torch.from_numpy(np.ascontiguousarray(src)))
         self.frame["auto_exposure"].copy_(torch.from_numpy(np.ascontiguousarray(ae)))
         _check(lib().soc_renderer_set_current_history(self.handle, h), "soc_renderer_set_current_history")
         torch.cuda.synchronize()

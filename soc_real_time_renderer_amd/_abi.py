@@ -189,6 +189,7 @@ FUNCTIONS = {
     "soc_abi_offsetof": (C.c_int64, [C.c_char_p, C.c_char_p]),
     "soc_last_error_string": (C.c_char_p, []),
     "soc_tuning_reload": (None, []),
+    "soc_check_block_shape": (C.c_int, [C.c_int32] * 4),
     "soc_device_arch": (C.c_char_p, []),
     "soc_globals_init_defaults": (_I, [_G, C.c_int32, C.c_int32]),
     "soc_globals_frame_update": (_I, [_G, C.POINTER(Camera), C.c_int32, C.c_int32, C.c_float, C.POINTER(C.c_uint32)]),

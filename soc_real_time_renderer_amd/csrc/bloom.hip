@@ -19,7 +19,7 @@ namespace {
 // ------------------------------------------------------------------------------------------------
 // downsample
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void bloom_down_generic(DImg src, DImg dst, float sxt, float syt) {
+__global__ __launch_bounds__(kWorkgroup) void bloom_down_generic(DImg src, DImg dst, float sxt, float syt) {
     const int x = blockIdx.x * BX + threadIdx.x, y = blockIdx.y * BY + threadIdx.y;
     if (x >= dst.w || y >= dst.h) return;
     const float u = centre_uv(x, dst.w), v = centre_uv(y, dst.h);
@@ -37,7 +37,7 @@ __global__ __launch_bounds__(256) void bloom_down_generic(DImg src, DImg dst, fl
 // ------------------------------------------------------------------------------------------------
 // upsample (result overwrites the destination: quirk Q5)
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void bloom_up_generic(DImg src, DImg dst, float X, float Y) {
+__global__ __launch_bounds__(kWorkgroup) void bloom_up_generic(DImg src, DImg dst, float X, float Y) {
     const int x = blockIdx.x * BX + threadIdx.x, y = blockIdx.y * BY + threadIdx.y;
     if (x >= dst.w || y >= dst.h) return;
     const float u = centre_uv(x, dst.w), v = centre_uv(y, dst.h);
@@ -51,7 +51,7 @@ __global__ __launch_bounds__(256) void bloom_up_generic(DImg src, DImg dst, floa
 }
 
 // dst is exactly twice src: the lower-mip coordinate of tap k is X/2 - 0.25 + k (weights 3/4, 1/4).
-__global__ __launch_bounds__(256) void bloom_up_double(DImg src, DImg dst) {
+__global__ __launch_bounds__(kWorkgroup) void bloom_up_double(DImg src, DImg dst) {
     const int x = blockIdx.x * BX + threadIdx.x, y = blockIdx.y * BY + threadIdx.y;
     if (x >= dst.w || y >= dst.h) return;
     auto AX = [&](int k) { return axis_from_fixed(128 * x - 64 + 256 * k, src.w); };
@@ -71,7 +71,7 @@ __global__ __launch_bounds__(256) void bloom_up_double(DImg src, DImg dst) {
 // so results are bit-identical.
 // ------------------------------------------------------------------------------------------------
 // same-size 13-tap downsample, 2x2 output pixels per lane from a 6x6 texel window
-__global__ __launch_bounds__(256) void bloom_down_same_q(DImg src, DImg dst, bool vec) {
+__global__ __launch_bounds__(kWorkgroup) void bloom_down_same_q(DImg src, DImg dst, bool vec) {
     const int m = blockIdx.x * BX + threadIdx.x, n = blockIdx.y * BY + threadIdx.y;
     const int X0 = 2 * m, Y0 = 2 * n;
     if (X0 >= dst.w || Y0 >= dst.h) return;
@@ -106,7 +106,7 @@ __global__ __launch_bounds__(256) void bloom_down_same_q(DImg src, DImg dst, boo
 }
 
 // same-size 9-tap tent upsample, 2x2 output pixels per lane from a 4x4 window
-__global__ __launch_bounds__(256) void bloom_up_same_q(DImg src, DImg dst, bool vec) {
+__global__ __launch_bounds__(kWorkgroup) void bloom_up_same_q(DImg src, DImg dst, bool vec) {
     const int m = blockIdx.x * BX + threadIdx.x, n = blockIdx.y * BY + threadIdx.y;
     const int X0 = 2 * m, Y0 = 2 * n;
     if (X0 >= dst.w || Y0 >= dst.h) return;
@@ -135,7 +135,7 @@ __global__ __launch_bounds__(256) void bloom_up_same_q(DImg src, DImg dst, bool 
 
 // 2:1 downsample: one output per lane, 6x6 source window; the 13 taps are w = 0.5 blends of the 2x2
 // blocks at source offsets 2x+k (k = -2..2), sharing the 30 horizontal lerps. Border pixels use tap().
-__global__ __launch_bounds__(256) void bloom_down_half_w(DImg src, DImg dst) {
+__global__ __launch_bounds__(kWorkgroup) void bloom_down_half_w(DImg src, DImg dst) {
     const int x = blockIdx.x * BX + threadIdx.x, y = blockIdx.y * BY + threadIdx.y;
     if (x >= dst.w || y >= dst.h) return;
     const bool interior = 2 * x - 2 >= 0 && 2 * x + 3 <= src.w - 1 && 2 * y - 2 >= 0 && 2 * y + 3 <= src.h - 1;
@@ -178,7 +178,7 @@ __global__ __launch_bounds__(256) void bloom_down_half_w(DImg src, DImg dst) {
 
 // 1:2 upsample: a 2x2 output quad per lane from the 5x5 source window around (m, n). Even outputs use
 // x-pairs (m-2..m) at w = 3/4, odd ones (m-1..m+1) at w = 1/4 (and likewise in y). Border quads use tap().
-__global__ __launch_bounds__(256) void bloom_up_double_q(DImg src, DImg dst, bool vec) {
+__global__ __launch_bounds__(kWorkgroup) void bloom_up_double_q(DImg src, DImg dst, bool vec) {
     const int m = blockIdx.x * BX + threadIdx.x, n = blockIdx.y * BY + threadIdx.y;
     if (m >= src.w || n >= src.h) return;
     const int X0 = 2 * m, Y0 = 2 * n;
@@ -271,11 +271,11 @@ int launch_bloom_down(const soc_img& hi, const soc_img& lo, hipStream_t s, int f
     const bool small = hi.width <= kFastMax && hi.height <= kFastMax;
     if (!force_generic && small && hi.width == lo.width && hi.height == lo.height) {
         dim3 g2(ceil_div(ceil_div(lo.width, 2), BX), ceil_div(ceil_div(lo.height, 2), BY));
-        bloom_down_same_q<<<g2, blk, 0, s>>>(src, dst, vec16(lo));
+        launch("bloom_down_same_q", kWorkgroup, bloom_down_same_q, g2, blk, 0, s, src, dst, vec16(lo));
     } else if (!force_generic && small && hi.width == 2 * lo.width && hi.height == 2 * lo.height) {
-        bloom_down_half_w<<<grd, blk, 0, s>>>(src, dst);
+        launch("bloom_down_half_w", kWorkgroup, bloom_down_half_w, grd, blk, 0, s, src, dst);
     } else {
-        bloom_down_generic<<<grd, blk, 0, s>>>(src, dst, 1.0f / (float)hi.width, 1.0f / (float)hi.height);
+        launch("bloom_down_generic", kWorkgroup, bloom_down_generic, grd, blk, 0, s, src, dst, 1.0f / (float)hi.width, 1.0f / (float)hi.height);
     }
     return check_launch("bloom_downsample");
 }
@@ -286,16 +286,16 @@ int launch_bloom_up(const soc_img& lo, const soc_img& hi, hipStream_t s, int for
     const bool small = hi.width <= kFastMax && hi.height <= kFastMax;
     if (!force_generic && small && hi.width == lo.width && hi.height == lo.height) {
         dim3 g2(ceil_div(ceil_div(hi.width, 2), BX), ceil_div(ceil_div(hi.height, 2), BY));
-        bloom_up_same_q<<<g2, blk, 0, s>>>(src, dst, vec16(hi));
+        launch("bloom_up_same_q", kWorkgroup, bloom_up_same_q, g2, blk, 0, s, src, dst, vec16(hi));
     } else if (!force_generic && small && hi.width == 2 * lo.width && hi.height == 2 * lo.height) {
         if ((long)hi.width * hi.height < quad_min_px()) {
-            bloom_up_double<<<grd, blk, 0, s>>>(src, dst);
+            launch("bloom_up_double", kWorkgroup, bloom_up_double, grd, blk, 0, s, src, dst);
         } else {
             dim3 g2(ceil_div(lo.width, BX), ceil_div(lo.height, BY));
-            bloom_up_double_q<<<g2, blk, 0, s>>>(src, dst, vec16(hi));
+            launch("bloom_up_double_q", kWorkgroup, bloom_up_double_q, g2, blk, 0, s, src, dst, vec16(hi));
         }
     } else {
-        bloom_up_generic<<<grd, blk, 0, s>>>(src, dst, 1.0f / (float)lo.width, 1.0f / (float)lo.height);
+        launch("bloom_up_generic", kWorkgroup, bloom_up_generic, grd, blk, 0, s, src, dst, 1.0f / (float)lo.width, 1.0f / (float)lo.height);
     }
     return check_launch("bloom_upsample");
 }

@@ -159,7 +159,7 @@ constexpr int W1_EW = W1_MW + 4, W1_EH = W1_MH + 4;           // emissive tile 7
 // the tile loads' latency hides behind the filter instead of being waited on (the one-tile kernel waits on its
 // loads and barriers for 61 % of its wave cycles, profiles/r03_sq_stalls.json: 47.5 -> 42.9 us serial at 4K). The
 // same arithmetic and bits as that one-tile-per-workgroup kernel.
-__global__ __launch_bounds__(256) void bloomw_down01p(DImg E, DImg M1, int ntx, int nty) {
+__global__ __launch_bounds__(kWorkgroup) void bloomw_down01p(DImg E, DImg M1, int ntx, int nty) {
     __shared__ uint2 et[W1_EH][W1_EW];
     __shared__ uint2 mt[W1_MH][W1_MW];
     constexpr int NT = W1_EW * W1_EH, KR = (NT + 255) / 256;
@@ -219,7 +219,7 @@ constexpr int W2_OW = 16, W2_OH = 8;                          // mip3 outputs pe
 constexpr int W2_MW = 2 * W2_OW + 4, W2_MH = 2 * W2_OH + 4;   // mip2 tile 36 x 20
 constexpr int W2_SW = 2 * W2_MW + 4, W2_SH = 2 * W2_MH + 4;   // mip1 tile 76 x 44
 
-__global__ __launch_bounds__(256) void bloomw_down23(DImg S1, DImg M3, int W2, int H2, int swz) {
+__global__ __launch_bounds__(kWorkgroup) void bloomw_down23(DImg S1, DImg M3, int W2, int H2, int swz) {
     __shared__ uint2 st[W2_SH][W2_SW];
     __shared__ uint2 mt[W2_MH][W2_MW];
     const int tid = threadIdx.x;
@@ -275,7 +275,7 @@ __device__ __forceinline__ void up12_into(const uint2 (*s)[SW], int sx0, int sy0
     }
 }
 
-__global__ __launch_bounds__(256) void bloomw_up32(DImg S3, DImg M1, int W2, int H2, bool vec, int swz) {
+__global__ __launch_bounds__(kWorkgroup) void bloomw_up32(DImg S3, DImg M1, int W2, int H2, bool vec, int swz) {
     __shared__ uint2 st[W3_SH][W3_SW];
     __shared__ uint2 mt[W3_MH][W3_MW];
     const int tid = threadIdx.x;
@@ -309,7 +309,7 @@ __global__ __launch_bounds__(256) void bloomw_up32(DImg S3, DImg M1, int W2, int
 constexpr int W4_MW = U_OW + 2, W4_MH = U_OH + 2;             // mip0 tile 66 x 18, origin (X0 - 1, Y0 - 1)
 constexpr int W4_SW = U_OW / 2 + 6, W4_SH = U_OH / 2 + 6;     // mip1 tile 38 x 14, origin (X0/2 - 3, Y0/2 - 3)
 
-__global__ __launch_bounds__(256) void bloomw_up10(DImg S1, DImg O, bool vec, int swz) {
+__global__ __launch_bounds__(kWorkgroup) void bloomw_up10(DImg S1, DImg O, bool vec, int swz) {
     __shared__ uint2 st[W4_SH][W4_SW];
     __shared__ uint2 mt[W4_MH][W4_MW + 2];   // +2: the pair loop writes whole pairs
     const int tid = threadIdx.x;
@@ -346,14 +346,19 @@ __global__ __launch_bounds__(256) void bloomw_up10(DImg S1, DImg O, bool vec, in
     }
 }
 
-// Workgroups of 256 lanes of `kernel` resident on the whole device at once (the persistent kernels' grid bound).
-template <typename K>
-int resident_set(K kernel) {
+// Workgroups of 256 lanes of bloomw_down01p resident on the whole device at once (the persistent kernel's grid bound),
+// queried once per device and cached (the occupancy query is not on the per-frame enqueue path).
+int down01p_resident_set() {
+    constexpr int kMaxDevices = 64;
+    static int cached[kMaxDevices] = {};
     int dev = 0, cus = 256, per = 0;
     (void)hipGetDevice(&dev);
+    if (dev >= 0 && dev < kMaxDevices && cached[dev]) return cached[dev];
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 256, 0);
-    return std::max(per, 1) * cus;
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, bloomw_down01p, 256, 0);
+    const int n = std::max(per, 1) * cus;
+    if (dev >= 0 && dev < kMaxDevices) cached[dev] = n;
+    return n;
 }
 
 bool a16(const soc_img& im) { return im.pitch_bytes % 16 == 0 && reinterpret_cast<uintptr_t>(im.data) % 16 == 0; }
@@ -366,20 +371,20 @@ int launch_bloom_weighted(const soc_img& emissive, const soc_img* mips, const so
     if (stage == 0 || stage == 1) {
         // persistent: one resident set of workgroups (a multiple of 8, so a workgroup's tiles stay on its XCD)
         const int ntx = ceil_div(mips[1].width, W1_OW), nty = ceil_div(mips[1].height, W1_OH);
-        const int grid = std::max(8, (std::min(ntx * nty, resident_set(bloomw_down01p)) / 8) * 8);
-        bloomw_down01p<<<grid, 256, 0, s>>>(E, M1, ntx, nty);
+        const int grid = std::max(8, (std::min(ntx * nty, down01p_resident_set()) / 8) * 8);
+        launch("bloomw_down01p", kWorkgroup, bloomw_down01p, grid, kWorkgroup, 0, s, E, M1, ntx, nty);
     }
     if (stage == 0 || stage == 2) {
         dim3 g(ceil_div(mips[3].width, W2_OW), ceil_div(mips[3].height, W2_OH));
-        bloomw_down23<<<g, 256, 0, s>>>(M1, M3, mips[2].width, mips[2].height, swz);
+        launch("bloomw_down23", kWorkgroup, bloomw_down23, g, kWorkgroup, 0, s, M1, M3, mips[2].width, mips[2].height, swz);
     }
     if (stage == 0 || stage == 3) {
         dim3 g(ceil_div(mips[1].width, U_OW), ceil_div(mips[1].height, U_OH));
-        bloomw_up32<<<g, 256, 0, s>>>(M3, M1, mips[2].width, mips[2].height, a16(mips[1]), swz);
+        launch("bloomw_up32", kWorkgroup, bloomw_up32, g, kWorkgroup, 0, s, M3, M1, mips[2].width, mips[2].height, a16(mips[1]), swz);
     }
     if (stage == 0 || stage == 4) {
         dim3 g(ceil_div(output.width, U_OW), ceil_div(output.height, U_OH));
-        bloomw_up10<<<g, 256, 0, s>>>(M1, O, a16(output), swz);
+        launch("bloomw_up10", kWorkgroup, bloomw_up10, g, kWorkgroup, 0, s, M1, O, a16(output), swz);
     }
     return check_launch("bloom_weighted");
 }

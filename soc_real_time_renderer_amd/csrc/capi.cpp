@@ -60,7 +60,36 @@ int tuning_knob(const char* name, int dflt) {
     return v;
 }
 
+namespace {
+thread_local std::string t_shape_error;   // a block shape launch() rejected since the last check_launch
+}  // namespace
+
+bool block_fits(const char* kernel, int bound, dim3 block) {
+    const long long lanes = (long long)block.x * block.y * block.z;
+    if (lanes >= 1 && lanes <= bound) return true;
+    char buf[256];
+    std::snprintf(buf, sizeof buf, "%s: block %ux%ux%u (%lld lanes) outside the kernel's launch bound of %d lanes", kernel,
+                  block.x, block.y, block.z, lanes, bound);
+    if (t_shape_error.empty()) t_shape_error = buf;
+    return false;
+}
+
+extern "C" int soc_check_block_shape(int32_t bound, int32_t bx, int32_t by, int32_t bz) {
+    if (bx < 0 || by < 0 || bz < 0) return set_error(SOC_E_INVALID_ARG, "soc_check_block_shape: negative extent");
+    if (!block_fits("soc_check_block_shape", bound, dim3((unsigned)bx, (unsigned)by, (unsigned)bz))) {
+        std::string m;
+        m.swap(t_shape_error);
+        return set_error(SOC_E_INVALID_ARG, "%s", m.c_str());
+    }
+    return SOC_OK;
+}
+
 int check_launch(const char* pass) {
+    if (!t_shape_error.empty()) {
+        std::string m;
+        m.swap(t_shape_error);
+        return set_error(SOC_E_INVALID_ARG, "%s: kernel not launched: %s", pass, m.c_str());
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_error(SOC_E_HIP, "%s: kernel launch failed: %s", pass, hipGetErrorString(e));
     return SOC_OK;
@@ -637,6 +666,10 @@ struct soc_renderer {
     bool sky_split = false, sky_split_active = false;
     // the caller's stream is ordered after all second-lane work of the previous call (its join or an equivalent wait)
     bool main_after_side = true;
+    // SOC_RENDERER_STATIC_INPUTS: a call of this graph has completed, so the frame inputs the caller wrote before its
+    // first call are ordered before the second lane (that call's fork). Until then every second-lane pass waits for the
+    // fork, as without the flag (the first call after create or a graph rebuild may follow the caller's input writes).
+    bool inputs_ordered = false;
 };
 
 namespace {
@@ -1002,6 +1035,7 @@ void derive_signals(soc_renderer* r) {
 }
 
 int build_graph(soc_renderer* r) {
+    r->inputs_ordered = false;
     destroy_pass_events(r);
     r->passes.clear();
     build_raster_passes(r);
@@ -1225,7 +1259,7 @@ extern "C" int soc_renderer_execute(soc_renderer* r, const soc_globals* g, int32
         if (lane[i] != 1) continue;
         bool carry_main = false;
         for (int j : r->passes[i].carry) carry_main |= static_lane(r, j) == 0;
-        if (!(r->flags & SOC_RENDERER_STATIC_INPUTS) || carry_main) pre_fork = false;
+        if (!(r->flags & SOC_RENDERER_STATIC_INPUTS) || !r->inputs_ordered || carry_main) pre_fork = false;
         needs_fork[i] = !pre_fork;
     }
     // Each lane is one in-order stream, so a wait on the other lane's pass at position k (in this call's issue order on
@@ -1273,8 +1307,9 @@ extern "C" int soc_renderer_execute(soc_renderer* r, const soc_globals* g, int32
     const bool side_joined = waited[0] >= next_pos[1] - 1;
     if (lanes && !side_joined &&
         (hipEventRecord(r->join_ev, r->side) != hipSuccess || hipStreamWaitEvent(s, r->join_ev, 0) != hipSuccess))
-        return abort_frame(r, s, false, set_error(SOC_E_HIP, "soc_renderer_execute: second lane join failed"));
+        return abort_frame(r, s, lanes, set_error(SOC_E_HIP, "soc_renderer_execute: second lane join failed"));
     r->main_after_side = true;
+    r->inputs_ordered = true;
     if (phase & SOC_PHASE_POST_EXPOSURE) r->hist = 1 - r->hist;   // ping-pong the TAA history
     return SOC_OK;
 }

@@ -419,7 +419,7 @@ __device__ __forceinline__ bool is_sky(const CloudParams& p, const DImg& depth, 
 
 // Single-kernel path (no workspace): 16x16 tiles, a tile without sky exits after its depth test.
 template <bool NOISE_R8>
-__global__ __launch_bounds__(256) void clouds_kernel(DImg depth, DImg noise, DImg target, CloudParams p) {
+__global__ __launch_bounds__(kWorkgroup) void clouds_kernel(DImg depth, DImg noise, DImg target, CloudParams p) {
     __shared__ uint32_t quads[kTable];
     const int x = blockIdx.x * TX + threadIdx.x, y = blockIdx.y * TY + threadIdx.y;
     const int tid = threadIdx.y * TX + threadIdx.x;
@@ -442,7 +442,7 @@ __global__ __launch_bounds__(256) void clouds_kernel(DImg depth, DImg noise, DIm
 // row-major inside a wave's quarter, so a wave of the march takes a compact 32x2 block. The list offset
 // costs ONE atomic per workgroup that has sky: device-scope atomics on one address serialise across
 // the XCDs (one per wave cost ~95 us at 4K).
-__global__ __launch_bounds__(256) void clouds_classify(DImg depth, DImg target, CloudParams p, int vec_store,
+__global__ __launch_bounds__(kWorkgroup) void clouds_classify(DImg depth, DImg target, CloudParams p, int vec_store,
                                                        uint32_t* __restrict__ counter, uint32_t* __restrict__ list) {
     __shared__ uint32_t wave_total[4];
     __shared__ uint32_t wg_base;
@@ -496,7 +496,7 @@ __global__ __launch_bounds__(256) void clouds_classify(DImg depth, DImg target, 
 
 // Three-kernel path, stage 2: the atmosphere of every listed sky pixel (no LDS, few registers, so many
 // more lanes are resident than in the cloud march), kept in fp32 in the workspace.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void clouds_atmosphere(CloudParams p, const uint32_t* __restrict__ counter,
+__global__ __launch_bounds__(kWorkgroup) __attribute__((amdgpu_waves_per_eu(8))) void clouds_atmosphere(CloudParams p, const uint32_t* __restrict__ counter,
                                                          const uint32_t* __restrict__ list, float4* __restrict__ atmos) {
     const uint32_t count = *counter;
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < count; i += gridDim.x * 256u) {
@@ -518,6 +518,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
 // are the bits the single-lane march computes. A workgroup whose pairs do not fit the list marks its
 // pixels for the single-lane march in resolve.
 constexpr int kShards = 8;
+// clouds_sunvis workgroup: 512 lanes (the 26 KiB noise table caps residency at 6 workgroups per CU: 512 lanes give the
+// full 8 waves per SIMD); its launch bound
+constexpr uint32_t kSunvisLanes = 512;
 constexpr uint32_t kInline = 0x80000000u;   // pix_mask flag: march this pixel in resolve
 
 struct PairBufs {
@@ -570,7 +573,7 @@ __device__ __forceinline__ void batch_slots(uint32_t mask, uint32_t lane, uint32
 }
 
 template <bool NOISE_R8>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void clouds_density(
+__global__ __launch_bounds__(kWorkgroup) __attribute__((amdgpu_waves_per_eu(6))) void clouds_density(
     DImg noise, CloudParams p, const uint32_t* __restrict__ counter, const uint32_t* __restrict__ list, PairBufs pb) {
     __shared__ uint32_t quads[kTable];
     __shared__ uint32_t offs[25][4];
@@ -693,7 +696,7 @@ __global__ __launch_bounds__(kSunvisThreads) __attribute__((amdgpu_waves_per_eu(
 }
 
 template <bool NOISE_R8>
-__global__ __launch_bounds__(256) void clouds_resolve(DImg noise, DImg target, CloudParams p, const uint32_t* __restrict__ counter,
+__global__ __launch_bounds__(kWorkgroup) void clouds_resolve(DImg noise, DImg target, CloudParams p, const uint32_t* __restrict__ counter,
                                                       const uint32_t* __restrict__ list, const float4* __restrict__ atmos,
                                                       PairBufs pb) {
     __shared__ uint32_t quads[kTable];
@@ -867,8 +870,8 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
     const bool r8 = noise.format == SOC_FMT_R8_UNORM;
     if (!workspace) {
         dim3 blk(TX, TY), grd(ceil_div(W, TX), ceil_div(H, TY));
-        if (r8) clouds_kernel<true><<<grd, blk, 0, s>>>(dimg(depth), dimg(noise), dimg(target), p);
-        else clouds_kernel<false><<<grd, blk, 0, s>>>(dimg(depth), dimg(noise), dimg(target), p);
+        if (r8) launch("clouds_kernel", kWorkgroup, clouds_kernel<true>, grd, blk, 0, s, dimg(depth), dimg(noise), dimg(target), p);
+        else launch("clouds_kernel", kWorkgroup, clouds_kernel<false>, grd, blk, 0, s, dimg(depth), dimg(noise), dimg(target), p);
         return check_launch("cloud_rendering");
     }
     // the caller sized the workspace for the target extent (soc_cloud_rendering_workspace_size)
@@ -878,14 +881,14 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
     hipError_t e = hipMemsetAsync(counter, 0, 256, s);
     if (e != hipSuccess) return set_error(SOC_E_HIP, "%s: %s", P, hipGetErrorString(e));
     const int vec_store = (target.pitch_bytes % 16 == 0) && (reinterpret_cast<uintptr_t>(target.data) % 16 == 0);
-    clouds_classify<<<dim3(ceil_div(W, 64), ceil_div(H, 16)), 256, 0, s>>>(dimg(depth), dimg(target), p, vec_store, counter, list);
+    launch("clouds_classify", kWorkgroup, clouds_classify, dim3(ceil_div(W, 64), ceil_div(H, 16)), kWorkgroup, 0, s, dimg(depth), dimg(target), p, vec_store, counter, list);
     // One resident wave set per kernel, grid-stride over the list / pairs: the long per-item work is
     // balanced over all SIMDs instead of running as a second, partially filled round.
     static int res_atmos = 0, res_density = 0, res_sunvis = 0, res_resolve = 0;
     if (!res_atmos) {
         res_atmos = resident_blocks(clouds_atmosphere);
         res_density = resident_blocks(clouds_density<false>);
-        res_sunvis = resident_blocks(clouds_sunvis<false, 512, true>, 512);
+        res_sunvis = resident_blocks(clouds_sunvis<false, kSunvisLanes, true>, kSunvisLanes);
         res_resolve = resident_blocks(clouds_resolve<false>);
     }
     const long long blocks = ((long long)W * H + 255) / 256;
@@ -897,22 +900,22 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
     // 1920x1080 -5 % after it); the same bits in every position (profiles/r03_ab_atmos_pos.txt, GPU identity test).
     const int apos_knob = tuning_knob("SOC_CLOUDS_ATMOS_POS", -1);
     const int apos = apos_knob >= 0 ? apos_knob : ((long long)W * H > 2560LL * 1440LL ? 2 : 0);
-    auto atmos = [&]() { clouds_atmosphere<<<grid(res_atmos, blocks), 256, 0, s>>>(p, counter, list, ws.atmos); };
+    auto atmos = [&]() { launch("clouds_atmosphere", kWorkgroup, clouds_atmosphere, grid(res_atmos, blocks), kWorkgroup, 0, s, p, counter, list, ws.atmos); };
     if (apos == 0) atmos();
     const DImg nz = dimg(noise), tg = dimg(target);
     const int density_grid = std::min(grid(res_density, blocks), (int)ws.pb.od_blocks);   // one od scratch per workgroup
     if (r8) {
-        clouds_density<true><<<density_grid, 256, 0, s>>>(nz, p, counter, list, ws.pb);
+        launch("clouds_density", kWorkgroup, clouds_density<true>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
         if (apos == 1) atmos();
-        clouds_sunvis<true, 512, true><<<grid(res_sunvis, blocks), 512, 0, s>>>(nz, p, list, ws.pb);
+        launch("clouds_sunvis", kSunvisLanes, clouds_sunvis<true, kSunvisLanes, true>, grid(res_sunvis, blocks), kSunvisLanes, 0, s, nz, p, list, ws.pb);
         if (apos == 2) atmos();
-        clouds_resolve<true><<<grid(res_resolve, blocks), 256, 0, s>>>(nz, tg, p, counter, list, ws.atmos, ws.pb);
+        launch("clouds_resolve", kWorkgroup, clouds_resolve<true>, grid(res_resolve, blocks), kWorkgroup, 0, s, nz, tg, p, counter, list, ws.atmos, ws.pb);
     } else {
-        clouds_density<false><<<density_grid, 256, 0, s>>>(nz, p, counter, list, ws.pb);
+        launch("clouds_density", kWorkgroup, clouds_density<false>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
         if (apos == 1) atmos();
-        clouds_sunvis<false, 512, true><<<grid(res_sunvis, blocks), 512, 0, s>>>(nz, p, list, ws.pb);
+        launch("clouds_sunvis", kSunvisLanes, clouds_sunvis<false, kSunvisLanes, true>, grid(res_sunvis, blocks), kSunvisLanes, 0, s, nz, p, list, ws.pb);
         if (apos == 2) atmos();
-        clouds_resolve<false><<<grid(res_resolve, blocks), 256, 0, s>>>(nz, tg, p, counter, list, ws.atmos, ws.pb);
+        launch("clouds_resolve", kWorkgroup, clouds_resolve<false>, grid(res_resolve, blocks), kWorkgroup, 0, s, nz, tg, p, counter, list, ws.atmos, ws.pb);
     }
     return check_launch("cloud_rendering");
 }

@@ -219,7 +219,7 @@ constexpr int BX = 64, BY = 4;
 // LIGHTS = false: no point / spot lights this frame (the reference default): the light loops are not
 // compiled in, which keeps the kernel at a fraction of the registers (more waves, more loads in flight).
 template <bool HIST, bool LIGHTS, int NT = 0>
-__global__ __launch_bounds__(256) void composition_pair(DImg target, DImg albedo, DImg emissive, DImg normal, DImg depth,
+__global__ __launch_bounds__(kWorkgroup) void composition_pair(DImg target, DImg albedo, DImg emissive, DImg normal, DImg depth,
                                                         DImg ssao, DImg shadow, DImg clouds, CompParams p) {
     // a wave covers 16x8 pixels (8 lanes x 2 pixels per row, 8 rows): every row segment is one
     // 128-B line of each G-buffer image, and the wave's shadow-map taps form a compact 2D patch
@@ -323,7 +323,7 @@ __global__ __launch_bounds__(256) void composition_pair(DImg target, DImg albedo
 // binned on the renderer's second lane right after CloudRendering, so Composition (sky_external) does not wait
 // for the clouds: the same tiling, texel fetch, f16 packing and bins as composition_pair's sky branch, hence
 // the same bits. 8-B stores of the sky pixels only (Composition writes the others concurrently).
-__global__ __launch_bounds__(256) void sky_compose_pair(DImg target, DImg depth, DImg clouds, CompParams p) {
+__global__ __launch_bounds__(kWorkgroup) void sky_compose_pair(DImg target, DImg depth, DImg clouds, CompParams p) {
     __shared__ uint32_t sh[4 * kBins];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     reinterpret_cast<uint4*>(sh + wave * kBins)[lane] = uint4{0u, 0u, 0u, 0u};
@@ -355,7 +355,7 @@ __global__ __launch_bounds__(256) void sky_compose_pair(DImg target, DImg depth,
     if (n) atomicAdd(&p.bins[((blockIdx.y * gridDim.x + blockIdx.x) & 7u) * kBins + threadIdx.x], n);
 }
 
-__global__ __launch_bounds__(256) void histogram_fold(uint32_t* __restrict__ scratch, uint32_t* __restrict__ bins) {
+__global__ __launch_bounds__(kBins) void histogram_fold(uint32_t* __restrict__ scratch, uint32_t* __restrict__ bins) {
     const int i = threadIdx.x;
     uint32_t s = 0;
 #pragma unroll
@@ -367,7 +367,7 @@ __global__ __launch_bounds__(256) void histogram_fold(uint32_t* __restrict__ scr
 }
 
 // Generic path: every input is sampled under the sampling contract.
-__global__ __launch_bounds__(256) void composition_generic(DImg target, DImg albedo, DImg emissive, DImg normal,
+__global__ __launch_bounds__(kWorkgroup) void composition_generic(DImg target, DImg albedo, DImg emissive, DImg normal,
                                                            DImg depth, DImg ssao, DImg shadow, DImg clouds, CompParams p) {
     const int x = blockIdx.x * BX + threadIdx.x, y = blockIdx.y * BY + threadIdx.y;
     if (x >= target.w || y >= target.h) return;
@@ -453,7 +453,7 @@ int composition_launch(const soc_globals* g, const soc_globals* d_globals, soc_i
     if (fast) {
         dim3 grd(ceil_div(W, 32), ceil_div(H, 16));
         const bool lights = (p.npl | p.nsl) != 0;
-#define SOC_COMP_PAIR(HI, LI) composition_pair<HI, LI><<<grd, 256, 0, hs(stream)>>>(dimg(target), dimg(albedo), \
+#define SOC_COMP_PAIR(HI, LI) launch("composition_pair", kWorkgroup, composition_pair<HI, LI>, grd, kWorkgroup, 0, hs(stream), dimg(target), dimg(albedo), \
             dimg(emissive), dimg(normal), dimg(depth), dimg(ssao), dimg(shadow), dimg(clouds), p)
         if (bins) {
             p.bins = scratch;
@@ -463,14 +463,14 @@ int composition_launch(const soc_globals* g, const soc_globals* d_globals, soc_i
             p.bf = bin_fast_params(p.lmin, p.lrange);
             if (lights) SOC_COMP_PAIR(true, true);
             else if (nt)
-                composition_pair<true, false, 3><<<grd, 256, 0, hs(stream)>>>(dimg(target), dimg(albedo), dimg(emissive),
+                launch("composition_pair", kWorkgroup, composition_pair<true, false, 3>, grd, kWorkgroup, 0, hs(stream), dimg(target), dimg(albedo), dimg(emissive),
                     dimg(normal), dimg(depth), dimg(ssao), dimg(shadow), dimg(clouds), p);
             else SOC_COMP_PAIR(true, false);
-            if (fold) histogram_fold<<<1, kBins, 0, hs(stream)>>>(scratch, bins);
+            if (fold) launch("histogram_fold", kBins, histogram_fold, 1, kBins, 0, hs(stream), scratch, bins);
         } else if (nt && !lights) {
             // non-temporal G-buffer loads and colour store (measured at 4K: 71.5 -> 68 us; TAA, the next
             // reader of depth, +3 us: the frame is unchanged). SOC_COMP_NT=0: default cache policy.
-            composition_pair<false, false, 3><<<grd, 256, 0, hs(stream)>>>(dimg(target), dimg(albedo), dimg(emissive),
+            launch("composition_pair", kWorkgroup, composition_pair<false, false, 3>, grd, kWorkgroup, 0, hs(stream), dimg(target), dimg(albedo), dimg(emissive),
                 dimg(normal), dimg(depth), dimg(ssao), dimg(shadow), dimg(clouds), p);
         } else {
             if (lights) SOC_COMP_PAIR(false, true);
@@ -479,7 +479,7 @@ int composition_launch(const soc_globals* g, const soc_globals* d_globals, soc_i
 #undef SOC_COMP_PAIR
     } else {
         dim3 blk(BX, BY), grd(ceil_div(W, BX), ceil_div(H, BY));
-        composition_generic<<<grd, blk, 0, hs(stream)>>>(dimg(target), dimg(albedo), dimg(emissive), dimg(normal),
+        launch("composition_generic", kWorkgroup, composition_generic, grd, blk, 0, hs(stream), dimg(target), dimg(albedo), dimg(emissive), dimg(normal),
                                                          dimg(depth), dimg(ssao), dimg(shadow), dimg(clouds), p);
     }
     return check_launch("composition");
@@ -510,7 +510,7 @@ int soc::sky_compose_launch(const soc_globals* g, soc_img target, soc_img depth,
     p.lrange = g->log_max_luminance - g->log_min_luminance;
     p.bf = bin_fast_params(p.lmin, p.lrange);
     const dim3 grd(ceil_div(target.width, 32), ceil_div(target.height, 16));
-    sky_compose_pair<<<grd, 256, 0, hs(stream)>>>(dimg(target), dimg(depth), dimg(clouds), p);
+    launch("sky_compose_pair", kWorkgroup, sky_compose_pair, grd, kWorkgroup, 0, hs(stream), dimg(target), dimg(depth), dimg(clouds), p);
     return check_launch("sky_compose");
 }
 
@@ -540,7 +540,7 @@ int soc::composition_luminance_histogram(const soc_globals* g, const soc_globals
 
 int soc::histogram_fold_launch(uint32_t* scratch, soc_auto_exposure* ae, soc_stream stream) {
     if (!scratch || !ae) return set_error(SOC_E_INVALID_ARG, "histogram fold: null scratch / auto exposure");
-    histogram_fold<<<1, kBins, 0, hs(stream)>>>(scratch, ae->histogram_buckets);
+    launch("histogram_fold", kBins, histogram_fold, 1, kBins, 0, hs(stream), scratch, ae->histogram_buckets);
     return check_launch("luminance_histogram_fold");
 }
 

@@ -185,9 +185,9 @@ extern "C" int soc_generate_luminance_histogram(const soc_globals* g, soc_img hd
     if (grid < 1) grid = 1;
     uint32_t* bins = ae->histogram_buckets;
     if (chunks)
-        histogram_chunks<<<grid, kThreads, 0, hs(stream)>>>(dimg(hdr), W, H, lmin, lrange, bin_fast_params(lmin, lrange), bins);
+        launch("histogram_chunks", kThreads, histogram_chunks, grid, kThreads, 0, hs(stream), dimg(hdr), W, H, lmin, lrange, bin_fast_params(lmin, lrange), bins);
     else
-        histogram_pixels<<<grid, kThreads, 0, hs(stream)>>>(dimg(hdr), W, H, lmin, lrange, bins);
+        launch("histogram_pixels", kThreads, histogram_pixels, grid, kThreads, 0, hs(stream), dimg(hdr), W, H, lmin, lrange, bins);
     return check_launch("generate_luminance_histogram");
 }
 
@@ -197,10 +197,10 @@ int soc::resolve_luminance_histogram(const soc_globals* g, soc_auto_exposure* ae
     float pixels = total_pixels ? (float)total_pixels
                                 : (float)(int32_t)((uint32_t)g->resolution[0] * (uint32_t)g->resolution[1]);
     if (wide_accumulator)
-        resolve_kernel<true><<<1, kBins, 0, hs(stream)>>>(ae, pixels, g->log_min_luminance, g->log_max_luminance,
+        launch("resolve_kernel", kBins, resolve_kernel<true>, 1, kBins, 0, hs(stream), ae, pixels, g->log_min_luminance, g->log_max_luminance,
                                                           g->target_luminance, g->delta_time, g->adjustment_speed, scratch);
     else
-        resolve_kernel<false><<<1, kBins, 0, hs(stream)>>>(ae, pixels, g->log_min_luminance, g->log_max_luminance,
+        launch("resolve_kernel", kBins, resolve_kernel<false>, 1, kBins, 0, hs(stream), ae, pixels, g->log_min_luminance, g->log_max_luminance,
                                                            g->target_luminance, g->delta_time, g->adjustment_speed, scratch);
     return check_launch("resolve_luminance_histogram");
 }

@@ -65,7 +65,7 @@ __device__ void downsample_64x64(float (*sh)[16][16], int lx, int ly, int gx, in
 }
 
 template <bool MAX>
-__global__ __launch_bounds__(256) void hiz_kernel(DImg depth, HizMips mips, uint32_t* __restrict__ counter,
+__global__ __launch_bounds__(kWorkgroup) void hiz_kernel(DImg depth, HizMips mips, uint32_t* __restrict__ counter,
                                                   uint32_t total, int res_w, int res_h) {
     __shared__ float sh[2][16][16];
     __shared__ bool last;
@@ -112,7 +112,7 @@ extern "C" int soc_generate_hiz(const soc_globals* g, soc_img depth, const soc_i
     if (hipMemsetAsync(counter, 0, sizeof(uint32_t), s) != hipSuccess)
         return set_error(SOC_E_HIP, "soc_generate_hiz: counter reset failed");
     const dim3 grd(ceil_div(W, 64), ceil_div(H, 64)), blk(16, 16);
-    if (op_max) hiz_kernel<true><<<grd, blk, 0, s>>>(dimg(depth), hm, counter, grd.x * grd.y, W, H);
-    else hiz_kernel<false><<<grd, blk, 0, s>>>(dimg(depth), hm, counter, grd.x * grd.y, W, H);
+    if (op_max) launch("hiz_kernel", kWorkgroup, hiz_kernel<true>, grd, blk, 0, s, dimg(depth), hm, counter, grd.x * grd.y, W, H);
+    else launch("hiz_kernel", kWorkgroup, hiz_kernel<false>, grd, blk, 0, s, dimg(depth), hm, counter, grd.x * grd.y, W, H);
     return check_launch("generate_hiz");
 }

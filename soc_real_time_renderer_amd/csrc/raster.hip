@@ -230,19 +230,19 @@ __device__ __forceinline__ TriSetup load_tri(const Workspace& ws, const uint32_t
     return tri_setup(ws.screen[a], ws.screen[b], ws.screen[c], p);
 }
 
-__global__ __launch_bounds__(256) void raster_setup(const float* __restrict__ pos, Workspace ws, RasterParams p) {
+__global__ __launch_bounds__(kWorkgroup) void raster_setup(const float* __restrict__ pos, Workspace ws, RasterParams p) {
     const int v = blockIdx.x * 256 + threadIdx.x;
     if (v == 0) *ws.counter = 0ull;
     if (v >= p.vertex_count) return;
     ws.screen[v] = clip_vertex(pos, v, p.model, p.vp, p.width, p.height);
 }
 
-__global__ __launch_bounds__(256) void raster_clear_vis(unsigned long long* vis, size_t n) {
+__global__ __launch_bounds__(kWorkgroup) void raster_clear_vis(unsigned long long* vis, size_t n) {
     const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
     if (i < n) vis[i] = ((unsigned long long)__float_as_uint(1.0f) << 32) | KEY_EMPTY;
 }
 
-__global__ __launch_bounds__(256) void raster_small(const uint32_t* __restrict__ idx, Workspace ws, RasterParams p,
+__global__ __launch_bounds__(kWorkgroup) void raster_small(const uint32_t* __restrict__ idx, Workspace ws, RasterParams p,
                                                     void* target, size_t pitch) {
     const int id = blockIdx.x * 256 + threadIdx.x;
     if (id >= p.triangle_count) return;
@@ -269,7 +269,7 @@ __device__ __forceinline__ float edge_max(f3 r, float x0, float x1, float y0, fl
 }
 
 // One wave per work item (triangle, 32x32 tile of its box): 64 lanes, 2 rows per step.
-__global__ __launch_bounds__(256) void raster_big(const uint32_t* __restrict__ idx, Workspace ws, RasterParams p,
+__global__ __launch_bounds__(kWorkgroup) void raster_big(const uint32_t* __restrict__ idx, Workspace ws, RasterParams p,
                                                   void* target, size_t pitch) {
     const unsigned long long c = *ws.counter;
     const uint32_t n_entries = (uint32_t)(c >> ENTRY_SHIFT), count = (uint32_t)(c & ((1ull << ENTRY_SHIFT) - 1));
@@ -547,7 +547,7 @@ __device__ __forceinline__ VtxData vertex_data(const soc_mesh& mesh, uint32_t v,
     return d;
 }
 
-__global__ __launch_bounds__(256) void gbuffer_vertex_setup(soc_mesh mesh, float4* __restrict__ vd, ResolveParams p) {
+__global__ __launch_bounds__(kWorkgroup) void gbuffer_vertex_setup(soc_mesh mesh, float4* __restrict__ vd, ResolveParams p) {
     const int v = blockIdx.x * 256 + threadIdx.x;
     if (v >= mesh.vertex_count) return;
     const VtxData d = vertex_data(mesh, (uint32_t)v, p);
@@ -565,7 +565,7 @@ __device__ __forceinline__ VtxData fetch_vertex(const soc_mesh& mesh, const floa
 }
 
 template <bool PRE>
-__global__ __launch_bounds__(256) void gbuffer_resolve(soc_mesh mesh, const soc_material* __restrict__ mats,
+__global__ __launch_bounds__(kWorkgroup) void gbuffer_resolve(soc_mesh mesh, const soc_material* __restrict__ mats,
                                                        const unsigned long long* __restrict__ vis, DImg depth,
                                                        DImg albedo, DImg emissive, DImg normal, DImg velocity,
                                                        const float4* __restrict__ vd, ResolveParams p) {
@@ -716,10 +716,10 @@ RasterParams make_raster_params(const soc_mesh* mesh, const float* vp, int W, in
 int launch_raster(const soc_mesh* mesh, const RasterParams& p, void* target, size_t pitch, void* workspace,
                   hipStream_t s, const char* pass) {
     Workspace ws = carve(workspace, mesh->vertex_count, mesh->triangle_count);
-    raster_setup<<<ceil_div(max(mesh->vertex_count, 1), 256), 256, 0, s>>>(mesh->positions, ws, p);
+    launch("raster_setup", kWorkgroup, raster_setup, ceil_div(max(mesh->vertex_count, 1), 256), kWorkgroup, 0, s, mesh->positions, ws, p);
     if (mesh->triangle_count > 0) {
-        raster_small<<<ceil_div(mesh->triangle_count, 256), 256, 0, s>>>(mesh->indices, ws, p, target, pitch);
-        raster_big<<<2048, 256, 0, s>>>(mesh->indices, ws, p, target, pitch);
+        launch("raster_small", kWorkgroup, raster_small, ceil_div(mesh->triangle_count, 256), kWorkgroup, 0, s, mesh->indices, ws, p, target, pitch);
+        launch("raster_big", kWorkgroup, raster_big, 2048, kWorkgroup, 0, s, mesh->indices, ws, p, target, pitch);
     }
     return check_launch(pass);
 }
@@ -745,7 +745,7 @@ extern "C" int soc_raster_visibility(const soc_mesh* mesh, const float view_proj
     hipStream_t s = hs(stream);
     if (clear) {
         const size_t n = (size_t)width * height;
-        raster_clear_vis<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(reinterpret_cast<unsigned long long*>(visibility), n);
+        launch("raster_clear_vis", kWorkgroup, raster_clear_vis, (unsigned)((n + 255) / 256), kWorkgroup, 0, s, reinterpret_cast<unsigned long long*>(visibility), n);
     }
     RasterParams p = make_raster_params(mesh, view_projection, width, height, cull);
     return launch_raster(mesh, p, visibility, (size_t)width * 8, workspace, s, "raster_visibility");
@@ -804,11 +804,11 @@ extern "C" int soc_gbuffer_resolve(const soc_globals* g, const soc_mesh* mesh, c
     if (workspace) {   // per-vertex outputs once, then the per-pixel resolve reads them
         const Workspace ws = carve(workspace, mesh->vertex_count, mesh->triangle_count);
         if (mesh->vertex_count > 0)
-            gbuffer_vertex_setup<<<ceil_div(mesh->vertex_count, 256), 256, 0, hs(stream)>>>(*mesh, ws.vdata, p);
-        gbuffer_resolve<true><<<grd, blk, 0, hs(stream)>>>(*mesh, d_materials, vis, dimg(depth), dimg(albedo),
+            launch("gbuffer_vertex_setup", kWorkgroup, gbuffer_vertex_setup, ceil_div(mesh->vertex_count, 256), kWorkgroup, 0, hs(stream), *mesh, ws.vdata, p);
+        launch("gbuffer_resolve", kWorkgroup, gbuffer_resolve<true>, grd, blk, 0, hs(stream), *mesh, d_materials, vis, dimg(depth), dimg(albedo),
                                                            dimg(emissive), dimg(normal), dimg(velocity), ws.vdata, p);
     } else {
-        gbuffer_resolve<false><<<grd, blk, 0, hs(stream)>>>(*mesh, d_materials, vis, dimg(depth), dimg(albedo),
+        launch("gbuffer_resolve", kWorkgroup, gbuffer_resolve<false>, grd, blk, 0, hs(stream), *mesh, d_materials, vis, dimg(depth), dimg(albedo),
                                                             dimg(emissive), dimg(normal), dimg(velocity), nullptr, p);
     }
     return check_launch("gbuffer_resolve");

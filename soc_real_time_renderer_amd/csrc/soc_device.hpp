@@ -11,6 +11,10 @@
 
 namespace soc {
 
+// Flat work-group bound of the 256-lane kernels: their __launch_bounds__ and the bound their launchers check
+// (soc_internal.hpp launch()).
+constexpr int kWorkgroup = 256;
+
 struct DImg {          // device view of a soc_img
     char* data;
     int w, h, pitch;

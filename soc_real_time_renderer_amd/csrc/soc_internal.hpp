@@ -56,8 +56,21 @@ inline float recip_rn(int n) {
     return n >= 1 && n <= 16384 ? 1.0f / (float)n : 0.0f;
 }
 
-// Checks the launch that was just issued.
+// Checks the launch that was just issued (and a block shape launch() rejected: SOC_E_INVALID_ARG).
 int check_launch(const char* pass);
+
+// Launch geometry. Every kernel's flat work-group bound (its __launch_bounds__ / amdgpu_flat_work_group_size) is a
+// named constant (kWorkgroup, kSunvisLanes, kSsaoTileLanes, kTaaLdsLanes, kThreads, kBins) that its launcher passes to
+// launch() as `bound`. A block of more lanes than the bound, or of none, is not launched: the host records
+// SOC_E_INVALID_ARG naming the kernel and the launcher's check_launch returns it, before any HIP call (a launch over
+// the bound would otherwise fail on the device as "unspecified launch failure").
+bool block_fits(const char* kernel, int bound, dim3 block);
+template <typename... P, typename... A>
+inline void launch(const char* kernel, int bound, void (*k)(P...), dim3 grid, dim3 block, size_t lds, hipStream_t s,
+                   A&&... args) {
+    if (!block_fits(kernel, bound, block)) return;
+    k<<<grid, block, lds, s>>>(static_cast<P>(args)...);
+}
 
 inline unsigned ceil_div(unsigned a, unsigned b) { return (a + b - 1) / b; }
 

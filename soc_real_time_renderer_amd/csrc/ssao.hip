@@ -62,7 +62,7 @@ __device__ float2 ssao_random_vec(float u, float v, int noise_w) {
     return float2{n1 / l, n2 / l};
 }
 
-__global__ __launch_bounds__(256) void ssao_noise_kernel(int tw, int th, int noise_w, float2* __restrict__ table) {
+__global__ __launch_bounds__(kWorkgroup) void ssao_noise_kernel(int tw, int th, int noise_w, float2* __restrict__ table) {
     const int x = blockIdx.x * 64 + threadIdx.x, y = blockIdx.y * 4 + threadIdx.y;
     if (x >= tw || y >= th) return;
     table[(size_t)y * tw + x] = ssao_random_vec(centre_uv(x, tw), centre_uv(y, th), noise_w);
@@ -286,7 +286,7 @@ __device__ __forceinline__ void ssao_pixel(int x, int y, const DImg& depth, cons
 }
 
 template <bool TABLE, bool SPARSE_IP, bool FULL>
-__global__ __launch_bounds__(256) void ssao_kernel(DImg depth, DImg normal, DImg target, const float2* __restrict__ table,
+__global__ __launch_bounds__(kWorkgroup) void ssao_kernel(DImg depth, DImg normal, DImg target, const float2* __restrict__ table,
                                                    SsaoParams p) {
     int bx, by;
     xcd_order(p.swz, bx, by);
@@ -326,6 +326,10 @@ struct LdsQuad {
     }
 };
 
+// The default tile: 64 x 16 half-res pixels (1024 lanes), a 32-texel halo (tile sweep: profiles/r03_ssao_tile_sweep.txt);
+// kSsaoTileLanes is the launch bound its launcher checks.
+constexpr int kSsaoTX = 64, kSsaoTY = 16, kSsaoHalo = 32, kSsaoTileLanes = kSsaoTX * kSsaoTY;
+
 template <bool TABLE, bool SPARSE_IP, bool FULL, int TXP, int TYP, int HALO, int UNROLL, bool PK = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(TXP * TYP, TXP * TYP)))
 __attribute__((amdgpu_waves_per_eu(TXP * TYP >= 1024 ? 8 : TXP * TYP >= 512 ? 4 : 2)))
@@ -356,7 +360,7 @@ void ssao_lds_kernel(DImg depth, DImg normal, DImg target, const float2* __restr
 }
 
 // ssao_blur.inl:91-106: 4x4 box at offsets -2..+1 (x outer, y inner), all taps on texel centres.
-__global__ __launch_bounds__(256) void ssao_blur_kernel(DImg src, DImg dst) {
+__global__ __launch_bounds__(kWorkgroup) void ssao_blur_kernel(DImg src, DImg dst) {
 #pragma clang fp contract(off)
     const int x = blockIdx.x * 64 + threadIdx.x, y = blockIdx.y * 4 + threadIdx.y;
     if (x >= dst.w || y >= dst.h) return;
@@ -372,7 +376,7 @@ __global__ __launch_bounds__(256) void ssao_blur_kernel(DImg src, DImg dst) {
 }
 
 // Generic blur for a target whose extent differs from the source (taps are real bilinear samples).
-__global__ __launch_bounds__(256) void ssao_blur_generic(DImg src, DImg dst, float tx, float ty) {
+__global__ __launch_bounds__(kWorkgroup) void ssao_blur_generic(DImg src, DImg dst, float tx, float ty) {
 #pragma clang fp contract(off)
     const int x = blockIdx.x * 64 + threadIdx.x, y = blockIdx.y * 4 + threadIdx.y;
     if (x >= dst.w || y >= dst.h) return;
@@ -425,7 +429,7 @@ extern "C" int soc_ssao_prepare_noise(soc_img normal, soc_img target, float* noi
     if (normal.width <= 0 || target.width <= 0 || target.height <= 0)
         return set_error(SOC_E_INVALID_ARG, "soc_ssao_prepare_noise: bad extents");
     dim3 blk(64, 4), grd(ceil_div(target.width, 64), ceil_div(target.height, 4));
-    ssao_noise_kernel<<<grd, blk, 0, hs(stream)>>>(target.width, target.height, normal.width,
+    launch("ssao_noise_kernel", kWorkgroup, ssao_noise_kernel, grd, blk, 0, hs(stream), target.width, target.height, normal.width,
                                                    reinterpret_cast<float2*>(noise_table));
     return check_launch("ssao_prepare_noise");
 }
@@ -453,7 +457,7 @@ extern "C" int soc_ssao_generation(const soc_globals* g, soc_img depth, soc_img 
     const float2* tb = reinterpret_cast<const float2*>(noise_table);
     hipStream_t st = hs(stream);
     DImg dd = dimg(depth), dn = dimg(normal), dt = dimg(target);
-#define SOC_SSAO_LAUNCH(T, B, F) ssao_kernel<T, B, F><<<grd, blk, 0, st>>>(dd, dn, dt, tb, p)
+#define SOC_SSAO_LAUNCH(T, B, F) launch("ssao_kernel", kWorkgroup, ssao_kernel<T, B, F>, grd, blk, 0, st, dd, dn, dt, tb, p)
     const bool full = p.ksize == SOC_SSAO_MAX_KERNEL;
     // default: the LDS-tiled kernel (64 x 16 pixels, 32-texel halo) in the contiguous-eighths XCD order; SOC_SSAO_TILE=0
     // selects the plain gather kernel (the same bits: tests/test_gpu_parity.py)
@@ -461,8 +465,9 @@ extern "C" int soc_ssao_generation(const soc_globals* g, soc_img depth, soc_img 
     if (noise_table && sip && full && tiled) {
         SsaoParams pt = p;
         pt.swz = 1;
-        const dim3 g(ceil_div(target.width, 64), ceil_div(target.height, 16));
-        ssao_lds_kernel<true, true, true, 64, 16, 32, 2, true><<<g, 1024, 0, st>>>(dd, dn, dt, tb, pt);
+        const dim3 g(ceil_div(target.width, kSsaoTX), ceil_div(target.height, kSsaoTY));
+        launch("ssao_lds_kernel", kSsaoTileLanes, ssao_lds_kernel<true, true, true, kSsaoTX, kSsaoTY, kSsaoHalo, 2, true>, g,
+               kSsaoTileLanes, 0, st, dd, dn, dt, tb, pt);
     } else if (noise_table && sip && full) SOC_SSAO_LAUNCH(true, true, true);
     else if (noise_table && sip) SOC_SSAO_LAUNCH(true, true, false);
     else if (noise_table) SOC_SSAO_LAUNCH(true, false, false);
@@ -480,9 +485,9 @@ extern "C" int soc_ssao_blur(const soc_globals* g, soc_img ssao, soc_img target,
     if (ssao.data == target.data) return set_error(SOC_E_INVALID_ARG, "soc_ssao_blur: source and target alias");
     dim3 blk(64, 4), grd(ceil_div(target.width, 64), ceil_div(target.height, 4));
     if (ssao.width == target.width && ssao.height == target.height && ssao.width <= 8192 && ssao.height <= 8192)
-        ssao_blur_kernel<<<grd, blk, 0, hs(stream)>>>(dimg(ssao), dimg(target));
+        launch("ssao_blur_kernel", kWorkgroup, ssao_blur_kernel, grd, blk, 0, hs(stream), dimg(ssao), dimg(target));
     else
-        ssao_blur_generic<<<grd, blk, 0, hs(stream)>>>(dimg(ssao), dimg(target), 1.0f / (float)ssao.width,
+        launch("ssao_blur_generic", kWorkgroup, ssao_blur_generic, grd, blk, 0, hs(stream), dimg(ssao), dimg(target), 1.0f / (float)ssao.width,
                                                        1.0f / (float)ssao.height);
     return check_launch("ssao_blur");
 }

@@ -48,7 +48,7 @@ __device__ __forceinline__ float gauss_w(int idx) {
 
 // Fast path: colour, depth and velocity have the target extent (== resolution): every neighbourhood
 // tap is a texel centre (clamped at the border), so plain loads replace the bilinear samples.
-__global__ __launch_bounds__(256) void taa_fast(DImg target, DImg cur, DImg prev, DImg vel, DImg pvel, DImg depth,
+__global__ __launch_bounds__(kWorkgroup) void taa_fast(DImg target, DImg cur, DImg prev, DImg vel, DImg pvel, DImg depth,
                                                 DImg vel_out, TaaParams p) {
     const int x = blockIdx.x * BX + threadIdx.x, y = blockIdx.y * BY + threadIdx.y;
     if (x >= target.w || y >= target.h) return;
@@ -260,7 +260,7 @@ __device__ __forceinline__ uint32_t from_right(uint32_t v) {  // lane i <- lane 
 // neighbours (62 output pairs per wave), so no lane issues a side-column load at all: the kernel is bound
 // by texture-path instructions, not bytes.
 template <bool TM, int NBR = 2>
-__global__ __launch_bounds__(256) void taa_pair2(DImg target, DImg cur, DImg prev, DImg vel, DImg pvel, DImg depth,
+__global__ __launch_bounds__(kWorkgroup) void taa_pair2(DImg target, DImg cur, DImg prev, DImg vel, DImg pvel, DImg depth,
                                                  DImg vel_out, TaaParams p, TmOut tm) {
     int tbx, tby;
     xcd_order(p.swz, tbx, tby);
@@ -336,7 +336,9 @@ constexpr int kTaaPairs = 64;                                     // output pair
 constexpr int kTaaTP = kTaaPairs + 2;                             // staged pairs (pair p0 - 1 .. p0 + 64)
 constexpr int kTaaTQ = kTaaPairs / 2 + 2;                         // staged depth quads (quad q0 - 1 .. q0 + 32)
 
-template <bool TM, int kTaaRows = 4>   // rows per workgroup: 4 measured against 2 and 8 (profiles/r03_ab_taa_lds.txt)
+constexpr int kTaaLdsRows = 4;                                   // rows per workgroup: 4 measured against 2 and 8
+constexpr int kTaaLdsLanes = 64 * kTaaLdsRows;                    // (profiles/r03_ab_taa_lds.txt); the launch bound
+template <bool TM, int kTaaRows = kTaaLdsRows>
 __global__ __launch_bounds__(64 * kTaaRows) void taa_lds(DImg target, DImg cur, DImg prev, DImg vel, DImg pvel, DImg depth,
                                                          DImg vel_out, TaaParams p, TmOut tm) {
     constexpr int kTaaTR = kTaaRows + 2, NT = 64 * kTaaRows;   // staged rows y0 - 1 .. y0 + kTaaRows
@@ -408,7 +410,7 @@ __global__ __launch_bounds__(64 * kTaaRows) void taa_lds(DImg target, DImg cur, 
                       [&]() { return vt[ty + 1][pl + 1]; });
 }
 
-__global__ __launch_bounds__(256) void taa_generic(DImg target, DImg cur, DImg prev, DImg vel, DImg pvel, DImg depth,
+__global__ __launch_bounds__(kWorkgroup) void taa_generic(DImg target, DImg cur, DImg prev, DImg vel, DImg pvel, DImg depth,
                                                    DImg vel_out, TaaParams p) {
     const int x = blockIdx.x * BX + threadIdx.x, y = blockIdx.y * BY + threadIdx.y;
     if (x >= target.w || y >= target.h) return;
@@ -436,7 +438,7 @@ __global__ __launch_bounds__(256) void taa_generic(DImg target, DImg cur, DImg p
     if (vel_out.data && x < vel.w && y < vel.h) row_ptr_w<uint2>(vel_out, y)[x] = row_ptr<uint2>(vel, y)[x];
 }
 
-__global__ __launch_bounds__(256) void copy_rows(const char* __restrict__ src, int spitch, char* __restrict__ dst,
+__global__ __launch_bounds__(kWorkgroup) void copy_rows(const char* __restrict__ src, int spitch, char* __restrict__ dst,
                                                  int dpitch, int row_bytes, int rows) {
     const int y = blockIdx.y;
     if (y >= rows) return;
@@ -509,30 +511,30 @@ int taa_launch(const soc_globals* g, soc_img target, soc_img current_color, soc_
         if (nbr == 3 && a16(depth)) {
             const dim3 gl(ceil_div(W / 2, kTaaPairs), ceil_div(H, 4));
             if (tm)
-                taa_lds<true><<<gl, blk_h, 0, hs(stream)>>>(dimg(target), dimg(current_color), dimg(previous_color),
+                launch("taa_lds", kTaaLdsLanes, taa_lds<true>, gl, blk_h, 0, hs(stream), dimg(target), dimg(current_color), dimg(previous_color),
                                                           dimg(current_velocity), dimg(previous_velocity), dimg(depth), vo, p, *tm);
             else
-                taa_lds<false><<<gl, blk_h, 0, hs(stream)>>>(dimg(target), dimg(current_color), dimg(previous_color),
+                launch("taa_lds", kTaaLdsLanes, taa_lds<false>, gl, blk_h, 0, hs(stream), dimg(target), dimg(current_color), dimg(previous_color),
                                                            dimg(current_velocity), dimg(previous_velocity), dimg(depth), vo, p,
                                                            TmOut{});
         } else if (tm && nbr >= 2)
-            taa_pair2<true, 2><<<g2_h, blk_h, 0, hs(stream)>>>(dimg(target), dimg(current_color), dimg(previous_color),
+            launch("taa_pair2", kWorkgroup, taa_pair2<true, 2>, g2_h, blk_h, 0, hs(stream), dimg(target), dimg(current_color), dimg(previous_color),
                                                        dimg(current_velocity), dimg(previous_velocity), dimg(depth), vo, p, *tm);
         else if (tm && nbr == 0)
-            taa_pair2<true, 0><<<g2, blk, 0, hs(stream)>>>(dimg(target), dimg(current_color), dimg(previous_color),
+            launch("taa_pair2", kWorkgroup, taa_pair2<true, 0>, g2, blk, 0, hs(stream), dimg(target), dimg(current_color), dimg(previous_color),
                                                        dimg(current_velocity), dimg(previous_velocity), dimg(depth), vo, p, *tm);
         else if (tm)
-            taa_pair2<true, 1><<<g2, blk, 0, hs(stream)>>>(dimg(target), dimg(current_color), dimg(previous_color),
+            launch("taa_pair2", kWorkgroup, taa_pair2<true, 1>, g2, blk, 0, hs(stream), dimg(target), dimg(current_color), dimg(previous_color),
                                                        dimg(current_velocity), dimg(previous_velocity), dimg(depth), vo, p, *tm);
         else
-            taa_pair2<false, 2><<<g2_h, blk_h, 0, hs(stream)>>>(dimg(target), dimg(current_color), dimg(previous_color),
+            launch("taa_pair2", kWorkgroup, taa_pair2<false, 2>, g2_h, blk_h, 0, hs(stream), dimg(target), dimg(current_color), dimg(previous_color),
                                                         dimg(current_velocity), dimg(previous_velocity), dimg(depth), vo, p,
                                                         TmOut{});
     } else if (fast)
-        taa_fast<<<grd, blk, 0, hs(stream)>>>(dimg(target), dimg(current_color), dimg(previous_color), dimg(current_velocity),
+        launch("taa_fast", kWorkgroup, taa_fast, grd, blk, 0, hs(stream), dimg(target), dimg(current_color), dimg(previous_color), dimg(current_velocity),
                                               dimg(previous_velocity), dimg(depth), vo, p);
     else
-        taa_generic<<<grd, blk, 0, hs(stream)>>>(dimg(target), dimg(current_color), dimg(previous_color),
+        launch("taa_generic", kWorkgroup, taa_generic, grd, blk, 0, hs(stream), dimg(target), dimg(current_color), dimg(previous_color),
                                                  dimg(current_velocity), dimg(previous_velocity), dimg(depth), vo, p);
     return check_launch("temporal_antialiasing");
 }
@@ -596,7 +598,7 @@ extern "C" int soc_copy_image(soc_img target, soc_img source, soc_stream stream)
         return SOC_OK;
     }
     dim3 grd(ceil_div(ceil_div(row_bytes, 16), 256), source.height);
-    copy_rows<<<grd, 256, 0, hs(stream)>>>(static_cast<const char*>(source.data), source.pitch_bytes,
+    launch("copy_rows", kWorkgroup, copy_rows, grd, kWorkgroup, 0, hs(stream), static_cast<const char*>(source.data), source.pitch_bytes,
                                            static_cast<char*>(target.data), target.pitch_bytes, row_bytes, source.height);
     return check_launch("copy_image");
 }

@@ -17,7 +17,7 @@ __device__ __forceinline__ f3 normalize_nc(f3 a) {
     return f3{a.x / l, a.y / l, a.z / l};
 }
 
-__global__ __launch_bounds__(256) void height_to_normal_kernel(DImg height, DImg target) {
+__global__ __launch_bounds__(kWorkgroup) void height_to_normal_kernel(DImg height, DImg target) {
 #pragma clang fp contract(off)
     const int x = blockIdx.x * 64 + threadIdx.x, y = blockIdx.y * 4 + threadIdx.y;
     const int W = height.w, H = height.h;
@@ -52,7 +52,7 @@ struct TessParams {
     float scale_x, scale_z, hscale, mid, off[3];
 };
 
-__global__ __launch_bounds__(256) void terrain_tess_vertices(DImg height, TessParams p, float* __restrict__ pos,
+__global__ __launch_bounds__(kWorkgroup) void terrain_tess_vertices(DImg height, TessParams p, float* __restrict__ pos,
                                                              float* __restrict__ nrm, float* __restrict__ uvs) {
 #pragma clang fp contract(off)
     const int k = blockIdx.x * 256 + threadIdx.x;
@@ -81,7 +81,7 @@ __global__ __launch_bounds__(256) void terrain_tess_vertices(DImg height, TessPa
 
 // Two triangles per tessellated quad, counter-clockwise seen from above, the diagonal alternating with the
 // triangle id's parity as the host terrain mesh (scene_synth.c).
-__global__ __launch_bounds__(256) void terrain_tess_indices(int nv, uint32_t* __restrict__ idx) {
+__global__ __launch_bounds__(kWorkgroup) void terrain_tess_indices(int nv, uint32_t* __restrict__ idx) {
     const int id = blockIdx.x * 256 + threadIdx.x, segs = nv - 1;
     if (id >= 2 * segs * segs) return;
     const int q = id >> 1, qi = q % segs, qj = q / segs;
@@ -123,8 +123,8 @@ extern "C" int soc_terrain_tessellate(const soc_globals* g, soc_img heightmap, i
     p.hscale = g->terrain_height_scale;
     p.mid = g->terrain_midpoint;
     for (int i = 0; i < 3; ++i) p.off[i] = g->terrain_offset[i];
-    terrain_tess_vertices<<<ceil_div(V, 256), 256, 0, hs(stream)>>>(dimg(heightmap), p, positions, normals, uvs);
-    terrain_tess_indices<<<ceil_div(T, 256), 256, 0, hs(stream)>>>(p.nv, indices);
+    launch("terrain_tess_vertices", kWorkgroup, terrain_tess_vertices, ceil_div(V, 256), kWorkgroup, 0, hs(stream), dimg(heightmap), p, positions, normals, uvs);
+    launch("terrain_tess_indices", kWorkgroup, terrain_tess_indices, ceil_div(T, 256), kWorkgroup, 0, hs(stream), p.nv, indices);
     return check_launch("terrain_tessellate");
 }
 
@@ -135,6 +135,6 @@ extern "C" int soc_height_to_normal(soc_img heightmap, soc_img normal_target, so
     if (heightmap.width != normal_target.width || heightmap.height != normal_target.height)
         return set_error(SOC_E_SHAPE, "soc_height_to_normal: the normal map must have the heightmap's extent");
     dim3 blk(64, 4), grd(ceil_div(heightmap.width, 64), ceil_div(heightmap.height, 4));
-    height_to_normal_kernel<<<grd, blk, 0, hs(stream)>>>(dimg(heightmap), dimg(normal_target));
+    launch("height_to_normal_kernel", kWorkgroup, height_to_normal_kernel, grd, blk, 0, hs(stream), dimg(heightmap), dimg(normal_target));
     return check_launch("height_to_normal");
 }

@@ -61,7 +61,7 @@ __device__ __forceinline__ uint32_t srgb_encode_code(float c, const SrgbTables& 
     return k;
 }
 
-__global__ __launch_bounds__(256) void mip_blit(DImg src, DImg dst, int srgb, SrgbTables tabs) {
+__global__ __launch_bounds__(kWorkgroup) void mip_blit(DImg src, DImg dst, int srgb, SrgbTables tabs) {
 #pragma clang fp contract(off)
     const int x = blockIdx.x * 64 + threadIdx.x, y = blockIdx.y * 4 + threadIdx.y;
     if (x >= dst.w || y >= dst.h) return;
@@ -114,7 +114,7 @@ extern "C" int soc_generate_mips(soc_img texture, soc_stream stream) {
         const size_t od = mip_offset(W, H, texture.pitch_bytes, k, wd, hd);
         const DImg src{base + os, ws, hs_, k == 1 ? texture.pitch_bytes : 4 * ws};
         const DImg dst{base + od, wd, hd, 4 * wd};
-        mip_blit<<<dim3(ceil_div(wd, 64), ceil_div(hd, 4)), dim3(64, 4), 0, hs(stream)>>>(src, dst, srgb, srgb_tables());
+        launch("mip_blit", kWorkgroup, mip_blit, dim3(ceil_div(wd, 64), ceil_div(hd, 4)), dim3(64, 4), 0, hs(stream), src, dst, srgb, srgb_tables());
     }
     return check_launch("generate_mips");
 }

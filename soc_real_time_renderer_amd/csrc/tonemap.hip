@@ -28,7 +28,7 @@ constexpr int BX = 64, BY = 4;
 
 // Fast path: same extent, even width, 16-B aligned source rows.
 template <int FMT>
-__global__ __launch_bounds__(256) void tonemap_pair(DImg src, DImg dst, const soc_auto_exposure* __restrict__ ae, TmParams p) {
+__global__ __launch_bounds__(kWorkgroup) void tonemap_pair(DImg src, DImg dst, const soc_auto_exposure* __restrict__ ae, TmParams p) {
     const int x = (blockIdx.x * BX + threadIdx.x) * 2, y = blockIdx.y * BY + threadIdx.y;
     if (x >= dst.w || y >= dst.h) return;
     const float expo = exp2f(ae->exposure);   // pow(2.0, exposure)
@@ -45,7 +45,7 @@ __global__ __launch_bounds__(256) void tonemap_pair(DImg src, DImg dst, const so
 }
 
 template <int FMT>
-__global__ __launch_bounds__(256) void tonemap_generic(DImg src, DImg dst, const soc_auto_exposure* __restrict__ ae, TmParams p) {
+__global__ __launch_bounds__(kWorkgroup) void tonemap_generic(DImg src, DImg dst, const soc_auto_exposure* __restrict__ ae, TmParams p) {
     const int x = blockIdx.x * BX + threadIdx.x, y = blockIdx.y * BY + threadIdx.y;
     if (x >= dst.w || y >= dst.h) return;
     const float expo = exp2f(ae->exposure);
@@ -61,10 +61,10 @@ void launch(const soc_img& color, const soc_img& target, const soc_auto_exposure
                       (reinterpret_cast<uintptr_t>(target.data) & 7u) == 0 && (target.pitch_bytes & 7) == 0;
     if (pair) {
         dim3 blk(BX, BY), grd(ceil_div(W / 2, BX), ceil_div(H, BY));
-        tonemap_pair<FMT><<<grd, blk, 0, s>>>(dimg(color), dimg(target), ae, p);
+        launch("tonemap_pair", kWorkgroup, tonemap_pair<FMT>, grd, blk, 0, s, dimg(color), dimg(target), ae, p);
     } else {
         dim3 blk(BX, BY), grd(ceil_div(W, BX), ceil_div(H, BY));
-        tonemap_generic<FMT><<<grd, blk, 0, s>>>(dimg(color), dimg(target), ae, p);
+        launch("tonemap_generic", kWorkgroup, tonemap_generic<FMT>, grd, blk, 0, s, dimg(color), dimg(target), ae, p);
     }
 }
 

@@ -37,3 +37,14 @@ def _tuning_knobs_fresh(monkeypatch):
         m = sys.modules["soc_real_time_renderer_amd"]
         if getattr(m, "_LIB", None) is not None:
             m.reload_tuning()
+
+
+def pytest_terminal_summary(terminalreporter):
+    """The achieved errors of the full-frame parity checks (helpers.frame_parity), one JSON line per frame."""
+    import json
+    h = sys.modules.get("helpers")
+    reps = getattr(h, "PARITY_REPORTS", None) if h else None
+    if reps:
+        terminalreporter.section("full-frame parity: achieved errors")
+        for r in reps:
+            terminalreporter.write_line(json.dumps(r))

@@ -76,6 +76,35 @@ def test_argument_errors_without_gpu(soc):
         soc.cloud_rendering(g, None, None, None, stream=0)
 
 
+def test_block_shape_over_the_launch_bound_is_rejected_without_gpu(soc):
+    """The launch-geometry check (soc_check_block_shape; every launcher applies it with its kernel's bound before the
+    launch): round 3's 64 x 16 SSAO-blur block against the kernel's 256-lane bound is refused on the host with
+    SOC_E_INVALID_ARG, the shapes the library launches pass, an empty block is refused."""
+    from soc_real_time_renderer_amd import _abi
+    lib = soc.lib()
+    assert lib.soc_check_block_shape(256, 64, 16, 1) == _abi.SOC_E_INVALID_ARG
+    assert b"1024 lanes" in lib.soc_last_error_string() and b"256" in lib.soc_last_error_string()
+    assert lib.soc_check_block_shape(256, 64, 4, 1) == 0
+    assert lib.soc_check_block_shape(1024, 1024, 1, 1) == 0       # the SSAO tile kernel
+    assert lib.soc_check_block_shape(512, 512, 1, 1) == 0         # clouds_sunvis
+    assert lib.soc_check_block_shape(512, 1024, 1, 1) == _abi.SOC_E_INVALID_ARG
+    assert lib.soc_check_block_shape(256, 0, 4, 1) == _abi.SOC_E_INVALID_ARG
+    assert lib.soc_check_block_shape(256, -1, 4, 1) == _abi.SOC_E_INVALID_ARG
+
+
+def test_every_launch_goes_through_the_geometry_check():
+    """No kernel is launched with a bare triple-chevron outside the checked launch() helper (soc_internal.hpp), and
+    every 256-lane kernel declares its bound through the shared kWorkgroup constant."""
+    import glob
+    import re
+    csrc = os.path.join(ROOT, "soc_real_time_renderer_amd", "csrc")
+    for f in glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.cpp")):
+        src = open(f).read()
+        assert "<<<" not in src, f
+        assert not re.search(r"__launch_bounds__\(\s*\d+\s*\)", src), f
+    assert "k<<<grid, block, lds, s>>>" in open(os.path.join(csrc, "soc_internal.hpp")).read()
+
+
 def test_library_is_a_gfx950_code_object():
     """The in-tree .so carries a gfx950 offload bundle (built by __graft_entry__.build)."""
     so = os.path.join(ROOT, "soc_real_time_renderer_amd", "lib", "libsoc_rt.so")

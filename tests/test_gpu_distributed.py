@@ -8,6 +8,10 @@ Checks, per frame:
   * the exchanged bins are the sum of the local ones on every rank;
   * every rank's exposure equals the oracle's wide resolve of the summed bins (|d| <= 1e-5), frame after
     frame (the exposure carries over: resolve_luminance_histogram.inl:75-79).
+Config C5 at its own size (`test_c5_4k_exchange_vs_oracle`): eight ranks on device 0, each rendering the bench's
+own C3 inputs for its camera (the Sponza-proxy mesh at 3840x2160, bench.build_inputs), two frames with the same checks;
+the local-bin check runs on each rank against the oracle histogram of its own 4K colour. Reference exchange point:
+renderer.cpp:1155-1168.
 And `bench.py --gpus 2` (self-launching its ranks) prints one line with n_gpus == 2.
 """
 import json
@@ -71,6 +75,41 @@ def test_rank_frames_exchange_vs_oracle(tmp_path, soc, oracle, ranks):
             assert abs(float(exposure[r, f]) - ae.exposure) <= 1e-5, (r, f, float(exposure[r, f]), ae.exposure)
         assert all(exposure[r, f] == exposure[0, f] for r in range(world))
     # the ranks rendered different cameras
+    for r in range(1, world):
+        assert not np.array_equal(local[0, 0], local[r, 0]), r
+
+
+def test_c5_4k_exchange_vs_oracle(tmp_path, soc, oracle):
+    import bench
+    from soc_real_time_renderer_amd import multi_gpu
+    ranks = 8
+    out = tmp_path / "c5.npz"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
+           "--master-addr", "127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "tests", "dist_frame_worker.py")]
+    p = subprocess.run(cmd, env=_env(SOC_DIST_OUT=str(out), SOC_DIST_CONFIG="c3"), capture_output=True, text=True,
+                       timeout=400)
+    errs = [ln for ln in p.stderr.splitlines() if "Error" in ln or "error" in ln]
+    assert p.returncode == 0, "\n".join(errs[:20]) + p.stdout[-2000:] + p.stderr[-4000:]
+    d = np.load(out)
+    world, W, H = int(d["world"]), int(d["W"]), int(d["H"])
+    assert (world, W, H) == (ranks, 3840, 2160)
+    local, reduced, exposure, local_ok = d["local"], d["reduced"], d["exposure"], d["local_ok"]
+    assert local_ok.all(), local_ok          # each rank: bins == the oracle histogram of its own GPU colour
+    assert (d["sky"] < 0.5).all()
+    g = bench.make_globals(W, H, multi_gpu.camera_for_rank(0))
+    ae = soc.AutoExposure()
+    for f in range(local.shape[1]):
+        for r in range(world):
+            assert int(local[r, f].astype(np.int64).sum()) == W * H
+        summed = local[:, f].astype(np.uint64).sum(axis=0)
+        assert int(summed.sum()) == world * W * H
+        for r in range(world):
+            assert np.array_equal(reduced[r, f].astype(np.uint64), summed), (r, f)
+        ae.histogram_buckets[:] = [int(v) for v in summed]
+        total, wide = multi_gpu.exposure_pixels(world, W, H)
+        oracle.resolve_luminance_histogram(g, ae, total, wide)
+        for r in range(world):
+            assert abs(float(exposure[r, f]) - ae.exposure) <= 1e-5, (r, f, float(exposure[r, f]), ae.exposure)
     for r in range(1, world):
         assert not np.array_equal(local[0, 0], local[r, 0]), r
 

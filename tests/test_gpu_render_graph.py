@@ -167,3 +167,33 @@ def test_checkpoint_resume_bit_identical(soc, tmp_path):
     rc.close()
     with pytest.raises(ValueError):
         soc.Renderer(_frame(soc, 64, 36, sponza_inputs(64, 36)[1])).load_state(ckpt)
+
+
+def test_checkpoint_rejected_before_any_write(soc):
+    """load_state checks the whole checkpoint before it writes anything: a history_index outside {0, 1} or an
+    AutoExposure block of another dtype raises ValueError and leaves the frame's history images and AutoExposure as
+    they were."""
+    W, H = 64, 36
+    _, gb = sponza_inputs(W, H, elapsed=10.0)
+    fr = _frame(soc, W, H, gb)
+    r = soc.Renderer(fr)
+    r.execute(globals_for_frames(W, H))
+    torch.cuda.synchronize()
+    st = r.save_state()
+    before = {"h0": fr["history_color"][0].clone(), "h1": fr["history_color"][1].clone(),
+              "ae": fr["auto_exposure"].clone()}
+    junk = dict(st)
+    junk["history_color"] = np.full_like(st["history_color"], 7.0)
+    for bad in ({**junk, "history_index": np.int32(-1)}, {**junk, "history_index": np.int32(2)},
+                {**junk, "auto_exposure": st["auto_exposure"].astype(np.float32)}):
+        with pytest.raises(ValueError):
+            r.load_state(bad)
+        torch.cuda.synchronize()
+        assert torch.equal(fr["history_color"][0], before["h0"]) and torch.equal(fr["history_color"][1], before["h1"])
+        assert torch.equal(fr["auto_exposure"], before["ae"])
+    r.close()
+
+
+def globals_for_frames(W, H):
+    from helpers import globals_for
+    return globals_for(W, H, elapsed=10.0)
