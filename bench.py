@@ -160,6 +160,28 @@ def valu_bound(kernel, us):
     return None
 
 
+def clouds_roofline(config, W, H, us):
+    """CloudRendering against the FP32 VALU / transcendental peaks: the reference GLSL's FLOPs and
+    transcendentals of this frame, tallied per function by tools/clouds_flops.py from an instrumented oracle run on the
+    same inputs (committed as profiles/*clouds_flops.json), over the pass's measured time `us` (the serial per-pass
+    loop: the pass alone on the GPU)."""
+    import glob
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import clouds_flops
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*clouds_flops.json")))
+    if not files or not us:
+        return None
+    with open(files[-1]) as fh:
+        t = json.load(fh)
+    c = t.get("configs", {}).get(config)
+    if c is None or list(t.get("resolution", [])) != [W, H]:
+        return None
+    r = clouds_flops.roofline(c, us)
+    r.update({"flops_per_frame": c["flops"], "transcendentals_per_frame": c["transcendentals"],
+              "per_sky_pixel": c["per_sky_pixel"], "source": os.path.relpath(files[-1], ROOT)})
+    return r
+
+
 def cpu_baseline(W, H, host_inputs, g):
     """The oracle (plain-C restatement, OpenMP over rows) timed on this box's host cores."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -442,7 +464,11 @@ def main():
                                             "gather_bound": (ssao_gather_bound(W, H, args.scene, ssao_ms * 1e3)
                                                              if args.config == "c3" else None),
                                             "valu_bound": (valu_bound(SSAO_KERNEL, ssao_ms * 1e3)
-                                                           if pmc_ok else None)}}},
+                                                           if pmc_ok else None)},
+                         # the largest pass of the frame is VALU-bound: its compute roofline
+                         "CloudRendering": (clouds_roofline({"c3b": "c3"}.get(args.config, args.config) if args.scene == "mesh" or terrain else "", W, H,
+                                                            ms_pass.get("CloudRendering", 0.0) * 1e3)
+                                            if not args.raster else None)}},
         "ranks": per_rank,
         "allreduce_us_per_frame": (round(sum(p["allreduce_us_per_frame"] for p in per_rank) / world, 2)
                                    if world > 1 else None),
