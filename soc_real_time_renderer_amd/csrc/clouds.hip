@@ -18,6 +18,14 @@
 #ifndef SOC_CLOUDS_PROFILE
 #define SOC_CLOUDS_PROFILE 0
 #endif
+// A/B builds (make variant): octave early exits (0: lower edge after octaves 2 and 3, 1: + the upper edge,
+// 2: + the lower edge after octave 1) and the correctly rounded altitude near the layer top (0 / 1).
+#ifndef SOC_CLOUDS_EXITS
+#define SOC_CLOUDS_EXITS 2
+#endif
+#ifndef SOC_CLOUDS_RN_TOP
+#define SOC_CLOUDS_RN_TOP 1
+#endif
 
 namespace soc {
 namespace {
@@ -142,7 +150,7 @@ __device__ __forceinline__ float cloud_height_rn(f3 p) {
 }
 __device__ __forceinline__ float layer_height(f3 p) {
     const float h = cloud_height(p);
-    return fabsf(h - kMaxH) < 2.0f ? cloud_height_rn(p) : h;
+    return (SOC_CLOUDS_RN_TOP && fabsf(h - kMaxH) < 2.0f) ? cloud_height_rn(p) : h;
 }
 
 // get_clouds, :235-262, for a point whose altitude h is already known to lie inside the layer.
@@ -162,13 +170,13 @@ __device__ float clouds_at(const C& cx, f3 p, float h) {
     constexpr float kSat = 0.6f + 1e-4f;
     // octave weight x noise normalisation as one constant per octave (powers of two apart: one fma per octave)
     float n = noise3(cx, cc) * (0.5f * kNoiseNorm);
-    if (n < 0.55f - 0.4375f - 1e-4f) return 0.0f;
+    if (SOC_CLOUDS_EXITS >= 2 && n < 0.55f - 0.4375f - 1e-4f) return 0.0f;
     n = __builtin_fmaf(noise3(cx, cc * 2.0f + mv), 0.25f * kNoiseNorm, n);
     if (n < 0.55f - 0.1875f - 1e-4f) return 0.0f;
-    if (n < kSat) {
+    if (SOC_CLOUDS_EXITS < 1 || n < kSat) {
         n = __builtin_fmaf(noise3(cx, cc * 7.0f - mv), 0.125f * kNoiseNorm, n);
         if (n < 0.55f - 0.0625f - 1e-4f) return 0.0f;
-        if (n < kSat) {
+        if (SOC_CLOUDS_EXITS < 1 || n < kSat) {
             // (cc + mv) 16 == fma(cc, 16, 16 mv) exactly: scaling by a power of two commutes with the rounding
             const f3 c4 = f3{__builtin_fmaf(cc.x, 16.0f, mv.x * 16.0f), __builtin_fmaf(cc.y, 16.0f, mv.y * 16.0f),
                              __builtin_fmaf(cc.z, 16.0f, mv.z * 16.0f)};

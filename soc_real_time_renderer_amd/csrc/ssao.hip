@@ -10,6 +10,11 @@
 // identical bits.
 #include "soc_internal.hpp"
 
+// Tap-pair loop unroll of the packed path (A/B builds: make variant SRC=ssao.hip DEFS=-DSOC_SSAO_PK_UNROLL=n)
+#ifndef SOC_SSAO_PK_UNROLL
+#define SOC_SSAO_PK_UNROLL 1
+#endif
+
 namespace soc {
 namespace {
 
@@ -204,7 +209,7 @@ __device__ __forceinline__ void ssao_pixel(int x, int y, const DImg& depth, cons
     if constexpr (PK && SPARSE_IP && FULL) {
         static_assert(SOC_SSAO_MAX_KERNEL % 2 == 0, "taps are paired");
         // the same per-tap operations as the scalar loop below, two taps per packed instruction
-#pragma unroll 1
+#pragma unroll SOC_SSAO_PK_UNROLL
         for (int i = 0; i < SOC_SSAO_MAX_KERNEL; i += 2) {
             const f2v kx = {kKernel.v[i][0], kKernel.v[i + 1][0]}, ky = {kKernel.v[i][1], kKernel.v[i + 1][1]},
                       kz = {kKernel.v[i][2], kKernel.v[i + 1][2]};
