@@ -18,14 +18,6 @@
 #ifndef SOC_CLOUDS_PROFILE
 #define SOC_CLOUDS_PROFILE 0
 #endif
-// A/B builds (make variant): octave early exits (0: lower edge after octaves 2 and 3, 1: + the upper edge,
-// 2: + the lower edge after octave 1) and the correctly rounded altitude near the layer top (0 / 1).
-#ifndef SOC_CLOUDS_EXITS
-#define SOC_CLOUDS_EXITS 2
-#endif
-#ifndef SOC_CLOUDS_RN_TOP
-#define SOC_CLOUDS_RN_TOP 1
-#endif
 
 namespace soc {
 namespace {
@@ -138,51 +130,28 @@ __device__ __forceinline__ float hw_length3(f3 v) { return __builtin_amdgcn_sqrt
 // Altitude above the planet of a point given relative to the camera's ground point.
 __device__ __forceinline__ float cloud_height(f3 p) { return hw_length3(f3{p.x, p.y + kEarthRadius, p.z}) - kEarthRadius; }
 
-// The same altitude with the oracle's (and the GLSL's as written) roundings: unfused x^2 + y^2 + z^2 and a correctly
-// rounded square root. At Earth scale one ulp of |p| is 0.5 m, so the hardware form above may put a point that lies
-// within about a metre of the layer's top on the other side of it; there the density jumps (the threshold
-// (1 - e^-5) e^-2 ~ 0.13 at the top, 0 above), and a flipped sun-march or view-march step moves a pixel by tens of
-// RGBA8 levels. Points that close to the top are rare (about 1 in 50 sun marches): they take this form.
-__device__ __forceinline__ float cloud_height_rn(f3 p) {
-    const float y = __fadd_rn(p.y, kEarthRadius);
-    const float d = __fadd_rn(__fadd_rn(__fmul_rn(p.x, p.x), __fmul_rn(y, y)), __fmul_rn(p.z, p.z));
-    return __fsub_rn(__fsqrt_rn(d), kEarthRadius);
-}
-__device__ __forceinline__ float layer_height(f3 p) {
-    const float h = cloud_height(p);
-    return (SOC_CLOUDS_RN_TOP && fabsf(h - kMaxH) < 2.0f) ? cloud_height_rn(p) : h;
-}
-
 // get_clouds, :235-262, for a point whose altitude h is already known to lie inside the layer.
 // The four octaves carry weights 1/2, 1/4, 1/8, 1/16 and each lies in [0, 1], so once the partial sum
 // plus the largest possible remainder stays below the smoothstep's lower edge 0.55 the result is
 // exactly 0 (smoothstep clamps to 0) and the remaining octaves are skipped. The 1e-4 margin covers the
-// fp32 rounding of the remainder, so the early exits never change a result. From above: the octaves only
-// add (each fma adds a non-negative product, and rounding is monotonic), so once the partial sum reaches the
-// upper edge 0.6 (+ the margin) the full sum does too, (n - 0.55) / 0.05 >= 1 clamps to t = 1 and the
-// smoothstep is exactly 1 whatever the remaining octaves add: they are skipped (the dense cloud interiors the
-// sun visibility marches through).
+// fp32 rounding of the remainder, so the early exits never change a result. (Round 4 measured two more exact exits
+// -- after octave 1, and once the partial sum reaches the upper edge 0.6, where the smoothstep saturates -- on the C3
+// and C4 frames: they fire on 0.5 % and 0-8 % of the evaluations and cost 1-2 % more time, profiles/r04_probe_clouds.txt.)
 template <typename C>
 __device__ float clouds_at(const C& cx, f3 p, float h) {
     p = f3{p.x + cx.cam_x, h, p.z + cx.cam_z};
     const f3 mv = f3{cx.time, 0.0f, cx.time};
     const f3 cc = p * 0.001f + mv;
-    constexpr float kSat = 0.6f + 1e-4f;
     // octave weight x noise normalisation as one constant per octave (powers of two apart: one fma per octave)
     float n = noise3(cx, cc) * (0.5f * kNoiseNorm);
-    if (SOC_CLOUDS_EXITS >= 2 && n < 0.55f - 0.4375f - 1e-4f) return 0.0f;
     n = __builtin_fmaf(noise3(cx, cc * 2.0f + mv), 0.25f * kNoiseNorm, n);
     if (n < 0.55f - 0.1875f - 1e-4f) return 0.0f;
-    if (SOC_CLOUDS_EXITS < 1 || n < kSat) {
-        n = __builtin_fmaf(noise3(cx, cc * 7.0f - mv), 0.125f * kNoiseNorm, n);
-        if (n < 0.55f - 0.0625f - 1e-4f) return 0.0f;
-        if (SOC_CLOUDS_EXITS < 1 || n < kSat) {
-            // (cc + mv) 16 == fma(cc, 16, 16 mv) exactly: scaling by a power of two commutes with the rounding
-            const f3 c4 = f3{__builtin_fmaf(cc.x, 16.0f, mv.x * 16.0f), __builtin_fmaf(cc.y, 16.0f, mv.y * 16.0f),
-                             __builtin_fmaf(cc.z, 16.0f, mv.z * 16.0f)};
-            n = __builtin_fmaf(noise3(cx, c4), 0.0625f * kNoiseNorm, n);
-        }
-    }
+    n = __builtin_fmaf(noise3(cx, cc * 7.0f - mv), 0.125f * kNoiseNorm, n);
+    if (n < 0.55f - 0.0625f - 1e-4f) return 0.0f;
+    // (cc + mv) 16 == fma(cc, 16, 16 mv) exactly: scaling by a power of two commutes with the rounding
+    const f3 c4 = f3{__builtin_fmaf(cc.x, 16.0f, mv.x * 16.0f), __builtin_fmaf(cc.y, 16.0f, mv.y * 16.0f),
+                     __builtin_fmaf(cc.z, 16.0f, mv.z * 16.0f)};
+    n = __builtin_fmaf(noise3(cx, c4), 0.0625f * kNoiseNorm, n);
     const float hh = p.y - kMinH;
     const float th = (1.0f - __expf(-0.01f * hh)) * __expf(-0.004f * hh);
     const float t = clampf((n - 0.55f) * (1.0f / (0.6f - 0.55f)), 0.0f, 1.0f);
@@ -192,7 +161,7 @@ __device__ float clouds_at(const C& cx, f3 p, float h) {
 
 template <typename C>
 __device__ __forceinline__ float get_clouds(const C& cx, f3 p) {
-    const float h = layer_height(p);
+    const float h = cloud_height(p);
     if (h < kMinH || h > kMaxH) return 0.0f;
     return clouds_at(cx, p, h);
 }
@@ -210,7 +179,7 @@ __device__ float sun_visibility(const C& cx, f3 p, f3 sun) {
     if (SOC_CLOUDS_PROFILE == 3) return 1.0f;
     const bool rising = dot3(f3{p.x, p.y + kEarthRadius, p.z}, sun) > 0.0f;
     for (int i = 0; i < 10; i++, pos = pos + inc) {
-        const float h = layer_height(pos);
+        const float h = cloud_height(pos);
         if (h > kMaxH && rising) break;
         if (h >= kMinH && h <= kMaxH) tr += clouds_at(cx, pos, h);
     }

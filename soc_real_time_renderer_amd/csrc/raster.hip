@@ -322,7 +322,6 @@ struct ResolveParams {
     Mat3 normal3;
     int width, height, triangle_count, material_count;
     int tex_pairs;   // share the footprint of same-extent normal image + albedo (tuning knob SOC_GB_TEX_PAIRS, default on)
-    int swz;         // tile order (xcd_order; tuning knob SOC_SWZ_GB)
 };
 
 __device__ __forceinline__ float srgb_to_linear(float c) {
@@ -574,9 +573,8 @@ __global__ __launch_bounds__(kWorkgroup) void gbuffer_resolve(soc_mesh mesh, con
     __shared__ float lut[256];
     lut[threadIdx.y * 64 + threadIdx.x] = srgb_to_linear(unorm8(threadIdx.y * 64 + threadIdx.x));
     __syncthreads();
-    int tx, ty;
-    xcd_order(p.swz, tx, ty);
-    const int x = tx * 64 + threadIdx.x, y = ty * 4 + threadIdx.y;
+    // row-major tiles: the XCD-aware orders measured 13-40 % slower here (profiles/r04_probe_gbuffer_order.txt)
+    const int x = blockIdx.x * 64 + threadIdx.x, y = blockIdx.y * 4 + threadIdx.y;
     if (x >= p.width || y >= p.height) return;
     const unsigned long long key = vis[(size_t)y * p.width + x];
     const uint32_t low = (uint32_t)key;
@@ -802,9 +800,6 @@ extern "C" int soc_gbuffer_resolve(const soc_globals* g, const soc_mesh* mesh, c
     p.triangle_count = mesh->triangle_count;
     p.material_count = material_count;
     p.tex_pairs = tuning_knob("SOC_GB_TEX_PAIRS", 1);
-    // tile order: row-major tiles put neighbouring 64 x 4 strips on different XCDs, so every XCD's L2 fetches the texture
-    // footprint of the whole frame (PMC traffic 2.8x the G-buffer bytes at 4K with the native textures)
-    p.swz = tuning_knob("SOC_SWZ_GB", 0);
     dim3 blk(64, 4), grd(ceil_div(W, 64), ceil_div(H, 4));
     const unsigned long long* vis = reinterpret_cast<const unsigned long long*>(visibility);
     if (workspace) {   // per-vertex outputs once, then the per-pixel resolve reads them

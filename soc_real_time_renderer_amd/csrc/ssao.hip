@@ -10,11 +10,6 @@
 // identical bits.
 #include "soc_internal.hpp"
 
-// Tap-pair loop unroll of the packed path (A/B builds: make variant SRC=ssao.hip DEFS=-DSOC_SSAO_PK_UNROLL=n)
-#ifndef SOC_SSAO_PK_UNROLL
-#define SOC_SSAO_PK_UNROLL 1
-#endif
-
 namespace soc {
 namespace {
 
@@ -208,8 +203,9 @@ __device__ __forceinline__ void ssao_pixel(int x, int y, const DImg& depth, cons
     float occ = 0.0f;
     if constexpr (PK && SPARSE_IP && FULL) {
         static_assert(SOC_SSAO_MAX_KERNEL % 2 == 0, "taps are paired");
-        // the same per-tap operations as the scalar loop below, two taps per packed instruction
-#pragma unroll SOC_SSAO_PK_UNROLL
+        // the same per-tap operations as the scalar loop below, two taps per packed instruction (not unrolled: unrolling
+        // 2 or 13 pairs measured 5x slower, profiles/r04_probe_ssao_unroll.txt)
+#pragma unroll 1
         for (int i = 0; i < SOC_SSAO_MAX_KERNEL; i += 2) {
             const f2v kx = {kKernel.v[i][0], kKernel.v[i + 1][0]}, ky = {kKernel.v[i][1], kKernel.v[i + 1][1]},
                       kz = {kKernel.v[i][2], kKernel.v[i + 1][2]};
