@@ -290,52 +290,117 @@ __device__ f3 volumetric_clouds(const Ctx& cx, f3 dir, f3 sun, f3 color, float d
 }
 
 // atmosphere, :353-439 (primary ray starts at iTime = elapsed_time: quirk Q10)
-__device__ f3 atmosphere(f3 r, f3 r0, f3 pSun, float iTime) {
-    const float iSun = 22.0f, rPlanet = 6371e3f, rAtmos = 6471e3f, kMie = 21e-6f, shRlh = 8e3f, shMie = 1.2e3f, g0 = 0.758f;
+constexpr float kRPlanet = 6371e3f, kRAtmos = 6471e3f, kShRlh = 8e3f, kShMie = 1.2e3f;
+constexpr float kExpR = -1.44269504f / kShRlh, kExpM = -1.44269504f / kShMie;   // exp(-h/sh) = exp2(h * kExp)
+
+// The secondary (sun) ray of a primary sample, :399-423: its (Rayleigh, Mie) optical depth. It depends on the sample
+// only through A = |iPos|^2 and PoD = iPos.pSun (and C2 = |pSun|^2): |iPos + pSun t|^2 = A + t (B + t C2), B = 2 PoD,
+// and rsi(iPos, pSun, rAtmos).y needs the same two dot products; exp(-h / sh) as exp2(|jPos| kExp - rPlanet kExp).
+// Per step two fmas, a sqrt and the two exponentials.
+__device__ __forceinline__ f2v secondary_od(float A, float PoD, float C2) {
+    const float cR = -kRPlanet * kExpR, cM = -kRPlanet * kExpM;
+    const float delta = PoD * PoD + kRAtmos * kRAtmos - A;
+    const float jStep = (delta < 0.0f ? -1.0f : -PoD + __builtin_amdgcn_sqrtf(delta)) / 8.0f;
+    const float B = 2.0f * PoD, half = jStep * 0.5f;
+    float jTime = 0.0f;
+    f2v jOd = {0.0f, 0.0f};
+    // two secondary steps per packed instruction (v_pk_fma_f32 / v_pk_add_f32), element-wise the same
+    // operations, and the same sequential jTime and accumulation chains: the same bits
+#pragma unroll 2
+    for (int j = 0; j < 8; j += 2) {
+        const float jT1 = jTime + jStep;
+        const f2v t = f2v{jTime, jT1} + f2v{half, half};
+        const f2v q = pfma(t, pfma(t, f2v{C2, C2}, f2v{B, B}), f2v{A, A});
+        const f2v len = {__builtin_amdgcn_sqrtf(q.x), __builtin_amdgcn_sqrtf(q.y)};
+        const f2v eR = pfma(len, f2v{kExpR, kExpR}, f2v{cR, cR}), eM = pfma(len, f2v{kExpM, kExpM}, f2v{cM, cM});
+        jOd = pfma(f2v{__builtin_amdgcn_exp2f(eR.x), __builtin_amdgcn_exp2f(eM.x)}, f2v{jStep, jStep}, jOd);
+        jOd = pfma(f2v{__builtin_amdgcn_exp2f(eR.y), __builtin_amdgcn_exp2f(eM.y)}, f2v{jStep, jStep}, jOd);
+        jTime = jT1 + jStep;
+    }
+    return jOd;
+}
+
+// Optical-depth table of the secondary ray (round 4). By the symmetry above, secondary_od is a function of the sample's
+// radius r = |iPos| and mu = PoD / r alone (for the frame's sun), the same for every sky pixel: the per-frame table holds
+// (log2 odR, log2 odM) on a kOdR x kOdM grid over r in [rPlanet, rAtmos] and mu in [-1, 1], and a primary sample
+// inside that shell reads
+// its secondary depths by bilinear interpolation of the logs (the depths are nearly exponential in r) instead of
+// marching the 8 secondary steps: 2 exponentials instead of 8 square roots and 16 exponentials. Against the march the
+// secondary attenuation exp(-(kMie odM + kRlh odR)) differs by 2e-8 (median) and at most 6e-4 (grazing sun near the
+// ground), 1.4e-5 for mu > 0.9 (the reference sun over the frame; tools/od_lut_check.py): within the pass's RGBA8
+// tolerance (tests/test_gpu_parity.py test_clouds_od_table_against_marched_secondary_rays). Samples above the shell
+// (the primary ray's 16 steps span the chord from the atmosphere's entry BEHIND the camera, so about half of an upward
+// ray's samples lie above 100 km) read its top row (depth ~0: the march's own depths there are below 1e-2 m, 1e-7 of the
+// exponent); samples below the ground march (see atmosphere()). Entries whose march is not
+// finite (a sun ray through the planet, whose attenuation the reference takes to 0) are stored as NaN, and samples that
+// read one march their secondary ray as before. SOC_CLOUDS_OD_LUT=0 marches every secondary ray (the single-lane kernel
+// always does).
+constexpr int kOdR = 256, kOdM = 512;
+constexpr float kOdRScale = (float)(kOdR - 1) / (kRAtmos - kRPlanet), kOdMScale = (float)(kOdM - 1) * 0.5f;
+struct OdLut {
+    const float2* t;   // [kOdR][kOdM] (log2 odR, log2 odM); nullptr: no table
+    float C2;
+};
+
+__global__ __launch_bounds__(kWorkgroup) void clouds_od_lut(float2* __restrict__ lut, float C2) {
+    const int i = (int)(blockIdx.x * kWorkgroup + threadIdx.x);
+    if (i >= kOdR * kOdM) return;
+    const int ir = i / kOdM, im = i - ir * kOdM;
+    const float r = kRPlanet + (float)ir * (1.0f / kOdRScale), mu = -1.0f + (float)im * (1.0f / kOdMScale);
+    const f2v od = secondary_od(r * r, r * mu, C2);
+    const float lo = 1e-30f;   // the top row (r = rAtmos: a zero-length ray)
+    const bool ok = od.x < 3.0e38f && od.y < 3.0e38f && od.x >= 0.0f && od.y >= 0.0f;   // NaN / inf fail
+    lut[i] = ok ? float2{__builtin_amdgcn_logf(fmaxf(od.x, lo)), __builtin_amdgcn_logf(fmaxf(od.y, lo))}
+                : float2{__builtin_nanf(""), __builtin_nanf("")};
+}
+
+// The secondary depths of a sample from the table (bilinear in (r, mu), then exp2), or NaN where the table has none.
+__device__ __forceinline__ f2v secondary_od_lut(const OdLut& L, float iLen, float PoD) {
+    const float fr = fminf(fmaxf((iLen - kRPlanet) * kOdRScale, 0.0f), (float)(kOdR - 1));
+    const float mu = PoD * __builtin_amdgcn_rcpf(iLen);
+    const float fm = fminf(fmaxf((mu + 1.0f) * kOdMScale, 0.0f), (float)(kOdM - 1));
+    const int ir = min((int)fr, kOdR - 2), im = min((int)fm, kOdM - 2);
+    const float wr = fr - (float)ir, wm = fm - (float)im;
+    const float2* row = L.t + ir * kOdM + im;
+    const float2 a = row[0], b = row[1], c = row[kOdM], d = row[kOdM + 1];
+    const f2v top = pfma(f2v{wm, wm}, f2v{b.x - a.x, b.y - a.y}, f2v{a.x, a.y});
+    const f2v bot = pfma(f2v{wm, wm}, f2v{d.x - c.x, d.y - c.y}, f2v{c.x, c.y});
+    const f2v l = pfma(f2v{wr, wr}, bot - top, top);
+    return f2v{__builtin_amdgcn_exp2f(l.x), __builtin_amdgcn_exp2f(l.y)};
+}
+
+__device__ f3 atmosphere(f3 r, f3 r0, f3 pSun, float iTime, const OdLut& L) {
+    const float iSun = 22.0f, kMie = 21e-6f, g0 = 0.758f;
     const f3 kRlh = f3{5.5e-6f, 13.0e-6f, 22.4e-6f};
     const float PI = 3.141592f;
     r = normalize3(r);
-    float2 p = rsi(r0, r, rAtmos);
+    float2 p = rsi(r0, r, kRAtmos);
     if (p.x > p.y) return f3{0.0f, 0.0f, 0.0f};
-    p.y = fminf(p.y, rsi(r0, r, rPlanet).x);
+    p.y = fminf(p.y, rsi(r0, r, kRPlanet).x);
     const float iStep = (p.y - p.x) / 16.0f;
     f3 totalRlh = f3{0, 0, 0}, totalMie = f3{0, 0, 0};
     f2v iOd = {0.0f, 0.0f};   // (Rayleigh, Mie) optical depth of the primary ray, one packed pair
     const float mu = dot3(r, pSun), mumu = mu * mu, gg = g0 * g0;
     const float pRlh = 3.0f / (16.0f * PI) * (1.0f + mumu);
     const float pMie = 3.0f / (8.0f * PI) * ((1.0f - gg) * (mumu + 1.0f)) / (powf(1.0f + gg - 2.0f * mu * g0, 1.5f) * (2.0f + gg));
-    const float kR = -1.44269504f / shRlh, kM = -1.44269504f / shMie;   // exp(-h/sh) = exp2(h * kR)
-    // secondary ray: |iPos + pSun t|^2 = A + t (B + t C) with A = |iPos|^2, B = 2 iPos.pSun, C = |pSun|^2
-    // (the rsi of the secondary ray needs the same two dot products), and exp(-h / sh) as
-    // exp2(|jPos| kR - rPlanet kR): per step two fmas, a sqrt and the two exponentials
-    const float C2 = dot3(pSun, pSun), cR = -rPlanet * kR, cM = -rPlanet * kM;
+    const float C2 = dot3(pSun, pSun), cR = -kRPlanet * kExpR, cM = -kRPlanet * kExpM;
     for (int i = 0; i < 16; i++) {
         const f3 iPos = r0 + r * (iTime + iStep * 0.5f);
         const float A = dot3(iPos, iPos), PoD = dot3(iPos, pSun);
         const float iLen = __builtin_amdgcn_sqrtf(A);
         // (odR, odM) and the accumulators as packed pairs: element-wise the scalar operations (the same bits)
-        const f2v ea = pfma(f2v{iLen, iLen}, f2v{kR, kM}, f2v{cR, cM});
+        const f2v ea = pfma(f2v{iLen, iLen}, f2v{kExpR, kExpM}, f2v{cR, cM});
         const f2v od = f2v{__builtin_amdgcn_exp2f(ea.x), __builtin_amdgcn_exp2f(ea.y)} * f2v{iStep, iStep};
         const float odR = od.x, odM = od.y;
         iOd = iOd + od;
-        // rsi(iPos, pSun, rAtmos).y (:97-106); the secondary ray starts inside the atmosphere
-        float delta = PoD * PoD + rAtmos * rAtmos - A;
-        const float jStep = (delta < 0.0f ? -1.0f : -PoD + __builtin_amdgcn_sqrtf(delta)) / 8.0f;
-        const float B = 2.0f * PoD, half = jStep * 0.5f;
-        float jTime = 0.0f;
-        f2v jOd = {0.0f, 0.0f};   // (Rayleigh, Mie) optical depth of the secondary ray
-        // two secondary steps per packed instruction (v_pk_fma_f32 / v_pk_add_f32), element-wise the same
-        // operations, and the same sequential jTime and accumulation chains: the same bits
-#pragma unroll 2
-        for (int j = 0; j < 8; j += 2) {
-            const float jT1 = jTime + jStep;
-            const f2v t = f2v{jTime, jT1} + f2v{half, half};
-            const f2v q = pfma(t, pfma(t, f2v{C2, C2}, f2v{B, B}), f2v{A, A});
-            const f2v len = {__builtin_amdgcn_sqrtf(q.x), __builtin_amdgcn_sqrtf(q.y)};
-            const f2v eR = pfma(len, f2v{kR, kR}, f2v{cR, cR}), eM = pfma(len, f2v{kM, kM}, f2v{cM, cM});
-            jOd = pfma(f2v{__builtin_amdgcn_exp2f(eR.x), __builtin_amdgcn_exp2f(eM.x)}, f2v{jStep, jStep}, jOd);
-            jOd = pfma(f2v{__builtin_amdgcn_exp2f(eR.y), __builtin_amdgcn_exp2f(eM.y)}, f2v{jStep, jStep}, jOd);
-            jTime = jT1 + jStep;
+        f2v jOd;
+        // below the planet's surface (a ray that hits the ground keeps stepping underground: its first sample is at
+        // elapsed_time and its step spans the whole chord, quirk Q10) the depths grow without bound: marched
+        if (L.t && iLen >= kRPlanet) {
+            jOd = secondary_od_lut(L, iLen, PoD);
+            if (!(jOd.x == jOd.x) || !(jOd.y == jOd.y)) jOd = secondary_od(A, PoD, C2);   // no table entry here
+        } else {
+            jOd = secondary_od(A, PoD, C2);
         }
         const f2v od_sum = iOd + jOd;
         const float fm = kMie * od_sum.y;
@@ -359,10 +424,10 @@ __device__ __forceinline__ f3 sky_dir(const CloudParams& p, int x, int y) {
     return normalize3(f3{rws.x, rws.y, rws.z});
 }
 
-__device__ __forceinline__ f3 sky_atmosphere(const CloudParams& p, f3 dir) {
+__device__ __forceinline__ f3 sky_atmosphere(const CloudParams& p, f3 dir, const OdLut& L = OdLut{nullptr, 0.0f}) {
     if (SOC_CLOUDS_PROFILE == 2 || SOC_CLOUDS_PROFILE == 3) return f3{0.1f, 0.2f, 0.3f};
     const f3 r0 = f3{0.0f + p.cam[0], 6372e3f + p.cam[1], 0.0f + p.cam[2]};
-    return atmosphere(dir, r0, f3{p.sun[0], p.sun[1], p.sun[2]}, p.elapsed);
+    return atmosphere(dir, r0, f3{p.sun[0], p.sun[1], p.sun[2]}, p.elapsed, L);
 }
 
 // Clouds over the atmosphere colour, sun factor, RGBA8 (main(), :466-477).
@@ -499,11 +564,12 @@ __global__ __launch_bounds__(kWorkgroup) void clouds_classify(DImg depth, DImg t
 // Three-kernel path, stage 2: the atmosphere of every listed sky pixel (no LDS, few registers, so many
 // more lanes are resident than in the cloud march), kept in fp32 in the workspace.
 __global__ __launch_bounds__(kWorkgroup) __attribute__((amdgpu_waves_per_eu(8))) void clouds_atmosphere(CloudParams p, const uint32_t* __restrict__ counter,
-                                                         const uint32_t* __restrict__ list, float4* __restrict__ atmos) {
+                                                         const uint32_t* __restrict__ list, float4* __restrict__ atmos,
+                                                         OdLut lut) {
     const uint32_t count = *counter;
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < count; i += gridDim.x * 256u) {
         const uint32_t e = list[i];
-        const f3 c = sky_atmosphere(p, sky_dir(p, (int)(e & 0xffffu), (int)(e >> 16)));
+        const f3 c = sky_atmosphere(p, sky_dir(p, (int)(e & 0xffffu), (int)(e >> 16)), lut);
         atmos[i] = float4{c.x, c.y, c.z, 0.0f};
     }
 }
@@ -790,7 +856,8 @@ using namespace soc;
 namespace {
 // Workspace: counters (256 B: [0] sky pixels, [8..15] pair counts per shard) | sky list (u32) |
 // atmosphere (float4) | per-pixel dense mask (u32) | per-batch first pair (u32) | march geometry (2 float4) | pairs (u32) |
-// (od, vis) per pair (float2) | od scratch of the density workgroups (24 x 256 float each, at most kDensityBlocks).
+// (od, vis) per pair (float2) | od scratch of the density workgroups (24 x 256 float each, at most kDensityBlocks) |
+// the secondary-ray optical-depth table (kOdR x kOdM float2, 1 MiB).
 // Pair capacity 2 per pixel of the image (8 shards).
 // Per 256-entry batch of the list: the physical index of its first pair (or kInline).
 // density workgroups the od scratch is sized for (the resident set: 6 per CU on 256 CUs is 1536)
@@ -800,6 +867,7 @@ struct CloudWs {
     uint32_t* list;
     float4* atmos;
     PairBufs pb;
+    float2* od_lut;   // secondary-ray optical-depth table (kOdR x kOdM)
     size_t bytes;
 };
 CloudWs cloud_ws_layout(void* base, size_t n) {
@@ -828,6 +896,8 @@ CloudWs cloud_ws_layout(void* base, size_t n) {
     w.pb.od_blocks = (uint32_t)std::min<size_t>(kDensityBlocks, (n + 255) / 256);
     w.pb.n = (uint32_t)n;
     off = al(off + (size_t)w.pb.od_blocks * 24 * 256 * 4);
+    w.od_lut = reinterpret_cast<float2*>(b + off);
+    off = al(off + (size_t)kOdR * kOdM * sizeof(float2));
     w.bytes = off;
     return w;
 }
@@ -902,7 +972,14 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
     // 1920x1080 -5 % after it); the same bits in every position (profiles/r03_ab_atmos_pos.txt, GPU identity test).
     const int apos_knob = tuning_knob("SOC_CLOUDS_ATMOS_POS", -1);
     const int apos = apos_knob >= 0 ? apos_knob : ((long long)W * H > 2560LL * 1440LL ? 2 : 0);
-    auto atmos = [&]() { launch("clouds_atmosphere", kWorkgroup, clouds_atmosphere, grid(res_atmos, blocks), kWorkgroup, 0, s, p, counter, list, ws.atmos); };
+    // the frame's secondary-ray table (SOC_CLOUDS_OD_LUT=0: march every secondary ray, the single-lane kernel's bits)
+    OdLut lut{nullptr, 0.0f};
+    if (tuning_knob("SOC_CLOUDS_OD_LUT", 1)) {
+        const float C2 = p.sun[0] * p.sun[0] + p.sun[1] * p.sun[1] + p.sun[2] * p.sun[2];   // dot3(pSun, pSun)
+        lut = OdLut{ws.od_lut, C2};
+        launch("clouds_od_lut", kWorkgroup, clouds_od_lut, ceil_div(kOdR * kOdM, kWorkgroup), kWorkgroup, 0, s, ws.od_lut, C2);
+    }
+    auto atmos = [&]() { launch("clouds_atmosphere", kWorkgroup, clouds_atmosphere, grid(res_atmos, blocks), kWorkgroup, 0, s, p, counter, list, ws.atmos, lut); };
     if (apos == 0) atmos();
     const DImg nz = dimg(noise), tg = dimg(target);
     const int density_grid = std::min(grid(res_density, blocks), (int)ws.pb.od_blocks);   // one od scratch per workgroup

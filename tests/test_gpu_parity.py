@@ -519,12 +519,14 @@ def test_clouds_pair_path_equals_single_lane(soc, monkeypatch, W, H, pitch, all_
     the single-lane kernel's bits: od and vis are evaluated at the same positions with the same
     additions and accumulated in the same order, with the atmosphere kernel in any of its positions in the lane
     (SOC_CLOUDS_ATMOS_POS 0 / 1 / 2). An all-sky frame overflows the pair lists (2 pairs per image pixel) and
-    exercises the per-batch single-lane fallback."""
+    exercises the per-batch single-lane fallback. The secondary-ray table is off here (SOC_CLOUDS_OD_LUT=0); the next test
+    bounds what it changes."""
     g, gb = sponza_inputs(W, H, camera=((-14.0, 2.2, 0.3), (0.0, pitch, 0.0)), elapsed=10.0)
     depth = np.ones_like(gb["depth"]) if all_sky else gb["depth"]
     a = torch.zeros(H, W, 4, dtype=torch.uint8, device=DEV)
     ws = soc.cloud_rendering_workspace(W, H)
     soc.cloud_rendering(g, dev(depth), dev(gb["noise"]), a, None)
+    monkeypatch.setenv("SOC_CLOUDS_OD_LUT", "0")   # every secondary ray marched, as the single-lane kernel does
     for pos in ("0", "1", "2"):
         monkeypatch.setenv("SOC_CLOUDS_ATMOS_POS", pos)
         soc.reload_tuning()
@@ -534,6 +536,29 @@ def test_clouds_pair_path_equals_single_lane(soc, monkeypatch, W, H, pitch, all_
         assert torch.equal(a, b), (pos, (a != b).float().mean().item())
     monkeypatch.delenv("SOC_CLOUDS_ATMOS_POS")
     soc.reload_tuning()
+
+
+@pytest.mark.parametrize("config", ["c3", "c4"])
+def test_clouds_od_table_against_marched_secondary_rays(soc, monkeypatch, config):
+    """The atmosphere's secondary-ray optical-depth table (clouds.hip clouds_od_lut, the default) against marching every
+    secondary ray (SOC_CLOUDS_OD_LUT=0) on the bench's 4K frames: the interpolated depths change a pixel by at most one
+    RGBA8 level, on at most 0.1 % of the sky pixels (the oracle comparisons of test_clouds and the 4K frame tests bound
+    the result against the reference restatement)."""
+    import bench
+    W, H = 3840, 2160
+    g, gb, _sh, _nz, _sc, fr = bench.build_inputs(config, "mesh", W, H, 0, torch.device(DEV, 0))
+    outs = []
+    for lut in ("1", "0"):
+        monkeypatch.setenv("SOC_CLOUDS_OD_LUT", lut)
+        soc.reload_tuning()
+        o = torch.zeros(H, W, 4, dtype=torch.uint8, device=DEV)
+        soc.cloud_rendering(g, fr["depth"], fr["noise"], o, fr["clouds_workspace"])
+        outs.append(o)
+    torch.cuda.synchronize()
+    d = (outs[0].int() - outs[1].int()).abs().amax(dim=-1)
+    sky = torch.from_numpy(gb["depth"] == 1.0).to(DEV)
+    assert int(d.max()) <= 1, int(d.max())
+    assert float((d[sky] > 0).float().mean()) <= 1e-3, float((d[sky] > 0).float().mean())
 
 
 # ------------------------------------------------------------------------------------------------ full frame
