@@ -49,7 +49,8 @@ inline hipStream_t hs(soc_stream s) { return reinterpret_cast<hipStream_t>(s); }
 
 // Integer tuning knob from the environment (`dflt` when unset), read once and cached until soc_tuning_reload():
 // only the variants the identity tests switch (SOC_SWZ_SSAO, SOC_SSAO_TILE, SOC_TAA_NBR, SOC_COMP_NT, SOC_GB_TEX_PAIRS,
-// SOC_CLOUDS_ATMOS_POS, SOC_RENDERER_SSAO_FIRST) are knobs; measured-and-rejected variants are removed.
+// SOC_CLOUDS_ATMOS_POS, SOC_RENDERER_SSAO_FIRST, SOC_CLOUDS_OD_LUT) and the variants under measurement (SOC_GB_WAVE) are
+// knobs; measured-and-rejected variants are removed.
 int tuning_knob(const char* name, int dflt);
 // RN(1 / n) for div_rn (soc_device.hpp), or 0 when n is outside the exhaustively checked range (1..16384).
 inline float recip_rn(int n) {

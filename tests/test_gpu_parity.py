@@ -170,8 +170,9 @@ def test_ssao_noise_table_is_bit_identical(soc):
 @pytest.mark.parametrize("W,H,inputs", [(97, 55, "boxes"), (1920, 1080, "boxes"), (1920, 1080, "mesh"), (3840, 2160, "mesh"),
                                          (130, 1200, "boxes"), (2000, 34, "boxes")])
 def test_ssao_tile_orders_bit_identical(soc, monkeypatch, W, H, inputs):
-    """The LDS-tiled kernel (default: depth tile + 32-texel halo in LDS, the other taps gathered) and the plain gather
-    kernel (SOC_SSAO_TILE=0) give the same bits, in every workgroup order of the gather kernel (row-major, XCD-aware
+    """The LDS-tiled kernel (default: depth tile + 32-texel halo in LDS, the other taps gathered), the tile with the
+    out-of-tile taps deferred to a dense second phase (SOC_SSAO_TILE=2) and the plain gather kernel (SOC_SSAO_TILE=0)
+    give the same bits, in every workgroup order of the gather kernel (row-major, XCD-aware
     eighths, horizontal and vertical XCD bands: SOC_SWZ_SSAO; the orders are bijections, also for ragged grids), on the
     box atrium and on the mesh (near geometry: many taps leave the tile), at odd, tall and wide extents (partial tiles,
     tiles hanging over every image edge)."""
@@ -187,7 +188,7 @@ def test_ssao_tile_orders_bit_identical(soc, monkeypatch, W, H, inputs):
         depth, normal = dev(gb["depth"]), dev(gb["normal"])
     table = torch.zeros((H // 2) * (W // 2) * 2, dtype=torch.float32, device=DEV)
     outs = []
-    for tile, swz in (("1", None), ("0", "0"), ("0", "1"), ("0", "4"), ("0", "16"), ("0", "-16"), ("0", "-3")):
+    for tile, swz in (("1", None), ("2", None), ("0", "0"), ("0", "1"), ("0", "4"), ("0", "16"), ("0", "-16"), ("0", "-3")):
         monkeypatch.setenv("SOC_SSAO_TILE", tile)
         if swz is None:
             monkeypatch.delenv("SOC_SWZ_SSAO", raising=False)
@@ -404,39 +405,53 @@ def test_taa(soc, oracle, W, H, inputs):
     assert np.array_equal(host(vout).view(np.uint16), gb["velocity"].view(np.uint16))
 
 
-@pytest.mark.parametrize("W,H", [(100, 40), (102, 42), (1920, 1080)])
-def test_taa_lane_shift_neighbours_identical(soc, oracle, monkeypatch, W, H):
+@pytest.mark.parametrize("W,H,noisy", [(100, 40, False), (102, 42, False), (102, 45, True), (1920, 1080, False),
+                                       (1920, 1080, True)])
+def test_taa_lane_shift_neighbours_identical(soc, oracle, monkeypatch, W, H, noisy):
     """Every neighbourhood source gives the bits of the per-lane loads (SOC_TAA_NBR=0): the LDS-staged tiles (3,
-    default), the side columns from the adjacent lanes (DPP wave shifts) with halo-only first / last lanes (2) and
-    with edge-lane loads (1). 100 px: 50 pairs in one 64-pair LDS tile row (14 lanes past the image) / a 62-pair
-    wave row (12 lanes past), 32-lane block rows of which the second has 18 lanes inside; 102 x 42: a partial last
-    depth quad (W % 4 == 2) and a last tile row with 2 of its 4 rows inside (H % 4 == 2); 1920 px: 15 LDS tiles,
-    15.5 wave rows."""
+    default), the LDS-staged tiles with two pixel pairs per lane and shared history rows (4), the side columns from the
+    adjacent lanes (DPP wave shifts) with halo-only first / last lanes (2) and with edge-lane loads (1). 100 px: 50
+    pairs in one 64-pair LDS tile row (14 lanes past the image) / a 62-pair wave row (12 lanes past), 32-lane block rows
+    of which the second has 18 lanes inside; 102 x 42: a partial last depth quad (W % 4 == 2) and a last tile row with
+    2 of its 4 rows inside (H % 4 == 2); 102 x 45: an odd height (the last two-row lanes have one row inside); 1920 px:
+    15 LDS tiles, 15.5 wave rows. noisy: per-pixel velocity noise of a few texels, so that vertically adjacent pixels
+    mostly take different history rows (the two-row lanes' unshared loads) instead of the next row (the shared one)."""
     g, gb = sponza_inputs(W, H)
     cur = dev(random_rgba16(H, W, seed=3, hi=3.0))
     prev = dev(random_rgba16(H, W, seed=4, hi=3.0))
-    pvel = gb["velocity"].copy()
+    velocity = gb["velocity"].copy()
+    if noisy:
+        rng = np.random.default_rng(5)
+        velocity[..., 0] += (rng.integers(-3, 4, (H, W)) / W).astype(np.float16)
+        velocity[..., 1] += (rng.integers(-3, 4, (H, W)) / H).astype(np.float16)
+    pvel = velocity.copy()
     pvel[..., :2] += np.float16(0.0015)
-    vel, pvel, depth = dev(gb["velocity"]), dev(pvel), dev(gb["depth"])
+    vel, pvel, depth = dev(velocity), dev(pvel), dev(gb["depth"])
     if (W * 4) % 16:   # the LDS tiles stage 16-B depth quads: a row pitch padded to 16 B (rows may be padded)
         dp = torch.zeros(H, W + 2, dtype=torch.float32, device=DEV)
         dp[:, :W] = depth
         depth = dp[:, :W]
     ae = soc.auto_exposure_buffer(exposure=0.37)
     outs = []
-    for nbr in ("3", "2", "1", "0"):
+    for nbr in ("3", "4", "2", "1", "0"):
         monkeypatch.setenv("SOC_TAA_NBR", nbr)
         soc.reload_tuning()
         t = torch.zeros(H, W, 4, dtype=torch.float16, device=DEV)
         o = torch.zeros(H, W, 4, dtype=torch.uint8, device=DEV)
-        soc.temporal_antialiasing_tone_mapping(g, t, cur, prev, vel, pvel, depth, ae, o)
-        outs.append((t, o))
+        vo = torch.zeros(H, W, 4, dtype=torch.float16, device=DEV)
+        soc.temporal_antialiasing_tone_mapping(g, t, cur, prev, vel, pvel, depth, ae, o, vo)
+        t2 = torch.zeros(H, W, 4, dtype=torch.float16, device=DEV)   # the TAA pass alone
+        soc.temporal_antialiasing(g, t2, cur, prev, vel, pvel, depth)
+        outs.append((t, o, vo, t2))
     torch.cuda.synchronize()
-    for t, o in outs[1:]:
+    for t, o, vo, t2 in outs[1:]:
         assert torch.equal(outs[0][0], t)
         assert torch.equal(outs[0][1], o)
+        assert torch.equal(outs[0][2], vo)
+        assert torch.equal(outs[0][0], t2)
+    assert torch.equal(outs[0][2], vel)
     ref = np.zeros((H, W, 4), np.float16)
-    oracle.temporal_antialiasing(g, ref, host(cur), host(prev), gb["velocity"], host(pvel), gb["depth"])
+    oracle.temporal_antialiasing(g, ref, host(cur), host(prev), velocity, host(pvel), gb["depth"])
     ok = f16_close(host(outs[0][0]), ref)
     assert ok.all(), ok.mean()
 
