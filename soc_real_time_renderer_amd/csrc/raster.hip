@@ -322,7 +322,8 @@ struct ResolveParams {
     Mat3 normal3;
     int width, height, triangle_count, material_count;
     int tex_pairs;   // share the footprint of same-extent normal image + albedo (tuning knob SOC_GB_TEX_PAIRS, default on)
-    int wave_shape;  // pixels of a wave: 0 = 64 x 1, 1 = 16 x 4, 2 = 8 x 8 (tuning knob SOC_GB_WAVE)
+    int wave_shape;  // pixels of a wave / workgroup: 0 = 64 x 1 / 64 x 4, 1 = 16 x 4 / 64 x 4, 2 = 8 x 8 / 32 x 8 (default),
+                     // 3 = 8 x 8 / 16 x 16, 4 = 8 x 8 / 8 x 32 (tuning knob SOC_GB_WAVE)
 };
 
 __device__ __forceinline__ float srgb_to_linear(float c) {
@@ -575,8 +576,8 @@ __global__ __launch_bounds__(kWorkgroup) void gbuffer_resolve(soc_mesh mesh, con
     lut[threadIdx.y * 64 + threadIdx.x] = srgb_to_linear(unorm8(threadIdx.y * 64 + threadIdx.x));
     __syncthreads();
     // row-major tiles: the XCD-aware orders measured 13-40 % slower here (profiles/r04_probe_gbuffer_order.txt).
-    // A wave covers 64 x 1 pixels (shape 0), 16 x 4 (1, the workgroup a 64 x 4 tile) or 8 x 8 (2, a 32 x 8 tile): a
-    // compact wave footprint shares the texture lines of the anisotropic taps in L1.
+    // A wave covers 64 x 1 pixels (shape 0), 16 x 4 (1, the workgroup a 64 x 4 tile) or 8 x 8 (2: a 32 x 8 tile, the
+    // default; 3: 16 x 16; 4: 8 x 32): a compact wave footprint shares the texture lines of the anisotropic taps in L1.
     const int lane = threadIdx.x, wave = threadIdx.y;
     int x, y;
     if (p.wave_shape == 1) {
@@ -585,6 +586,12 @@ __global__ __launch_bounds__(kWorkgroup) void gbuffer_resolve(soc_mesh mesh, con
     } else if (p.wave_shape == 2) {
         x = blockIdx.x * 32 + wave * 8 + (lane & 7);
         y = blockIdx.y * 8 + (lane >> 3);
+    } else if (p.wave_shape == 3) {
+        x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+        y = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    } else if (p.wave_shape == 4) {
+        x = blockIdx.x * 8 + (lane & 7);
+        y = blockIdx.y * 32 + wave * 8 + (lane >> 3);
     } else {
         x = blockIdx.x * 64 + lane;
         y = blockIdx.y * 4 + wave;
@@ -814,9 +821,12 @@ extern "C" int soc_gbuffer_resolve(const soc_globals* g, const soc_mesh* mesh, c
     p.triangle_count = mesh->triangle_count;
     p.material_count = material_count;
     p.tex_pairs = tuning_knob("SOC_GB_TEX_PAIRS", 1);
-    p.wave_shape = tuning_knob("SOC_GB_WAVE", 0);
+    p.wave_shape = tuning_knob("SOC_GB_WAVE", 2);   // 8 x 8-pixel waves: 687 -> 626 us at 4K (profiles/r04_probe_gbuffer_wave.txt)
     dim3 blk(64, 4), grd(ceil_div(W, 64), ceil_div(H, 4));
     if (p.wave_shape == 2) grd = dim3(ceil_div(W, 32), ceil_div(H, 8));
+    else if (p.wave_shape == 3) grd = dim3(ceil_div(W, 16), ceil_div(H, 16));
+    else if (p.wave_shape == 4) grd = dim3(ceil_div(W, 8), ceil_div(H, 32));
+    else if (p.wave_shape != 0 && p.wave_shape != 1) return set_error(SOC_E_INVALID_ARG, "soc_gbuffer_resolve: SOC_GB_WAVE %d", p.wave_shape);
     const unsigned long long* vis = reinterpret_cast<const unsigned long long*>(visibility);
     if (workspace) {   // per-vertex outputs once, then the per-pixel resolve reads them
         const Workspace ws = carve(workspace, mesh->vertex_count, mesh->triangle_count);

@@ -134,16 +134,9 @@ __device__ __forceinline__ f2v aff2(const Aff& a, f2v kx, f2v ky, f2v kz) {
 // One half-res pixel of SSAOGenerationTask (:176-214); `quad` fetches a tap's 2x2 D32 texels.
 // PK (sparse inverse projection, full kernel only): the taps in pairs, the affine forms, weights, range test and
 // smoothstep of both taps as packed f32 operations; per tap the same operations in the same order (bit-identical).
-// MODE (PK only; the deferred-tap tiles): 0 = every tap; 1 = the deferred-tap tile, one code path for its two phases
-// (a second inlined copy of the pixel runs out of SGPRs): with `tile_only`, the tile's taps only: if a tap pair has a
-// texel quad outside the tile, return the first such pair's index in `stop` and the occlusion summed before it in
-// `occ_out` (nothing is stored); without, resume at tap `i_start` with the occlusion `occ_in` (the sum continues in the
-// same order; Quad loads the out-of-tile taps).
-template <bool TABLE, bool SPARSE_IP, bool FULL, class Quad, int UNROLL = SOC_SSAO_MAX_KERNEL, bool PK = false, int MODE = 0>
+template <bool TABLE, bool SPARSE_IP, bool FULL, class Quad, int UNROLL = SOC_SSAO_MAX_KERNEL, bool PK = false>
 __device__ __forceinline__ void ssao_pixel(int x, int y, const DImg& depth, const DImg& normal, const DImg& target,
-                                           const float2* __restrict__ table, const SsaoParams& p, const Quad& quad,
-                                           int i_start = 0, float occ_in = 0.0f, bool tile_only = false,
-                                           int* stop = nullptr, float* occ_out = nullptr) {
+                                           const float2* __restrict__ table, const SsaoParams& p, const Quad& quad) {
     // no implicit contraction: every fused multiply-add below is an explicit fma, so the per-pixel arithmetic does not
     // depend on how the surrounding kernel is unrolled or scheduled (ssao_kernel and ssao_lds_kernel give the same bits)
 #pragma clang fp contract(off)
@@ -207,15 +200,13 @@ __device__ __forceinline__ void ssao_pixel(int x, int y, const DImg& depth, cons
     const Aff dzr = Aff{p.bias * ir, t.z, b.z, n.z};
     const int W = depth.w, H = depth.h;
     const float cx0 = p.c0x, cy0 = p.c0y, tmax_x = p.tmx, tmax_y = p.tmy;   // texel (or sub-texel) space
-    float occ = MODE == 1 ? occ_in : 0.0f;
-    int stop_i = -1;
-    float occ_stop = 0.0f;
+    float occ = 0.0f;
     if constexpr (PK && SPARSE_IP && FULL) {
         static_assert(SOC_SSAO_MAX_KERNEL % 2 == 0, "taps are paired");
         // the same per-tap operations as the scalar loop below, two taps per packed instruction (not unrolled: unrolling
         // 2 or 13 pairs measured 5x slower, profiles/r04_probe_ssao_unroll.txt)
 #pragma unroll 1
-        for (int i = MODE == 1 ? i_start : 0; i < SOC_SSAO_MAX_KERNEL; i += 2) {
+        for (int i = 0; i < SOC_SSAO_MAX_KERNEL; i += 2) {
             const f2v kx = {kKernel.v[i][0], kKernel.v[i + 1][0]}, ky = {kKernel.v[i][1], kKernel.v[i + 1][1]},
                       kz = {kKernel.v[i][2], kKernel.v[i + 1][2]};
             const f2v ww = aff2(aw, kx, ky, kz);
@@ -225,11 +216,6 @@ __device__ __forceinline__ void ssao_pixel(int x, int y, const DImg& depth, cons
             const int fy0 = (int)__builtin_amdgcn_fmed3f(Y.x, 0.5f, tmax_y), fy1 = (int)__builtin_amdgcn_fmed3f(Y.y, 0.5f, tmax_y);
             const f2v wx = f2v{(float)(fx0 & 255), (float)(fx1 & 255)} * bc2(1.0f / 256.0f);
             const f2v wy = f2v{(float)(fy0 & 255), (float)(fy1 & 255)} * bc2(1.0f / 256.0f);
-            if constexpr (MODE == 1) {   // no early exit (the wave runs every pair anyway): remember where and what
-                const bool out = tile_only && !(quad.inside(fx0 >> 8, fy0 >> 8) && quad.inside(fx1 >> 8, fy1 >> 8));
-                occ_stop = (stop_i < 0 && out) ? occ : occ_stop;
-                stop_i = (stop_i < 0 && out) ? i : stop_i;
-            }
             float a0, a1, a2, a3, b0, b1, b2, b3;
             quad(fx0 >> 8, fy0 >> 8, a0, a1, a2, a3);
             quad(fx1 >> 8, fy1 >> 8, b0, b1, b2, b3);
@@ -296,11 +282,6 @@ __device__ __forceinline__ void ssao_pixel(int x, int y, const DImg& depth, cons
         }
     }
     }
-    if (MODE == 1 && stop_i >= 0) {
-        *stop = stop_i;
-        *occ_out = occ_stop;
-        return;
-    }
     occ = 1.0f - occ * p.inv_ksize;
     row_ptr_w<uint8_t>(target, y)[x] = (uint8_t)to_unorm8(occ);
 }
@@ -325,21 +306,15 @@ struct SsaoTile {
     static constexpr int TW = 2 * TXP + 2 * HALO, TH = 2 * TYP + 2 * HALO, THREADS = TXP * TYP;
 };
 
-template <int TXP, int TYP, int HALO, bool FALLBACK = true>
+template <int TXP, int TYP, int HALO>
 struct LdsQuad {
     const float* tile;
     int gx0, gy0;
     GlobalQuad g;
-    bool fb = true;   // !FALLBACK: load the out-of-tile taps only if fb (the deferred tile's second phase)
-    // the texel quad (x0, y0) .. (x0 + 1, y0 + 1) lies in the tile
-    __device__ __forceinline__ bool inside(int x0, int y0) const {
-        constexpr int TW = SsaoTile<TXP, TYP, HALO>::TW, TH = SsaoTile<TXP, TYP, HALO>::TH;
-        return (unsigned)(x0 - gx0) < (unsigned)(TW - 1) && (unsigned)(y0 - gy0) < (unsigned)(TH - 1);
-    }
     __device__ __forceinline__ void operator()(int x0, int y0, float& t0, float& t1, float& b0, float& b1) const {
-        constexpr int TW = SsaoTile<TXP, TYP, HALO>::TW;
+        constexpr int TW = SsaoTile<TXP, TYP, HALO>::TW, TH = SsaoTile<TXP, TYP, HALO>::TH;
         const int lx = x0 - gx0, ly = y0 - gy0;
-        const bool in = inside(x0, y0);
+        const bool in = (unsigned)lx < (unsigned)(TW - 1) && (unsigned)ly < (unsigned)(TH - 1);
         // ly * TW + lx as one full-rate v_mad_u32_u24 (the compiler otherwise selects v_mad_u64_u32 for it)
         uint32_t i;
         asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(i) : "v"(ly), "s"((uint32_t)TW), "v"(lx));
@@ -348,7 +323,7 @@ struct LdsQuad {
         t1 = tile[i + 1];
         b0 = tile[i + TW];
         b1 = tile[i + TW + 1];
-        if ((FALLBACK || fb) && !in) g(x0, y0, t0, t1, b0, b1);
+        if (!in) g(x0, y0, t0, t1, b0, b1);
     }
 };
 
@@ -383,73 +358,6 @@ void ssao_lds_kernel(DImg depth, DImg normal, DImg target, const float2* __restr
     if (x >= target.w || y >= target.h) return;
     const LdsQuad<TXP, TYP, HALO> quad{reinterpret_cast<const float*>(tile4), gx0, gy0, GlobalQuad{rsrc, depth.pitch}};
     ssao_pixel<TABLE, SPARSE_IP, FULL, LdsQuad<TXP, TYP, HALO>, UNROLL, PK>(x, y, depth, normal, target, table, p, quad);
-}
-
-// Deferred out-of-tile taps (SOC_SSAO_TILE=2): the tile pass runs every pixel's taps from LDS only (no global load,
-// no exec-masked wait on a few lanes' gathers). A pixel whose next tap pair leaves the tile stops there and is appended
-// to a workgroup list (its pixel, the pair index and its partial occlusion); after a barrier the workgroup's lanes take
-// the list densely and finish those pixels from the pair they stopped at (tile taps from LDS, the others from the D32
-// image). The occlusion sum keeps its order, so the same bits as ssao_kernel.
-template <int TXP, int TYP, int HALO>
-__global__ __attribute__((amdgpu_flat_work_group_size(TXP * TYP, TXP * TYP)))
-__attribute__((amdgpu_waves_per_eu(TXP * TYP >= 1024 ? 8 : TXP * TYP >= 512 ? 4 : 2)))
-void ssao_defer_kernel(DImg depth, DImg normal, DImg target, const float2* __restrict__ table, SsaoParams p) {
-    using T = SsaoTile<TXP, TYP, HALO>;
-    static_assert(T::THREADS <= 1024 && SOC_SSAO_MAX_KERNEL / 2 <= 64, "list entry: 10-bit lane, 6-bit tap pair");
-    __shared__ float4 tile4[T::TW * T::TH / 4];
-    // the list: 6 B per lane, so that with the 72-KiB tile two workgroups still fit a CU's 160 KiB of LDS
-    __shared__ uint16_t dlist[T::THREADS];
-    __shared__ float docc[T::THREADS];
-    __shared__ uint32_t dcount;
-    int bx, by;
-    xcd_order(p.swz, bx, by);
-    const int tid = threadIdx.x;
-    const int gx0 = bx * 2 * TXP - HALO, gy0 = by * 2 * TYP - HALO;
-    const __amdgpu_buffer_rsrc_t rsrc = depth_rsrc(depth);
-    if (tid == 0) dcount = 0u;
-    constexpr int Q = T::TW / 4;
-    for (int i = tid; i < Q * T::TH; i += T::THREADS) {
-        const int r = i / Q, c = i - r * Q;
-        const int gy = min(max(gy0 + r, 0), depth.h - 1);
-        const int off = __mul24(gy, depth.pitch) + (gx0 + 4 * c) * 4;
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0);
-        tile4[i] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
-    }
-    __syncthreads();
-    auto pixel_of = [&](int t, int& x, int& y) {
-        const int w = t >> 6, lane = t & 63;
-        x = bx * TXP + (w % (TXP / 32)) * 32 + (lane & 31);
-        y = by * TYP + (w / (TXP / 32)) * 2 + (lane >> 5);
-    };
-    const float* tf = reinterpret_cast<const float*>(tile4);
-    // phase 1: the lane's own pixel from the tile
-    {
-        int x, y;
-        pixel_of(tid, x, y);
-        int stop = -1;
-        float occ = 0.0f;
-        if (x < target.w && y < target.h) {
-            LdsQuad<TXP, TYP, HALO, false> q{tf, gx0, gy0, GlobalQuad{rsrc, depth.pitch}};
-            q.fb = false;
-            ssao_pixel<true, true, true, LdsQuad<TXP, TYP, HALO, false>, 2, true, 1>(x, y, depth, normal, target, table, p, q, 0,
-                                                                                      0.0f, true, &stop, &occ);
-        }
-        if (stop >= 0) {
-            const uint32_t slot = atomicAdd(&dcount, 1u);
-            dlist[slot] = (uint16_t)(tid | (stop >> 1) << 10);
-            docc[slot] = occ;
-        }
-    }
-    __syncthreads();
-    // phase 2: list entry tid (a lane appends at most one entry, so the list fits the workgroup: no loop)
-    if ((uint32_t)tid < dcount) {
-        const uint32_t e = dlist[tid];
-        int x, y;
-        pixel_of((int)(e & 1023u), x, y);
-        const LdsQuad<TXP, TYP, HALO, true> q{tf, gx0, gy0, GlobalQuad{rsrc, depth.pitch}};
-        ssao_pixel<true, true, true, LdsQuad<TXP, TYP, HALO, true>, 2, true, 1>(x, y, depth, normal, target, table, p, q,
-                                                                                 (int)(e >> 10) * 2, docc[tid], false);
-    }
 }
 
 // ssao_blur.inl:91-106: 4x4 box at offsets -2..+1 (x outer, y inner), all taps on texel centres.
@@ -553,15 +461,9 @@ extern "C" int soc_ssao_generation(const soc_globals* g, soc_img depth, soc_img 
 #define SOC_SSAO_LAUNCH(T, B, F) launch("ssao_kernel", kWorkgroup, ssao_kernel<T, B, F>, grd, blk, 0, st, dd, dn, dt, tb, p)
     const bool full = p.ksize == SOC_SSAO_MAX_KERNEL;
     // default: the LDS-tiled kernel (64 x 16 pixels, 32-texel halo) in the contiguous-eighths XCD order; SOC_SSAO_TILE=0
-    // selects the plain gather kernel, 2 the deferred out-of-tile taps (the same bits: tests/test_gpu_parity.py)
-    const int tiled = tuning_knob("SOC_SSAO_TILE", 1);
-    if (noise_table && sip && full && tiled == 2) {
-        SsaoParams pt = p;
-        pt.swz = 1;
-        const dim3 g(ceil_div(target.width, kSsaoTX), ceil_div(target.height, kSsaoTY));
-        launch("ssao_defer_kernel", kSsaoTileLanes, ssao_defer_kernel<kSsaoTX, kSsaoTY, kSsaoHalo>, g, kSsaoTileLanes, 0, st,
-               dd, dn, dt, tb, pt);
-    } else if (noise_table && sip && full && tiled) {
+    // selects the plain gather kernel (the same bits: tests/test_gpu_parity.py)
+    const bool tiled = tuning_knob("SOC_SSAO_TILE", 1) != 0;
+    if (noise_table && sip && full && tiled) {
         SsaoParams pt = p;
         pt.swz = 1;
         const dim3 g(ceil_div(target.width, kSsaoTX), ceil_div(target.height, kSsaoTY));

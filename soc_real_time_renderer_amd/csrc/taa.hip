@@ -417,119 +417,6 @@ __global__ __launch_bounds__(64 * kTaaRows) void taa_lds(DImg target, DImg cur, 
                       [&]() { return vt[ty + 1][pl + 1]; }, HistLoad{prev, pvel});
 }
 
-// Two pixel pairs per lane, stacked (rows y, y + 1): a workgroup of 64 x 4 lanes covers 128 x 8 output pixels and
-// stages 10 rows instead of 6 per 4. The lane reads the 4 neighbourhood rows once for both pairs, and row y + 1's
-// history taps reuse row y's lower history row wherever they are the same texels (same column pair, the next row:
-// the usual case under a smooth velocity field), so a quad costs 3 history rows per image instead of 4. Only loads
-// are shared: every pixel reaches taa_pair_tail with the same values as in taa_pair2 / taa_lds, so the same bits.
-constexpr int kTaaQuadRows = 2 * kTaaLdsRows;                     // output rows per workgroup
-#ifndef SOC_TAA_QUAD_WAVES
-#define SOC_TAA_QUAD_WAVES 1   // minimum waves per SIMD the register allocation must allow (A/B builds)
-#endif
-template <bool TM>
-__global__ __launch_bounds__(kTaaLdsLanes) __attribute__((amdgpu_waves_per_eu(SOC_TAA_QUAD_WAVES))) void taa_quad(DImg target, DImg cur, DImg prev, DImg vel, DImg pvel, DImg depth,
-                                                         DImg vel_out, TaaParams p, TmOut tm) {
-    constexpr int kTR = kTaaQuadRows + 2, NT = kTaaLdsLanes;     // staged rows y0 - 1 .. y0 + 8
-    __shared__ uint4 ct[kTR][kTaaTP];
-    __shared__ uint4 vt[kTR][kTaaTP];
-    __shared__ float4 dt[kTR][kTaaTQ];
-    int tbx, tby;
-    xcd_order(p.swz, tbx, tby);
-    const int W = target.w, H = target.h;
-    const int tid = threadIdx.x + threadIdx.y * 64;
-    const int p0 = tbx * kTaaPairs, y0 = tby * kTaaQuadRows, q0 = tbx * (kTaaPairs / 2);
-    const int npairs = W >> 1, nquads = (W + 3) >> 2;
-    for (int i = tid; i < kTR * kTaaTP; i += NT) {
-        const int r = i / kTaaTP, c = i - r * kTaaTP;
-        const int sy = min(max(y0 - 1 + r, 0), H - 1), sp = min(max(p0 - 1 + c, 0), npairs - 1);
-        ct[r][c] = row_ptr<uint4>(cur, sy)[sp];
-        vt[r][c] = row_ptr<uint4>(vel, sy)[sp];
-    }
-    for (int i = tid; i < kTR * kTaaTQ; i += NT) {
-        const int r = i / kTaaTQ, c = i - r * kTaaTQ;
-        const int sy = min(max(y0 - 1 + r, 0), H - 1), sq = min(max(q0 - 1 + c, 0), nquads - 1);
-        const float* drow = row_ptr<float>(depth, sy);
-        if (4 * sq + 3 < W) dt[r][c] = *reinterpret_cast<const float4*>(drow + 4 * sq);
-        else dt[r][c] = float4{drow[4 * sq], drow[min(4 * sq + 1, W - 1)], drow[min(4 * sq + 2, W - 1)], drow[min(4 * sq + 3, W - 1)]};
-    }
-    __syncthreads();
-    const int pl = threadIdx.x, t2 = 2 * (int)threadIdx.y;
-    const int x0 = 2 * (p0 + pl), ya = y0 + t2;
-    if (x0 >= W || ya >= H) return;
-    const int xl = max(x0 - 1, 0), xr = min(x0 + 2, W - 1);
-    const float* dtf = reinterpret_cast<const float*>(dt);
-    const int dbase = 4 * (q0 - 1);
-    // the 3 neighbourhood rows of output row yy (image rows yy + 1 .. yy - 1, clamped) from the staged tiles
-    auto nbhd = [&](int yy, int (&rows)[3], h2 (&Cxy)[3][4], h2 (&Czw)[3][4], float (&D)[3][4]) {
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-            const int tr = yy + 1 - r - (y0 - 1);
-            rows[r] = min(max(yy + 1 - r, 0), H - 1);
-            const uint4 mid = ct[tr][pl + 1];
-            uint2 L = uint2{ct[tr][pl].z, ct[tr][pl].w}, R = uint2{ct[tr][pl + 2].x, ct[tr][pl + 2].y};
-            const float* drow = dtf + tr * 4 * kTaaTQ - dbase;
-            const float2 dmid = *reinterpret_cast<const float2*>(drow + x0);
-            float dl = drow[x0 - 1], dr = drow[x0 + 2];
-            if (x0 == 0) { L = uint2{mid.x, mid.y}; dl = dmid.x; }
-            if (x0 + 2 >= W) { R = uint2{mid.z, mid.w}; dr = dmid.y; }
-            Cxy[r][0] = as_h2(L.x);
-            Czw[r][0] = as_h2(L.y);
-            Cxy[r][1] = as_h2(mid.x);
-            Czw[r][1] = as_h2(mid.y);
-            Cxy[r][2] = as_h2(mid.z);
-            Czw[r][2] = as_h2(mid.w);
-            Cxy[r][3] = as_h2(R.x);
-            Czw[r][3] = as_h2(R.y);
-            D[r][0] = dl;
-            D[r][1] = dmid.x;
-            D[r][2] = dmid.y;
-            D[r][3] = dr;
-        }
-    };
-    const float exposure = TM ? tm.ae->exposure : 0.0f;
-    const uint32_t* vtw = reinterpret_cast<const uint32_t*>(vt);
-    auto vel_at = [&](int bx, int by) {
-        const int tr = by - (y0 - 1), c = (bx >> 1) - (p0 - 1);
-        return vtw[(tr * kTaaTP + c) * 4 + 2 * (bx & 1)];
-    };
-    // row ya's lower history rows (per pixel k and image: colour, velocity) and where they are
-    u4a8 keep[2][2];
-    int kx[2], ky[2];
-    auto hist_a = [&](int k, int which, const Axis& ax, const Axis& ay, u4a8& r0, u4a8& r1) {
-        const DImg& im = which ? pvel : prev;
-        r0 = *reinterpret_cast<const u4a8*>(row_ptr<uint2>(im, ay.i0) + ax.i0);
-        r1 = *reinterpret_cast<const u4a8*>(row_ptr<uint2>(im, ay.i1) + ax.i0);
-        keep[k][which] = r1;
-        kx[k] = ax.i0;
-        ky[k] = ay.i1;
-    };
-    auto hist_b = [&](int k, int which, const Axis& ax, const Axis& ay, u4a8& r0, u4a8& r1) {
-        const DImg& im = which ? pvel : prev;
-        if (ax.i0 == kx[k] && ay.i0 == ky[k]) r0 = keep[k][which];
-        else r0 = *reinterpret_cast<const u4a8*>(row_ptr<uint2>(im, ay.i0) + ax.i0);
-        r1 = *reinterpret_cast<const u4a8*>(row_ptr<uint2>(im, ay.i1) + ax.i0);
-    };
-    {
-        int rows[3];
-        h2 Cxy[3][4], Czw[3][4];
-        float D[3][4];
-        nbhd(ya, rows, Cxy, Czw, D);
-        taa_pair_tail<TM>(target, prev, pvel, vel_out, p, tm, x0, ya, xl, xr, rows, Cxy, Czw, D, exposure, vel_at,
-                          [&]() { return vt[t2 + 1][pl + 1]; }, hist_a);
-    }
-    if (ya + 1 >= H) return;
-    // re-read the shared neighbourhood rows from LDS instead of keeping them in registers (106 VGPRs instead of 122)
-    asm volatile("" ::: "memory");
-    {
-        int rows[3];
-        h2 Cxy[3][4], Czw[3][4];
-        float D[3][4];
-        nbhd(ya + 1, rows, Cxy, Czw, D);
-        taa_pair_tail<TM>(target, prev, pvel, vel_out, p, tm, x0, ya + 1, xl, xr, rows, Cxy, Czw, D, exposure, vel_at,
-                          [&]() { return vt[t2 + 2][pl + 1]; }, hist_b);
-    }
-}
-
 __global__ __launch_bounds__(kWorkgroup) void taa_generic(DImg target, DImg cur, DImg prev, DImg vel, DImg pvel, DImg depth,
                                                    DImg vel_out, TaaParams p) {
     const int x = blockIdx.x * BX + threadIdx.x, y = blockIdx.y * BY + threadIdx.y;
@@ -624,20 +511,11 @@ int taa_launch(const soc_globals* g, soc_img target, soc_img current_color, soc_
         // 32 x 8 lanes (64 x 8 pixels): the 3-row neighbourhood reloads 10 rows per 8 instead of 6 per 4
         const int by = 8, bxl = 256 / by;
         dim3 blk(bxl, by), g2(ceil_div(W / 2, bxl), ceil_div(H, by));
-        // neighbourhood source: 4 = LDS-staged tiles, two pairs per lane (taa_quad), 3 = LDS-staged tiles (default; both
-        // need a 16-B aligned depth image), 2 = halo lanes, 1 = lane
+        // neighbourhood source: 3 = LDS-staged tiles (default; needs a 16-B aligned depth image), 2 = halo lanes, 1 = lane
         // shifts + edge-lane loads, 0 = every lane loads its side columns (the same bits, tests/test_gpu_parity.py)
         const int nbr = tuning_knob("SOC_TAA_NBR", 3);
         const dim3 blk_h(64, 4), g2_h(ceil_div(W / 2, 62), ceil_div(H, 4));
-        if (nbr == 4 && a16(depth)) {
-            const dim3 gq(ceil_div(W / 2, kTaaPairs), ceil_div(H, kTaaQuadRows));
-            if (tm)
-                launch("taa_quad", kTaaLdsLanes, taa_quad<true>, gq, blk_h, 0, hs(stream), dimg(target), dimg(current_color),
-                       dimg(previous_color), dimg(current_velocity), dimg(previous_velocity), dimg(depth), vo, p, *tm);
-            else
-                launch("taa_quad", kTaaLdsLanes, taa_quad<false>, gq, blk_h, 0, hs(stream), dimg(target), dimg(current_color),
-                       dimg(previous_color), dimg(current_velocity), dimg(previous_velocity), dimg(depth), vo, p, TmOut{});
-        } else if (nbr == 3 && a16(depth)) {
+        if (nbr == 3 && a16(depth)) {
             const dim3 gl(ceil_div(W / 2, kTaaPairs), ceil_div(H, 4));
             if (tm)
                 launch("taa_lds", kTaaLdsLanes, taa_lds<true>, gl, blk_h, 0, hs(stream), dimg(target), dimg(current_color), dimg(previous_color),

@@ -390,7 +390,8 @@ def test_sponza_mesh_mipmapped_gbuffer_vs_oracle(soc, oracle, tex):
 @pytest.mark.parametrize("tex", [128, 96])
 def test_mipmapped_gbuffer_shared_footprint_bit_identical(soc, monkeypatch, tex):
     """The resolve samples a material's normal image and albedo of one extent with one shared footprint / tap /
-    lod computation (SOC_GB_TEX_PAIRS, default on): the same bits as sampling them one after the other."""
+    lod computation (SOC_GB_TEX_PAIRS, default on): the same bits as sampling them one after the other. Every
+    wave / workgroup shape (SOC_GB_WAVE 0-4; 270 rows: partial tiles of 8, 16 and 32 rows) gives the same bits."""
     W, H = 480, 270
     g = globals_for(W, H)
     _, dm = _mesh_scene()
@@ -401,8 +402,9 @@ def test_mipmapped_gbuffer_shared_footprint_bit_identical(soc, monkeypatch, tex)
     vis = torch.zeros((H, W), dtype=torch.int64, device=DEV)
     raster.raster_visibility(dm, vp, raster.CULL_FRONT, vis, ws)
     outs = []
-    for pairs in ("1", "0"):
+    for pairs, wave in (("1", "2"), ("0", "2"), ("1", "0"), ("1", "1"), ("1", "3"), ("1", "4")):
         monkeypatch.setenv("SOC_GB_TEX_PAIRS", pairs)
+        monkeypatch.setenv("SOC_GB_WAVE", wave)
         soc.reload_tuning()
         out = {k: torch.zeros((H, W, 4), dtype=torch.float16, device=DEV) for k in ("albedo", "emissive", "normal", "velocity")}
         out["depth"] = torch.zeros((H, W), dtype=torch.float32, device=DEV)
@@ -410,9 +412,11 @@ def test_mipmapped_gbuffer_shared_footprint_bit_identical(soc, monkeypatch, tex)
                                out["velocity"], ws)
         outs.append(out)
     monkeypatch.delenv("SOC_GB_TEX_PAIRS")
+    monkeypatch.delenv("SOC_GB_WAVE")
     soc.reload_tuning()
-    for k in outs[0]:
-        assert torch.equal(outs[0][k], outs[1][k]), k
+    for o in outs[1:]:
+        for k in outs[0]:
+            assert torch.equal(outs[0][k], o[k]), k
 
 
 @pytest.mark.parametrize("size,grid,level", [(1024, 100, 3), (128, 100, 3), (64, 17, 5), (32, 2, 1)])
