@@ -23,7 +23,7 @@ shift
 bench_line() {   # name, bench args...
   local n=$1; shift
   timeout -k 10 400 python bench.py "$@" > gpurun_out/$n.json 2> gpurun_out/$n.err || { echo "bench $n failed"; tail -5 gpurun_out/$n.err; exit 1; }
-  python -c "import json;d=json.load(open('gpurun_out/$n.json'));pk=d['roofline'].get('per_kernel',{});print('$n', d['value'], 'fps', d['ms_per_step'], 'ms', 'frac', d['roofline']['frac'], {k[:11]: v['avg_launch_us'] for k, v in pk.items()}, d['ms_per_group'])"
+  python -c "import json;d=json.load(open('gpurun_out/$n.json'));pk=d['roofline'].get('per_kernel',{});print('$n', d['value'], 'fps', d['ms_per_step'], 'ms', 'frac', d['roofline']['frac'], {k[:11]: v['avg_launch_us'] for k, v in pk.items() if v}, d['ms_per_group'])"
 }
 
 kernel_trace() {   # tag, bench args...
