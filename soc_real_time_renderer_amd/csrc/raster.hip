@@ -32,6 +32,10 @@ constexpr int SMALL_PIXELS = 64;    // bounding boxes up to this many pixels are
 #define SOC_RASTER_TILE 32
 #endif
 constexpr int TILE = SOC_RASTER_TILE;   // large-triangle work item: a TILE x TILE tile of its bounding box
+#ifndef SOC_RASTER_FIXED_COLS
+#define SOC_RASTER_FIXED_COLS 0   // A/B builds: raster_big's lanes as 32 x 2 pixels whatever the item's width
+#endif
+static_assert(TILE == 32 || SOC_RASTER_FIXED_COLS, "raster_big's lane layout covers items up to 32 pixels wide");
 constexpr uint32_t KEY_EMPTY = 0xFFFFFFFFu;
 
 struct RasterParams {
@@ -104,6 +108,34 @@ struct TriSetup {
     bool live;
 };
 
+// Screen bounding box of the part of a triangle in front of the depth-clip plane z_c = 0: its vertices there and its
+// edges' crossings of the plane, projected (wide: a point at w <= 1e-20, the box is the whole image). Plain values and
+// flags in a struct (a capturing lambda here had its two flags spilled to scratch).
+struct BBox {
+    float minx = 3.0e38f, maxx = -3.0e38f, miny = 3.0e38f, maxy = -3.0e38f;
+    bool any = false, wide = false;
+};
+__device__ __forceinline__ void bbox_add(BBox& b, float X, float Y, float Wc) {
+#pragma clang fp contract(off)
+    if (!(Wc > 1e-20f)) {
+        b.wide = true;
+        return;
+    }
+    const float x = X / Wc, y = Y / Wc;
+    b.minx = fminf(b.minx, x); b.maxx = fmaxf(b.maxx, x);
+    b.miny = fminf(b.miny, y); b.maxy = fmaxf(b.maxy, y);
+    b.any = true;
+}
+// vertex a, and where the edge a -> b crosses z_c = 0
+__device__ __forceinline__ void bbox_edge(BBox& bb, float4 a, float4 b) {
+#pragma clang fp contract(off)
+    if (a.z >= 0.0f) bbox_add(bb, a.x, a.y, a.w);
+    if ((a.z >= 0.0f) != (b.z >= 0.0f)) {
+        const float u = a.z / (a.z - b.z);
+        bbox_add(bb, a.x + u * (b.x - a.x), a.y + u * (b.y - a.y), a.w + u * (b.w - a.w));
+    }
+}
+
 // Triangle setup: the adjugate rows r_i of [v0 v1 v2] (v = (X, Y, W)), det = v0 . r0. Facing is the
 // sign of det (= the sign of the framebuffer area when every w > 0; Vulkan a = -area/2 < 0 is
 // clockwise = front, the reference pipelines' winding: see soc_rt.h). Bounding box from the projected vertices when every w > 1e-6, else the
@@ -127,25 +159,12 @@ __device__ __forceinline__ TriSetup tri_setup(float4 A, float4 B, float4 C, cons
     // covered centres. The oracle scans the whole image for such triangles; coverage itself is decided
     // per pixel by the edge functions only, so the results are identical.
     {
-        const float4 P[3] = {A, B, C};
-        float minx = 3.0e38f, maxx = -3.0e38f, miny = 3.0e38f, maxy = -3.0e38f;
-        bool any = false, wide = false;
-        auto add = [&](float X, float Y, float Wc) {
-            if (!(Wc > 1e-20f)) { wide = true; return; }
-            const float x = X / Wc, y = Y / Wc;
-            minx = fminf(minx, x); maxx = fmaxf(maxx, x);
-            miny = fminf(miny, y); maxy = fmaxf(maxy, y);
-            any = true;
-        };
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const float4 a = P[i], b = P[(i + 1) % 3];
-            if (a.z >= 0.0f) add(a.x, a.y, a.w);
-            if ((a.z >= 0.0f) != (b.z >= 0.0f)) {   // edge crosses z_c = 0
-                const float u = a.z / (a.z - b.z);
-                add(a.x + u * (b.x - a.x), a.y + u * (b.y - a.y), a.w + u * (b.w - a.w));
-            }
-        }
+        BBox bb;
+        bbox_edge(bb, A, B);
+        bbox_edge(bb, B, C);
+        bbox_edge(bb, C, A);
+        const float minx = bb.minx, maxx = bb.maxx, miny = bb.miny, maxy = bb.maxy;
+        const bool any = bb.any, wide = bb.wide;
         if (!any && !wide) return t;   // wholly behind the depth-clip plane
         const float W = (float)p.width, H = (float)p.height;
         if (wide || minx != minx || miny != miny || maxx != maxx || maxy != maxy) {
@@ -260,6 +279,119 @@ __global__ __launch_bounds__(kWorkgroup) void raster_small(const uint32_t* __res
         for (int x = t.px0; x <= t.px1; ++x) shade(t, id, x, y, p, target, pitch);
 }
 
+// Load-balanced small triangles (default; SOC_RASTER_SMALL_LB=0: raster_small). A wave's small triangles (box <= 64
+// pixels) have 47 box pixels on average and up to 64, so one lane scanning its own box keeps the wave for the largest
+// box with most lanes idle. Here the wave's small triangles are compacted into LDS (setup, first pixel index in the
+// wave's concatenated boxes) and the lanes take the concatenated pixels 64 at a time: the owner of pixel k is the last
+// triangle starting at or before k (a marker per start, then a max-scan across the wave). The large triangles append
+// their tile ranges with one atomic per wave (a wave prefix sum of their tile counts) instead of one per triangle; the
+// entries stay in increasing range order. Every pixel runs the same shade() with the same setup: the same atomics.
+struct SmallTri {
+    float r[9], z[3], w[3], bias;
+    int id, px0, py0, bw;
+    uint32_t magic;   // ceil(65536 / bw): (q magic) >> 16 == q / bw for q < 64 (checked for every bw <= 64)
+    uint32_t start;   // first pixel in the wave's concatenation
+    uint32_t pad[2];
+};
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = (uint32_t)__shfl_up((int)v, d, 64);
+        if (lane >= d) v += o;
+    }
+    return v;
+}
+__device__ __forceinline__ int wave_incl_max(int v, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int o = __shfl_up(v, d, 64);
+        if (lane >= d) v = max(v, o);
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(kWorkgroup) void raster_small_lb(const uint32_t* __restrict__ idx, Workspace ws, RasterParams p,
+                                                       void* target, size_t pitch) {
+    __shared__ SmallTri st[kWorkgroup / 64][64];
+    __shared__ int mk[kWorkgroup / 64][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int id = blockIdx.x * kWorkgroup + threadIdx.x;
+    TriSetup t;
+    t.live = false;
+    if (id < p.triangle_count) t = load_tri(ws, idx, id, p);
+    int bw = 0, bh = 0;
+    long long n = 0;
+    if (t.live) {
+        bw = t.px1 - t.px0 + 1;
+        bh = t.py1 - t.py0 + 1;
+        n = (long long)bw * bh;
+    }
+    const bool big = t.live && n > p.small_pixels, small = t.live && !big;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    // large triangles: one 64-bit atomicAdd per wave, slots and tile ranges by wave prefix
+    const unsigned long long bmask = __ballot(big);
+    if (bmask) {   // wave-uniform
+        const uint32_t chunks = big ? (uint32_t)(((bw + TILE - 1) / TILE) * ((bh + TILE - 1) / TILE)) : 0u;
+        const uint32_t cincl = wave_incl_sum(chunks, lane);
+        const uint32_t ctot = (uint32_t)__shfl((int)cincl, 63, 64);
+        unsigned long long old = 0;
+        if (lane == 0) old = atomicAdd(ws.counter, ((unsigned long long)__builtin_popcountll(bmask) << ENTRY_SHIFT) + ctot);
+        const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)old, 0, 64), hi = (uint32_t)__shfl((int)(uint32_t)(old >> 32), 0, 64);
+        old = ((unsigned long long)hi << 32) | lo;
+        if (big) {
+            const unsigned long long mine =
+                old + ((unsigned long long)__builtin_popcountll(bmask & lt) << ENTRY_SHIFT) + (cincl - chunks);
+            ws.entries[mine >> ENTRY_SHIFT] = uint2{(uint32_t)id, (uint32_t)mine};
+        }
+    }
+    // small triangles: compacted in lane order, their boxes concatenated
+    const unsigned long long smask = __ballot(small);
+    if (!smask) return;   // wave-uniform
+    const uint32_t srank = (uint32_t)__builtin_popcountll(smask & lt);
+    const uint32_t ns = small ? (uint32_t)n : 0u;
+    const uint32_t pincl = wave_incl_sum(ns, lane);
+    const uint32_t total = (uint32_t)__shfl((int)pincl, 63, 64);
+    if (small) {
+        SmallTri& e = st[w][srank];
+        e.r[0] = t.r0.x; e.r[1] = t.r0.y; e.r[2] = t.r0.z;
+        e.r[3] = t.r1.x; e.r[4] = t.r1.y; e.r[5] = t.r1.z;
+        e.r[6] = t.r2.x; e.r[7] = t.r2.y; e.r[8] = t.r2.z;
+        e.z[0] = t.z0; e.z[1] = t.z1; e.z[2] = t.z2;
+        e.w[0] = t.w0; e.w[1] = t.w1; e.w[2] = t.w2;
+        e.bias = t.bias;
+        e.id = id;
+        e.px0 = t.px0;
+        e.py0 = t.py0;
+        e.bw = bw;
+        e.magic = (65536u + (uint32_t)bw - 1u) / (uint32_t)bw;
+        e.start = pincl - ns;
+    }
+    int carry = 0;
+#pragma unroll 1
+    for (uint32_t base = 0; base < total; base += 64) {
+        mk[w][lane] = -1;
+        __builtin_amdgcn_wave_barrier();
+        if (small && pincl - ns >= base && pincl - ns < base + 64) mk[w][pincl - ns - base] = (int)srank;
+        __builtin_amdgcn_wave_barrier();
+        const int o = max(wave_incl_max(mk[w][lane], lane), carry);
+        carry = __shfl(o, 63, 64);
+        const uint32_t k = base + (uint32_t)lane;
+        if (k < total) {
+            const SmallTri& e = st[w][o];
+            TriSetup s;
+            s.r0 = f3{e.r[0], e.r[1], e.r[2]};
+            s.r1 = f3{e.r[3], e.r[4], e.r[5]};
+            s.r2 = f3{e.r[6], e.r[7], e.r[8]};
+            s.z0 = e.z[0]; s.z1 = e.z[1]; s.z2 = e.z[2];
+            s.w0 = e.w[0]; s.w1 = e.w[1]; s.w2 = e.w[2];
+            s.bias = e.bias;
+            const uint32_t q = k - e.start, yo = (q * e.magic) >> 16, xo = q - yo * (uint32_t)e.bw;
+            shade(s, e.id, e.px0 + (int)xo, e.py0 + (int)yo, p, target, pitch);
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 // Upper bound of the edge function over the pixel centres of [x0, x1] x [y0, y1] (a corner), minus a
 // rounding margin: < 0 means no centre of the tile can pass this edge.
 __device__ __forceinline__ float edge_max(f3 r, float x0, float x1, float y0, float y1) {
@@ -308,9 +440,19 @@ __global__ __launch_bounds__(kWorkgroup) void raster_big(const uint32_t* __restr
         if (edge_max(t.r0, fx0, fx1, fy0, fy1) < 0.0f || edge_max(t.r1, fx0, fx1, fy0, fy1) < 0.0f ||
             edge_max(t.r2, fx0, fx1, fy0, fy1) < 0.0f)
             continue;
+#if SOC_RASTER_FIXED_COLS
         const int x = x0 + (lane % TILE);
         if (x > x1) continue;
         for (int y = y0 + lane / TILE; y <= y1; y += 64 / TILE) shade(t, (int)item.x, x, y, p, target, pitch);
+#else
+        // the wave's lanes as cols x (64 / cols) pixels, cols the smallest power of two >= the item's width (4..TILE):
+        // a narrow box (the median large triangle's is 14 x 15 pixels at 4K) keeps most lanes on its pixels
+        const int cw = x1 - x0 + 1;
+        const int lc = cw <= 4 ? 2 : cw <= 8 ? 3 : cw <= 16 ? 4 : 5;   // log2 cols (TILE = 32)
+        const int x = x0 + (lane & ((1 << lc) - 1));
+        if (x > x1) continue;
+        for (int y = y0 + (lane >> lc); y <= y1; y += 64 >> lc) shade(t, (int)item.x, x, y, p, target, pitch);
+#endif
     }
 }
 
@@ -566,8 +708,11 @@ __device__ __forceinline__ VtxData fetch_vertex(const soc_mesh& mesh, const floa
     return VtxData{vd[4 * v], vd[4 * v + 1], vd[4 * v + 2], vd[4 * v + 3]};
 }
 
+#ifndef SOC_GB_WAVES
+#define SOC_GB_WAVES 5   // waves per SIMD the resolve's registers allow: 96 VGPRs, no spill (A/B builds: 1 = unconstrained)
+#endif
 template <bool PRE>
-__global__ __launch_bounds__(kWorkgroup) void gbuffer_resolve(soc_mesh mesh, const soc_material* __restrict__ mats,
+__global__ __launch_bounds__(kWorkgroup) __attribute__((amdgpu_waves_per_eu(SOC_GB_WAVES))) void gbuffer_resolve(soc_mesh mesh, const soc_material* __restrict__ mats,
                                                        const unsigned long long* __restrict__ vis, DImg depth,
                                                        DImg albedo, DImg emissive, DImg normal, DImg velocity,
                                                        const float4* __restrict__ vd, ResolveParams p) {
@@ -628,6 +773,21 @@ __global__ __launch_bounds__(kWorkgroup) void gbuffer_resolve(soc_mesh mesh, con
     const float v = b0 * uv[2 * ia + 1] + b1 * uv[2 * ib + 1] + b2 * uv[2 * ic + 1];
     const uint32_t mi = mesh.materials ? min(mesh.materials[id], (uint32_t)(p.material_count - 1)) : 0u;
     const soc_material& m = mats[mi];
+    // velocity and depth first: the clip positions are dead before the texture taps (123 -> fewer live VGPRs there)
+    {
+        f4 vel = f4{0.0f, 0.0f, 0.0f, 0.0f};
+        if (!(m.flags & SOC_MATERIAL_ZERO_VELOCITY)) {
+            const float4 ca = VA.cc, cb = VB.cc, cd = VC.cc, pa = VA.pc, pb = VB.pc, pd = VC.pc;
+            const float cx = b0 * ca.x + b1 * cb.x + b2 * cd.x, cy = b0 * ca.y + b1 * cb.y + b2 * cd.y;
+            const float cw = b0 * ca.z + b1 * cb.z + b2 * cd.z;
+            const float px = b0 * pa.x + b1 * pb.x + b2 * pd.x, py = b0 * pa.y + b1 * pb.y + b2 * pd.y;
+            const float pw = b0 * pa.z + b1 * pb.z + b2 * pd.z;
+            vel = f4{((cx / cw) * 0.5f + 0.5f) - ((px / pw) * 0.5f + 0.5f), ((cy / cw) * 0.5f + 0.5f) - ((py / pw) * 0.5f + 0.5f),
+                     0.0f, 1.0f};
+        }
+        row_ptr_w<float>(depth, y)[x] = __uint_as_float((uint32_t)(key >> 32));
+        row_ptr_w<uint2>(velocity, y)[x] = pack_h4(vel);
+    }
     f3 n;
     if ((m.flags & SOC_MATERIAL_NORMAL_MAP) && m.normal_map.data) {   // draw_terrain.inl:206-219
         const DImg nm{static_cast<char*>(m.normal_map.data), m.normal_map.width, m.normal_map.height, m.normal_map.pitch_bytes};
@@ -694,22 +854,10 @@ __global__ __launch_bounds__(kWorkgroup) void gbuffer_resolve(soc_mesh mesh, con
         em = f3{e.x * m.emissive_factor[0], e.y * m.emissive_factor[1], e.z * m.emissive_factor[2]};
     }
     const f4 al = pair ? al_pair : tex(m.albedo);
-    f4 vel = f4{0.0f, 0.0f, 0.0f, 0.0f};
-    if (!(m.flags & SOC_MATERIAL_ZERO_VELOCITY)) {
-        const float4 ca = VA.cc, cb = VB.cc, cd = VC.cc, pa = VA.pc, pb = VB.pc, pd = VC.pc;
-        const float cx = b0 * ca.x + b1 * cb.x + b2 * cd.x, cy = b0 * ca.y + b1 * cb.y + b2 * cd.y;
-        const float cw = b0 * ca.z + b1 * cb.z + b2 * cd.z;
-        const float px = b0 * pa.x + b1 * pb.x + b2 * pd.x, py = b0 * pa.y + b1 * pb.y + b2 * pd.y;
-        const float pw = b0 * pa.z + b1 * pb.z + b2 * pd.z;
-        vel = f4{((cx / cw) * 0.5f + 0.5f) - ((px / pw) * 0.5f + 0.5f), ((cy / cw) * 0.5f + 0.5f) - ((py / pw) * 0.5f + 0.5f),
-                 0.0f, 1.0f};
-    }
-    row_ptr_w<float>(depth, y)[x] = __uint_as_float((uint32_t)(key >> 32));
     row_ptr_w<uint2>(albedo, y)[x] = pack_h4(f4{al.x * m.albedo_factor[0] + em.x, al.y * m.albedo_factor[1] + em.y,
                                                 al.z * m.albedo_factor[2] + em.z, 1.0f});
     row_ptr_w<uint2>(emissive, y)[x] = pack_h4(f4{em.x, em.y, em.z, 1.0f});
     row_ptr_w<uint2>(normal, y)[x] = pack_h4(f4{n.x, n.y, n.z, 1.0f});
-    row_ptr_w<uint2>(velocity, y)[x] = pack_h4(vel);
 }
 
 int check_mesh(const soc_mesh* mesh, const char* pass, bool attributes) {
@@ -740,7 +888,11 @@ int launch_raster(const soc_mesh* mesh, const RasterParams& p, void* target, siz
     Workspace ws = carve(workspace, mesh->vertex_count, mesh->triangle_count);
     launch("raster_setup", kWorkgroup, raster_setup, ceil_div(max(mesh->vertex_count, 1), 256), kWorkgroup, 0, s, mesh->positions, ws, p);
     if (mesh->triangle_count > 0) {
-        launch("raster_small", kWorkgroup, raster_small, ceil_div(mesh->triangle_count, 256), kWorkgroup, 0, s, mesh->indices, ws, p, target, pitch);
+        if (tuning_knob("SOC_RASTER_SMALL_LB", 1))
+            launch("raster_small_lb", kWorkgroup, raster_small_lb, ceil_div(mesh->triangle_count, kWorkgroup), kWorkgroup, 0, s,
+                   mesh->indices, ws, p, target, pitch);
+        else
+            launch("raster_small", kWorkgroup, raster_small, ceil_div(mesh->triangle_count, 256), kWorkgroup, 0, s, mesh->indices, ws, p, target, pitch);
         launch("raster_big", kWorkgroup, raster_big, 2048, kWorkgroup, 0, s, mesh->indices, ws, p, target, pitch);
     }
     return check_launch(pass);

@@ -1,7 +1,7 @@
 """Time one pass alone on the GPU for A/B library builds (soc_real_time_renderer_amd/csrc `make variant`), on the bench's
 own inputs, and hash its output so exact variants can be checked for identical bits.
 
-    python tools/pass_probe.py --pass clouds|ssao|gbuffer|taa --configs c3,c4 --variants libsoc_rt.so,libsoc_rt_x.so [--reps 100] [--rounds 3]
+    python tools/pass_probe.py --pass clouds|ssao|gbuffer|taa|raster --configs c3,c4 --variants libsoc_rt.so,libsoc_rt_x.so [--reps 100] [--rounds 3]
 
 A variant is a library file name (SOC_RT_LIB_VARIANT) or NAME=VALUE (a tuning knob on the default library). Each
 variant runs in its own process; the rounds interleave the variants so clock drift hits
@@ -46,6 +46,25 @@ def child(pass_name, configs, reps):
             run = lambda: raster.gbuffer_resolve(g, sc["mesh"], sc["materials"], sc["material_count"], vis,  # noqa: E731
                                                  fr["depth"], fr["albedo"], fr["emissive"], fr["normal"], fr["velocity"],
                                                  sc["workspace"])
+        elif pass_name == "raster":   # DepthPrepass (visibility) + SunShadowDraw (4096^2 depth) of the mesh
+            import numpy as np
+            from soc_real_time_renderer_amd import raster
+            sc = _sc
+            vis = torch.empty((H, W), dtype=torch.int64, device=dev)
+            shadow = torch.ones((4096, 4096), dtype=torch.float32, device=dev)
+            vp = np.ctypeslib.as_array(g.camera_projection_view_matrix)
+            svp = np.ctypeslib.as_array(g.sun_info.projection_view_matrix)
+
+            class Both:   # digest over both outputs
+                def cpu(self):
+                    return torch.cat([vis.view(torch.int32).reshape(-1), shadow.view(torch.int32).reshape(-1)]).cpu()
+            tgt = Both()
+
+            def run():
+                raster.raster_visibility(sc["mesh"], vp, raster.CULL_FRONT, vis, sc["workspace"])
+                shadow.fill_(1.0)
+                raster.raster_depth(sc["mesh"], svp, raster.CULL_BACK, shadow, sc["workspace"], raster.SHADOW_BIAS_CONSTANT,
+                                    raster.SHADOW_BIAS_SLOPE)
         elif pass_name == "taa":   # the fused TemporalAntiAliasing + ToneMapping launch (SOC_TAA_NBR picks the kernel)
             hc, hv = fr["history_color"], fr["history_velocity"]
             gen = torch.Generator(device=dev).manual_seed(1)
