@@ -144,6 +144,14 @@ __device__ __forceinline__ TriSetup tri_setup(float4 A, float4 B, float4 C, cons
 #pragma clang fp contract(off)
     TriSetup t;
     t.live = false;
+    // Wholly beyond the far plane: every vertex has w_c > 0 and z_c > w_c (1 + 2^-12). A covered pixel's E_i are >= 0, so
+    // z_ndc = sum E_i z_i / sum E_i w_i sums non-negative terms, each fp32 rounding is relative (<= 7 of 2^-24 in all),
+    // and the ratio is >= min z_i / w_i >= 1 + 2^-12: the computed z_ndc is > 1 and cover() clips every pixel. Skipping
+    // the triangle writes the same (nothing). The sun's orthographic frustum leaves most of the mesh beyond its far plane.
+    {
+        constexpr float kFar = 1.0f + 1.0f / 4096.0f;
+        if (A.w > 0.0f && B.w > 0.0f && C.w > 0.0f && A.z > A.w * kFar && B.z > B.w * kFar && C.z > C.w * kFar) return t;
+    }
     const f3 v0{A.x, A.y, A.w}, v1{B.x, B.y, B.w}, v2{C.x, C.y, C.w};
     f3 r0 = cross_exact(v1, v2), r1 = cross_exact(v2, v0), r2 = cross_exact(v0, v1);
     const float det = v0.x * r0.x + v0.y * r0.y + v0.z * r0.z;
@@ -277,119 +285,6 @@ __global__ __launch_bounds__(kWorkgroup) void raster_small(const uint32_t* __res
     }
     for (int y = t.py0; y <= t.py1; ++y)
         for (int x = t.px0; x <= t.px1; ++x) shade(t, id, x, y, p, target, pitch);
-}
-
-// Load-balanced small triangles (default; SOC_RASTER_SMALL_LB=0: raster_small). A wave's small triangles (box <= 64
-// pixels) have 47 box pixels on average and up to 64, so one lane scanning its own box keeps the wave for the largest
-// box with most lanes idle. Here the wave's small triangles are compacted into LDS (setup, first pixel index in the
-// wave's concatenated boxes) and the lanes take the concatenated pixels 64 at a time: the owner of pixel k is the last
-// triangle starting at or before k (a marker per start, then a max-scan across the wave). The large triangles append
-// their tile ranges with one atomic per wave (a wave prefix sum of their tile counts) instead of one per triangle; the
-// entries stay in increasing range order. Every pixel runs the same shade() with the same setup: the same atomics.
-struct SmallTri {
-    float r[9], z[3], w[3], bias;
-    int id, px0, py0, bw;
-    uint32_t magic;   // ceil(65536 / bw): (q magic) >> 16 == q / bw for q < 64 (checked for every bw <= 64)
-    uint32_t start;   // first pixel in the wave's concatenation
-    uint32_t pad[2];
-};
-__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v, int lane) {
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = (uint32_t)__shfl_up((int)v, d, 64);
-        if (lane >= d) v += o;
-    }
-    return v;
-}
-__device__ __forceinline__ int wave_incl_max(int v, int lane) {
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int o = __shfl_up(v, d, 64);
-        if (lane >= d) v = max(v, o);
-    }
-    return v;
-}
-
-__global__ __launch_bounds__(kWorkgroup) void raster_small_lb(const uint32_t* __restrict__ idx, Workspace ws, RasterParams p,
-                                                       void* target, size_t pitch) {
-    __shared__ SmallTri st[kWorkgroup / 64][64];
-    __shared__ int mk[kWorkgroup / 64][64];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int id = blockIdx.x * kWorkgroup + threadIdx.x;
-    TriSetup t;
-    t.live = false;
-    if (id < p.triangle_count) t = load_tri(ws, idx, id, p);
-    int bw = 0, bh = 0;
-    long long n = 0;
-    if (t.live) {
-        bw = t.px1 - t.px0 + 1;
-        bh = t.py1 - t.py0 + 1;
-        n = (long long)bw * bh;
-    }
-    const bool big = t.live && n > p.small_pixels, small = t.live && !big;
-    const unsigned long long lt = (1ull << lane) - 1ull;
-    // large triangles: one 64-bit atomicAdd per wave, slots and tile ranges by wave prefix
-    const unsigned long long bmask = __ballot(big);
-    if (bmask) {   // wave-uniform
-        const uint32_t chunks = big ? (uint32_t)(((bw + TILE - 1) / TILE) * ((bh + TILE - 1) / TILE)) : 0u;
-        const uint32_t cincl = wave_incl_sum(chunks, lane);
-        const uint32_t ctot = (uint32_t)__shfl((int)cincl, 63, 64);
-        unsigned long long old = 0;
-        if (lane == 0) old = atomicAdd(ws.counter, ((unsigned long long)__builtin_popcountll(bmask) << ENTRY_SHIFT) + ctot);
-        const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)old, 0, 64), hi = (uint32_t)__shfl((int)(uint32_t)(old >> 32), 0, 64);
-        old = ((unsigned long long)hi << 32) | lo;
-        if (big) {
-            const unsigned long long mine =
-                old + ((unsigned long long)__builtin_popcountll(bmask & lt) << ENTRY_SHIFT) + (cincl - chunks);
-            ws.entries[mine >> ENTRY_SHIFT] = uint2{(uint32_t)id, (uint32_t)mine};
-        }
-    }
-    // small triangles: compacted in lane order, their boxes concatenated
-    const unsigned long long smask = __ballot(small);
-    if (!smask) return;   // wave-uniform
-    const uint32_t srank = (uint32_t)__builtin_popcountll(smask & lt);
-    const uint32_t ns = small ? (uint32_t)n : 0u;
-    const uint32_t pincl = wave_incl_sum(ns, lane);
-    const uint32_t total = (uint32_t)__shfl((int)pincl, 63, 64);
-    if (small) {
-        SmallTri& e = st[w][srank];
-        e.r[0] = t.r0.x; e.r[1] = t.r0.y; e.r[2] = t.r0.z;
-        e.r[3] = t.r1.x; e.r[4] = t.r1.y; e.r[5] = t.r1.z;
-        e.r[6] = t.r2.x; e.r[7] = t.r2.y; e.r[8] = t.r2.z;
-        e.z[0] = t.z0; e.z[1] = t.z1; e.z[2] = t.z2;
-        e.w[0] = t.w0; e.w[1] = t.w1; e.w[2] = t.w2;
-        e.bias = t.bias;
-        e.id = id;
-        e.px0 = t.px0;
-        e.py0 = t.py0;
-        e.bw = bw;
-        e.magic = (65536u + (uint32_t)bw - 1u) / (uint32_t)bw;
-        e.start = pincl - ns;
-    }
-    int carry = 0;
-#pragma unroll 1
-    for (uint32_t base = 0; base < total; base += 64) {
-        mk[w][lane] = -1;
-        __builtin_amdgcn_wave_barrier();
-        if (small && pincl - ns >= base && pincl - ns < base + 64) mk[w][pincl - ns - base] = (int)srank;
-        __builtin_amdgcn_wave_barrier();
-        const int o = max(wave_incl_max(mk[w][lane], lane), carry);
-        carry = __shfl(o, 63, 64);
-        const uint32_t k = base + (uint32_t)lane;
-        if (k < total) {
-            const SmallTri& e = st[w][o];
-            TriSetup s;
-            s.r0 = f3{e.r[0], e.r[1], e.r[2]};
-            s.r1 = f3{e.r[3], e.r[4], e.r[5]};
-            s.r2 = f3{e.r[6], e.r[7], e.r[8]};
-            s.z0 = e.z[0]; s.z1 = e.z[1]; s.z2 = e.z[2];
-            s.w0 = e.w[0]; s.w1 = e.w[1]; s.w2 = e.w[2];
-            s.bias = e.bias;
-            const uint32_t q = k - e.start, yo = (q * e.magic) >> 16, xo = q - yo * (uint32_t)e.bw;
-            shade(s, e.id, e.px0 + (int)xo, e.py0 + (int)yo, p, target, pitch);
-        }
-        __builtin_amdgcn_wave_barrier();
-    }
 }
 
 // Upper bound of the edge function over the pixel centres of [x0, x1] x [y0, y1] (a corner), minus a
@@ -888,11 +783,7 @@ int launch_raster(const soc_mesh* mesh, const RasterParams& p, void* target, siz
     Workspace ws = carve(workspace, mesh->vertex_count, mesh->triangle_count);
     launch("raster_setup", kWorkgroup, raster_setup, ceil_div(max(mesh->vertex_count, 1), 256), kWorkgroup, 0, s, mesh->positions, ws, p);
     if (mesh->triangle_count > 0) {
-        if (tuning_knob("SOC_RASTER_SMALL_LB", 1))
-            launch("raster_small_lb", kWorkgroup, raster_small_lb, ceil_div(mesh->triangle_count, kWorkgroup), kWorkgroup, 0, s,
-                   mesh->indices, ws, p, target, pitch);
-        else
-            launch("raster_small", kWorkgroup, raster_small, ceil_div(mesh->triangle_count, 256), kWorkgroup, 0, s, mesh->indices, ws, p, target, pitch);
+        launch("raster_small", kWorkgroup, raster_small, ceil_div(mesh->triangle_count, 256), kWorkgroup, 0, s, mesh->indices, ws, p, target, pitch);
         launch("raster_big", kWorkgroup, raster_big, 2048, kWorkgroup, 0, s, mesh->indices, ws, p, target, pitch);
     }
     return check_launch(pass);

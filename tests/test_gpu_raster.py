@@ -80,32 +80,6 @@ def test_visibility_triangle_soup_bit_exact(soc, oracle, n, big):
     assert (raster.visibility_triangles(ref) >= 0).mean() > 0.05
 
 
-@pytest.mark.parametrize("W,H", [(3840, 2160), (333, 187)])
-def test_raster_small_paths_bit_identical(soc, monkeypatch, W, H):
-    """The load-balanced small-triangle kernel (default) and the lane-per-triangle one (SOC_RASTER_SMALL_LB=0) give the
-    same visibility buffer and shadow map on the Sponza-proxy mesh (260k triangles, most of them small at 333 x 187)."""
-    import bench
-    g = bench.make_globals(W, H, bench.multi_gpu.camera_for_rank(0))
-    sc = raster.scene_setup(g, scene.SPONZA_MESH, tex_size=64, device=DEV)
-    vp = np.ctypeslib.as_array(g.camera_projection_view_matrix)
-    svp = np.ctypeslib.as_array(g.sun_info.projection_view_matrix)
-    outs = []
-    for lb in ("1", "0"):
-        monkeypatch.setenv("SOC_RASTER_SMALL_LB", lb)
-        soc.reload_tuning()
-        vis = torch.zeros((H, W), dtype=torch.int64, device=DEV)
-        raster.raster_visibility(sc["mesh"], vp, raster.CULL_FRONT, vis, sc["workspace"])
-        sh = torch.ones((2048, 2048), dtype=torch.float32, device=DEV)
-        raster.raster_depth(sc["mesh"], svp, raster.CULL_BACK, sh, sc["workspace"], raster.SHADOW_BIAS_CONSTANT,
-                            raster.SHADOW_BIAS_SLOPE)
-        outs.append((vis, sh))
-    monkeypatch.delenv("SOC_RASTER_SMALL_LB")
-    soc.reload_tuning()
-    assert torch.equal(outs[0][0], outs[1][0])
-    assert torch.equal(outs[0][1], outs[1][1])
-    assert (raster.visibility_triangles(host(outs[0][0])) >= 0).mean() > 0.3
-
-
 def test_visibility_accumulates_without_clear(soc, oracle):
     """clear = 0 keeps the previous contents: two draws equal one draw of the concatenated mesh when the
     second mesh's triangle ids continue the first's (here: the same mesh twice -> identical buffer)."""
