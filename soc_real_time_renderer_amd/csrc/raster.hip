@@ -417,13 +417,64 @@ __device__ __forceinline__ Axis axis_repeat_level(float u, int n) {
 
 // Bilinear REPEAT sample of one level (its image view already resolved) of a packed mip chain, from the
 // level's two axes (computed once when two textures of the same extent share them).
+#ifndef SOC_GB_FAST_FILTER
+#define SOC_GB_FAST_FILTER 1
+#endif
+#if SOC_GB_FAST_FILTER
+typedef unsigned short gb_u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t gb_udot2(uint32_t a, uint32_t b) {
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(gb_u16x2, a), __builtin_bit_cast(gb_u16x2, b), 0u, false);
+}
+// Bilinear of the RGBA8 texels a b (top row) / c d with the contract's 8-bit weights (w = k / 256, exact).
+// UNORM: the exact integer bilinear per channel (v_dot2_u32_u16: a_k (256 - kx) + b_k kx per row, then across the rows;
+// at most 255 * 65536 < 2^24, exact in fp32), one conversion and one scale per channel. sRGB: the LUT-decoded channels,
+// each lerp fma(w, q - p, p). Against the oracle's unorm8-then-lerp chain this changes fp32 roundings only (the
+// G-buffer's RGBA16F tolerance; the GPU LUT already differs from the oracle's powf by an ulp).
+__device__ __forceinline__ f4 bilerp_rgba8(uint32_t ua, uint32_t ub, uint32_t uc, uint32_t ud, float wx, float wy, bool srgb,
+                                           const float* lut) {
+    if (!srgb) {
+        const uint32_t kx = (uint32_t)(wx * 256.0f), ky = (uint32_t)(wy * 256.0f);
+        const uint32_t wxp = (256u - kx) | (kx << 16), wyp = (256u - ky) | (ky << 16);
+        constexpr float kScale = 1.0f / (255.0f * 65536.0f);
+        auto ch = [&](uint32_t k) {   // channel k: bytes k of (a, b) and of (c, d) as 16-bit pairs
+            const uint32_t sel = k | 0x0c00u | ((4u + k) << 16) | 0x0c000000u;
+            const uint32_t top = gb_udot2(__builtin_amdgcn_perm(ub, ua, sel), wxp);
+            const uint32_t bot = gb_udot2(__builtin_amdgcn_perm(ud, uc, sel), wxp);
+            return (float)gb_udot2(top | (bot << 16), wyp) * kScale;
+        };
+        return f4{ch(0), ch(1), ch(2), ch(3)};
+    }
+    auto ch = [&](float a, float b, float c, float d) {
+        const float top = __builtin_fmaf(wx, b - a, a), bot = __builtin_fmaf(wx, d - c, c);
+        return __builtin_fmaf(wy, bot - top, top);
+    };
+    return f4{ch(lut[ua & 255u], lut[ub & 255u], lut[uc & 255u], lut[ud & 255u]),
+              ch(lut[(ua >> 8) & 255u], lut[(ub >> 8) & 255u], lut[(uc >> 8) & 255u], lut[(ud >> 8) & 255u]),
+              ch(lut[(ua >> 16) & 255u], lut[(ub >> 16) & 255u], lut[(uc >> 16) & 255u], lut[(ud >> 16) & 255u]),
+              ch(unorm8(ua >> 24), unorm8(ub >> 24), unorm8(uc >> 24), unorm8(ud >> 24))};
+}
+// trilinear blend of two levels' samples: fma(f, s1 - s0, s0) per channel
+__device__ __forceinline__ f4 lerp_levels(f4 s0, f4 s1, float f) {
+    return f4{__builtin_fmaf(f, s1.x - s0.x, s0.x), __builtin_fmaf(f, s1.y - s0.y, s0.y), __builtin_fmaf(f, s1.z - s0.z, s0.z),
+              __builtin_fmaf(f, s1.w - s0.w, s0.w)};
+}
+#else
+__device__ __forceinline__ f4 lerp_levels(f4 s0, f4 s1, float f) {
+    return f4{lerp_w(s0.x, s1.x, f), lerp_w(s0.y, s1.y, f), lerp_w(s0.z, s1.z, f), lerp_w(s0.w, s1.w, f)};
+}
+#endif
+
 __device__ __forceinline__ f4 sample_level_ax(const DImg& im, const Axis& ax, const Axis& ay, bool srgb, const float* lut) {
     uint32_t ua, ub, uc, ud;
     texel_row_pair(im, ax.i0, ax.i1, ay.i0, ua, ub);
     texel_row_pair(im, ax.i0, ax.i1, ay.i1, uc, ud);
+#if SOC_GB_FAST_FILTER
+    return bilerp_rgba8(ua, ub, uc, ud, ax.w, ay.w, srgb, lut);
+#else
     const f4 a = decode_rgba8(ua, srgb, lut), b = decode_rgba8(ub, srgb, lut);
     const f4 c = decode_rgba8(uc, srgb, lut), d = decode_rgba8(ud, srgb, lut);
     return bilerp4(a, b, c, d, ax.w, ay.w);
+#endif
 }
 __device__ __forceinline__ f4 sample_texture(const soc_img& tex, float u, float v, const float* lut) {
     if (!tex.data) return f4{1.0f, 1.0f, 1.0f, 1.0f};
@@ -480,10 +531,7 @@ __device__ __forceinline__ f4 sample_texture_mip(const soc_img& tex, float u, fl
             sv = v + t * dv;
         }
         f4 s0 = sample_level(im0, su, sv, srgb, lut);
-        if (lq & 255) {
-            const f4 s1 = sample_level(im1, su, sv, srgb, lut);
-            s0 = f4{lerp_w(s0.x, s1.x, f), lerp_w(s0.y, s1.y, f), lerp_w(s0.z, s1.z, f), lerp_w(s0.w, s1.w, f)};
-        }
+        if (lq & 255) s0 = lerp_levels(s0, sample_level(im1, su, sv, srgb, lut), f);
         acc = f4{acc.x + s0.x, acc.y + s0.y, acc.z + s0.z, acc.w + s0.w};
     }
     if (n == 1) return acc;
@@ -521,9 +569,7 @@ __device__ __forceinline__ void sample_texture_mip2(const soc_img& ta, const soc
     const bool xmajor = px >= py;
     const float du = xmajor ? gr.dudx : gr.dudy, dv = xmajor ? gr.dvdx : gr.dvdy;
     f4 acca = f4{0.0f, 0.0f, 0.0f, 0.0f}, accb = acca;
-    auto tri = [&](f4 s0, const f4& s1) {
-        return f4{lerp_w(s0.x, s1.x, f), lerp_w(s0.y, s1.y, f), lerp_w(s0.z, s1.z, f), lerp_w(s0.w, s1.w, f)};
-    };
+    auto tri = [&](f4 s0, const f4& s1) { return lerp_levels(s0, s1, f); };
     for (int i = 1; i <= n; ++i) {
         float su = u, sv = v;
         if (n > 1) {

@@ -139,10 +139,24 @@ struct TmOut {
 
 // The history taps of pixel k of the pair (0: colour, 1: velocity): the texel pairs (i0, i0 + 1) of rows ay.i0 and
 // ay.i1, one 16-B load per row.
+// The velocity history needs only the RG words of its two texels (words 0 and 2 of the pair): a 12-byte load (the
+// pair's first 12 bytes, in bounds: the texel i0 + 1 exists) instead of 16 moves a quarter fewer bytes through the
+// texture data path, this kernel's bound (TD busy 0.86, profiles/r04_raster_frame_sq_counters.json).
+#ifndef SOC_TAA_PVEL12
+#define SOC_TAA_PVEL12 1
+#endif
+typedef uint32_t u3a4 __attribute__((ext_vector_type(3))) __attribute__((aligned(4)));
 struct HistLoad {
     const DImg& prev;
     const DImg& pvel;
     __device__ __forceinline__ void operator()(int, int which, const Axis& ax, const Axis& ay, u4a8& r0, u4a8& r1) const {
+        if (SOC_TAA_PVEL12 && which) {
+            const u3a4 a = *reinterpret_cast<const u3a4*>(row_ptr<uint2>(pvel, ay.i0) + ax.i0);
+            const u3a4 b = *reinterpret_cast<const u3a4*>(row_ptr<uint2>(pvel, ay.i1) + ax.i0);
+            r0 = u4a8{a.x, a.y, a.z, 0u};
+            r1 = u4a8{b.x, b.y, b.z, 0u};
+            return;
+        }
         const DImg& im = which ? pvel : prev;
         r0 = *reinterpret_cast<const u4a8*>(row_ptr<uint2>(im, ay.i0) + ax.i0);
         r1 = *reinterpret_cast<const u4a8*>(row_ptr<uint2>(im, ay.i1) + ax.i0);
