@@ -603,6 +603,22 @@ __device__ __forceinline__ f3 mat3_vec_exact(const Mat3& M, f3 v) {
     return f3{m[0] * v.x + m[3] * v.y + m[6] * v.z, m[1] * v.x + m[4] * v.y + m[7] * v.z, m[2] * v.x + m[5] * v.y + m[8] * v.z};
 }
 
+// Per-pixel normalize of the resolve (the interpolated normal and the TBN): v_rsq_f32 and three multiplies instead of the
+// correctly rounded sqrt and three IEEE divisions (~40 VALU each, five per normal-mapped pixel). A few fp32 ulps against
+// the oracle's normalize, stored as RGBA16F (the G-buffer tolerance); a zero vector still gives NaN. The per-vertex
+// normal (gbuffer_vertex_setup) stays exact. SOC_GB_FAST_NORMALIZE=0 builds the exact form (A/B).
+#ifndef SOC_GB_FAST_NORMALIZE
+#define SOC_GB_FAST_NORMALIZE 1
+#endif
+__device__ __forceinline__ f3 normalize_exact(f3 a);
+__device__ __forceinline__ f3 normalize_px(f3 a) {
+#if SOC_GB_FAST_NORMALIZE
+    const float k = __builtin_amdgcn_rsqf(__builtin_fmaf(a.z, a.z, __builtin_fmaf(a.y, a.y, a.x * a.x)));
+    return f3{a.x * k, a.y * k, a.z * k};
+#else
+    return normalize_exact(a);
+#endif
+}
 __device__ __forceinline__ f3 normalize_exact(f3 a) {
 #pragma clang fp contract(off)
     const float l = sqrtf(a.x * a.x + a.y * a.y + a.z * a.z);
@@ -733,10 +749,10 @@ __global__ __launch_bounds__(kWorkgroup) __attribute__((amdgpu_waves_per_eu(SOC_
     if ((m.flags & SOC_MATERIAL_NORMAL_MAP) && m.normal_map.data) {   // draw_terrain.inl:206-219
         const DImg nm{static_cast<char*>(m.normal_map.data), m.normal_map.width, m.normal_map.height, m.normal_map.pitch_bytes};
         const f4 t = sample_h4(nm, u, v);
-        n = normalize_exact(f3{t.x, t.y, t.z});
+        n = normalize_px(f3{t.x, t.y, t.z});
     } else {
         const float4 na = VA.n, nb = VB.n, nc = VC.n;
-        n = normalize_exact(f3{b0 * na.x + b1 * nb.x + b2 * nc.x, b0 * na.y + b1 * nb.y + b2 * nc.y,
+        n = normalize_px(f3{b0 * na.x + b1 * nb.x + b2 * nc.x, b0 * na.y + b1 * nb.y + b2 * nc.y,
                                b0 * na.z + b1 * nb.z + b2 * nc.z});
     }
     const bool tbn = (m.flags & SOC_MATERIAL_NORMAL_TEXTURE) && m.normal_image.data;
@@ -783,10 +799,10 @@ __global__ __launch_bounds__(kWorkgroup) __attribute__((amdgpu_waves_per_eu(SOC_
         const f4 t = pair ? t_pair : tex(m.normal_image);
         const f3 tn{t.x * 2.0f - 1.0f, t.y * 2.0f - 1.0f, t.z * 2.0f - 1.0f};
         const float st1t = gr.dvdx, st2t = gr.dvdy;
-        const f3 N = normalize_exact(n);
-        const f3 T = normalize_exact(f3{Q1.x * st2t - Q2.x * st1t, Q1.y * st2t - Q2.y * st1t, Q1.z * st2t - Q2.z * st1t});
-        const f3 B = normalize_exact(cross_exact(N, T));
-        n = normalize_exact(f3{T.x * tn.x + B.x * tn.y + N.x * tn.z, T.y * tn.x + B.y * tn.y + N.y * tn.z,
+        const f3 N = normalize_px(n);
+        const f3 T = normalize_px(f3{Q1.x * st2t - Q2.x * st1t, Q1.y * st2t - Q2.y * st1t, Q1.z * st2t - Q2.z * st1t});
+        const f3 B = normalize_px(cross_exact(N, T));
+        n = normalize_px(f3{T.x * tn.x + B.x * tn.y + N.x * tn.z, T.y * tn.x + B.y * tn.y + N.y * tn.z,
                                T.z * tn.x + B.z * tn.y + N.z * tn.z});
     }
     f3 em = f3{0.0f, 0.0f, 0.0f};
