@@ -263,3 +263,34 @@ def test_raster_matches_the_scene_generator(oracle, scene_id, camera, cull):
         n_tri = m["normals"][m["indices"][tri[both], 0]]
         n_ref = gb["normal"][both][:, :3].astype(np.float32)
         assert (np.abs(n_tri - n_ref).max(axis=1) < 1e-3).mean() >= 0.995
+
+
+def test_far_plane_rejection_is_exact(oracle):
+    """The GPU triangle setup skips a triangle whose three vertices all have w_c > 0 and z_c > w_c (1 + 2^-12)
+    (raster.hip tri_setup): it claims every covered pixel's computed z_ndc is then > 1, so depth clipping drops them
+    all. Checked here with the oracle's own coverage and depth arithmetic (the GPU's, operation for operation) on
+    triangles that pass the test by a hair or by a lot, under a projection whose w varies per vertex: none covers a
+    pixel. A control set just inside the far plane covers pixels, so the check is not vacuous."""
+    W, H = 160, 90
+    vp = np.zeros(16, np.float32)   # GLSL column-major: X = x, Y = y, Z = z, W = 0.5 z + 0.5
+    vp[0], vp[5], vp[10], vp[11], vp[15] = 1.0, 1.0, 1.0, 0.5, 0.5
+    rng = np.random.default_rng(12)
+    n = 3000
+    thr = (1 + 2.0 ** -12) / (1 - 2.0 ** -12)   # z > thr  <=>  z > w (1 + 2^-12) in exact arithmetic
+    z = np.where(rng.random((n, 3)) < 0.7, thr + rng.random((n, 3)) * 1e-5, thr + rng.random((n, 3)) * 2.0)
+    xy = rng.uniform(-1.5, 1.5, (n, 3, 2)) * (0.5 * z[..., None] + 0.5)   # x_ndc, y_ndc within +-1.5
+    pos = np.concatenate([xy, z[..., None]], -1).astype(np.float32).reshape(-1, 3)
+    f = np.float32
+    zc = pos[:, 2] * f(1.0)                                    # the oracle's / GPU's mat_vec rows, summed in order
+    wc = (f(0.0) * pos[:, 0] + f(0.0) * pos[:, 1]) + pos[:, 2] * f(0.5) + f(0.5)
+    far = (wc > 0) & (zc > wc * f(1.0 + 2.0 ** -12))
+    keep = far.reshape(n, 3).all(1)
+    assert keep.mean() > 0.9
+    idx = np.arange(3 * n, dtype=np.uint32).reshape(n, 3)[keep]
+    tri, _ = vis_of(oracle, mesh_np(pos, idx), W, H, raster.CULL_NONE, vp)
+    assert (tri < 0).all(), int((tri >= 0).sum())
+    # control: the same triangles just inside the far plane (z_ndc < 1) do cover pixels
+    pos_in = pos.copy()
+    pos_in[:, 2] = np.float32(0.999)
+    tri_in, _ = vis_of(oracle, mesh_np(pos_in, idx), W, H, raster.CULL_NONE, vp)
+    assert (tri_in >= 0).mean() > 0.3
