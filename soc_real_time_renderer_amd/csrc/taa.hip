@@ -377,18 +377,8 @@ __global__ __launch_bounds__(64 * kTaaRows) void taa_lds(DImg target, DImg cur, 
     for (int i = tid; i < kTaaTR * kTaaTP; i += NT) {
         const int r = i / kTaaTP, c = i - r * kTaaTP;
         const int sy = min(max(y0 - 1 + r, 0), H - 1), sp = min(max(p0 - 1 + c, 0), npairs - 1);
-#if SOC_TAA_NT_STAGE   // A/B builds: the staged rows as non-temporal loads
-        {
-            typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-            const v4u a = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(row_ptr<uint4>(cur, sy) + sp));
-            const v4u b = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(row_ptr<uint4>(vel, sy) + sp));
-            ct[r][c] = uint4{a.x, a.y, a.z, a.w};
-            vt[r][c] = uint4{b.x, b.y, b.z, b.w};
-        }
-#else
         ct[r][c] = row_ptr<uint4>(cur, sy)[sp];
         vt[r][c] = row_ptr<uint4>(vel, sy)[sp];
-#endif
     }
     for (int i = tid; i < kTaaTR * kTaaTQ; i += NT) {
         const int r = i / kTaaTQ, c = i - r * kTaaTQ;
@@ -439,103 +429,6 @@ __global__ __launch_bounds__(64 * kTaaRows) void taa_lds(DImg target, DImg cur, 
                           return vtw[(tr * kTaaTP + c) * 4 + 2 * (bx & 1)];
                       },
                       [&]() { return vt[ty + 1][pl + 1]; }, HistLoad{prev, pvel});
-}
-
-// Persistent taa_lds (SOC_TAA_PERSIST): each workgroup walks the tiles of its XCD's horizontal band (contiguous tile
-// rows: the halo rows stay in that XCD's L2) and stages the NEXT tile's colour / velocity pairs and depth quads into a
-// second LDS buffer with LDS-DMA (global_load_lds_dwordx4: no registers) while it resolves the current one, so the
-// staging latency hides behind the history gathers and the arithmetic. Two buffers of 15.9 KiB: 5 workgroups per CU,
-// as taa_lds. The per-pixel code is taa_lds's (the same values from LDS): the same bits. Needs W % 4 == 0 (whole depth
-// quads) and 16-B aligned rows.
-template <bool TM>
-#ifndef SOC_TAA_PERSIST_WAVES
-#define SOC_TAA_PERSIST_WAVES 5   // 96 VGPRs (24 B of scratch); 1 = unconstrained: 116 VGPRs, 4 waves/SIMD (A/B builds)
-#endif
-__global__ __launch_bounds__(kTaaLdsLanes) __attribute__((amdgpu_waves_per_eu(SOC_TAA_PERSIST_WAVES))) void taa_ldsp(DImg target, DImg cur, DImg prev, DImg vel, DImg pvel, DImg depth,
-                                                        DImg vel_out, TaaParams p, TmOut tm, int tiles_x, int ntiles) {
-    constexpr int kRows = kTaaLdsRows, kTR = kRows + 2, NT = kTaaLdsLanes;
-    __shared__ uint4 ctb[2][kTR * kTaaTP];
-    __shared__ uint4 vtb[2][kTR * kTaaTP];
-    __shared__ float4 dtb[2][kTR * kTaaTQ];
-    typedef __attribute__((address_space(3))) void* lds_ptr;
-    const int W = target.w, H = target.h;
-    const int lane = threadIdx.x, ty = threadIdx.y, tid = lane + ty * 64;
-    const int npairs = W >> 1, nquads = W >> 2;
-    const int xcd = (int)blockIdx.x & 7, slot = (int)blockIdx.x >> 3, nslot = (int)gridDim.x >> 3;
-    const int band0 = (int)((long long)ntiles * xcd / 8), band1 = (int)((long long)ntiles * (xcd + 1) / 8);
-    auto stage = [&](int t, int b) {   // LDS-DMA: lane l of a wave-instruction lands at the wave's base + 16 l
-        const int tbx = t % tiles_x, tby = t / tiles_x;
-        const int p0 = tbx * kTaaPairs, y0 = tby * kRows, q0 = tbx * (kTaaPairs / 2);
-        for (int i = tid; i < kTR * kTaaTP; i += NT) {
-            const int r = i / kTaaTP, c = i - r * kTaaTP;
-            const int sy = min(max(y0 - 1 + r, 0), H - 1), sp = min(max(p0 - 1 + c, 0), npairs - 1);
-            __builtin_amdgcn_global_load_lds((const void*)(row_ptr<uint4>(cur, sy) + sp), (lds_ptr)(&ctb[b][i - lane]), 16, 0, 0);
-            __builtin_amdgcn_global_load_lds((const void*)(row_ptr<uint4>(vel, sy) + sp), (lds_ptr)(&vtb[b][i - lane]), 16, 0, 0);
-        }
-        for (int i = tid; i < kTR * kTaaTQ; i += NT) {
-            const int r = i / kTaaTQ, c = i - r * kTaaTQ;
-            const int sy = min(max(y0 - 1 + r, 0), H - 1), sq = min(max(q0 - 1 + c, 0), nquads - 1);
-            __builtin_amdgcn_global_load_lds((const void*)(row_ptr<float>(depth, sy) + 4 * sq), (lds_ptr)(&dtb[b][i - lane]), 16,
-                                             0, 0);
-        }
-    };
-    int t = band0 + slot;
-    if (t >= band1) return;   // workgroup-uniform
-    stage(t, 0);
-    const float exposure = TM ? tm.ae->exposure : 0.0f;
-#pragma unroll 1
-    for (int b = 0;; b ^= 1) {
-        const int tn = t + nslot;
-        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this wave's DMA into buffer b has landed
-        __syncthreads();                     // every wave's has, and buffer b ^ 1 is free (its tile is resolved)
-        if (tn < band1) stage(tn, b ^ 1);
-        const int tbx = t % tiles_x, tby = t / tiles_x;
-        const int p0 = tbx * kTaaPairs, y0 = tby * kRows, q0 = tbx * (kTaaPairs / 2);
-        const int x0 = 2 * (p0 + lane), y = y0 + ty;
-        if (x0 < W && y < H) {
-            const uint4(*ct)[kTaaTP] = reinterpret_cast<const uint4(*)[kTaaTP]>(ctb[b]);
-            const uint4(*vt)[kTaaTP] = reinterpret_cast<const uint4(*)[kTaaTP]>(vtb[b]);
-            const int xl = max(x0 - 1, 0), xr = min(x0 + 2, W - 1);
-            const float* dtf = reinterpret_cast<const float*>(dtb[b]);
-            const int dbase = 4 * (q0 - 1);
-            h2 Cxy[3][4], Czw[3][4];
-            float D[3][4];
-            int rows[3];
-#pragma unroll
-            for (int r = 0; r < 3; ++r) {
-                const int tr = ty + 2 - r;
-                rows[r] = min(max(y + 1 - r, 0), H - 1);
-                const uint4 mid = ct[tr][lane + 1];
-                uint2 L = uint2{ct[tr][lane].z, ct[tr][lane].w}, R = uint2{ct[tr][lane + 2].x, ct[tr][lane + 2].y};
-                const float* drow = dtf + tr * 4 * kTaaTQ - dbase;
-                const float2 dmid = *reinterpret_cast<const float2*>(drow + x0);
-                float dl = drow[x0 - 1], dr = drow[x0 + 2];
-                if (x0 == 0) { L = uint2{mid.x, mid.y}; dl = dmid.x; }
-                if (x0 + 2 >= W) { R = uint2{mid.z, mid.w}; dr = dmid.y; }
-                Cxy[r][0] = as_h2(L.x);
-                Czw[r][0] = as_h2(L.y);
-                Cxy[r][1] = as_h2(mid.x);
-                Czw[r][1] = as_h2(mid.y);
-                Cxy[r][2] = as_h2(mid.z);
-                Czw[r][2] = as_h2(mid.w);
-                Cxy[r][3] = as_h2(R.x);
-                Czw[r][3] = as_h2(R.y);
-                D[r][0] = dl;
-                D[r][1] = dmid.x;
-                D[r][2] = dmid.y;
-                D[r][3] = dr;
-            }
-            const uint32_t* vtw = reinterpret_cast<const uint32_t*>(vt);
-            taa_pair_tail<TM>(target, prev, pvel, vel_out, p, tm, x0, y, xl, xr, rows, Cxy, Czw, D, exposure,
-                              [&](int bx, int by) {
-                                  const int tr = by - (y0 - 1), c = (bx >> 1) - (p0 - 1);
-                                  return vtw[(tr * kTaaTP + c) * 4 + 2 * (bx & 1)];
-                              },
-                              [&]() { return vt[ty + 1][lane + 1]; }, HistLoad{prev, pvel});
-        }
-        if (tn >= band1) break;
-        t = tn;
-    }
 }
 
 __global__ __launch_bounds__(kWorkgroup) void taa_generic(DImg target, DImg cur, DImg prev, DImg vel, DImg pvel, DImg depth,
@@ -636,29 +529,7 @@ int taa_launch(const soc_globals* g, soc_img target, soc_img current_color, soc_
         // shifts + edge-lane loads, 0 = every lane loads its side columns (the same bits, tests/test_gpu_parity.py)
         const int nbr = tuning_knob("SOC_TAA_NBR", 3);
         const dim3 blk_h(64, 4), g2_h(ceil_div(W / 2, 62), ceil_div(H, 4));
-        static int persist_grid[64] = {};   // resident workgroups of taa_ldsp per device, a multiple of 8 (XCD bands)
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        if (nbr == 3 && a16(depth) && W % 4 == 0 && tuning_knob("SOC_TAA_PERSIST", 0) && dev >= 0 && dev < 64) {
-            if (!persist_grid[dev]) {
-                int per_cu = 0, cus = 256;
-                hipDeviceProp_t prop;
-                if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0) cus = prop.multiProcessorCount;
-                if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, taa_ldsp<true>, kTaaLdsLanes, 0) != hipSuccess ||
-                    per_cu < 1)
-                    per_cu = 4;
-                persist_grid[dev] = max(8, (per_cu * cus) / 8 * 8);
-            }
-            const int tiles_x = ceil_div(W / 2, kTaaPairs), ntiles = tiles_x * ceil_div(H, kTaaLdsRows);
-            if (tm)
-                launch("taa_ldsp", kTaaLdsLanes, taa_ldsp<true>, persist_grid[dev], blk_h, 0, hs(stream), dimg(target),
-                       dimg(current_color), dimg(previous_color), dimg(current_velocity), dimg(previous_velocity), dimg(depth), vo,
-                       p, *tm, tiles_x, ntiles);
-            else
-                launch("taa_ldsp", kTaaLdsLanes, taa_ldsp<false>, persist_grid[dev], blk_h, 0, hs(stream), dimg(target),
-                       dimg(current_color), dimg(previous_color), dimg(current_velocity), dimg(previous_velocity), dimg(depth), vo,
-                       p, TmOut{}, tiles_x, ntiles);
-        } else if (nbr == 3 && a16(depth)) {
+        if (nbr == 3 && a16(depth)) {
             const dim3 gl(ceil_div(W / 2, kTaaPairs), ceil_div(H, 4));
             if (tm)
                 launch("taa_lds", kTaaLdsLanes, taa_lds<true>, gl, blk_h, 0, hs(stream), dimg(target), dimg(current_color), dimg(previous_color),

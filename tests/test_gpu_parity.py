@@ -408,7 +408,7 @@ def test_taa(soc, oracle, W, H, inputs):
                                        (1920, 1080, True)])
 def test_taa_lane_shift_neighbours_identical(soc, oracle, monkeypatch, W, H, noisy):
     """Every neighbourhood source gives the bits of the per-lane loads (SOC_TAA_NBR=0): the LDS-staged tiles (3,
-    default; persistent with LDS-DMA double buffering, SOC_TAA_PERSIST=1 where W % 4 == 0, and one tile per workgroup), the side columns from the adjacent lanes (DPP wave shifts) with halo-only first / last lanes (2) and with
+    default), the side columns from the adjacent lanes (DPP wave shifts) with halo-only first / last lanes (2) and with
     edge-lane loads (1). 100 px: 50
     pairs in one 64-pair LDS tile row (14 lanes past the image) / a 62-pair wave row (12 lanes past), 32-lane block rows
     of which the second has 18 lanes inside; 102 x 42: a partial last depth quad (W % 4 == 2) and a last tile row with
@@ -432,9 +432,8 @@ def test_taa_lane_shift_neighbours_identical(soc, oracle, monkeypatch, W, H, noi
         depth = dp[:, :W]
     ae = soc.auto_exposure_buffer(exposure=0.37)
     outs = []
-    for nbr, persist in (("3", "1"), ("3", "0"), ("2", "0"), ("1", "0"), ("0", "0")):
+    for nbr in ("3", "2", "1", "0"):
         monkeypatch.setenv("SOC_TAA_NBR", nbr)
-        monkeypatch.setenv("SOC_TAA_PERSIST", persist)
         soc.reload_tuning()
         t = torch.zeros(H, W, 4, dtype=torch.float16, device=DEV)
         o = torch.zeros(H, W, 4, dtype=torch.uint8, device=DEV)
