@@ -627,20 +627,29 @@ __device__ __forceinline__ void batch_slots(uint32_t mask, uint32_t lane, uint32
         if (lane == 0) offs[st][wave] = (uint32_t)__builtin_popcountll(b);
     }
     __syncthreads();
-    if (tid == 0) {
-        uint32_t acc = 0;
-        for (int st = 0; st < 24; ++st)
-            for (int w = 0; w < 4; ++w) {
-                const uint32_t c = offs[st][w];
-                offs[st][w] = acc;
-                acc += c;
-            }
-        offs[24][0] = acc;
+    // the exclusive scan of the 96 counts in (step, wave) order by wave 0: lane l < 48 takes counts 2l and 2l + 1, a wave
+    // prefix sum of the pairs (6 shuffle steps) instead of one lane's 96 dependent LDS round trips (the same sums)
+    if (tid < 64) {
+        uint32_t* flat = &offs[0][0];
+        const uint32_t c0 = lane < 48 ? flat[2 * lane] : 0u, c1 = lane < 48 ? flat[2 * lane + 1] : 0u;
+        uint32_t incl = c0 + c1;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = (uint32_t)__shfl_up((int)incl, d, 64);
+            if ((int)lane >= d) incl += o;
+        }
+        const uint32_t excl = incl - (c0 + c1);
+        if (lane < 48) {
+            flat[2 * lane] = excl;
+            flat[2 * lane + 1] = excl + c0;
+        }
+        if (lane == 47) offs[24][0] = incl;
     }
     __syncthreads();
 }
 
 template <bool NOISE_R8>
+// 6 waves/SIMD: 80 VGPRs with 20 B of scratch, measured faster than 5 waves without a spill (profiles/r04_probe_clouds_scan.txt)
 __global__ __launch_bounds__(kWorkgroup) __attribute__((amdgpu_waves_per_eu(6))) void clouds_density(
     DImg noise, CloudParams p, const uint32_t* __restrict__ counter, const uint32_t* __restrict__ list, PairBufs pb) {
     __shared__ uint32_t quads[kTable];
