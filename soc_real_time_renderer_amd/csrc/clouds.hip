@@ -369,20 +369,31 @@ __device__ __forceinline__ f2v secondary_od_lut(const OdLut& L, float iLen, floa
     return f2v{__builtin_amdgcn_exp2f(l.x), __builtin_amdgcn_exp2f(l.y)};
 }
 
-__device__ f3 atmosphere(f3 r, f3 r0, f3 pSun, float iTime, const OdLut& L) {
-    const float iSun = 22.0f, kMie = 21e-6f, g0 = 0.758f;
-    const f3 kRlh = f3{5.5e-6f, 13.0e-6f, 22.4e-6f};
-    const float PI = 3.141592f;
-    r = normalize3(r);
-    float2 p = rsi(r0, r, kRAtmos);
-    if (p.x > p.y) return f3{0.0f, 0.0f, 0.0f};
-    p.y = fminf(p.y, rsi(r0, r, kRPlanet).x);
-    const float iStep = (p.y - p.x) / 16.0f;
-    f3 totalRlh = f3{0, 0, 0}, totalMie = f3{0, 0, 0};
-    f2v iOd = {0.0f, 0.0f};   // (Rayleigh, Mie) optical depth of the primary ray, one packed pair
+constexpr float kAtmSun = 22.0f, kAtmMie = 21e-6f, kAtmG = 0.758f;
+__device__ __forceinline__ f3 atm_krlh() { return f3{5.5e-6f, 13.0e-6f, 22.4e-6f}; }
+
+// The phase-weighted sum of the atmosphere's in-scattering integrals (:435-438) for the normalised view ray r.
+__device__ __forceinline__ f3 atmosphere_phase(f3 r, f3 pSun, f3 totalRlh, f3 totalMie) {
+    const float PI = 3.141592f, g0 = kAtmG;
     const float mu = dot3(r, pSun), mumu = mu * mu, gg = g0 * g0;
     const float pRlh = 3.0f / (16.0f * PI) * (1.0f + mumu);
     const float pMie = 3.0f / (8.0f * PI) * ((1.0f - gg) * (mumu + 1.0f)) / (powf(1.0f + gg - 2.0f * mu * g0, 1.5f) * (2.0f + gg));
+    return ((atm_krlh() * pRlh) * totalRlh + totalMie * (pMie * kAtmMie)) * kAtmSun;
+}
+
+// The in-scattering integrals totalRlh / totalMie of the normalised view ray r (:375-433); false when the ray misses the
+// atmosphere (the colour is then 0).
+__device__ __forceinline__ bool atmosphere_integrals(f3 r, f3 r0, f3 pSun, float iTime, const OdLut& L, f3& totalRlh,
+                                                     f3& totalMie) {
+    const float kMie = kAtmMie;
+    const f3 kRlh = atm_krlh();
+    float2 p = rsi(r0, r, kRAtmos);
+    if (p.x > p.y) return false;
+    p.y = fminf(p.y, rsi(r0, r, kRPlanet).x);
+    const float iStep = (p.y - p.x) / 16.0f;
+    totalRlh = f3{0, 0, 0};
+    totalMie = f3{0, 0, 0};
+    f2v iOd = {0.0f, 0.0f};   // (Rayleigh, Mie) optical depth of the primary ray, one packed pair
     const float C2 = dot3(pSun, pSun), cR = -kRPlanet * kExpR, cM = -kRPlanet * kExpM;
     for (int i = 0; i < 16; i++) {
         const f3 iPos = r0 + r * (iTime + iStep * 0.5f);
@@ -410,7 +421,79 @@ __device__ f3 atmosphere(f3 r, f3 r0, f3 pSun, float iTime, const OdLut& L) {
         totalMie = totalMie + attn * odM;
         iTime += iStep;
     }
-    return ((kRlh * pRlh) * totalRlh + totalMie * (pMie * kMie)) * iSun;
+    return true;
+}
+
+__device__ f3 atmosphere(f3 r, f3 r0, f3 pSun, float iTime, const OdLut& L) {
+    r = normalize3(r);
+    f3 totalRlh, totalMie;
+    if (!atmosphere_integrals(r, r0, pSun, iTime, L, totalRlh, totalMie)) return f3{0.0f, 0.0f, 0.0f};
+    return atmosphere_phase(r, pSun, totalRlh, totalMie);
+}
+
+// Sky-view table (round 4). The camera position r0, the sun and iTime are fixed for the frame, so the integrals are a
+// function of the view direction alone, and by the mirror symmetry across the vertical plane through the sun, of the
+// direction's elevation sine e = r.up and its azimuth away from the sun's, as u = sin(az / 2). They change branch where
+// the ray grazes the planet (e = +-eh, eh = sqrt(1 - rPlanet^2 / |r0|^2)): below -eh the ray hits the ground ahead, within
+// (-eh, eh) it misses (the reference's rsi returns -1 and the primary step spans the chord behind the camera), above +eh
+// the line's ground hit lies behind (quirk Q10's min keeps it). One kSvT x kSvU table per branch, rows dense towards
+// the grazing direction (e = boundary +- t^2 span, with a margin dl inside the branch so that the entries' own fp32
+// branch test is unambiguous; the middle band linear in e); each pixel takes the branch from the same planet-intersection
+// discriminant rsi computes, interpolates (totalRlh, totalMie) bilinearly and applies its exact phase functions. Against
+// evaluating every pixel (float64 study over the C3 / C4 view frusta, tools/sky_table_check.py): at most 0.04 RGBA8
+// levels. SOC_CLOUDS_SKY_TABLE=0 evaluates every pixel (the single-lane kernel always does).
+constexpr int kSvT = 128, kSvU = 64, kSvEntries = 3 * kSvT * kSvU;
+struct SkyTab {
+    const float4* t;   // [3][kSvT][kSvU] x 2: (totalRlh.xyz, totalMie.x), (totalMie.yz, -, -); nullptr: no table
+    float upx, upy, upz, shx, shy, shz, btx, bty, btz;   // frame: up = r0 / |r0|, the sun's horizontal direction, up x sh
+    float eh, dl;
+};
+__device__ __forceinline__ f3 sv_dir(const SkyTab& st, int b, float t, float u) {
+    const float eh = st.eh, dl = st.dl;
+    const float e = b == 0 ? -(eh + dl) - t * t * (1.0f - eh - dl)
+                  : b == 1 ? -(eh - dl) + t * 2.0f * (eh - dl) : (eh + dl) + t * t * (1.0f - eh - dl);
+    const float c = 1.0f - 2.0f * u * u, sn = sqrtf(fmaxf(1.0f - c * c, 0.0f)), ce = sqrtf(fmaxf(1.0f - e * e, 0.0f));
+    return f3{st.upx * e + ce * (c * st.shx + sn * st.btx), st.upy * e + ce * (c * st.shy + sn * st.bty),
+              st.upz * e + ce * (c * st.shz + sn * st.btz)};
+}
+__global__ __launch_bounds__(kWorkgroup) void clouds_sky_table(float4* __restrict__ tab, CloudParams p, SkyTab st, OdLut L) {
+    const int i = (int)(blockIdx.x * kWorkgroup + threadIdx.x);
+    if (i >= kSvEntries) return;
+    const int b = i / (kSvT * kSvU), rem = i - b * (kSvT * kSvU), ti = rem / kSvU, uj = rem - ti * kSvU;
+    const f3 r = normalize3(sv_dir(st, b, (float)ti / (float)(kSvT - 1), (float)uj / (float)(kSvU - 1)));
+    const f3 r0 = f3{0.0f + p.cam[0], 6372e3f + p.cam[1], 0.0f + p.cam[2]};
+    f3 R = f3{0.0f, 0.0f, 0.0f}, M = R;
+    if (!atmosphere_integrals(r, r0, f3{p.sun[0], p.sun[1], p.sun[2]}, p.elapsed, L, R, M)) R = M = f3{0.0f, 0.0f, 0.0f};
+    tab[2 * i] = float4{R.x, R.y, R.z, M.x};
+    tab[2 * i + 1] = float4{M.y, M.z, 0.0f, 0.0f};
+}
+__device__ f3 atmosphere_table(f3 r, f3 r0, f3 pSun, const SkyTab& st) {
+    r = normalize3(r);
+    const float2 pa = rsi(r0, r, kRAtmos);
+    if (pa.x > pa.y) return f3{0.0f, 0.0f, 0.0f};
+    // the branch atmosphere_integrals takes: rsi(r0, r, rPlanet)'s discriminant and the sign of r0.r
+    const float PoD = dot3(r0, r), delta = PoD * PoD + kRPlanet * kRPlanet - dot3(r0, r0);
+    const int b = delta < 0.0f ? 1 : (PoD >= 0.0f ? 2 : 0);
+    const f3 up = f3{st.upx, st.upy, st.upz};
+    const float e = dot3(r, up), eh = st.eh, dl = st.dl;
+    float t = b == 0 ? sqrtf(fmaxf((-(eh + dl) - e) / (1.0f - eh - dl), 0.0f))
+            : b == 1 ? (e + (eh - dl)) / (2.0f * (eh - dl)) : sqrtf(fmaxf((e - (eh + dl)) / (1.0f - eh - dl), 0.0f));
+    t = fminf(fmaxf(t, 0.0f), 1.0f);
+    const f3 dh = f3{r.x - up.x * e, r.y - up.y * e, r.z - up.z * e};
+    const float nh = length3(dh);
+    const float c = nh > 0.0f ? fminf(fmaxf((dh.x * st.shx + dh.y * st.shy + dh.z * st.shz) / nh, -1.0f), 1.0f) : 1.0f;
+    const float u = sqrtf(fmaxf((1.0f - c) * 0.5f, 0.0f));
+    const float ft = t * (float)(kSvT - 1), fu = u * (float)(kSvU - 1);
+    const int i0 = min((int)ft, kSvT - 2), j0 = min((int)fu, kSvU - 2);
+    const float wt = ft - (float)i0, wu = fu - (float)j0;
+    const float4* row = st.t + 2 * ((b * kSvT + i0) * kSvU + j0);
+    auto lerp4 = [](float4 a, float4 c4, float w) {
+        return float4{a.x + w * (c4.x - a.x), a.y + w * (c4.y - a.y), a.z + w * (c4.z - a.z), a.w + w * (c4.w - a.w)};
+    };
+    const float4 a0 = lerp4(row[0], row[2], wu), a1 = lerp4(row[1], row[3], wu);
+    const float4 b0 = lerp4(row[2 * kSvU], row[2 * kSvU + 2], wu), b1 = lerp4(row[2 * kSvU + 1], row[2 * kSvU + 3], wu);
+    const float4 v0 = lerp4(a0, b0, wt), v1 = lerp4(a1, b1, wt);
+    return atmosphere_phase(r, pSun, f3{v0.x, v0.y, v0.z}, f3{v0.w, v1.x, v1.y});
 }
 
 constexpr int TX = 16, TY = 16;
@@ -563,13 +646,17 @@ __global__ __launch_bounds__(kWorkgroup) void clouds_classify(DImg depth, DImg t
 
 // Three-kernel path, stage 2: the atmosphere of every listed sky pixel (no LDS, few registers, so many
 // more lanes are resident than in the cloud march), kept in fp32 in the workspace.
+template <bool TAB>
 __global__ __launch_bounds__(kWorkgroup) __attribute__((amdgpu_waves_per_eu(8))) void clouds_atmosphere(CloudParams p, const uint32_t* __restrict__ counter,
                                                          const uint32_t* __restrict__ list, float4* __restrict__ atmos,
-                                                         OdLut lut) {
+                                                         OdLut lut, SkyTab st) {
     const uint32_t count = *counter;
+    const f3 r0 = f3{0.0f + p.cam[0], 6372e3f + p.cam[1], 0.0f + p.cam[2]}, sun = f3{p.sun[0], p.sun[1], p.sun[2]};
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < count; i += gridDim.x * 256u) {
         const uint32_t e = list[i];
-        const f3 c = sky_atmosphere(p, sky_dir(p, (int)(e & 0xffffu), (int)(e >> 16)), lut);
+        const f3 dir = sky_dir(p, (int)(e & 0xffffu), (int)(e >> 16));
+        const f3 c = TAB && SOC_CLOUDS_PROFILE != 2 && SOC_CLOUDS_PROFILE != 3 ? atmosphere_table(dir, r0, sun, st)
+                                                                             : sky_atmosphere(p, dir, lut);
         atmos[i] = float4{c.x, c.y, c.z, 0.0f};
     }
 }
@@ -877,6 +964,7 @@ struct CloudWs {
     float4* atmos;
     PairBufs pb;
     float2* od_lut;   // secondary-ray optical-depth table (kOdR x kOdM)
+    float4* sky_tab;  // sky-view table (kSvEntries x 2 float4)
     size_t bytes;
 };
 CloudWs cloud_ws_layout(void* base, size_t n) {
@@ -907,6 +995,8 @@ CloudWs cloud_ws_layout(void* base, size_t n) {
     off = al(off + (size_t)w.pb.od_blocks * 24 * 256 * 4);
     w.od_lut = reinterpret_cast<float2*>(b + off);
     off = al(off + (size_t)kOdR * kOdM * sizeof(float2));
+    w.sky_tab = reinterpret_cast<float4*>(b + off);
+    off = al(off + (size_t)kSvEntries * 2 * sizeof(float4));
     w.bytes = off;
     return w;
 }
@@ -967,7 +1057,7 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
     // balanced over all SIMDs instead of running as a second, partially filled round.
     static int res_atmos = 0, res_density = 0, res_sunvis = 0, res_resolve = 0;
     if (!res_atmos) {
-        res_atmos = resident_blocks(clouds_atmosphere);
+        res_atmos = resident_blocks(clouds_atmosphere<false>);
         res_density = resident_blocks(clouds_density<false>);
         res_sunvis = resident_blocks(clouds_sunvis<false, kSunvisLanes, true>, kSunvisLanes);
         res_resolve = resident_blocks(clouds_resolve<false>);
@@ -988,7 +1078,42 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
         lut = OdLut{ws.od_lut, C2};
         launch("clouds_od_lut", kWorkgroup, clouds_od_lut, ceil_div(kOdR * kOdM, kWorkgroup), kWorkgroup, 0, s, ws.od_lut, C2);
     }
-    auto atmos = [&]() { launch("clouds_atmosphere", kWorkgroup, clouds_atmosphere, grid(res_atmos, blocks), kWorkgroup, 0, s, p, counter, list, ws.atmos, lut); };
+    // the frame's sky-view table (needs the secondary-ray table; SOC_CLOUDS_SKY_TABLE=0: every pixel evaluated)
+    SkyTab st{};
+    st.t = nullptr;
+    if (lut.t && tuning_knob("SOC_CLOUDS_SKY_TABLE", 1)) {
+        const double r0x = (double)(0.0f + p.cam[0]), r0y = (double)(6372e3f + p.cam[1]), r0z = (double)(0.0f + p.cam[2]);
+        const double rl = std::sqrt(r0x * r0x + r0y * r0y + r0z * r0z);
+        const double ux = r0x / rl, uy = r0y / rl, uz = r0z / rl;
+        const double sx = p.sun[0], sy = p.sun[1], sz = p.sun[2], su = sx * ux + sy * uy + sz * uz;
+        double hx = sx - su * ux, hy = sy - su * uy, hz = sz - su * uz, hl = std::sqrt(hx * hx + hy * hy + hz * hz);
+        if (!(hl > 1e-9)) {   // sun at the zenith: any horizontal axis
+            hx = uy; hy = -ux; hz = 0.0;
+            hl = std::sqrt(hx * hx + hy * hy);
+            if (!(hl > 1e-9)) { hx = 1.0; hy = 0.0; hz = 0.0; hl = 1.0; }
+        }
+        hx /= hl; hy /= hl; hz /= hl;
+        const double bx = uy * hz - uz * hy, by = uz * hx - ux * hz, bz = ux * hy - uy * hx;
+        const double q = (double)kRPlanet / rl;
+        st.t = ws.sky_tab;
+        st.upx = (float)ux; st.upy = (float)uy; st.upz = (float)uz;
+        st.shx = (float)hx; st.shy = (float)hy; st.shz = (float)hz;
+        st.btx = (float)bx; st.bty = (float)by; st.btz = (float)bz;
+        st.eh = q < 1.0 ? (float)std::sqrt(1.0 - q * q) : 0.0f;
+        st.dl = 3e-5f;   // margin inside each branch: the fp32 discriminant is ambiguous within ~1e-5 of the grazing elevation
+        if (!(st.eh > 4.0f * st.dl)) st.t = nullptr;   // camera at or below the surface: no table
+        if (st.t)
+            launch("clouds_sky_table", kWorkgroup, clouds_sky_table, ceil_div(kSvEntries, kWorkgroup), kWorkgroup, 0, s, ws.sky_tab, p,
+                   st, lut);
+    }
+    auto atmos = [&]() {
+        if (st.t)
+            launch("clouds_atmosphere", kWorkgroup, clouds_atmosphere<true>, grid(res_atmos, blocks), kWorkgroup, 0, s, p, counter,
+                   list, ws.atmos, lut, st);
+        else
+            launch("clouds_atmosphere", kWorkgroup, clouds_atmosphere<false>, grid(res_atmos, blocks), kWorkgroup, 0, s, p, counter,
+                   list, ws.atmos, lut, st);
+    };
     if (apos == 0) atmos();
     const DImg nz = dimg(noise), tg = dimg(target);
     const int density_grid = std::min(grid(res_density, blocks), (int)ws.pb.od_blocks);   // one od scratch per workgroup

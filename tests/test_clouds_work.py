@@ -59,3 +59,13 @@ def test_od_table_accuracy():
     mx = float(line.split("max")[-1])
     up = float([ln for ln in p.stdout.splitlines() if "mu > 0.9" in ln][0].split("max")[-1])
     assert mx <= 1e-3 and up <= 5e-5, p.stdout
+
+
+def test_sky_table_accuracy():
+    """The sky-view table's interpolation error (tools/sky_table_check.py, float64, the C3 and C4 view frusta sampled
+    every 24 pixels): well under one RGBA8 level of the atmosphere colour (0.15 measured, at the grazing rows)."""
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "sky_table_check.py"), "--sub", "24"],
+                       capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-2000:]
+    worst = float(p.stdout.strip().splitlines()[-1].split()[2])
+    assert worst < 0.5, p.stdout
