@@ -859,10 +859,12 @@ __global__ __launch_bounds__(kSunvisThreads) __attribute__((amdgpu_waves_per_eu(
     }
 }
 
-template <bool NOISE_R8>
-__global__ __launch_bounds__(kWorkgroup) void clouds_resolve(DImg noise, DImg target, CloudParams p, const uint32_t* __restrict__ counter,
+// TAB: the atmosphere colour from the sky-view table here (no clouds_atmosphere launch, no per-pixel colour buffer);
+// else read from the atmosphere kernel's output.
+template <bool NOISE_R8, bool TAB = false>
+__global__ __launch_bounds__(kWorkgroup) __attribute__((amdgpu_waves_per_eu(5))) void clouds_resolve(DImg noise, DImg target, CloudParams p, const uint32_t* __restrict__ counter,
                                                       const uint32_t* __restrict__ list, const float4* __restrict__ atmos,
-                                                      PairBufs pb) {
+                                                      PairBufs pb, SkyTab st) {
     __shared__ uint32_t quads[kTable];
     __shared__ uint32_t offs[25][4];
     const uint32_t count = *counter;
@@ -889,9 +891,13 @@ __global__ __launch_bounds__(kWorkgroup) void clouds_resolve(DImg noise, DImg ta
         f3 color = f3{0.0f, 0.0f, 0.0f}, dir = f3{0.0f, 1.0f, 0.0f};
         if (valid) {
             e = list[i];
-            const float4 a = atmos[i];
-            color = f3{a.x, a.y, a.z};
             dir = sky_dir(p, (int)(e & 0xffffu), (int)(e >> 16));
+            if (TAB) {
+                color = atmosphere_table(dir, f3{0.0f + p.cam[0], 6372e3f + p.cam[1], 0.0f + p.cam[2]}, sun, st);
+            } else {
+                const float4 a = atmos[i];
+                color = f3{a.x, a.y, a.z};
+            }
         }
         const int x = (int)(e & 0xffffu), y = (int)(e >> 16);
         if (SOC_CLOUDS_PROFILE == 1) {
@@ -1060,7 +1066,7 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
         res_atmos = resident_blocks(clouds_atmosphere<false>);
         res_density = resident_blocks(clouds_density<false>);
         res_sunvis = resident_blocks(clouds_sunvis<false, kSunvisLanes, true>, kSunvisLanes);
-        res_resolve = resident_blocks(clouds_resolve<false>);
+        res_resolve = resident_blocks(clouds_resolve<false, true>);
     }
     const long long blocks = ((long long)W * H + 255) / 256;
     if (SOC_CLOUDS_PROFILE >= 4) return check_launch("cloud_rendering");
@@ -1106,7 +1112,10 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
             launch("clouds_sky_table", kWorkgroup, clouds_sky_table, ceil_div(kSvEntries, kWorkgroup), kWorkgroup, 0, s, ws.sky_tab, p,
                    st, lut);
     }
+    // with the table the resolve looks the atmosphere up itself (SOC_CLOUDS_ATMOS_FOLD=0: the atmosphere kernel from the table)
+    const bool fold = st.t && tuning_knob("SOC_CLOUDS_ATMOS_FOLD", 1);
     auto atmos = [&]() {
+        if (fold) return;
         if (st.t)
             launch("clouds_atmosphere", kWorkgroup, clouds_atmosphere<true>, grid(res_atmos, blocks), kWorkgroup, 0, s, p, counter,
                    list, ws.atmos, lut, st);
@@ -1114,21 +1123,27 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
             launch("clouds_atmosphere", kWorkgroup, clouds_atmosphere<false>, grid(res_atmos, blocks), kWorkgroup, 0, s, p, counter,
                    list, ws.atmos, lut, st);
     };
+    auto resolve = [&](auto k) {
+        launch("clouds_resolve", kWorkgroup, k, grid(res_resolve, blocks), kWorkgroup, 0, s, dimg(noise), dimg(target), p, counter,
+               list, ws.atmos, ws.pb, st);
+    };
     if (apos == 0) atmos();
-    const DImg nz = dimg(noise), tg = dimg(target);
+    const DImg nz = dimg(noise);
     const int density_grid = std::min(grid(res_density, blocks), (int)ws.pb.od_blocks);   // one od scratch per workgroup
     if (r8) {
         launch("clouds_density", kWorkgroup, clouds_density<true>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
         if (apos == 1) atmos();
         launch("clouds_sunvis", kSunvisLanes, clouds_sunvis<true, kSunvisLanes, true>, grid(res_sunvis, blocks), kSunvisLanes, 0, s, nz, p, list, ws.pb);
         if (apos == 2) atmos();
-        launch("clouds_resolve", kWorkgroup, clouds_resolve<true>, grid(res_resolve, blocks), kWorkgroup, 0, s, nz, tg, p, counter, list, ws.atmos, ws.pb);
+        if (fold) resolve(clouds_resolve<true, true>);
+        else resolve(clouds_resolve<true, false>);
     } else {
         launch("clouds_density", kWorkgroup, clouds_density<false>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
         if (apos == 1) atmos();
         launch("clouds_sunvis", kSunvisLanes, clouds_sunvis<false, kSunvisLanes, true>, grid(res_sunvis, blocks), kSunvisLanes, 0, s, nz, p, list, ws.pb);
         if (apos == 2) atmos();
-        launch("clouds_resolve", kWorkgroup, clouds_resolve<false>, grid(res_resolve, blocks), kWorkgroup, 0, s, nz, tg, p, counter, list, ws.atmos, ws.pb);
+        if (fold) resolve(clouds_resolve<false, true>);
+        else resolve(clouds_resolve<false, false>);
     }
     return check_launch("cloud_rendering");
 }
