@@ -587,61 +587,81 @@ __global__ __launch_bounds__(kWorkgroup) void clouds_kernel(DImg depth, DImg noi
 
 // Three-kernel path, stage 1 (classify). Every pixel first gets the constant non-sky colour (a sky pixel
 // is overwritten by the march later in stream order); sky pixels are appended to a compact list.
-// A workgroup covers a 64x16 tile, each wave a 32x8 quarter (every row of a wave one full 128-B line of
+// A workgroup covers 64x16 tiles, each wave a 32x8 quarter of one (every row of a wave one full 128-B line of
 // depth and of the target), each lane 4 horizontal pixels (one 16-B store). Entries are ordered
 // row-major inside a wave's quarter, so a wave of the march takes a compact 32x2 block. The list offset
 // costs ONE atomic per workgroup that has sky: device-scope atomics on one address serialise across
 // the XCDs (one per wave cost ~95 us at 4K).
+// kClassifyTiles 64x16 tiles stacked vertically per workgroup (a 64x64 region): one list atomic per region instead of per
+// tile. The atomics on the one counter serialise across the XCDs: at one per 64x16 tile they cost C4 34 of its 59 us
+// (profiles/r04_probe_clouds_classify.txt).
+constexpr int kClassifyTiles = 4;
 __global__ __launch_bounds__(kWorkgroup) void clouds_classify(DImg depth, DImg target, CloudParams p, int vec_store,
                                                        uint32_t* __restrict__ counter, uint32_t* __restrict__ list) {
-    __shared__ uint32_t wave_total[4];
+    __shared__ uint32_t wave_total[kClassifyTiles][4];
     __shared__ uint32_t wg_base;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int x0 = blockIdx.x * 64 + (wave & 1) * 32 + (lane & 7) * 4;
-    const int y = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
     const int W = min(p.res_x, target.w), H = min(p.res_y, target.h);
     const uint32_t other = pack_unorm8x4(f4{0.2f, 0.4f, 1.0f, 1.0f});
-    uint32_t mask = 0;   // bit k: pixel (x0 + k, y) is sky
-    if (y < H) {
-        // all 16 depth loads issued together (clamped coordinates, no per-pixel branch)
-        float d[4];
-        const float ray_v = div_rn((float)y, p.res_y_m1, p.r_res_y_m1);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) d[k] = sample_f32(depth, div_rn((float)min(x0 + k, W - 1), p.res_x_m1, p.r_res_x_m1), ray_v);
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (x0 + k < W && d[k] == 1.0f) mask |= 1u << k;
-        uint32_t* row = row_ptr_w<uint32_t>(target, y);
-        if (vec_store && x0 + 3 < W) {
-            *reinterpret_cast<uint4*>(row + x0) = uint4{other, other, other, other};
-        } else {
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (x0 + k < W) row[x0 + k] = other;
-        }
-    }
     const unsigned long long below = (1ull << lane) - 1ull;
-    uint32_t before = 0, total = 0;
+    uint32_t masks = 0;   // bits 4k..4k+3: pixels (x0 + 0..3, y_k) of tile k are sky
+    uint32_t before[kClassifyTiles];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const unsigned long long b = __ballot((mask >> k) & 1u);
-        before += (uint32_t)__builtin_popcountll(b & below);
-        total += (uint32_t)__builtin_popcountll(b);
+    for (int k = 0; k < kClassifyTiles; ++k) {
+        const int y = (blockIdx.y * kClassifyTiles + k) * 16 + (wave >> 1) * 8 + (lane >> 3);
+        uint32_t mask = 0;   // bit j: pixel (x0 + j, y) is sky
+        if (y < H) {
+            // all 16 depth loads issued together (clamped coordinates, no per-pixel branch)
+            float d[4];
+            const float ray_v = div_rn((float)y, p.res_y_m1, p.r_res_y_m1);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) d[j] = sample_f32(depth, div_rn((float)min(x0 + j, W - 1), p.res_x_m1, p.r_res_x_m1), ray_v);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (x0 + j < W && d[j] == 1.0f) mask |= 1u << j;
+            uint32_t* row = row_ptr_w<uint32_t>(target, y);
+            if (vec_store && x0 + 3 < W) {
+                *reinterpret_cast<uint4*>(row + x0) = uint4{other, other, other, other};
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (x0 + j < W) row[x0 + j] = other;
+            }
+        }
+        uint32_t b4 = 0, total = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const unsigned long long b = __ballot((mask >> j) & 1u);
+            b4 += (uint32_t)__builtin_popcountll(b & below);
+            total += (uint32_t)__builtin_popcountll(b);
+        }
+        before[k] = b4;
+        masks |= mask << (4 * k);
+        if (lane == 0) wave_total[k][wave] = total;
     }
-    if (lane == 0) wave_total[wave] = total;
     __syncthreads();
     if (threadIdx.x == 0) {
-        const uint32_t sum = wave_total[0] + wave_total[1] + wave_total[2] + wave_total[3];
-        if (SOC_CLOUDS_PROFILE == 5) wg_base = (blockIdx.y * gridDim.x + blockIdx.x) * 1024u;
+        uint32_t sum = 0;
+        for (int k = 0; k < kClassifyTiles; ++k) sum += wave_total[k][0] + wave_total[k][1] + wave_total[k][2] + wave_total[k][3];
+        if (SOC_CLOUDS_PROFILE == 5) wg_base = (blockIdx.y * gridDim.x + blockIdx.x) * (1024u * kClassifyTiles);
         else wg_base = sum ? atomicAdd(counter, sum) : 0u;
     }
     __syncthreads();
-    if (!mask) return;
-    uint32_t at = wg_base + before;
-    for (int w = 0; w < wave; ++w) at += wave_total[w];
+    if (!masks) return;
+    // entries in tile order, then wave order, then the wave's row-major order (as one tile per workgroup gave)
+    uint32_t tile_base = wg_base;
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-        if ((mask >> k) & 1u) list[at++] = ((uint32_t)y << 16) | (uint32_t)(x0 + k);
+    for (int k = 0; k < kClassifyTiles; ++k) {
+        const uint32_t mask = (masks >> (4 * k)) & 15u;
+        const int y = (blockIdx.y * kClassifyTiles + k) * 16 + (wave >> 1) * 8 + (lane >> 3);
+        uint32_t at = tile_base + before[k];
+        for (int w = 0; w < wave; ++w) at += wave_total[k][w];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if ((mask >> j) & 1u) list[at++] = ((uint32_t)y << 16) | (uint32_t)(x0 + j);
+        tile_base += wave_total[k][0] + wave_total[k][1] + wave_total[k][2] + wave_total[k][3];
+    }
 }
 
 // Three-kernel path, stage 2: the atmosphere of every listed sky pixel (no LDS, few registers, so many
@@ -708,10 +728,14 @@ __device__ __forceinline__ uint32_t pair_offset(const uint32_t (*offs)[4], uint3
 // (ballots per wave, then one lane scans the 24 x 4 counts).
 __device__ __forceinline__ void batch_slots(uint32_t mask, uint32_t lane, uint32_t wave, uint32_t (*offs)[4],
                                             uint32_t& /*unused*/, uint32_t tid) {
+    if (__ballot(mask != 0u) == 0ull) {   // no dense step in this wave (C4's below-horizon sky): 24 zero counts
+        if (lane < 24) offs[lane][wave] = 0u;
+    } else {
 #pragma unroll 1
-    for (uint32_t st = 0; st < 24; ++st) {
-        const unsigned long long b = __ballot((mask >> st) & 1u);
-        if (lane == 0) offs[st][wave] = (uint32_t)__builtin_popcountll(b);
+        for (uint32_t st = 0; st < 24; ++st) {
+            const unsigned long long b = __ballot((mask >> st) & 1u);
+            if (lane == 0) offs[st][wave] = (uint32_t)__builtin_popcountll(b);
+        }
     }
     __syncthreads();
     // the exclusive scan of the 96 counts in (step, wave) order by wave 0: lane l < 48 takes counts 2l and 2l + 1, a wave
@@ -799,7 +823,7 @@ __global__ __launch_bounds__(kWorkgroup) __attribute__((amdgpu_waves_per_eu(6)))
         for (uint32_t k = fail_from + tid; k < pb.cap && k < fail_from + offs[24][0]; k += 256u)
             pb.pairs[shard * pb.cap + k] = 0xffffffffu;
         if (i < count) pb.pix_mask[i] = mask | ((slot_base & kInline) ? kInline : 0u);
-        if (!(slot_base & kInline)) {   // workgroup-uniform
+        if (!(slot_base & kInline) && __ballot(mask != 0u) != 0ull) {   // workgroup-uniform, then wave-uniform
             // uniform loop: the ballot of every step sees every lane of the wave
             for (uint32_t st = 0; st < 24; ++st) {
                 const uint32_t rank = mask_ballot_rank(mask, st, lane);
@@ -887,6 +911,9 @@ __global__ __launch_bounds__(kWorkgroup) __attribute__((amdgpu_waves_per_eu(5)))
         } else {
             batch_slots(mask, lane, wave, offs, dummy, tid);   // the slot layout of clouds_density
         }
+        // a wave none of whose pixels has a dense step (C4: most of its sky lies below the horizon) has nothing to
+        // accumulate: it skips the 24-step ballot loop
+        const bool any_dense = __ballot(mask != 0u) != 0ull;
         uint32_t e = 0;
         f3 color = f3{0.0f, 0.0f, 0.0f}, dir = f3{0.0f, 1.0f, 0.0f};
         if (valid) {
@@ -922,7 +949,7 @@ __global__ __launch_bounds__(kWorkgroup) __attribute__((amdgpu_waves_per_eu(5)))
             f3 scattering = f3{0.0f, 0.0f, 0.0f};
             float transmittance = 1.0f;
             // steps in order; the ballot runs on every lane of the wave (uniform loop)
-            for (uint32_t st = 0; st < 24; ++st) {
+            for (uint32_t st = 0; any_dense && st < 24; ++st) {
                 const uint32_t rank = mask_ballot_rank(mask, st, lane);
                 if (march && ((mask >> st) & 1u)) {
                     const float2 ov = pb.odvis[base + offs[st][wave] + rank];
@@ -1058,7 +1085,8 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
     hipError_t e = hipMemsetAsync(counter, 0, 256, s);
     if (e != hipSuccess) return set_error(SOC_E_HIP, "%s: %s", P, hipGetErrorString(e));
     const int vec_store = (target.pitch_bytes % 16 == 0) && (reinterpret_cast<uintptr_t>(target.data) % 16 == 0);
-    launch("clouds_classify", kWorkgroup, clouds_classify, dim3(ceil_div(W, 64), ceil_div(H, 16)), kWorkgroup, 0, s, dimg(depth), dimg(target), p, vec_store, counter, list);
+    launch("clouds_classify", kWorkgroup, clouds_classify, dim3(ceil_div(W, 64), ceil_div(H, 16 * kClassifyTiles)), kWorkgroup, 0, s,
+           dimg(depth), dimg(target), p, vec_store, counter, list);
     // One resident wave set per kernel, grid-stride over the list / pairs: the long per-item work is
     // balanced over all SIMDs instead of running as a second, partially filled round.
     static int res_atmos = 0, res_density = 0, res_sunvis = 0, res_resolve = 0;
