@@ -342,8 +342,10 @@ struct OdLut {
     float C2;
 };
 
-__global__ __launch_bounds__(kWorkgroup) void clouds_od_lut(float2* __restrict__ lut, float C2) {
+// zero: the frame's 256-B counter block, cleared here (the lane's first kernel) instead of by a separate fill launch
+__global__ __launch_bounds__(kWorkgroup) void clouds_od_lut(float2* __restrict__ lut, float C2, uint32_t* __restrict__ zero) {
     const int i = (int)(blockIdx.x * kWorkgroup + threadIdx.x);
+    if (i < 64) zero[i] = 0u;
     if (i >= kOdR * kOdM) return;
     const int ir = i / kOdM, im = i - ir * kOdM;
     const float r = kRPlanet + (float)ir * (1.0f / kOdRScale), mu = -1.0f + (float)im * (1.0f / kOdMScale);
@@ -1082,8 +1084,17 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
     CloudWs ws = cloud_ws_layout(workspace, (size_t)target.width * (size_t)target.height);
     uint32_t* counter = ws.counter;
     uint32_t* list = ws.list;
-    hipError_t e = hipMemsetAsync(counter, 0, 256, s);
-    if (e != hipSuccess) return set_error(SOC_E_HIP, "%s: %s", P, hipGetErrorString(e));
+    // the frame's secondary-ray table (SOC_CLOUDS_OD_LUT=0: march every secondary ray, the single-lane kernel's bits);
+    // its kernel also clears the counter block, else a fill does
+    OdLut lut{nullptr, 0.0f};
+    if (SOC_CLOUDS_PROFILE < 4 && tuning_knob("SOC_CLOUDS_OD_LUT", 1)) {
+        const float C2 = p.sun[0] * p.sun[0] + p.sun[1] * p.sun[1] + p.sun[2] * p.sun[2];   // dot3(pSun, pSun)
+        lut = OdLut{ws.od_lut, C2};
+        launch("clouds_od_lut", kWorkgroup, clouds_od_lut, ceil_div(kOdR * kOdM, kWorkgroup), kWorkgroup, 0, s, ws.od_lut, C2, counter);
+    } else {
+        hipError_t e = hipMemsetAsync(counter, 0, 256, s);
+        if (e != hipSuccess) return set_error(SOC_E_HIP, "%s: %s", P, hipGetErrorString(e));
+    }
     const int vec_store = (target.pitch_bytes % 16 == 0) && (reinterpret_cast<uintptr_t>(target.data) % 16 == 0);
     launch("clouds_classify", kWorkgroup, clouds_classify, dim3(ceil_div(W, 64), ceil_div(H, 16 * kClassifyTiles)), kWorkgroup, 0, s,
            dimg(depth), dimg(target), p, vec_store, counter, list);
@@ -1105,13 +1116,6 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
     // 1920x1080 -5 % after it); the same bits in every position (profiles/r03_ab_atmos_pos.txt, GPU identity test).
     const int apos_knob = tuning_knob("SOC_CLOUDS_ATMOS_POS", -1);
     const int apos = apos_knob >= 0 ? apos_knob : ((long long)W * H > 2560LL * 1440LL ? 2 : 0);
-    // the frame's secondary-ray table (SOC_CLOUDS_OD_LUT=0: march every secondary ray, the single-lane kernel's bits)
-    OdLut lut{nullptr, 0.0f};
-    if (tuning_knob("SOC_CLOUDS_OD_LUT", 1)) {
-        const float C2 = p.sun[0] * p.sun[0] + p.sun[1] * p.sun[1] + p.sun[2] * p.sun[2];   // dot3(pSun, pSun)
-        lut = OdLut{ws.od_lut, C2};
-        launch("clouds_od_lut", kWorkgroup, clouds_od_lut, ceil_div(kOdR * kOdM, kWorkgroup), kWorkgroup, 0, s, ws.od_lut, C2);
-    }
     // the frame's sky-view table (needs the secondary-ray table; SOC_CLOUDS_SKY_TABLE=0: every pixel evaluated)
     SkyTab st{};
     st.t = nullptr;
