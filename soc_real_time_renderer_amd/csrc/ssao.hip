@@ -329,7 +329,16 @@ struct LdsQuad {
 
 // The default tile: 64 x 16 half-res pixels (1024 lanes), a 32-texel halo (tile sweep: profiles/r03_ssao_tile_sweep.txt);
 // kSsaoTileLanes is the launch bound its launcher checks.
-constexpr int kSsaoTX = 64, kSsaoTY = 16, kSsaoHalo = 32, kSsaoTileLanes = kSsaoTX * kSsaoTY;
+#ifndef SOC_SSAO_TILE_TX
+#define SOC_SSAO_TILE_TX 64   // A/B builds: the tile's half-res extent and halo
+#endif
+#ifndef SOC_SSAO_TILE_TY
+#define SOC_SSAO_TILE_TY 16
+#endif
+#ifndef SOC_SSAO_HALO
+#define SOC_SSAO_HALO 32
+#endif
+constexpr int kSsaoTX = SOC_SSAO_TILE_TX, kSsaoTY = SOC_SSAO_TILE_TY, kSsaoHalo = SOC_SSAO_HALO, kSsaoTileLanes = kSsaoTX * kSsaoTY;
 
 template <bool TABLE, bool SPARSE_IP, bool FULL, int TXP, int TYP, int HALO, int UNROLL, bool PK = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(TXP * TYP, TXP * TYP)))
