@@ -146,6 +146,9 @@ struct TmOut {
 #define SOC_TAA_PVEL12 1
 #endif
 typedef uint32_t u3a4 __attribute__((ext_vector_type(3))) __attribute__((aligned(4)));
+#ifndef SOC_TAA_HIST_PAIR
+#define SOC_TAA_HIST_PAIR 1
+#endif
 struct HistLoad {
     const DImg& prev;
     const DImg& pvel;
@@ -160,6 +163,30 @@ struct HistLoad {
         const DImg& im = which ? pvel : prev;
         r0 = *reinterpret_cast<const u4a8*>(row_ptr<uint2>(im, ay.i0) + ax.i0);
         r1 = *reinterpret_cast<const u4a8*>(row_ptr<uint2>(im, ay.i1) + ax.i0);
+    }
+    // Both pixels of the pair on the same history rows with adjacent footprints (texels i0, i0 + 1 and i0 + 1, i0 + 2):
+    // the three texels of each row in one 16-B + one 8-B load (colour) or one 16-B + one 4-B load (velocity RG words),
+    // instead of two 16-B (two 12-B) loads. The same texels.
+    __device__ __forceinline__ void pair(int which, const Axis& ax, const Axis& ay, u4a8 (&r0)[2], u4a8 (&r1)[2]) const {
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const int row = r ? ay.i1 : ay.i0;
+            u4a8 a, b;
+            if (which) {
+                const uint32_t* w = reinterpret_cast<const uint32_t*>(row_ptr<uint2>(pvel, row) + ax.i0);
+                const u4a8 q = *reinterpret_cast<const u4a8*>(w);
+                const uint32_t w4 = w[4];
+                a = u4a8{q.x, q.y, q.z, 0u};
+                b = u4a8{q.z, 0u, w4, 0u};
+            } else {
+                const uint2* t = row_ptr<uint2>(prev, row) + ax.i0;
+                const u4a8 q = *reinterpret_cast<const u4a8*>(t);
+                const uint2 t2 = t[2];
+                a = q;
+                b = u4a8{q.z, q.w, t2.x, t2.y};
+            }
+            if (r) { r1[0] = a; r1[1] = b; } else { r0[0] = a; r0[1] = b; }
+        }
     }
 };
 
@@ -189,6 +216,10 @@ __device__ __forceinline__ void taa_pair_tail(const DImg& target, const DImg& pr
     const int colx[4] = {xl, x0, x0 + 1, xr};
     const float v = centre_uv_rn(y, H, p.rh);
     uint2 outp[2];
+    // per pixel: the closest-depth velocity and the history footprint; then the history loads of the pair (combined
+    // when the footprints are adjacent on the same rows, SOC_TAA_HIST_PAIR); then the resolve
+    float velx_[2], vely_[2], vx_[2], vy_[2];
+    Axis hax_[2], hay_[2];
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
         const int x = x0 + k;
@@ -207,6 +238,27 @@ __device__ __forceinline__ void taa_pair_tail(const DImg& target, const DImg& pr
                 bi = closest == d ? r * 4 + c : bi;
             }
         const int bx = colx[bi & 3], by = rows[bi >> 2];
+        const uint32_t vv = vel_at(bx, by);
+        velx_[k] = half_f<0>(vv);
+        vely_[k] = half_f<1>(vv);
+        vx_[k] = u - velx_[k];
+        vy_[k] = v - vely_[k];
+        hax_[k] = axis_clamp(vx_[k], prev.w);   // prev and pvel: same extent
+        hay_[k] = axis_clamp(vy_[k], prev.h);
+    }
+    u4a8 ch0[2], ch1[2], vh0[2], vh1[2];
+    if (SOC_TAA_HIST_PAIR && hay_[0].i0 == hay_[1].i0 && hax_[1].i0 == hax_[0].i0 + 1) {
+        hist.pair(0, hax_[0], hay_[0], ch0, ch1);
+        hist.pair(1, hax_[0], hay_[0], vh0, vh1);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            hist(k, 0, hax_[k], hay_[k], ch0[k], ch1[k]);
+            hist(k, 1, hax_[k], hay_[k], vh0[k], vh1[k]);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
         const h2 mnxy = __builtin_elementwise_min(__builtin_elementwise_min(nxy[k], nxy[k + 1]), nxy[k + 2]);
         const h2 mnzw = __builtin_elementwise_min(__builtin_elementwise_min(nzw[k], nzw[k + 1]), nzw[k + 2]);
         const h2 mxxy = __builtin_elementwise_max(__builtin_elementwise_max(xxy[k], xxy[k + 1]), xxy[k + 2]);
@@ -216,15 +268,13 @@ __device__ __forceinline__ void taa_pair_tail(const DImg& target, const DImg& pr
         const v2f bzw = __builtin_elementwise_fma(szw[k + 2], q, __builtin_elementwise_fma(szw[k + 1], hlf, szw[k] * q));
         const uint32_t cxy = __builtin_bit_cast(uint32_t, Cxy[1][k + 2]), czw = __builtin_bit_cast(uint32_t, Czw[1][k + 2]);
         // quirk Q7: the (+1, 0) neighbour is "the" colour
-        const uint32_t vv = vel_at(bx, by);
-        const float velx = half_f<0>(vv), vely = half_f<1>(vv);
+        const float velx = velx_[k], vely = vely_[k];
         // resolve (:172-189)
         float accum = p.accum0;
-        const float vx = u - velx, vy = v - vely;
-        const Axis hax = axis_clamp(vx, prev.w), hay = axis_clamp(vy, prev.h);   // prev and pvel: same extent
+        const float vx = vx_[k], vy = vy_[k];
+        const Axis hax = hax_[k], hay = hay_[k];
         float a4[4], pv[2];
-        u4a8 h0, h1;
-        hist(k, 0, hax, hay, h0, h1);
+        u4a8 h0 = ch0[k], h1 = ch1[k];
         a4[0] = bilerp_h<0>(h0.x, h0.z, h1.x, h1.z, hax.w, hay.w);
         a4[1] = bilerp_h<1>(h0.x, h0.z, h1.x, h1.z, hax.w, hay.w);
         a4[2] = bilerp_h<0>(h0.y, h0.w, h1.y, h1.w, hax.w, hay.w);
@@ -240,7 +290,8 @@ __device__ __forceinline__ void taa_pair_tail(const DImg& target, const DImg& pr
         const float ic = 1.0f - accum;
         const v2f oxy = v2f{__builtin_fmaf(half_f<0>(cxy), accum, a4[0] * ic), __builtin_fmaf(half_f<1>(cxy), accum, a4[1] * ic)};
         const v2f ozw = v2f{__builtin_fmaf(half_f<0>(czw), accum, a4[2] * ic), __builtin_fmaf(half_f<1>(czw), accum, a4[3] * ic)};
-        hist(k, 1, hax, hay, h0, h1);
+        h0 = vh0[k];
+        h1 = vh1[k];
         pv[0] = bilerp_h<0>(h0.x, h0.z, h1.x, h1.z, hax.w, hay.w);
         pv[1] = bilerp_h<1>(h0.x, h0.z, h1.x, h1.z, hax.w, hay.w);
         const float dvx = pv[0] - velx, dvy = pv[1] - vely;
