@@ -346,6 +346,84 @@ __global__ __launch_bounds__(kWorkgroup) void bloomw_up10(DImg S1, DImg O, bool 
     }
 }
 
+// W4 in separable form: both filters of the pass are rank 1 (up 1:2: w (x) w; up 1:1: (1 2 1) (x) (1 2 1)), so each is a
+// horizontal pass into an fp32 LDS tile and a vertical pass: per mip0 entry 4 + 4 taps instead of 16, per output 3 + 3
+// instead of 9. The same weights and footprints (the mip0 entries still rounded to RGBA16F, as the chain stores them);
+// the sums are grouped by rows, so the last fp32 bits may differ from bloomw_up10 (within the RGBA16F tolerance).
+struct P3 {
+    float r[W4_SH > W4_MH ? W4_SH : W4_MH][W4_MW];   // largest of the two intermediates (14 x 66 and 18 x 64)
+    float g[W4_SH > W4_MH ? W4_SH : W4_MH][W4_MW];
+    float b[W4_SH > W4_MH ? W4_SH : W4_MH][W4_MW];
+};
+__global__ __launch_bounds__(kWorkgroup) void bloomw_up10s(DImg S1, DImg O, bool vec, int swz) {
+    __shared__ uint2 st[W4_SH][W4_SW];
+    __shared__ uint2 mt[W4_MH][W4_MW];
+    __shared__ P3 hp;   // horizontal sums: first of the 1:2 pass (st rows x mip0 columns), then of the 1:1 pass
+    const int tid = threadIdx.x;
+    int tbx, tby;
+    xcd_order(swz, tbx, tby);
+    const int X0 = tbx * U_OW, Y0 = tby * U_OH;
+    const int mx0 = X0 - 1, my0 = Y0 - 1;
+    const int sx0 = X0 / 2 - 3, sy0 = Y0 / 2 - 3;
+    const int W0 = O.w, H0 = O.h;
+    load_tile<W4_SW, W4_SH>(S1, sx0, sy0, st, tid);
+    __syncthreads();
+    // 1:2 horizontal: hp[sr][c] for mip0 column c (coordinate clamp(mx0 + c)) on mip1 tile row sr
+    for (int i = tid; i < W4_SH * W4_MW; i += 256) {
+        const int sr = i / W4_MW, c = i - sr * W4_MW;
+        const int q = clampi(mx0 + c, 0, W0 - 1), px = q & 1, c0 = (q >> 1) - 2 + px - sx0;
+        C3 a{0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) madd(a, st[sr][c0 + k], u12_w(px, k));
+        hp.r[sr][c] = a.r;
+        hp.g[sr][c] = a.g;
+        hp.b[sr][c] = a.b;
+    }
+    __syncthreads();
+    // 1:2 vertical: the mip0 entries (RGBA16F, as stored by the chain)
+    for (int i = tid; i < W4_MH * W4_MW; i += 256) {
+        const int r = i / W4_MW, c = i - r * W4_MW;
+        const int cy = clampi(my0 + r, 0, H0 - 1), py = cy & 1, r0 = (cy >> 1) - 2 + py - sy0;
+        C3 a{0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float w = u12_w(py, k);
+            a.r = __builtin_fmaf(hp.r[r0 + k][c], w, a.r);
+            a.g = __builtin_fmaf(hp.g[r0 + k][c], w, a.g);
+            a.b = __builtin_fmaf(hp.b[r0 + k][c], w, a.b);
+        }
+        mt[r][c] = pack3(a);
+    }
+    __syncthreads();
+    // 1:1 horizontal: hp[r][x - X0] over mip0 row r for output column x (tile columns x - mx0 - 1 .. + 1)
+    for (int i = tid; i < W4_MH * U_OW; i += 256) {
+        const int r = i / U_OW, c = i - r * U_OW;   // tile column c + 1
+        C3 a{0.0f, 0.0f, 0.0f};
+        madd(a, mt[r][c], 1.0f);
+        madd(a, mt[r][c + 1], 2.0f);
+        madd(a, mt[r][c + 2], 1.0f);
+        hp.r[r][c] = a.r;
+        hp.g[r][c] = a.g;
+        hp.b[r][c] = a.b;
+    }
+    __syncthreads();
+    // 1:1 vertical and the stores (pairs)
+    for (int i = tid; i < (U_OW / 2) * U_OH; i += 256) {
+        const int r = i / (U_OW / 2), pc = i - r * (U_OW / 2);
+        const int x = X0 + 2 * pc, y = Y0 + r;
+        if (x >= O.w || y >= O.h) continue;
+        C3 o[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int c = 2 * pc + k;
+            o[k].r = __builtin_fmaf(hp.r[r + 2][c], 1.0f / 16.0f, __builtin_fmaf(hp.r[r + 1][c], 2.0f / 16.0f, hp.r[r][c] * (1.0f / 16.0f)));
+            o[k].g = __builtin_fmaf(hp.g[r + 2][c], 1.0f / 16.0f, __builtin_fmaf(hp.g[r + 1][c], 2.0f / 16.0f, hp.g[r][c] * (1.0f / 16.0f)));
+            o[k].b = __builtin_fmaf(hp.b[r + 2][c], 1.0f / 16.0f, __builtin_fmaf(hp.b[r + 1][c], 2.0f / 16.0f, hp.b[r][c] * (1.0f / 16.0f)));
+        }
+        store2(O, x, y, pack3(o[0]), pack3(o[1]), vec);
+    }
+}
+
 // Workgroups of 256 lanes of bloomw_down01p resident on the whole device at once (the persistent kernel's grid bound),
 // queried once per device and cached (the occupancy query is not on the per-frame enqueue path).
 int down01p_resident_set() {
@@ -384,7 +462,10 @@ int launch_bloom_weighted(const soc_img& emissive, const soc_img* mips, const so
     }
     if (stage == 0 || stage == 4) {
         dim3 g(ceil_div(output.width, U_OW), ceil_div(output.height, U_OH));
-        launch("bloomw_up10", kWorkgroup, bloomw_up10, g, kWorkgroup, 0, s, M1, O, a16(output), swz);
+        if (tuning_knob("SOC_BLOOM_UP_SEP", 1))
+            launch("bloomw_up10s", kWorkgroup, bloomw_up10s, g, kWorkgroup, 0, s, M1, O, a16(output), swz);
+        else
+            launch("bloomw_up10", kWorkgroup, bloomw_up10, g, kWorkgroup, 0, s, M1, O, a16(output), swz);
     }
     return check_launch("bloom_weighted");
 }
