@@ -303,6 +303,82 @@ __global__ __launch_bounds__(kWorkgroup) void bloomw_up32(DImg S3, DImg M1, int 
     }
 }
 
+// W3 in separable form (both 1:2 filters are w (x) w): each 1:2 stage as a horizontal pass into an fp32 LDS tile and a
+// vertical pass, 4 + 4 taps instead of 16; mip2 still rounded to RGBA16F (within the RGBA16F tolerance, as bloomw_up10s).
+struct P3u {
+    float r[W3_MH][U_OW], g[W3_MH][U_OW], b[W3_MH][U_OW];   // 10 x 36 (first stage) and 12 x 64 (second) fit
+};
+__global__ __launch_bounds__(kWorkgroup) void bloomw_up32s(DImg S3, DImg M1, int W2, int H2, bool vec, int swz) {
+    __shared__ uint2 st[W3_SH][W3_SW];
+    __shared__ uint2 mt[W3_MH][W3_MW];
+    __shared__ P3u hp;
+    const int tid = threadIdx.x;
+    int tbx, tby;
+    xcd_order(swz, tbx, tby);
+    const int X0 = tbx * U_OW, Y0 = tby * U_OH;
+    const int mx0 = X0 / 2 - 2, my0 = Y0 / 2 - 2;
+    const int sx0 = mx0 / 2 - 2, sy0 = my0 / 2 - 2;
+    load_tile<W3_SW, W3_SH>(S3, sx0, sy0, st, tid);
+    __syncthreads();
+    for (int i = tid; i < W3_SH * W3_MW; i += 256) {   // mip3 rows x mip2 columns (clamped coordinates)
+        const int sr = i / W3_MW, c = i - sr * W3_MW;
+        const int q = clampi(mx0 + c, 0, W2 - 1), px = q & 1, c0 = (q >> 1) - 2 + px - sx0;
+        C3 a{0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) madd(a, st[sr][c0 + k], u12_w(px, k));
+        hp.r[sr][c] = a.r;
+        hp.g[sr][c] = a.g;
+        hp.b[sr][c] = a.b;
+    }
+    __syncthreads();
+    for (int i = tid; i < W3_MH * W3_MW; i += 256) {   // the mip2 entries
+        const int r = i / W3_MW, c = i - r * W3_MW;
+        const int cy = clampi(my0 + r, 0, H2 - 1), py = cy & 1, r0 = (cy >> 1) - 2 + py - sy0;
+        C3 a{0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float w = u12_w(py, k);
+            a.r = __builtin_fmaf(hp.r[r0 + k][c], w, a.r);
+            a.g = __builtin_fmaf(hp.g[r0 + k][c], w, a.g);
+            a.b = __builtin_fmaf(hp.b[r0 + k][c], w, a.b);
+        }
+        mt[r][c] = pack3(a);
+    }
+    __syncthreads();
+    for (int i = tid; i < W3_MH * U_OW; i += 256) {   // mip2 rows x mip1 output columns
+        const int r = i / U_OW, ox = i - r * U_OW;
+        const int x = X0 + ox, px = x & 1, c0 = (x >> 1) - 2 + px - mx0;
+        C3 a{0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) madd(a, mt[r][c0 + k], u12_w(px, k));
+        hp.r[r][ox] = a.r;
+        hp.g[r][ox] = a.g;
+        hp.b[r][ox] = a.b;
+    }
+    __syncthreads();
+    for (int i = tid; i < (U_OW / 2) * U_OH; i += 256) {
+        const int r = i / (U_OW / 2), pc = i - r * (U_OW / 2);
+        const int x = X0 + 2 * pc, y = Y0 + r;
+        if (x >= M1.w || y >= M1.h) continue;
+        const int py = y & 1, r0 = (y >> 1) - 2 + py - my0;
+        C3 o[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int c = 2 * pc + k;
+            C3 a{0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float w = u12_w(py, j);
+                a.r = __builtin_fmaf(hp.r[r0 + j][c], w, a.r);
+                a.g = __builtin_fmaf(hp.g[r0 + j][c], w, a.g);
+                a.b = __builtin_fmaf(hp.b[r0 + j][c], w, a.b);
+            }
+            o[k] = a;
+        }
+        store2(M1, x, y, pack3(o[0]), pack3(o[1]), vec);
+    }
+}
+
 // ================================================================================================
 // W4: mip1 -> [mip0, LDS] -> output (64 x 16 outputs per workgroup)
 // ================================================================================================
@@ -458,7 +534,10 @@ int launch_bloom_weighted(const soc_img& emissive, const soc_img* mips, const so
     }
     if (stage == 0 || stage == 3) {
         dim3 g(ceil_div(mips[1].width, U_OW), ceil_div(mips[1].height, U_OH));
-        launch("bloomw_up32", kWorkgroup, bloomw_up32, g, kWorkgroup, 0, s, M3, M1, mips[2].width, mips[2].height, a16(mips[1]), swz);
+        if (tuning_knob("SOC_BLOOM_UP_SEP", 1))
+            launch("bloomw_up32s", kWorkgroup, bloomw_up32s, g, kWorkgroup, 0, s, M3, M1, mips[2].width, mips[2].height, a16(mips[1]), swz);
+        else
+            launch("bloomw_up32", kWorkgroup, bloomw_up32, g, kWorkgroup, 0, s, M3, M1, mips[2].width, mips[2].height, a16(mips[1]), swz);
     }
     if (stage == 0 || stage == 4) {
         dim3 g(ceil_div(output.width, U_OW), ceil_div(output.height, U_OH));
