@@ -535,7 +535,11 @@ typedef struct soc_material {
     soc_img normal_map;                /* RGBA16F, used with SOC_MATERIAL_NORMAL_MAP */
     soc_img normal_image;              /* RGBA8_UNORM tangent-space normal texture, with SOC_MATERIAL_NORMAL_TEXTURE */
     float max_anisotropy;              /* with SOC_MATERIAL_MIPMAPPED: 16 in the reference (texture.cpp:129-130) */
-    int32_t pad2[3];
+    int32_t pad2;
+    /* optional, with SOC_MATERIAL_MIPMAPPED and a normal_image of the albedo's extent: the two mip chains interleaved
+     * texel by texel (soc_pair_textures), which the G-buffer resolve then reads with one load per texel row pair for
+     * both textures (the same texels and results); NULL: the two images are read separately */
+    void* paired_texels;
 } soc_material;
 #define SOC_MATERIAL_ZERO_VELOCITY 1   /* write velocity 0 (the terrain draw, draw_terrain.inl:221) */
 #define SOC_MATERIAL_NORMAL_MAP 2      /* normal = normalize(bilinear normal_map(uv).xyz) (draw_terrain.inl:206-219) */
@@ -602,6 +606,12 @@ size_t soc_mip_chain_bytes(int32_t width, int32_t height, int32_t pitch_bytes);
  * nearest sRGB code: the largest k with linear >= the midpoint of codes k-1 and k), RGBA8_UNORM and alpha
  * round to nearest. Runs once per texture at load (upload), one launch per level on `stream`. */
 int soc_generate_mips(soc_img texture, soc_stream stream);
+/* A material's albedo and normal image mip chains (both generated, one extent) interleaved texel by texel into
+ * `paired` (soc_paired_texels_bytes(width, height) bytes, device): level k holds, for texel i of its tight
+ * w_k x h_k rows, the albedo texel then the normal texel (8 B), levels packed after one another from level 0.
+ * Runs once per material at load, on `stream`. */
+size_t soc_paired_texels_bytes(int32_t width, int32_t height);
+int soc_pair_textures(soc_img albedo, soc_img normal_image, void* paired, soc_stream stream);
 
 /* HeightToNormalTask (height_to_normal.inl:52-83): RGBA8 heightmap (.r) -> RGBA16F normal map of the same
  * extent; run once at terrain load (renderer.cpp:158-190). */

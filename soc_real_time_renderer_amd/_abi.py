@@ -128,7 +128,7 @@ class Material(C.Structure):
     _fields_ = [("albedo", SocImg), ("emissive", SocImg), ("albedo_factor", C.c_float * 4),
                 ("emissive_factor", C.c_float * 4), ("flags", C.c_int32), ("has_emissive", C.c_int32),
                 ("pad", C.c_int32 * 2), ("normal_map", SocImg), ("normal_image", SocImg),
-                ("max_anisotropy", C.c_float), ("pad2", C.c_int32 * 3)]
+                ("max_anisotropy", C.c_float), ("pad2", C.c_int32), ("paired_texels", C.c_void_p)]
 
 
 class RasterScene(C.Structure):
@@ -238,6 +238,7 @@ FUNCTIONS = {
     "soc_renderer_reset_timing": (_I, [_P]),
     "soc_renderer_pass_stats": (_I, [_P, C.c_int32, C.POINTER(C.c_float), C.POINTER(C.c_int32)]),
     "soc_raster_workspace_size": (C.c_size_t, [C.c_int32, C.c_int32]),
+    "soc_paired_texels_bytes": (C.c_size_t, [C.c_int32, C.c_int32]),
     "soc_renderer_set_raster_scene": (_I, [_P, C.POINTER(RasterScene)]),
     "soc_height_to_normal": (_I, [_IMG, _IMG, _P]),
     "soc_terrain_tess_counts": (_I, [_I, _I, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
@@ -245,6 +246,7 @@ FUNCTIONS = {
     "soc_mip_level_count": (_I, [_I, _I]),
     "soc_mip_chain_bytes": (C.c_size_t, [_I, _I, _I]),
     "soc_generate_mips": (_I, [_IMG, _P]),
+    "soc_pair_textures": (_I, [_IMG, _IMG, _P, _P]),
     "soc_generate_hiz": (_I, [_G, _IMG, C.POINTER(SocImg), C.c_int32, C.c_int32, _P, _P]),
     "soc_renderer_metrics_json": (C.c_int64, [_P, C.c_uint64, C.c_char_p, C.c_size_t]),
     "soc_read_image": (_I, [_IMG, _P, C.c_int32, _P]),

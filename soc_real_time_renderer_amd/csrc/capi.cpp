@@ -211,7 +211,7 @@ const FieldInfo kFields[] = {
     F(soc_mesh, vertex_count), F(soc_mesh, triangle_count), F(soc_mesh, model_matrix), F(soc_mesh, normal_matrix),
     F(soc_material, albedo), F(soc_material, emissive), F(soc_material, albedo_factor), F(soc_material, emissive_factor),
     F(soc_material, flags), F(soc_material, has_emissive), F(soc_material, pad), F(soc_material, normal_map),
-    F(soc_material, normal_image), F(soc_material, max_anisotropy), F(soc_material, pad2),
+    F(soc_material, normal_image), F(soc_material, max_anisotropy), F(soc_material, pad2), F(soc_material, paired_texels),
     F(soc_raster_scene, mesh), F(soc_raster_scene, materials), F(soc_raster_scene, material_count),
     F(soc_raster_scene, shadow), F(soc_raster_scene, visibility), F(soc_raster_scene, workspace),
     F(soc_entity, position), F(soc_entity, rotation), F(soc_entity, scale), F(soc_entity, components),

@@ -359,6 +359,7 @@ struct ResolveParams {
     Mat3 normal3;
     int width, height, triangle_count, material_count;
     int tex_pairs;   // share the footprint of same-extent normal image + albedo (tuning knob SOC_GB_TEX_PAIRS, default on)
+    int paired;      // read a material's paired_texels when it has them (tuning knob SOC_GB_PAIRED, default on)
     int wave_shape;  // pixels of a wave / workgroup: 0 = 64 x 1 / 64 x 4, 1 = 16 x 4 / 64 x 4, 2 = 8 x 8 / 32 x 8 (default),
                      // 3 = 8 x 8 / 16 x 16, 4 = 8 x 8 / 8 x 32 (tuning knob SOC_GB_WAVE)
 };
@@ -597,6 +598,96 @@ __device__ __forceinline__ void sample_texture_mip2(const soc_img& ta, const soc
     rb = f4{accb.x / fn, accb.y / fn, accb.z / fn, accb.w / fn};
 }
 
+// sample_texture_mip2 from the material's paired texels (soc_pair_textures: albedo and normal texel interleaved, 8 B):
+// each tap row of both textures is one 16-B load (two 8-B loads at the REPEAT seam) instead of one 8-B load per
+// texture. The same texels reach the same filter arithmetic: the same bits as sample_texture_mip2 (GPU test).
+__device__ __forceinline__ DImg paired_level(const void* paired, int W, int H, int k) {
+    int wk, hk;
+    const size_t off = mip_offset(W, H, 8 * W, k, wk, hk, 8);
+    return DImg{static_cast<char*>(const_cast<void*>(paired)) + off, wk, hk, 8 * wk};
+}
+typedef uint32_t u4a8g __attribute__((ext_vector_type(4))) __attribute__((aligned(8)));
+__device__ __forceinline__ void paired_row(const DImg& im, int x0, int x1, int y, uint32_t& a0, uint32_t& n0, uint32_t& a1,
+                                           uint32_t& n1) {
+    const uint2* row = row_ptr<uint2>(im, y);
+    if (x1 == x0 + 1) {
+        const u4a8g t = *reinterpret_cast<const u4a8g*>(row + x0);
+        a0 = t.x; n0 = t.y; a1 = t.z; n1 = t.w;
+    } else {
+        const uint2 p = row[x0], q = row[x1];
+        a0 = p.x; n0 = p.y; a1 = q.x; n1 = q.y;
+    }
+}
+__device__ __forceinline__ void sample_paired_level(const DImg& im, const Axis& ax, const Axis& ay, bool sn, bool sa,
+                                                    const float* lut, f4& rn, f4& ra) {
+    uint32_t a0, n0, a1, n1, a2, n2, a3, n3;
+    paired_row(im, ax.i0, ax.i1, ay.i0, a0, n0, a1, n1);
+    paired_row(im, ax.i0, ax.i1, ay.i1, a2, n2, a3, n3);
+#if SOC_GB_FAST_FILTER
+    rn = bilerp_rgba8(n0, n1, n2, n3, ax.w, ay.w, sn, lut);
+    ra = bilerp_rgba8(a0, a1, a2, a3, ax.w, ay.w, sa, lut);
+#else
+    rn = bilerp4(decode_rgba8(n0, sn, lut), decode_rgba8(n1, sn, lut), decode_rgba8(n2, sn, lut), decode_rgba8(n3, sn, lut), ax.w, ay.w);
+    ra = bilerp4(decode_rgba8(a0, sa, lut), decode_rgba8(a1, sa, lut), decode_rgba8(a2, sa, lut), decode_rgba8(a3, sa, lut), ax.w, ay.w);
+#endif
+}
+// ta: the normal image, tb: the albedo (their extent and formats); results as sample_texture_mip2's (ra: normal, rb: albedo)
+__device__ __forceinline__ void sample_texture_mip2p(const soc_img& ta, const soc_img& tb, const void* paired, float u, float v,
+                                                     const UVGrad& gr, float max_aniso, const float* lut, f4& ra, f4& rb) {
+#pragma clang fp contract(off)
+    const bool sa = ta.format == SOC_FMT_RGBA8_SRGB, sb = tb.format == SOC_FMT_RGBA8_SRGB;
+    const int L = mip_levels(ta.width, ta.height);
+    const float W = (float)ta.width, H = (float)ta.height;
+    const float ax = gr.dudx * W, ay = gr.dvdx * H, bx = gr.dudy * W, by = gr.dvdy * H;
+    const float px = sqrtf(ax * ax + ay * ay), py = sqrtf(bx * bx + by * by);
+    const float pmax = fmaxf(px, py), pmin = fminf(px, py);
+    int n = 1;
+    if (max_aniso > 1.0f && pmax > 0.0f && pmax <= 3.4e38f) {
+        const float cap = floorf(max_aniso);
+        n = (int)(pmin > 0.0f ? fminf(ceilf(pmax / pmin), cap) : cap);
+    }
+    int lq = 0;
+    const float rho = pmax / (float)n;
+    if (rho > 0.0f && rho <= 3.4e38f) {
+        const float lam = fminf(fmaxf(det_log2(rho), -64.0f), 64.0f);
+        lq = min(max((int)floorf(lam * 256.0f + 0.5f), 0), (L - 1) * 256);
+    }
+    const int l0 = lq >> 8, l1 = min(l0 + 1, L - 1);
+    const float f = (float)(lq & 255) * (1.0f / 256.0f);
+    const DImg p0 = paired_level(paired, ta.width, ta.height, l0), p1 = paired_level(paired, ta.width, ta.height, l1);
+    const bool xmajor = px >= py;
+    const float du = xmajor ? gr.dudx : gr.dudy, dv = xmajor ? gr.dvdx : gr.dvdy;
+    f4 acca = f4{0.0f, 0.0f, 0.0f, 0.0f}, accb = acca;
+    for (int i = 1; i <= n; ++i) {
+        float su = u, sv = v;
+        if (n > 1) {
+            const float t = (float)i / (float)(n + 1) - 0.5f;
+            su = u + t * du;
+            sv = v + t * dv;
+        }
+        const Axis x0 = axis_repeat_level(su, p0.w), y0 = axis_repeat_level(sv, p0.h);
+        f4 pa, pb;
+        sample_paired_level(p0, x0, y0, sa, sb, lut, pa, pb);
+        if (lq & 255) {
+            const Axis x1 = axis_repeat_level(su, p1.w), y1 = axis_repeat_level(sv, p1.h);
+            f4 qa, qb;
+            sample_paired_level(p1, x1, y1, sa, sb, lut, qa, qb);
+            pa = lerp_levels(pa, qa, f);
+            pb = lerp_levels(pb, qb, f);
+        }
+        acca = f4{acca.x + pa.x, acca.y + pa.y, acca.z + pa.z, acca.w + pa.w};
+        accb = f4{accb.x + pb.x, accb.y + pb.y, accb.z + pb.z, accb.w + pb.w};
+    }
+    if (n == 1) {
+        ra = acca;
+        rb = accb;
+        return;
+    }
+    const float fn = (float)n;
+    ra = f4{acca.x / fn, acca.y / fn, acca.z / fn, acca.w / fn};
+    rb = f4{accb.x / fn, accb.y / fn, accb.z / fn, accb.w / fn};
+}
+
 __device__ __forceinline__ f3 mat3_vec_exact(const Mat3& M, f3 v) {
 #pragma clang fp contract(off)
     const float* m = M.m;
@@ -794,7 +885,10 @@ __global__ __launch_bounds__(kWorkgroup) __attribute__((amdgpu_waves_per_eu(SOC_
     const bool pair = tbn && mipped && p.tex_pairs && m.albedo.data && m.albedo.width == m.normal_image.width &&
                       m.albedo.height == m.normal_image.height;
     f4 t_pair{0.0f, 0.0f, 0.0f, 0.0f}, al_pair = t_pair;
-    if (pair) sample_texture_mip2(m.normal_image, m.albedo, u, v, gr, m.max_anisotropy, lut, t_pair, al_pair);
+    if (pair && m.paired_texels && p.paired)
+        sample_texture_mip2p(m.normal_image, m.albedo, m.paired_texels, u, v, gr, m.max_anisotropy, lut, t_pair, al_pair);
+    else if (pair)
+        sample_texture_mip2(m.normal_image, m.albedo, u, v, gr, m.max_anisotropy, lut, t_pair, al_pair);
     if (tbn) {   // g_buffer_generation.inl:197-211
         const f4 t = pair ? t_pair : tex(m.normal_image);
         const f3 tn{t.x * 2.0f - 1.0f, t.y * 2.0f - 1.0f, t.z * 2.0f - 1.0f};
@@ -926,6 +1020,7 @@ extern "C" int soc_gbuffer_resolve(const soc_globals* g, const soc_mesh* mesh, c
     p.triangle_count = mesh->triangle_count;
     p.material_count = material_count;
     p.tex_pairs = tuning_knob("SOC_GB_TEX_PAIRS", 1);
+    p.paired = tuning_knob("SOC_GB_PAIRED", 1);
     p.wave_shape = tuning_knob("SOC_GB_WAVE", 2);   // 8 x 8-pixel waves: 687 -> 626 us at 4K (profiles/r04_probe_gbuffer_wave.txt)
     dim3 blk(64, 4), grd(ceil_div(W, 64), ceil_div(H, 4));
     if (p.wave_shape == 2) grd = dim3(ceil_div(W, 32), ceil_div(H, 8));

@@ -210,12 +210,12 @@ __host__ __device__ __forceinline__ int mip_levels(int w, int h) {
     while (m > 0) { ++n; m >>= 1; }
     return n;
 }
-__host__ __device__ __forceinline__ size_t mip_offset(int w, int h, int pitch, int k, int& wk, int& hk) {
+__host__ __device__ __forceinline__ size_t mip_offset(int w, int h, int pitch, int k, int& wk, int& hk, int bpp = 4) {
     size_t off = 0;
     wk = w;
     hk = h;
     for (int j = 1; j <= k; ++j) {
-        off += j == 1 ? (size_t)pitch * h : (size_t)4 * wk * hk;
+        off += j == 1 ? (size_t)pitch * h : (size_t)bpp * wk * hk;
         wk = wk > 1 ? wk >> 1 : 1;
         hk = hk > 1 ? hk >> 1 : 1;
     }

@@ -84,10 +84,45 @@ __global__ __launch_bounds__(kWorkgroup) void mip_blit(DImg src, DImg dst, int s
     row_ptr_w<uint32_t>(dst, y)[x] = out;
 }
 
+// One level of the paired chain: texel i of the level's tight rows <- (albedo texel, normal texel).
+__global__ __launch_bounds__(kWorkgroup) void pair_level(DImg a, DImg n, uint2* __restrict__ dst) {
+    const int x = blockIdx.x * 64 + threadIdx.x, y = blockIdx.y * 4 + threadIdx.y;
+    if (x >= a.w || y >= a.h) return;
+    dst[(size_t)y * a.w + x] = uint2{row_ptr<uint32_t>(a, y)[x], row_ptr<uint32_t>(n, y)[x]};
+}
+
 }  // namespace
 }  // namespace soc
 
 using namespace soc;
+
+extern "C" size_t soc_paired_texels_bytes(int32_t width, int32_t height) {
+    if (width <= 0 || height <= 0) return 0;
+    int wk, hk;
+    const int L = mip_levels(width, height);
+    return mip_offset(width, height, 8 * width, L - 1, wk, hk, 8) + (size_t)8 * wk * hk;
+}
+
+extern "C" int soc_pair_textures(soc_img albedo, soc_img normal_image, void* paired, soc_stream stream) {
+    const auto rgba8 = [](const soc_img& t) { return t.format == SOC_FMT_RGBA8_UNORM || t.format == SOC_FMT_RGBA8_SRGB; };
+    if (!rgba8(albedo) || !rgba8(normal_image) || !albedo.data || !normal_image.data || !paired)
+        return set_error(SOC_E_INVALID_ARG, "soc_pair_textures: two RGBA8 textures with data and a target are required");
+    if (albedo.width != normal_image.width || albedo.height != normal_image.height || albedo.width <= 0 || albedo.height <= 0 ||
+        albedo.pitch_bytes < albedo.width * 4 || normal_image.pitch_bytes < normal_image.width * 4)
+        return set_error(SOC_E_SHAPE, "soc_pair_textures: the textures must share one extent");
+    const int W = albedo.width, H = albedo.height, L = mip_levels(W, H);
+    for (int k = 0; k < L; ++k) {
+        int wa, ha, wn, hn, wp, hp;
+        const size_t oa = mip_offset(W, H, albedo.pitch_bytes, k, wa, ha);
+        const size_t on = mip_offset(W, H, normal_image.pitch_bytes, k, wn, hn);
+        const size_t op = mip_offset(W, H, 8 * W, k, wp, hp, 8);
+        const DImg a{static_cast<char*>(albedo.data) + oa, wa, ha, k ? 4 * wa : albedo.pitch_bytes};
+        const DImg n{static_cast<char*>(normal_image.data) + on, wn, hn, k ? 4 * wn : normal_image.pitch_bytes};
+        launch("pair_level", kWorkgroup, pair_level, dim3(ceil_div(wa, 64), ceil_div(ha, 4)), dim3(64, 4), 0, hs(stream), a, n,
+               reinterpret_cast<uint2*>(static_cast<char*>(paired) + op));
+    }
+    return check_launch("pair_textures");
+}
 
 extern "C" int32_t soc_mip_level_count(int32_t width, int32_t height) {
     return width > 0 && height > 0 ? mip_levels(width, height) : 0;

@@ -160,7 +160,22 @@ def material(albedo=None, emissive=None, albedo_factor=(1.0, 1.0, 1.0, 1.0), emi
     m.normal_image = tex_img(normal_texture, FMT_RGBA8_UNORM) if normal_texture is not None else img(None)
     if normal_texture is not None:
         m.flags |= MATERIAL_NORMAL_TEXTURE
+    if (mipped and albedo is not None and normal_texture is not None and isinstance(albedo.buf, torch.Tensor)
+            and albedo.buf.is_cuda and (albedo.width, albedo.height) == (normal_texture.width, normal_texture.height)):
+        m.paired_texels = paired_texels(albedo, normal_texture)
     return m
+
+
+def paired_texels(albedo: MipTexture, normal_texture: MipTexture, stream=None) -> int:
+    """soc_pair_textures: the two device mip chains interleaved texel by texel (the G-buffer resolve then reads both
+    textures of a tap row with one load). The buffer lives as long as the normal texture (kept on it); returns its
+    device address for soc_material.paired_texels."""
+    n = int(lib().soc_paired_texels_bytes(albedo.width, albedo.height))
+    buf = torch.empty(n, dtype=torch.uint8, device=albedo.buf.device)
+    _check(lib().soc_pair_textures(albedo.img(), normal_texture.img(), C.c_void_p(buf.data_ptr()), _stream(stream)),
+           "pair_textures")
+    normal_texture.paired = buf
+    return buf.data_ptr()
 
 
 def materials_device(mats: Sequence[Material], device="cuda") -> torch.Tensor:

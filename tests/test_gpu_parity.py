@@ -89,13 +89,16 @@ def test_bloom_chain_bit_exact(soc, oracle, W, H):
         assert np.array_equal(host(mips_d[i])[..., :3].view(np.uint16), mips_h[i][..., :3].view(np.uint16)), i
 
 
+@pytest.mark.parametrize("sep", ["1", "0"])
 @pytest.mark.parametrize("W,H", [(64, 40), (200, 136), (968, 552), (1920, 1080), (3840, 2160)])
-def test_bloom_weighted_chain(soc, W, H):
+def test_bloom_weighted_chain(soc, monkeypatch, W, H, sep):
     """The weighted-form chain (bloom_w.hip, 4 kernels) against the reference's 8 separate passes
     (bit-exact to the oracle): output and the observable mips (1 upswept, 3 downswept) within the
     RGBA16F tolerance, and almost all texels bit-identical (the weights are the taps' exact weights;
     only the fp32 rounding order differs). Stage by stage equals the whole chain; the emissive input of
-    a separate output is untouched."""
+    a separate output is untouched. sep: the upsample launches in separable form (default) or 2-D."""
+    monkeypatch.setenv("SOC_BLOOM_UP_SEP", sep)
+    soc.reload_tuning()
     g = globals_for(W, H)
     em = dev(random_rgba16(H, W, seed=23, hi=16.0))
     shapes = [(H >> i, W >> i, 4) for i in range(4)]

@@ -391,7 +391,9 @@ def test_sponza_mesh_mipmapped_gbuffer_vs_oracle(soc, oracle, tex):
 def test_mipmapped_gbuffer_shared_footprint_bit_identical(soc, monkeypatch, tex):
     """The resolve samples a material's normal image and albedo of one extent with one shared footprint / tap /
     lod computation (SOC_GB_TEX_PAIRS, default on): the same bits as sampling them one after the other. Every
-    wave / workgroup shape (SOC_GB_WAVE 0-4; 270 rows: partial tiles of 8, 16 and 32 rows) gives the same bits."""
+    wave / workgroup shape (SOC_GB_WAVE 0-4; 270 rows: partial tiles of 8, 16 and 32 rows) gives the same bits, and
+    so does reading both textures from the material's interleaved paired texels (soc_pair_textures, SOC_GB_PAIRED,
+    default on) instead of the two images."""
     W, H = 480, 270
     g = globals_for(W, H)
     _, dm = _mesh_scene()
@@ -401,10 +403,13 @@ def test_mipmapped_gbuffer_shared_footprint_bit_identical(soc, monkeypatch, tex)
     ws = dm.workspace()
     vis = torch.zeros((H, W), dtype=torch.int64, device=DEV)
     raster.raster_visibility(dm, vp, raster.CULL_FRONT, vis, ws)
+    assert sum(1 for m in mats_d if m.paired_texels) > 0
     outs = []
-    for pairs, wave in (("1", "2"), ("0", "2"), ("1", "0"), ("1", "1"), ("1", "3"), ("1", "4")):
+    for pairs, wave, paired in (("1", "2", "1"), ("1", "2", "0"), ("0", "2", "1"), ("1", "0", "1"), ("1", "1", "0"),
+                                ("1", "3", "1"), ("1", "4", "0")):
         monkeypatch.setenv("SOC_GB_TEX_PAIRS", pairs)
         monkeypatch.setenv("SOC_GB_WAVE", wave)
+        monkeypatch.setenv("SOC_GB_PAIRED", paired)
         soc.reload_tuning()
         out = {k: torch.zeros((H, W, 4), dtype=torch.float16, device=DEV) for k in ("albedo", "emissive", "normal", "velocity")}
         out["depth"] = torch.zeros((H, W), dtype=torch.float32, device=DEV)
@@ -413,6 +418,7 @@ def test_mipmapped_gbuffer_shared_footprint_bit_identical(soc, monkeypatch, tex)
         outs.append(out)
     monkeypatch.delenv("SOC_GB_TEX_PAIRS")
     monkeypatch.delenv("SOC_GB_WAVE")
+    monkeypatch.delenv("SOC_GB_PAIRED")
     soc.reload_tuning()
     for o in outs[1:]:
         for k in outs[0]:
