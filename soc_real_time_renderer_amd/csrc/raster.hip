@@ -269,20 +269,45 @@ __global__ __launch_bounds__(kWorkgroup) void raster_clear_vis(unsigned long lon
     if (i < n) vis[i] = ((unsigned long long)__float_as_uint(1.0f) << 32) | KEY_EMPTY;
 }
 
+// The large triangles' entries are reserved once per workgroup: an LDS atomic gives each its offset in the workgroup's
+// share and one global atomic on the packed counter reserves the share (one returning atomic on the one counter per
+// wave cost ~40 us at 4K: the counter serialises them). The packed adds keep the entry slots and their tile ranges
+// increasing together, as raster_big's search needs (SOC_RASTER_WG_ENTRIES=0: one atomic per wave, as before).
+#ifndef SOC_RASTER_WG_ENTRIES
+#define SOC_RASTER_WG_ENTRIES 1
+#endif
 __global__ __launch_bounds__(kWorkgroup) void raster_small(const uint32_t* __restrict__ idx, Workspace ws, RasterParams p,
                                                     void* target, size_t pitch) {
     const int id = blockIdx.x * 256 + threadIdx.x;
-    if (id >= p.triangle_count) return;
-    const TriSetup t = load_tri(ws, idx, id, p);
-    if (!t.live) return;
+    TriSetup t{};
+    t.live = false;
+    if (id < p.triangle_count) t = load_tri(ws, idx, id, p);
     const int bw = t.px1 - t.px0 + 1, bh = t.py1 - t.py0 + 1;
-    const long long n = (long long)bw * bh;
-    if (n > p.small_pixels) {
+    const bool big = t.live && (long long)bw * bh > p.small_pixels;
+    if (SOC_RASTER_WG_ENTRIES) {
+        __shared__ unsigned long long wg_acc, wg_base;
+        if (threadIdx.x == 0) wg_acc = 0ull;
+        __syncthreads();
+        unsigned long long local = 0ull;
+        if (big) {
+            const uint32_t chunks = (uint32_t)(((bw + TILE - 1) / TILE) * ((bh + TILE - 1) / TILE));
+            local = atomicAdd(&wg_acc, (1ull << ENTRY_SHIFT) + chunks);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0 && wg_acc) wg_base = atomicAdd(ws.counter, wg_acc);
+        __syncthreads();
+        if (big) {
+            const unsigned long long old = wg_base + local;
+            ws.entries[old >> ENTRY_SHIFT] = uint2{(uint32_t)id, (uint32_t)old};
+            return;
+        }
+    } else if (big) {
         const uint32_t chunks = (uint32_t)(((bw + TILE - 1) / TILE) * ((bh + TILE - 1) / TILE));
         const unsigned long long old = atomicAdd(ws.counter, (1ull << ENTRY_SHIFT) + chunks);
         ws.entries[old >> ENTRY_SHIFT] = uint2{(uint32_t)id, (uint32_t)old};
         return;
     }
+    if (!t.live) return;
     for (int y = t.py0; y <= t.py1; ++y)
         for (int x = t.px0; x <= t.px1; ++x) shade(t, id, x, y, p, target, pitch);
 }
