@@ -660,6 +660,10 @@ struct soc_renderer {
     hipEvent_t fork_ev = nullptr, join_ev = nullptr;
     // 8 partial luminance histograms of the fused composition + histogram pass (renderer-owned, 8 KiB)
     uint32_t* hist_scratch = nullptr;
+    // a raster workspace of the sun shadow draw's own, so it can run on the second lane beside the depth prepass and
+    // the G-buffer (they share scene.workspace's screen vertices and entry lists otherwise)
+    void* shadow_ws = nullptr;
+    size_t shadow_ws_bytes = 0;
     // this execute call runs both phases: the resolve folds the partial histograms itself (no fold launch)
     bool fold_in_resolve = false;
     // sky split configured (graph) / active this frame (the pair path applies at the globals' resolution)
@@ -722,12 +726,16 @@ void build_raster_passes(soc_renderer* r) {
                  return soc_raster_visibility(&r->scene.mesh, g->camera_projection_view_matrix, SOC_CULL_FRONT,
                                               r->scene.visibility, d.width, d.height, 1, r->scene.workspace, (soc_stream)s);
              });
+    // With its own workspace the shadow draw reads nothing the main lane writes in the frame: it runs on the second lane
+    // beside the depth prepass and the G-buffer (SOC_RENDERER_SHADOW_LANE=0: on the main lane, in the shared workspace).
+    const bool shadow_lane = r->shadow_ws && tuning_knob("SOC_RENDERER_SHADOW_LANE", 1);
     if (r->scene.shadow)
         add_pass(r, "SunShadowDraw", "Shadows", pre, 0, res_mask({SOC_RES_SUN_SHADOW}),
-                 [r](const soc_globals* g, hipStream_t s) {
+                 [r, shadow_lane](const soc_globals* g, hipStream_t s) {
                      return soc_raster_depth(&r->scene.mesh, g->sun_info.projection_view_matrix, SOC_CULL_BACK, 1.25f,
-                                             1.75f, r->img.shadow, r->scene.workspace, (soc_stream)s);
-                 });
+                                             1.75f, r->img.shadow, shadow_lane ? r->shadow_ws : r->scene.workspace,
+                                             (soc_stream)s);
+                 }, shadow_lane ? SOC_PASS_ASYNC : 0);
     // GBufferGenerationTask uses (renderer.cpp:993-1005): albedo, emissive, normal, velocity, depth
     add_pass(r, "GBufferGeneration", "Rendering G-Buffer", pre, res_mask({SOC_RES_VISIBILITY}),
              res_mask({SOC_RES_ALBEDO, SOC_RES_EMISSIVE, SOC_RES_NORMAL, SOC_RES_VELOCITY, SOC_RES_DEPTH}),
@@ -1079,6 +1087,7 @@ extern "C" void soc_renderer_destroy(soc_renderer* r) {
     if (r->join_ev) (void)hipEventDestroy(r->join_ev);
     if (r->side) (void)hipStreamDestroy(r->side);
     if (r->hist_scratch) (void)hipFree(r->hist_scratch);
+    if (r->shadow_ws) (void)hipFree(r->shadow_ws);
     delete r;
 }
 
@@ -1322,6 +1331,16 @@ extern "C" int soc_renderer_set_raster_scene(soc_renderer* r, const soc_raster_s
             return set_error(SOC_E_INVALID_ARG, "soc_renderer_set_raster_scene: incomplete scene");
         if (scene->shadow && !r->img.shadow.data)
             return set_error(SOC_E_INVALID_ARG, "soc_renderer_set_raster_scene: shadow pass needs images.shadow");
+    }
+    if (scene && scene->shadow) {
+        const size_t need = soc_raster_workspace_size(scene->mesh.vertex_count, scene->mesh.triangle_count);
+        if (need > r->shadow_ws_bytes) {
+            if (r->shadow_ws) (void)hipFree(r->shadow_ws);
+            r->shadow_ws = nullptr;
+            r->shadow_ws_bytes = 0;
+            if (hipMalloc(&r->shadow_ws, need) != hipSuccess) r->shadow_ws = nullptr;   // then the shared workspace
+            else r->shadow_ws_bytes = need;
+        }
     }
     r->has_scene = scene != nullptr;
     if (scene) r->scene = *scene;
