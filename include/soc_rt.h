@@ -637,7 +637,9 @@ typedef struct soc_raster_scene {
     uint64_t* visibility;              /* width*height u64, device */
     void* workspace;                   /* soc_raster_workspace_size(mesh) bytes, device */
 } soc_raster_scene;
-int soc_renderer_set_raster_scene(soc_renderer* r, const soc_raster_scene* scene);   /* NULL: clear */
+/* NULL: clear. With shadow = 1 the renderer allocates a second raster workspace (soc_raster_workspace_size of the mesh)
+ * for the sun shadow draw, which then runs on its second lane beside the depth prepass and the G-buffer. */
+int soc_renderer_set_raster_scene(soc_renderer* r, const soc_raster_scene* scene);
 
 /* --- Headless output and metrics (replaces the swapchain present of tone_mapping.inl:
  * 172-176 and the ImGui "GPU Metric" window of renderer.cpp:769-806) ------------------------------- */
