@@ -216,7 +216,7 @@ def cpu_baseline(W, H, host_inputs, g):
             "ms_per_pass_median": {k: round(float(np.median(v)) * 1e3, 2) for k, v in times.items()}}
 
 
-def build_inputs(config, scene_name, W, H, rank, device, mips=True):
+def build_inputs(config, scene_name, W, H, rank, device, mips=True, output_format=None):
     """The frame inputs of a bench configuration (shared with the 4K C3 parity test): globals of rank `rank`'s camera,
     the G-buffer + 4096^2 sun shadow map (the Sponza-proxy mesh rasterised once by the HIP rasteriser, or the
     host-synthesised box atrium / terrain), the noise texture, and the device frame images holding them.
@@ -243,7 +243,8 @@ def build_inputs(config, scene_name, W, H, rank, device, mips=True):
         gb = scene.gbuffer(g, W, H, scene_id=scene_id)
         shadow = scene.shadow_map(g, 4096, scene_id=scene_id)
     noise = scene.noise_texture()
-    fr = soc.alloc_frame(W, H, device, bloom_output=True)
+    fr = soc.alloc_frame(W, H, device, bloom_output=True,
+                         **({} if output_format is None else {"output_format": output_format}))
     for k in ("albedo", "emissive", "normal", "velocity", "depth"):
         fr[k].copy_(torch.from_numpy(gb[k]))
     fr["shadow"].copy_(torch.from_numpy(shadow))
@@ -277,6 +278,9 @@ def main():
     ap.add_argument("--metrics-jsonl", default="", help="one GPU-metric JSON line per profiled frame")
     ap.add_argument("--no-mips", action="store_true",
                     help="mesh scene: level-0 bilinear textures instead of the reference's mip chains + 16x anisotropic sampler")
+    ap.add_argument("--exchange", action="store_true",
+                    help="take the multi-GPU frame path at any N: PRE -> histogram all-reduce (RCCL, a world-size-1 "
+                         "group at N = 1) -> POST, with the all-reduce timed (SURVEY.md §8e)")
     ap.add_argument("--raster", action="store_true",
                     help="end-to-end frame: rasterise the scene mesh into the G-buffer and the 4096^2 sun shadow "
                          "map every frame (DepthPrepass / SunShadowDraw / GBufferGeneration in the graph)")
@@ -290,7 +294,8 @@ def main():
     dev_index = 0 if os.environ.get("SOC_BENCH_SHARE_DEVICE") == "1" else local_rank
     torch.cuda.set_device(dev_index)
     device = torch.device("cuda", dev_index)
-    multi_gpu.init(device, backend=os.environ.get("SOC_DIST_BACKEND", "nccl"))
+    multi_gpu.init(device, backend=os.environ.get("SOC_DIST_BACKEND", "nccl"), force_exchange=args.exchange)
+    exchange = multi_gpu.exchange_active()
     W = args.width or (1920 if args.config == "c2" else 3840)
     H = args.height or (1080 if args.config == "c2" else 2160)
 
@@ -318,7 +323,7 @@ def main():
 
     def frame(timed=False):
         ev = None
-        if timed and world > 1:
+        if timed and exchange:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             xev.append(ev)
         # PRE, RCCL all-reduce of the 1 KiB histogram (N > 1), POST
@@ -448,8 +453,8 @@ def main():
                                f"{' with 128 point lights' if args.config == 'c3b' else ''}, auto-exposure, "
                                f"TAA, AgX tone map",
                    "resolution": [W, H], "f_sky": round(f_sky, 4), "parallelism": f"frame-per-gpu x{world}",
-                   "histogram_allreduce": world > 1,
-                   "collective_backend": (dist.get_backend() if world > 1 else None),
+                   "histogram_allreduce": exchange,
+                   "collective_backend": (dist.get_backend() if exchange else None),
                    "sky_lane": ("CloudRendering + SkyCompose on a concurrent stream; " +
                                 ("the clouds of frame N+1 may start before frame N's TAA (static inputs)"
                                  if not args.no_static_inputs else "forked at every frame start")),
@@ -483,7 +488,7 @@ def main():
                                             if not args.raster else None)}},
         "ranks": per_rank,
         "allreduce_us_per_frame": (round(sum(p["allreduce_us_per_frame"] for p in per_rank) / world, 2)
-                                   if world > 1 else None),
+                                   if exchange else None),
         "ms_per_pass": ms_pass,
         "ms_per_group": ms_group,
         "gbs_per_pass": pass_gbs,
@@ -497,7 +502,7 @@ def main():
         out["cpu_baseline"] = None
     print(json.dumps(out), flush=True)
     r.close()
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

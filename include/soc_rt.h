@@ -420,6 +420,11 @@ int soc_renderer_reset_timing(soc_renderer* r);
 /* Sum of the pass's durations (ms) over the frames recorded since the last reset (at most the last
  * SOC_RENDERER_TIMING_RING) and their count. Needs a completed stream. */
 int soc_renderer_pass_stats(soc_renderer* r, int32_t index, float* total_ms, int32_t* frames);
+/* The recorded frames' start / end event times of the pass (ms after the caller's hipEvent `base`, recorded on the same
+ * device before them), oldest first; at most n entries; returns the count written or < 0. Needs a completed stream.
+ * For checking the pass events against a kernel trace of the same run (tools/event_trace_check.py). */
+int32_t soc_renderer_pass_event_times(soc_renderer* r, int32_t index, void* base, float* start_ms, float* end_ms,
+                                      int32_t n);
 /* Index (0/1) of the history_color slot holding this frame's TAA result (= tone-map input). */
 int32_t soc_renderer_current_history(const soc_renderer* r);
 /* Restore that index when resuming from a checkpoint of the temporal state (SURVEY.md §5 "Checkpoint / resume"; the
@@ -536,9 +541,10 @@ typedef struct soc_material {
     soc_img normal_image;              /* RGBA8_UNORM tangent-space normal texture, with SOC_MATERIAL_NORMAL_TEXTURE */
     float max_anisotropy;              /* with SOC_MATERIAL_MIPMAPPED: 16 in the reference (texture.cpp:129-130) */
     int32_t pad2;
-    /* optional, with SOC_MATERIAL_MIPMAPPED and a normal_image of the albedo's extent: the two mip chains interleaved
-     * texel by texel (soc_pair_textures), which the G-buffer resolve then reads with one load per texel row pair for
-     * both textures (the same texels and results); NULL: the two images are read separately */
+    /* optional, read only with SOC_MATERIAL_PAIRED_TEXELS set (with SOC_MATERIAL_MIPMAPPED and a normal_image of the
+     * albedo's extent): the two mip chains interleaved texel by texel (soc_pair_textures), which the G-buffer resolve
+     * then reads with one load per texel row pair for both textures (the same texels and results); without the flag
+     * the two images are read separately. The field took bytes that were padding before: zero-initialise the struct. */
     void* paired_texels;
 } soc_material;
 #define SOC_MATERIAL_ZERO_VELOCITY 1   /* write velocity 0 (the terrain draw, draw_terrain.inl:221) */
@@ -557,6 +563,9 @@ typedef struct soc_material {
  * derivative of the longer axis (EXT_texture_filter_anisotropic's reference filter; N = 1 samples uv itself);
  * trilinear = lerp of the bilinear REPEAT samples of levels floor(lod) and floor(lod) + 1. */
 #define SOC_MATERIAL_MIPMAPPED 8
+/* paired_texels holds the soc_pair_textures buffer of this material's albedo + normal_image (explicit opt-in: a caller
+ * that fills the struct field by field without zeroing it never has stale padding read as a pointer) */
+#define SOC_MATERIAL_PAIRED_TEXELS 16
 
 #define SOC_CULL_NONE 0
 #define SOC_CULL_FRONT 1               /* depth prepass / G-buffer (depth_prepass.inl:45) */

@@ -26,6 +26,7 @@ _FUNCS = {
     "soc_oracle_bloom_upsample": (C.c_int, [_G, _IMG, _IMG]),
     "soc_oracle_ssao_generation": (C.c_int, [_G, _IMG, _IMG, _IMG]),
     "soc_oracle_ssao_generation_rv": (C.c_int, [_G, _IMG, _IMG, C.c_void_p, _IMG]),
+    "soc_oracle_ssao_random_vectors": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_void_p]),
     "soc_oracle_ssao_blur": (C.c_int, [_G, _IMG, _IMG]),
     "soc_oracle_cloud_rendering": (C.c_int, [_G, _IMG, _IMG, _IMG]),
     "soc_oracle_composition": (C.c_int, [_G] + [_IMG] * 8),
@@ -107,6 +108,13 @@ def ssao_generation_rv(g, depth, normal, rv_table, target):
     assert t.size == 2 * target.shape[0] * target.shape[1]
     _rc(lib().soc_oracle_ssao_generation_rv(C.byref(g), _img(depth), _img(normal), t.ctypes.data, _img(target)),
         "ssao_generation_rv")
+
+
+def ssao_random_vectors(normal_width, tw, th):
+    """The oracle's (th, tw, 2) float32 SSAO random vectors (ssao_generation.inl:184-188, the Q8 hash)."""
+    out = np.zeros((th, tw, 2), np.float32)
+    _rc(lib().soc_oracle_ssao_random_vectors(int(normal_width), int(tw), int(th), out.ctypes.data), "ssao_random_vectors")
+    return out
 
 
 def ssao_blur(g, ssao, target):

@@ -503,6 +503,24 @@ int soc_oracle_ssao_generation_rv(const soc_globals* g, soc_img depth, soc_img n
     return ssao_generation(g, depth, normal, target, rv_table);
 }
 
+/* The oracle's per-pixel random vectors (x, y) of a (tw x th) SSAO target (the :184-188 expression above, uv at the
+   target's pixel centres, noise frequency from the normal image's width), for comparing with a GPU table (Q8). */
+int soc_oracle_ssao_random_vectors(int32_t normal_width, int32_t tw, int32_t th, float* out) {
+    if (normal_width <= 0 || tw <= 0 || th <= 0 || !out) return SOC_E_INVALID_ARG;
+#pragma omp parallel for schedule(static)
+    for (int y = 0; y < th; ++y)
+        for (int x = 0; x < tw; ++x) {
+            const v2 uv = V2(((float)x + 0.5f) / (float)tw, ((float)y + 0.5f) / (float)th);
+            float n1 = ssao_noise(uv, (float)(normal_width * 2));
+            v2 puv = V2(powf(uv.x, 1.1f), powf(uv.y, 1.1f));
+            float n2 = ssao_noise(puv, powf((float)normal_width * 4.2f, 1.5f + uv.x / 10.0f));
+            v3 rv = normalize3(V3(n1, n2, 0.0f));
+            out[2 * ((size_t)y * (size_t)tw + (size_t)x)] = rv.x;
+            out[2 * ((size_t)y * (size_t)tw + (size_t)x) + 1] = rv.y;
+        }
+    return SOC_OK;
+}
+
 int soc_oracle_ssao_blur(const soc_globals* g, soc_img ssao, soc_img target) {
     (void)g;
     if (!valid(&ssao) || !valid(&target) || ssao.format != SOC_FMT_R8_UNORM || target.format != SOC_FMT_R8_UNORM)

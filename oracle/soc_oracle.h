@@ -29,6 +29,7 @@ int soc_oracle_ssao_generation(const soc_globals* g, soc_img depth, soc_img norm
    arithmetic from the Q8 hash's sinf precision in the parity checks. */
 int soc_oracle_ssao_generation_rv(const soc_globals* g, soc_img depth, soc_img normal, const float* rv_table,
                                   soc_img target);
+int soc_oracle_ssao_random_vectors(int32_t normal_width, int32_t tw, int32_t th, float* out);
 int soc_oracle_ssao_blur(const soc_globals* g, soc_img ssao, soc_img target);
 int soc_oracle_cloud_rendering(const soc_globals* g, soc_img depth, soc_img noise, soc_img target);
 int soc_oracle_composition(const soc_globals* g, soc_img target, soc_img albedo, soc_img emissive,

@@ -447,6 +447,15 @@ class Renderer:
             out.append((n, gname, (tot.value / cnt.value) if cnt.value else float("nan"), cnt.value))
         return out
 
+    def pass_event_times(self, index: int, base_event, n: int = 256):
+        """(start_ms, end_ms) arrays of the pass's recorded frames, oldest first, in ms after `base_event` (a recorded
+        torch.cuda.Event of the same device; stream must be idle)."""
+        s0, s1 = (C.c_float * n)(), (C.c_float * n)()
+        m = int(lib().soc_renderer_pass_event_times(self.handle, index, C.c_void_p(base_event.cuda_event), s0, s1, n))
+        if m < 0:
+            _check(m, "soc_renderer_pass_event_times")
+        return np.array(s0[:m], np.float64), np.array(s1[:m], np.float64)
+
     def add_pass(self, name: str, fn, reads=(), writes=(), phase: int = PHASE_PRE_EXPOSURE, group: str = "",
                  before: Optional[str] = None, async_compute: bool = False) -> None:
         """Register a caller pass (soc_renderer_add_pass): `fn(globals_ptr, frame_images_ptr, stream_handle)` records

@@ -171,6 +171,7 @@ MATERIAL_ZERO_VELOCITY = 1
 MATERIAL_NORMAL_MAP = 2
 MATERIAL_NORMAL_TEXTURE = 4
 MATERIAL_MIPMAPPED = 8
+MATERIAL_PAIRED_TEXELS = 16
 
 STRUCTS = {"soc_img": SocImg, "soc_globals": Globals, "soc_sun_info": SunInfo, "soc_point_light": PointLight,
            "soc_spot_light": SpotLight, "soc_auto_exposure": AutoExposure, "soc_camera": Camera,
@@ -237,6 +238,8 @@ FUNCTIONS = {
     "soc_renderer_set_pass_timing": (_I, [_P, C.c_int32, C.c_int32]),
     "soc_renderer_reset_timing": (_I, [_P]),
     "soc_renderer_pass_stats": (_I, [_P, C.c_int32, C.POINTER(C.c_float), C.POINTER(C.c_int32)]),
+    "soc_renderer_pass_event_times": (C.c_int32, [_P, C.c_int32, _P, C.POINTER(C.c_float), C.POINTER(C.c_float),
+                                                  C.c_int32]),
     "soc_raster_workspace_size": (C.c_size_t, [C.c_int32, C.c_int32]),
     "soc_paired_texels_bytes": (C.c_size_t, [C.c_int32, C.c_int32]),
     "soc_renderer_set_raster_scene": (_I, [_P, C.POINTER(RasterScene)]),

@@ -1323,6 +1323,13 @@ extern "C" int soc_renderer_execute(soc_renderer* r, const soc_globals* g, int32
     return SOC_OK;
 }
 
+// The sun shadow draw's own workspace (SOC_RENDERER_SHADOW_LANE). Tuning knob SOC_TEST_FAIL_SHADOW_WS=1 injects the
+// allocation failure for the tests (a real hipMalloc that fails, so HIP's last error is set as by a true OOM).
+static hipError_t shadow_ws_alloc(void** p, size_t n) {
+    if (tuning_knob("SOC_TEST_FAIL_SHADOW_WS", 0)) return hipMalloc(p, (size_t)1 << 62);
+    return hipMalloc(p, n);
+}
+
 extern "C" int soc_renderer_set_raster_scene(soc_renderer* r, const soc_raster_scene* scene) {
     if (!r) return set_error(SOC_E_INVALID_ARG, "soc_renderer_set_raster_scene: null renderer");
     if (scene) {
@@ -1338,8 +1345,14 @@ extern "C" int soc_renderer_set_raster_scene(soc_renderer* r, const soc_raster_s
             if (r->shadow_ws) (void)hipFree(r->shadow_ws);
             r->shadow_ws = nullptr;
             r->shadow_ws_bytes = 0;
-            if (hipMalloc(&r->shadow_ws, need) != hipSuccess) r->shadow_ws = nullptr;   // then the shared workspace
-            else r->shadow_ws_bytes = need;
+            // on failure: the shared workspace; clear HIP's sticky last error so the next pass's check_launch() does
+            // not report this allocation's out-of-memory as a launch failure
+            if (shadow_ws_alloc(&r->shadow_ws, need) != hipSuccess) {
+                r->shadow_ws = nullptr;
+                (void)hipGetLastError();
+            } else {
+                r->shadow_ws_bytes = need;
+            }
         }
     }
     r->has_scene = scene != nullptr;
@@ -1524,6 +1537,22 @@ extern "C" int soc_renderer_pass_stats(soc_renderer* r, int32_t i, float* total_
     *total_ms = (float)sum;
     *frames = p.count;
     return SOC_OK;
+}
+
+extern "C" int32_t soc_renderer_pass_event_times(soc_renderer* r, int32_t i, void* base, float* start_ms, float* end_ms,
+                                                 int32_t n) {
+    if (!r || i < 0 || i >= (int32_t)r->passes.size() || !base || !start_ms || !end_ms || n < 0)
+        return set_error(SOC_E_INVALID_ARG, "soc_renderer_pass_event_times: bad arguments");
+    auto& p = r->passes[i];
+    const int first = p.count < SOC_RENDERER_TIMING_RING ? 0 : p.next;   // the oldest recorded slot
+    const int m = std::min(p.count, n);
+    for (int k = 0; k < m; ++k) {
+        const int slot = (first + (p.count - m) + k) % SOC_RENDERER_TIMING_RING;
+        hipError_t e = hipEventElapsedTime(&start_ms[k], (hipEvent_t)base, p.ev0[slot]);
+        if (e == hipSuccess) e = hipEventElapsedTime(&end_ms[k], (hipEvent_t)base, p.ev1[slot]);
+        if (e != hipSuccess) return set_error(SOC_E_HIP, "soc_renderer_pass_event_times: %s", hipGetErrorString(e));
+    }
+    return m;
 }
 
 extern "C" int32_t soc_renderer_current_history(const soc_renderer* r) { return r ? r->hist : -1; }

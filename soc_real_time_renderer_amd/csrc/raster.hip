@@ -910,7 +910,7 @@ __global__ __launch_bounds__(kWorkgroup) __attribute__((amdgpu_waves_per_eu(SOC_
     const bool pair = tbn && mipped && p.tex_pairs && m.albedo.data && m.albedo.width == m.normal_image.width &&
                       m.albedo.height == m.normal_image.height;
     f4 t_pair{0.0f, 0.0f, 0.0f, 0.0f}, al_pair = t_pair;
-    if (pair && m.paired_texels && p.paired)
+    if (pair && (m.flags & SOC_MATERIAL_PAIRED_TEXELS) && m.paired_texels && p.paired)
         sample_texture_mip2p(m.normal_image, m.albedo, m.paired_texels, u, v, gr, m.max_anisotropy, lut, t_pair, al_pair);
     else if (pair)
         sample_texture_mip2(m.normal_image, m.albedo, u, v, gr, m.max_anisotropy, lut, t_pair, al_pair);

@@ -27,13 +27,38 @@ def env() -> Tuple[int, int, int]:
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
-def init(device: Optional[torch.device] = None, backend: str = "nccl") -> None:
+# exchange even without peers (init(force_exchange=True)): a world-size-1 group still runs the real collective, so
+# the PRE -> all-reduce -> POST path (RCCL on the AutoExposure bins) is exercised on a 1-GPU box
+_FORCE_EXCHANGE = False
+
+
+def init(device: Optional[torch.device] = None, backend: str = "nccl", force_exchange: bool = False) -> None:
+    """Join the process group (torch.distributed.run environment). Without peers nothing is initialised unless
+    `force_exchange`: then a world-size-1 group is created and every frame takes the exchange path."""
+    global _FORCE_EXCHANGE
     _, world, _ = env()
-    if world > 1 and not dist.is_initialized():
+    _FORCE_EXCHANGE = bool(force_exchange)
+    if (world > 1 or force_exchange) and not dist.is_initialized():
+        if world == 1:   # no launcher: a one-rank rendezvous on the loopback address
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
+            os.environ.setdefault("LOCAL_RANK", "0")
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            if "MASTER_PORT" not in os.environ:
+                import socket
+                s = socket.socket()
+                s.bind(("127.0.0.1", 0))
+                os.environ["MASTER_PORT"] = str(s.getsockname()[1])
+                s.close()
         if backend == "nccl":
             dist.init_process_group(backend, device_id=device)
         else:
             dist.init_process_group(backend)
+
+
+def exchange_active(group=None) -> bool:
+    """True when frames take PRE -> histogram all-reduce -> POST (peers, or a forced world-size-1 group)."""
+    return dist.is_initialized() and (dist.get_world_size(group) > 1 or _FORCE_EXCHANGE)
 
 
 def camera_for_rank(rank: int):
@@ -62,7 +87,7 @@ def exposure_pixels(world: int, width: int, height: int) -> Tuple[int, bool]:
 
 def exchange_histogram(bins: torch.Tensor, group=None) -> None:
     """Sum the per-rank 256-bin histograms in place (u32 bins viewed as int32: two's-complement wrap)."""
-    if dist.is_initialized() and dist.get_world_size(group) > 1:
+    if exchange_active(group):
         dist.all_reduce(bins, op=dist.ReduceOp.SUM, group=group)
 
 
@@ -79,7 +104,7 @@ def render_frame(renderer, g, bins: torch.Tensor, group=None, exchange_events=No
     Without peers the frame is one call (the resolve then folds the fused pass's partial histograms).
     `exchange_events` = (start, end) CUDA events recorded on the current stream around the exchange."""
     from . import PHASE_ALL, PHASE_POST_EXPOSURE, PHASE_PRE_EXPOSURE
-    if not (dist.is_initialized() and dist.get_world_size(group) > 1):
+    if not exchange_active(group):
         renderer.execute(g, PHASE_ALL)
         return
     renderer.execute(g, PHASE_PRE_EXPOSURE)

@@ -17,7 +17,8 @@ import torch
 
 from . import _abi, _check, _gp, _ptr, _stream, img, lib
 from ._abi import (CULL_BACK, CULL_FRONT, CULL_NONE, FMT_RGBA8_SRGB, FMT_RGBA8_UNORM, MATERIAL_MIPMAPPED,
-                   MATERIAL_NORMAL_MAP, MATERIAL_NORMAL_TEXTURE, MATERIAL_ZERO_VELOCITY, Material, Mesh, SocImg)
+                   MATERIAL_NORMAL_MAP, MATERIAL_NORMAL_TEXTURE, MATERIAL_PAIRED_TEXELS, MATERIAL_ZERO_VELOCITY, Material, Mesh,
+                   SocImg)
 
 __all__ = ["CULL_NONE", "CULL_FRONT", "CULL_BACK", "MATERIAL_ZERO_VELOCITY", "MeshBuffers", "MipTexture", "material",
            "normal_matrix", "materials_device", "raster_visibility", "raster_depth", "gbuffer_resolve",
@@ -161,20 +162,33 @@ def material(albedo=None, emissive=None, albedo_factor=(1.0, 1.0, 1.0, 1.0), emi
     if normal_texture is not None:
         m.flags |= MATERIAL_NORMAL_TEXTURE
     if (mipped and albedo is not None and normal_texture is not None and isinstance(albedo.buf, torch.Tensor)
-            and albedo.buf.is_cuda and (albedo.width, albedo.height) == (normal_texture.width, normal_texture.height)):
+            and isinstance(normal_texture.buf, torch.Tensor) and albedo.buf.is_cuda and normal_texture.buf.is_cuda
+            and albedo.buf.device == normal_texture.buf.device
+            and (albedo.width, albedo.height) == (normal_texture.width, normal_texture.height)):
         m.paired_texels = paired_texels(albedo, normal_texture)
+        m.flags |= MATERIAL_PAIRED_TEXELS
     return m
 
 
 def paired_texels(albedo: MipTexture, normal_texture: MipTexture, stream=None) -> int:
     """soc_pair_textures: the two device mip chains interleaved texel by texel (the G-buffer resolve then reads both
-    textures of a tap row with one load). The buffer lives as long as the normal texture (kept on it); returns its
-    device address for soc_material.paired_texels."""
+    textures of a tap row with one load). Returns its device address for soc_material.paired_texels (with
+    SOC_MATERIAL_PAIRED_TEXELS). The buffer is kept on the normal texture, one per albedo it was paired with (the entry
+    also holds the albedo, so its id is not reused): a normal texture shared by several materials, or a material built
+    twice, never frees a buffer a live material points at, and the same pair is interleaved once."""
+    if normal_texture.buf.device != albedo.buf.device:
+        raise ValueError("paired_texels: albedo and normal texture on different devices")
+    cache = getattr(normal_texture, "paired", None)
+    if not isinstance(cache, dict):
+        cache = normal_texture.paired = {}
+    hit = cache.get(id(albedo))
+    if hit is not None and hit[0] is albedo:
+        return hit[1].data_ptr()
     n = int(lib().soc_paired_texels_bytes(albedo.width, albedo.height))
     buf = torch.empty(n, dtype=torch.uint8, device=albedo.buf.device)
     _check(lib().soc_pair_textures(albedo.img(), normal_texture.img(), C.c_void_p(buf.data_ptr()), _stream(stream)),
            "pair_textures")
-    normal_texture.paired = buf
+    cache[id(albedo)] = (albedo, buf)
     return buf.data_ptr()
 
 

@@ -8,7 +8,8 @@ renderer.cpp:1155-1168), then POST_EXPOSURE with the wide resolve over N*W*H pix
 every rank saw to $SOC_DIST_OUT (npz) for the test to check against the oracle.
 
 SOC_BENCH_SHARE_DEVICE=1 puts all ranks on device 0 and the backend is gloo (RCCL refuses two ranks on
-one device), so the test runs on a 1-GPU box.
+one device), so the test runs on a 1-GPU box. With one rank, SOC_DIST_BACKEND=nccl and SOC_DIST_FORCE=1 the frames
+take the same path through a world-size-1 RCCL group: the all-reduce runs on the AutoExposure bins on the device.
 
 SOC_DIST_CONFIG=c3 runs config C5 at its own size instead: every rank renders
 bench.build_inputs("c3", "mesh", 3840, 2160, rank) -- its own camera of the Sponza-proxy mesh, rasterised by the HIP
@@ -37,7 +38,9 @@ def main():
     dev_index = 0 if os.environ.get("SOC_BENCH_SHARE_DEVICE") == "1" else local_rank
     torch.cuda.set_device(dev_index)
     device = torch.device("cuda", dev_index)
-    multi_gpu.init(device, backend=os.environ.get("SOC_DIST_BACKEND", "gloo"))
+    # SOC_DIST_FORCE=1: the exchange path even at world size 1 (a one-rank RCCL group on a 1-GPU box)
+    multi_gpu.init(device, backend=os.environ.get("SOC_DIST_BACKEND", "gloo"),
+                   force_exchange=os.environ.get("SOC_DIST_FORCE") == "1")
     c5 = os.environ.get("SOC_DIST_CONFIG", "") == "c3"
     if c5:
         import bench
@@ -58,11 +61,21 @@ def main():
     r.set_exposure_pixels(*multi_gpu.exposure_pixels(world, w, h))
     bins = fr["auto_exposure"][1:]
     rec = {"local": [], "reduced": [], "exposure": [], "color": [], "local_ok": [], "sky": []}
+    # no host synchronisation between the phases: the bins and the colour are snapshotted on the frame stream, so
+    # the exchange is checked in stream order against the renderer's lanes (the all-reduce is issued on the caller's
+    # stream the renderer's main lane runs on)
     for _ in range(FRAMES):
         r.execute(g, soc.PHASE_PRE_EXPOSURE)
+        local = bins.clone()
+        color_d = fr["color"].clone()
+        multi_gpu.exchange_histogram(bins)
+        reduced = bins.clone()
+        r.execute(g, soc.PHASE_POST_EXPOSURE)
         torch.cuda.synchronize()
-        rec["local"].append(bins.cpu().numpy().view(np.uint32).copy())
-        color = fr["color"].cpu().numpy()
+        rec["local"].append(local.cpu().numpy().view(np.uint32).copy())
+        rec["reduced"].append(reduced.cpu().numpy().view(np.uint32).copy())
+        color = color_d.cpu().numpy()
+        del color_d
         if c5:   # the oracle histogram of this rank's own GPU colour, here (a 4K colour image per rank and frame)
             ref = soc.AutoExposure()
             oracle.generate_luminance_histogram(g, color, ref)
@@ -70,11 +83,6 @@ def main():
             rec["sky"].append(float((fr["depth"] == 1.0).float().mean()))
         else:
             rec["color"].append(color.copy())
-        multi_gpu.exchange_histogram(bins)
-        torch.cuda.synchronize()
-        rec["reduced"].append(bins.cpu().numpy().view(np.uint32).copy())
-        r.execute(g, soc.PHASE_POST_EXPOSURE)
-        torch.cuda.synchronize()
         rec["exposure"].append(soc.exposure_of(fr["auto_exposure"]))
         # the resolve clears the bins for the next frame (resolve_luminance_histogram.inl:63)
         assert int(bins.abs().sum()) == 0

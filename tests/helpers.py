@@ -93,8 +93,10 @@ PARITY_REPORTS = []
 #   SSAO given the GPU's random-vector table (the Q8 hash isolated): within 2 levels on >= 99.5 %, at most
 #   SSAO_COND_FLIPS tap flips anywhere.
 # * Passes whose inputs are the G-buffer, against the oracle's own: SSAO R8 within 2 levels on >= 99.5 %, mean
-#   <= 0.5 levels, at most SSAO_FLIPS tap flips anywhere (one tap's range test changing side moves a pixel by its
-#   range x 255 / 26 <= 9.8 levels); clouds RGBA8 within 2 levels on >= 99.5 % of the pixels.
+#   <= 0.5 levels, at most SSAO_FLIPS tap flips (one tap's range test changing side moves a pixel by its
+#   range x 255 / 26 <= 9.8 levels) on every pixel whose random vector equals the oracle's bit for bit (where the Q8
+#   hash differs the tap pattern rotates and only the statistical bound applies); clouds RGBA8 within 2 levels on >= 99.5 % of the sky pixels, within 16 levels on
+#   >= 99.99 % and at most CLOUDS_MAX levels anywhere.
 # * End to end (the oracle's frame from the same G-buffer): colour within 1e-3 + 2e-3|ref| on every pixel whose
 #   upstream inputs (the 2x2 AO texels it samples, and for a sky pixel its clouds texel) equal the oracle's, and on
 #   every pixel within that tolerance plus the difference the oracle itself propagates from the GPU's AO and clouds
@@ -103,6 +105,7 @@ PARITY_REPORTS = []
 SSAO_STEP = 255.0 / 26.0
 SSAO_FLIPS = 4
 SSAO_COND_FLIPS = 2
+CLOUDS_MAX = 96        # RGBA8 levels: hard maximum of a clouds texel against the oracle's (measured worst 69, C4)
 
 
 def _levels(d):
@@ -138,7 +141,8 @@ def ao_footprint(diff_half, W, H):
     return (d[np.ix_(y0, x0)] | d[np.ix_(y0, x1)] | d[np.ix_(y1, x0)] | d[np.ix_(y1, x1)])
 
 
-def frame_parity(soc, oracle, g, fr, hf, ae_ref, q, label, exposure_before, total_pixels=0, wide=False, check=True):
+def frame_parity(soc, oracle, g, fr, hf, ae_ref, q, label, exposure_before, total_pixels=0, wide=False, check=True,
+                 masks=None):
     """Full-frame parity of one executed render-graph frame `fr` (device images, synchronised) against the oracle
     frame `hf` of the same inputs (oracle.frame already run; `ae_ref` its AutoExposure, `q` the history slot both wrote,
     `exposure_before` the GPU's exposure before the frame). Records the achieved errors in PARITY_REPORTS and,
@@ -161,15 +165,23 @@ def frame_parity(soc, oracle, g, fr, hf, ae_ref, q, label, exposure_before, tota
                    "levels": _levels(d_ao)}
     if fr.get("ssao_noise_table") is not None:
         sc = np.zeros_like(ssao)
-        oracle.ssao_generation_rv(g, hf["depth"], hf["normal"], cpu(fr["ssao_noise_table"]), sc)
+        table = cpu(fr["ssao_noise_table"]).reshape(ssao.shape[0], ssao.shape[1], 2)
+        oracle.ssao_generation_rv(g, hf["depth"], hf["normal"], table, sc)
         d_sc = np.abs(ssao.astype(np.int32) - sc.astype(np.int32))
         rep["ssao_cond"] = {"within2": float((d_sc <= 2).mean()), "max": int(d_sc.max()), "levels": _levels(d_sc),
                             "worst": _worst(d_sc, gpu=ssao, oracle=sc)}
+        # Q8: pixels whose GPU random vector (accurate sinf on the GPU) is not bit-equal to the oracle's (libm sinf of
+        # arguments up to ~1e5): there the whole tap pattern rotates, so only the statistical bound applies
+        rv = oracle.ssao_random_vectors(hf["normal"].shape[1], ssao.shape[1], ssao.shape[0])
+        hash_differs = (table.view(np.uint32) != rv.view(np.uint32)).any(axis=-1)
+        rep["ssao"]["hash_differs"] = float(hash_differs.mean())
+        rep["ssao"]["max_where_hash_equal"] = int(d_ao[~hash_differs].max()) if (~hash_differs).any() else 0
     d_bl = np.abs(blur.astype(np.int32) - hf["ssao_blur"].astype(np.int32))
     rep["ssao_blur_e2e_max"] = int(d_bl.max())
     # --- clouds against the oracle's
     d_cl = np.abs(clouds.astype(np.int32) - hf["clouds"].astype(np.int32)).max(axis=-1)
-    rep["clouds"] = {"within2": float((d_cl[sky] <= 2).mean()) if sky.any() else 1.0, "max": int(d_cl.max()),
+    rep["clouds"] = {"within2": float((d_cl[sky] <= 2).mean()) if sky.any() else 1.0,
+                     "within16": float((d_cl[sky] <= 16).mean()) if sky.any() else 1.0, "max": int(d_cl.max()),
                      "levels": _levels(d_cl[sky]) if sky.any() else {},
                      "worst": _worst(d_cl, gpu=clouds[..., :3], oracle=hf["clouds"][..., :3])}
 
@@ -201,6 +213,9 @@ def frame_parity(soc, oracle, g, fr, hf, ae_ref, q, label, exposure_before, tota
     u = tol_units(color, hf["color"]).max(axis=-1)
     upstream = ao_footprint(d_bl > 0, W, H) & ~sky
     upstream |= sky & (d_cl > 0)
+    if masks is not None:   # for callers that bound a later stage where its inputs equal the oracle's
+        masks["upstream"] = upstream
+        masks["sky"] = sky
     strict = u <= 1
     prop = np.abs(cc.astype(np.float32) - hf["color"].astype(np.float32))
     with np.errstate(invalid="ignore"):
@@ -230,8 +245,11 @@ def frame_parity(soc, oracle, g, fr, hf, ae_ref, q, label, exposure_before, tota
         sc_ = rep["ssao_cond"]
         assert sc_["within2"] >= 0.995 and sc_["max"] <= 2 + SSAO_COND_FLIPS * SSAO_STEP, rep
     assert rep["ssao"]["within2"] >= 0.995 and rep["ssao"]["mean"] <= 0.5, rep
-    assert rep["ssao"]["max"] <= 2 + SSAO_FLIPS * SSAO_STEP, rep
+    assert rep["ssao"].get("max_where_hash_equal", rep["ssao"]["max"]) <= 2 + SSAO_FLIPS * SSAO_STEP, rep
     assert rep["clouds"]["within2"] >= 0.995, rep
+    # the tail of the clouds differences is bounded too: the largest measured were 69 / 38 levels on two C4
+    # pixels (a steep transmittance amplifying 1-ulp exp2 / sqrt differences), 16+ on 3e-5 of them
+    assert rep["clouds"]["within16"] >= 0.9999 and rep["clouds"]["max"] <= CLOUDS_MAX, rep
     assert c["strict_where_upstream_equal"] == 1.0 and c["over_budget"] == 0, rep
     assert sum(n for k, n in rep["framebuffer_levels"].items() if k <= 1) >= 0.999 * out.size, rep
     assert rep["exposure_delta"] <= 1e-5, rep

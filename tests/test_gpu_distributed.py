@@ -38,19 +38,22 @@ def _port():
 
 def _env(**kw):
     env = dict(os.environ)
-    env.update(SOC_BENCH_SHARE_DEVICE="1", SOC_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0",
-               OMP_NUM_THREADS="2", **kw)
+    env.update({"SOC_BENCH_SHARE_DEVICE": "1", "SOC_DIST_BACKEND": "gloo", "HSA_ENABLE_IPC_MODE_LEGACY": "0",
+                "OMP_NUM_THREADS": "2", **kw})
     return env
 
 
-@pytest.mark.parametrize("ranks", [2, 8])
-def test_rank_frames_exchange_vs_oracle(tmp_path, soc, oracle, ranks):
+@pytest.mark.parametrize("ranks,backend", [(1, "nccl"), (2, "gloo"), (8, "gloo")])
+def test_rank_frames_exchange_vs_oracle(tmp_path, soc, oracle, ranks, backend):
+    """(1, nccl): the real collective (RCCL) at world size 1 -- PRE -> dist.all_reduce on the device AutoExposure bins ->
+    POST, the renderer's second (sky) lane on -- on the 1-GPU box; the multi-rank cases share device 0 over gloo."""
     from helpers import globals_for
     from soc_real_time_renderer_amd import multi_gpu
     out = tmp_path / "dist.npz"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
            "--master-addr", "127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "tests", "dist_frame_worker.py")]
-    p = subprocess.run(cmd, env=_env(SOC_DIST_OUT=str(out)), capture_output=True, text=True, timeout=240)
+    extra = dict(SOC_DIST_BACKEND="nccl", SOC_DIST_FORCE="1", SOC_BENCH_SHARE_DEVICE="0") if backend == "nccl" else {}
+    p = subprocess.run(cmd, env=_env(SOC_DIST_OUT=str(out), **extra), capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     d = np.load(out)
     world, W, H = int(d["world"]), int(d["W"]), int(d["H"])
@@ -112,6 +115,23 @@ def test_c5_4k_exchange_vs_oracle(tmp_path, soc, oracle):
             assert abs(float(exposure[r, f]) - ae.exposure) <= 1e-5, (r, f, float(exposure[r, f]), ae.exposure)
     for r in range(1, world):
         assert not np.array_equal(local[0, 0], local[r, 0]), r
+
+
+def test_bench_exchange_rccl_world1():
+    """bench.py --exchange at N = 1: the frames take PRE -> RCCL all-reduce (a world-size-1 group) -> POST and the line
+    carries the backend and the all-reduce time per frame (SURVEY.md §8e's report)."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--exchange", "--steps", "20", "--warmup", "5",
+           "--width", "640", "--height", "360", "--no-cpu-baseline", "--profile-frames", "2"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 1
+    assert out["config"]["histogram_allreduce"] is True
+    assert out["config"]["collective_backend"] == "nccl"
+    assert out["allreduce_us_per_frame"] is not None and out["allreduce_us_per_frame"] > 0
 
 
 def test_bench_gpus2_self_launch():

@@ -606,6 +606,49 @@ def test_clouds_sky_table_against_every_pixel(soc, monkeypatch, config):
     assert frac <= 0.02, frac
 
 
+@pytest.mark.parametrize("cam_y", [2.2, 900.0])
+def test_clouds_tables_sun_sweep(soc, monkeypatch, cam_y):
+    """the two per-frame atmosphere tables (clouds.hip clouds_od_lut, clouds_sky_table) away from the bench's
+    sun and camera: sun elevations from below the horizon to the zenith (the sky table's fallback axis), two azimuths,
+    camera heights 2.2 and 900, an all-sky 960x540 frame looking at the horizon and up. Sky-view table on vs every
+    pixel evaluated (SOC_CLOUDS_SKY_TABLE), and the secondary-ray table vs every secondary ray marched
+    (SOC_CLOUDS_OD_LUT, sky table off): at most one RGBA8 level anywhere (cloud_rendering.inl:353-439)."""
+    W, H = 960, 540
+    worst = {}
+    for pitch in (0.0, 0.7):
+        g, gb = sponza_inputs(W, H, camera=((-14.0, cam_y, 0.3), (0.0, pitch, 0.0)), elapsed=10.0)
+        depth = dev(np.ones_like(gb["depth"]))
+        noise = dev(gb["noise"])
+        ws = soc.cloud_rendering_workspace(W, H)
+        for elev in (-8.0, 3.0, 35.0, 90.0):
+            for az in (0.0, 2.4):
+                e, a_ = np.radians(elev), az
+                d = -np.array([np.cos(e) * np.cos(a_), np.sin(e), np.cos(e) * np.sin(a_)], np.float32)
+                if elev == 90.0:
+                    d = np.array([0.0, -1.0, 0.0], np.float32)
+                g.sun_info.direction[:] = [float(v) for v in d]
+                for knob, other in (("SOC_CLOUDS_SKY_TABLE", {}), ("SOC_CLOUDS_OD_LUT", {"SOC_CLOUDS_SKY_TABLE": "0"})):
+                    outs = []
+                    for v in ("1", "0"):
+                        for k, vv in other.items():
+                            monkeypatch.setenv(k, vv)
+                        monkeypatch.setenv(knob, v)
+                        soc.reload_tuning()
+                        o = torch.zeros(H, W, 4, dtype=torch.uint8, device=DEV)
+                        soc.cloud_rendering(g, depth, noise, o, ws)
+                        outs.append(o)
+                    for k in list(other) + [knob]:
+                        monkeypatch.delenv(k)
+                    torch.cuda.synchronize()
+                    diff = (outs[0].int() - outs[1].int()).abs().amax(dim=-1)
+                    key = (knob, pitch, elev, az)
+                    worst[key] = (int(diff.max()), float((diff > 0).float().mean()))
+    soc.reload_tuning()
+    print("clouds tables sun sweep (max levels, fraction differing):", worst)
+    bad = {k: v for k, v in worst.items() if v[0] > 1}
+    assert not bad, bad
+
+
 # ------------------------------------------------------------------------------------------------ full frame
 @pytest.mark.parametrize("W,H,frames,inputs", [(256, 144, 3, "sponza"), (1920, 1080, 2, "sponza"),
                                                (320, 180, 2, "terrain"), (960, 540, 2, "terrain"),

@@ -156,10 +156,17 @@ def test_gbuffer_resolve(soc, oracle, scene_id, camera, W, H):
         assert torch.equal(out[k], out2[k]), k
 
 
-@pytest.mark.parametrize("scene_id,camera", [(scene.SPONZA_PROXY, SPONZA_CAMERA), (scene.TERRAIN, TERRAIN_CAMERA)])
-def test_render_graph_raster_head(soc, scene_id, camera):
+@pytest.mark.parametrize("scene_id,camera,fail_ws", [(scene.SPONZA_PROXY, SPONZA_CAMERA, False),
+                                                    (scene.TERRAIN, TERRAIN_CAMERA, False),
+                                                    (scene.SPONZA_PROXY, SPONZA_CAMERA, True)])
+def test_render_graph_raster_head(soc, monkeypatch, scene_id, camera, fail_ws):
     """DepthPrepass / SunShadowDraw / GBufferGeneration inside the render graph: 3 frames equal the same
-    frames fed with G-buffer + shadow images rasterised by the standalone calls."""
+    frames fed with G-buffer + shadow images rasterised by the standalone calls. fail_ws: the shadow draw's own
+    workspace allocation fails (injected, SOC_TEST_FAIL_SHADOW_WS): the graph falls back to the shared workspace and
+    every frame still executes (the failed hipMalloc's sticky error is not reported by the next launch check)."""
+    if fail_ws:
+        monkeypatch.setenv("SOC_TEST_FAIL_SHADOW_WS", "1")
+        soc.reload_tuning()
     W, H = 640, 360
     g = globals_for(W, H, camera=camera, elapsed=10.0)
     sc = raster.scene_setup(g, scene_id, tex_size=128)
@@ -423,6 +430,51 @@ def test_mipmapped_gbuffer_shared_footprint_bit_identical(soc, monkeypatch, tex)
     for o in outs[1:]:
         for k in outs[0]:
             assert torch.equal(outs[0][k], o[k]), k
+
+
+def test_paired_texels_shared_normal_texture(soc, monkeypatch):
+    """materials that share one normal texture (or a material built twice) each keep a live paired-texel
+    buffer (one per albedo, never overwritten), the flag SOC_MATERIAL_PAIRED_TEXELS opts the resolve in, and the
+    G-buffer of the shared-normal materials equals the one read from the separate images (SOC_GB_PAIRED=0)."""
+    W, H = 480, 270
+    g = globals_for(W, H)
+    _, dm = _mesh_scene()
+    mats0, keep = raster.sponza_mesh_materials(64, DEV, mips=True)
+    shared = next(i for i in range(len(mats0)) if keep[2 * i] is not None and keep[2 * i + 1] is not None)
+    nrm = keep[2 * shared + 1]
+    # every material takes the first textured material's normal image; the first one is built twice
+    mats, ptrs = [], []
+    for i in range(len(mats0)):
+        a = keep[2 * i]
+        if a is None or (a.width, a.height) != (nrm.width, nrm.height):
+            mats.append(mats0[i])
+            continue
+        m = raster.material(albedo=a, normal_texture=nrm)
+        if i == shared:
+            m2 = raster.material(albedo=a, normal_texture=nrm)
+            assert m2.paired_texels == m.paired_texels      # the same pair is interleaved once
+        assert m.flags & raster.MATERIAL_PAIRED_TEXELS
+        mats.append(m)
+        ptrs.append(m.paired_texels)
+    assert len(set(ptrs)) == len(ptrs) > 1                   # one live buffer per albedo
+    live = {v[1].data_ptr() for v in nrm.paired.values()}
+    assert set(ptrs) <= live
+    dmats = raster.materials_device(mats)
+    vis = torch.zeros((H, W), dtype=torch.int64, device=DEV)
+    ws = dm.workspace()
+    raster.raster_visibility(dm, np.ctypeslib.as_array(g.camera_projection_view_matrix), raster.CULL_FRONT, vis, ws)
+    outs = []
+    for paired in ("1", "0"):
+        monkeypatch.setenv("SOC_GB_PAIRED", paired)
+        soc.reload_tuning()
+        out = {k: torch.zeros((H, W, 4), dtype=torch.float16, device=DEV) for k in ("albedo", "emissive", "normal", "velocity")}
+        out["depth"] = torch.zeros((H, W), dtype=torch.float32, device=DEV)
+        raster.gbuffer_resolve(g, dm, dmats, len(mats), vis, out["depth"], out["albedo"], out["emissive"], out["normal"],
+                               out["velocity"], ws)
+        outs.append(out)
+    torch.cuda.synchronize()
+    for k in outs[0]:
+        assert torch.equal(outs[0][k], outs[1][k]), k
 
 
 @pytest.mark.parametrize("size,grid,level", [(1024, 100, 3), (128, 100, 3), (64, 17, 5), (32, 2, 1)])
