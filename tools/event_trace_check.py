@@ -6,9 +6,11 @@ Composition was shorter than the kernel's trace duration, but the two came from 
       the bench's C3 frame loop (bench.build_inputs, the bench's renderer flags) with the bench's pass events on
       Composition(+histogram) and SSAOGeneration; writes every timed frame's event times (ms after a base event
       recorded before the timed frames) to OUT.json. Run it under `rocprofv3 --kernel-trace` to get the trace.
+      (bench.py itself writes the same file for its timed frames with SOC_BENCH_EVENTS_OUT=OUT.json.)
   python tools/event_trace_check.py compare OUT.json KERNEL_TRACE.csv
-      aligns the events with the trace's launches of the same kernels (the last N launches of each) and prints, per
-      kernel, the event interval, the trace duration and where each event falls against the kernel's begin / end.
+      aligns the events with the trace's launches of the same kernels (launches warmup .. warmup + frames of each)
+      and prints, per kernel, the event interval, the trace duration and where each event falls against the kernel's
+      begin / end.
 """
 import csv
 import json
@@ -71,7 +73,7 @@ def compare(events_json, trace_csv):
     for name, key in KERNELS.items():
         e = ev["passes"][name]
         e0, e1 = np.array(e["start_ms"]) * 1e6, np.array(e["end_ms"]) * 1e6   # ns after the base event
-        tl = trace_launches(trace_csv, key)[-n:]
+        tl = trace_launches(trace_csv, key)[ev["warmup"]:ev["warmup"] + n]
         tb, te = tl[:, 0], tl[:, 1]
         offs[name] = float(np.median(te - e1))    # trace clock = event clock + offset, if end events mark kernel ends
         out["kernels"][name] = {"event_us": float((e1 - e0).mean() / 1e3), "trace_us": float((te - tb).mean() / 1e3),

@@ -1,8 +1,11 @@
-"""Agreement of the bench line's roofline durations with rocprofv3: the bench measures the north-star kernels with HIP
-events on their stream over its timed frames (lanes concurrent); this takes a `tools/gpu.sh kt` kernel trace of the
-same configuration (`bench.py --steps K --warmup W`: W warm-up frames, K timed frames, then the serial per-pass
-profile frames) and averages each kernel over its timed launches only, so both numbers describe the same kind of
-launch. The kernel trace's own `--stats` average mixes the three segments.
+"""Agreement of the bench line's roofline durations with rocprofv3. The bench measures the north-star kernels with HIP
+events on their stream twice: alone (the serial per-pass profile frames: the roofline's headline) and in its timed
+frames (lanes concurrent: `in_frame`). This takes a `tools/gpu.sh kt` kernel trace of the same command (`bench.py
+--steps K --warmup W`: W warm-up frames, K timed frames, then the serial per-pass profile frames) and averages each
+kernel over the same kind of launch: the profile frames for the headline, the timed frames for in_frame. The kernel
+trace's own `--stats` average mixes the three segments. A kernel trace changes how the two lanes overlap, so the
+in-frame pair of an untraced bench run and a traced run need not agree; within one traced run events and trace do
+(tools/event_trace_check.py, SOC_BENCH_EVENTS_OUT).
 
 usage: python tools/roofline_check.py BENCH_JSON KT_DIR [--warmup W] [--steps K] > profiles/<tag>_roofline_check.json
 (W and K default to the bench line's own, i.e. a kernel trace of the same command)
@@ -38,14 +41,19 @@ def main():
     for name, key in KERNELS.items():
         d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows if key in r["Kernel_Name"]]
         timed = d[warmup:warmup + steps]
-        ev = line["roofline"]["per_kernel"][name]["avg_launch_us"]
-        rp = sum(timed) / len(timed)
-        out["kernels"][name] = {"bench_events_us": ev, "rocprof_timed_us": round(rp, 2),
-                                "rocprof_profile_frames_us": round(sum(d[warmup + steps:]) / max(1, len(d[warmup + steps:])), 2),
-                                "ratio": round(ev / rp, 3)}
+        prof = d[warmup + steps:]
+        pk = line["roofline"]["per_kernel"][name]
+        ev = pk["avg_launch_us"]                      # alone
+        ev_frame = (pk.get("in_frame") or {}).get("avg_launch_us")
+        rp = sum(prof) / max(1, len(prof))
+        rp_frame = sum(timed) / len(timed)
+        out["kernels"][name] = {"bench_events_alone_us": ev, "rocprof_profile_frames_us": round(rp, 2),
+                                "ratio": round(ev / rp, 3),
+                                "bench_events_in_frame_us": ev_frame, "rocprof_timed_frames_us": round(rp_frame, 2),
+                                "ratio_in_frame_cross_run": round(ev_frame / rp_frame, 3) if ev_frame else None}
         pair_events += ev
         pair_rocprof += rp
-    out["pair"] = {"bench_events_us": round(pair_events, 2), "rocprof_timed_us": round(pair_rocprof, 2),
+    out["pair"] = {"bench_events_alone_us": round(pair_events, 2), "rocprof_profile_frames_us": round(pair_rocprof, 2),
                    "ratio": round(pair_events / pair_rocprof, 3)}
     json.dump(out, sys.stdout, indent=1)
     print()
