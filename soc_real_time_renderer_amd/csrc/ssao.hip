@@ -623,8 +623,8 @@ extern "C" int soc_ssao_generation(const soc_globals* g, soc_img depth, soc_img 
         SsaoParams pt = p;
         pt.swz = 1;
         const dim3 g(ceil_div(target.width, kSsaoTX), ceil_div(target.height, kSsaoTY));
-        // SOC_SSAO_PIPE (default 1): the software-pipelined tap loop (the same bits)
-        if (tuning_knob("SOC_SSAO_PIPE", 1))
+        // SOC_SSAO_PIPE=1: the software-pipelined tap loop (the same bits)
+        if (tuning_knob("SOC_SSAO_PIPE", 0))
             launch("ssao_lds_kernel", kSsaoTileLanes,
                    ssao_lds_kernel<true, true, true, kSsaoTX, kSsaoTY, kSsaoHalo, 2, true, true>, g, kSsaoTileLanes, 0, st,
                    dd, dn, dt, tb, pt);
