@@ -703,13 +703,18 @@ constexpr uint32_t kInline = 0x80000000u;   // pix_mask flag: march this pixel i
 struct PairBufs {
     uint32_t* counts;     // [kShards] pair counts (workspace counter block)
     uint32_t* pairs;      // [kShards * cap] (list index << 5) | step
-    float2* odvis;        // [kShards * cap] (od, vis)
+    float* od;            // [kShards * cap] od of each pair's step (clouds_density)
+    float* vis;           // [kShards * cap] sun visibility of each pair's step (clouds_sunvis); od and vis in two dense
+                          // arrays (round 5: one float2 array took each kernel's 4-byte writes at an 8-byte stride, so
+                          // every written line was half written)
     uint32_t* pix_mask;   // [W*H] per list entry: dense-step mask | kInline
     uint32_t* batch_base; // [W*H/256] per 256-entry batch: physical index of its first pair | kInline
     float4* geom;         // [W*H] x 2 per list entry: (start, dither), (inc, stepLength) of its march (density
-                          // writes it for upward rays; sunvis and resolve read it instead of re-deriving it)
+                          // writes it for upward rays when store_geom; sunvis and resolve read it instead of re-deriving
+                          // it; store_geom == 0: they re-derive it from the list entry, the same bits)
     float* od_tmp;        // [od_blocks][24][256]: per density workgroup, the od of its current batch's dense steps until
-                          // their pair slots are known; density then stores od in odvis[slot].x, and sunvis only adds vis
+                          // their pair slots are known; density then stores od in od[slot], and sunvis only adds vis
+    uint32_t store_geom;  // tuning knob SOC_CLOUDS_GEOM
     uint32_t od_blocks;   // density workgroups the od scratch holds (the density grid is clamped to it)
     uint32_t n;           // list capacity (W*H)
     uint32_t cap;         // pairs per shard
@@ -761,6 +766,22 @@ __device__ __forceinline__ void batch_slots(uint32_t mask, uint32_t lane, uint32
     __syncthreads();
 }
 
+// The march geometry and dither of list entry i: stored by clouds_density (store_geom), or re-derived from the entry's
+// pixel with the same functions (the same bits; a few dozen VALU against the ~1,500 of a pair's sun march, and no 32-B
+// geometry read per pair).
+__device__ __forceinline__ MarchGeom pair_geometry(const CloudParams& p, const uint32_t* __restrict__ list, const PairBufs& pb,
+                                                   uint32_t i, float& dither) {
+    if (pb.store_geom) {
+        const float4 g0 = pb.geom[2 * i], g1 = pb.geom[2 * i + 1];
+        dither = g0.w;
+        return MarchGeom{f3{g0.x, g0.y, g0.z}, f3{g1.x, g1.y, g1.z}, g1.w};
+    }
+    const uint32_t e = list[i];
+    const int x = (int)(e & 0xffffu), y = (int)(e >> 16);
+    dither = bayer16((float)x, (float)y);
+    return march_geometry(sky_dir(p, x, y));
+}
+
 template <bool NOISE_R8>
 // 6 waves/SIMD: 80 VGPRs with 20 B of scratch, measured faster than 5 waves without a spill (profiles/r04_probe_clouds_scan.txt)
 __global__ __launch_bounds__(kWorkgroup) __attribute__((amdgpu_waves_per_eu(6))) void clouds_density(
@@ -791,8 +812,10 @@ __global__ __launch_bounds__(kWorkgroup) __attribute__((amdgpu_waves_per_eu(6)))
             if (SOC_CLOUDS_PROFILE != 1 && !(dir.y < 0.0f)) {
                 const MarchGeom mg = march_geometry(dir);
                 const float dither = bayer16((float)x, (float)y);
-                pb.geom[2 * i] = float4{mg.start.x, mg.start.y, mg.start.z, dither};
-                pb.geom[2 * i + 1] = float4{mg.inc.x, mg.inc.y, mg.inc.z, mg.stepLength};
+                if (pb.store_geom) {
+                    pb.geom[2 * i] = float4{mg.start.x, mg.start.y, mg.start.z, dither};
+                    pb.geom[2 * i + 1] = float4{mg.inc.x, mg.inc.y, mg.inc.z, mg.stepLength};
+                }
                 for (int s = 0; s < 24; s++) {
                     const float od = get_clouds(cx, step_position(mg, dither, s)) * mg.stepLength;
                     if (!(od <= 0.0f)) {
@@ -832,7 +855,7 @@ __global__ __launch_bounds__(kWorkgroup) __attribute__((amdgpu_waves_per_eu(6)))
                 if ((mask >> st) & 1u) {
                     const uint32_t slot = slot_base + pair_offset(offs, st, wave, rank);
                     pb.pairs[slot] = (i << 5) | st;
-                    reinterpret_cast<float*>(pb.odvis)[2 * (size_t)slot] = od_tmp[st * 256];   // this lane's own write
+                    pb.od[slot] = od_tmp[st * 256];   // this lane's own write
                 }
             }
         }
@@ -876,12 +899,12 @@ __global__ __launch_bounds__(kSunvisThreads) __attribute__((amdgpu_waves_per_eu(
         const uint32_t pr = pb.pairs[phys];
         if (pr == 0xffffffffu) continue;   // slot of an overflowed batch
         const uint32_t i = pr >> 5, step = pr & 31u;
-        const float4 g0 = pb.geom[2 * i], g1 = pb.geom[2 * i + 1];   // the pixel's march, from clouds_density
-        const MarchGeom mg{f3{g0.x, g0.y, g0.z}, f3{g1.x, g1.y, g1.z}, g1.w};
-        const f3 cp = step_position(mg, g0.w, (int)step);
-        // od of the step is already in odvis[phys].x (clouds_density)
+        float dither;
+        const MarchGeom mg = pair_geometry(p, list, pb, i, dither);
+        const f3 cp = step_position(mg, dither, (int)step);
+        // od of the step is already in od[phys] (clouds_density)
         const float vis = SOC_CLOUDS_PROFILE == 3 ? 1.0f : sun_visibility(cx, cp, sun);
-        reinterpret_cast<float*>(pb.odvis)[2 * (size_t)phys + 1] = vis;
+        pb.vis[phys] = vis;
     }
 }
 
@@ -944,8 +967,12 @@ __global__ __launch_bounds__(kWorkgroup) __attribute__((amdgpu_waves_per_eu(5)))
             MarchGeom mg{};
             MarchShade ms{};
             if (march) {
-                const float4 g0 = pb.geom[2 * i], g1 = pb.geom[2 * i + 1];
-                mg = MarchGeom{f3{g0.x, g0.y, g0.z}, f3{g1.x, g1.y, g1.z}, g1.w};
+                if (pb.store_geom) {
+                    const float4 g0 = pb.geom[2 * i], g1 = pb.geom[2 * i + 1];
+                    mg = MarchGeom{f3{g0.x, g0.y, g0.z}, f3{g1.x, g1.y, g1.z}, g1.w};
+                } else {
+                    mg = march_geometry(dir);   // dir: this lane's own sky_dir, as clouds_density derived it
+                }
                 ms = march_shade(dir, sun, skyl);
             }
             f3 scattering = f3{0.0f, 0.0f, 0.0f};
@@ -954,8 +981,8 @@ __global__ __launch_bounds__(kWorkgroup) __attribute__((amdgpu_waves_per_eu(5)))
             for (uint32_t st = 0; any_dense && st < 24; ++st) {
                 const uint32_t rank = mask_ballot_rank(mask, st, lane);
                 if (march && ((mask >> st) & 1u)) {
-                    const float2 ov = pb.odvis[base + offs[st][wave] + rank];
-                    march_accumulate(ms, sun_color, ov.x, ov.y, scattering, transmittance);
+                    const uint32_t slot = base + offs[st][wave] + rank;
+                    march_accumulate(ms, sun_color, pb.od[slot], pb.vis[slot], scattering, transmittance);
                 }
             }
             if (march) color = march_finish(mg, color, scattering, transmittance);
@@ -987,7 +1014,7 @@ using namespace soc;
 namespace {
 // Workspace: counters (256 B: [0] sky pixels, [8..15] pair counts per shard) | sky list (u32) |
 // atmosphere (float4) | per-pixel dense mask (u32) | per-batch first pair (u32) | march geometry (2 float4) | pairs (u32) |
-// (od, vis) per pair (float2) | od scratch of the density workgroups (24 x 256 float each, at most kDensityBlocks) |
+// od per pair (float) | vis per pair (float) | od scratch of the density workgroups (24 x 256 float each, at most kDensityBlocks) |
 // the secondary-ray optical-depth table (kOdR x kOdM float2, 1 MiB).
 // Pair capacity 2 per pixel of the image (8 shards).
 // Per 256-entry batch of the list: the physical index of its first pair (or kInline).
@@ -1022,8 +1049,10 @@ CloudWs cloud_ws_layout(void* base, size_t n) {
     w.pb.cap = (uint32_t)((2 * n + kShards - 1) / kShards);
     w.pb.pairs = reinterpret_cast<uint32_t*>(b + off);
     off = al(off + (size_t)kShards * w.pb.cap * 4);
-    w.pb.odvis = reinterpret_cast<float2*>(b + off);
-    off = al(off + (size_t)kShards * w.pb.cap * 8);
+    w.pb.od = reinterpret_cast<float*>(b + off);
+    off = al(off + (size_t)kShards * w.pb.cap * 4);
+    w.pb.vis = reinterpret_cast<float*>(b + off);
+    off = al(off + (size_t)kShards * w.pb.cap * 4);
     w.pb.od_tmp = reinterpret_cast<float*>(b + off);
     w.pb.od_blocks = (uint32_t)std::min<size_t>(kDensityBlocks, (n + 255) / 256);
     w.pb.n = (uint32_t)n;
@@ -1082,6 +1111,7 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
     }
     // the caller sized the workspace for the target extent (soc_cloud_rendering_workspace_size)
     CloudWs ws = cloud_ws_layout(workspace, (size_t)target.width * (size_t)target.height);
+    ws.pb.store_geom = (uint32_t)tuning_knob("SOC_CLOUDS_GEOM", 1);
     uint32_t* counter = ws.counter;
     uint32_t* list = ws.list;
     // the frame's secondary-ray table (SOC_CLOUDS_OD_LUT=0: march every secondary ray, the single-lane kernel's bits);
