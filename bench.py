@@ -135,7 +135,8 @@ def valu_bound(kernel, us):
     for rows in t.get("runs", {}).values():
         if kernel in rows:
             r = rows[kernel]
-            return {"valu_issue_us": r["issue_bound_us"], "frac_of_launch": round(r["issue_bound_us"] / us, 3),
+            issue = r.get("valu_issue_us", r.get("issue_bound_us"))
+            return {"valu_issue_us": issue, "frac_of_launch": round(issue / us, 3),
                     "serial_us": r["us"], "source": os.path.relpath(files[-1], ROOT)}
     return None
 

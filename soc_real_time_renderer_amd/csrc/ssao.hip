@@ -133,20 +133,14 @@ __device__ __forceinline__ f2v aff2(const Aff& a, f2v kx, f2v ky, f2v kz) {
 
 // The per-pixel part of SSAOGenerationTask (:176-194) before the tap loop: the view position, the view-space normal,
 // the random-vector TBN and the tap loop's per-pixel affine forms. `skip`: a sky pixel (zero normal), written as 255.
-struct SsaoForms {           // the pipelined loop's per-pixel forms, packed per tap (ssao_taps_pipelined)
-    f2v xy0, xy1, xy2, xy3;   // (x', y') affine forms
-    f2v wd0, wd1, wd2, wd3;   // (w', (s.z - frag.z) / r)
-    float A1, B1;
-};
 struct SsaoPixel {
     bool skip;
     f3 frag;
     Aff ax, ay, aw, az, dzr;
     float A1, B1;
-    SsaoForms F;              // with FORMS
 };
 
-template <bool TABLE, bool FORMS = false>
+template <bool TABLE>
 __device__ __forceinline__ SsaoPixel ssao_setup(int x, int y, const DImg& depth, const DImg& normal, const DImg& target,
                                                 const float2* __restrict__ table, const SsaoParams& p) {
     // no implicit contraction: every fused multiply-add below is an explicit fma, so the per-pixel arithmetic does not
@@ -213,18 +207,6 @@ __device__ __forceinline__ SsaoPixel ssao_setup(int x, int y, const DImg& depth,
     px.A1 = (frag.z * ip[11] - ip[10]) * ir;
     px.B1 = (frag.z * ip[15] - ip[14]) * ir;
     px.dzr = Aff{p.bias * ir, t.z, b.z, n.z};
-    if constexpr (FORMS) {   // built from the values themselves, not through the Aff members (which spilled)
-        px.F.xy0 = f2v{px.ax.a0, px.ay.a0};
-        px.F.xy1 = f2v{px.ax.a1, px.ay.a1};
-        px.F.xy2 = f2v{px.ax.a2, px.ay.a2};
-        px.F.xy3 = f2v{px.ax.a3, px.ay.a3};
-        px.F.wd0 = f2v{px.aw.a0, p.bias * ir};
-        px.F.wd1 = f2v{px.aw.a1, t.z};
-        px.F.wd2 = f2v{px.aw.a2, b.z};
-        px.F.wd3 = f2v{px.aw.a3, n.z};
-        px.F.A1 = px.A1;
-        px.F.B1 = px.B1;
-    }
     return px;
 }
 
@@ -333,89 +315,6 @@ __device__ __forceinline__ void ssao_pixel(int x, int y, const DImg& depth, cons
     row_ptr_w<uint8_t>(target, y)[x] = (uint8_t)to_unorm8(occ);
 }
 
-// The tap loop software-pipelined (round 5): a pair's projection, fixed-point coordinates and texel loads (stage A: LDS,
-// or the D32 image for out-of-tile taps) are issued one pair ahead of the previous pair's bilinear, range test and
-// accumulation (stage B), so a pair's load latency (an out-of-tile tap's L2 / HBM round trip above all) runs under
-// the other pair's arithmetic instead of parking the wave. The affine forms are packed per tap instead of per tap
-// pair, (x', y') and (w', dz), so no per-pixel coefficient is held twice as a broadcast pair. Element by element the
-// same IEEE operations in the same order as the PK loop of ssao_pixel: the same bits.
-struct SsaoFetch {
-    float a0, a1, a2, a3, b0, b1, b2, b3;   // the two taps' 2x2 texels
-    uint32_t w;                             // their sub-texel weights: bytes (x_a, y_a, x_b, y_b) of the fixed-point coords
-    f2v dz;                                 // (s.z - frag.z) / r of both taps
-};
-
-// The tap pairs' kernel vectors in LDS, (kx_a, kx_b, ky_a, ky_b) + (kz_a, kz_b, -, -) per pair: read with two
-// broadcast ds_reads, so the loop issues no scalar load (SMEM shares lgkmcnt with LDS and returns out of order: a
-// scalar load in the loop makes the wave drain every outstanding tap read, lgkmcnt(0), before its next pair).
-struct KPair { float4 xy; float4 z; };
-constexpr int kKernelPairs = SOC_SSAO_MAX_KERNEL / 2;
-
-template <class Quad>
-__device__ __forceinline__ void ssao_stage_a(const SsaoForms& F, const KPair* kt, int i, float cx0, float cy0,
-                                             float tmax_x, float tmax_y, const Quad& quad, SsaoFetch& f) {
-#pragma clang fp contract(off)
-    const float4 kq = kt[i >> 1].xy;
-    const float2 kz = *reinterpret_cast<const float2*>(&kt[i >> 1].z);
-    const float kxa = kq.x, kya = kq.z, kza = kz.x;
-    const float kxb = kq.y, kyb = kq.w, kzb = kz.y;
-    const f2v XYa = pfma(F.xy3, bc2(kza), pfma(F.xy2, bc2(kya), pfma(F.xy1, bc2(kxa), F.xy0)));
-    const f2v WDa = pfma(F.wd3, bc2(kza), pfma(F.wd2, bc2(kya), pfma(F.wd1, bc2(kxa), F.wd0)));
-    const f2v XYb = pfma(F.xy3, bc2(kzb), pfma(F.xy2, bc2(kyb), pfma(F.xy1, bc2(kxb), F.xy0)));
-    const f2v WDb = pfma(F.wd3, bc2(kzb), pfma(F.wd2, bc2(kyb), pfma(F.wd1, bc2(kxb), F.wd0)));
-    const float rwa = fast_rcp(WDa.x), rwb = fast_rcp(WDb.x);
-    const int fxa = (int)__builtin_amdgcn_fmed3f(__builtin_fmaf(XYa.x, rwa, cx0), 0.5f, tmax_x);
-    const int fya = (int)__builtin_amdgcn_fmed3f(__builtin_fmaf(XYa.y, rwa, cy0), 0.5f, tmax_y);
-    const int fxb = (int)__builtin_amdgcn_fmed3f(__builtin_fmaf(XYb.x, rwb, cx0), 0.5f, tmax_x);
-    const int fyb = (int)__builtin_amdgcn_fmed3f(__builtin_fmaf(XYb.y, rwb, cy0), 0.5f, tmax_y);
-    // the four low bytes in one register (v_perm_b32: selector 0x0c = zero byte)
-    f.w = __builtin_amdgcn_perm((uint32_t)fya, (uint32_t)fxa, 0x0c0c0400u) |
-          __builtin_amdgcn_perm((uint32_t)fyb, (uint32_t)fxb, 0x04000c0cu);
-    f.dz = f2v{WDa.y, WDb.y};
-    quad(fxa >> 8, fya >> 8, f.a0, f.a1, f.a2, f.a3);
-    quad(fxb >> 8, fyb >> 8, f.b0, f.b1, f.b2, f.b3);
-}
-
-__device__ __forceinline__ float ssao_stage_b(const SsaoForms& F, const float* ip, const SsaoFetch& f, float occ) {
-#pragma clang fp contract(off)
-    // (v_cvt_f32_ubyte0..3)
-    const f2v wx = f2v{(float)(f.w & 255u), (float)((f.w >> 16) & 255u)} * bc2(1.0f / 256.0f);
-    const f2v wy = f2v{(float)((f.w >> 8) & 255u), (float)(f.w >> 24)} * bc2(1.0f / 256.0f);
-    const float atop = __builtin_fmaf(wx.x, f.a1 - f.a0, f.a0), abot = __builtin_fmaf(wx.x, f.a3 - f.a2, f.a2);
-    const float btop = __builtin_fmaf(wx.y, f.b1 - f.b0, f.b0), bbot = __builtin_fmaf(wx.y, f.b3 - f.b2, f.b2);
-    const f2v dd = {__builtin_fmaf(wy.x, abot - atop, atop), __builtin_fmaf(wy.y, bbot - btop, btop)};
-    const f2v vw = pfma(bc2(ip[11]), dd, bc2(ip[15]));
-    const f2v d1 = {__builtin_fmaf(dd.x, F.A1, F.B1), __builtin_fmaf(dd.y, F.A1, F.B1)};
-    const f2v q = vw * f2v{fast_rcp(fabsf(d1.x)), fast_rcp(fabsf(d1.y))};
-    const f2v rc = {__builtin_amdgcn_fmed3f(q.x, 0.0f, 1.0f), __builtin_amdgcn_fmed3f(q.y, 0.0f, 1.0f)};
-    const f2v range = rc * rc * pfma(bc2(-2.0f), rc, bc2(3.0f));   // smoothstep(0, 1, x)
-    const f2v d2 = pfma(f.dz, vw, d1);
-    occ += (d2.x <= 0.0f) ? range.x : 0.0f;
-    occ += (d2.y <= 0.0f) ? range.y : 0.0f;
-    return occ;
-}
-
-template <class Quad>
-__device__ __forceinline__ float ssao_taps_pipelined(const SsaoForms& F, const KPair* kt, const SsaoParams& p,
-                                                     const Quad& quad) {
-#pragma clang fp contract(off)
-    const float* ip = p.inv_proj.m;
-    const float cx0 = p.c0x, cy0 = p.c0y, tmax_x = p.tmx, tmax_y = p.tmy;
-    static_assert(SOC_SSAO_MAX_KERNEL % 4 == 2, "13 pairs: a prologue pair, then two pairs per trip");
-    float occ = 0.0f;
-    SsaoFetch f0, f1;
-    ssao_stage_a(F, kt, 0, cx0, cy0, tmax_x, tmax_y, quad, f0);
-    // two pairs per trip, so the in-flight fetch alternates between f0 and f1 without register copies
-#pragma unroll 1
-    for (int i = 2; i < SOC_SSAO_MAX_KERNEL; i += 4) {
-        ssao_stage_a(F, kt, i, cx0, cy0, tmax_x, tmax_y, quad, f1);
-        occ = ssao_stage_b(F, ip, f0, occ);
-        ssao_stage_a(F, kt, i + 2, cx0, cy0, tmax_x, tmax_y, quad, f0);
-        occ = ssao_stage_b(F, ip, f1, occ);
-    }
-    return ssao_stage_b(F, ip, f0, occ);
-}
-
 template <bool TABLE, bool SPARSE_IP, bool FULL>
 __global__ __launch_bounds__(kWorkgroup) void ssao_kernel(DImg depth, DImg normal, DImg target, const float2* __restrict__ table,
                                                    SsaoParams p) {
@@ -470,24 +369,15 @@ struct LdsQuad {
 #endif
 constexpr int kSsaoTX = SOC_SSAO_TILE_TX, kSsaoTY = SOC_SSAO_TILE_TY, kSsaoHalo = SOC_SSAO_HALO, kSsaoTileLanes = kSsaoTX * kSsaoTY;
 
-template <bool TABLE, bool SPARSE_IP, bool FULL, int TXP, int TYP, int HALO, int UNROLL, bool PK = false, bool PIPE = false>
+template <bool TABLE, bool SPARSE_IP, bool FULL, int TXP, int TYP, int HALO, int UNROLL, bool PK = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(TXP * TYP, TXP * TYP)))
 __attribute__((amdgpu_waves_per_eu(TXP * TYP >= 1024 ? 8 : TXP * TYP >= 512 ? 4 : 2)))
 void ssao_lds_kernel(DImg depth, DImg normal, DImg target, const float2* __restrict__ table, SsaoParams p) {
     using T = SsaoTile<TXP, TYP, HALO>;
     __shared__ float4 tile4[T::TW * T::TH / 4];
-    __shared__ KPair ktab[PIPE ? kKernelPairs : 1];
     int bx, by;
     xcd_order(p.swz, bx, by);
     const int tid = threadIdx.x;
-    if constexpr (PIPE) {
-        if (tid < kKernelPairs * 8) {   // ssao_generation.inl:74-103 in the tap-pair layout of ssao_stage_a
-            const int q = tid >> 3, e = tid & 7;
-            const int tap = 2 * q + (e & 1), comp = e < 4 ? (e >> 1) : 2;
-            float* dst = reinterpret_cast<float*>(&ktab[q]);
-            dst[e < 4 ? e : 4 + (e & 1)] = kKernel.v[tap][comp];
-        }
-    }
     const int gx0 = bx * 2 * TXP - HALO, gy0 = by * 2 * TYP - HALO;
     const __amdgpu_buffer_rsrc_t rsrc = depth_rsrc(depth);
     // stage the tile: rows clamped into the image; columns left of the image give a negative (out-of-range) offset,
@@ -505,15 +395,7 @@ void ssao_lds_kernel(DImg depth, DImg normal, DImg target, const float2* __restr
     const int x = bx * TXP + (w % (TXP / 32)) * 32 + (lane & 31), y = by * TYP + (w / (TXP / 32)) * 2 + (lane >> 5);
     if (x >= target.w || y >= target.h) return;
     const LdsQuad<TXP, TYP, HALO> quad{reinterpret_cast<const float*>(tile4), gx0, gy0, GlobalQuad{rsrc, depth.pitch}};
-    if constexpr (PIPE) {
-        static_assert(TABLE && SPARSE_IP && FULL, "the pipelined tap loop is the full-kernel sparse-projection path");
-        const SsaoPixel px = ssao_setup<TABLE, true>(x, y, depth, normal, target, table, p);
-        const float occ = px.skip ? 0.0f : ssao_taps_pipelined(px.F, ktab, p, quad);
-        row_ptr_w<uint8_t>(target, y)[x] = px.skip ? (uint8_t)255 : (uint8_t)to_unorm8(1.0f - occ * p.inv_ksize);
-    } else {
-        ssao_pixel<TABLE, SPARSE_IP, FULL, LdsQuad<TXP, TYP, HALO>, UNROLL, PK>(x, y, depth, normal, target, table, p,
-                                                                              quad);
-    }
+    ssao_pixel<TABLE, SPARSE_IP, FULL, LdsQuad<TXP, TYP, HALO>, UNROLL, PK>(x, y, depth, normal, target, table, p, quad);
 }
 
 // ssao_blur.inl:91-106: 4x4 box at offsets -2..+1 (x outer, y inner), all taps on texel centres.
@@ -623,14 +505,8 @@ extern "C" int soc_ssao_generation(const soc_globals* g, soc_img depth, soc_img 
         SsaoParams pt = p;
         pt.swz = 1;
         const dim3 g(ceil_div(target.width, kSsaoTX), ceil_div(target.height, kSsaoTY));
-        // SOC_SSAO_PIPE=1: the software-pipelined tap loop (the same bits)
-        if (tuning_knob("SOC_SSAO_PIPE", 0))
-            launch("ssao_lds_kernel", kSsaoTileLanes,
-                   ssao_lds_kernel<true, true, true, kSsaoTX, kSsaoTY, kSsaoHalo, 2, true, true>, g, kSsaoTileLanes, 0, st,
-                   dd, dn, dt, tb, pt);
-        else
-            launch("ssao_lds_kernel", kSsaoTileLanes, ssao_lds_kernel<true, true, true, kSsaoTX, kSsaoTY, kSsaoHalo, 2, true>,
-                   g, kSsaoTileLanes, 0, st, dd, dn, dt, tb, pt);
+        launch("ssao_lds_kernel", kSsaoTileLanes, ssao_lds_kernel<true, true, true, kSsaoTX, kSsaoTY, kSsaoHalo, 2, true>, g,
+               kSsaoTileLanes, 0, st, dd, dn, dt, tb, pt);
     } else if (noise_table && sip && full) SOC_SSAO_LAUNCH(true, true, true);
     else if (noise_table && sip) SOC_SSAO_LAUNCH(true, true, false);
     else if (noise_table) SOC_SSAO_LAUNCH(true, false, false);

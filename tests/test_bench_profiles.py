@@ -27,7 +27,7 @@ def test_ssao_bounds():
     """The VALU issue model of the current kernels (profiles/*valu_model.json)."""
     import bench
     vb = bench.valu_bound(bench.SSAO_KERNEL, 110.0)
-    assert vb is not None and 50.0 < vb["valu_issue_us"] < 110.0
+    assert vb is not None and 20.0 < vb["valu_issue_us"] < 110.0
     assert abs(vb["frac_of_launch"] - vb["valu_issue_us"] / 110.0) < 1e-3
     assert bench.valu_bound("no_such_kernel", 1.0) is None
 

@@ -177,8 +177,7 @@ def test_ssao_tile_orders_bit_identical(soc, monkeypatch, W, H, inputs):
     kernel (SOC_SSAO_TILE=0) give the same bits, in every workgroup order of the gather kernel (row-major, XCD-aware
     eighths, horizontal and vertical XCD bands: SOC_SWZ_SSAO; the orders are bijections, also for ragged grids), on the
     box atrium and on the mesh (near geometry: many taps leave the tile), at odd, tall and wide extents (partial tiles,
-    tiles hanging over every image edge). The tiled kernel with the software-pipelined tap loop (SOC_SSAO_PIPE=1 and 0)
-    too."""
+    tiles hanging over every image edge)."""
     if inputs == "mesh":
         from soc_real_time_renderer_amd import raster, scene
         import bench
@@ -191,11 +190,8 @@ def test_ssao_tile_orders_bit_identical(soc, monkeypatch, W, H, inputs):
         depth, normal = dev(gb["depth"]), dev(gb["normal"])
     table = torch.zeros((H // 2) * (W // 2) * 2, dtype=torch.float32, device=DEV)
     outs = []
-    for tile, swz, pipe in (("1", None, "1"), ("1", None, "0"), ("0", "0", None), ("0", "1", None), ("0", "4", None),
-                            ("0", "16", None), ("0", "-16", None), ("0", "-3", None)):
+    for tile, swz in (("1", None), ("0", "0"), ("0", "1"), ("0", "4"), ("0", "16"), ("0", "-16"), ("0", "-3")):
         monkeypatch.setenv("SOC_SSAO_TILE", tile)
-        if pipe is not None:
-            monkeypatch.setenv("SOC_SSAO_PIPE", pipe)
         if swz is None:
             monkeypatch.delenv("SOC_SWZ_SSAO", raising=False)
         else:
@@ -207,7 +203,6 @@ def test_ssao_tile_orders_bit_identical(soc, monkeypatch, W, H, inputs):
         outs.append(host(out))
     monkeypatch.delenv("SOC_SSAO_TILE")
     monkeypatch.delenv("SOC_SWZ_SSAO", raising=False)
-    monkeypatch.delenv("SOC_SSAO_PIPE", raising=False)
     soc.reload_tuning()
     for o in outs[1:]:
         assert np.array_equal(o, outs[0]), int((o != outs[0]).sum())

@@ -3,7 +3,7 @@ own inputs, and hash its output so exact variants can be checked for identical b
 
     python tools/pass_probe.py --pass clouds|ssao|gbuffer|taa|raster --configs c3,c4 --variants libsoc_rt.so,libsoc_rt_x.so [--reps 100] [--rounds 3]
 
-A variant is a library file name (SOC_RT_LIB_VARIANT) or NAME=VALUE (a tuning knob on the default library). Each
+A variant is a library file name (SOC_RT_LIB_VARIANT) or NAME=VALUE[+NAME=VALUE...] (tuning knobs on the default library). Each
 variant runs in its own process; the rounds interleave the variants so clock drift hits
 them alike. Prints one line per (round, variant, config): mean microseconds per launch and the output digest.
 """
@@ -108,7 +108,8 @@ def main():
         return
     for r in range(a.rounds):
         for v in a.variants.split(","):
-            env = dict(os.environ, **({v.split("=")[0]: v.split("=")[1]} if "=" in v else {"SOC_RT_LIB_VARIANT": v}))
+            # NAME=VALUE[+NAME=VALUE...]: tuning knobs on the default library; else a library file name
+            env = dict(os.environ, **(dict(kv.split("=", 1) for kv in v.split("+")) if "=" in v else {"SOC_RT_LIB_VARIANT": v}))
             p = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", "--pass", a.pass_name, "--configs",
                                 a.configs, "--reps", str(a.reps)], env=env, capture_output=True, text=True, timeout=600)
             line = [ln for ln in p.stdout.splitlines() if ln.startswith("PROBE ")]
