@@ -12,8 +12,9 @@
 #   tools/gpu.sh pmc TAG "<counters>" ... [-- bench args]
 #                                               one rocprofv3 --pmc pass per counter group (kernel trace only) + summary
 #   tools/gpu.sh traffic TAG [bench args]       FETCH_SIZE / WRITE_SIZE passes -> per-kernel HBM traffic table
-#   tools/gpu.sh round TAG                      the round-end measurement set (bench lines C3/C2/C3b/C4/raster C2/C3/C4, frame PNG,
-#                                               kernel trace + traffic of the default command)
+#   tools/gpu.sh round TAG                      the round-end measurement set (bench lines C3/C2/C3b/C4/raster C2/C3/C4, the RCCL
+#                                               exchange line, frame PNG, kernel trace + same-run event check + traffic)
+#   tools/gpu.sh valu TAG                       VALU issue calibration + the serial frame's SQ counters -> valu model
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
@@ -96,10 +97,22 @@ case $cmd in
     bench_line ${t}_bench_raster_c3 --raster --no-cpu-baseline
     bench_line ${t}_bench_raster_c4 --config c4 --raster --no-cpu-baseline
     bench_line ${t}_frame_c3_960 --raster --no-cpu-baseline --width 960 --height 540 --steps 5 --warmup 2 --write-frame gpurun_out/${t}_frame_raster_c3_960x540.png
-    kernel_trace $t
+    bench_line ${t}_bench_exchange --exchange --no-cpu-baseline
+    # the kernel trace of the default command, with the bench's per-frame pass events of the same run (event_trace_check)
+    SOC_BENCH_EVENTS_OUT=gpurun_out/${t}_events.json kernel_trace $t
     python tools/roofline_check.py gpurun_out/${t}_bench.json gpurun_out/${t}_kt > gpurun_out/${t}_roofline_check.json
+    python tools/event_trace_check.py compare gpurun_out/${t}_events.json "$(find gpurun_out/${t}_kt -name '*kernel_trace.csv' | head -1)" > gpurun_out/${t}_event_trace_check.json
     pmc_passes $t FETCH_SIZE WRITE_SIZE
     python tools/pmc_summary.py gpurun_out/${t}_pmc --traffic gpurun_out/${t}_pmc_traffic.json --scene mesh > gpurun_out/${t}_pmc_summary.json ;;
+  valu)
+    # VALU issue calibration: the microbenchmark, its counter check, the serial-lane frame's counters
+    t=${1:?tag}
+    hipcc --offload-arch=gfx950 -O3 -o gpurun_out/valu_rate tools/microbench/valu_rate.hip || exit 1
+    timeout -k 10 120 ./gpurun_out/valu_rate > gpurun_out/${t}_valu_rate.txt 2>&1 || { echo valu_rate failed; exit 1; }
+    rm -rf gpurun_out/${t}_vr_pmc
+    timeout -s KILL 90 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d gpurun_out/${t}_vr_pmc -o run -- ./gpurun_out/valu_rate > gpurun_out/${t}_vr_pmc.log 2>&1 || { echo valu pmc failed; exit 1; }
+    pmc_passes ${t}sq "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" -- --no-sky-lane
+    python tools/valu_calibrate.py gpurun_out/${t}_valu_rate.txt gpurun_out/${t}_vr_pmc gpurun_out/${t}sq_pmc > gpurun_out/${t}_valu_model.json && echo "valu model: gpurun_out/${t}_valu_model.json" ;;
   *)
     echo "unknown command $cmd"; exit 2 ;;
 esac
