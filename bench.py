@@ -312,6 +312,17 @@ def main():
 
     for _ in range(args.warmup):
         frame()
+    # the renderer's sky-lane queue probe (soc_renderer_side_queue) runs over its first 65 frames and decides at the
+    # first frame after they completed: untimed frames until then, the same count on every rank (each frame of the
+    # exchange path is a collective)
+    probe_frames = 0
+    if not args.no_sky_lane and r.side_queue() == -1:
+        probe_frames = max(0, 66 - args.warmup)
+        for _ in range(probe_frames):
+            frame()
+        torch.cuda.synchronize()
+        frame()
+        probe_frames += 1
     torch.cuda.synchronize()
 
     # HIP events around the north-star kernels on the launch stream, inside the timed region
@@ -457,6 +468,9 @@ def main():
                    "sky_lane": ("CloudRendering + SkyCompose on a concurrent stream; " +
                                 ("the clouds of frame N+1 may start before frame N's TAA (static inputs)"
                                  if not args.no_static_inputs else "forked at every frame start")),
+                   "sky_lane_queue": {1: "high priority", 2: "low priority", 0: "normal priority",
+                                      -1: "not chosen"}.get(r.side_queue(), "?"),
+                   "untimed_lane_probe_frames": probe_frames,
                    "raster": (f"in-frame: DepthPrepass + SunShadowDraw (4096^2) + GBufferGeneration of the "
                               f"{int(sc['mesh'].struct.triangle_count)}-triangle scene mesh") if args.raster
                    else "off: G-buffer and shadow map are resident inputs"},
@@ -493,11 +507,28 @@ def main():
         out["cpu_baseline"] = cpu_baseline(W, H, host_inputs, g)
     else:
         out["cpu_baseline"] = None
-    print(json.dumps(out), flush=True)
+    emit(json.dumps(out))
     r.close()
     if dist.is_initialized():
         dist.destroy_process_group()
 
 
+_RESULT_FD = None   # the process's original stdout when run as a script (everything else goes to stderr)
+
+
+def emit(line):
+    """The bench's one stdout line. Run as a script, fd 1 is pointed at stderr for the whole run (RCCL prints its
+    version banner to stdout when a communicator is created, and native code may print too), and the result line
+    alone is written to the saved original stdout."""
+    if _RESULT_FD is None:
+        print(line, flush=True)
+    else:
+        sys.stdout.flush()
+        os.write(_RESULT_FD, (line + "\n").encode())
+
+
 if __name__ == "__main__":
+    sys.stdout.flush()
+    _RESULT_FD = os.dup(1)
+    os.dup2(2, 1)
     main()

@@ -435,6 +435,10 @@ int soc_renderer_set_current_history(soc_renderer* r, int32_t index);
  * stream of the current device, forked from `stream` at the start of the PRE phase and joined before
  * Composition, so it overlaps bloom and SSAO. Results are identical either way. */
 int soc_renderer_set_async(soc_renderer* r, int32_t enable);
+/* The sky lane's hardware queue: 1 = a high-priority stream, 2 = low priority, 0 = normal priority (a queue HIP may
+ * share with the caller's stream), -1 = not chosen yet (tuning knob SOC_RENDERER_SIDE_QUEUE=3, the default: the first
+ * 64 frames run half at each priority and the faster is kept) or no sky lane created. Same results either way. */
+int32_t soc_renderer_side_queue(const soc_renderer* r);
 
 /* --- Pass declaration (the Daxa task-uses block + TaskGraph::add_task, e.g. composition.inl:10-21 and
  * renderer.cpp:1103-1117) ------------------------------------------------------------------------

@@ -456,6 +456,10 @@ class Renderer:
             _check(m, "soc_renderer_pass_event_times")
         return np.array(s0[:m], np.float64), np.array(s1[:m], np.float64)
 
+    def side_queue(self) -> int:
+        """The sky lane's hardware-queue priority (soc_renderer_side_queue): 1 high, 2 low, 0 normal, -1 not chosen."""
+        return int(lib().soc_renderer_side_queue(self.handle))
+
     def add_pass(self, name: str, fn, reads=(), writes=(), phase: int = PHASE_PRE_EXPOSURE, group: str = "",
                  before: Optional[str] = None, async_compute: bool = False) -> None:
         """Register a caller pass (soc_renderer_add_pass): `fn(globals_ptr, frame_images_ptr, stream_handle)` records

@@ -658,6 +658,14 @@ struct soc_renderer {
     int side_device = -1;
     hipStream_t side = nullptr;
     hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+    // the second lane's hardware queue (ensure_side_lane): a stream of high or low priority, so the lane never shares
+    // the caller's queue. Auto mode (the default) times frames with each and keeps the faster: lane_q = {high, low},
+    // side_queue = 1 (high) / 2 (low) once chosen, -1 while the probe runs; 0 = normal priority (shared pool).
+    hipStream_t lane_q[2] = {nullptr, nullptr};
+    int side_queue = -1;
+    int probe_frames = 0;
+    hipEvent_t probe_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t switch_ev = nullptr;
     // 8 partial luminance histograms of the fused composition + histogram pass (renderer-owned, 8 KiB)
     uint32_t* hist_scratch = nullptr;
     // a raster workspace of the sun shadow draw's own, so it can run on the second lane beside the depth prepass and
@@ -1077,15 +1085,15 @@ extern "C" soc_renderer* soc_renderer_create(const soc_frame_images* images, uin
     return r;
 }
 
+static void destroy_side_lane(soc_renderer* r);
+
 extern "C" void soc_renderer_destroy(soc_renderer* r) {
     if (!r) return;
     destroy_pass_events(r);
     for (auto& e : r->staging_ev)
         if (e) (void)hipEventDestroy(e);
     if (r->staging) (void)hipHostFree(r->staging);
-    if (r->fork_ev) (void)hipEventDestroy(r->fork_ev);
-    if (r->join_ev) (void)hipEventDestroy(r->join_ev);
-    if (r->side) (void)hipStreamDestroy(r->side);
+    destroy_side_lane(r);
     if (r->hist_scratch) (void)hipFree(r->hist_scratch);
     if (r->shadow_ws) (void)hipFree(r->shadow_ws);
     delete r;
@@ -1124,26 +1132,109 @@ static int run_pass(soc_renderer::Pass& p, const soc_globals* g, hipStream_t s) 
     return SOC_OK;
 }
 
+// The second lane's stream(s) and events (all of them: a device change rebuilds the lane there).
+static void destroy_side_lane(soc_renderer* r) {
+    for (hipEvent_t* e : {&r->fork_ev, &r->join_ev, &r->switch_ev, &r->probe_ev[0], &r->probe_ev[1], &r->probe_ev[2], &r->probe_ev[3]})
+        if (*e) { (void)hipEventDestroy(*e); *e = nullptr; }
+    if (r->lane_q[0] || r->lane_q[1]) {
+        for (auto& q : r->lane_q)
+            if (q) { (void)hipStreamDestroy(q); q = nullptr; }
+    } else if (r->side) {
+        (void)hipStreamDestroy(r->side);
+    }
+    r->side = nullptr;
+    r->side_queue = -1;
+    r->probe_frames = 0;
+}
+
+// HIP maps streams onto at most GPU_MAX_HW_QUEUES (4) hardware queues per priority, reusing the least-used queue once
+// the pool is full. With RCCL's and torch's streams created first (a process group), a normal-priority second lane was
+// given the caller's queue and the two lanes ran serialised (bench --exchange 0.79 vs 0.62 ms per frame, DESIGN.md §11
+// r5.8). A stream of another priority comes from a pool of its own, so the lane keeps a queue of its own whatever the
+// caller created. Which priority is faster depends on which lane is the frame's critical path (C3: the main lane, the
+// sky lane low is 5 % faster than high; C4: the sky lane, high is 10 % faster than low): tuning knob
+// SOC_RENDERER_SIDE_QUEUE 3 (default) times both (frame_lane_probe), 1 = high, 2 = low, 0 = normal priority.
 static int ensure_side_lane(soc_renderer* r) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return set_error(SOC_E_HIP, "soc_renderer_execute: hipGetDevice failed");
     if (r->side && r->side_device == dev) return SOC_OK;
     if (r->side) {   // the caller moved to another device: rebuild the lane (and its events) there
-        (void)hipStreamDestroy(r->side);
-        (void)hipEventDestroy(r->fork_ev);
-        (void)hipEventDestroy(r->join_ev);
+        destroy_side_lane(r);
         for (auto& p : r->passes)
             if (p.done) { (void)hipEventDestroy(p.done); p.done = nullptr; p.done_recorded = false; }
-        r->side = nullptr;
-        r->fork_ev = r->join_ev = nullptr;
     }
-    const hipError_t se = hipStreamCreateWithFlags(&r->side, hipStreamNonBlocking);
+    int sq = tuning_knob("SOC_RENDERER_SIDE_QUEUE", 3);
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess || least == greatest) sq = 0;
+    hipError_t se = hipSuccess;
+    if (sq == 3) {
+        se = hipStreamCreateWithPriority(&r->lane_q[0], hipStreamNonBlocking, greatest);
+        if (se == hipSuccess) se = hipStreamCreateWithPriority(&r->lane_q[1], hipStreamNonBlocking, least);
+        if (se == hipSuccess) se = hipEventCreateWithFlags(&r->switch_ev, hipEventDisableTiming);
+        for (auto& e : r->probe_ev)
+            if (se == hipSuccess) se = hipEventCreate(&e);
+        r->side = r->lane_q[0];
+        r->side_queue = -1;
+        r->probe_frames = 0;
+    } else if (sq == 1 || sq == 2) {
+        se = hipStreamCreateWithPriority(&r->side, hipStreamNonBlocking, sq == 2 ? least : greatest);
+        r->side_queue = sq;
+    } else {
+        se = hipStreamCreateWithFlags(&r->side, hipStreamNonBlocking);
+        r->side_queue = 0;
+    }
     if (se != hipSuccess ||
         hipEventCreateWithFlags(&r->fork_ev, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&r->join_ev, hipEventDisableTiming) != hipSuccess)
+        hipEventCreateWithFlags(&r->join_ev, hipEventDisableTiming) != hipSuccess) {
+        destroy_side_lane(r);
         return set_error(SOC_E_HIP, "soc_renderer_execute: second lane stream/event creation failed");
+    }
     r->side_device = dev;
     return SOC_OK;
+}
+
+// Move the second lane to stream q: q waits for everything queued on the current lane stream, so the lane stays one
+// in-order sequence (the passes' done events recorded on the old stream stay valid for waits).
+static int switch_side_lane(soc_renderer* r, hipStream_t q) {
+    if (q == r->side) return SOC_OK;
+    if (hipEventRecord(r->switch_ev, r->side) != hipSuccess || hipStreamWaitEvent(q, r->switch_ev, 0) != hipSuccess)
+        return set_error(SOC_E_HIP, "soc_renderer_execute: second lane switch failed");
+    r->side = q;
+    return SOC_OK;
+}
+
+// Auto mode's probe, at the start of each frame (a call with the PRE phase): frames [0, 32) run the sky lane at high
+// priority, [32, 64) at low; timing events on the caller's stream at frames 8, 32, 40, 64 give each setting's mean
+// frame interval over 24 frames (the first 8 after a switch skipped). Once the last event has completed (queried, never
+// waited on), the faster setting is kept for the renderer's life.
+static int frame_lane_probe(soc_renderer* r, hipStream_t s) {
+    if (r->side_queue != -1 || !r->lane_q[0]) return SOC_OK;
+    constexpr int kWindow = 32, kSkip = 8;
+    const int f = r->probe_frames;
+    if (f <= 2 * kWindow) {
+        const int slot = f == kSkip ? 0 : f == kWindow ? 1 : f == kWindow + kSkip ? 2 : f == 2 * kWindow ? 3 : -1;
+        if (slot >= 0 && hipEventRecord(r->probe_ev[slot], s) != hipSuccess)
+            return set_error(SOC_E_HIP, "soc_renderer_execute: lane probe event failed");
+        if (f == kWindow) {
+            int rc = switch_side_lane(r, r->lane_q[1]);
+            if (rc) return rc;
+        }
+        r->probe_frames++;
+        return SOC_OK;
+    }
+    if (hipEventQuery(r->probe_ev[3]) != hipSuccess) {   // not reached yet (or an error: the lane stays as it is)
+        (void)hipGetLastError();
+        return SOC_OK;
+    }
+    float hi = 0.0f, lo = 0.0f;
+    if (hipEventElapsedTime(&hi, r->probe_ev[0], r->probe_ev[1]) != hipSuccess ||
+        hipEventElapsedTime(&lo, r->probe_ev[2], r->probe_ev[3]) != hipSuccess) {
+        (void)hipGetLastError();
+        r->side_queue = 2;
+        return SOC_OK;
+    }
+    r->side_queue = hi < lo ? 1 : 2;
+    return switch_side_lane(r, r->lane_q[r->side_queue - 1]);
 }
 
 // Lane of pass i with the second lane on or off: 0 = the caller's stream, 1 = the renderer's second lane.
@@ -1230,6 +1321,7 @@ extern "C" int soc_renderer_execute(soc_renderer* r, const soc_globals* g, int32
     bool forked_wait = false;
     if (lanes) {
         int rc = ensure_side_lane(r);
+        if (!rc && (phase & SOC_PHASE_PRE_EXPOSURE)) rc = frame_lane_probe(r, s);
         if (rc) return rc;
         if (hipEventRecord(r->fork_ev, s) != hipSuccess)
             return set_error(SOC_E_HIP, "soc_renderer_execute: second lane fork failed");
@@ -1538,6 +1630,8 @@ extern "C" int soc_renderer_pass_stats(soc_renderer* r, int32_t i, float* total_
     *frames = p.count;
     return SOC_OK;
 }
+
+extern "C" int32_t soc_renderer_side_queue(const soc_renderer* r) { return (r && r->side) ? r->side_queue : -1; }
 
 extern "C" int32_t soc_renderer_pass_event_times(soc_renderer* r, int32_t i, void* base, float* start_ms, float* end_ms,
                                                  int32_t n) {

@@ -125,8 +125,9 @@ def test_bench_exchange_rccl_world1():
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
-    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, p.stdout
+    # the line is the whole of stdout: RCCL's version banner and other native prints go to stderr (bench.emit)
+    lines = p.stdout.splitlines()
+    assert len(lines) == 1 and lines[0].startswith("{"), p.stdout
     out = json.loads(lines[0])
     assert out["n_gpus"] == 1
     assert out["config"]["histogram_allreduce"] is True

@@ -915,6 +915,51 @@ def test_render_graph_static_inputs_bit_identical(soc, inputs):
             assert torch.equal(a[k], b[k]), k
 
 
+@pytest.mark.parametrize("inputs", ["sponza", "terrain"])
+def test_sky_lane_queue_probe_bit_identical(soc, monkeypatch, inputs):
+    """The sky lane's hardware queue (SOC_RENDERER_SIDE_QUEUE): auto (3, default) runs frames 0-31 on a high-priority
+    stream, 32-63 on a low-priority one and then keeps the faster, moving the lane between streams with an event wait;
+    1 / 2 fix it, 0 is the normal-priority stream. Every frame's output and the final temporal state have the same bits
+    in every mode (72 frames with per-frame globals, static inputs: the clouds of frame N+1 start before frame N's TAA,
+    also across the switches), and auto has chosen a queue by the end."""
+    import ctypes as C
+    W, H = 1920, 1080
+    g0, gb = (sponza_inputs if inputs == "sponza" else terrain_inputs)(W, H, elapsed=10.0)
+    outs, chosen = [], []
+    for mode in ("0", "3", "1", "2"):
+        monkeypatch.setenv("SOC_RENDERER_SIDE_QUEUE", mode)
+        soc.reload_tuning()
+        fr = soc.alloc_frame(W, H, DEV, bloom_output=True)
+        for k in ("albedo", "emissive", "normal", "velocity", "depth"):
+            fr[k].copy_(torch.from_numpy(gb[k]))
+        fr["shadow"] = dev(gb["shadow"])
+        fr["noise"].copy_(torch.from_numpy(gb["noise"]))
+        r = soc.Renderer(fr, static_inputs=True)
+        cam = soc.make_camera((-14.0, 2.2, 0.3), (0.0, -0.42, 0.0))
+        ji = C.c_uint32(0)
+        g = soc.globals_defaults(W, H)
+        seq = []
+        for f in range(72):
+            soc.frame_update(g, cam, W, H, 0.016, ji)
+            cam.position[0] += 0.01
+            r.execute(g)
+            seq.append(fr["output"].clone())
+            if f == 66:
+                torch.cuda.synchronize()   # the probe's last event has completed: the next frame decides
+        torch.cuda.synchronize()
+        seq.append(fr["auto_exposure"].clone())
+        seq.append(r.resolved().clone())
+        outs.append(seq)
+        chosen.append(r.side_queue())
+        r.close()
+    monkeypatch.delenv("SOC_RENDERER_SIDE_QUEUE")
+    soc.reload_tuning()
+    assert chosen[0] == 0 and chosen[1] in (1, 2) and chosen[2] == 1 and chosen[3] == 2, chosen
+    for o in outs[1:]:
+        for f, (a, b) in enumerate(zip(outs[0], o)):
+            assert torch.equal(a, b), f
+
+
 def test_static_inputs_first_call_after_async_input_write(soc):
     """SOC_RENDERER_STATIC_INPUTS: the first call after create (and after a graph rebuild) forks the second
     lane before CloudRendering, so inputs the caller wrote on its stream just before that call are seen. The terrain
