@@ -253,6 +253,10 @@ __global__ __launch_bounds__(kWorkgroup) void composition_pair(DImg target, DImg
         ShadePre pre[2];
         f3 alb[2], nrm[2], wps[2];
         uint32_t lit = 0u;
+        // NT & 4: both pixels' AO taps (3 half-res texels per row) as one 8-B load per row, issued with the G-buffer
+        // loads (not after the depth test), for sky pixels too (in bounds, unused); the same bits as sample_r8
+        float aop[2] = {0.0f, 0.0f};
+        if (NT & 4) sample_r8_pair(bo, centre_uv_rn(x, target.w, p.rw), centre_uv_rn(x + 1, target.w, p.rw), v, aop[0], aop[1]);
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
             const float u = centre_uv_rn(x + k, target.w, p.rw);
@@ -273,7 +277,7 @@ __global__ __launch_bounds__(kWorkgroup) void composition_pair(DImg target, DImg
                 const f4 cl = fetch_rgba8(clouds, x + k, y);
                 c = f4{cl.x, cl.y, cl.z, 1.0f};
             } else {
-                const float ao = (SOC_COMP_PROFILE & 2) ? u : sample_r8(bo, u, v);
+                const float ao = (SOC_COMP_PROFILE & 2) ? u : (NT & 4) ? aop[k] : sample_r8(bo, u, v);
                 if (LIGHTS) {
                     pre[k] = shade_pre(p, u, v, d, f3{em.x, em.y, em.z}, f3{nn.x, nn.y, nn.z}, ao, bs);
                     alb[k] = f3{al.x, al.y, al.z};
@@ -435,6 +439,8 @@ int composition_launch(const soc_globals* g, const soc_globals* d_globals, soc_i
     // non-temporal G-buffer loads and colour store (default); SOC_COMP_NT=0 selects the default cache policy for the
     // variant-identity test
     const bool nt = tuning_knob("SOC_COMP_NT", 3) == 3;
+    // SOC_COMP_AOP=0: the AO taps as 4 byte loads per pixel after the depth test (round 4); 1: sample_r8_pair
+    const bool aop = tuning_knob("SOC_COMP_AOP", 1) != 0;
     p.swz = 0;   // row-major (the strip order measured 66 -> 77 us)
     p.rw = recip_rn(target.width);
     p.rh = recip_rn(target.height);
@@ -462,11 +468,17 @@ int composition_launch(const soc_globals* g, const soc_globals* d_globals, soc_i
             p.lrange = g->log_max_luminance - g->log_min_luminance;
             p.bf = bin_fast_params(p.lmin, p.lrange);
             if (lights) SOC_COMP_PAIR(true, true);
+            else if (nt && aop)
+                launch("composition_pair", kWorkgroup, composition_pair<true, false, 7>, grd, kWorkgroup, 0, hs(stream), dimg(target), dimg(albedo), dimg(emissive),
+                    dimg(normal), dimg(depth), dimg(ssao), dimg(shadow), dimg(clouds), p);
             else if (nt)
                 launch("composition_pair", kWorkgroup, composition_pair<true, false, 3>, grd, kWorkgroup, 0, hs(stream), dimg(target), dimg(albedo), dimg(emissive),
                     dimg(normal), dimg(depth), dimg(ssao), dimg(shadow), dimg(clouds), p);
             else SOC_COMP_PAIR(true, false);
             if (fold) launch("histogram_fold", kBins, histogram_fold, 1, kBins, 0, hs(stream), scratch, bins);
+        } else if (nt && !lights && aop) {
+            launch("composition_pair", kWorkgroup, composition_pair<false, false, 7>, grd, kWorkgroup, 0, hs(stream), dimg(target), dimg(albedo), dimg(emissive),
+                dimg(normal), dimg(depth), dimg(ssao), dimg(shadow), dimg(clouds), p);
         } else if (nt && !lights) {
             // non-temporal G-buffer loads and colour store (measured at 4K: 71.5 -> 68 us; TAA, the next
             // reader of depth, +3 us: the frame is unchanged). SOC_COMP_NT=0: default cache policy.

@@ -204,6 +204,25 @@ __device__ __forceinline__ float sample_r8(const BufImg& b, float u, float v) {
     return bilerp1(unorm8(a), unorm8(c), unorm8(d), unorm8(e), ax.w, ay.w);
 }
 
+// sample_r8 at two coordinates of one row v whose taps span at most 8 bytes from the first tap's dword (a pixel pair
+// reading a half-resolution image: 3 texels per row): one 8-B load per row for both samples instead of 8 byte loads,
+// the same texels, weights and arithmetic (same bits); other spans, and a load that would pass the row's pitch, take
+// the per-byte form.
+__device__ __forceinline__ void sample_r8_pair(const BufImg& b, float u0, float u1, float v, float& s0, float& s1) {
+    const Axis a0 = axis_clamp(u0, b.w), a1 = axis_clamp(u1, b.w), ay = axis_clamp(v, b.h);
+    const int base = a0.i0 & ~3;
+    if (a1.i0 >= a0.i0 && a1.i1 - base <= 7 && base + 8 <= b.pitch) {
+        const uint64_t r0 = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(b.r, buf_row(b, ay.i0) + base, 0, 0));
+        const uint64_t r1 = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(b.r, buf_row(b, ay.i1) + base, 0, 0));
+        auto t = [&](uint64_t r, int i) { return unorm8((uint32_t)(r >> (8 * (i - base))) & 255u); };
+        s0 = bilerp1(t(r0, a0.i0), t(r0, a0.i1), t(r1, a0.i0), t(r1, a0.i1), a0.w, ay.w);
+        s1 = bilerp1(t(r0, a1.i0), t(r0, a1.i1), t(r1, a1.i0), t(r1, a1.i1), a1.w, ay.w);
+        return;
+    }
+    s0 = sample_r8(b, u0, v);
+    s1 = sample_r8(b, u1, v);
+}
+
 // Packed mip chain (soc_rt.h soc_generate_mips): level count and the byte offset / extent of level k.
 __host__ __device__ __forceinline__ int mip_levels(int w, int h) {
     int m = w > h ? w : h, n = 0;

@@ -221,23 +221,36 @@ def test_ssao_blur_bit_exact(soc, oracle, W, H):
 
 
 # ------------------------------------------------------------------------------------------------ composition
-def test_composition_cache_policy_variants_bit_identical(soc, monkeypatch):
-    """The non-temporal load/store variant of the fast path (default) gives the plain variant's bits."""
-    W, H = 1920, 1080
+@pytest.mark.parametrize("W,H", [(1920, 1080), (130, 1200), (2002, 34), (66, 4)])
+def test_composition_cache_policy_variants_bit_identical(soc, monkeypatch, W, H):
+    """The non-temporal load/store variant of the fast path (default) gives the plain variant's bits, and so do the
+    pixel pair's AO taps as one 8-B row load per row (SOC_COMP_AOP, default) against per-texel byte loads, with and
+    without the fused histogram (same bins), at extents whose half-res AO rows end at every byte of a dword."""
     g, gb = sponza_inputs(W, H)
     shadow = dev(random_shadow(256, seed=3))
     rng = np.random.default_rng(5)
-    ssao = dev(rng.integers(120, 256, (H // 2, W // 2), dtype=np.uint8))
+    ssao = dev(rng.integers(0, 256, (H // 2, W // 2), dtype=np.uint8))
     clouds = dev(rng.integers(0, 256, (H, W, 4), dtype=np.uint8))
     ins = [dev(gb[k]) for k in ("albedo", "emissive", "normal", "depth")]
-    outs = []
-    for nt in ("3", "0"):
+    outs, bins = [], []
+    for nt, aop in (("3", "1"), ("3", "0"), ("0", "1"), ("0", "0")):
         monkeypatch.setenv("SOC_COMP_NT", nt)
+        monkeypatch.setenv("SOC_COMP_AOP", aop)
         soc.reload_tuning()
         out = torch.zeros(H, W, 4, dtype=torch.float16, device=DEV)
         soc.composition(g, out, *ins, ssao, shadow, clouds)
         outs.append(host(out))
-    assert np.array_equal(outs[0].view(np.uint16), outs[1].view(np.uint16))
+        out2 = torch.zeros(H, W, 4, dtype=torch.float16, device=DEV)
+        ae = soc.auto_exposure_buffer()
+        soc.composition_luminance_histogram(g, out2, *ins, ssao, shadow, clouds, ae, soc.histogram_scratch())
+        assert np.array_equal(host(out2).view(np.uint16), outs[-1].view(np.uint16))
+        bins.append(host(ae))
+    monkeypatch.delenv("SOC_COMP_NT")
+    monkeypatch.delenv("SOC_COMP_AOP")
+    soc.reload_tuning()
+    for o, b in zip(outs[1:], bins[1:]):
+        assert np.array_equal(outs[0].view(np.uint16), o.view(np.uint16))
+        assert np.array_equal(bins[0], b)
 
 
 @pytest.mark.parametrize("W,H,inputs", [(64, 36, "boxes"), (97, 55, "boxes"), (512, 288, "boxes"), (1920, 1080, "boxes"),
