@@ -140,17 +140,55 @@ struct SsaoPixel {
     float A1, B1;
 };
 
+// The per-pixel fetches of the setup: the normal sample, the random vector, and (SsaoDepth) the centre depth tap.
+struct SsaoFetch {
+    f4 nn;
+    float2 rv2;
+};
+
 template <bool TABLE>
-__device__ __forceinline__ SsaoPixel ssao_setup(int x, int y, const DImg& depth, const DImg& normal, const DImg& target,
+__device__ __forceinline__ SsaoFetch ssao_fetch(int x, int y, float u, float v, const DImg& normal, const DImg& target,
                                                 const float2* __restrict__ table, const SsaoParams& p) {
+    SsaoFetch f;
+    f.nn = sample_h4(normal, u, v);   // normal = mat3(view) * normalize(texture(normal, uv).rgb), :178
+    f.rv2 = TABLE ? table[(size_t)y * target.w + x] : ssao_random_vec(u, v, p.noise_w);
+    return f;
+}
+
+// ssao_fetch in two halves: the loads (issued early, their values not yet used) and the bilinear of the normal
+// (sample_h4's taps and arithmetic: the same bits). Needs normal.w >= 2 and the table (the tiled kernel's case).
+struct SsaoFetchRaw {
+    soc_u4a4 p0, p1;
+    Axis ax, ay;
+    float2 rv2;
+};
+__device__ __forceinline__ SsaoFetchRaw ssao_fetch_issue(int x, int y, float u, float v, const DImg& normal,
+                                                         const DImg& target, const float2* __restrict__ table) {
+    SsaoFetchRaw r;
+    r.ax = axis_clamp(u, normal.w);
+    r.ay = axis_clamp(v, normal.h);
+    r.p0 = *reinterpret_cast<const soc_u4a4*>(row_ptr<uint2>(normal, r.ay.i0) + r.ax.i0);
+    r.p1 = *reinterpret_cast<const soc_u4a4*>(row_ptr<uint2>(normal, r.ay.i1) + r.ax.i0);
+    r.rv2 = table[(size_t)y * target.w + x];
+    return r;
+}
+__device__ __forceinline__ SsaoFetch ssao_fetch_finish(const SsaoFetchRaw& r) {
+    SsaoFetch f;
+    f.nn = bilerp4(unpack_h4(uint2{r.p0.x, r.p0.y}), unpack_h4(uint2{r.p0.z, r.p0.w}), unpack_h4(uint2{r.p1.x, r.p1.y}),
+                   unpack_h4(uint2{r.p1.z, r.p1.w}), r.ax.w, r.ay.w);
+    f.rv2 = r.rv2;
+    return f;
+}
+
+// ssao_setup given the fetches; depth_at(u, v) returns the centre depth tap (depth_tap, or the same texels from LDS).
+template <class DepthAt>
+__device__ __forceinline__ SsaoPixel ssao_setup_from(float u, float v, const SsaoFetch& f, const DepthAt& depth_at,
+                                                     const SsaoParams& p) {
     // no implicit contraction: every fused multiply-add below is an explicit fma, so the per-pixel arithmetic does not
     // depend on how the surrounding kernel is unrolled or scheduled (ssao_kernel and ssao_lds_kernel give the same bits)
 #pragma clang fp contract(off)
     SsaoPixel px;
-    const float u = centre_uv_rn(x, target.w, p.rw), v = centre_uv_rn(y, target.h, p.rh);
-
-    // normal = mat3(view) * normalize(texture(normal, uv).rgb), :178
-    const f4 nn = sample_h4(normal, u, v);
+    const f4 nn = f.nn;
     // A zero normal (the G-buffer's clear value: sky) normalises to NaN; every sample's s.z + bias is then NaN,
     // no comparison adds occlusion, and the result is 1 - 0 / kernel_size = 255 whatever the taps read. Write
     // it without the 26 taps (the same bits as the full evaluation).
@@ -159,7 +197,7 @@ __device__ __forceinline__ SsaoPixel ssao_setup(int x, int y, const DImg& depth,
     // frag_position = get_view_position_from_depth(in_uv, depth), :177: inv_proj (ndc, depth, 1) as fma chains, then
     // one reciprocal of w for the three divisions (the setup is a quarter of the pass's instructions; within the
     // SSAO tolerance of DESIGN.md §5)
-    const float d = depth_tap(depth, u, v);
+    const float d = depth_at(u, v);
     const float* IP = p.inv_proj.m;
     const float ex = u * 2.0f - 1.0f, ey = v * 2.0f - 1.0f;
     auto ip_row = [&](int r) {
@@ -176,7 +214,7 @@ __device__ __forceinline__ SsaoPixel ssao_setup(int x, int y, const DImg& depth,
                     __builtin_fmaf(V[9], nu.z, __builtin_fmaf(V[5], nu.y, V[1] * nu.x)),
                     __builtin_fmaf(V[10], nu.z, __builtin_fmaf(V[6], nu.y, V[2] * nu.x))};
 
-    float2 rv2 = TABLE ? table[(size_t)y * target.w + x] : ssao_random_vec(u, v, p.noise_w);
+    const float2 rv2 = f.rv2;
     // tangent = normalize(rv - n dot(rv, n)) with rv.z = 0 (a zero vector gives NaN, as normalize does)
     const float rn = __builtin_fmaf(rv2.y, n.y, rv2.x * n.x);
     const f3 tu = f3{__builtin_fmaf(-n.x, rn, rv2.x), __builtin_fmaf(-n.y, rn, rv2.y), -n.z * rn};
@@ -210,14 +248,32 @@ __device__ __forceinline__ SsaoPixel ssao_setup(int x, int y, const DImg& depth,
     return px;
 }
 
+template <bool TABLE>
+__device__ __forceinline__ SsaoPixel ssao_setup(int x, int y, const DImg& depth, const DImg& normal, const DImg& target,
+                                                const float2* __restrict__ table, const SsaoParams& p) {
+    const float u = centre_uv_rn(x, target.w, p.rw), v = centre_uv_rn(y, target.h, p.rh);
+    return ssao_setup_from(u, v, ssao_fetch<TABLE>(x, y, u, v, normal, target, table, p),
+                           [&](float uu, float vv) { return depth_tap(depth, uu, vv); }, p);
+}
+
 // One half-res pixel of SSAOGenerationTask (:176-214); `quad` fetches a tap's 2x2 D32 texels.
 // PK (sparse inverse projection, full kernel only): the taps in pairs, the affine forms, weights, range test and
 // smoothstep of both taps as packed f32 operations; per tap the same operations in the same order (bit-identical).
+template <bool SPARSE_IP, bool FULL, class Quad, int UNROLL = SOC_SSAO_MAX_KERNEL, bool PK = false>
+__device__ __forceinline__ void ssao_pixel_px(int x, int y, const SsaoPixel& px, const DImg& depth, const DImg& target,
+                                              const SsaoParams& p, const Quad& quad);
+
 template <bool TABLE, bool SPARSE_IP, bool FULL, class Quad, int UNROLL = SOC_SSAO_MAX_KERNEL, bool PK = false>
 __device__ __forceinline__ void ssao_pixel(int x, int y, const DImg& depth, const DImg& normal, const DImg& target,
                                            const float2* __restrict__ table, const SsaoParams& p, const Quad& quad) {
+    ssao_pixel_px<SPARSE_IP, FULL, Quad, UNROLL, PK>(x, y, ssao_setup<TABLE>(x, y, depth, normal, target, table, p), depth,
+                                                    target, p, quad);
+}
+
+template <bool SPARSE_IP, bool FULL, class Quad, int UNROLL, bool PK>
+__device__ __forceinline__ void ssao_pixel_px(int x, int y, const SsaoPixel& px, const DImg& depth, const DImg& target,
+                                              const SsaoParams& p, const Quad& quad) {
 #pragma clang fp contract(off)
-    const SsaoPixel px = ssao_setup<TABLE>(x, y, depth, normal, target, table, p);
     if (px.skip) {
         row_ptr_w<uint8_t>(target, y)[x] = 255;
         return;
@@ -356,6 +412,33 @@ struct LdsQuad {
     }
 };
 
+// Stage the workgroup's depth tile: rows clamped into the image; columns left of the image give a negative
+// (out-of-range) offset, which the buffer load returns as 0. No tap reads a texel outside the image (taps clamp to
+// [0, n - 2]). Every lane issues all its 16-B loads before its first LDS store (one memory latency, not one per load).
+template <int TXP, int TYP, int HALO>
+__device__ __forceinline__ void ssao_stage_tile(float4* tile4, __amdgpu_buffer_rsrc_t rsrc, const DImg& depth, int gx0, int gy0,
+                                                int tid) {
+    using T = SsaoTile<TXP, TYP, HALO>;
+    constexpr int Q = T::TW / 4, N = Q * T::TH, K = (N + T::THREADS - 1) / T::THREADS;
+    float4 v[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int i = tid + k * T::THREADS;
+        if (N % T::THREADS == 0 || i < N) {
+            const int r = i / Q, c = i - r * Q;
+            const int gy = min(max(gy0 + r, 0), depth.h - 1);
+            const int off = __mul24(gy, depth.pitch) + (gx0 + 4 * c) * 4;
+            const auto w = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0);
+            v[k] = make_float4(__uint_as_float(w[0]), __uint_as_float(w[1]), __uint_as_float(w[2]), __uint_as_float(w[3]));
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int i = tid + k * T::THREADS;
+        if (N % T::THREADS == 0 || i < N) tile4[i] = v[k];
+    }
+}
+
 // The default tile: 64 x 16 half-res pixels (1024 lanes), a 32-texel halo (tile sweep: profiles/r03_ssao_tile_sweep.txt);
 // kSsaoTileLanes is the launch bound its launcher checks.
 #ifndef SOC_SSAO_TILE_TX
@@ -369,7 +452,13 @@ struct LdsQuad {
 #endif
 constexpr int kSsaoTX = SOC_SSAO_TILE_TX, kSsaoTY = SOC_SSAO_TILE_TY, kSsaoHalo = SOC_SSAO_HALO, kSsaoTileLanes = kSsaoTX * kSsaoTY;
 
-template <bool TABLE, bool SPARSE_IP, bool FULL, int TXP, int TYP, int HALO, int UNROLL, bool PK = false>
+// EARLY (tuning knob SOC_SSAO_EARLY): 2 (default) stages the tile with every load of a lane issued before its first LDS
+// store (ssao_stage_tile; the round-4 loop waited on each load in turn); 1 in addition fetches the pixel's normal texels
+// and random vector before the workgroup barrier (their latency overlaps the staging) and reads its centre depth tap
+// from the staged tile; 0 = the round-4 kernel. The same texels and arithmetic, so the same bits (GPU identity test).
+// Measured alone (C3 / C4): 98.8 / 77.2 us (0), 97.8 / 74.5 (1), 97.0 / 73.5 (2); the frame unchanged
+// (profiles/r05_probe_ssao_early.txt).
+template <bool TABLE, bool SPARSE_IP, bool FULL, int TXP, int TYP, int HALO, int UNROLL, bool PK = false, int EARLY = 0>
 __global__ __attribute__((amdgpu_flat_work_group_size(TXP * TYP, TXP * TYP)))
 __attribute__((amdgpu_waves_per_eu(TXP * TYP >= 1024 ? 8 : TXP * TYP >= 512 ? 4 : 2)))
 void ssao_lds_kernel(DImg depth, DImg normal, DImg target, const float2* __restrict__ table, SsaoParams p) {
@@ -380,15 +469,40 @@ void ssao_lds_kernel(DImg depth, DImg normal, DImg target, const float2* __restr
     const int tid = threadIdx.x;
     const int gx0 = bx * 2 * TXP - HALO, gy0 = by * 2 * TYP - HALO;
     const __amdgpu_buffer_rsrc_t rsrc = depth_rsrc(depth);
+    if constexpr (EARLY == 1) {
+        const int w = tid >> 6, lane = tid & 63;
+        const int x = bx * TXP + (w % (TXP / 32)) * 32 + (lane & 31), y = by * TYP + (w / (TXP / 32)) * 2 + (lane >> 5);
+        const bool inside = x < target.w && y < target.h;
+        const float u = centre_uv_rn(x, target.w, p.rw), v = centre_uv_rn(y, target.h, p.rh);
+        static_assert(TABLE, "the early fetch reads the random-vector table");
+        SsaoFetchRaw fr{};
+        if (inside) fr = ssao_fetch_issue(x, y, u, v, normal, target, table);
+        ssao_stage_tile<TXP, TYP, HALO>(tile4, rsrc, depth, gx0, gy0, tid);
+        __syncthreads();
+        if (!inside) return;
+        const float* tile = reinterpret_cast<const float*>(tile4);
+        const SsaoPixel px = ssao_setup_from(u, v, ssao_fetch_finish(fr), [&](float uu, float vv) {
+            const Axis ax = axis_clamp(uu, depth.w), ay = axis_clamp(vv, depth.h);
+            const int i = (ay.i0 - gy0) * T::TW + (ax.i0 - gx0);
+            return bilerp1(tile[i], tile[i + 1], tile[i + T::TW], tile[i + T::TW + 1], ax.w, ay.w);
+        }, p);
+        const LdsQuad<TXP, TYP, HALO> quad{tile, gx0, gy0, GlobalQuad{rsrc, depth.pitch}};
+        ssao_pixel_px<SPARSE_IP, FULL, LdsQuad<TXP, TYP, HALO>, UNROLL, PK>(x, y, px, depth, target, p, quad);
+        return;
+    }
     // stage the tile: rows clamped into the image; columns left of the image give a negative (out-of-range) offset,
     // which the buffer load returns as 0. No tap reads a texel outside the image (taps clamp to [0, n - 2]).
-    constexpr int Q = T::TW / 4;
-    for (int i = tid; i < Q * T::TH; i += T::THREADS) {
-        const int r = i / Q, c = i - r * Q;
-        const int gy = min(max(gy0 + r, 0), depth.h - 1);
-        const int off = __mul24(gy, depth.pitch) + (gx0 + 4 * c) * 4;
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0);
-        tile4[i] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+    if constexpr (EARLY == 2) {
+        ssao_stage_tile<TXP, TYP, HALO>(tile4, rsrc, depth, gx0, gy0, tid);
+    } else {
+        constexpr int Q = T::TW / 4;
+        for (int i = tid; i < Q * T::TH; i += T::THREADS) {
+            const int r = i / Q, c = i - r * Q;
+            const int gy = min(max(gy0 + r, 0), depth.h - 1);
+            const int off = __mul24(gy, depth.pitch) + (gx0 + 4 * c) * 4;
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0);
+            tile4[i] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+        }
     }
     __syncthreads();
     const int w = tid >> 6, lane = tid & 63;
@@ -505,8 +619,18 @@ extern "C" int soc_ssao_generation(const soc_globals* g, soc_img depth, soc_img 
         SsaoParams pt = p;
         pt.swz = 1;
         const dim3 g(ceil_div(target.width, kSsaoTX), ceil_div(target.height, kSsaoTY));
-        launch("ssao_lds_kernel", kSsaoTileLanes, ssao_lds_kernel<true, true, true, kSsaoTX, kSsaoTY, kSsaoHalo, 2, true>, g,
-               kSsaoTileLanes, 0, st, dd, dn, dt, tb, pt);
+        const int early = tuning_knob("SOC_SSAO_EARLY", 2);
+        if (early == 1)
+            launch("ssao_lds_kernel", kSsaoTileLanes,
+                   ssao_lds_kernel<true, true, true, kSsaoTX, kSsaoTY, kSsaoHalo, 2, true, 1>, g, kSsaoTileLanes, 0, st, dd,
+                   dn, dt, tb, pt);
+        else if (early == 2)
+            launch("ssao_lds_kernel", kSsaoTileLanes,
+                   ssao_lds_kernel<true, true, true, kSsaoTX, kSsaoTY, kSsaoHalo, 2, true, 2>, g, kSsaoTileLanes, 0, st, dd,
+                   dn, dt, tb, pt);
+        else
+            launch("ssao_lds_kernel", kSsaoTileLanes, ssao_lds_kernel<true, true, true, kSsaoTX, kSsaoTY, kSsaoHalo, 2, true>,
+                   g, kSsaoTileLanes, 0, st, dd, dn, dt, tb, pt);
     } else if (noise_table && sip && full) SOC_SSAO_LAUNCH(true, true, true);
     else if (noise_table && sip) SOC_SSAO_LAUNCH(true, true, false);
     else if (noise_table) SOC_SSAO_LAUNCH(true, false, false);

@@ -174,7 +174,8 @@ def test_ssao_noise_table_is_bit_identical(soc):
                                          (130, 1200, "boxes"), (2000, 34, "boxes")])
 def test_ssao_tile_orders_bit_identical(soc, monkeypatch, W, H, inputs):
     """The LDS-tiled kernel (default: depth tile + 32-texel halo in LDS, the other taps gathered) and the plain gather
-    kernel (SOC_SSAO_TILE=0) give the same bits, in every workgroup order of the gather kernel (row-major, XCD-aware
+    kernel (SOC_SSAO_TILE=0) give the same bits (the tiled kernel with its per-pixel fetches issued before the barrier
+    and the centre depth from the tile, SOC_SSAO_EARLY=1; its staging loads all issued first, 2, the default; neither, 0), in every workgroup order of the gather kernel (row-major, XCD-aware
     eighths, horizontal and vertical XCD bands: SOC_SWZ_SSAO; the orders are bijections, also for ragged grids), on the
     box atrium and on the mesh (near geometry: many taps leave the tile), at odd, tall and wide extents (partial tiles,
     tiles hanging over every image edge)."""
@@ -190,8 +191,10 @@ def test_ssao_tile_orders_bit_identical(soc, monkeypatch, W, H, inputs):
         depth, normal = dev(gb["depth"]), dev(gb["normal"])
     table = torch.zeros((H // 2) * (W // 2) * 2, dtype=torch.float32, device=DEV)
     outs = []
-    for tile, swz in (("1", None), ("0", "0"), ("0", "1"), ("0", "4"), ("0", "16"), ("0", "-16"), ("0", "-3")):
+    for tile, swz, early in (("1", None, "1"), ("1", None, "0"), ("1", None, "2"), ("0", "0", "1"), ("0", "1", "1"),
+                             ("0", "4", "1"), ("0", "16", "1"), ("0", "-16", "1"), ("0", "-3", "1")):
         monkeypatch.setenv("SOC_SSAO_TILE", tile)
+        monkeypatch.setenv("SOC_SSAO_EARLY", early)
         if swz is None:
             monkeypatch.delenv("SOC_SWZ_SSAO", raising=False)
         else:
@@ -202,6 +205,7 @@ def test_ssao_tile_orders_bit_identical(soc, monkeypatch, W, H, inputs):
         soc.ssao_generation(g, depth, normal, out, table)
         outs.append(host(out))
     monkeypatch.delenv("SOC_SSAO_TILE")
+    monkeypatch.delenv("SOC_SSAO_EARLY")
     monkeypatch.delenv("SOC_SWZ_SSAO", raising=False)
     soc.reload_tuning()
     for o in outs[1:]:
