@@ -26,6 +26,8 @@ constexpr int kNoise = 64, kNoiseMask = 63;
 // LDS quad table: 81 x 81 entries (64 + the 17-texel tap offset), so the second tap of get_3d_noise is
 // the first tap's address plus a constant (an immediate ds_read offset) with no wrap arithmetic.
 constexpr int kTap2 = 17, kTW = kNoise + kTap2, kTable = kTW * kTW;
+// the quad tables padded to whole 16-B chunks (prebuilt in the workspace by clouds_od_lut, copied into LDS)
+constexpr int kTableU32 = (kTable + 3) & ~3, kTableU2 = (kTable + 1) & ~1;
 constexpr float kEarthRadius = 6371000.0f, kMinH = 1600.0f, kMaxH = 500.0f + 1600.0f, kSunBrightness = 3.0f;
 constexpr float kPi = 3.14159265358979f;   // acos(-1.0) in fp32
 constexpr float kLn2 = 0.693147182f;       // log(2.0) in fp32
@@ -342,9 +344,40 @@ struct OdLut {
     float C2;
 };
 
+// Entry i of the quad tables stage_noise / stage_noise_wide build (the same bytes).
+template <bool NOISE_R8>
+__device__ __forceinline__ uint4 noise_quad_texels(const DImg& noise, int i) {
+    const int ny = i / kTW, nx = (i - ny * kTW) & kNoiseMask;
+    const int nyw = ny & kNoiseMask;
+    const int nx1 = (nx + 1) & kNoiseMask, ny1 = (nyw + 1) & kNoiseMask;
+    auto texel = [&](int tx, int ty) -> uint32_t {
+        if (NOISE_R8) return row_ptr<uint8_t>(noise, ty)[tx];
+        return row_ptr<uint32_t>(noise, ty)[tx] & 0xffu;
+    };
+    return uint4{texel(nx, nyw), texel(nx1, nyw), texel(nx, ny1), texel(nx1, ny1)};
+}
+
 // zero: the frame's 256-B counter block, cleared here (the lane's first kernel) instead of by a separate fill launch
-__global__ __launch_bounds__(kWorkgroup) void clouds_od_lut(float2* __restrict__ lut, float C2, uint32_t* __restrict__ zero) {
+// Blocks past the table's (lut_blocks) build the frame's noise quad tables (noise_quads: 4 bytes per entry, as
+// stage_noise; noise_wide: 16-bit pairs, as stage_noise_wide; the padding entries zero) for the march kernels' LDS.
+template <bool NOISE_R8>
+__global__ __launch_bounds__(kWorkgroup) void clouds_od_lut(float2* __restrict__ lut, float C2, uint32_t* __restrict__ zero,
+                                                     int lut_blocks, DImg noise, uint32_t* __restrict__ noise_quads,
+                                                     uint2* __restrict__ noise_wide) {
+    if ((int)blockIdx.x >= lut_blocks) {
+        const int e = (int)(blockIdx.x - lut_blocks) * kWorkgroup + (int)threadIdx.x;
+        if (e >= kTableU32) return;
+        uint4 t = uint4{0u, 0u, 0u, 0u};
+        if (e < kTable) t = noise_quad_texels<NOISE_R8>(noise, e);
+        noise_quads[e] = t.x | (t.y << 8) | (t.z << 16) | (t.w << 24);
+        if (e < kTableU2) noise_wide[e] = uint2{t.x | (t.y << 16), t.z | (t.w << 16)};
+        return;
+    }
     const int i = (int)(blockIdx.x * kWorkgroup + threadIdx.x);
+    if (!lut) {
+        if (i < 64) zero[i] = 0u;
+        return;
+    }
     if (i < 64) zero[i] = 0u;
     if (i >= kOdR * kOdM) return;
     const int ir = i / kOdM, im = i - ir * kOdM;
@@ -564,6 +597,25 @@ __device__ __forceinline__ void stage_noise_wide(const DImg& noise, uint2* quads
     }
 }
 
+// Copy a prebuilt quad table (N16 16-B chunks) into LDS: each lane issues its loads in batches of 4 before their LDS
+// stores (the per-texel staging loop took 4 byte loads per entry and waited on every round: 26 rounds for a
+// 256-lane workgroup).
+template <int N16>
+__device__ __forceinline__ void stage_noise_table(const uint4* __restrict__ src, uint4* dst, int tid, int nthreads) {
+    for (int k0 = tid; k0 < N16; k0 += 4 * nthreads) {
+        const int k1 = k0 + nthreads, k2 = k1 + nthreads, k3 = k2 + nthreads;
+        const uint4 a = src[k0];
+        uint4 b = uint4{0u, 0u, 0u, 0u}, c = b, d = b;
+        if (k1 < N16) b = src[k1];
+        if (k2 < N16) c = src[k2];
+        if (k3 < N16) d = src[k3];
+        dst[k0] = a;
+        if (k1 < N16) dst[k1] = b;
+        if (k2 < N16) dst[k2] = c;
+        if (k3 < N16) dst[k3] = d;
+    }
+}
+
 __device__ __forceinline__ bool is_sky(const CloudParams& p, const DImg& depth, int x, int y) {
     return sample_f32(depth, div_rn((float)x, p.res_x_m1, p.r_res_x_m1), div_rn((float)y, p.res_y_m1, p.r_res_y_m1)) ==
            1.0f;   // textureLod(depth, ray_uv, 0), :458
@@ -714,6 +766,8 @@ struct PairBufs {
                           // it; store_geom == 0: they re-derive it from the list entry, the same bits)
     float* od_tmp;        // [od_blocks][24][256]: per density workgroup, the od of its current batch's dense steps until
                           // their pair slots are known; density then stores od in od[slot], and sunvis only adds vis
+    const uint32_t* noise_quads;  // [kTableU32] the frame's noise quad table (clouds_od_lut), or nullptr: stage_noise
+    const uint2* noise_wide;      // [kTableU2] the same as 16-bit pairs (stage_noise_wide)
     uint32_t store_geom;  // tuning knob SOC_CLOUDS_GEOM
     uint32_t od_blocks;   // density workgroups the od scratch holds (the density grid is clamped to it)
     uint32_t n;           // list capacity (W*H)
@@ -786,13 +840,15 @@ template <bool NOISE_R8>
 // 6 waves/SIMD: 80 VGPRs with 20 B of scratch, measured faster than 5 waves without a spill (profiles/r04_probe_clouds_scan.txt)
 __global__ __launch_bounds__(kWorkgroup) __attribute__((amdgpu_waves_per_eu(6))) void clouds_density(
     DImg noise, CloudParams p, const uint32_t* __restrict__ counter, const uint32_t* __restrict__ list, PairBufs pb) {
-    __shared__ uint32_t quads[kTable];
+    __shared__ uint4 quads4[kTableU32 / 4];
+    uint32_t* quads = reinterpret_cast<uint32_t*>(quads4);
     __shared__ uint32_t offs[25][4];
     __shared__ uint32_t wg_base;
     const uint32_t count = *counter;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (blockIdx.x * 256u >= count) return;
-    stage_noise<NOISE_R8>(noise, quads, tid, 256);
+    if (pb.noise_quads) stage_noise_table<kTableU32 / 4>(reinterpret_cast<const uint4*>(pb.noise_quads), quads4, tid, 256);
+    else stage_noise<NOISE_R8>(noise, quads, tid, 256);
     __syncthreads();
     Ctx cx;
     cx.quads = quads;
@@ -869,7 +925,9 @@ template <bool NOISE_R8, uint32_t kSunvisThreads, bool WIDE = false>
 __global__ __launch_bounds__(kSunvisThreads) __attribute__((amdgpu_waves_per_eu(kSunvisThreads == 512 && !WIDE ? 8 : 6))) void clouds_sunvis(
     DImg noise, CloudParams p, const uint32_t* __restrict__ list, PairBufs pb) {
     using Q = typename std::conditional<WIDE, uint2, uint32_t>::type;
-    __shared__ Q quads[kTable];
+    constexpr int kN16 = WIDE ? kTableU2 / 2 : kTableU32 / 4;
+    __shared__ uint4 quads4[kN16];
+    Q* quads = reinterpret_cast<Q*>(quads4);
     __shared__ uint32_t pre[kShards + 1];
     const uint32_t tid = threadIdx.x;
     if (tid == 0) {
@@ -883,7 +941,9 @@ __global__ __launch_bounds__(kSunvisThreads) __attribute__((amdgpu_waves_per_eu(
     __syncthreads();
     const uint32_t total = pre[kShards];
     if (blockIdx.x * kSunvisThreads >= total) return;
-    if constexpr (WIDE) stage_noise_wide<NOISE_R8>(noise, quads, tid, kSunvisThreads);
+    const void* pre_tab = WIDE ? static_cast<const void*>(pb.noise_wide) : static_cast<const void*>(pb.noise_quads);
+    if (pre_tab) stage_noise_table<kN16>(static_cast<const uint4*>(pre_tab), quads4, tid, kSunvisThreads);
+    else if constexpr (WIDE) stage_noise_wide<NOISE_R8>(noise, quads, tid, kSunvisThreads);
     else stage_noise<NOISE_R8>(noise, quads, tid, kSunvisThreads);
     __syncthreads();
     CtxT<Q> cx;
@@ -1026,6 +1086,8 @@ struct CloudWs {
     float4* atmos;
     PairBufs pb;
     float2* od_lut;   // secondary-ray optical-depth table (kOdR x kOdM)
+    uint32_t* noise_quads;   // [kTableU32] noise quad tables (clouds_od_lut)
+    uint2* noise_wide;       // [kTableU2]
     float4* sky_tab;  // sky-view table (kSvEntries x 2 float4)
     size_t bytes;
 };
@@ -1061,6 +1123,10 @@ CloudWs cloud_ws_layout(void* base, size_t n) {
     off = al(off + (size_t)kOdR * kOdM * sizeof(float2));
     w.sky_tab = reinterpret_cast<float4*>(b + off);
     off = al(off + (size_t)kSvEntries * 2 * sizeof(float4));
+    w.noise_quads = reinterpret_cast<uint32_t*>(b + off);
+    off = al(off + (size_t)kTableU32 * 4);
+    w.noise_wide = reinterpret_cast<uint2*>(b + off);
+    off = al(off + (size_t)kTableU2 * 8);
     w.bytes = off;
     return w;
 }
@@ -1116,14 +1182,25 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
     uint32_t* list = ws.list;
     // the frame's secondary-ray table (SOC_CLOUDS_OD_LUT=0: march every secondary ray, the single-lane kernel's bits);
     // its kernel also clears the counter block, else a fill does
+    // The same kernel builds the frame's noise quad tables (SOC_CLOUDS_NOISE_TABLE=0: each march workgroup stages them
+    // from the noise image texel by texel, the same bytes).
     OdLut lut{nullptr, 0.0f};
-    if (SOC_CLOUDS_PROFILE < 4 && tuning_knob("SOC_CLOUDS_OD_LUT", 1)) {
-        const float C2 = p.sun[0] * p.sun[0] + p.sun[1] * p.sun[1] + p.sun[2] * p.sun[2];   // dot3(pSun, pSun)
-        lut = OdLut{ws.od_lut, C2};
-        launch("clouds_od_lut", kWorkgroup, clouds_od_lut, ceil_div(kOdR * kOdM, kWorkgroup), kWorkgroup, 0, s, ws.od_lut, C2, counter);
-    } else {
-        hipError_t e = hipMemsetAsync(counter, 0, 256, s);
-        if (e != hipSuccess) return set_error(SOC_E_HIP, "%s: %s", P, hipGetErrorString(e));
+    const bool use_lut = SOC_CLOUDS_PROFILE < 4 && tuning_knob("SOC_CLOUDS_OD_LUT", 1);
+    const bool noise_tab = tuning_knob("SOC_CLOUDS_NOISE_TABLE", 1) != 0;
+    const float C2 = p.sun[0] * p.sun[0] + p.sun[1] * p.sun[1] + p.sun[2] * p.sun[2];   // dot3(pSun, pSun)
+    if (use_lut) lut = OdLut{ws.od_lut, C2};
+    ws.pb.noise_quads = noise_tab ? ws.noise_quads : nullptr;
+    ws.pb.noise_wide = noise_tab ? ws.noise_wide : nullptr;
+    {
+        const int lut_blocks = use_lut ? ceil_div(kOdR * kOdM, kWorkgroup) : 1;
+        const int blocks_all = lut_blocks + (noise_tab ? ceil_div(kTableU32, kWorkgroup) : 0);
+        float2* lt = use_lut ? ws.od_lut : nullptr;
+        if (noise.format == SOC_FMT_R8_UNORM)
+            launch("clouds_od_lut", kWorkgroup, clouds_od_lut<true>, blocks_all, kWorkgroup, 0, s, lt, C2, counter, lut_blocks,
+                   dimg(noise), ws.noise_quads, ws.noise_wide);
+        else
+            launch("clouds_od_lut", kWorkgroup, clouds_od_lut<false>, blocks_all, kWorkgroup, 0, s, lt, C2, counter, lut_blocks,
+                   dimg(noise), ws.noise_quads, ws.noise_wide);
     }
     const int vec_store = (target.pitch_bytes % 16 == 0) && (reinterpret_cast<uintptr_t>(target.data) % 16 == 0);
     launch("clouds_classify", kWorkgroup, clouds_classify, dim3(ceil_div(W, 64), ceil_div(H, 16 * kClassifyTiles)), kWorkgroup, 0, s,

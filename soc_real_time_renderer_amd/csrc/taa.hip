@@ -410,7 +410,9 @@ constexpr int kTaaTQ = kTaaPairs / 2 + 2;                         // staged dept
 
 constexpr int kTaaLdsRows = 4;                                   // rows per workgroup: 4 measured against 2 and 8
 constexpr int kTaaLdsLanes = 64 * kTaaLdsRows;                    // (profiles/r03_ab_taa_lds.txt); the launch bound
-template <bool TM, int kTaaRows = kTaaLdsRows>
+// SF (SOC_TAA_NBR=4, default): every staging load of a lane is issued before its first LDS store, so the staging costs
+// one memory latency instead of one per loop round (2 colour / velocity rounds and a depth round); the same values.
+template <bool TM, int kTaaRows = kTaaLdsRows, bool SF = false>
 __global__ __launch_bounds__(64 * kTaaRows) void taa_lds(DImg target, DImg cur, DImg prev, DImg vel, DImg pvel, DImg depth,
                                                          DImg vel_out, TaaParams p, TmOut tm) {
     constexpr int kTaaTR = kTaaRows + 2, NT = 64 * kTaaRows;   // staged rows y0 - 1 .. y0 + kTaaRows
@@ -425,18 +427,56 @@ __global__ __launch_bounds__(64 * kTaaRows) void taa_lds(DImg target, DImg cur, 
     const int npairs = W >> 1, nquads = (W + 3) >> 2;
     // staging: rows clamped into the image, pairs / quads clamped into the row (the clamped copies are never read:
     // the border columns come from the lane's own pixels, as in taa_pair2)
-    for (int i = tid; i < kTaaTR * kTaaTP; i += NT) {
-        const int r = i / kTaaTP, c = i - r * kTaaTP;
-        const int sy = min(max(y0 - 1 + r, 0), H - 1), sp = min(max(p0 - 1 + c, 0), npairs - 1);
-        ct[r][c] = row_ptr<uint4>(cur, sy)[sp];
-        vt[r][c] = row_ptr<uint4>(vel, sy)[sp];
-    }
-    for (int i = tid; i < kTaaTR * kTaaTQ; i += NT) {
+    auto depth_quad = [&](int i) {
         const int r = i / kTaaTQ, c = i - r * kTaaTQ;
         const int sy = min(max(y0 - 1 + r, 0), H - 1), sq = min(max(q0 - 1 + c, 0), nquads - 1);
         const float* drow = row_ptr<float>(depth, sy);
-        if (4 * sq + 3 < W) dt[r][c] = *reinterpret_cast<const float4*>(drow + 4 * sq);
-        else dt[r][c] = float4{drow[4 * sq], drow[min(4 * sq + 1, W - 1)], drow[min(4 * sq + 2, W - 1)], drow[min(4 * sq + 3, W - 1)]};
+        if (4 * sq + 3 < W) return *reinterpret_cast<const float4*>(drow + 4 * sq);
+        return float4{drow[4 * sq], drow[min(4 * sq + 1, W - 1)], drow[min(4 * sq + 2, W - 1)], drow[min(4 * sq + 3, W - 1)]};
+    };
+    if constexpr (SF) {
+        constexpr int NP = kTaaTR * kTaaTP, ND = kTaaTR * kTaaTQ;
+        static_assert(NP > NT && NP <= 2 * NT && ND <= NT, "two colour / velocity rounds and one depth round");
+        auto pair_off = [&](int i, int& r, int& c, const uint4*& cs, const uint4*& vs) {
+            r = i / kTaaTP;
+            c = i - r * kTaaTP;
+            const int sy = min(max(y0 - 1 + r, 0), H - 1), sp = min(max(p0 - 1 + c, 0), npairs - 1);
+            cs = row_ptr<uint4>(cur, sy) + sp;
+            vs = row_ptr<uint4>(vel, sy) + sp;
+        };
+        int r0, c0, r1, c1;
+        const uint4 *cs0, *vs0, *cs1, *vs1;
+        pair_off(tid, r0, c0, cs0, vs0);
+        const bool second = tid + NT < NP, hasd = tid < ND;
+        pair_off(second ? tid + NT : tid, r1, c1, cs1, vs1);
+        const uint4 ca = *cs0, va = *vs0;
+        uint4 cb = uint4{0u, 0u, 0u, 0u}, vb = cb;
+        if (second) { cb = *cs1; vb = *vs1; }
+        // the depth quad as one 16-B buffer load even for the last quad of a row with W % 4 != 0: its texels past the
+        // row end (the next row's, or 0 past the image) are never read (the border columns come from the pair itself)
+        float4 dq = float4{0.0f, 0.0f, 0.0f, 0.0f};
+        if (hasd) {
+            const int r = tid / kTaaTQ, c = tid - r * kTaaTQ;
+            const int sy = min(max(y0 - 1 + r, 0), H - 1), sq = min(max(q0 - 1 + c, 0), nquads - 1);
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(depth.data, 0, depth.pitch * depth.h, 0x00020000);
+            const auto w = __builtin_amdgcn_raw_buffer_load_b128(rs, __mul24(sy, depth.pitch) + 16 * sq, 0, 0);
+            dq = make_float4(__uint_as_float(w[0]), __uint_as_float(w[1]), __uint_as_float(w[2]), __uint_as_float(w[3]));
+        }
+        ct[r0][c0] = ca;
+        vt[r0][c0] = va;
+        if (second) { ct[r1][c1] = cb; vt[r1][c1] = vb; }
+        if (hasd) dt[tid / kTaaTQ][tid % kTaaTQ] = dq;
+    } else {
+        for (int i = tid; i < kTaaTR * kTaaTP; i += NT) {
+            const int r = i / kTaaTP, c = i - r * kTaaTP;
+            const int sy = min(max(y0 - 1 + r, 0), H - 1), sp = min(max(p0 - 1 + c, 0), npairs - 1);
+            ct[r][c] = row_ptr<uint4>(cur, sy)[sp];
+            vt[r][c] = row_ptr<uint4>(vel, sy)[sp];
+        }
+        for (int i = tid; i < kTaaTR * kTaaTQ; i += NT) {
+            const int r = i / kTaaTQ, c = i - r * kTaaTQ;
+            dt[r][c] = depth_quad(i);
+        }
     }
     __syncthreads();
     const int pl = threadIdx.x, ty = threadIdx.y;
@@ -578,9 +618,19 @@ int taa_launch(const soc_globals* g, soc_img target, soc_img current_color, soc_
         dim3 blk(bxl, by), g2(ceil_div(W / 2, bxl), ceil_div(H, by));
         // neighbourhood source: 3 = LDS-staged tiles (default; needs a 16-B aligned depth image), 2 = halo lanes, 1 = lane
         // shifts + edge-lane loads, 0 = every lane loads its side columns (the same bits, tests/test_gpu_parity.py)
-        const int nbr = tuning_knob("SOC_TAA_NBR", 3);
+        const int nbr = tuning_knob("SOC_TAA_NBR", 4);
         const dim3 blk_h(64, 4), g2_h(ceil_div(W / 2, 62), ceil_div(H, 4));
-        if (nbr == 3 && a16(depth)) {
+        if (nbr == 4 && a16(depth)) {
+            const dim3 gl(ceil_div(W / 2, kTaaPairs), ceil_div(H, 4));
+            if (tm)
+                launch("taa_lds", kTaaLdsLanes, taa_lds<true, kTaaLdsRows, true>, gl, blk_h, 0, hs(stream), dimg(target),
+                       dimg(current_color), dimg(previous_color), dimg(current_velocity), dimg(previous_velocity), dimg(depth), vo,
+                       p, *tm);
+            else
+                launch("taa_lds", kTaaLdsLanes, taa_lds<false, kTaaLdsRows, true>, gl, blk_h, 0, hs(stream), dimg(target),
+                       dimg(current_color), dimg(previous_color), dimg(current_velocity), dimg(previous_velocity), dimg(depth), vo,
+                       p, TmOut{});
+        } else if (nbr == 3 && a16(depth)) {
             const dim3 gl(ceil_div(W / 2, kTaaPairs), ceil_div(H, 4));
             if (tm)
                 launch("taa_lds", kTaaLdsLanes, taa_lds<true>, gl, blk_h, 0, hs(stream), dimg(target), dimg(current_color), dimg(previous_color),

@@ -427,8 +427,8 @@ def test_taa(soc, oracle, W, H, inputs):
 @pytest.mark.parametrize("W,H,noisy", [(100, 40, False), (102, 42, False), (102, 45, True), (1920, 1080, False),
                                        (1920, 1080, True)])
 def test_taa_lane_shift_neighbours_identical(soc, oracle, monkeypatch, W, H, noisy):
-    """Every neighbourhood source gives the bits of the per-lane loads (SOC_TAA_NBR=0): the LDS-staged tiles (3,
-    default), the side columns from the adjacent lanes (DPP wave shifts) with halo-only first / last lanes (2) and with
+    """Every neighbourhood source gives the bits of the per-lane loads (SOC_TAA_NBR=0): the LDS-staged tiles with every
+    staging load issued first (4, default) and staged round by round (3), the side columns from the adjacent lanes (DPP wave shifts) with halo-only first / last lanes (2) and with
     edge-lane loads (1). 100 px: 50
     pairs in one 64-pair LDS tile row (14 lanes past the image) / a 62-pair wave row (12 lanes past), 32-lane block rows
     of which the second has 18 lanes inside; 102 x 42: a partial last depth quad (W % 4 == 2) and a last tile row with
@@ -452,7 +452,7 @@ def test_taa_lane_shift_neighbours_identical(soc, oracle, monkeypatch, W, H, noi
         depth = dp[:, :W]
     ae = soc.auto_exposure_buffer(exposure=0.37)
     outs = []
-    for nbr in ("3", "2", "1", "0"):
+    for nbr in ("4", "3", "2", "1", "0"):
         monkeypatch.setenv("SOC_TAA_NBR", nbr)
         soc.reload_tuning()
         t = torch.zeros(H, W, 4, dtype=torch.float16, device=DEV)
@@ -561,16 +561,34 @@ def test_clouds_pair_path_equals_single_lane(soc, monkeypatch, W, H, pitch, all_
     ws = soc.cloud_rendering_workspace(W, H)
     soc.cloud_rendering(g, dev(depth), dev(gb["noise"]), a, None)
     monkeypatch.setenv("SOC_CLOUDS_OD_LUT", "0")   # every secondary ray marched, as the single-lane kernel does
-    for pos, geom in (("0", "1"), ("1", "1"), ("2", "1"), ("2", "0")):
+    for pos, geom, ntab in (("0", "1", "1"), ("1", "1", "1"), ("2", "1", "1"), ("2", "0", "1"), ("2", "1", "0")):
         monkeypatch.setenv("SOC_CLOUDS_ATMOS_POS", pos)
         monkeypatch.setenv("SOC_CLOUDS_GEOM", geom)   # the march geometry stored by density, or re-derived per pair
+        monkeypatch.setenv("SOC_CLOUDS_NOISE_TABLE", ntab)   # noise quads prebuilt once per frame, or staged per workgroup
         soc.reload_tuning()
         b = torch.zeros_like(a)
         soc.cloud_rendering(g, dev(depth), dev(gb["noise"]), b, ws)
         torch.cuda.synchronize()
-        assert torch.equal(a, b), (pos, geom, (a != b).float().mean().item())
+        assert torch.equal(a, b), (pos, geom, ntab, (a != b).float().mean().item())
+    # with the secondary-ray table (the default) the prebuilt noise quads give the per-workgroup staging's bits too, for
+    # the R8 and the RGBA8 noise image
+    monkeypatch.delenv("SOC_CLOUDS_OD_LUT")
+    noise_rgba = dev(gb["noise"]).clone()
+    noise_rgba[..., 1:] = 77
+    noise_r8 = noise_rgba[..., 0].contiguous()
+    outs = []
+    for nz in (noise_r8, noise_rgba):
+        for ntab in ("1", "0"):
+            monkeypatch.setenv("SOC_CLOUDS_NOISE_TABLE", ntab)
+            soc.reload_tuning()
+            b = torch.zeros_like(a)
+            soc.cloud_rendering(g, dev(depth), nz, b, ws)
+            outs.append(b)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[2], outs[3]) and torch.equal(outs[0], outs[2])
     monkeypatch.delenv("SOC_CLOUDS_ATMOS_POS")
     monkeypatch.delenv("SOC_CLOUDS_GEOM")
+    monkeypatch.delenv("SOC_CLOUDS_NOISE_TABLE")
     soc.reload_tuning()
 
 
