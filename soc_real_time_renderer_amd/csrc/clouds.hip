@@ -836,7 +836,7 @@ __device__ __forceinline__ MarchGeom pair_geometry(const CloudParams& p, const u
     return march_geometry(sky_dir(p, x, y));
 }
 
-template <bool NOISE_R8>
+template <bool NOISE_R8, int DB = 1>
 // 6 waves/SIMD: 80 VGPRs with 20 B of scratch, measured faster than 5 waves without a spill (profiles/r04_probe_clouds_scan.txt)
 __global__ __launch_bounds__(kWorkgroup) __attribute__((amdgpu_waves_per_eu(6))) void clouds_density(
     DImg noise, CloudParams p, const uint32_t* __restrict__ counter, const uint32_t* __restrict__ list, PairBufs pb) {
@@ -905,13 +905,34 @@ __global__ __launch_bounds__(kWorkgroup) __attribute__((amdgpu_waves_per_eu(6)))
             pb.pairs[shard * pb.cap + k] = 0xffffffffu;
         if (i < count) pb.pix_mask[i] = mask | ((slot_base & kInline) ? kInline : 0u);
         if (!(slot_base & kInline) && __ballot(mask != 0u) != 0ull) {   // workgroup-uniform, then wave-uniform
-            // uniform loop: the ballot of every step sees every lane of the wave
-            for (uint32_t st = 0; st < 24; ++st) {
-                const uint32_t rank = mask_ballot_rank(mask, st, lane);
-                if ((mask >> st) & 1u) {
-                    const uint32_t slot = slot_base + pair_offset(offs, st, wave, rank);
-                    pb.pairs[slot] = (i << 5) | st;
-                    pb.od[slot] = od_tmp[st * 256];   // this lane's own write
+            // uniform loop: the ballot of every step sees every lane of the wave. DB > 1: the lane's od scratch of DB
+            // steps is read together (every lane, every step: its own scratch, always in bounds) before the stores, one
+            // memory latency per DB steps instead of one per dense step (the same values)
+            if constexpr (DB == 1) {
+                for (uint32_t st = 0; st < 24; ++st) {
+                    const uint32_t rank = mask_ballot_rank(mask, st, lane);
+                    if ((mask >> st) & 1u) {
+                        const uint32_t slot = slot_base + pair_offset(offs, st, wave, rank);
+                        pb.pairs[slot] = (i << 5) | st;
+                        pb.od[slot] = od_tmp[st * 256];   // this lane's own write
+                    }
+                }
+            } else {
+                static_assert(24 % DB == 0, "whole step batches");
+                for (uint32_t s0 = 0; s0 < 24; s0 += DB) {
+                    float odv[DB];
+#pragma unroll
+                    for (int b = 0; b < DB; ++b) odv[b] = od_tmp[(s0 + b) * 256];
+#pragma unroll
+                    for (int b = 0; b < DB; ++b) {
+                        const uint32_t st = s0 + b;
+                        const uint32_t rank = mask_ballot_rank(mask, st, lane);
+                        if ((mask >> st) & 1u) {
+                            const uint32_t slot = slot_base + pair_offset(offs, st, wave, rank);
+                            pb.pairs[slot] = (i << 5) | st;
+                            pb.od[slot] = odv[b];
+                        }
+                    }
                 }
             }
         }
@@ -970,7 +991,7 @@ __global__ __launch_bounds__(kSunvisThreads) __attribute__((amdgpu_waves_per_eu(
 
 // TAB: the atmosphere colour from the sky-view table here (no clouds_atmosphere launch, no per-pixel colour buffer);
 // else read from the atmosphere kernel's output.
-template <bool NOISE_R8, bool TAB = false>
+template <bool NOISE_R8, bool TAB = false, int RB = 1>
 __global__ __launch_bounds__(kWorkgroup) __attribute__((amdgpu_waves_per_eu(5))) void clouds_resolve(DImg noise, DImg target, CloudParams p, const uint32_t* __restrict__ counter,
                                                       const uint32_t* __restrict__ list, const float4* __restrict__ atmos,
                                                       PairBufs pb, SkyTab st) {
@@ -1037,12 +1058,35 @@ __global__ __launch_bounds__(kWorkgroup) __attribute__((amdgpu_waves_per_eu(5)))
             }
             f3 scattering = f3{0.0f, 0.0f, 0.0f};
             float transmittance = 1.0f;
-            // steps in order; the ballot runs on every lane of the wave (uniform loop)
-            for (uint32_t st = 0; any_dense && st < 24; ++st) {
-                const uint32_t rank = mask_ballot_rank(mask, st, lane);
-                if (march && ((mask >> st) & 1u)) {
-                    const uint32_t slot = base + offs[st][wave] + rank;
-                    march_accumulate(ms, sun_color, pb.od[slot], pb.vis[slot], scattering, transmittance);
+            // steps in order; the ballot runs on every lane of the wave (uniform loop). RB > 1: the od / vis loads of RB
+            // steps are issued together (a lane without that dense step loads slot 0 and discards it), then accumulated
+            // in step order: one memory latency per RB steps instead of one per step (the same values, the same bits)
+            if constexpr (RB == 1) {
+                for (uint32_t st = 0; any_dense && st < 24; ++st) {
+                    const uint32_t rank = mask_ballot_rank(mask, st, lane);
+                    if (march && ((mask >> st) & 1u)) {
+                        const uint32_t slot = base + offs[st][wave] + rank;
+                        march_accumulate(ms, sun_color, pb.od[slot], pb.vis[slot], scattering, transmittance);
+                    }
+                }
+            } else {
+                static_assert(24 % RB == 0, "whole step batches");
+                for (uint32_t s0 = 0; any_dense && s0 < 24; s0 += RB) {
+                    float odv[RB], visv[RB];
+                    uint32_t has = 0u;
+#pragma unroll
+                    for (int b = 0; b < RB; ++b) {
+                        const uint32_t st = s0 + b;
+                        const uint32_t rank = mask_ballot_rank(mask, st, lane);
+                        const bool h = march && ((mask >> st) & 1u);
+                        has |= (h ? 1u : 0u) << b;
+                        const uint32_t slot = h ? base + offs[st][wave] + rank : 0u;
+                        odv[b] = pb.od[slot];
+                        visv[b] = pb.vis[slot];
+                    }
+#pragma unroll
+                    for (int b = 0; b < RB; ++b)
+                        if ((has >> b) & 1u) march_accumulate(ms, sun_color, odv[b], visv[b], scattering, transmittance);
                 }
             }
             if (march) color = march_finish(mg, color, scattering, transmittance);
@@ -1268,20 +1312,32 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
     };
     if (apos == 0) atmos();
     const DImg nz = dimg(noise);
+    // the resolve's od / vis loads issued in batches of this many steps (1: one step at a time)
+    const int rb = tuning_knob("SOC_CLOUDS_RESOLVE_BATCH", 4);
+    // the density kernel's od scratch read back in batches of this many steps (1: one dense step at a time)
+    const int db = tuning_knob("SOC_CLOUDS_DENSITY_BATCH", 8);
     const int density_grid = std::min(grid(res_density, blocks), (int)ws.pb.od_blocks);   // one od scratch per workgroup
     if (r8) {
-        launch("clouds_density", kWorkgroup, clouds_density<true>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
+        if (db == 4) launch("clouds_density", kWorkgroup, clouds_density<true, 4>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
+        else if (db == 8) launch("clouds_density", kWorkgroup, clouds_density<true, 8>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
+        else launch("clouds_density", kWorkgroup, clouds_density<true>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
         if (apos == 1) atmos();
         launch("clouds_sunvis", kSunvisLanes, clouds_sunvis<true, kSunvisLanes, true>, grid(res_sunvis, blocks), kSunvisLanes, 0, s, nz, p, list, ws.pb);
         if (apos == 2) atmos();
-        if (fold) resolve(clouds_resolve<true, true>);
+        if (fold && rb == 4) resolve(clouds_resolve<true, true, 4>);
+        else if (fold && rb == 8) resolve(clouds_resolve<true, true, 8>);
+        else if (fold) resolve(clouds_resolve<true, true>);
         else resolve(clouds_resolve<true, false>);
     } else {
-        launch("clouds_density", kWorkgroup, clouds_density<false>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
+        if (db == 4) launch("clouds_density", kWorkgroup, clouds_density<false, 4>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
+        else if (db == 8) launch("clouds_density", kWorkgroup, clouds_density<false, 8>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
+        else launch("clouds_density", kWorkgroup, clouds_density<false>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
         if (apos == 1) atmos();
         launch("clouds_sunvis", kSunvisLanes, clouds_sunvis<false, kSunvisLanes, true>, grid(res_sunvis, blocks), kSunvisLanes, 0, s, nz, p, list, ws.pb);
         if (apos == 2) atmos();
-        if (fold) resolve(clouds_resolve<false, true>);
+        if (fold && rb == 4) resolve(clouds_resolve<false, true, 4>);
+        else if (fold && rb == 8) resolve(clouds_resolve<false, true, 8>);
+        else if (fold) resolve(clouds_resolve<false, true>);
         else resolve(clouds_resolve<false, false>);
     }
     return check_launch("cloud_rendering");

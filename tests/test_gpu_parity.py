@@ -576,16 +576,23 @@ def test_clouds_pair_path_equals_single_lane(soc, monkeypatch, W, H, pitch, all_
     noise_rgba = dev(gb["noise"]).clone()
     noise_rgba[..., 1:] = 77
     noise_r8 = noise_rgba[..., 0].contiguous()
+    # ... and the resolve's od / vis loads (batches of 4, default, or 8 steps) and the density's od scratch reads (8, default, or 4) give
+    # the one-step loops' bits
     outs = []
     for nz in (noise_r8, noise_rgba):
-        for ntab in ("1", "0"):
+        for ntab, rb, dbt in (("1", "4", "4"), ("0", "4", "4"), ("1", "1", "1"), ("1", "8", "8"), ("1", "4", "1")):
             monkeypatch.setenv("SOC_CLOUDS_NOISE_TABLE", ntab)
+            monkeypatch.setenv("SOC_CLOUDS_RESOLVE_BATCH", rb)
+            monkeypatch.setenv("SOC_CLOUDS_DENSITY_BATCH", dbt)
             soc.reload_tuning()
             b = torch.zeros_like(a)
             soc.cloud_rendering(g, dev(depth), nz, b, ws)
             outs.append(b)
     torch.cuda.synchronize()
-    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[2], outs[3]) and torch.equal(outs[0], outs[2])
+    monkeypatch.delenv("SOC_CLOUDS_RESOLVE_BATCH")
+    monkeypatch.delenv("SOC_CLOUDS_DENSITY_BATCH")
+    for o in outs[1:]:
+        assert torch.equal(outs[0], o)
     monkeypatch.delenv("SOC_CLOUDS_ATMOS_POS")
     monkeypatch.delenv("SOC_CLOUDS_GEOM")
     monkeypatch.delenv("SOC_CLOUDS_NOISE_TABLE")
