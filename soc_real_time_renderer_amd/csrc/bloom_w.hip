@@ -53,12 +53,26 @@ __device__ __forceinline__ void madd(C3& a, uint2 t, float w) {
 }
 __device__ __forceinline__ uint2 pack3(const C3& c) { return pack_h4(f4{c.r, c.g, c.b, 1.0f}); }
 
-// Clamp-to-edge tile load: t[r][c] = im[clamp(oy + r)][clamp(ox + c)].
+// Clamp-to-edge tile load: t[r][c] = im[clamp(oy + r)][clamp(ox + c)]. Each lane issues its loads four at a time
+// before their LDS stores (one memory latency per four rounds of the 256-lane loop instead of one per round).
 template <int TW, int TH>
 __device__ __forceinline__ void load_tile(const DImg& im, int ox, int oy, uint2 (*t)[TW], int tid) {
-    for (int i = tid; i < TW * TH; i += 256) {
+    constexpr int N = TW * TH;
+    auto at = [&](int i) {
         const int r = i / TW, c = i - r * TW;
-        t[r][c] = row_ptr<uint2>(im, clampi(oy + r, 0, im.h - 1))[clampi(ox + c, 0, im.w - 1)];
+        return row_ptr<uint2>(im, clampi(oy + r, 0, im.h - 1)) + clampi(ox + c, 0, im.w - 1);
+    };
+    for (int i0 = tid; i0 < N; i0 += 4 * 256) {
+        const int i1 = i0 + 256, i2 = i1 + 256, i3 = i2 + 256;
+        const uint2 a = *at(i0);
+        uint2 b = uint2{0u, 0u}, c = b, d = b;
+        if (i1 < N) b = *at(i1);
+        if (i2 < N) c = *at(i2);
+        if (i3 < N) d = *at(i3);
+        t[i0 / TW][i0 % TW] = a;
+        if (i1 < N) t[i1 / TW][i1 % TW] = b;
+        if (i2 < N) t[i2 / TW][i2 % TW] = c;
+        if (i3 < N) t[i3 / TW][i3 % TW] = d;
     }
 }
 
