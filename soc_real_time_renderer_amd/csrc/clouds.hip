@@ -942,7 +942,7 @@ __global__ __launch_bounds__(kWorkgroup) __attribute__((amdgpu_waves_per_eu(6)))
 
 // 512-lane workgroups: the 26 KiB noise table per workgroup caps residency at 6 workgroups per CU, so 256 lanes
 // give 6 waves per SIMD and 512 lanes give the full 8 (one table per 8 waves).
-template <bool NOISE_R8, uint32_t kSunvisThreads, bool WIDE = false>
+template <bool NOISE_R8, uint32_t kSunvisThreads, bool WIDE = false, bool PF = false>
 __global__ __launch_bounds__(kSunvisThreads) __attribute__((amdgpu_waves_per_eu(kSunvisThreads == 512 && !WIDE ? 8 : 6))) void clouds_sunvis(
     DImg noise, CloudParams p, const uint32_t* __restrict__ list, PairBufs pb) {
     using Q = typename std::conditional<WIDE, uint2, uint32_t>::type;
@@ -973,11 +973,33 @@ __global__ __launch_bounds__(kSunvisThreads) __attribute__((amdgpu_waves_per_eu(
     cx.cam_z = p.cam[2];
     cx.time = -1.0f * 0.02f * p.elapsed;
     const f3 sun = f3{p.sun[0], p.sun[1], p.sun[2]};
-    for (uint32_t v = blockIdx.x * kSunvisThreads + tid; v < total; v += gridDim.x * kSunvisThreads) {
+    auto phys_of = [&](uint32_t v) {
         int k = 0;
         while (k + 1 < kShards && v >= pre[k + 1]) ++k;
-        const uint32_t phys = (uint32_t)k * pb.cap + (v - pre[k]);
-        const uint32_t pr = pb.pairs[phys];
+        return (uint32_t)k * pb.cap + (v - pre[k]);
+    };
+    const uint32_t stride = gridDim.x * kSunvisThreads;
+    // PF: the next pair's list word is loaded one iteration ahead (its latency overlaps this pair's sun march; the
+    // geometry load that depends on it is the only wait left at the top of an iteration)
+    uint32_t v0 = blockIdx.x * kSunvisThreads + tid;
+    uint32_t phys_n = 0, pr_n = 0xffffffffu;
+    if (PF && v0 < total) {
+        phys_n = phys_of(v0);
+        pr_n = pb.pairs[phys_n];
+    }
+    for (uint32_t v = v0; v < total; v += stride) {
+        uint32_t phys, pr;
+        if constexpr (PF) {
+            phys = phys_n;
+            pr = pr_n;
+            if (v + stride < total) {
+                phys_n = phys_of(v + stride);
+                pr_n = pb.pairs[phys_n];
+            }
+        } else {
+            phys = phys_of(v);
+            pr = pb.pairs[phys];
+        }
         if (pr == 0xffffffffu) continue;   // slot of an overflowed batch
         const uint32_t i = pr >> 5, step = pr & 31u;
         float dither;
@@ -1316,13 +1338,18 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
     const int rb = tuning_knob("SOC_CLOUDS_RESOLVE_BATCH", 4);
     // the density kernel's od scratch read back in batches of this many steps (1: one dense step at a time)
     const int db = tuning_knob("SOC_CLOUDS_DENSITY_BATCH", 8);
+    // the sun-visibility kernel's next pair word loaded one iteration ahead
+    const bool sv_pf = tuning_knob("SOC_CLOUDS_SUNVIS_PF", 1) != 0;
     const int density_grid = std::min(grid(res_density, blocks), (int)ws.pb.od_blocks);   // one od scratch per workgroup
     if (r8) {
         if (db == 4) launch("clouds_density", kWorkgroup, clouds_density<true, 4>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
         else if (db == 8) launch("clouds_density", kWorkgroup, clouds_density<true, 8>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
         else launch("clouds_density", kWorkgroup, clouds_density<true>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
         if (apos == 1) atmos();
-        launch("clouds_sunvis", kSunvisLanes, clouds_sunvis<true, kSunvisLanes, true>, grid(res_sunvis, blocks), kSunvisLanes, 0, s, nz, p, list, ws.pb);
+        if (sv_pf)
+            launch("clouds_sunvis", kSunvisLanes, clouds_sunvis<true, kSunvisLanes, true, true>, grid(res_sunvis, blocks), kSunvisLanes, 0, s, nz, p, list, ws.pb);
+        else
+            launch("clouds_sunvis", kSunvisLanes, clouds_sunvis<true, kSunvisLanes, true>, grid(res_sunvis, blocks), kSunvisLanes, 0, s, nz, p, list, ws.pb);
         if (apos == 2) atmos();
         if (fold && rb == 4) resolve(clouds_resolve<true, true, 4>);
         else if (fold && rb == 8) resolve(clouds_resolve<true, true, 8>);
@@ -1333,7 +1360,10 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
         else if (db == 8) launch("clouds_density", kWorkgroup, clouds_density<false, 8>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
         else launch("clouds_density", kWorkgroup, clouds_density<false>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
         if (apos == 1) atmos();
-        launch("clouds_sunvis", kSunvisLanes, clouds_sunvis<false, kSunvisLanes, true>, grid(res_sunvis, blocks), kSunvisLanes, 0, s, nz, p, list, ws.pb);
+        if (sv_pf)
+            launch("clouds_sunvis", kSunvisLanes, clouds_sunvis<false, kSunvisLanes, true, true>, grid(res_sunvis, blocks), kSunvisLanes, 0, s, nz, p, list, ws.pb);
+        else
+            launch("clouds_sunvis", kSunvisLanes, clouds_sunvis<false, kSunvisLanes, true>, grid(res_sunvis, blocks), kSunvisLanes, 0, s, nz, p, list, ws.pb);
         if (apos == 2) atmos();
         if (fold && rb == 4) resolve(clouds_resolve<false, true, 4>);
         else if (fold && rb == 8) resolve(clouds_resolve<false, true, 8>);

@@ -580,10 +580,12 @@ def test_clouds_pair_path_equals_single_lane(soc, monkeypatch, W, H, pitch, all_
     # the one-step loops' bits
     outs = []
     for nz in (noise_r8, noise_rgba):
-        for ntab, rb, dbt in (("1", "4", "4"), ("0", "4", "4"), ("1", "1", "1"), ("1", "8", "8"), ("1", "4", "1")):
+        for ntab, rb, dbt, pf in (("1", "4", "8", "1"), ("0", "4", "4", "1"), ("1", "1", "1", "0"), ("1", "8", "8", "1"),
+                                  ("1", "4", "1", "0")):
             monkeypatch.setenv("SOC_CLOUDS_NOISE_TABLE", ntab)
             monkeypatch.setenv("SOC_CLOUDS_RESOLVE_BATCH", rb)
             monkeypatch.setenv("SOC_CLOUDS_DENSITY_BATCH", dbt)
+            monkeypatch.setenv("SOC_CLOUDS_SUNVIS_PF", pf)   # the sun-visibility kernel's next pair word loaded ahead
             soc.reload_tuning()
             b = torch.zeros_like(a)
             soc.cloud_rendering(g, dev(depth), nz, b, ws)
@@ -591,6 +593,7 @@ def test_clouds_pair_path_equals_single_lane(soc, monkeypatch, W, H, pitch, all_
     torch.cuda.synchronize()
     monkeypatch.delenv("SOC_CLOUDS_RESOLVE_BATCH")
     monkeypatch.delenv("SOC_CLOUDS_DENSITY_BATCH")
+    monkeypatch.delenv("SOC_CLOUDS_SUNVIS_PF")
     for o in outs[1:]:
         assert torch.equal(outs[0], o)
     monkeypatch.delenv("SOC_CLOUDS_ATMOS_POS")
