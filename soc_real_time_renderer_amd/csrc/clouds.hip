@@ -1282,7 +1282,15 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
     }
     const long long blocks = ((long long)W * H + 255) / 256;
     if (SOC_CLOUDS_PROFILE >= 4) return check_launch("cloud_rendering");
+    // SOC_CLOUDS_GRID_MULT: the sun-visibility and resolve grids as this many times the resident wave set (1: one
+    // persistent set; more: workgroups queue behind each other, so the dispatcher can place the main lane's workgroups
+    // between them instead of on what a persistent set leaves). The same bits at any grid. Default 2: C3 1678 -> 1699 fps,
+    // C2 5313 -> 5526, C4 unchanged; 3 measured C3 1644, C4 1342; 4 / 8: C3 1646 / 1629 (profiles/r05_ab_clouds_grid_mult.txt).
+    const int gmul = std::max(1, tuning_knob("SOC_CLOUDS_GRID_MULT", 2));
     auto grid = [&](int res, long long items_blocks) { return (int)std::max(1LL, std::min<long long>(res, items_blocks)); };
+    auto grid_m = [&](int res, long long items_blocks) {
+        return (int)std::max(1LL, std::min<long long>((long long)res * gmul, items_blocks));
+    };
     // Position of the atmosphere kernel in the lane (it feeds only the resolve): before the density march (0), before
     // the sun visibility (1) or after it (2). Default: after it above 1440p (C3 +0.7 %, C4 +5 % at 3840x2160: the
     // atmosphere's long transcendental run then overlaps the frame's TAA instead of its SSAO), first otherwise (C2
@@ -1329,7 +1337,7 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
                    list, ws.atmos, lut, st);
     };
     auto resolve = [&](auto k) {
-        launch("clouds_resolve", kWorkgroup, k, grid(res_resolve, blocks), kWorkgroup, 0, s, dimg(noise), dimg(target), p, counter,
+        launch("clouds_resolve", kWorkgroup, k, grid_m(res_resolve, blocks), kWorkgroup, 0, s, dimg(noise), dimg(target), p, counter,
                list, ws.atmos, ws.pb, st);
     };
     if (apos == 0) atmos();
@@ -1347,9 +1355,9 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
         else launch("clouds_density", kWorkgroup, clouds_density<true>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
         if (apos == 1) atmos();
         if (sv_pf)
-            launch("clouds_sunvis", kSunvisLanes, clouds_sunvis<true, kSunvisLanes, true, true>, grid(res_sunvis, blocks), kSunvisLanes, 0, s, nz, p, list, ws.pb);
+            launch("clouds_sunvis", kSunvisLanes, clouds_sunvis<true, kSunvisLanes, true, true>, grid_m(res_sunvis, blocks), kSunvisLanes, 0, s, nz, p, list, ws.pb);
         else
-            launch("clouds_sunvis", kSunvisLanes, clouds_sunvis<true, kSunvisLanes, true>, grid(res_sunvis, blocks), kSunvisLanes, 0, s, nz, p, list, ws.pb);
+            launch("clouds_sunvis", kSunvisLanes, clouds_sunvis<true, kSunvisLanes, true>, grid_m(res_sunvis, blocks), kSunvisLanes, 0, s, nz, p, list, ws.pb);
         if (apos == 2) atmos();
         if (fold && rb == 4) resolve(clouds_resolve<true, true, 4>);
         else if (fold && rb == 8) resolve(clouds_resolve<true, true, 8>);
@@ -1361,9 +1369,9 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
         else launch("clouds_density", kWorkgroup, clouds_density<false>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
         if (apos == 1) atmos();
         if (sv_pf)
-            launch("clouds_sunvis", kSunvisLanes, clouds_sunvis<false, kSunvisLanes, true, true>, grid(res_sunvis, blocks), kSunvisLanes, 0, s, nz, p, list, ws.pb);
+            launch("clouds_sunvis", kSunvisLanes, clouds_sunvis<false, kSunvisLanes, true, true>, grid_m(res_sunvis, blocks), kSunvisLanes, 0, s, nz, p, list, ws.pb);
         else
-            launch("clouds_sunvis", kSunvisLanes, clouds_sunvis<false, kSunvisLanes, true>, grid(res_sunvis, blocks), kSunvisLanes, 0, s, nz, p, list, ws.pb);
+            launch("clouds_sunvis", kSunvisLanes, clouds_sunvis<false, kSunvisLanes, true>, grid_m(res_sunvis, blocks), kSunvisLanes, 0, s, nz, p, list, ws.pb);
         if (apos == 2) atmos();
         if (fold && rb == 4) resolve(clouds_resolve<false, true, 4>);
         else if (fold && rb == 8) resolve(clouds_resolve<false, true, 8>);
