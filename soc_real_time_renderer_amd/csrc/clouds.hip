@@ -1145,7 +1145,7 @@ namespace {
 // Pair capacity 2 per pixel of the image (8 shards).
 // Per 256-entry batch of the list: the physical index of its first pair (or kInline).
 // density workgroups the od scratch is sized for (the resident set: 6 per CU on 256 CUs is 1536)
-constexpr size_t kDensityBlocks = 2048;
+constexpr size_t kDensityBlocks = 4096;
 struct CloudWs {
     uint32_t* counter;
     uint32_t* list;
@@ -1348,7 +1348,11 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
     const int db = tuning_knob("SOC_CLOUDS_DENSITY_BATCH", 8);
     // the sun-visibility kernel's next pair word loaded one iteration ahead
     const bool sv_pf = tuning_knob("SOC_CLOUDS_SUNVIS_PF", 1) != 0;
-    const int density_grid = std::min(grid(res_density, blocks), (int)ws.pb.od_blocks);   // one od scratch per workgroup
+    // one od scratch per workgroup; SOC_CLOUDS_DENSITY_MULT: the grid as this many times the resident set (as gmul).
+    // Default 1: 2 measured C3 1710 -> 1697 fps, C4 1321 -> 1358 (profiles/r05_ab_clouds_density_mult.txt)
+    const int dmul = std::max(1, tuning_knob("SOC_CLOUDS_DENSITY_MULT", 1));
+    const int density_grid = std::min((int)std::max(1LL, std::min<long long>((long long)res_density * dmul, blocks)),
+                                      (int)ws.pb.od_blocks);
     if (r8) {
         if (db == 4) launch("clouds_density", kWorkgroup, clouds_density<true, 4>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
         else if (db == 8) launch("clouds_density", kWorkgroup, clouds_density<true, 8>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
