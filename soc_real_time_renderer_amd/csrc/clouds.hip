@@ -1205,6 +1205,11 @@ extern "C" size_t soc_cloud_rendering_workspace_size(int32_t width, int32_t heig
 
 extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img noise, soc_img target, void* workspace,
                                    soc_stream stream) {
+    return soc::cloud_rendering_launch(g, depth, noise, target, workspace, stream, 0);
+}
+
+int soc::cloud_rendering_launch(const soc_globals* g, soc_img depth, soc_img noise, soc_img target, void* workspace,
+                                soc_stream stream, int density_mult) {
     static const char* P = "soc_cloud_rendering";
     if (!g) return set_error(SOC_E_INVALID_ARG, "%s: null globals", P);
     int rc = check_img(depth, SOC_FMT_D32F, P, "depth");
@@ -1350,7 +1355,7 @@ extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img 
     const bool sv_pf = tuning_knob("SOC_CLOUDS_SUNVIS_PF", 1) != 0;
     // one od scratch per workgroup; SOC_CLOUDS_DENSITY_MULT: the grid as this many times the resident set (as gmul).
     // Default 1: 2 measured C3 1710 -> 1697 fps, C4 1321 -> 1358 (profiles/r05_ab_clouds_density_mult.txt)
-    const int dmul = std::max(1, tuning_knob("SOC_CLOUDS_DENSITY_MULT", 1));
+    const int dmul = density_mult >= 1 ? density_mult : std::max(1, tuning_knob("SOC_CLOUDS_DENSITY_MULT", 1));
     const int density_grid = std::min((int)std::max(1LL, std::min<long long>((long long)res_density * dmul, blocks)),
                                       (int)ws.pb.od_blocks);
     if (r8) {
