@@ -56,7 +56,7 @@ from soc_real_time_renderer_amd import multi_gpu, raster, scene  # noqa: E402
 from soc_real_time_renderer_amd.scene import sponza_mesh  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
-SSAO_KERNEL = "ssao_lds_kernel<true, true, true, 64, 16, 32, 2, true>"   # the default SSAOGeneration kernel (ssao.hip)
+SSAO_KERNEL = "ssao_lds_kernel<true, true, true, 64, 16, 32, 2, true, 2>"   # the default SSAOGeneration kernel (ssao.hip)
 
 
 def make_globals(W, H, camera):
@@ -123,9 +123,10 @@ def pmc_traffic(kernel, W, H, scene_name="mesh"):
 
 
 def valu_bound(kernel, us):
-    """The kernel's VALU issue time from the committed issue model (profiles/*valu_model.json: SQ_INSTS_VALU and
-    SQ_INSTS_VALU_TRANS_F32 per launch of the same C3 command at 4 cycles per wave64 VALU instruction and +5.5 per
-    transcendental over 1024 SIMDs at 2.4 GHz, tools/valu_model.py) against its measured time `us`, or None."""
+    """The kernel's VALU issue time from the committed issue model (profiles/*valu_model.json, tools/valu_calibrate.py:
+    SQ_INSTS_VALU per launch of the same C3 command at the measured cost of one wave64 VALU instruction over 1024 SIMDs
+    at the launch's clock) against its measured time `us`, or None. A model written before a template
+    signature change matches on the kernel's base name when it holds one instantiation of it."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*valu_model.json")))
     if not files:
@@ -133,6 +134,10 @@ def valu_bound(kernel, us):
     with open(files[-1]) as fh:
         t = json.load(fh)
     for rows in t.get("runs", {}).values():
+        if kernel not in rows:
+            base = [n for n in rows if n.split("<")[0] == kernel.split("<")[0]]
+            if len(base) == 1:
+                kernel = base[0]
         if kernel in rows:
             r = rows[kernel]
             issue = r.get("valu_issue_us", r.get("issue_bound_us"))
@@ -404,7 +409,7 @@ def main():
     pass_gbs = {n: round(algo[n] / (ms * 1e-3) / 1e9, 1) for n, _, ms, _ in stats if ms > 0 and n in algo}
     # the committed PMC table comes from the default command (C3, G-buffer resident): other workloads get null
     pmc_ok = args.config == "c3" and not args.raster
-    comp_kernel = "composition_pair<true, false, 3>" if comp != "Composition" else "composition_pair<false, false, 3>"
+    comp_kernel = "composition_pair<true, false, 7>" if comp != "Composition" else "composition_pair<false, false, 7>"
     traffic, traffic_src = pmc_traffic(comp_kernel, W, H, args.scene) if pmc_ok else (None, None)
     ssao_traffic, _ = pmc_traffic(SSAO_KERNEL, W, H, args.scene) if pmc_ok else (None, None)
     pair_traffic = traffic + ssao_traffic if traffic is not None and ssao_traffic is not None else None
