@@ -436,8 +436,9 @@ int soc_renderer_set_current_history(soc_renderer* r, int32_t index);
  * Composition, so it overlaps bloom and SSAO. Results are identical either way. */
 int soc_renderer_set_async(soc_renderer* r, int32_t enable);
 /* The sky lane's hardware queue: 1 = a high-priority stream, 2 = low priority, 0 = normal priority (a queue HIP may
- * share with the caller's stream), -1 = not chosen yet (tuning knob SOC_RENDERER_SIDE_QUEUE=3, the default: the first
- * 64 frames run half at each priority and the faster is kept) or no sky lane created. Same results either way. */
+ * share with the caller's stream), -1 = not chosen yet (tuning knob SOC_RENDERER_SIDE_QUEUE=3, the default: frames
+ * 16-271 run in eight windows alternating high / low priority as ABBA pairs; high is kept if it is faster by more than
+ * 1.5 % once their timing events have completed, else low) or no sky lane created. Same results either way. */
 int32_t soc_renderer_side_queue(const soc_renderer* r);
 
 /* --- Pass declaration (the Daxa task-uses block + TaskGraph::add_task, e.g. composition.inl:10-21 and

@@ -664,7 +664,7 @@ struct soc_renderer {
     hipStream_t lane_q[2] = {nullptr, nullptr};
     int side_queue = -1;
     int probe_frames = 0;
-    hipEvent_t probe_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t probe_ev[16] = {};
     hipEvent_t switch_ev = nullptr;
     // 8 partial luminance histograms of the fused composition + histogram pass (renderer-owned, 8 KiB)
     uint32_t* hist_scratch = nullptr;
@@ -830,10 +830,11 @@ void build_passes_tail(soc_renderer* r) {
     add_pass(r, "CloudRendering", "Sky Rendering", pre, res_mask({SOC_RES_DEPTH, SOC_RES_NOISE}), res_mask({SOC_RES_CLOUDS}),
              [r](const soc_globals* g, hipStream_t s) {
                  // a sky lane at high priority (the lane probe found the frame sky-bound): the density grid at twice
-                 // the resident set (C4 +2.7 %, C3 -0.8 %: profiles/r05_ab_clouds_density_mult.txt); else the knob
-                 const int dmul = (r->side_queue == 1 && tuning_knob("SOC_RENDERER_SKY_DENSITY_MULT", 1)) ? 2 : 0;
+                 // the resident set (C4 +2.7 %, C3 -0.8 %: profiles/r05_ab_clouds_density_mult.txt) and the hoisted
+                 // classification (C4 +1.8 %, C3 -1.1 %); else the knobs
+                 const bool sky_bound = r->side_queue == 1 && tuning_knob("SOC_RENDERER_SKY_BOUND_VARIANTS", 1);
                  return soc::cloud_rendering_launch(g, r->img.depth, r->img.noise, r->img.clouds, r->img.clouds_workspace,
-                                                    (soc_stream)s, dmul);
+                                                    (soc_stream)s, sky_bound);
              }, SOC_PASS_ASYNC);
     if (r->sky_split)
         add_pass(r, "SkyCompose", "Sky Rendering", pre, res_mask({SOC_RES_CLOUDS, SOC_RES_DEPTH}), sky_w,
@@ -1137,8 +1138,10 @@ static int run_pass(soc_renderer::Pass& p, const soc_globals* g, hipStream_t s) 
 
 // The second lane's stream(s) and events (all of them: a device change rebuilds the lane there).
 static void destroy_side_lane(soc_renderer* r) {
-    for (hipEvent_t* e : {&r->fork_ev, &r->join_ev, &r->switch_ev, &r->probe_ev[0], &r->probe_ev[1], &r->probe_ev[2], &r->probe_ev[3]})
+    for (hipEvent_t* e : {&r->fork_ev, &r->join_ev, &r->switch_ev})
         if (*e) { (void)hipEventDestroy(*e); *e = nullptr; }
+    for (auto& e : r->probe_ev)
+        if (e) { (void)hipEventDestroy(e); e = nullptr; }
     if (r->lane_q[0] || r->lane_q[1]) {
         for (auto& q : r->lane_q)
             if (q) { (void)hipStreamDestroy(q); q = nullptr; }
@@ -1155,8 +1158,9 @@ static void destroy_side_lane(soc_renderer* r) {
 // given the caller's queue and the two lanes ran serialised (bench --exchange 0.79 vs 0.62 ms per frame, DESIGN.md §11
 // r5.8). A stream of another priority comes from a pool of its own, so the lane keeps a queue of its own whatever the
 // caller created. Which priority is faster depends on which lane is the frame's critical path (C3: the main lane, the
-// sky lane low is 5 % faster than high; C4: the sky lane, high is 10 % faster than low): tuning knob
-// SOC_RENDERER_SIDE_QUEUE 3 (default) times both (frame_lane_probe), 1 = high, 2 = low, 0 = normal priority.
+// sky lane low is 5 % faster than high; C4: the sky lane, high is 3-10 % faster than low): tuning knob
+// SOC_RENDERER_SIDE_QUEUE 3 (default) times both over the first 273 frames (frame_lane_probe), 1 = high, 2 = low,
+// 0 = normal priority.
 static int ensure_side_lane(soc_renderer* r) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return set_error(SOC_E_HIP, "soc_renderer_execute: hipGetDevice failed");
@@ -1206,37 +1210,49 @@ static int switch_side_lane(soc_renderer* r, hipStream_t q) {
     return SOC_OK;
 }
 
-// Auto mode's probe, at the start of each frame (a call with the PRE phase): frames [0, 32) run the sky lane at high
-// priority, [32, 64) at low; timing events on the caller's stream at frames 8, 32, 40, 64 give each setting's mean
-// frame interval over 24 frames (the first 8 after a switch skipped). Once the last event has completed (queried, never
-// waited on), the faster setting is kept for the renderer's life.
+// Auto mode's probe, at the start of each frame (a call with the PRE phase): after 16 frames left to the clocks, eight
+// windows of 32 frames run the sky lane at high, low, low, high, high, low, low, high priority; timing events on the
+// caller's stream at each window's frames 8 and 32 give its mean frame interval over 24 frames (the first 8 after a
+// switch skipped). The ABBA order cancels a linear drift of the clocks over the probe (a plain high-then-low order read
+// the warm-up as a slower high lane). High is kept only if its windows are faster by more than 1.5 % (C3 and C2
+// prefer low by 1-5 %, C4 high by 3-10 %; short C2 frames measured within the noise, profiles/r05_ab_lane_probe.txt),
+// once the last event has completed (queried, never waited on), for the renderer's life.
 static int frame_lane_probe(soc_renderer* r, hipStream_t s) {
     if (r->side_queue != -1 || !r->lane_q[0]) return SOC_OK;
-    constexpr int kWindow = 32, kSkip = 8;
+    constexpr int kStart = 16, kWindow = 32, kSkip = 8, kWins = 8, kEnd = kStart + kWins * kWindow;
+    constexpr bool kHigh[kWins] = {true, false, false, true, true, false, false, true};
     const int f = r->probe_frames;
-    if (f <= 2 * kWindow) {
-        const int slot = f == kSkip ? 0 : f == kWindow ? 1 : f == kWindow + kSkip ? 2 : f == 2 * kWindow ? 3 : -1;
-        if (slot >= 0 && hipEventRecord(r->probe_ev[slot], s) != hipSuccess)
-            return set_error(SOC_E_HIP, "soc_renderer_execute: lane probe event failed");
-        if (f == kWindow) {
-            int rc = switch_side_lane(r, r->lane_q[1]);
-            if (rc) return rc;
+    if (f <= kEnd) {
+        if (f >= kStart) {
+            const int w = (f - kStart) / kWindow, o = (f - kStart) % kWindow;
+            int slot = -1;
+            if (o == kSkip && w < kWins) slot = 2 * w;
+            else if (o == 0 && w > 0) slot = 2 * (w - 1) + 1;
+            if (slot >= 0 && hipEventRecord(r->probe_ev[slot], s) != hipSuccess)
+                return set_error(SOC_E_HIP, "soc_renderer_execute: lane probe event failed");
+            if (o == 0 && w < kWins) {
+                int rc = switch_side_lane(r, r->lane_q[kHigh[w] ? 0 : 1]);
+                if (rc) return rc;
+            }
         }
         r->probe_frames++;
         return SOC_OK;
     }
-    if (hipEventQuery(r->probe_ev[3]) != hipSuccess) {   // not reached yet (or an error: the lane stays as it is)
+    if (hipEventQuery(r->probe_ev[2 * kWins - 1]) != hipSuccess) {   // not reached yet (or an error: the lane stays)
         (void)hipGetLastError();
         return SOC_OK;
     }
     float hi = 0.0f, lo = 0.0f;
-    if (hipEventElapsedTime(&hi, r->probe_ev[0], r->probe_ev[1]) != hipSuccess ||
-        hipEventElapsedTime(&lo, r->probe_ev[2], r->probe_ev[3]) != hipSuccess) {
-        (void)hipGetLastError();
-        r->side_queue = 2;
-        return SOC_OK;
+    for (int w = 0; w < kWins; ++w) {
+        float t = 0.0f;
+        if (hipEventElapsedTime(&t, r->probe_ev[2 * w], r->probe_ev[2 * w + 1]) != hipSuccess) {
+            (void)hipGetLastError();
+            r->side_queue = 2;
+            return switch_side_lane(r, r->lane_q[1]);
+        }
+        (kHigh[w] ? hi : lo) += t;
     }
-    r->side_queue = hi < lo ? 1 : 2;
+    r->side_queue = (hi < 0.985f * lo) ? 1 : 2;
     return switch_side_lane(r, r->lane_q[r->side_queue - 1]);
 }
 

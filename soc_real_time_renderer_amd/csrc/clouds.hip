@@ -650,6 +650,11 @@ __global__ __launch_bounds__(kWorkgroup) void clouds_kernel(DImg depth, DImg noi
 // tile. The atomics on the one counter serialise across the XCDs: at one per 64x16 tile they cost C4 34 of its 59 us
 // (profiles/r04_probe_clouds_classify.txt).
 constexpr int kClassifyTiles = 4;
+// HOIST: every tile's depth samples issued before the first tile's stores (one memory round trip instead of four; the
+// same samples). Faster alone (C3 299 -> 291 us, C4 541 -> 504 us CloudRendering) but in the frame only where the sky
+// lane is the critical path (C4 +1.8 %; C3 -1.1 %, C2 -1 %: profiles/r05_ab_clouds_classify_hoist.txt), so the render
+// graph selects it for a sky-bound frame (a high-priority sky lane) and the standalone pass by SOC_CLOUDS_CLASSIFY_HOIST.
+template <bool HOIST>
 __global__ __launch_bounds__(kWorkgroup) void clouds_classify(DImg depth, DImg target, CloudParams p, int vec_store,
                                                        uint32_t* __restrict__ counter, uint32_t* __restrict__ list) {
     __shared__ uint32_t wave_total[kClassifyTiles][4];
@@ -661,16 +666,41 @@ __global__ __launch_bounds__(kWorkgroup) void clouds_classify(DImg depth, DImg t
     const unsigned long long below = (1ull << lane) - 1ull;
     uint32_t masks = 0;   // bits 4k..4k+3: pixels (x0 + 0..3, y_k) of tile k are sky
     uint32_t before[kClassifyTiles];
+    // HOIST: every tile's depth samples issued before the first tile's stores (rows clamped into the image; a row past
+    // H is not used), so the 4 tiles cost one memory round trip instead of four
+    float dk[kClassifyTiles][4];
+    auto load_all = [&](auto sample) {
+#pragma unroll
+        for (int k = 0; k < kClassifyTiles; ++k) {
+            const int y = min((blockIdx.y * kClassifyTiles + k) * 16 + (wave >> 1) * 8 + (lane >> 3), H - 1);
+            const float ray_v = div_rn((float)y, p.res_y_m1, p.r_res_y_m1);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) dk[k][j] = sample(div_rn((float)min(x0 + j, W - 1), p.res_x_m1, p.r_res_x_m1), ray_v);
+        }
+    };
+    if (HOIST && depth.w >= 2) {   // sample_f32's row-pair form without its per-sample extent test (same texels, weights)
+        load_all([&](float u, float v) {
+            const Axis ax = axis_clamp(u, depth.w), ay = axis_clamp(v, depth.h);
+            typedef float f2u4 __attribute__((ext_vector_type(2))) __attribute__((aligned(4)));
+            const f2u4 r0 = *reinterpret_cast<const f2u4*>(row_ptr<float>(depth, ay.i0) + ax.i0);
+            const f2u4 r1 = *reinterpret_cast<const f2u4*>(row_ptr<float>(depth, ay.i1) + ax.i0);
+            return bilerp1(r0.x, r0.y, r1.x, r1.y, ax.w, ay.w);
+        });
+    } else if (HOIST) {
+        load_all([&](float u, float v) { return sample_f32(depth, u, v); });
+    }
 #pragma unroll
     for (int k = 0; k < kClassifyTiles; ++k) {
         const int y = (blockIdx.y * kClassifyTiles + k) * 16 + (wave >> 1) * 8 + (lane >> 3);
         uint32_t mask = 0;   // bit j: pixel (x0 + j, y) is sky
         if (y < H) {
-            // all 16 depth loads issued together (clamped coordinates, no per-pixel branch)
-            float d[4];
-            const float ray_v = div_rn((float)y, p.res_y_m1, p.r_res_y_m1);
+            if (!HOIST) {   // the round-4 order: this tile's samples, then its stores
+                const float ray_v = div_rn((float)y, p.res_y_m1, p.r_res_y_m1);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) d[j] = sample_f32(depth, div_rn((float)min(x0 + j, W - 1), p.res_x_m1, p.r_res_x_m1), ray_v);
+                for (int j = 0; j < 4; ++j)
+                    dk[k][j] = sample_f32(depth, div_rn((float)min(x0 + j, W - 1), p.res_x_m1, p.r_res_x_m1), ray_v);
+            }
+            const float* d = dk[k];
 #pragma unroll
             for (int j = 0; j < 4; ++j)
                 if (x0 + j < W && d[j] == 1.0f) mask |= 1u << j;
@@ -1205,11 +1235,11 @@ extern "C" size_t soc_cloud_rendering_workspace_size(int32_t width, int32_t heig
 
 extern "C" int soc_cloud_rendering(const soc_globals* g, soc_img depth, soc_img noise, soc_img target, void* workspace,
                                    soc_stream stream) {
-    return soc::cloud_rendering_launch(g, depth, noise, target, workspace, stream, 0);
+    return soc::cloud_rendering_launch(g, depth, noise, target, workspace, stream, false);
 }
 
 int soc::cloud_rendering_launch(const soc_globals* g, soc_img depth, soc_img noise, soc_img target, void* workspace,
-                                soc_stream stream, int density_mult) {
+                                soc_stream stream, bool sky_bound) {
     static const char* P = "soc_cloud_rendering";
     if (!g) return set_error(SOC_E_INVALID_ARG, "%s: null globals", P);
     int rc = check_img(depth, SOC_FMT_D32F, P, "depth");
@@ -1274,8 +1304,13 @@ int soc::cloud_rendering_launch(const soc_globals* g, soc_img depth, soc_img noi
                    dimg(noise), ws.noise_quads, ws.noise_wide);
     }
     const int vec_store = (target.pitch_bytes % 16 == 0) && (reinterpret_cast<uintptr_t>(target.data) % 16 == 0);
-    launch("clouds_classify", kWorkgroup, clouds_classify, dim3(ceil_div(W, 64), ceil_div(H, 16 * kClassifyTiles)), kWorkgroup, 0, s,
-           dimg(depth), dimg(target), p, vec_store, counter, list);
+    const bool hoist = sky_bound || tuning_knob("SOC_CLOUDS_CLASSIFY_HOIST", 0);
+    if (hoist)
+        launch("clouds_classify", kWorkgroup, clouds_classify<true>, dim3(ceil_div(W, 64), ceil_div(H, 16 * kClassifyTiles)),
+               kWorkgroup, 0, s, dimg(depth), dimg(target), p, vec_store, counter, list);
+    else
+        launch("clouds_classify", kWorkgroup, clouds_classify<false>, dim3(ceil_div(W, 64), ceil_div(H, 16 * kClassifyTiles)),
+               kWorkgroup, 0, s, dimg(depth), dimg(target), p, vec_store, counter, list);
     // One resident wave set per kernel, grid-stride over the list / pairs: the long per-item work is
     // balanced over all SIMDs instead of running as a second, partially filled round.
     static int res_atmos = 0, res_density = 0, res_sunvis = 0, res_resolve = 0;
@@ -1355,7 +1390,7 @@ int soc::cloud_rendering_launch(const soc_globals* g, soc_img depth, soc_img noi
     const bool sv_pf = tuning_knob("SOC_CLOUDS_SUNVIS_PF", 1) != 0;
     // one od scratch per workgroup; SOC_CLOUDS_DENSITY_MULT: the grid as this many times the resident set (as gmul).
     // Default 1: 2 measured C3 1710 -> 1697 fps, C4 1321 -> 1358 (profiles/r05_ab_clouds_density_mult.txt)
-    const int dmul = density_mult >= 1 ? density_mult : std::max(1, tuning_knob("SOC_CLOUDS_DENSITY_MULT", 1));
+    const int dmul = sky_bound ? 2 : std::max(1, tuning_knob("SOC_CLOUDS_DENSITY_MULT", 1));
     const int density_grid = std::min((int)std::max(1LL, std::min<long long>((long long)res_density * dmul, blocks)),
                                       (int)ws.pb.od_blocks);
     if (r8) {

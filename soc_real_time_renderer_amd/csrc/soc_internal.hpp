@@ -97,10 +97,11 @@ bool composition_pair_applicable(const soc_globals* g, const soc_img& target, co
                                  const soc_img& clouds);
 // The sky pixels of the colour image (depth == 1 -> clouds texel) and their bins into the 8 partial histograms:
 // the second-lane half of a Composition run with sky_external.
-// soc_cloud_rendering with the density grid multiplier given (density_mult < 1: the SOC_CLOUDS_DENSITY_MULT knob); the
-// render graph passes 2 when its sky lane runs at high priority (a sky-bound frame). The same bits for any value.
+// soc_cloud_rendering; sky_bound (the render graph's sky lane runs at high priority): the variants that are faster
+// only where the sky lane is the frame's critical path (the density grid at twice the resident set, the classification's
+// hoisted depth samples). The same bits either way.
 int cloud_rendering_launch(const soc_globals* g, soc_img depth, soc_img noise, soc_img target, void* workspace,
-                           soc_stream stream, int density_mult);
+                           soc_stream stream, bool sky_bound);
 int sky_compose_launch(const soc_globals* g, soc_img target, soc_img depth, soc_img clouds, uint32_t* scratch,
                        soc_stream stream);
 int histogram_fold_launch(uint32_t* scratch, soc_auto_exposure* ae, soc_stream stream);

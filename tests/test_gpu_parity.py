@@ -580,8 +580,10 @@ def test_clouds_pair_path_equals_single_lane(soc, monkeypatch, W, H, pitch, all_
     # the one-step loops' bits
     outs = []
     for nz in (noise_r8, noise_rgba):
-        for ntab, rb, dbt, pf in (("1", "4", "8", "1"), ("0", "4", "4", "1"), ("1", "1", "1", "0"), ("1", "8", "8", "1"),
-                                  ("1", "4", "1", "0")):
+        for ntab, rb, dbt, pf, hoist in (("1", "4", "8", "1", "0"), ("0", "4", "4", "1", "1"), ("1", "1", "1", "0", "0"),
+                                         ("1", "8", "8", "1", "1"), ("1", "4", "1", "0", "0")):
+            monkeypatch.setenv("SOC_CLOUDS_CLASSIFY_HOIST", hoist)   # the classification's depth samples hoisted
+            monkeypatch.setenv("SOC_CLOUDS_DENSITY_MULT", "2" if hoist == "1" else "1")
             monkeypatch.setenv("SOC_CLOUDS_NOISE_TABLE", ntab)
             monkeypatch.setenv("SOC_CLOUDS_RESOLVE_BATCH", rb)
             monkeypatch.setenv("SOC_CLOUDS_DENSITY_BATCH", dbt)
@@ -594,6 +596,8 @@ def test_clouds_pair_path_equals_single_lane(soc, monkeypatch, W, H, pitch, all_
     monkeypatch.delenv("SOC_CLOUDS_RESOLVE_BATCH")
     monkeypatch.delenv("SOC_CLOUDS_DENSITY_BATCH")
     monkeypatch.delenv("SOC_CLOUDS_SUNVIS_PF")
+    monkeypatch.delenv("SOC_CLOUDS_CLASSIFY_HOIST")
+    monkeypatch.delenv("SOC_CLOUDS_DENSITY_MULT")
     for o in outs[1:]:
         assert torch.equal(outs[0], o)
     monkeypatch.delenv("SOC_CLOUDS_ATMOS_POS")
@@ -962,11 +966,11 @@ def test_render_graph_static_inputs_bit_identical(soc, inputs):
 
 @pytest.mark.parametrize("inputs", ["sponza", "terrain"])
 def test_sky_lane_queue_probe_bit_identical(soc, monkeypatch, inputs):
-    """The sky lane's hardware queue (SOC_RENDERER_SIDE_QUEUE): auto (3, default) runs frames 0-31 on a high-priority
-    stream, 32-63 on a low-priority one and then keeps the faster, moving the lane between streams with an event wait;
-    1 / 2 fix it, 0 is the normal-priority stream. Every frame's output and the final temporal state have the same bits
-    in every mode (72 frames with per-frame globals, static inputs: the clouds of frame N+1 start before frame N's TAA,
-    also across the switches), and auto has chosen a queue by the end."""
+    """The sky lane's hardware queue (SOC_RENDERER_SIDE_QUEUE): auto (3, default) runs frames 16-271 in eight windows
+    alternating between a high- and a low-priority stream (ABBA pairs) and then keeps one, moving the lane between
+    streams with an event wait; 1 / 2 fix it, 0 is the normal-priority stream. Every frame's output (every 4th texel)
+    and the final temporal state have the same bits in every mode (278 frames with per-frame globals, static inputs: the
+    clouds of frame N+1 start before frame N's TAA, also across the switches), and auto has chosen a queue by the end."""
     import ctypes as C
     W, H = 1920, 1080
     g0, gb = (sponza_inputs if inputs == "sponza" else terrain_inputs)(W, H, elapsed=10.0)
@@ -984,14 +988,15 @@ def test_sky_lane_queue_probe_bit_identical(soc, monkeypatch, inputs):
         ji = C.c_uint32(0)
         g = soc.globals_defaults(W, H)
         seq = []
-        for f in range(72):
+        for f in range(278):
             soc.frame_update(g, cam, W, H, 0.016, ji)
-            cam.position[0] += 0.01
+            cam.position[0] += 0.003
             r.execute(g)
-            seq.append(fr["output"].clone())
-            if f == 66:
+            seq.append(fr["output"][::4, ::4].clone())   # every 4th texel of every frame (and the final state in full)
+            if f == 274:
                 torch.cuda.synchronize()   # the probe's last event has completed: the next frame decides
         torch.cuda.synchronize()
+        seq.append(fr["output"].clone())
         seq.append(fr["auto_exposure"].clone())
         seq.append(r.resolved().clone())
         outs.append(seq)
