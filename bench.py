@@ -317,12 +317,12 @@ def main():
 
     for _ in range(args.warmup):
         frame()
-    # the renderer's sky-lane queue probe (soc_renderer_side_queue) runs over its first 273 frames and decides at the
-    # first frame after they completed: untimed frames until then, the same count on every rank (each frame of the
-    # exchange path is a collective)
+    # the renderer's sky-lane queue probe (soc_renderer_side_queue) spans its first side_queue_probe_frames() frames and
+    # decides at the first frame after they completed: untimed frames until then, the same count on every rank (each
+    # frame of the exchange path is a collective; the ranks share the resolution, so the count)
     probe_frames = 0
     if not args.no_sky_lane and r.side_queue() == -1:
-        probe_frames = max(0, 274 - args.warmup)
+        probe_frames = max(0, r.side_queue_probe_frames() - args.warmup)
         for _ in range(probe_frames):
             frame()
         torch.cuda.synchronize()

@@ -436,10 +436,13 @@ int soc_renderer_set_current_history(soc_renderer* r, int32_t index);
  * Composition, so it overlaps bloom and SSAO. Results are identical either way. */
 int soc_renderer_set_async(soc_renderer* r, int32_t enable);
 /* The sky lane's hardware queue: 1 = a high-priority stream, 2 = low priority, 0 = normal priority (a queue HIP may
- * share with the caller's stream), -1 = not chosen yet (tuning knob SOC_RENDERER_SIDE_QUEUE=3, the default: frames
- * 16-271 run in eight windows alternating high / low priority as ABBA pairs; high is kept if it is faster by more than
- * 1.5 % once their timing events have completed, else low) or no sky lane created. Same results either way. */
+ * share with the caller's stream), -1 = not chosen yet (tuning knob SOC_RENDERER_SIDE_QUEUE=3, the default: after 16
+ * frames, eight windows of 32-128 frames alternate high / low priority as ABBA pairs; high is kept if it is faster by
+ * more than 1.5 % once their timing events have completed, else low) or no sky lane created. Same results either way. */
 int32_t soc_renderer_side_queue(const soc_renderer* r);
+/* Frames the auto probe spans from the renderer's first call (the choice is made at the first call after they have
+ * completed on the GPU); 0 when no probe runs. A caller that times frames runs at least this many first. */
+int32_t soc_renderer_side_queue_probe_frames(const soc_renderer* r);
 
 /* --- Pass declaration (the Daxa task-uses block + TaskGraph::add_task, e.g. composition.inl:10-21 and
  * renderer.cpp:1103-1117) ------------------------------------------------------------------------

@@ -460,6 +460,10 @@ class Renderer:
         """The sky lane's hardware-queue priority (soc_renderer_side_queue): 1 high, 2 low, 0 normal, -1 not chosen."""
         return int(lib().soc_renderer_side_queue(self.handle))
 
+    def side_queue_probe_frames(self) -> int:
+        """Frames the sky-lane queue probe spans from the first call (0: no probe)."""
+        return int(lib().soc_renderer_side_queue_probe_frames(self.handle))
+
     def add_pass(self, name: str, fn, reads=(), writes=(), phase: int = PHASE_PRE_EXPOSURE, group: str = "",
                  before: Optional[str] = None, async_compute: bool = False) -> None:
         """Register a caller pass (soc_renderer_add_pass): `fn(globals_ptr, frame_images_ptr, stream_handle)` records

@@ -241,6 +241,7 @@ FUNCTIONS = {
     "soc_renderer_pass_event_times": (C.c_int32, [_P, C.c_int32, _P, C.POINTER(C.c_float), C.POINTER(C.c_float),
                                                   C.c_int32]),
     "soc_renderer_side_queue": (C.c_int32, [_P]),
+    "soc_renderer_side_queue_probe_frames": (C.c_int32, [_P]),
     "soc_raster_workspace_size": (C.c_size_t, [C.c_int32, C.c_int32]),
     "soc_paired_texels_bytes": (C.c_size_t, [C.c_int32, C.c_int32]),
     "soc_renderer_set_raster_scene": (_I, [_P, C.POINTER(RasterScene)]),

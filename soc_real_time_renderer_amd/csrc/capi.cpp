@@ -832,7 +832,10 @@ void build_passes_tail(soc_renderer* r) {
                  // a sky lane at high priority (the lane probe found the frame sky-bound): the density grid at twice
                  // the resident set (C4 +2.7 %, C3 -0.8 %: profiles/r05_ab_clouds_density_mult.txt) and the hoisted
                  // classification (C4 +1.8 %, C3 -1.1 %); else the knobs
-                 const bool sky_bound = r->side_queue == 1 && tuning_knob("SOC_RENDERER_SKY_BOUND_VARIANTS", 1);
+                 // (also during the lane probe's high-priority windows, so the probe compares the two alternatives
+                 // as they run: high with these variants against low without)
+                 const bool high = r->side_queue == 1 || (r->side_queue == -1 && r->lane_q[0] && r->side == r->lane_q[0]);
+                 const bool sky_bound = high && tuning_knob("SOC_RENDERER_SKY_BOUND_VARIANTS", 1);
                  return soc::cloud_rendering_launch(g, r->img.depth, r->img.noise, r->img.clouds, r->img.clouds_workspace,
                                                     (soc_stream)s, sky_bound);
              }, SOC_PASS_ASYNC);
@@ -1211,15 +1214,26 @@ static int switch_side_lane(soc_renderer* r, hipStream_t q) {
 }
 
 // Auto mode's probe, at the start of each frame (a call with the PRE phase): after 16 frames left to the clocks, eight
-// windows of 32 frames run the sky lane at high, low, low, high, high, low, low, high priority; timing events on the
-// caller's stream at each window's frames 8 and 32 give its mean frame interval over 24 frames (the first 8 after a
-// switch skipped). The ABBA order cancels a linear drift of the clocks over the probe (a plain high-then-low order read
+// windows (32 frames at 4K, up to 128 for smaller frames: probe_window) run the sky lane at high, low, low, high, high,
+// low, low, high priority; timing events on the caller's stream at each window's frame 8 and its end give its mean
+// frame interval (the first 8 after a switch skipped). The ABBA order cancels a linear drift of the clocks over the probe (a plain high-then-low order read
 // the warm-up as a slower high lane). High is kept only if its windows are faster by more than 1.5 % (C3 and C2
 // prefer low by 1-5 %, C4 high by 3-10 %; short C2 frames measured within the noise, profiles/r05_ab_lane_probe.txt),
 // once the last event has completed (queried, never waited on), for the renderer's life.
+// Frames per probe window: 32 at 3840x2160 and above, more for smaller frames (their intervals are shorter, so a
+// 32-frame window is within the timing noise), up to 128.
+static int probe_window(const soc_renderer* r) {
+    const long long px = (long long)r->img.color.width * r->img.color.height;
+    if (px <= 0) return 32;
+    return (int)std::min<long long>(128, std::max<long long>(32, 32LL * 8294400LL / px));
+}
+constexpr int kProbeStart = 16, kProbeWins = 8;
+static int probe_end(const soc_renderer* r) { return kProbeStart + kProbeWins * probe_window(r); }
+
 static int frame_lane_probe(soc_renderer* r, hipStream_t s) {
     if (r->side_queue != -1 || !r->lane_q[0]) return SOC_OK;
-    constexpr int kStart = 16, kWindow = 32, kSkip = 8, kWins = 8, kEnd = kStart + kWins * kWindow;
+    const int kStart = kProbeStart, kWindow = probe_window(r), kSkip = 8, kEnd = probe_end(r);
+    constexpr int kWins = kProbeWins;
     constexpr bool kHigh[kWins] = {true, false, false, true, true, false, false, true};
     const int f = r->probe_frames;
     if (f <= kEnd) {
@@ -1651,6 +1665,11 @@ extern "C" int soc_renderer_pass_stats(soc_renderer* r, int32_t i, float* total_
 }
 
 extern "C" int32_t soc_renderer_side_queue(const soc_renderer* r) { return (r && r->side) ? r->side_queue : -1; }
+
+extern "C" int32_t soc_renderer_side_queue_probe_frames(const soc_renderer* r) {
+    if (!r || !r->async || tuning_knob("SOC_RENDERER_SIDE_QUEUE", 3) != 3) return 0;
+    return probe_end(r) + 1;
+}
 
 extern "C" int32_t soc_renderer_pass_event_times(soc_renderer* r, int32_t i, void* base, float* start_ms, float* end_ms,
                                                  int32_t n) {

@@ -966,16 +966,18 @@ def test_render_graph_static_inputs_bit_identical(soc, inputs):
 
 @pytest.mark.parametrize("inputs", ["sponza", "terrain"])
 def test_sky_lane_queue_probe_bit_identical(soc, monkeypatch, inputs):
-    """The sky lane's hardware queue (SOC_RENDERER_SIDE_QUEUE): auto (3, default) runs frames 16-271 in eight windows
-    alternating between a high- and a low-priority stream (ABBA pairs) and then keeps one, moving the lane between
-    streams with an event wait; 1 / 2 fix it, 0 is the normal-priority stream. Every frame's output (every 4th texel)
-    and the final temporal state have the same bits in every mode (278 frames with per-frame globals, static inputs: the
-    clouds of frame N+1 start before frame N's TAA, also across the switches), and auto has chosen a queue by the end."""
+    """The sky lane's hardware queue (SOC_RENDERER_SIDE_QUEUE): auto (3, default) runs eight windows alternating between
+    a high- and a low-priority stream (ABBA pairs; with the sky-bound clouds variants in the high windows) and then keeps
+    one, moving the lane between streams with an event wait; 1 / 2 fix it, 0 is the normal-priority stream. Every
+    frame's output (every 8th texel) and the final temporal state have the same bits in every mode (the probe's frames
+    + 3, per-frame globals, static inputs: the clouds of frame N+1 start before frame N's TAA, also across the
+    switches), and auto has chosen a queue by the end."""
     import ctypes as C
     W, H = 1920, 1080
     g0, gb = (sponza_inputs if inputs == "sponza" else terrain_inputs)(W, H, elapsed=10.0)
     outs, chosen = [], []
-    for mode in ("0", "3", "1", "2"):
+    n_frames = 0
+    for mode in ("3", "0", "1", "2"):   # auto first: its probe length sets the frame count of every mode
         monkeypatch.setenv("SOC_RENDERER_SIDE_QUEUE", mode)
         soc.reload_tuning()
         fr = soc.alloc_frame(W, H, DEV, bloom_output=True)
@@ -988,13 +990,16 @@ def test_sky_lane_queue_probe_bit_identical(soc, monkeypatch, inputs):
         ji = C.c_uint32(0)
         g = soc.globals_defaults(W, H)
         seq = []
-        for f in range(278):
+        if mode == "3":
+            n_frames = r.side_queue_probe_frames() + 3
+            assert n_frames > 16
+        for f in range(n_frames):
             soc.frame_update(g, cam, W, H, 0.016, ji)
-            cam.position[0] += 0.003
+            cam.position[0] += 0.001
             r.execute(g)
-            seq.append(fr["output"][::4, ::4].clone())   # every 4th texel of every frame (and the final state in full)
-            if f == 274:
-                torch.cuda.synchronize()   # the probe's last event has completed: the next frame decides
+            seq.append(fr["output"][::8, ::8].clone())   # every 8th texel of every frame (and the final state in full)
+            if f == n_frames - 3:
+                torch.cuda.synchronize()   # the probe's last event has completed: the next frames decide
         torch.cuda.synchronize()
         seq.append(fr["output"].clone())
         seq.append(fr["auto_exposure"].clone())
@@ -1004,7 +1009,7 @@ def test_sky_lane_queue_probe_bit_identical(soc, monkeypatch, inputs):
         r.close()
     monkeypatch.delenv("SOC_RENDERER_SIDE_QUEUE")
     soc.reload_tuning()
-    assert chosen[0] == 0 and chosen[1] in (1, 2) and chosen[2] == 1 and chosen[3] == 2, chosen
+    assert chosen[0] in (1, 2) and chosen[1] == 0 and chosen[2] == 1 and chosen[3] == 2, chosen
     for o in outs[1:]:
         for f, (a, b) in enumerate(zip(outs[0], o)):
             assert torch.equal(a, b), f
