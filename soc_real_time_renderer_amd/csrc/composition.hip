@@ -327,6 +327,9 @@ __global__ __launch_bounds__(kWorkgroup) void composition_pair(DImg target, DImg
 // binned on the renderer's second lane right after CloudRendering, so Composition (sky_external) does not wait
 // for the clouds: the same tiling, texel fetch, f16 packing and bins as composition_pair's sky branch, hence
 // the same bits. 8-B stores of the sky pixels only (Composition writes the others concurrently).
+// CP (clouds rows 8-B aligned): a pair's two clouds texels in one 8-B load, issued once the depth shows a sky pixel in
+// the pair (one dependent load level instead of two); else the per-pixel form. The same texels.
+template <bool CP>
 __global__ __launch_bounds__(kWorkgroup) void sky_compose_pair(DImg target, DImg depth, DImg clouds, CompParams p) {
     __shared__ uint32_t sh[4 * kBins];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -339,13 +342,26 @@ __global__ __launch_bounds__(kWorkgroup) void sky_compose_pair(DImg target, DImg
     uint2 outp[2] = {uint2{0u, 0u}, uint2{0u, 0u}};
     if (inside) {
         const float2 d2 = row_ptr<float2>(depth, y)[x >> 1];
+        const bool s0 = d2.x == 1.0f, s1 = d2.y == 1.0f;
+        if (!CP) {
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            if ((k ? d2.y : d2.x) != 1.0f) continue;
-            const f4 cl = fetch_rgba8(clouds, x + k, y);
-            outp[k] = pack_h4(f4{cl.x, cl.y, cl.z, 1.0f});
-            row_ptr_w<uint2>(target, y)[x + k] = outp[k];
-            mine |= 1u << k;
+            for (int k = 0; k < 2; ++k) {
+                if (!(k ? s1 : s0)) continue;
+                const f4 cl = fetch_rgba8(clouds, x + k, y);
+                outp[k] = pack_h4(f4{cl.x, cl.y, cl.z, 1.0f});
+                row_ptr_w<uint2>(target, y)[x + k] = outp[k];
+                mine |= 1u << k;
+            }
+        } else if (s0 || s1) {   // both clouds texels of the pair in one 8-B load (the pair's x is even)
+            const uint2 cw = row_ptr<uint2>(clouds, y)[x >> 1];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                if (!(k ? s1 : s0)) continue;
+                const f4 cl = unpack_rgba8(k ? cw.y : cw.x);
+                outp[k] = pack_h4(f4{cl.x, cl.y, cl.z, 1.0f});
+                row_ptr_w<uint2>(target, y)[x + k] = outp[k];
+                mine |= 1u << k;
+            }
         }
     }
     const f4 c0 = unpack_h4(outp[0]), c1 = unpack_h4(outp[1]);
@@ -522,7 +538,14 @@ int soc::sky_compose_launch(const soc_globals* g, soc_img target, soc_img depth,
     p.lrange = g->log_max_luminance - g->log_min_luminance;
     p.bf = bin_fast_params(p.lmin, p.lrange);
     const dim3 grd(ceil_div(target.width, 32), ceil_div(target.height, 16));
-    launch("sky_compose_pair", kWorkgroup, sky_compose_pair, grd, kWorkgroup, 0, hs(stream), dimg(target), dimg(depth), dimg(clouds), p);
+    const bool cp = (clouds.pitch_bytes % 8) == 0 && (reinterpret_cast<uintptr_t>(clouds.data) % 8) == 0 &&
+                    tuning_knob("SOC_SKY_COMPOSE_PAIR_LOAD", 1);
+    if (cp)
+        launch("sky_compose_pair", kWorkgroup, sky_compose_pair<true>, grd, kWorkgroup, 0, hs(stream), dimg(target), dimg(depth),
+               dimg(clouds), p);
+    else
+        launch("sky_compose_pair", kWorkgroup, sky_compose_pair<false>, grd, kWorkgroup, 0, hs(stream), dimg(target), dimg(depth),
+               dimg(clouds), p);
     return check_launch("sky_compose");
 }
 

@@ -71,10 +71,10 @@ __device__ __forceinline__ T* row_ptr_w(const DImg& im, int y) {
 __device__ __forceinline__ f4 fetch_h4(const DImg& im, int x, int y) { return unpack_h4(row_ptr<uint2>(im, y)[x]); }
 __device__ __forceinline__ float fetch_f32(const DImg& im, int x, int y) { return row_ptr<float>(im, y)[x]; }
 __device__ __forceinline__ float fetch_r8(const DImg& im, int x, int y) { return unorm8(row_ptr<uint8_t>(im, y)[x]); }
-__device__ __forceinline__ f4 fetch_rgba8(const DImg& im, int x, int y) {
-    uint32_t v = row_ptr<uint32_t>(im, y)[x];
+__device__ __forceinline__ f4 unpack_rgba8(uint32_t v) {
     return f4{unorm8(v & 0xffu), unorm8((v >> 8) & 0xffu), unorm8((v >> 16) & 0xffu), unorm8(v >> 24)};
 }
+__device__ __forceinline__ f4 fetch_rgba8(const DImg& im, int x, int y) { return unpack_rgba8(row_ptr<uint32_t>(im, y)[x]); }
 
 // ---------------------------------------------------------------------------------------------
 // sampling contract (clamp-to-edge, 8-bit sub-texel precision)

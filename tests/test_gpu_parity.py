@@ -896,15 +896,18 @@ def test_render_graph_c3b_lights(soc, oracle):
 
 
 @pytest.mark.parametrize("phases", ["one-call", "split"])
-def test_render_graph_sky_split_bit_identical(soc, phases):
+def test_render_graph_sky_split_bit_identical(soc, monkeypatch, phases):
     """Sky split: the second lane writes and bins the colour image's sky pixels after the clouds, Composition skips
     them and does not wait. Against Composition writing them itself: the same bits over 3 frames (colour, output,
-    exposure, resolved history), for one-call frames and PRE / POST frames (the multi-GPU shape)."""
+    exposure, resolved history), for one-call frames and PRE / POST frames (the multi-GPU shape), with the sky pass
+    reading a pixel pair's clouds texels in one load (default) or one by one (SOC_SKY_COMPOSE_PAIR_LOAD=0)."""
     W, H = 1920, 1080
     g, gb = sponza_inputs(W, H, elapsed=10.0, camera=((-14.0, 2.2, 0.3), (0.0, -0.9, 0.0)))   # looking up: more sky
     assert (gb["depth"] == 1.0).mean() > 0.05
     outs = []
-    for split in (True, False):
+    for split, cp in ((True, "1"), (True, "0"), (False, "1")):
+        monkeypatch.setenv("SOC_SKY_COMPOSE_PAIR_LOAD", cp)
+        soc.reload_tuning()
         fr = soc.alloc_frame(W, H, DEV, bloom_output=True)
         for k in ("albedo", "emissive", "normal", "velocity", "depth"):
             fr[k].copy_(torch.from_numpy(gb[k]))
@@ -921,6 +924,8 @@ def test_render_graph_sky_split_bit_identical(soc, phases):
         outs.append({k: fr[k].clone() for k in ("clouds", "color", "output", "auto_exposure")})
         outs[-1]["resolved"] = r.resolved().clone()
         r.close()
+    monkeypatch.delenv("SOC_SKY_COMPOSE_PAIR_LOAD")
+    soc.reload_tuning()
     for o in outs[1:]:
         for k in outs[0]:
             assert torch.equal(outs[0][k], o[k]), k
