@@ -80,9 +80,11 @@ def point_lights_c3b(n=128, seed=0x3B):
             for _ in range(n)]
 
 
-def algorithmic_bytes(W, H, f_sky):
-    """Bytes each pass must move at the reference formats, per launch."""
+def algorithmic_bytes(W, H, f_sky, velocity_slots=False):
+    """Bytes each pass must move at the reference formats, per launch. velocity_slots: the velocity
+    history by slot rotation (SOC_RENDERER_VELOCITY_SLOTS), so TAA writes no velocity copy."""
     P = W * H
+    vcopy = 0.0 if velocity_slots else 8.0
     b = {
         "BloomDownsample - 0": 16.0 * P, "BloomDownsample - 1": (8.0 + 2.0) * P, "BloomDownsample - 2": (2.0 + 0.5) * P,
         "BloomDownsample - 3": (0.5 + 0.125) * P, "BloomUpsample - 3": (0.125 + 0.5) * P,
@@ -95,10 +97,10 @@ def algorithmic_bytes(W, H, f_sky):
         # fused composition + histogram: the bins come from the stored pixels in registers (+1 KiB)
         "Composition+GenerateLuminanceHistogram": (40.25 + 4.0 * f_sky) * P,
         "ResolveLuminanceHistogram": 2.0 * 1028.0,
-        "TemporalAntiAliasing": 52.0 * P,   # 44 B/px reference TAA + 8 B/px fused velocity history write
+        "TemporalAntiAliasing": (44.0 + vcopy) * P,   # 44 B/px reference TAA + 8 B/px fused velocity history write
         "ToneMapping": 12.0 * P,
         # fused TAA + tone map: the tone map reads the resolved pixels from registers (writes 4 B/px)
-        "TemporalAntiAliasing+ToneMapping": (52.0 + 4.0) * P,
+        "TemporalAntiAliasing+ToneMapping": (44.0 + vcopy + 4.0) * P,
     }
     return b
 
@@ -258,6 +260,10 @@ def main():
     ap.add_argument("--no-sky-lane", action="store_true", help="run CloudRendering on the frame stream too")
     ap.add_argument("--no-static-inputs", action="store_true",
                     help="fork the second lane at every frame start (no cross-frame overlap of the clouds)")
+    ap.add_argument("--no-velocity-slots", action="store_true",
+                    help="velocity history as the reference's per-frame copy (fused into TAA) instead of slot rotation "
+                         "(SOC_RENDERER_VELOCITY_SLOTS: the G-buffer's velocity lives in the history slot the next frame "
+                         "reads as previous)")
     ap.add_argument("--unfused-histogram", action="store_true",
                     help="Composition and the luminance histogram as two launches (SOC_RENDERER_UNFUSED_HISTOGRAM)")
     ap.add_argument("--write-frame", default="", help="write the last frame: tone-mapped framebuffer (.png) or HDR composition colour (.exr, f16)")
@@ -292,8 +298,14 @@ def main():
     f_sky = float((gb["depth"] == 1.0).mean())
     # the G-buffer, shadow map and noise stay resident and unchanged between frames (or come from the raster head):
     # the second lane may start a frame's clouds before the previous frame's TAA is done (SOC_RENDERER_STATIC_INPUTS)
+    # velocity history by slot rotation: the G-buffer's velocity is produced into the history slot the next frame reads
+    # as its previous velocity (the raster head writes it there every frame; the resident G-buffer holds it in both)
+    vslots = not args.no_velocity_slots
+    if vslots:
+        for hv in fr["history_velocity"]:
+            hv.copy_(fr["velocity"])
     r = soc.Renderer(fr, sky_lane=not args.no_sky_lane, fused_histogram=not args.unfused_histogram,
-                     static_inputs=not args.no_static_inputs)
+                     static_inputs=not args.no_static_inputs, velocity_slots=vslots)
     if args.raster:
         if sc is None:
             sc = raster.scene_setup(g, scene_id, tex_size=1024, device=device)
@@ -393,7 +405,7 @@ def main():
     for n, gname, ms, _ in stats:
         ms_group[gname] = round(ms_group.get(gname, 0.0) + ms, 4)
 
-    algo = algorithmic_bytes(W, H, f_sky)
+    algo = algorithmic_bytes(W, H, f_sky, velocity_slots=vslots)
     # Two durations per north-star kernel: alone = the serial per-pass loop above (every pass evented,
     # second lane off: nothing shares the CUs with the kernel), and in-frame = the timed frames' events (lanes
     # concurrent: the sky lane's kernels share the CUs, so the duration also carries their share). The roofline's
@@ -476,6 +488,8 @@ def main():
                    "sky_lane_queue": {1: "high priority", 2: "low priority", 0: "normal priority",
                                       -1: "not chosen"}.get(r.side_queue(), "?"),
                    "untimed_lane_probe_frames": probe_frames,
+                   "velocity_history": ("slot rotation (the G-buffer's velocity in the slot the next frame reads; "
+                                        "no copy)" if vslots else "copy fused into TAA"),
                    "raster": (f"in-frame: DepthPrepass + SunShadowDraw (4096^2) + GBufferGeneration of the "
                               f"{int(sc['mesh'].struct.triangle_count)}-triangle scene mesh") if args.raster
                    else "off: G-buffer and shadow map are resident inputs"},

@@ -399,6 +399,15 @@ typedef struct soc_renderer soc_renderer;
  * second lane's intermediate CLOUDS image may then already hold the next frame's clouds when work the caller queued
  * between two calls reads it: a caller that reads CLOUDS between frames leaves the flag off. */
 #define SOC_RENDERER_STATIC_INPUTS 256
+/* Velocity history by slot rotation instead of a copy. The reference copies the velocity image into
+ * previous_velocity after TAA every frame (CopyImageTask, renderer.cpp:1185-1189; without this flag the TAA launch
+ * writes that copy into the history_velocity slot it resolves into). With the flag, the frame's velocity image IS that
+ * slot: the velocity producer (GBufferGeneration of the raster head, or the caller) writes frame N's velocity into
+ * history_velocity[1 - soc_renderer_current_history(r)] (read before executing frame N), TAA reads it there and frame
+ * N + 1 reads it as its previous velocity, so no copy is made. images.velocity is then unused; caller passes receive the
+ * slot as `images->velocity`, and VELOCITY / PREVIOUS_VELOCITY declared by a pass count as uses of both slots. Same
+ * results as the copy for the same velocity fields. */
+#define SOC_RENDERER_VELOCITY_SLOTS 512
 
 soc_renderer* soc_renderer_create(const soc_frame_images* images, uint32_t flags);
 void soc_renderer_destroy(soc_renderer* r);

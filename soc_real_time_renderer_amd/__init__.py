@@ -356,7 +356,8 @@ class Renderer:
 
     def __init__(self, frame: dict, timing: bool = False, stream=None, fused_bloom: bool = True, sky_lane: bool = True,
                  fused_tonemap: bool = True, fused_histogram: bool = True,
-                 exact_bloom: bool = False, sky_split: bool = True, static_inputs: bool = False):
+                 exact_bloom: bool = False, sky_split: bool = True, static_inputs: bool = False,
+                 velocity_slots: bool = False):
         self.frame = frame
         fi = FrameImages()
         for k in ("albedo", "emissive", "normal", "depth", "velocity", "shadow", "noise", "ssao", "ssao_blur", "clouds",
@@ -378,7 +379,8 @@ class Renderer:
                  | (0 if sky_lane else _abi.RENDERER_SERIAL) | (0 if fused_tonemap else _abi.RENDERER_UNFUSED_TONEMAP)
                  | (0 if fused_histogram else _abi.RENDERER_UNFUSED_HISTOGRAM)
                  | (_abi.RENDERER_EXACT_BLOOM if exact_bloom else 0) | (0 if sky_split else _abi.RENDERER_NO_SKY_SPLIT)
-                 | (_abi.RENDERER_STATIC_INPUTS if static_inputs else 0))
+                 | (_abi.RENDERER_STATIC_INPUTS if static_inputs else 0)
+                 | (_abi.RENDERER_VELOCITY_SLOTS if velocity_slots else 0))
         h = lib().soc_renderer_create(C.byref(fi), flags)
         if not h:
             raise SocError(-1, lib().soc_last_error_string().decode())
@@ -528,6 +530,11 @@ class Renderer:
 
     def current_history(self) -> int:
         return int(lib().soc_renderer_current_history(self.handle))
+
+    def velocity_slot(self) -> int:
+        """With velocity_slots (SOC_RENDERER_VELOCITY_SLOTS): the history_velocity slot the NEXT frame's velocity goes
+        into (its producer writes it there; TAA reads it there and the frame after as its previous velocity)."""
+        return 1 - self.current_history()
 
     def resolved(self) -> torch.Tensor:
         return self.frame["history_color"][self.current_history()]

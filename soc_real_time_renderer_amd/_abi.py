@@ -40,6 +40,7 @@ RENDERER_EXACT_BLOOM = 32
 RENDERER_UNFUSED_HISTOGRAM = 64
 RENDERER_NO_SKY_SPLIT = 128
 RENDERER_STATIC_INPUTS = 256
+RENDERER_VELOCITY_SLOTS = 512
 HISTOGRAM_SCRATCH_WORDS = 2048
 
 Mat4 = C.c_float * 16

@@ -693,14 +693,28 @@ uint64_t res_mask(std::initializer_list<int> ids) {
     return m;
 }
 
+// SOC_RENDERER_VELOCITY_SLOTS: the frame's velocity image is the history_velocity slot the next frame reads as its
+// previous velocity, so VELOCITY and PREVIOUS_VELOCITY name the two slots of one ping-pong pair; a use of either is
+// taken as a use of both, which orders a next frame's velocity write after every reader of the slot it overwrites.
+uint64_t widen_velocity(const soc_renderer* r, uint64_t m) {
+    const uint64_t both = (1ull << SOC_RES_VELOCITY) | (1ull << SOC_RES_PREVIOUS_VELOCITY);
+    return (r->flags & SOC_RENDERER_VELOCITY_SLOTS) && (m & both) ? m | both : m;
+}
+
+// The frame's velocity image: images.velocity, or with SOC_RENDERER_VELOCITY_SLOTS the history_velocity slot this frame
+// resolves into (the reference copies velocity there after TAA, renderer.cpp:1185-1189; here its producer writes it there).
+soc_img frame_velocity(const soc_renderer* r) {
+    return (r->flags & SOC_RENDERER_VELOCITY_SLOTS) ? r->img.history_velocity[1 - r->hist] : r->img.velocity;
+}
+
 soc_renderer::Pass& add_pass(soc_renderer* r, std::string name, std::string group, int phase, uint64_t reads,
                              uint64_t writes, PassFn fn, uint32_t flags = 0) {
     soc_renderer::Pass p;
     p.name = std::move(name);
     p.group = std::move(group);
     p.phase = phase;
-    p.reads = reads;
-    p.writes = writes;
+    p.reads = widen_velocity(r, reads);
+    p.writes = widen_velocity(r, writes);
     p.flags = flags;
     p.run = std::move(fn);
     r->passes.push_back(std::move(p));
@@ -750,8 +764,8 @@ void build_raster_passes(soc_renderer* r) {
              [r](const soc_globals* g, hipStream_t s) {
                  const soc_frame_images& I = r->img;
                  return soc_gbuffer_resolve(g, &r->scene.mesh, r->scene.materials, r->scene.material_count,
-                                            r->scene.visibility, I.depth, I.albedo, I.emissive, I.normal, I.velocity,
-                                            r->scene.workspace, (soc_stream)s);
+                                            r->scene.visibility, I.depth, I.albedo, I.emissive, I.normal,
+                                            frame_velocity(r), r->scene.workspace, (soc_stream)s);
              });
 }
 
@@ -888,12 +902,14 @@ void build_passes_tail(soc_renderer* r) {
                  return soc::resolve_luminance_histogram(g, r->img.auto_exposure, r->total_pixels, r->wide,
                                                          r->fold_in_resolve ? r->hist_scratch : nullptr, (soc_stream)s);
              });
-    // renderer.cpp:1170-1198: TAA + both history copies (ping-pong + fused velocity history), and
+    // renderer.cpp:1170-1198: TAA + both history copies (ping-pong + fused velocity history; with
+    // SOC_RENDERER_VELOCITY_SLOTS the velocity is already in its history slot: no copy), and
     // renderer.cpp:1210-1217: tone mapping, fused into the TAA launch for an RGBA8 (UNORM or SRGB) framebuffer
+    const bool vslots = r->flags & SOC_RENDERER_VELOCITY_SLOTS;
     const uint64_t taa_reads = res_mask({SOC_RES_COLOR, SOC_RES_PREVIOUS_COLOR, SOC_RES_VELOCITY,
                                          SOC_RES_PREVIOUS_VELOCITY, SOC_RES_DEPTH}) |
                                (r->sky_split ? res_mask({SOC_RES_SKY_COLOR}) : 0);
-    const uint64_t taa_writes = res_mask({SOC_RES_RESOLVED, SOC_RES_PREVIOUS_VELOCITY});
+    const uint64_t taa_writes = vslots ? res_mask({SOC_RES_RESOLVED}) : res_mask({SOC_RES_RESOLVED, SOC_RES_PREVIOUS_VELOCITY});
     const bool fuse_tm = !(r->flags & SOC_RENDERER_UNFUSED_TONEMAP) &&
                          (I.output.format == SOC_FMT_RGBA8_UNORM || I.output.format == SOC_FMT_RGBA8_SRGB);
     if (fuse_tm) {
@@ -902,18 +918,21 @@ void build_passes_tail(soc_renderer* r) {
                  [r](const soc_globals* g, hipStream_t s) {
                      const auto& I = r->img;
                      const int p = r->hist, q = 1 - r->hist;
+                     const bool slots = r->flags & SOC_RENDERER_VELOCITY_SLOTS;
                      return soc_temporal_antialiasing_tone_mapping(g, I.history_color[q], I.color, I.history_color[p],
-                                                                   I.velocity, I.history_velocity[p], I.depth,
-                                                                   I.history_velocity[q], I.auto_exposure, I.output,
-                                                                   (soc_stream)s);
+                                                                   frame_velocity(r), I.history_velocity[p], I.depth,
+                                                                   slots ? soc_img{} : I.history_velocity[q],
+                                                                   I.auto_exposure, I.output, (soc_stream)s);
                  });
     } else {
         add_pass(r, "TemporalAntiAliasing", "Temporal Anti-Aliasing", post, taa_reads, taa_writes,
                  [r](const soc_globals* g, hipStream_t s) {
                      const auto& I = r->img;
                      const int p = r->hist, q = 1 - r->hist;
-                     return soc_temporal_antialiasing(g, I.history_color[q], I.color, I.history_color[p], I.velocity,
-                                                      I.history_velocity[p], I.depth, I.history_velocity[q], (soc_stream)s);
+                     const bool slots = r->flags & SOC_RENDERER_VELOCITY_SLOTS;
+                     return soc_temporal_antialiasing(g, I.history_color[q], I.color, I.history_color[p],
+                                                      frame_velocity(r), I.history_velocity[p], I.depth,
+                                                      slots ? soc_img{} : I.history_velocity[q], (soc_stream)s);
                  });
         add_pass(r, "ToneMapping", "Tone Mapping", post, res_mask({SOC_RES_RESOLVED, SOC_RES_AUTO_EXPOSURE}),
                  res_mask({SOC_RES_OUTPUT}), [r](const soc_globals* g, hipStream_t s) {
@@ -931,6 +950,7 @@ soc_frame_images callback_view(const soc_renderer* r) {
     v.history_color[1] = r->img.history_color[q];
     v.history_velocity[0] = r->img.history_velocity[p];
     v.history_velocity[1] = r->img.history_velocity[q];
+    v.velocity = frame_velocity(r);
     return v;
 }
 
@@ -958,8 +978,8 @@ int insert_user_passes(soc_renderer* r) {
         p.name = up.name;
         p.group = up.group;
         p.phase = up.desc.phase;
-        p.reads = widen_sky(r, desc_mask(up.desc.reads, up.desc.read_count));
-        p.writes = widen_sky(r, desc_mask(up.desc.writes, up.desc.write_count));
+        p.reads = widen_velocity(r, widen_sky(r, desc_mask(up.desc.reads, up.desc.read_count)));
+        p.writes = widen_velocity(r, widen_sky(r, desc_mask(up.desc.writes, up.desc.write_count)));
         p.flags = up.desc.flags;
         const soc_pass_callback fn = up.fn;
         void* user = up.user;
@@ -1078,6 +1098,12 @@ extern "C" soc_renderer* soc_renderer_create(const soc_frame_images* images, uin
     }
     if (!images->auto_exposure) {
         set_error(SOC_E_INVALID_ARG, "soc_renderer_create: auto_exposure buffer required");
+        return nullptr;
+    }
+    if ((flags & SOC_RENDERER_VELOCITY_SLOTS) &&
+        (!images->history_velocity[0].data || !images->history_velocity[1].data ||
+         images->history_velocity[0].data == images->history_velocity[1].data)) {
+        set_error(SOC_E_INVALID_ARG, "soc_renderer_create: SOC_RENDERER_VELOCITY_SLOTS needs two distinct history_velocity images");
         return nullptr;
     }
     soc_renderer* r = new soc_renderer();

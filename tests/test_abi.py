@@ -39,6 +39,20 @@ def test_ctypes_table_covers_header():
     assert set(declared_functions()) == set(_abi.FUNCTIONS)
 
 
+def test_renderer_flags_match_header():
+    """Every SOC_RENDERER_* flag bit of the header has its ctypes constant with the same value (and the bits are
+    distinct), so a Python caller sets the flag the C side tests."""
+    from soc_real_time_renderer_amd import _abi
+    src = open(HEADER).read()
+    flags = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define SOC_RENDERER_([A-Z_]+)\s+(\d+)", src)}
+    flags.pop("TIMING_RING")   # a ring length, not a flag
+    assert {"STATIC_INPUTS", "VELOCITY_SLOTS", "SERIAL"} <= set(flags)
+    for name, value in flags.items():
+        assert getattr(_abi, "RENDERER_" + name) == value, name
+        assert value & (value - 1) == 0, name
+    assert len(set(flags.values())) == len(flags)
+
+
 @pytest.mark.parametrize("name", ["soc_img", "soc_globals", "soc_sun_info", "soc_point_light", "soc_spot_light",
                                   "soc_auto_exposure", "soc_camera", "soc_frame_images", "soc_mesh", "soc_material",
                                   "soc_raster_scene"])

@@ -28,7 +28,11 @@ def test_bench_frame_4k_vs_oracle(soc, oracle, config, sky_range):
     W, H = (1920, 1080) if config == "c2" else (3840, 2160)
     dev = torch.device("cuda", 0)
     g, gb, shadow, noise, sc, fr = bench.build_inputs(config, "mesh", W, H, 0, dev)
-    r = soc.Renderer(fr, static_inputs=True)          # the bench's renderer flags
+    # the bench's renderer flags: static inputs, and the velocity history by slot rotation (the resident velocity in
+    # both history slots, as bench.py sets it up; the oracle's frame is given the same history)
+    for hv in fr["history_velocity"]:
+        hv.copy_(fr["velocity"])
+    r = soc.Renderer(fr, static_inputs=True, velocity_slots=True)
     r.set_exposure_pixels(W * H, False)
     assert r.pass_names() == ["BloomDownsample - 0+1", "BloomDownsample - 2+3", "BloomUpsample - 3+2",
                               "BloomUpsample - 1+0", "SSAOGeneration", "SSAOBlur", "CloudRendering",
@@ -38,6 +42,8 @@ def test_bench_frame_4k_vs_oracle(soc, oracle, config, sky_range):
     f_sky = float((gb["depth"] == 1.0).mean())
     assert sky_range[0] < f_sky < sky_range[1], f_sky
     hf = host_frame(W, H, {**gb, "shadow": shadow, "noise": noise})
+    for hv in hf["history_velocity"]:
+        hv[...] = gb["velocity"]
     ae = soc.AutoExposure()
     hist = 0
     for f in range(2):

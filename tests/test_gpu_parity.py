@@ -969,6 +969,60 @@ def test_render_graph_static_inputs_bit_identical(soc, inputs):
             assert torch.equal(a[k], b[k]), k
 
 
+def test_velocity_slots_bit_identical(soc):
+    """SOC_RENDERER_VELOCITY_SLOTS: the frame's velocity is written into the history_velocity slot the next frame reads as
+    its previous velocity (Renderer.velocity_slot()), instead of TAA copying images.velocity there (renderer.cpp:1185-1189).
+    Four frames with a different velocity field each (written by the caller before the frame) and a moving camera: every
+    frame's colour, framebuffer and resolved history, and the final velocity history slot, have the same bits as the
+    copy. A caller pass declaring VELOCITY receives the slot as images->velocity, and its declared uses widen to both
+    slots (PREVIOUS_VELOCITY too), which orders the next frame's velocity write after it."""
+    import ctypes as C
+    W, H = 1920, 1080
+    _g0, gb = sponza_inputs(W, H, elapsed=10.0)
+    gen = torch.Generator(device=DEV).manual_seed(7)
+    base = torch.from_numpy(gb["velocity"]).to(DEV)
+    fields = [base + (torch.rand(base.shape, generator=gen, device=DEV).half() - 0.5) * (0.002 * f) for f in range(4)]
+    outs = []
+    for slots in (False, True):
+        fr = soc.alloc_frame(W, H, DEV, bloom_output=True)
+        for k in ("albedo", "emissive", "normal", "velocity", "depth"):
+            fr[k].copy_(torch.from_numpy(gb[k]))
+        fr["shadow"] = dev(gb["shadow"])
+        fr["noise"].copy_(torch.from_numpy(gb["noise"]))
+        r = soc.Renderer(fr, velocity_slots=slots)
+        seen = []
+
+        def probe(gp, images, s):
+            seen.append(images.contents.velocity.data)
+            return 0
+        r.add_pass("VelocityProbe", probe, reads=["VELOCITY"], phase=soc.PHASE_POST_EXPOSURE)
+        idx = r.pass_names().index("VelocityProbe")
+        reads, _writes = r.pass_uses(idx)
+        assert ("PREVIOUS_VELOCITY" in reads) == slots, reads
+        cam = soc.make_camera((-14.0, 2.2, 0.3), (0.0, -0.42, 0.0))
+        ji = C.c_uint32(0)
+        g = soc.globals_defaults(W, H)
+        seq, expect = [], []
+        for f in range(4):
+            soc.frame_update(g, cam, W, H, 0.016, ji)
+            cam.position[0] += 0.05
+            target = fr["history_velocity"][r.velocity_slot()] if slots else fr["velocity"]
+            target.copy_(fields[f])
+            expect.append(target.data_ptr())
+            r.execute(g)
+            seq.append({k: fr[k].clone() for k in ("color", "output")} | {"resolved": r.resolved().clone()})
+        torch.cuda.synchronize()
+        seq.append({"velocity_history": fr["history_velocity"][r.current_history()].clone(),
+                    "auto_exposure": fr["auto_exposure"].clone()})
+        assert seen == expect, (slots, seen, expect)
+        outs.append(seq)
+        r.close()
+    for a, b in zip(*outs):
+        for k in a:
+            assert torch.equal(a[k], b[k]), k
+    assert torch.equal(outs[1][-1]["velocity_history"], fields[-1])
+
+
 @pytest.mark.parametrize("inputs", ["sponza", "terrain"])
 def test_sky_lane_queue_probe_bit_identical(soc, monkeypatch, inputs):
     """The sky lane's hardware queue (SOC_RENDERER_SIDE_QUEUE): auto (3, default) runs eight windows alternating between

@@ -156,6 +156,34 @@ def test_gbuffer_resolve(soc, oracle, scene_id, camera, W, H):
         assert torch.equal(out[k], out2[k]), k
 
 
+def test_render_graph_raster_head_velocity_slots(soc):
+    """SOC_RENDERER_VELOCITY_SLOTS with the raster head: GBufferGeneration writes the frame's velocity straight into the
+    history_velocity slot the next frame reads as previous (no TAA copy); 3 frames have the same colour, framebuffer and
+    velocity history bits as the copy."""
+    W, H = 640, 360
+    g = globals_for(W, H, camera=SPONZA_CAMERA, elapsed=10.0)
+    sc = raster.scene_setup(g, scene.SPONZA_PROXY, tex_size=128)
+    outs = []
+    for slots in (False, True):
+        fr = soc.alloc_frame(W, H, DEV, bloom_output=True)
+        fr["noise"].copy_(torch.from_numpy(scene.noise_texture()))
+        fr["shadow"] = torch.zeros((1024, 1024), dtype=torch.float32, device=DEV)
+        vis = torch.zeros((H, W), dtype=torch.int64, device=DEV)
+        r = soc.Renderer(fr, velocity_slots=slots)
+        r.set_raster_scene(sc["mesh"], sc["materials"], sc["material_count"], vis, sc["workspace"], shadow=True)
+        seq = []
+        for _ in range(3):
+            r.execute(g)
+            seq.append({k: fr[k].clone() for k in ("color", "output")})
+        torch.cuda.synchronize()
+        seq.append({"velocity_history": fr["history_velocity"][r.current_history()].clone()})
+        outs.append(seq)
+        r.close()
+    for a, b in zip(*outs):
+        for k in a:
+            assert torch.equal(a[k], b[k]), k
+
+
 @pytest.mark.parametrize("scene_id,camera,fail_ws", [(scene.SPONZA_PROXY, SPONZA_CAMERA, False),
                                                     (scene.TERRAIN, TERRAIN_CAMERA, False),
                                                     (scene.SPONZA_PROXY, SPONZA_CAMERA, True)])

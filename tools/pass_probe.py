@@ -73,8 +73,10 @@ def child(pass_name, configs, reps):
             hv[0].copy_(fr["velocity"])
             ae = fr["auto_exposure"]
             tgt = hc[1]
+            # SOC_PROBE_TAA_VOUT=0: no fused velocity-history write (the renderer's velocity slots, SOC_RENDERER_VELOCITY_SLOTS)
+            vout = hv[1] if os.environ.get("SOC_PROBE_TAA_VOUT", "1") != "0" else None
             run = lambda: soc.temporal_antialiasing_tone_mapping(g, hc[1], fr["color"], hc[0], fr["velocity"],  # noqa: E731
-                                                                 hv[0], fr["depth"], ae, fr["output"], hv[1])
+                                                                 hv[0], fr["depth"], ae, fr["output"], vout)
         else:
             raise SystemExit(f"unknown pass {pass_name}")
         for _ in range(10):
