@@ -80,11 +80,14 @@ def point_lights_c3b(n=128, seed=0x3B):
             for _ in range(n)]
 
 
-def algorithmic_bytes(W, H, f_sky, velocity_slots=False):
+def algorithmic_bytes(W, H, f_sky, velocity_slots=False, bloom_in_composition=False):
     """Bytes each pass must move at the reference formats, per launch. velocity_slots: the velocity
-    history by slot rotation (SOC_RENDERER_VELOCITY_SLOTS), so TAA writes no velocity copy."""
+    history by slot rotation (SOC_RENDERER_VELOCITY_SLOTS), so TAA writes no velocity copy. bloom_in_composition: the
+    bloom chain's last stage inside Composition (SOC_RENDERER_BLOOM_IN_COMPOSITION), which reads mip1 (2 B/px) instead
+    of the bloom output (8 B/px)."""
     P = W * H
     vcopy = 0.0 if velocity_slots else 8.0
+    em = 2.0 if bloom_in_composition else 8.0
     b = {
         "BloomDownsample - 0": 16.0 * P, "BloomDownsample - 1": (8.0 + 2.0) * P, "BloomDownsample - 2": (2.0 + 0.5) * P,
         "BloomDownsample - 3": (0.5 + 0.125) * P, "BloomUpsample - 3": (0.125 + 0.5) * P,
@@ -95,7 +98,7 @@ def algorithmic_bytes(W, H, f_sky, velocity_slots=False):
         "SSAOGeneration": 12.25 * P, "SSAOBlur": 0.5 * P, "CloudRendering": 8.0 * P,
         "Composition": (40.25 + 4.0 * f_sky) * P, "GenerateLuminanceHistogram": 8.0 * P,
         # fused composition + histogram: the bins come from the stored pixels in registers (+1 KiB)
-        "Composition+GenerateLuminanceHistogram": (40.25 + 4.0 * f_sky) * P,
+        "Composition+GenerateLuminanceHistogram": (40.25 - 8.0 + em + 4.0 * f_sky) * P,
         "ResolveLuminanceHistogram": 2.0 * 1028.0,
         "TemporalAntiAliasing": (44.0 + vcopy) * P,   # 44 B/px reference TAA + 8 B/px fused velocity history write
         "ToneMapping": 12.0 * P,
@@ -264,6 +267,9 @@ def main():
                     help="velocity history as the reference's per-frame copy (fused into TAA) instead of slot rotation "
                          "(SOC_RENDERER_VELOCITY_SLOTS: the G-buffer's velocity lives in the history slot the next frame "
                          "reads as previous)")
+    ap.add_argument("--no-bloom-in-composition", action="store_true",
+                    help="the bloom chain's last stage as its own pass writing the full-resolution bloom output "
+                         "(default: computed inside the fused Composition launch, SOC_RENDERER_BLOOM_IN_COMPOSITION)")
     ap.add_argument("--unfused-histogram", action="store_true",
                     help="Composition and the luminance histogram as two launches (SOC_RENDERER_UNFUSED_HISTOGRAM)")
     ap.add_argument("--write-frame", default="", help="write the last frame: tone-mapped framebuffer (.png) or HDR composition colour (.exr, f16)")
@@ -305,7 +311,8 @@ def main():
         for hv in fr["history_velocity"]:
             hv.copy_(fr["velocity"])
     r = soc.Renderer(fr, sky_lane=not args.no_sky_lane, fused_histogram=not args.unfused_histogram,
-                     static_inputs=not args.no_static_inputs, velocity_slots=vslots)
+                     static_inputs=not args.no_static_inputs, velocity_slots=vslots,
+                     bloom_in_composition=not args.no_bloom_in_composition)
     if args.raster:
         if sc is None:
             sc = raster.scene_setup(g, scene_id, tex_size=1024, device=device)
@@ -405,7 +412,10 @@ def main():
     for n, gname, ms, _ in stats:
         ms_group[gname] = round(ms_group.get(gname, 0.0) + ms, 4)
 
-    algo = algorithmic_bytes(W, H, f_sky, velocity_slots=vslots)
+    # the renderer computes the bloom's last stage inside Composition in frames whose sky lane is the critical path
+    # (SOC_RENDERER_BLOOM_IN_COMPOSITION: the lane probe chose a high-priority sky lane)
+    bloom_in_comp = not args.no_bloom_in_composition and "BloomUpsample - 3+2" in names and r.side_queue() == 1
+    algo = algorithmic_bytes(W, H, f_sky, velocity_slots=vslots, bloom_in_composition=bloom_in_comp)
     # Two durations per north-star kernel: alone = the serial per-pass loop above (every pass evented,
     # second lane off: nothing shares the CUs with the kernel), and in-frame = the timed frames' events (lanes
     # concurrent: the sky lane's kernels share the CUs, so the duration also carries their share). The roofline's
@@ -488,6 +498,9 @@ def main():
                    "sky_lane_queue": {1: "high priority", 2: "low priority", 0: "normal priority",
                                       -1: "not chosen"}.get(r.side_queue(), "?"),
                    "untimed_lane_probe_frames": probe_frames,
+                   "bloom_last_stage": ("inside Composition (mip1 -> [mip0] -> emissive term per tile in LDS; the "
+                                        "full-resolution bloom output is not written)" if bloom_in_comp
+                                        else "its own pass (writes the bloom output)"),
                    "velocity_history": ("slot rotation (the G-buffer's velocity in the slot the next frame reads; "
                                         "no copy)" if vslots else "copy fused into TAA"),
                    "raster": (f"in-frame: DepthPrepass + SunShadowDraw (4096^2) + GBufferGeneration of the "

@@ -408,6 +408,14 @@ typedef struct soc_renderer soc_renderer;
  * slot as `images->velocity`, and VELOCITY / PREVIOUS_VELOCITY declared by a pass count as uses of both slots. Same
  * results as the copy for the same velocity fields. */
 #define SOC_RENDERER_VELOCITY_SLOTS 512
+/* The bloom chain's last stage (upsample 1 + 0: mip1 -> [mip0] -> bloom output, renderer.cpp:1044-1062) may be computed
+ * inside the fused Composition + histogram launch, per 32 x 16 tile in LDS, from BLOOM_MIP1 (the same values per pixel,
+ * rounded to RGBA16F as the chain stores them, so the same colour bits). The renderer does so in frames whose sky lane
+ * is the critical path (soc_renderer_side_queue() == 1); the chain's fourth pass is then skipped and the
+ * full-resolution bloom output (images.bloom_output, or the emissive image in place) is NOT written. Composition
+ * declares BLOOM_MIP1 besides the bloom output. Applies with the weighted chain and the fused histogram's pair path. A
+ * caller that reads the bloom output leaves the flag off. */
+#define SOC_RENDERER_BLOOM_IN_COMPOSITION 1024
 
 soc_renderer* soc_renderer_create(const soc_frame_images* images, uint32_t flags);
 void soc_renderer_destroy(soc_renderer* r);

@@ -357,7 +357,7 @@ class Renderer:
     def __init__(self, frame: dict, timing: bool = False, stream=None, fused_bloom: bool = True, sky_lane: bool = True,
                  fused_tonemap: bool = True, fused_histogram: bool = True,
                  exact_bloom: bool = False, sky_split: bool = True, static_inputs: bool = False,
-                 velocity_slots: bool = False):
+                 velocity_slots: bool = False, bloom_in_composition: bool = False):
         self.frame = frame
         fi = FrameImages()
         for k in ("albedo", "emissive", "normal", "depth", "velocity", "shadow", "noise", "ssao", "ssao_blur", "clouds",
@@ -380,7 +380,8 @@ class Renderer:
                  | (0 if fused_histogram else _abi.RENDERER_UNFUSED_HISTOGRAM)
                  | (_abi.RENDERER_EXACT_BLOOM if exact_bloom else 0) | (0 if sky_split else _abi.RENDERER_NO_SKY_SPLIT)
                  | (_abi.RENDERER_STATIC_INPUTS if static_inputs else 0)
-                 | (_abi.RENDERER_VELOCITY_SLOTS if velocity_slots else 0))
+                 | (_abi.RENDERER_VELOCITY_SLOTS if velocity_slots else 0)
+                 | (_abi.RENDERER_BLOOM_IN_COMPOSITION if bloom_in_composition else 0))
         h = lib().soc_renderer_create(C.byref(fi), flags)
         if not h:
             raise SocError(-1, lib().soc_last_error_string().decode())

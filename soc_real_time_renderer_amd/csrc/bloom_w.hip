@@ -18,7 +18,7 @@
 // by the next upsample (quirk Q5 overwrites them), so mips[0] and mips[2] are not written: their final
 // contents are unobservable in the reference graph. An intermediate tile entry at an out-of-image
 // coordinate holds the value of the clamped coordinate, which is what the next pass's clamped taps read.
-#include "soc_internal.hpp"
+#include "bloom_w.hpp"
 
 namespace soc {
 // The chain's fixed-ratio fast paths apply when the four mips halve exactly (the reference's mip chain at even
@@ -37,44 +37,6 @@ bool bloom_fused_applicable(const soc_img& emissive, const soc_img* mips, int mi
 
 namespace soc {
 namespace {
-
-__device__ __forceinline__ int clampi(int v, int lo, int hi) { return min(max(v, lo), hi); }
-
-struct C3 {
-    float r, g, b;
-};
-__device__ __forceinline__ float lo16(uint32_t u) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(u & 0xffffu)); }
-__device__ __forceinline__ float hi16(uint32_t u) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(u >> 16)); }
-// a += w * texel.rgb (one v_fma_mix_f32 per channel)
-__device__ __forceinline__ void madd(C3& a, uint2 t, float w) {
-    a.r = __builtin_fmaf(lo16(t.x), w, a.r);
-    a.g = __builtin_fmaf(hi16(t.x), w, a.g);
-    a.b = __builtin_fmaf(lo16(t.y), w, a.b);
-}
-__device__ __forceinline__ uint2 pack3(const C3& c) { return pack_h4(f4{c.r, c.g, c.b, 1.0f}); }
-
-// Clamp-to-edge tile load: t[r][c] = im[clamp(oy + r)][clamp(ox + c)]. Each lane issues its loads four at a time
-// before their LDS stores (one memory latency per four rounds of the 256-lane loop instead of one per round).
-template <int TW, int TH>
-__device__ __forceinline__ void load_tile(const DImg& im, int ox, int oy, uint2 (*t)[TW], int tid) {
-    constexpr int N = TW * TH;
-    auto at = [&](int i) {
-        const int r = i / TW, c = i - r * TW;
-        return row_ptr<uint2>(im, clampi(oy + r, 0, im.h - 1)) + clampi(ox + c, 0, im.w - 1);
-    };
-    for (int i0 = tid; i0 < N; i0 += 4 * 256) {
-        const int i1 = i0 + 256, i2 = i1 + 256, i3 = i2 + 256;
-        const uint2 a = *at(i0);
-        uint2 b = uint2{0u, 0u}, c = b, d = b;
-        if (i1 < N) b = *at(i1);
-        if (i2 < N) c = *at(i2);
-        if (i3 < N) d = *at(i3);
-        t[i0 / TW][i0 % TW] = a;
-        if (i1 < N) t[i1 / TW][i1 % TW] = b;
-        if (i2 < N) t[i2 / TW][i2 % TW] = c;
-        if (i3 < N) t[i3 / TW][i3 % TW] = d;
-    }
-}
 
 // Two horizontally adjacent outputs, one 16-B store when the row allows it.
 __device__ __forceinline__ void store2(const DImg& im, int x, int y, uint2 a, uint2 b, bool vec) {
@@ -125,10 +87,6 @@ __device__ __forceinline__ C3 down21(const uint2 (*t)[TW], int c0, int r0) {
 
 // up 1:2: the pair of horizontally adjacent outputs (2X, 2X+1) of output row y (parity py) from the
 // 5x4 lower-texel block whose top-left tile texel is (X - 2, Y - 2 + py)
-__device__ __forceinline__ constexpr float u12_w(int parity, int k) {   // k = 0..3 along the 4-texel footprint
-    constexpr int E[4] = {1, 5, 7, 3}, O[4] = {3, 7, 5, 1};
-    return (float)(parity ? O[k] : E[k]) * (1.0f / 16.0f);
-}
 template <int TW>
 __device__ __forceinline__ void up12_pair(const uint2 (*t)[TW], int c0, int r0, int py, C3& even, C3& odd) {
     even = C3{0.0f, 0.0f, 0.0f};
@@ -440,76 +398,20 @@ __global__ __launch_bounds__(kWorkgroup) void bloomw_up10(DImg S1, DImg O, bool 
 // horizontal pass into an fp32 LDS tile and a vertical pass: per mip0 entry 4 + 4 taps instead of 16, per output 3 + 3
 // instead of 9. The same weights and footprints (the mip0 entries still rounded to RGBA16F, as the chain stores them);
 // the sums are grouped by rows, so the last fp32 bits may differ from bloomw_up10 (within the RGBA16F tolerance).
-struct P3 {
-    float r[W4_SH > W4_MH ? W4_SH : W4_MH][W4_MW];   // largest of the two intermediates (14 x 66 and 18 x 64)
-    float g[W4_SH > W4_MH ? W4_SH : W4_MH][W4_MW];
-    float b[W4_SH > W4_MH ? W4_SH : W4_MH][W4_MW];
-};
 __global__ __launch_bounds__(kWorkgroup) void bloomw_up10s(DImg S1, DImg O, bool vec, int swz) {
-    __shared__ uint2 st[W4_SH][W4_SW];
-    __shared__ uint2 mt[W4_MH][W4_MW];
-    __shared__ P3 hp;   // horizontal sums: first of the 1:2 pass (st rows x mip0 columns), then of the 1:1 pass
+    __shared__ Up10Tile<U_OW, U_OH> t;   // bloom_w.hpp (shared with Composition's in-kernel upsample)
     const int tid = threadIdx.x;
     int tbx, tby;
     xcd_order(swz, tbx, tby);
     const int X0 = tbx * U_OW, Y0 = tby * U_OH;
-    const int mx0 = X0 - 1, my0 = Y0 - 1;
-    const int sx0 = X0 / 2 - 3, sy0 = Y0 / 2 - 3;
-    const int W0 = O.w, H0 = O.h;
-    load_tile<W4_SW, W4_SH>(S1, sx0, sy0, st, tid);
-    __syncthreads();
-    // 1:2 horizontal: hp[sr][c] for mip0 column c (coordinate clamp(mx0 + c)) on mip1 tile row sr
-    for (int i = tid; i < W4_SH * W4_MW; i += 256) {
-        const int sr = i / W4_MW, c = i - sr * W4_MW;
-        const int q = clampi(mx0 + c, 0, W0 - 1), px = q & 1, c0 = (q >> 1) - 2 + px - sx0;
-        C3 a{0.0f, 0.0f, 0.0f};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) madd(a, st[sr][c0 + k], u12_w(px, k));
-        hp.r[sr][c] = a.r;
-        hp.g[sr][c] = a.g;
-        hp.b[sr][c] = a.b;
-    }
-    __syncthreads();
-    // 1:2 vertical: the mip0 entries (RGBA16F, as stored by the chain)
-    for (int i = tid; i < W4_MH * W4_MW; i += 256) {
-        const int r = i / W4_MW, c = i - r * W4_MW;
-        const int cy = clampi(my0 + r, 0, H0 - 1), py = cy & 1, r0 = (cy >> 1) - 2 + py - sy0;
-        C3 a{0.0f, 0.0f, 0.0f};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const float w = u12_w(py, k);
-            a.r = __builtin_fmaf(hp.r[r0 + k][c], w, a.r);
-            a.g = __builtin_fmaf(hp.g[r0 + k][c], w, a.g);
-            a.b = __builtin_fmaf(hp.b[r0 + k][c], w, a.b);
-        }
-        mt[r][c] = pack3(a);
-    }
-    __syncthreads();
-    // 1:1 horizontal: hp[r][x - X0] over mip0 row r for output column x (tile columns x - mx0 - 1 .. + 1)
-    for (int i = tid; i < W4_MH * U_OW; i += 256) {
-        const int r = i / U_OW, c = i - r * U_OW;   // tile column c + 1
-        C3 a{0.0f, 0.0f, 0.0f};
-        madd(a, mt[r][c], 1.0f);
-        madd(a, mt[r][c + 1], 2.0f);
-        madd(a, mt[r][c + 2], 1.0f);
-        hp.r[r][c] = a.r;
-        hp.g[r][c] = a.g;
-        hp.b[r][c] = a.b;
-    }
-    __syncthreads();
+    t.build(S1, X0, Y0, O.w, O.h, tid);
     // 1:1 vertical and the stores (pairs)
     for (int i = tid; i < (U_OW / 2) * U_OH; i += 256) {
         const int r = i / (U_OW / 2), pc = i - r * (U_OW / 2);
         const int x = X0 + 2 * pc, y = Y0 + r;
         if (x >= O.w || y >= O.h) continue;
         C3 o[2];
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const int c = 2 * pc + k;
-            o[k].r = __builtin_fmaf(hp.r[r + 2][c], 1.0f / 16.0f, __builtin_fmaf(hp.r[r + 1][c], 2.0f / 16.0f, hp.r[r][c] * (1.0f / 16.0f)));
-            o[k].g = __builtin_fmaf(hp.g[r + 2][c], 1.0f / 16.0f, __builtin_fmaf(hp.g[r + 1][c], 2.0f / 16.0f, hp.g[r][c] * (1.0f / 16.0f)));
-            o[k].b = __builtin_fmaf(hp.b[r + 2][c], 1.0f / 16.0f, __builtin_fmaf(hp.b[r + 1][c], 2.0f / 16.0f, hp.b[r][c] * (1.0f / 16.0f)));
-        }
+        t.out(r, 2 * pc, o);
         store2(O, x, y, pack3(o[0]), pack3(o[1]), vec);
     }
 }

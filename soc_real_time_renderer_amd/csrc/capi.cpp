@@ -676,6 +676,8 @@ struct soc_renderer {
     bool fold_in_resolve = false;
     // sky split configured (graph) / active this frame (the pair path applies at the globals' resolution)
     bool sky_split = false, sky_split_active = false;
+    bool bloom_in_comp = false;          // SOC_RENDERER_BLOOM_IN_COMPOSITION applies to this graph
+    bool bloom_in_comp_active = false;   // ... and this frame computes the bloom's last stage inside Composition
     // the caller's stream is ordered after all second-lane work of the previous call (its join or an equivalent wait)
     bool main_after_side = true;
     // SOC_RENDERER_STATIC_INPUTS: a call of this graph has completed, so the frame inputs the caller wrote before its
@@ -778,17 +780,31 @@ void build_passes(soc_renderer* r) {
     const int dst_res = I.bloom_output.data ? SOC_RES_BLOOM_OUTPUT : SOC_RES_EMISSIVE;
     const int mip[4] = {SOC_RES_BLOOM_MIP0, SOC_RES_BLOOM_MIP1, SOC_RES_BLOOM_MIP2, SOC_RES_BLOOM_MIP3};
     const bool chain_ok = bloom_fused_applicable(I.emissive, I.bloom_mips, nm, bloom_dst);
+    r->bloom_in_comp = false;
     if (chain_ok && !(r->flags & (SOC_RENDERER_EXACT_BLOOM | SOC_RENDERER_UNFUSED_BLOOM))) {
         // weighted form (bloom_w.hip): 4 launches, mip0 / mip2 only in LDS, within the RGBA16F tolerance
         static const char* names[4] = {"BloomDownsample - 0+1", "BloomDownsample - 2+3", "BloomUpsample - 3+2",
                                        "BloomUpsample - 1+0"};
         const uint64_t rd[4] = {res_mask({SOC_RES_EMISSIVE}), res_mask({mip[1]}), res_mask({mip[3]}), res_mask({mip[1]})};
         const uint64_t wr[4] = {res_mask({mip[1]}), res_mask({mip[3]}), res_mask({mip[1]}), res_mask({dst_res})};
-        for (int st = 1; st <= 4; ++st)
-            add_pass(r, names[st - 1], "Bloom", pre, rd[st - 1], wr[st - 1], [r, st](const soc_globals* g, hipStream_t s) {
+        // SOC_RENDERER_BLOOM_IN_COMPOSITION: where the fused composition + histogram's pair path applies, the last stage
+        // (mip1 -> [mip0] -> output) may run inside that launch (composition_pair<..., BL>) in a frame whose sky lane is
+        // the critical path (the lane probe chose high priority): the fourth pass is then skipped and the bloom output
+        // not written. Beside a low-priority sky lane the fused kernel's 19 KiB of LDS per workgroup do not fit next to
+        // the sun-visibility march's noise tables (C3: Composition 76 -> 122 us in the frame, -0.6 % fps; C4 +2.9 %,
+        // profiles/r05_ab_bloom_in_composition.txt), so those frames keep the separate pass.
+        soc_globals gres{};
+        gres.resolution[0] = I.color.width;
+        gres.resolution[1] = I.color.height;
+        r->bloom_in_comp = (r->flags & SOC_RENDERER_BLOOM_IN_COMPOSITION) && !(r->flags & SOC_RENDERER_UNFUSED_HISTOGRAM) &&
+                           soc::composition_pair_applicable(&gres, I.color, I.albedo, bloom_dst, I.normal, I.depth, I.clouds);
+        for (int st = 1; st <= 4; ++st) {
+            auto& bp = add_pass(r, names[st - 1], "Bloom", pre, rd[st - 1], wr[st - 1], [r, st](const soc_globals* g, hipStream_t s) {
                 const soc_img& dst = r->img.bloom_output.data ? r->img.bloom_output : r->img.emissive;
                 return soc_bloom_weighted_stage(g, r->img.emissive, r->img.bloom_mips, 4, dst, st, (soc_stream)s);
             });
+            if (st == 4 && r->bloom_in_comp) bp.skip = [r] { return r->bloom_in_comp_active; };
+        }
         return;
     }
     // renderer.cpp:1024-1042: the bit-exact per-pass chain (SOC_RENDERER_EXACT_BLOOM / _UNFUSED_BLOOM, or mips that do
@@ -862,7 +878,8 @@ void build_passes_tail(soc_renderer* r) {
     // renderer.cpp:1103-1117 (composition uses) and 1155-1162 (histogram): one launch by default (the colour
     // is binned as it is written), two with SOC_RENDERER_UNFUSED_HISTOGRAM (measured in composition.hip)
     const uint64_t comp_reads = res_mask({SOC_RES_ALBEDO, em_res, SOC_RES_NORMAL, SOC_RES_DEPTH, SOC_RES_SSAO_BLUR,
-                                          SOC_RES_SUN_SHADOW}) | (r->sky_split ? 0 : res_mask({SOC_RES_CLOUDS}));
+                                          SOC_RES_SUN_SHADOW}) | (r->bloom_in_comp ? res_mask({SOC_RES_BLOOM_MIP1}) : 0) |
+                                (r->sky_split ? 0 : res_mask({SOC_RES_CLOUDS}));
     if (fused_hist) {
         add_pass(r, "Composition+GenerateLuminanceHistogram", "Composition", pre, comp_reads,
                  res_mask({SOC_RES_COLOR, SOC_RES_HISTOGRAM_PARTIALS}), [r](const soc_globals* g, hipStream_t s) {
@@ -871,7 +888,8 @@ void build_passes_tail(soc_renderer* r) {
                      return soc::composition_luminance_histogram(g, I.d_globals, I.color, I.albedo, em, I.normal, I.depth,
                                                                  I.ssao_blur, I.shadow, I.clouds, I.auto_exposure,
                                                                  r->hist_scratch, false, (soc_stream)s,
-                                                                 r->sky_split_active);
+                                                                 r->sky_split_active,
+                                                                 r->bloom_in_comp_active ? &I.bloom_mips[1] : nullptr);
                  });
         // the 8 partial histograms of the fused launch into the AutoExposure bins. Before a multi-GPU exchange
         // (PRE and POST in separate calls) the fold must precede it; in a one-call frame the resolve folds them
@@ -1322,6 +1340,9 @@ extern "C" int soc_renderer_execute(soc_renderer* r, const soc_globals* g, int32
     hipStream_t s = hs(stream);
     r->fold_in_resolve = (phase & SOC_PHASE_ALL) == SOC_PHASE_ALL && !(r->flags & SOC_RENDERER_UNFUSED_HISTOGRAM);
     if (phase & SOC_PHASE_PRE_EXPOSURE) {
+        // the bloom's last stage inside Composition in a frame whose sky lane is the critical path (see build_passes)
+        // (the lane's choice, kept while set_async(0) serialises a frame, so a serial profiling frame runs the same kernels)
+        r->bloom_in_comp_active = r->bloom_in_comp && r->side_queue == 1;
         const soc_img& em = r->img.bloom_output.data ? r->img.bloom_output : r->img.emissive;
         r->sky_split_active = r->sky_split && soc::composition_pair_applicable(g, r->img.color, r->img.albedo, em,
                                                                                r->img.normal, r->img.depth, r->img.clouds);

@@ -9,6 +9,9 @@
 // 89 -> 75 us at 4K against 128x1 strips). Full-res taps are plain loads (a centre sample under the
 // sampling contract is the texel itself). The dead volumetric-fog block (:176-196, zeroed at :196)
 // is not computed.
+#include <type_traits>
+
+#include "bloom_w.hpp"
 #include "luminance.hpp"
 #include "soc_internal.hpp"
 
@@ -218,9 +221,14 @@ constexpr int BX = 64, BY = 4;
 // device atomic per workgroup: 16,200 of them serialise across the XCDs, 68 -> 207 us.)
 // LIGHTS = false: no point / spot lights this frame (the reference default): the light loops are not
 // compiled in, which keeps the kernel at a fraction of the registers (more waves, more loads in flight).
-template <bool HIST, bool LIGHTS, int NT = 0>
+// BL (SOC_RENDERER_BLOOM_IN_COMPOSITION): the bloom chain's last upsample pair (mip1 -> [mip0] -> output, bloomw_up10s)
+// is computed for the workgroup's 32 x 16 tile in LDS (Up10Tile, bloom_w.hpp: the same values per pixel, rounded to
+// RGBA16F as the chain stores its output) while the G-buffer loads are in flight, and used as the emissive input, so
+// the full-resolution bloom output is neither written by the chain nor read back here (16 B/px). `emissive` unused.
+template <bool HIST, bool LIGHTS, int NT = 0, bool BL = false>
 __global__ __launch_bounds__(kWorkgroup) void composition_pair(DImg target, DImg albedo, DImg emissive, DImg normal, DImg depth,
-                                                        DImg ssao, DImg shadow, DImg clouds, CompParams p) {
+                                                        DImg ssao, DImg shadow, DImg clouds, CompParams p, DImg mip1) {
+    static_assert(!BL || HIST, "the in-kernel bloom runs in the fused-histogram kernel (no early exit before its barriers)");
     // a wave covers 16x8 pixels (8 lanes x 2 pixels per row, 8 rows): every row segment is one
     // 128-B line of each G-buffer image, and the wave's shadow-map taps form a compact 2D patch
     // (a 128x1 strip maps to a line across the 4096^2 map and touches a new line per tap)
@@ -240,23 +248,36 @@ __global__ __launch_bounds__(kWorkgroup) void composition_pair(DImg target, DImg
     // buffer descriptors + 32-bit offsets (one multiply-add per image row instead of 64-bit pointer math)
     const BufImg bd = buf_img(depth), ba = buf_img(albedo), be = buf_img(emissive), bn = buf_img(normal);
     const BufImg bt = buf_img(target), bs = buf_img(shadow), bo = buf_img(ssao);
+    const float v = centre_uv_rn(y, target.h, p.rh);
+    // once-read streams non-temporal (NT & 1: keep L2 for the shadow-map / AO gathers); aux bit 1 = nt
+    constexpr int ld_aux = (NT & 1) ? 2 : 0;
+    float2 d2 = float2{0.0f, 0.0f};
+    uint4 a4 = uint4{0u, 0u, 0u, 0u}, e4 = a4, n4 = a4;
+    // NT & 4: both pixels' AO taps (3 half-res texels per row) as one 8-B load per row, issued with the G-buffer
+    // loads (not after the depth test), for sky pixels too (in bounds, unused); the same bits as sample_r8
+    float aop[2] = {0.0f, 0.0f};
     if (inside) {
-        const float v = centre_uv_rn(y, target.h, p.rh);
-        // once-read streams non-temporal (NT & 1: keep L2 for the shadow-map / AO gathers); aux bit 1 = nt
-        constexpr int ld_aux = (NT & 1) ? 2 : 0;
-        const float2 d2 = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(bd.r, buf_row(bd, y) + x * 4, 0, ld_aux));
-        const uint4 a4 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ba.r, buf_row(ba, y) + x * 8, 0, ld_aux));
-        const uint4 e4 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(be.r, buf_row(be, y) + x * 8, 0, ld_aux));
-        const uint4 n4 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(bn.r, buf_row(bn, y) + x * 8, 0, ld_aux));
+        d2 = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(bd.r, buf_row(bd, y) + x * 4, 0, ld_aux));
+        a4 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ba.r, buf_row(ba, y) + x * 8, 0, ld_aux));
+        if (!BL) e4 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(be.r, buf_row(be, y) + x * 8, 0, ld_aux));
+        n4 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(bn.r, buf_row(bn, y) + x * 8, 0, ld_aux));
+        if (NT & 4) sample_r8_pair(bo, centre_uv_rn(x, target.w, p.rw), centre_uv_rn(x + 1, target.w, p.rw), v, aop[0], aop[1]);
+    }
+    if constexpr (BL) {   // every lane takes part in the tile's barriers; the pair's bloom as the chain stores it
+        __shared__ Up10Tile<32, 16> bl;
+        const int X0 = bx * 32, Y0 = by * 16;
+        bl.build(mip1, X0, Y0, target.w, target.h, threadIdx.x);
+        C3 o[2];
+        bl.out(y - Y0, x - X0, o);
+        const uint2 b0 = pack3(o[0]), b1 = pack3(o[1]);
+        e4 = uint4{b0.x, b0.y, b1.x, b1.y};
+    }
+    if (inside) {
         // LIGHTS: the light sum of the lane's two pixels runs once, as packed pairs (light_sum<f2v>, the same bits per
         // pixel as light_sum<float>); a sky pixel of the pair rides along in the other half and is discarded
         ShadePre pre[2];
         f3 alb[2], nrm[2], wps[2];
         uint32_t lit = 0u;
-        // NT & 4: both pixels' AO taps (3 half-res texels per row) as one 8-B load per row, issued with the G-buffer
-        // loads (not after the depth test), for sky pixels too (in bounds, unused); the same bits as sample_r8
-        float aop[2] = {0.0f, 0.0f};
-        if (NT & 4) sample_r8_pair(bo, centre_uv_rn(x, target.w, p.rw), centre_uv_rn(x + 1, target.w, p.rw), v, aop[0], aop[1]);
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
             const float u = centre_uv_rn(x + k, target.w, p.rw);
@@ -417,9 +438,12 @@ using namespace soc;
 namespace {
 // bins != nullptr: the fused histogram variant if the pair path applies at the globals' resolution
 // (returns 1 otherwise, having launched nothing)
+// bloom_mip1 != nullptr (the render graph under SOC_RENDERER_BLOOM_IN_COMPOSITION): the bloom output is computed in the
+// kernel from the chain's mip1 (composition_pair<..., BL>); needs the fused histogram and the pair path.
 int composition_launch(const soc_globals* g, const soc_globals* d_globals, soc_img target, soc_img albedo, soc_img emissive,
                        soc_img normal, soc_img depth, soc_img ssao, soc_img shadow, soc_img clouds, uint32_t* bins,
-                       uint32_t* scratch, soc_stream stream, bool fold = true, bool sky_external = false) {
+                       uint32_t* scratch, soc_stream stream, bool fold = true, bool sky_external = false,
+                       const soc_img* bloom_mip1 = nullptr) {
     static const char* P = "soc_composition";
     if (!g) return set_error(SOC_E_INVALID_ARG, "%s: null globals", P);
     int rc = check_img(target, SOC_FMT_RGBA16F, P, "target");
@@ -472,34 +496,48 @@ int composition_launch(const soc_globals* g, const soc_globals* d_globals, soc_i
                       aligned16(normal) && (reinterpret_cast<uintptr_t>(depth.data) & 7u) == 0 && (depth.pitch_bytes & 7) == 0;
     if (bins && !(fast && W == g->resolution[0] && H == g->resolution[1])) return 1;
     if (sky_external && !bins) return set_error(SOC_E_INVALID_ARG, "%s: sky_external needs the fused histogram", P);
+    if (bloom_mip1) {
+        rc = check_img(*bloom_mip1, SOC_FMT_RGBA16F, P, "bloom mip1");
+        if (rc) return rc;
+        if (!bins || !fast || bloom_mip1->width * 2 != W || bloom_mip1->height * 2 != H)
+            return set_error(SOC_E_SHAPE, "%s: the in-kernel bloom needs the fused histogram's pair path and mip1 = W/2 x H/2", P);
+    }
     if (fast) {
         dim3 grd(ceil_div(W, 32), ceil_div(H, 16));
         const bool lights = (p.npl | p.nsl) != 0;
 #define SOC_COMP_PAIR(HI, LI) launch("composition_pair", kWorkgroup, composition_pair<HI, LI>, grd, kWorkgroup, 0, hs(stream), dimg(target), dimg(albedo), \
-            dimg(emissive), dimg(normal), dimg(depth), dimg(ssao), dimg(shadow), dimg(clouds), p)
+            dimg(emissive), dimg(normal), dimg(depth), dimg(ssao), dimg(shadow), dimg(clouds), p, DImg{})
         if (bins) {
             p.bins = scratch;
             p.sky_external = sky_external ? 1 : 0;
             p.lmin = g->log_min_luminance;
             p.lrange = g->log_max_luminance - g->log_min_luminance;
             p.bf = bin_fast_params(p.lmin, p.lrange);
-            if (lights) SOC_COMP_PAIR(true, true);
+            if (bloom_mip1 && lights)
+                launch("composition_pair", kWorkgroup, composition_pair<true, true, 0, true>, grd, kWorkgroup, 0, hs(stream),
+                       dimg(target), dimg(albedo), dimg(emissive), dimg(normal), dimg(depth), dimg(ssao), dimg(shadow),
+                       dimg(clouds), p, dimg(*bloom_mip1));
+            else if (bloom_mip1)
+                launch("composition_pair", kWorkgroup, composition_pair<true, false, 7, true>, grd, kWorkgroup, 0, hs(stream),
+                       dimg(target), dimg(albedo), dimg(emissive), dimg(normal), dimg(depth), dimg(ssao), dimg(shadow),
+                       dimg(clouds), p, dimg(*bloom_mip1));
+            else if (lights) SOC_COMP_PAIR(true, true);
             else if (nt && aop)
                 launch("composition_pair", kWorkgroup, composition_pair<true, false, 7>, grd, kWorkgroup, 0, hs(stream), dimg(target), dimg(albedo), dimg(emissive),
-                    dimg(normal), dimg(depth), dimg(ssao), dimg(shadow), dimg(clouds), p);
+                    dimg(normal), dimg(depth), dimg(ssao), dimg(shadow), dimg(clouds), p, DImg{});
             else if (nt)
                 launch("composition_pair", kWorkgroup, composition_pair<true, false, 3>, grd, kWorkgroup, 0, hs(stream), dimg(target), dimg(albedo), dimg(emissive),
-                    dimg(normal), dimg(depth), dimg(ssao), dimg(shadow), dimg(clouds), p);
+                    dimg(normal), dimg(depth), dimg(ssao), dimg(shadow), dimg(clouds), p, DImg{});
             else SOC_COMP_PAIR(true, false);
             if (fold) launch("histogram_fold", kBins, histogram_fold, 1, kBins, 0, hs(stream), scratch, bins);
         } else if (nt && !lights && aop) {
             launch("composition_pair", kWorkgroup, composition_pair<false, false, 7>, grd, kWorkgroup, 0, hs(stream), dimg(target), dimg(albedo), dimg(emissive),
-                dimg(normal), dimg(depth), dimg(ssao), dimg(shadow), dimg(clouds), p);
+                dimg(normal), dimg(depth), dimg(ssao), dimg(shadow), dimg(clouds), p, DImg{});
         } else if (nt && !lights) {
             // non-temporal G-buffer loads and colour store (measured at 4K: 71.5 -> 68 us; TAA, the next
             // reader of depth, +3 us: the frame is unchanged). SOC_COMP_NT=0: default cache policy.
             launch("composition_pair", kWorkgroup, composition_pair<false, false, 3>, grd, kWorkgroup, 0, hs(stream), dimg(target), dimg(albedo), dimg(emissive),
-                dimg(normal), dimg(depth), dimg(ssao), dimg(shadow), dimg(clouds), p);
+                dimg(normal), dimg(depth), dimg(ssao), dimg(shadow), dimg(clouds), p, DImg{});
         } else {
             if (lights) SOC_COMP_PAIR(false, true);
             else SOC_COMP_PAIR(false, false);
@@ -559,12 +597,13 @@ extern "C" int soc_composition(const soc_globals* g, const soc_globals* d_global
 int soc::composition_luminance_histogram(const soc_globals* g, const soc_globals* d_globals, soc_img target,
                                          soc_img albedo, soc_img emissive, soc_img normal, soc_img depth, soc_img ssao,
                                          soc_img shadow, soc_img clouds, soc_auto_exposure* ae, uint32_t* scratch,
-                                         bool fold, soc_stream stream, bool sky_external) {
+                                         bool fold, soc_stream stream, bool sky_external, const soc_img* bloom_mip1) {
     if (!g || !ae || !scratch)
         return set_error(SOC_E_INVALID_ARG, "soc_composition_luminance_histogram: null globals / auto exposure / scratch");
     int rc = composition_launch(g, d_globals, target, albedo, emissive, normal, depth, ssao, shadow, clouds,
-                                ae->histogram_buckets, scratch, stream, fold, sky_external);
+                                ae->histogram_buckets, scratch, stream, fold, sky_external, bloom_mip1);
     if (rc <= 0) return rc;   // launched (or failed validation)
+    if (bloom_mip1) return set_error(SOC_E_SHAPE, "composition: the in-kernel bloom needs the pair path");
     if (sky_external) return set_error(SOC_E_INVALID_ARG, "composition: sky_external needs the pair path");
     // not fusable: the two passes back to back (same results)
     rc = composition_launch(g, d_globals, target, albedo, emissive, normal, depth, ssao, shadow, clouds, nullptr, nullptr,

@@ -90,7 +90,7 @@ int launch_bloom_weighted(const soc_img& emissive, const soc_img* mips, const so
 int composition_luminance_histogram(const soc_globals* g, const soc_globals* d_globals, soc_img target, soc_img albedo,
                                     soc_img emissive, soc_img normal, soc_img depth, soc_img ssao, soc_img shadow,
                                     soc_img clouds, soc_auto_exposure* ae, uint32_t* scratch, bool fold, soc_stream stream,
-                                    bool sky_external = false);
+                                    bool sky_external = false, const soc_img* bloom_mip1 = nullptr);
 // The fused pair path applies to these images at the globals' resolution (composition.hip).
 bool composition_pair_applicable(const soc_globals* g, const soc_img& target, const soc_img& albedo,
                                  const soc_img& emissive, const soc_img& normal, const soc_img& depth,

@@ -28,11 +28,12 @@ def test_bench_frame_4k_vs_oracle(soc, oracle, config, sky_range):
     W, H = (1920, 1080) if config == "c2" else (3840, 2160)
     dev = torch.device("cuda", 0)
     g, gb, shadow, noise, sc, fr = bench.build_inputs(config, "mesh", W, H, 0, dev)
-    # the bench's renderer flags: static inputs, and the velocity history by slot rotation (the resident velocity in
-    # both history slots, as bench.py sets it up; the oracle's frame is given the same history)
+    # the bench's renderer flags: static inputs, the velocity history by slot rotation (the resident velocity in both
+    # history slots, as bench.py sets it up; the oracle's frame is given the same history) and the bloom chain's last
+    # stage inside Composition
     for hv in fr["history_velocity"]:
         hv.copy_(fr["velocity"])
-    r = soc.Renderer(fr, static_inputs=True, velocity_slots=True)
+    r = soc.Renderer(fr, static_inputs=True, velocity_slots=True, bloom_in_composition=True)
     r.set_exposure_pixels(W * H, False)
     assert r.pass_names() == ["BloomDownsample - 0+1", "BloomDownsample - 2+3", "BloomUpsample - 3+2",
                               "BloomUpsample - 1+0", "SSAOGeneration", "SSAOBlur", "CloudRendering",
@@ -51,6 +52,10 @@ def test_bench_frame_4k_vs_oracle(soc, oracle, config, sky_range):
         r.execute(g)
         hf["emissive"][...] = gb["emissive"]          # the bench writes bloom into bloom_output (emissive kept)
         hist = oracle.frame(g, hf, ae, hist=hist)
+        # where Composition computed the bloom in-kernel (a frame with a high-priority sky lane), its output
+        # materialised from the GPU's mip1 by the chain's own last stage (the same bits:
+        # test_bloom_in_composition_bit_identical) for frame_parity's conditional checks; else the same values again
+        soc.bloom_weighted_stage(g, fr["emissive"], fr["bloom_mips"], fr["bloom_output"], stage=4)
         torch.cuda.synchronize()
         assert r.current_history() == hist
         frame_parity(soc, oracle, g, fr, hf, ae, hist, f"{config} {W}x{H} frame {f}", e0)

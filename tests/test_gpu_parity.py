@@ -1023,6 +1023,66 @@ def test_velocity_slots_bit_identical(soc):
     assert torch.equal(outs[1][-1]["velocity_history"], fields[-1])
 
 
+@pytest.mark.parametrize("inputs,lights", [("sponza", False), ("terrain", False), ("sponza", True)])
+def test_bloom_in_composition_bit_identical(soc, monkeypatch, inputs, lights):
+    """SOC_RENDERER_BLOOM_IN_COMPOSITION: the bloom chain's last stage (mip1 -> [mip0] -> output) computed per 32 x 16
+    tile inside the fused Composition + histogram launch instead of its own pass (bloomw_up10s, 64 x 16 tiles) writing
+    the full-resolution bloom output that Composition reads back; active in frames whose sky lane is the critical path
+    (here forced: a high-priority sky lane, SOC_RENDERER_SIDE_QUEUE=1). Three frames with per-frame
+    globals: the colour, framebuffer, exposure and resolved history have the same bits (the bloom values are functions
+    of their clamped coordinates only, rounded to RGBA16F as the chain stores them), with and without point lights (the
+    lights kernel); Composition declares BLOOM_MIP1, and the fourth bloom pass is skipped: the bloom output image is not
+    written."""
+    import ctypes as C
+
+    import bench
+    monkeypatch.setenv("SOC_RENDERER_SIDE_QUEUE", "1")
+    soc.reload_tuning()
+    W, H = 1920, 1080
+    g0, gb = (sponza_inputs if inputs == "sponza" else terrain_inputs)(W, H, elapsed=10.0)
+    # a dense emissive field on top of the scene's (the box atrium's lamps cover 0.7 % of the pixels, the terrain none)
+    gen = torch.Generator(device=DEV).manual_seed(3)
+    emis = torch.from_numpy(gb["emissive"]).to(DEV) + (torch.rand((H, W, 4), generator=gen, device=DEV) ** 4 * 3).half()
+    outs = []
+    for fused in (False, True):
+        fr = soc.alloc_frame(W, H, DEV, bloom_output=True)
+        for k in ("albedo", "normal", "velocity", "depth"):
+            fr[k].copy_(torch.from_numpy(gb[k]))
+        fr["emissive"].copy_(emis)
+        fr["shadow"] = dev(gb["shadow"])
+        fr["noise"].copy_(torch.from_numpy(gb["noise"]))
+        fr["bloom_output"].fill_(7.0)
+        r = soc.Renderer(fr, static_inputs=True, bloom_in_composition=fused)
+        names = r.pass_names()
+        assert "BloomUpsample - 1+0" in names, names
+        reads, _w = r.pass_uses(names.index("Composition+GenerateLuminanceHistogram"))
+        assert ("BLOOM_MIP1" in reads) == fused and "BLOOM_OUTPUT" in reads, reads
+        cam = soc.make_camera((-14.0, 2.2, 0.3), (0.0, -0.42, 0.0))
+        ji = C.c_uint32(0)
+        g = soc.globals_defaults(W, H)
+        seq = []
+        for f in range(3):
+            soc.frame_update(g, cam, W, H, 0.016, ji)
+            if lights:
+                soc.scene_update(g, bench.point_lights_c3b())
+            cam.position[0] += 0.05
+            r.execute(g)
+            seq.append({k: fr[k].clone() for k in ("color", "output")})
+            if f == 0:   # the lane takes its (forced) queue in the first call: in-kernel from the second frame on
+                assert r.side_queue() == 1
+                fr["bloom_output"].fill_(7.0)
+        torch.cuda.synchronize()
+        seq.append({"auto_exposure": fr["auto_exposure"].clone(), "resolved": r.resolved().clone()})
+        assert bool((fr["bloom_output"] == 7.0).all()) == fused
+        outs.append(seq)
+        r.close()
+    monkeypatch.delenv("SOC_RENDERER_SIDE_QUEUE")
+    soc.reload_tuning()
+    for a, b in zip(*outs):
+        for k in a:
+            assert torch.equal(a[k], b[k]), k
+
+
 @pytest.mark.parametrize("inputs", ["sponza", "terrain"])
 def test_sky_lane_queue_probe_bit_identical(soc, monkeypatch, inputs):
     """The sky lane's hardware queue (SOC_RENDERER_SIDE_QUEUE): auto (3, default) runs eight windows alternating between
