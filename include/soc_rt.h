@@ -411,7 +411,8 @@ typedef struct soc_renderer soc_renderer;
 /* The bloom chain's last stage (upsample 1 + 0: mip1 -> [mip0] -> bloom output, renderer.cpp:1044-1062) may be computed
  * inside the fused Composition + histogram launch, per 32 x 16 tile in LDS, from BLOOM_MIP1 (the same values per pixel,
  * rounded to RGBA16F as the chain stores them, so the same colour bits). The renderer does so in frames whose sky lane
- * is the critical path (soc_renderer_side_queue() == 1); the chain's fourth pass is then skipped and the
+ * is the critical path (a high-priority sky lane: soc_renderer_side_queue() == 1, and the lane probe's high-priority
+ * windows); the chain's fourth pass then records nothing and the
  * full-resolution bloom output (images.bloom_output, or the emissive image in place) is NOT written. Composition
  * declares BLOOM_MIP1 besides the bloom output. Applies with the weighted chain and the fused histogram's pair path. A
  * caller that reads the bloom output leaves the flag off. */
@@ -455,7 +456,7 @@ int soc_renderer_set_async(soc_renderer* r, int32_t enable);
 /* The sky lane's hardware queue: 1 = a high-priority stream, 2 = low priority, 0 = normal priority (a queue HIP may
  * share with the caller's stream), -1 = not chosen yet (tuning knob SOC_RENDERER_SIDE_QUEUE=3, the default: after 16
  * frames, eight windows of 32-128 frames alternate high / low priority as ABBA pairs; high is kept if it is faster by
- * more than 1.5 % once their timing events have completed, else low) or no sky lane created. Same results either way. */
+ * more than 2 % once their timing events have completed, else low) or no sky lane created. Same results either way. */
 int32_t soc_renderer_side_queue(const soc_renderer* r);
 /* Frames the auto probe spans from the renderer's first call (the choice is made at the first call after they have
  * completed on the GPU); 0 when no probe runs. A caller that times frames runs at least this many first. */

@@ -677,7 +677,6 @@ struct soc_renderer {
     // sky split configured (graph) / active this frame (the pair path applies at the globals' resolution)
     bool sky_split = false, sky_split_active = false;
     bool bloom_in_comp = false;          // SOC_RENDERER_BLOOM_IN_COMPOSITION applies to this graph
-    bool bloom_in_comp_active = false;   // ... and this frame computes the bloom's last stage inside Composition
     // the caller's stream is ordered after all second-lane work of the previous call (its join or an equivalent wait)
     bool main_after_side = true;
     // SOC_RENDERER_STATIC_INPUTS: a call of this graph has completed, so the frame inputs the caller wrote before its
@@ -708,6 +707,16 @@ uint64_t widen_velocity(const soc_renderer* r, uint64_t m) {
 soc_img frame_velocity(const soc_renderer* r) {
     return (r->flags & SOC_RENDERER_VELOCITY_SLOTS) ? r->img.history_velocity[1 - r->hist] : r->img.velocity;
 }
+
+// The sky lane runs at high priority in this frame: chosen by the lane probe (or the knob), or one of the probe's
+// high-priority windows. Evaluated inside the pass callbacks, after this call's frame_lane_probe.
+bool sky_lane_high(const soc_renderer* r) {
+    return r->side_queue == 1 || (r->side_queue == -1 && r->lane_q[0] && r->side == r->lane_q[0]);
+}
+// SOC_RENDERER_BLOOM_IN_COMPOSITION in this frame: the bloom's last stage inside Composition where the sky lane is the
+// critical path (high priority, as the lane probe's high windows too, so the probe times what would run), the fourth
+// bloom pass then recording nothing. Both callbacks of a frame see the same lane (set before the passes are issued).
+bool bloom_in_comp_active(const soc_renderer* r) { return r->bloom_in_comp && sky_lane_high(r); }
 
 soc_renderer::Pass& add_pass(soc_renderer* r, std::string name, std::string group, int phase, uint64_t reads,
                              uint64_t writes, PassFn fn, uint32_t flags = 0) {
@@ -789,8 +798,8 @@ void build_passes(soc_renderer* r) {
         const uint64_t wr[4] = {res_mask({mip[1]}), res_mask({mip[3]}), res_mask({mip[1]}), res_mask({dst_res})};
         // SOC_RENDERER_BLOOM_IN_COMPOSITION: where the fused composition + histogram's pair path applies, the last stage
         // (mip1 -> [mip0] -> output) may run inside that launch (composition_pair<..., BL>) in a frame whose sky lane is
-        // the critical path (the lane probe chose high priority): the fourth pass is then skipped and the bloom output
-        // not written. Beside a low-priority sky lane the fused kernel's 19 KiB of LDS per workgroup do not fit next to
+        // the critical path (high priority, bloom_in_comp_active): the fourth pass then records nothing and the bloom
+        // output is not written. Beside a low-priority sky lane the fused kernel's 19 KiB of LDS per workgroup do not fit next to
         // the sun-visibility march's noise tables (C3: Composition 76 -> 122 us in the frame, -0.6 % fps; C4 +2.9 %,
         // profiles/r05_ab_bloom_in_composition.txt), so those frames keep the separate pass.
         soc_globals gres{};
@@ -798,13 +807,12 @@ void build_passes(soc_renderer* r) {
         gres.resolution[1] = I.color.height;
         r->bloom_in_comp = (r->flags & SOC_RENDERER_BLOOM_IN_COMPOSITION) && !(r->flags & SOC_RENDERER_UNFUSED_HISTOGRAM) &&
                            soc::composition_pair_applicable(&gres, I.color, I.albedo, bloom_dst, I.normal, I.depth, I.clouds);
-        for (int st = 1; st <= 4; ++st) {
-            auto& bp = add_pass(r, names[st - 1], "Bloom", pre, rd[st - 1], wr[st - 1], [r, st](const soc_globals* g, hipStream_t s) {
+        for (int st = 1; st <= 4; ++st)
+            add_pass(r, names[st - 1], "Bloom", pre, rd[st - 1], wr[st - 1], [r, st](const soc_globals* g, hipStream_t s) {
+                if (st == 4 && bloom_in_comp_active(r)) return (int)SOC_OK;   // Composition computes it this frame
                 const soc_img& dst = r->img.bloom_output.data ? r->img.bloom_output : r->img.emissive;
                 return soc_bloom_weighted_stage(g, r->img.emissive, r->img.bloom_mips, 4, dst, st, (soc_stream)s);
             });
-            if (st == 4 && r->bloom_in_comp) bp.skip = [r] { return r->bloom_in_comp_active; };
-        }
         return;
     }
     // renderer.cpp:1024-1042: the bit-exact per-pass chain (SOC_RENDERER_EXACT_BLOOM / _UNFUSED_BLOOM, or mips that do
@@ -864,8 +872,7 @@ void build_passes_tail(soc_renderer* r) {
                  // classification (C4 +1.8 %, C3 -1.1 %); else the knobs
                  // (also during the lane probe's high-priority windows, so the probe compares the two alternatives
                  // as they run: high with these variants against low without)
-                 const bool high = r->side_queue == 1 || (r->side_queue == -1 && r->lane_q[0] && r->side == r->lane_q[0]);
-                 const bool sky_bound = high && tuning_knob("SOC_RENDERER_SKY_BOUND_VARIANTS", 1);
+                 const bool sky_bound = sky_lane_high(r) && tuning_knob("SOC_RENDERER_SKY_BOUND_VARIANTS", 1);
                  return soc::cloud_rendering_launch(g, r->img.depth, r->img.noise, r->img.clouds, r->img.clouds_workspace,
                                                     (soc_stream)s, sky_bound);
              }, SOC_PASS_ASYNC);
@@ -889,7 +896,7 @@ void build_passes_tail(soc_renderer* r) {
                                                                  I.ssao_blur, I.shadow, I.clouds, I.auto_exposure,
                                                                  r->hist_scratch, false, (soc_stream)s,
                                                                  r->sky_split_active,
-                                                                 r->bloom_in_comp_active ? &I.bloom_mips[1] : nullptr);
+                                                                 bloom_in_comp_active(r) ? &I.bloom_mips[1] : nullptr);
                  });
         // the 8 partial histograms of the fused launch into the AutoExposure bins. Before a multi-GPU exchange
         // (PRE and POST in separate calls) the fold must precede it; in a one-call frame the resolve folds them
@@ -1261,8 +1268,9 @@ static int switch_side_lane(soc_renderer* r, hipStream_t q) {
 // windows (32 frames at 4K, up to 128 for smaller frames: probe_window) run the sky lane at high, low, low, high, high,
 // low, low, high priority; timing events on the caller's stream at each window's frame 8 and its end give its mean
 // frame interval (the first 8 after a switch skipped). The ABBA order cancels a linear drift of the clocks over the probe (a plain high-then-low order read
-// the warm-up as a slower high lane). High is kept only if its windows are faster by more than 1.5 % (C3 and C2
-// prefer low by 1-5 %, C4 high by 3-10 %; short C2 frames measured within the noise, profiles/r05_ab_lane_probe.txt),
+// the warm-up as a slower high lane). High is kept only if its windows are faster by more than 2 % (C3 prefers low by
+// ~1 %, C4 and C2 high by 3-10 % with the in-Composition bloom of high windows; at 1.5 % C3 took high in 2 of 6 runs,
+// profiles/r05_ab_lane_probe.txt),
 // once the last event has completed (queried, never waited on), for the renderer's life.
 // Frames per probe window: 32 at 3840x2160 and above, more for smaller frames (their intervals are shorter, so a
 // 32-frame window is within the timing noise), up to 128.
@@ -1310,7 +1318,7 @@ static int frame_lane_probe(soc_renderer* r, hipStream_t s) {
         }
         (kHigh[w] ? hi : lo) += t;
     }
-    r->side_queue = (hi < 0.985f * lo) ? 1 : 2;
+    r->side_queue = (hi < 0.98f * lo) ? 1 : 2;
     return switch_side_lane(r, r->lane_q[r->side_queue - 1]);
 }
 
@@ -1340,9 +1348,6 @@ extern "C" int soc_renderer_execute(soc_renderer* r, const soc_globals* g, int32
     hipStream_t s = hs(stream);
     r->fold_in_resolve = (phase & SOC_PHASE_ALL) == SOC_PHASE_ALL && !(r->flags & SOC_RENDERER_UNFUSED_HISTOGRAM);
     if (phase & SOC_PHASE_PRE_EXPOSURE) {
-        // the bloom's last stage inside Composition in a frame whose sky lane is the critical path (see build_passes)
-        // (the lane's choice, kept while set_async(0) serialises a frame, so a serial profiling frame runs the same kernels)
-        r->bloom_in_comp_active = r->bloom_in_comp && r->side_queue == 1;
         const soc_img& em = r->img.bloom_output.data ? r->img.bloom_output : r->img.emissive;
         r->sky_split_active = r->sky_split && soc::composition_pair_applicable(g, r->img.color, r->img.albedo, em,
                                                                                r->img.normal, r->img.depth, r->img.clouds);
