@@ -1176,13 +1176,14 @@ static int upload_lights(soc_renderer* r, const soc_globals* g, hipStream_t s) {
     return SOC_OK;
 }
 
-// Flags of the renderer's GPU-side events: the per-pass timing and lane-probe events and the cross-lane pass events
-// order / time work on this device only, so they skip the system-scope fence (hipEventDisableSystemFence: the L2
-// writeback + invalidate a default event record implies on AMD GPUs, and the cold caches it leaves the next kernel):
-// C3 +0.5 %, C4 +0.6 %, C2 +3.7 % (profiles/r05_ab_event_fence.txt); SOC_RENDERER_EVENT_FENCE=0 restores the default.
-// The fork / join events that order the renderer against the caller's stream keep the default.
-static unsigned device_event_flags(bool timing) {
-    return (timing ? 0u : (unsigned)hipEventDisableTiming) |
+// Flags of the renderer's cross-lane synchronisation events (a pass's `done`, the lane switch): they order work on
+// this device only, so they skip the system-scope fence (hipEventDisableSystemFence: the L2 writeback + invalidate a
+// default event record implies on AMD GPUs, and the cold caches it leaves the next kernel; SOC_RENDERER_EVENT_FENCE=0
+// restores the default). Timing events keep the default: without the fence a start event's timestamp may be taken after
+// the next kernel has begun (6.5 us into SSAO, tools/event_trace_check.py), so the pass events would no longer bracket
+// their kernels. The fork / join events that order the renderer against the caller's stream keep the default too.
+static unsigned device_event_flags() {
+    return (unsigned)hipEventDisableTiming |
            (tuning_knob("SOC_RENDERER_EVENT_FENCE", 1) == 1 ? (unsigned)hipEventDisableSystemFence : 0u);
 }
 
@@ -1241,9 +1242,9 @@ static int ensure_side_lane(soc_renderer* r) {
     if (sq == 3) {
         se = hipStreamCreateWithPriority(&r->lane_q[0], hipStreamNonBlocking, greatest);
         if (se == hipSuccess) se = hipStreamCreateWithPriority(&r->lane_q[1], hipStreamNonBlocking, least);
-        if (se == hipSuccess) se = hipEventCreateWithFlags(&r->switch_ev, device_event_flags(false));
+        if (se == hipSuccess) se = hipEventCreateWithFlags(&r->switch_ev, device_event_flags());
         for (auto& e : r->probe_ev)
-            if (se == hipSuccess) se = hipEventCreateWithFlags(&e, device_event_flags(true));
+            if (se == hipSuccess) se = hipEventCreate(&e);
         r->side = r->lane_q[0];
         r->side_queue = -1;
         r->probe_frames = 0;
@@ -1491,7 +1492,7 @@ extern "C" int soc_renderer_execute(soc_renderer* r, const soc_globals* g, int32
         if (rc) return abort_frame(r, s, lanes, rc);
         pos[i] = next_pos[L]++;
         if (p.signal) {
-            if (!p.done && hipEventCreateWithFlags(&p.done, device_event_flags(false)) != hipSuccess)
+            if (!p.done && hipEventCreateWithFlags(&p.done, device_event_flags()) != hipSuccess)
                 return abort_frame(r, s, lanes, set_error(SOC_E_HIP, "soc_renderer_execute: hipEventCreate failed"));
             if (hipEventRecord(p.done, ls) != hipSuccess)
                 return abort_frame(r, s, lanes, set_error(SOC_E_HIP, "soc_renderer_execute: %s: event record failed", p.name.c_str()));
@@ -1696,8 +1697,7 @@ extern "C" int soc_renderer_set_pass_timing(soc_renderer* r, int32_t index, int3
             p.ev0.assign(SOC_RENDERER_TIMING_RING, nullptr);
             p.ev1.assign(SOC_RENDERER_TIMING_RING, nullptr);
             for (int k = 0; k < SOC_RENDERER_TIMING_RING; ++k)
-                if (hipEventCreateWithFlags(&p.ev0[k], device_event_flags(true)) != hipSuccess ||
-                    hipEventCreateWithFlags(&p.ev1[k], device_event_flags(true)) != hipSuccess)
+                if (hipEventCreate(&p.ev0[k]) != hipSuccess || hipEventCreate(&p.ev1[k]) != hipSuccess)
                     return set_error(SOC_E_HIP, "soc_renderer_set_pass_timing: hipEventCreate failed");
         }
         p.timed = enable != 0;
