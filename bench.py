@@ -375,7 +375,9 @@ def main():
     stats_timed = {n: ms for n, _, ms, cnt in r.pass_stats() if cnt}
     events_out = os.environ.get("SOC_BENCH_EVENTS_OUT")   # every timed frame's pass events, for tools/event_trace_check.py
     if events_out and rank == 0 and not probe_no_events:
-        dump = {"frames": args.steps, "warmup": args.warmup, "passes": {}}
+        # "warmup": the frames before the timed ones (warm-up + the lane probe's untimed frames), i.e. the launches of
+        # each kernel that tools/event_trace_check.py skips in the trace
+        dump = {"frames": args.steps, "warmup": args.warmup + probe_frames, "passes": {}}
         for i in timed:
             s0, s1 = r.pass_event_times(i, base_ev, args.steps)
             dump["passes"][names[i]] = {"start_ms": s0.tolist(), "end_ms": s1.tolist()}

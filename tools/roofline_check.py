@@ -1,7 +1,8 @@
 """Agreement of the bench line's roofline durations with rocprofv3. The bench measures the north-star kernels with HIP
 events on their stream twice: alone (the serial per-pass profile frames: the roofline's headline) and in its timed
 frames (lanes concurrent: `in_frame`). This takes a `tools/gpu.sh kt` kernel trace of the same command (`bench.py
---steps K --warmup W`: W warm-up frames, K timed frames, then the serial per-pass profile frames) and averages each
+--steps K --warmup W`: W warm-up frames, the untimed lane-probe frames, K timed frames, then the serial per-pass profile
+frames) and averages each
 kernel over the same kind of launch: the profile frames for the headline, the timed frames for in_frame. The kernel
 trace's own `--stats` average mixes the three segments. A kernel trace changes how the two lanes overlap, so the
 in-frame pair of an untraced bench run and a traced run need not agree; within one traced run events and trace do
@@ -34,9 +35,13 @@ def main():
     line = json.load(open(bench_json))
     warmup = line["warmup"] if warmup is None else warmup
     steps = line["steps"] if steps is None else steps
+    # the untimed frames the bench runs after the warm-up until the renderer's lane probe has decided
+    probe = int(line.get("config", {}).get("untimed_lane_probe_frames") or 0)
+    warmup += probe
     trace = glob.glob(os.path.join(kt_dir, "**", "*kernel_trace.csv"), recursive=True)[0]
     rows = sorted(csv.DictReader(open(trace)), key=lambda r: int(r["Start_Timestamp"]))
-    out = {"bench_line": bench_json, "kernel_trace": trace, "warmup": warmup, "timed": steps, "kernels": {}}
+    out = {"bench_line": bench_json, "kernel_trace": trace, "warmup": warmup, "untimed_lane_probe_frames": probe,
+           "timed": steps, "kernels": {}}
     pair_events = pair_rocprof = 0.0
     for name, key in KERNELS.items():
         d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows if key in r["Kernel_Name"]]
