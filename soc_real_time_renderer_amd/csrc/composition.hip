@@ -69,6 +69,10 @@ __device__ __forceinline__ f2v vneg_pi(f2v x, f2v r) {
     const f2v q = f2v{3.14159265358979f, 3.14159265358979f} - r;
     return f2v{x.x < 0.0f ? q.x : r.x, x.y < 0.0f ? q.y : r.y};
 }
+__device__ __forceinline__ float vnan_outside1(float x, float r) { return fabsf(x) > 1.0f ? __builtin_nanf("") : r; }
+__device__ __forceinline__ f2v vnan_outside1(f2v x, f2v r) {
+    return f2v{fabsf(x.x) > 1.0f ? __builtin_nanf("") : r.x, fabsf(x.y) > 1.0f ? __builtin_nanf("") : r.y};
+}
 __device__ __forceinline__ float vdiv(float a, float b) { return a / b; }
 __device__ __forceinline__ f2v vdiv(f2v a, float b) { return f2v{a.x / b, a.y / b}; }
 template <class T> __device__ __forceinline__ T vdot(const V3<T>& a, const V3<T>& b) {
@@ -92,9 +96,28 @@ __device__ __forceinline__ T acos_fast(T x) {
     return vneg_pi(x, r);
 }
 
+// exp(-acos(c)^2), the specular term of composition.inl:135-138, as one degree-10 polynomial in c (least squares on
+// [-1, 1], fp32 Horner): |error| <= 1.1e-6 for c >= -0.9 and <= 2.6e-5 at c = -1, where the term itself is 5e-5 (acos is
+// not analytic there; exp(-acos^2) is tiny). Ten FMAs instead of acos_fast's polynomial, square root and select plus
+// the exponential: two transcendentals less per light and pixel. NaN outside [-1, 1], as acos (and acos_fast) give.
+// SOC_COMP_SPEC_POLY=0 (build-time) keeps acos_fast + exp2.
+#ifndef SOC_COMP_SPEC_POLY
+#define SOC_COMP_SPEC_POLY 1
+#endif
+template <class T>
+__device__ __forceinline__ T spec_exp_acos2(T c) {
+    constexpr float k[11] = {0.08480516821146011f,  0.26642516255378723f,  0.33367738127708435f,   0.21618370711803436f,
+                             0.07947526127099991f,  0.017337322235107422f, 0.0017174964305013418f, -0.00019129738211631775f,
+                             0.0007113117026165128f, 0.00020575939561240375f, -0.00034820116707123816f};
+    T r = bcv(k[10], c);
+#pragma unroll
+    for (int i = 9; i >= 0; --i) r = vfma(r, c, bcv(k[i], c));
+    return vnan_outside1(c, r);
+}
+
 // The light loops of composition.inl:124-160, per light: L = light - pos, one rsqrt gives light_dir and the
-// attenuation 1 / distance^2; dot(normalize(light_dir + view_dir), n) with one more rsqrt; acos on the native
-// units (acos_fast) and exp(-x^2) as a native exp2. The pixel's view_dir is hoisted out of the loop and the
+// attenuation 1 / distance^2; dot(normalize(light_dir + view_dir), n) with one more rsqrt; the specular
+// exp(-acos(x)^2) as one polynomial (spec_exp_acos2). The pixel's view_dir is hoisted out of the loop and the
 // frag_color (albedo) factor out of the sum. Within the RGBA16F tolerance of the oracle's libm restatement.
 // Light records are wave-uniform (scalar loads from the device globals).
 template <class T>
@@ -111,8 +134,10 @@ __device__ __forceinline__ V3<T> light_sum(const soc_globals* __restrict__ dg, u
         inv = vrsq(vdot(l, l));
         ld = V3<T>{l.x * inv, l.y * inv, l.z * inv};
         const V3<T> h = {ld.x + view_dir.x, ld.y + view_dir.y, ld.z + view_dir.z};
-        const T nh = acos_fast(vdot(h, n) * vrsq(vdot(h, h)));
+        const T c = vdot(h, n) * vrsq(vdot(h, h));
         const T diffuse = vmax0(vdot(n, ld));
+        if (SOC_COMP_SPEC_POLY) return (diffuse + spec_exp_acos2(c)) * (inv * inv);
+        const T nh = acos_fast(c);
         return (diffuse + vexp2((nh * nh) * nlog2e)) * (inv * inv);
     };
     auto add = [&](const float* col, T s) {
