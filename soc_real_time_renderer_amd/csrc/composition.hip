@@ -143,7 +143,12 @@ __device__ __forceinline__ V3<T> light_sum(const soc_globals* __restrict__ dg, u
     auto add = [&](const float* col, T s) {
         acc = V3<T>{vfma(bcv(col[0], z), s, acc.x), vfma(bcv(col[1], z), s, acc.y), vfma(bcv(col[2], z), s, acc.z)};
     };
-#pragma unroll 4
+// 2 lights per round (4: 108 VGPRs, 4 waves per SIMD); with the fused-histogram lights kernel held to 6 waves per SIMD
+// (70 VGPRs, no spill): C3b 782 -> 799 fps (profiles/r05_ab_light_loop.txt)
+#ifndef SOC_COMP_LIGHT_UNROLL
+#define SOC_COMP_LIGHT_UNROLL 2
+#endif
+#pragma unroll SOC_COMP_LIGHT_UNROLL
     for (uint32_t i = 0; i < npl; ++i) {            // calculate_point_light, :124-139
         const soc_point_light& L = dg->point_lights[i];
         T inv;
@@ -250,8 +255,11 @@ constexpr int BX = 64, BY = 4;
 // is computed for the workgroup's 32 x 16 tile in LDS (Up10Tile, bloom_w.hpp: the same values per pixel, rounded to
 // RGBA16F as the chain stores its output) while the G-buffer loads are in flight, and used as the emissive input, so
 // the full-resolution bloom output is neither written by the chain nor read back here (16 B/px). `emissive` unused.
+#ifndef SOC_COMP_LIGHT_WAVES
+#define SOC_COMP_LIGHT_WAVES 6
+#endif
 template <bool HIST, bool LIGHTS, int NT = 0, bool BL = false>
-__global__ __launch_bounds__(kWorkgroup) void composition_pair(DImg target, DImg albedo, DImg emissive, DImg normal, DImg depth,
+__global__ __launch_bounds__(kWorkgroup) __attribute__((amdgpu_waves_per_eu(LIGHTS && !BL ? SOC_COMP_LIGHT_WAVES : 1))) void composition_pair(DImg target, DImg albedo, DImg emissive, DImg normal, DImg depth,
                                                         DImg ssao, DImg shadow, DImg clouds, CompParams p, DImg mip1) {
     static_assert(!BL || HIST, "the in-kernel bloom runs in the fused-histogram kernel (no early exit before its barriers)");
     // a wave covers 16x8 pixels (8 lanes x 2 pixels per row, 8 rows): every row segment is one
