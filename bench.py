@@ -119,9 +119,11 @@ def pmc_traffic(kernel, W, H, scene_name="mesh"):
         t = json.load(fh)
     ks = t.get("kernels", {})
     k = ks.get(kernel)
-    if k is None:   # a table from before a template-signature change: the one instantiation of that kernel
-        base = [v for n, v in ks.items() if n.split("<")[0] == kernel.split("<")[0]]
-        k = base[0] if len(base) == 1 else None
+    if k is None:   # a table from another template signature: the one instantiation of that kernel, or the one whose
+        # arguments start with the given ones (a table with fewer template arguments than the name asked for, or more)
+        base = [(n, v) for n, v in ks.items() if n.split("<")[0] == kernel.split("<")[0]]
+        pre = [(n, v) for n, v in base if n.rstrip(">").startswith(kernel.rstrip(">")) or kernel.rstrip(">").startswith(n.rstrip(">"))]
+        k = base[0][1] if len(base) == 1 else (pre[0][1] if len(pre) == 1 else None)
     if not k or list(t.get("resolution", [])) != [W, H] or t.get("scene", "boxes") != scene_name:
         return None, None
     return k["hbm_bytes"], os.path.relpath(files[-1], ROOT)
@@ -433,7 +435,9 @@ def main():
     pass_gbs = {n: round(algo[n] / (ms * 1e-3) / 1e9, 1) for n, _, ms, _ in stats if ms > 0 and n in algo}
     # the committed PMC table comes from the default command (C3, G-buffer resident): other workloads get null
     pmc_ok = args.config == "c3" and not args.raster
-    comp_kernel = "composition_pair<true, false, 7>" if comp != "Composition" else "composition_pair<false, false, 7>"
+    # the Composition kernel the timed frames ran (its fourth template argument: the in-kernel bloom of a sky-bound frame)
+    comp_kernel = (f"composition_pair<true, false, 7, {'true' if bloom_in_comp else 'false'}>" if comp != "Composition"
+                   else "composition_pair<false, false, 7, false>")
     traffic, traffic_src = pmc_traffic(comp_kernel, W, H, args.scene) if pmc_ok else (None, None)
     ssao_traffic, _ = pmc_traffic(SSAO_KERNEL, W, H, args.scene) if pmc_ok else (None, None)
     pair_traffic = traffic + ssao_traffic if traffic is not None and ssao_traffic is not None else None

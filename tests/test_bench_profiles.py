@@ -10,15 +10,18 @@ sys.path.insert(0, ROOT)
 
 def test_pmc_traffic_of_the_headline_kernels():
     import bench
-    comp, src = bench.pmc_traffic("composition_pair<true, false, 3>", 3840, 2160, "mesh")
+    comp, src = bench.pmc_traffic("composition_pair<true, false, 7, false>", 3840, 2160, "mesh")
     ssao, _ = bench.pmc_traffic(bench.SSAO_KERNEL, 3840, 2160, "mesh")
     assert src and os.path.exists(os.path.join(ROOT, src))
     algo = bench.algorithmic_bytes(3840, 2160, 0.0)
     # measured HBM bytes per launch: at least the algorithmic minimum's order, no more than a few times it
     assert 0.9 * algo["SSAOGeneration"] < ssao < 3.5 * algo["SSAOGeneration"]
     assert comp > 0.9 * 40.25 * 3840 * 2160
-    # a template-signature change still finds the one instantiation of that kernel
+    # a template-signature change still finds the one instantiation of that kernel, or the one whose arguments extend
+    # (or are extended by) the name asked for; an ambiguous name finds none
     assert bench.pmc_traffic("ssao_lds_kernel<true, true, true, 7>", 3840, 2160, "mesh")[0] == ssao
+    assert bench.pmc_traffic("composition_pair<true, false, 7, false, 1>", 3840, 2160, "mesh")[0] == comp
+    assert bench.pmc_traffic("composition_pair<true>", 3840, 2160, "mesh")[0] is None
     # another workload's table is not used
     assert bench.pmc_traffic(bench.SSAO_KERNEL, 1920, 1080, "mesh") == (None, None)
 
