@@ -1,7 +1,7 @@
 """Time one pass alone on the GPU for A/B library builds (soc_real_time_renderer_amd/csrc `make variant`), on the bench's
 own inputs, and hash its output so exact variants can be checked for identical bits.
 
-    python tools/pass_probe.py --pass clouds|ssao|gbuffer|taa|raster --configs c3,c4 --variants libsoc_rt.so,libsoc_rt_x.so [--reps 100] [--rounds 3]
+    python tools/pass_probe.py --pass clouds|ssao|gbuffer|taa|raster|bloom1 --configs c3,c4 --variants libsoc_rt.so,libsoc_rt_x.so [--reps 100] [--rounds 3]
 
 A variant is a library file name (SOC_RT_LIB_VARIANT) or NAME=VALUE[+NAME=VALUE...] (tuning knobs on the default library). Each
 variant runs in its own process; the rounds interleave the variants so clock drift hits
@@ -77,6 +77,12 @@ def child(pass_name, configs, reps):
             vout = hv[1] if os.environ.get("SOC_PROBE_TAA_VOUT", "1") != "0" else None
             run = lambda: soc.temporal_antialiasing_tone_mapping(g, hc[1], fr["color"], hc[0], fr["velocity"],  # noqa: E731
                                                                  hv[0], fr["depth"], ae, fr["output"], vout)
+        elif pass_name == "bloom1":   # the weighted bloom chain's first stage (emissive -> [mip0] -> mip1, bloomw_down01p)
+            tgt = fr["bloom_mips"][1]
+            out_img = fr.get("bloom_output")
+            if out_img is None:
+                out_img = torch.zeros(H, W, 4, dtype=torch.float16, device=dev)
+            run = lambda: soc.bloom_weighted_stage(g, fr["emissive"], fr["bloom_mips"], out_img, stage=1)  # noqa: E731
         else:
             raise SystemExit(f"unknown pass {pass_name}")
         for _ in range(10):
