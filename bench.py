@@ -209,6 +209,55 @@ def cpu_baseline(W, H, host_inputs, g):
             "ms_per_pass_median": {k: round(float(np.median(v)) * 1e3, 2) for k, v in times.items()}}
 
 
+REFERENCE_GROUPS = ("Depth Prepass", "Composition", "Tone Mapping", "Bloom", "Depth Of Field", "Shadows",
+                    "Rendering G-Buffer", "Screen Space Reflections", "Ambient Occlusion", "Auto Exposure",
+                    "Sky Rendering", "Temporal Anti-Aliasing")   # renderer.cpp:576-587
+# fused launches -> (the unfused passes whose time ratio splits them, their groups)
+FUSED_SPLIT = {"Composition+GenerateLuminanceHistogram": (("Composition", "GenerateLuminanceHistogram"),
+                                                          ("Composition", "Auto Exposure")),
+               "TemporalAntiAliasing+ToneMapping": (("TemporalAntiAliasing", "ToneMapping"),
+                                                    ("Temporal Anti-Aliasing", "Tone Mapping"))}
+
+
+def unfused_group_ms(fr, renderer_kw, g, frames):
+    """The serial per-pass loop of a renderer with the reference's pass structure (composition, histogram, TAA and tone
+    map as separate launches; bloom in its own passes) on the same frame images: ms per pass name and per reference
+    group. After the timed region; it renders into the same images (their contents are not used afterwards)."""
+    kw = dict(renderer_kw, fused_histogram=False, bloom_in_composition=False, sky_lane=False)
+    ru = soc.Renderer(fr, fused_tonemap=False, **kw)
+    ru.set_pass_timing(-1, True)
+    for _ in range(2):
+        ru.execute(g)
+    torch.cuda.synchronize()
+    ru.reset_timing()
+    for _ in range(max(1, frames)):
+        ru.execute(g)
+    torch.cuda.synchronize()
+    st = [x for x in ru.pass_stats() if x[3]]
+    ru.close()
+    groups = {k: 0.0 for k in REFERENCE_GROUPS}
+    for n, gname, ms, _ in st:
+        groups[gname] = groups.get(gname, 0.0) + ms
+    return {"passes": {n: round(ms, 4) for n, _, ms, _ in st}, "groups": {k: round(v, 4) for k, v in groups.items()}}
+
+
+def reference_groups(stats, no_launch, unfused):
+    """ms per reference group from the serial loop's passes; fused launches split by the unfused passes' time ratio."""
+    out = {k: 0.0 for k in REFERENCE_GROUPS}
+    for n, gname, ms, _ in stats:
+        if n in no_launch:
+            continue
+        if n in FUSED_SPLIT and unfused:
+            (pa, pb), (ga, gb_) = FUSED_SPLIT[n]
+            ta, tb = unfused["passes"].get(pa), unfused["passes"].get(pb)
+            if ta and tb:
+                out[ga] = out.get(ga, 0.0) + ms * ta / (ta + tb)
+                out[gb_] = out.get(gb_, 0.0) + ms * tb / (ta + tb)
+                continue
+        out[gname] = out.get(gname, 0.0) + ms
+    return {k: round(v, 4) for k, v in out.items()}
+
+
 def build_inputs(config, scene_name, W, H, rank, device, mips=True, output_format=None):
     """The frame inputs of a bench configuration (shared with the 4K C3 parity test): globals of rank `rank`'s camera,
     the G-buffer + 4096^2 sun shadow map (the Sponza-proxy mesh rasterised once by the HIP rasteriser, or the
@@ -281,6 +330,10 @@ def main():
     ap.add_argument("--exchange", action="store_true",
                     help="take the multi-GPU frame path at any N: PRE -> histogram all-reduce (RCCL, a world-size-1 "
                          "group at N = 1) -> POST, with the all-reduce timed (SURVEY.md §8e)")
+    ap.add_argument("--sky-lane-queue", choices=("auto", "low", "high", "probe"), default="auto",
+                    help="the sky lane's hardware queue (SOC_RENDERER_SKY_LANE_HIGH / _PROBE): auto = the configuration's "
+                         "fixed choice (low for c3 / c3b, whose main lane is the critical path; high for the sky-bound "
+                         "c2 / c4 frames), so a command runs the same kernels every time; probe = round 5's timed choice")
     ap.add_argument("--raster", action="store_true",
                     help="end-to-end frame: rasterise the scene mesh into the G-buffer and the 4096^2 sun shadow "
                          "map every frame (DepthPrepass / SunShadowDraw / GBufferGeneration in the graph)")
@@ -312,9 +365,11 @@ def main():
     if vslots:
         for hv in fr["history_velocity"]:
             hv.copy_(fr["velocity"])
-    r = soc.Renderer(fr, sky_lane=not args.no_sky_lane, fused_histogram=not args.unfused_histogram,
-                     static_inputs=not args.no_static_inputs, velocity_slots=vslots,
-                     bloom_in_composition=not args.no_bloom_in_composition)
+    lane_q = args.sky_lane_queue if args.sky_lane_queue != "auto" else ("low" if args.config in ("c3", "c3b") else "high")
+    renderer_kw = dict(sky_lane=not args.no_sky_lane, fused_histogram=not args.unfused_histogram,
+                       static_inputs=not args.no_static_inputs, velocity_slots=vslots,
+                       bloom_in_composition=not args.no_bloom_in_composition, sky_lane_queue=lane_q)
+    r = soc.Renderer(fr, **renderer_kw)
     if args.raster:
         if sc is None:
             sc = raster.scene_setup(g, scene_id, tex_size=1024, device=device)
@@ -338,11 +393,11 @@ def main():
 
     for _ in range(args.warmup):
         frame()
-    # the renderer's sky-lane queue probe (soc_renderer_side_queue) spans its first side_queue_probe_frames() frames and
-    # decides at the first frame after they completed: untimed frames until then, the same count on every rank (each
-    # frame of the exchange path is a collective; the ranks share the resolution, so the count)
+    # the sky-lane queue is fixed by the configuration (no timing probe): --warmup frames exactly. Only --sky-lane-queue
+    # probe runs the renderer's probe, in extra untimed frames until it has chosen (the same count on every rank: each
+    # frame of the exchange path is a collective)
     probe_frames = 0
-    if not args.no_sky_lane and r.side_queue() == -1:
+    if lane_q == "probe" and not args.no_sky_lane and r.side_queue() == -1:
         probe_frames = max(0, r.side_queue_probe_frames() - args.warmup)
         for _ in range(probe_frames):
             frame()
@@ -411,14 +466,13 @@ def main():
             soc.write_png(args.write_frame, soc.read_image(fr["output"]))
     r.set_async(not args.no_sky_lane)
     stats = [st for st in stats if st[3]]     # passes with no work this frame (the folded fold pass) have no record
-    ms_pass = {n: round(ms, 4) for n, _, ms, _ in stats}
-    ms_group = {}
-    for n, gname, ms, _ in stats:
-        ms_group[gname] = round(ms_group.get(gname, 0.0) + ms, 4)
-
     # the renderer computes the bloom's last stage inside Composition in frames whose sky lane is the critical path
-    # (SOC_RENDERER_BLOOM_IN_COMPOSITION: the lane probe chose a high-priority sky lane)
+    # (SOC_RENDERER_BLOOM_IN_COMPOSITION with a high-priority sky lane): the fourth bloom pass then launches nothing
     bloom_in_comp = not args.no_bloom_in_composition and "BloomUpsample - 3+2" in names and r.side_queue() == 1
+    no_launch = {"BloomUpsample - 1+0"} if bloom_in_comp else set()
+    ms_pass = {n: (None if n in no_launch else round(ms, 4)) for n, _, ms, _ in stats}
+    ms_group_unfused = unfused_group_ms(fr, renderer_kw, g, args.profile_frames) if not args.raster else None
+    ms_group = reference_groups(stats, no_launch, ms_group_unfused)
     algo = algorithmic_bytes(W, H, f_sky, velocity_slots=vslots, bloom_in_composition=bloom_in_comp)
     # Two durations per north-star kernel: alone = the serial per-pass loop above (every pass evented,
     # second lane off: nothing shares the CUs with the kernel), and in-frame = the timed frames' events (lanes
@@ -432,7 +486,9 @@ def main():
     ssao_ms = ms_pass.get("SSAOGeneration", ssao_frame_ms)
     ns_bytes = algo[comp] + algo["SSAOGeneration"]
     ns_us = (comp_ms + ssao_ms) * 1e3
-    pass_gbs = {n: round(algo[n] / (ms * 1e-3) / 1e9, 1) for n, _, ms, _ in stats if ms > 0 and n in algo}
+    # GB/s of every pass that launched work (a pass that launched nothing this frame reports null, not its event overhead)
+    pass_gbs = {n: (None if n in no_launch else round(algo[n] / (ms * 1e-3) / 1e9, 1))
+                for n, _, ms, _ in stats if ms > 0 and n in algo}
     # the committed PMC table comes from the default command (C3, G-buffer resident): other workloads get null
     pmc_ok = args.config == "c3" and not args.raster
     # the Composition kernel the timed frames ran (its fourth template argument: the in-kernel bloom of a sky-bound frame)
@@ -503,6 +559,8 @@ def main():
                                  if not args.no_static_inputs else "forked at every frame start")),
                    "sky_lane_queue": {1: "high priority", 2: "low priority", 0: "normal priority",
                                       -1: "not chosen"}.get(r.side_queue(), "?"),
+                   "sky_lane_queue_choice": ("timed probe" if lane_q == "probe" else
+                                             f"fixed ({lane_q}: {'--sky-lane-queue' if args.sky_lane_queue != 'auto' else 'the configuration default'})"),
                    "untimed_lane_probe_frames": probe_frames,
                    "bloom_last_stage": ("inside Composition (mip1 -> [mip0] -> emissive term per tile in LDS; the "
                                         "full-resolution bloom output is not written)" if bloom_in_comp
@@ -535,7 +593,14 @@ def main():
         "allreduce_us_per_frame": (round(sum(p["allreduce_us_per_frame"] for p in per_rank) / world, 2)
                                    if exchange else None),
         "ms_per_pass": ms_pass,
+        # the reference's 12 GPU-metric groups (renderer.cpp:558-588) from the serial per-pass loop; a fused launch's time
+        # is split between its groups in the ratio of the same passes unfused (ms_per_group_unfused: the reference's own
+        # pass structure, one launch per task, measured in the same run)
         "ms_per_group": ms_group,
+        "ms_per_group_basis": ("serial per-pass loop; Composition+GenerateLuminanceHistogram split into Composition / "
+                               "Auto Exposure and TemporalAntiAliasing+ToneMapping into Temporal Anti-Aliasing / Tone "
+                               "Mapping by the unfused passes' time ratio"),
+        "ms_per_group_unfused": ms_group_unfused,
         "gbs_per_pass": pass_gbs,
     }
     if not args.no_cpu_baseline and world == 1:

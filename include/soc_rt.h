@@ -417,6 +417,13 @@ typedef struct soc_renderer soc_renderer;
  * declares BLOOM_MIP1 besides the bloom output. Applies with the weighted chain and the fused histogram's pair path. A
  * caller that reads the bloom output leaves the flag off. */
 #define SOC_RENDERER_BLOOM_IN_COMPOSITION 1024
+/* The sky lane's hardware queue (soc_renderer_side_queue): a low-priority stream by default (frames whose main lane is
+ * the critical path, e.g. the Sponza frames at 4K); SOC_RENDERER_SKY_LANE_HIGH a high-priority stream (sky-bound frames:
+ * the terrain / 1080p frames), which also selects the sky-bound variants (BLOOM_IN_COMPOSITION, the clouds' density grid
+ * at twice the resident set, hoisted classification); SOC_RENDERER_SKY_LANE_PROBE times both over the first frames and
+ * keeps the faster (round 5's default; the choice can then differ between runs). Same results in every case. */
+#define SOC_RENDERER_SKY_LANE_HIGH 2048
+#define SOC_RENDERER_SKY_LANE_PROBE 4096
 
 soc_renderer* soc_renderer_create(const soc_frame_images* images, uint32_t flags);
 void soc_renderer_destroy(soc_renderer* r);
@@ -454,9 +461,9 @@ int soc_renderer_set_current_history(soc_renderer* r, int32_t index);
  * Composition, so it overlaps bloom and SSAO. Results are identical either way. */
 int soc_renderer_set_async(soc_renderer* r, int32_t enable);
 /* The sky lane's hardware queue: 1 = a high-priority stream, 2 = low priority, 0 = normal priority (a queue HIP may
- * share with the caller's stream), -1 = not chosen yet (tuning knob SOC_RENDERER_SIDE_QUEUE=3, the default: after 16
- * frames, eight windows of 32-128 frames alternate high / low priority as ABBA pairs; high is kept if it is faster by
- * more than 2 % once their timing events have completed, else low) or no sky lane created. Same results either way. */
+ * share with the caller's stream), -1 = not chosen yet (SOC_RENDERER_SKY_LANE_PROBE: after 16 frames, eight windows of
+ * 32-128 frames alternate high / low priority as ABBA pairs; high is kept if it is faster by more than 2 % once their
+ * timing events have completed, else low) or no sky lane created. Same results either way. */
 int32_t soc_renderer_side_queue(const soc_renderer* r);
 /* Frames the auto probe spans from the renderer's first call (the choice is made at the first call after they have
  * completed on the GPU); 0 when no probe runs. A caller that times frames runs at least this many first. */

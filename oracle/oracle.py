@@ -46,6 +46,9 @@ _FUNCS = {
     "soc_oracle_generate_hiz": (C.c_int, [_G, _IMG, C.POINTER(_IMG), C.c_int32, C.c_int32]),
     "soc_oracle_luminance_bin": (C.c_uint32, [C.c_float] * 5),
     "soc_oracle_log2": (C.c_float, [C.c_float]),
+    "soc_oracle_det_sin": (C.c_float, [C.c_float]),
+    "soc_oracle_det_cos": (C.c_float, [C.c_float]),
+    "soc_oracle_det_pow": (C.c_float, [C.c_float, C.c_float]),
     "soc_oracle_f32_to_f16": (C.c_uint16, [C.c_float]),
     "soc_oracle_f16_to_f32": (C.c_float, [C.c_uint16]),
     "soc_oracle_clouds_counters": (None, [C.POINTER(C.c_uint64)]),

@@ -413,8 +413,142 @@ static const float k_ssao_kernel[SOC_SSAO_MAX_KERNEL][3] = {
     {-0.4800232f, -0.1899473f, 0.2398808f}, {0.6389147f, 0.1191014f, 0.5271206f},   {0.1932822f, -0.3692099f, 0.6060588f},
     {-0.3465451f, -0.1654651f, 0.6746758f}, {0.2448421f, -0.1610962f, 0.1289366f}};
 
-/* ssao_generation.inl:139-141 */
-static inline float ssao_rand(v2 c) { return fractf(sinf(c.x * 12.9898f + c.y * 78.233f) * 43758.5453f); }
+/* Deterministic sin / cos / pow of float arguments for the SSAO noise (quirk Q8: the hash fract(sin(a) * 43758.5453)
+   turns a 1-ulp difference of sin into ~3e-3 of the hash, so the oracle and the GPU's random-vector table must evaluate
+   sin identically, not merely accurately). Each is evaluated in double with IEEE add / mul / fma / div and rint only
+   (no libm), and rounded to float once: an accurate sinf / cosf / powf (the correctly rounded result except where the
+   double value lies within ~1e-16 of a float rounding boundary) whose bits do not depend on a math library. The GPU
+   table (ssao.hip det_sin / det_cos / det_pow, same operation sequence) gives the same bits, which the GPU suite checks
+   (frame_parity "hash_differs" = 0). Range reduction: Cody-Waite with the three-part pi/2 of fdlibm's __ieee754_rem_pio2
+   (exact for |x| < 2^20 pi/2, far beyond the hash's |arg| <= ~1e5); kernels: Taylor series on |r| <= pi/4 to 1/21!. */
+static const double k_pio2_1 = 1.57079632673412561417e+00, k_pio2_2 = 6.07710050630396597660e-11,
+                    k_pio2_3 = 2.02226624879595063154e-21, k_2_pi = 6.36619772367581382433e-01;
+static double det_sin_poly(double r) {
+    const double r2 = r * r;
+    double p = 1.9572941063391263e-20;
+    p = fma(p, r2, -8.22063524662433e-18);
+    p = fma(p, r2, 2.8114572543455206e-15);
+    p = fma(p, r2, -7.647163731819816e-13);
+    p = fma(p, r2, 1.6059043836821613e-10);
+    p = fma(p, r2, -2.505210838544172e-08);
+    p = fma(p, r2, 2.7557319223985893e-06);
+    p = fma(p, r2, -0.0001984126984126984);
+    p = fma(p, r2, 0.008333333333333333);
+    p = fma(p, r2, -0.16666666666666666);
+    return fma(r * r2, p, r);
+}
+static double det_cos_poly(double r) {
+    const double r2 = r * r;
+    double p = 4.110317623312165e-19;
+    p = fma(p, r2, -1.5619206968586225e-16);
+    p = fma(p, r2, 4.779477332387385e-14);
+    p = fma(p, r2, -1.1470745597729725e-11);
+    p = fma(p, r2, 2.08767569878681e-09);
+    p = fma(p, r2, -2.755731922398589e-07);
+    p = fma(p, r2, 2.48015873015873e-05);
+    p = fma(p, r2, -0.001388888888888889);
+    p = fma(p, r2, 0.041666666666666664);
+    p = fma(p, r2, -0.5);
+    return fma(r2, p, 1.0);
+}
+/* quadrant q of x (x = q pi/2 + r) and the reduced argument r */
+static double det_reduce(float x, long long* q) {
+    const double d = (double)x;
+    const double k = rint(d * k_2_pi);
+    double r = fma(-k, k_pio2_1, d);
+    r = fma(-k, k_pio2_2, r);
+    r = fma(-k, k_pio2_3, r);
+    *q = (long long)k;
+    return r;
+}
+static float det_sin(float x) {
+    long long q;
+    const double r = det_reduce(x, &q);
+    const int k = (int)(q & 3);
+    const double v = (k & 1) ? det_cos_poly(r) : det_sin_poly(r);
+    return (float)((k & 2) ? -v : v);
+}
+static float det_cos(float x) {
+    long long q;
+    const double r = det_reduce(x, &q);
+    const int k = (int)((q + 1) & 3);   /* cos x = sin(x + pi/2) */
+    const double v = (k & 1) ? det_cos_poly(r) : det_sin_poly(r);
+    return (float)((k & 2) ? -v : v);
+}
+/* pow(x, y) for finite x > 0 (the noise's uv and 4.2 W; GLSL pow is undefined for x < 0): exp(y ln x) in double,
+   ln x = e ln2 + 2 atanh((m - 1) / (m + 1)) with m in [sqrt(1/2), sqrt(2)), exp by k ln2 + r, |r| <= ln2 / 2. */
+static const double k_ln2_hi = 6.93147180369123816490e-01, k_ln2_lo = 1.90821492927058770002e-10,
+                    k_inv_ln2 = 1.44269504088896338700e+00;
+static float det_pow(float x, float y) {
+    if (!(x > 0.0f) || !isfinite(x) || !isfinite(y)) return powf(x, y);   /* outside the hash's domain (not reached) */
+    uint32_t b;
+    memcpy(&b, &x, 4);
+    int e = (int)((b >> 23) & 255u) - 127;
+    if (e == -127) {   /* subnormal: scale by 2^32 first (exact) */
+        float xs = x * 4294967296.0f;
+        memcpy(&b, &xs, 4);
+        e = (int)((b >> 23) & 255u) - 127 - 32;
+    }
+    const uint32_t mb = (b & 0x007fffffu) | 0x3f800000u;
+    float mf;
+    memcpy(&mf, &mb, 4);
+    double m = (double)mf;
+    if (m > 1.4142135623730951) { m *= 0.5; e += 1; }
+    const double s = (m - 1.0) / (m + 1.0), s2 = s * s;
+    double p = 0.04;   /* 1/25 */
+    p = fma(p, s2, 0.043478260869565216);
+    p = fma(p, s2, 0.047619047619047616);
+    p = fma(p, s2, 0.05263157894736842);
+    p = fma(p, s2, 0.058823529411764705);
+    p = fma(p, s2, 0.06666666666666667);
+    p = fma(p, s2, 0.07692307692307693);
+    p = fma(p, s2, 0.09090909090909091);
+    p = fma(p, s2, 0.1111111111111111);
+    p = fma(p, s2, 0.14285714285714285);
+    p = fma(p, s2, 0.2);
+    p = fma(p, s2, 0.3333333333333333);
+    const double lnm = 2.0 * fma(s * s2, p, s);
+    const double lnx = fma((double)e, k_ln2_hi, fma((double)e, k_ln2_lo, lnm));
+    const double z = (double)y * lnx;
+    const double k = rint(z * k_inv_ln2);
+    double r = fma(-k, k_ln2_hi, z);
+    r = fma(-k, k_ln2_lo, r);
+    double q = 8.896791392450574e-22;
+    q = fma(q, r, 1.9572941063391263e-20);
+    q = fma(q, r, 4.110317623312165e-19);
+    q = fma(q, r, 8.22063524662433e-18);
+    q = fma(q, r, 1.5619206968586225e-16);
+    q = fma(q, r, 2.8114572543455206e-15);
+    q = fma(q, r, 4.779477332387385e-14);
+    q = fma(q, r, 7.647163731819816e-13);
+    q = fma(q, r, 1.1470745597729725e-11);
+    q = fma(q, r, 1.6059043836821613e-10);
+    q = fma(q, r, 2.08767569878681e-09);
+    q = fma(q, r, 2.505210838544172e-08);
+    q = fma(q, r, 2.755731922398589e-07);
+    q = fma(q, r, 2.7557319223985893e-06);
+    q = fma(q, r, 2.48015873015873e-05);
+    q = fma(q, r, 0.0001984126984126984);
+    q = fma(q, r, 0.001388888888888889);
+    q = fma(q, r, 0.008333333333333333);
+    q = fma(q, r, 0.041666666666666664);
+    q = fma(q, r, 0.16666666666666666);
+    q = fma(q, r, 0.5);
+    q = fma(q, r, 1.0);
+    q = fma(q, r, 1.0);
+    if (!(k > -1000.0 && k < 1000.0)) return (float)(k > 0.0 ? INFINITY : 0.0);
+    const uint64_t sb = (uint64_t)((long long)k + 1023) << 52;
+    double sc;
+    memcpy(&sc, &sb, 8);
+    return (float)(q * sc);
+}
+
+float soc_oracle_det_sin(float x) { return det_sin(x); }
+float soc_oracle_det_cos(float x) { return det_cos(x); }
+float soc_oracle_det_pow(float x, float y) { return det_pow(x, y); }
+
+/* ssao_generation.inl:139-141 (sin: det_sin above) */
+static inline float ssao_rand(v2 c) { return fractf(det_sin(c.x * 12.9898f + c.y * 78.233f) * 43758.5453f); }
 
 /* ssao_generation.inl:143-155 */
 static float ssao_noise(v2 p, float freq) {
@@ -423,7 +557,7 @@ static float ssao_noise(v2 p, float freq) {
     v2 ij = V2(floorf(q.x), floorf(q.y));
     /* mod(p, unit) = p - unit * floor(p / unit) */
     v2 xy = V2((p.x - unit * floorf(p.x / unit)) / unit, (p.y - unit * floorf(p.y / unit)) / unit);
-    xy = V2(0.5f * (1.0f - cosf(3.14159265359f * xy.x)), 0.5f * (1.0f - cosf(3.14159265359f * xy.y)));
+    xy = V2(0.5f * (1.0f - det_cos(3.14159265359f * xy.x)), 0.5f * (1.0f - det_cos(3.14159265359f * xy.y)));
     float a = ssao_rand(V2(ij.x + 0.0f, ij.y + 0.0f));
     float b = ssao_rand(V2(ij.x + 1.0f, ij.y + 0.0f));
     float c = ssao_rand(V2(ij.x + 0.0f, ij.y + 1.0f));
@@ -467,8 +601,8 @@ static int ssao_generation(const soc_globals* g, soc_img depth, soc_img normal, 
                 rv = V3(e[0], e[1], 0.0f);
             } else {
                 float n1 = ssao_noise(uv, (float)(ndx * 2));
-                v2 puv = V2(powf(uv.x, 1.1f), powf(uv.y, 1.1f));
-                float n2 = ssao_noise(puv, powf((float)ndx * 4.2f, 1.5f + uv.x / 10.0f));
+                v2 puv = V2(det_pow(uv.x, 1.1f), det_pow(uv.y, 1.1f));
+                float n2 = ssao_noise(puv, det_pow((float)ndx * 4.2f, 1.5f + uv.x / 10.0f));
                 rv = normalize3(V3(n1, n2, 0.0f));
             }
             v3 t = normalize3(sub3(rv, muls3(n, dot3(rv, n))));
@@ -512,8 +646,8 @@ int soc_oracle_ssao_random_vectors(int32_t normal_width, int32_t tw, int32_t th,
         for (int x = 0; x < tw; ++x) {
             const v2 uv = V2(((float)x + 0.5f) / (float)tw, ((float)y + 0.5f) / (float)th);
             float n1 = ssao_noise(uv, (float)(normal_width * 2));
-            v2 puv = V2(powf(uv.x, 1.1f), powf(uv.y, 1.1f));
-            float n2 = ssao_noise(puv, powf((float)normal_width * 4.2f, 1.5f + uv.x / 10.0f));
+            v2 puv = V2(det_pow(uv.x, 1.1f), det_pow(uv.y, 1.1f));
+            float n2 = ssao_noise(puv, det_pow((float)normal_width * 4.2f, 1.5f + uv.x / 10.0f));
             v3 rv = normalize3(V3(n1, n2, 0.0f));
             out[2 * ((size_t)y * (size_t)tw + (size_t)x)] = rv.x;
             out[2 * ((size_t)y * (size_t)tw + (size_t)x) + 1] = rv.y;

@@ -62,6 +62,11 @@ int soc_oracle_generate_hiz(const soc_globals* g, soc_img depth, const soc_img* 
 /* Scalar helpers exposed for known-answer tests. */
 uint32_t soc_oracle_luminance_bin(float r, float g, float b, float log_min, float log_max);
 float soc_oracle_log2(float x);
+/* The SSAO noise hash's deterministic sin / cos / pow (quirk Q8; the same operation sequence as ssao.hip's random-vector
+   table): double evaluation with IEEE operations only, one rounding to float. */
+float soc_oracle_det_sin(float x);
+float soc_oracle_det_cos(float x);
+float soc_oracle_det_pow(float x, float y);
 uint16_t soc_oracle_f32_to_f16(float x);
 float soc_oracle_f16_to_f32(uint16_t h);
 /* Per-sky-pixel operation tallies of the clouds pass (filled by the last soc_oracle_cloud_rendering

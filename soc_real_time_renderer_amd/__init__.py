@@ -357,7 +357,11 @@ class Renderer:
     def __init__(self, frame: dict, timing: bool = False, stream=None, fused_bloom: bool = True, sky_lane: bool = True,
                  fused_tonemap: bool = True, fused_histogram: bool = True,
                  exact_bloom: bool = False, sky_split: bool = True, static_inputs: bool = False,
-                 velocity_slots: bool = False, bloom_in_composition: bool = False):
+                 velocity_slots: bool = False, bloom_in_composition: bool = False, sky_lane_queue: str = "low"):
+        """sky_lane_queue: the sky lane's hardware queue, "low" (default), "high" (sky-bound frames) or "probe" (timed
+        choice over the first frames; SOC_RENDERER_SKY_LANE_HIGH / _PROBE)."""
+        if sky_lane_queue not in ("low", "high", "probe"):
+            raise ValueError(f"sky_lane_queue must be low, high or probe, not {sky_lane_queue!r}")
         self.frame = frame
         fi = FrameImages()
         for k in ("albedo", "emissive", "normal", "depth", "velocity", "shadow", "noise", "ssao", "ssao_blur", "clouds",
@@ -381,7 +385,8 @@ class Renderer:
                  | (_abi.RENDERER_EXACT_BLOOM if exact_bloom else 0) | (0 if sky_split else _abi.RENDERER_NO_SKY_SPLIT)
                  | (_abi.RENDERER_STATIC_INPUTS if static_inputs else 0)
                  | (_abi.RENDERER_VELOCITY_SLOTS if velocity_slots else 0)
-                 | (_abi.RENDERER_BLOOM_IN_COMPOSITION if bloom_in_composition else 0))
+                 | (_abi.RENDERER_BLOOM_IN_COMPOSITION if bloom_in_composition else 0)
+                 | {"low": 0, "high": _abi.RENDERER_SKY_LANE_HIGH, "probe": _abi.RENDERER_SKY_LANE_PROBE}[sky_lane_queue])
         h = lib().soc_renderer_create(C.byref(fi), flags)
         if not h:
             raise SocError(-1, lib().soc_last_error_string().decode())

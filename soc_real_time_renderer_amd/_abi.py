@@ -42,6 +42,8 @@ RENDERER_NO_SKY_SPLIT = 128
 RENDERER_STATIC_INPUTS = 256
 RENDERER_VELOCITY_SLOTS = 512
 RENDERER_BLOOM_IN_COMPOSITION = 1024
+RENDERER_SKY_LANE_HIGH = 2048
+RENDERER_SKY_LANE_PROBE = 4096
 HISTOGRAM_SCRATCH_WORDS = 2048
 
 Mat4 = C.c_float * 16

@@ -677,6 +677,7 @@ struct soc_renderer {
     // sky split configured (graph) / active this frame (the pair path applies at the globals' resolution)
     bool sky_split = false, sky_split_active = false;
     bool bloom_in_comp = false;          // SOC_RENDERER_BLOOM_IN_COMPOSITION applies to this graph
+    bool bloom_in_comp_ok = false;       // ... and the fused pair path applies at this frame's globals resolution
     // the caller's stream is ordered after all second-lane work of the previous call (its join or an equivalent wait)
     bool main_after_side = true;
     // SOC_RENDERER_STATIC_INPUTS: a call of this graph has completed, so the frame inputs the caller wrote before its
@@ -716,7 +717,9 @@ bool sky_lane_high(const soc_renderer* r) {
 // SOC_RENDERER_BLOOM_IN_COMPOSITION in this frame: the bloom's last stage inside Composition where the sky lane is the
 // critical path (high priority, as the lane probe's high windows too, so the probe times what would run), the fourth
 // bloom pass then recording nothing. Both callbacks of a frame see the same lane (set before the passes are issued).
-bool bloom_in_comp_active(const soc_renderer* r) { return r->bloom_in_comp && sky_lane_high(r); }
+// Re-checked every frame: a frame whose globals resolution differs from the images takes Composition's generic
+// path, which cannot compute the bloom, so the fourth pass must run then.
+bool bloom_in_comp_active(const soc_renderer* r) { return r->bloom_in_comp && r->bloom_in_comp_ok && sky_lane_high(r); }
 
 soc_renderer::Pass& add_pass(soc_renderer* r, std::string name, std::string group, int phase, uint64_t reads,
                              uint64_t writes, PassFn fn, uint32_t flags = 0) {
@@ -1176,15 +1179,15 @@ static int upload_lights(soc_renderer* r, const soc_globals* g, hipStream_t s) {
     return SOC_OK;
 }
 
-// Flags of the renderer's cross-lane synchronisation events (a pass's `done`, the lane switch): they order work on
-// this device only, so they skip the system-scope fence (hipEventDisableSystemFence: the L2 writeback + invalidate a
-// default event record implies on AMD GPUs, and the cold caches it leaves the next kernel; SOC_RENDERER_EVENT_FENCE=0
-// restores the default). Timing events keep the default: without the fence a start event's timestamp may be taken after
-// the next kernel has begun (6.5 us into SSAO, tools/event_trace_check.py), so the pass events would no longer bracket
-// their kernels. The fork / join events that order the renderer against the caller's stream keep the default too.
+// Flags of the renderer's cross-lane synchronisation events (a pass's `done`, the lane switch): they order CloudRendering /
+// SkyCompose writes before the Composition / TAA reads on another hardware queue of a multi-XCD device, so they keep the
+// default system-scope release (the L2 writeback an event record implies) (round 5 had made them fence-free
+// for a gain within noise). SOC_RENDERER_EVENT_FENCE=1 drops the fence (hipEventDisableSystemFence), a measurement knob
+// only. Timing events keep the default too: without the fence a start event's timestamp may be taken after the next kernel
+// has begun (6.5 us into SSAO, tools/event_trace_check.py).
 static unsigned device_event_flags() {
     return (unsigned)hipEventDisableTiming |
-           (tuning_knob("SOC_RENDERER_EVENT_FENCE", 1) == 1 ? (unsigned)hipEventDisableSystemFence : 0u);
+           (tuning_knob("SOC_RENDERER_EVENT_FENCE", 0) == 1 ? (unsigned)hipEventDisableSystemFence : 0u);
 }
 
 static int run_pass(soc_renderer::Pass& p, const soc_globals* g, hipStream_t s) {
@@ -1223,9 +1226,10 @@ static void destroy_side_lane(soc_renderer* r) {
 // given the caller's queue and the two lanes ran serialised (bench --exchange 0.79 vs 0.62 ms per frame, DESIGN.md §11
 // r5.8). A stream of another priority comes from a pool of its own, so the lane keeps a queue of its own whatever the
 // caller created. Which priority is faster depends on which lane is the frame's critical path (C3: the main lane, the
-// sky lane low is 5 % faster than high; C4: the sky lane, high is 3-10 % faster than low): tuning knob
-// SOC_RENDERER_SIDE_QUEUE 3 (default) times both over the first 273 frames (frame_lane_probe), 1 = high, 2 = low,
-// 0 = normal priority.
+// sky lane low; C4 / C2: the sky lane, high is 3-10 % faster than low). The flags fix it (round 6: one queue per
+// configuration, so a command runs the same kernels every time): low by default, SOC_RENDERER_SKY_LANE_HIGH high,
+// SOC_RENDERER_SKY_LANE_PROBE the round-5 timed probe (frame_lane_probe: both timed over the first 273 frames). Tuning
+// knob SOC_RENDERER_SIDE_QUEUE overrides (1 = high, 2 = low, 3 = probe, 0 = normal priority).
 static int ensure_side_lane(soc_renderer* r) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return set_error(SOC_E_HIP, "soc_renderer_execute: hipGetDevice failed");
@@ -1235,7 +1239,10 @@ static int ensure_side_lane(soc_renderer* r) {
         for (auto& p : r->passes)
             if (p.done) { (void)hipEventDestroy(p.done); p.done = nullptr; p.done_recorded = false; }
     }
-    int sq = tuning_knob("SOC_RENDERER_SIDE_QUEUE", 3);
+    // the lane's queue is fixed by the flags (deterministic: the same kernels every run): low priority by
+    // default, high with SOC_RENDERER_SKY_LANE_HIGH, the timed probe only with SOC_RENDERER_SKY_LANE_PROBE
+    const int sq_flags = (r->flags & SOC_RENDERER_SKY_LANE_HIGH) ? 1 : (r->flags & SOC_RENDERER_SKY_LANE_PROBE) ? 3 : 2;
+    int sq = tuning_knob("SOC_RENDERER_SIDE_QUEUE", sq_flags);
     int least = 0, greatest = 0;
     if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess || least == greatest) sq = 0;
     hipError_t se = hipSuccess;
@@ -1360,8 +1367,10 @@ extern "C" int soc_renderer_execute(soc_renderer* r, const soc_globals* g, int32
     r->fold_in_resolve = (phase & SOC_PHASE_ALL) == SOC_PHASE_ALL && !(r->flags & SOC_RENDERER_UNFUSED_HISTOGRAM);
     if (phase & SOC_PHASE_PRE_EXPOSURE) {
         const soc_img& em = r->img.bloom_output.data ? r->img.bloom_output : r->img.emissive;
-        r->sky_split_active = r->sky_split && soc::composition_pair_applicable(g, r->img.color, r->img.albedo, em,
-                                                                               r->img.normal, r->img.depth, r->img.clouds);
+        const bool pair_ok = soc::composition_pair_applicable(g, r->img.color, r->img.albedo, em, r->img.normal,
+                                                             r->img.depth, r->img.clouds);
+        r->sky_split_active = r->sky_split && pair_ok;
+        r->bloom_in_comp_ok = pair_ok;
         // the graph was derived with Composition independent of the clouds: it cannot fall back to reading them
         if (r->sky_split && !r->sky_split_active)
             return set_error(SOC_E_SHAPE, "soc_renderer_execute: globals resolution %dx%d differs from the frame images %dx%d",

@@ -22,6 +22,40 @@
 namespace soc {
 namespace {
 
+// The pass's transcendentals: the hardware approximations (default: v_exp_f32, v_sqrt_f32, v_log_f32, v_rcp_f32, ~1 ulp)
+// or the library's accurate forms (SOC_CLOUDS_PRECISE=1: a parity-study build, tools/clouds_parity_probe.py, which
+// measures what the approximations change against the oracle's libm).
+#ifndef SOC_CLOUDS_PRECISE
+#define SOC_CLOUDS_PRECISE 0
+#endif
+// SOC_CLOUDS_EXACT (default 1): the chain from the view ray to every noise tap (march geometry, step positions, altitude,
+// noise coordinates, sub-texel fixed point) with the reference's operation order and roundings, so it selects the same
+// texels and weights as the oracle (the file is compiled without implicit contraction; intended fmas are explicit).
+// 0 = round 5's fused forms (fewer instructions, taps an ulp away). See noise3.
+#ifndef SOC_CLOUDS_EXACT
+#define SOC_CLOUDS_EXACT 1
+#endif
+__device__ __forceinline__ float cl_exp(float x) {
+    if constexpr (SOC_CLOUDS_PRECISE != 0) return expf(x);
+    else return __expf(x);
+}
+__device__ __forceinline__ float cl_exp2(float x) {
+    if constexpr (SOC_CLOUDS_PRECISE != 0) return exp2f(x);
+    else return __builtin_amdgcn_exp2f(x);
+}
+__device__ __forceinline__ float cl_sqrt(float x) {
+    if constexpr (SOC_CLOUDS_PRECISE != 0) return sqrtf(x);
+    else return __builtin_amdgcn_sqrtf(x);
+}
+__device__ __forceinline__ float cl_log2(float x) {
+    if constexpr (SOC_CLOUDS_PRECISE != 0) return log2f(x);
+    else return __builtin_amdgcn_logf(x);
+}
+__device__ __forceinline__ float cl_rcp(float x) {
+    if constexpr (SOC_CLOUDS_PRECISE != 0) return 1.0f / x;
+    else return __builtin_amdgcn_rcpf(x);
+}
+
 constexpr int kNoise = 64, kNoiseMask = 63;
 // LDS quad table: 81 x 81 entries (64 + the 17-texel tap offset), so the second tap of get_3d_noise is
 // the first tap's address plus a constant (an immediate ds_read offset) with no wrap arithmetic.
@@ -105,32 +139,67 @@ __device__ __forceinline__ int floor_to_int(float x) {
 typedef float f2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2v pfma(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
 
-// get_3d_noise, :219-233
+// One bilinear REPEAT tap of the noise .x at the fixed-point texel coordinate (fx, fy) (8 fractional bits), from the LDS
+// quad table: 65536 x 255 x the bilinear (exact in integers).
+template <typename Q>
+__device__ __forceinline__ uint32_t noise_tap(const Q* quads, int fx, int fy) {
+    const uint32_t wx = (uint32_t)fx & 255u, wy = (uint32_t)fy & 255u;
+    const uint32_t ix = ((uint32_t)fx >> 8) & kNoiseMask, iy = ((uint32_t)fy >> 8) & kNoiseMask;
+    return quad_bilerp_u(quads[iy * (uint32_t)kTW + ix], wx * 65535u + 256u, wy * 65535u + 256u);
+}
+
+// get_3d_noise, :219-233.
+// SOC_CLOUDS_EXACT (default): the coordinates with the reference's (and the oracle's) roundings: coord = pos.xy / 64 +
+// p 17/64 (both terms exact, so one fma is the same sum), the second tap at coord + 17/64 (rounded: near a binade edge
+// it is not the first tap + 17 texels), and the sampling contract's fixed point t = RN(coord 64 - 0.5),
+// fx = floor(RN(t 256 + 0.5)) (coord 64 and t 256 are exact, so each is one fma). A noise coordinate one ulp off moves a
+// tap across a 1/256 sub-texel step in a few percent of the evaluations, and the smoothstep at 0.55..0.6 amplifies the
+// density change: the fused form below put 6 % of C3's sky texels one RGBA8 level off the oracle's
+// (tools/clouds_parity_probe.py). SOC_CLOUDS_EXACT=0 (round 5): 256 pos.x + 4352 p - 127.5 in one rounding, the
+// second tap at +17 texels.
 template <typename Q>
 __device__ __forceinline__ float noise3(const CtxT<Q>& cx, f3 pos) {
     const float p = floorf(pos.z);
     const float f = pos.z - p;
-    // fixed-point texel coordinate of the first tap: (u 64 - 0.5) 256 + 0.5 with u = pos.x / 64 + p 17/64,
-    // i.e. 256 pos.x + 4352 p - 127.5 (one rounding instead of four; within the pass tolerance)
-    const float base = __builtin_fmaf(p, 4352.0f, -127.5f);
-    const int fx = floor_to_int(__builtin_fmaf(pos.x, 256.0f, base));
-    const int fy = floor_to_int(__builtin_fmaf(pos.y, 256.0f, base));
-    const uint32_t wx = (uint32_t)fx & 255u, wy = (uint32_t)fy & 255u;
-    const uint32_t wxp = wx * 65535u + 256u, wyp = wy * 65535u + 256u;
-    const uint32_t ix = ((uint32_t)fx >> 8) & kNoiseMask, iy = ((uint32_t)fy >> 8) & kNoiseMask;
-    const Q* t = cx.quads + (iy * (uint32_t)kTW + ix);
-    const Q q0 = t[0], q1 = t[kTap2 * kTW + kTap2];
-    const float a = (float)quad_bilerp_u(q0, wxp, wyp), b = (float)quad_bilerp_u(q1, wxp, wyp);
+    float a, b;
+    if constexpr (SOC_CLOUDS_EXACT != 0) {
+        const float pz = p * 0.265625f;   // p * zStretch: exact
+        const float ux = __builtin_fmaf(pos.x, 0.015625f, pz), uy = __builtin_fmaf(pos.y, 0.015625f, pz);
+        const float vx = ux + 0.265625f, vy = uy + 0.265625f;
+        auto fixed = [](float u) { return floor_to_int(__builtin_fmaf(__builtin_fmaf(u, 64.0f, -0.5f), 256.0f, 0.5f)); };
+        a = (float)noise_tap(cx.quads, fixed(ux), fixed(uy));
+        b = (float)noise_tap(cx.quads, fixed(vx), fixed(vy));
+    } else {
+        // fixed-point texel coordinate of the first tap: (u 64 - 0.5) 256 + 0.5 with u = pos.x / 64 + p 17/64,
+        // i.e. 256 pos.x + 4352 p - 127.5 (one rounding instead of four)
+        const float base = __builtin_fmaf(p, 4352.0f, -127.5f);
+        const int fx = floor_to_int(__builtin_fmaf(pos.x, 256.0f, base));
+        const int fy = floor_to_int(__builtin_fmaf(pos.y, 256.0f, base));
+        const uint32_t wx = (uint32_t)fx & 255u, wy = (uint32_t)fy & 255u;
+        const uint32_t wxp = wx * 65535u + 256u, wyp = wy * 65535u + 256u;
+        const uint32_t ix = ((uint32_t)fx >> 8) & kNoiseMask, iy = ((uint32_t)fy >> 8) & kNoiseMask;
+        const Q* t = cx.quads + (iy * (uint32_t)kTW + ix);
+        const Q q0 = t[0], q1 = t[kTap2 * kTW + kTap2];
+        a = (float)quad_bilerp_u(q0, wxp, wyp);
+        b = (float)quad_bilerp_u(q1, wxp, wyp);
+    }
     return __builtin_fmaf(f, b - a, a);   // x 1 / (255 65536) = the noise value; the caller folds it into the octave weight
 }
 constexpr float kNoiseNorm = 1.0f / (255.0f * 65536.0f);
 
 // |v| with the hardware square root (1 ulp). Every length in this pass is an Earth-scale distance
 // (|v| ~ 6.4e6 m, ulp 0.5 m), far from the denormal range the full-precision sequence guards.
-__device__ __forceinline__ float hw_length3(f3 v) { return __builtin_amdgcn_sqrtf(dot3(v, v)); }
+__device__ __forceinline__ float hw_length3(f3 v) { return cl_sqrt(dot3(v, v)); }
+// The altitude's length with the correctly rounded square root under SOC_CLOUDS_EXACT: one ulp of |p + R e_y| is 0.5 m of
+// altitude, which moves the y noise coordinate by ~0.13 sub-texel steps (the hardware square root's 1-ulp error flipped
+// taps in ~1 of 8 evaluations)
+__device__ __forceinline__ float alt_length3(f3 v) {
+    if constexpr (SOC_CLOUDS_EXACT != 0) return sqrtf(dot3(v, v));
+    else return hw_length3(v);
+}
 
 // Altitude above the planet of a point given relative to the camera's ground point.
-__device__ __forceinline__ float cloud_height(f3 p) { return hw_length3(f3{p.x, p.y + kEarthRadius, p.z}) - kEarthRadius; }
+__device__ __forceinline__ float cloud_height(f3 p) { return alt_length3(f3{p.x, p.y + kEarthRadius, p.z}) - kEarthRadius; }
 
 // get_clouds, :235-262, for a point whose altitude h is already known to lie inside the layer.
 // The four octaves carry weights 1/2, 1/4, 1/8, 1/16 and each lies in [0, 1], so once the partial sum
@@ -155,7 +224,7 @@ __device__ float clouds_at(const C& cx, f3 p, float h) {
                      __builtin_fmaf(cc.z, 16.0f, mv.z * 16.0f)};
     n = __builtin_fmaf(noise3(cx, c4), 0.0625f * kNoiseNorm, n);
     const float hh = p.y - kMinH;
-    const float th = (1.0f - __expf(-0.01f * hh)) * __expf(-0.004f * hh);
+    const float th = (1.0f - cl_exp(-0.01f * hh)) * cl_exp(-0.004f * hh);
     const float t = clampf((n - 0.55f) * (1.0f / (0.6f - 0.55f)), 0.0f, 1.0f);
     const float clouds = t * t * (3.0f - 2.0f * t) * th;
     return clouds * 0.03f;
@@ -185,7 +254,7 @@ __device__ float sun_visibility(const C& cx, f3 p, f3 sun) {
         if (h > kMaxH && rising) break;
         if (h >= kMinH && h <= kMaxH) tr += clouds_at(cx, pos, h);
     }
-    return __expf(-tr * rSteps);
+    return cl_exp(-tr * rSteps);
 }
 
 __device__ __forceinline__ float hg_phase(float x, float g) {
@@ -205,8 +274,8 @@ __device__ f3 scattering_top(f3 sun) {
     dl = 1.0f / dl;
     const float odl = 100000.0f * dl;
     const f3 sv = total * od, sl = total * odl;
-    const f3 av = f3{__expf(-total.x * od), __expf(-total.y * od), __expf(-total.z * od)};
-    const f3 al = f3{__expf(-total.x * odl), __expf(-total.y * odl), __expf(-total.z * odl)};
+    const f3 av = f3{cl_exp(-total.x * od), cl_exp(-total.y * od), cl_exp(-total.z * od)};
+    const f3 al = f3{cl_exp(-total.x * odl), cl_exp(-total.y * odl), cl_exp(-total.z * odl)};
     const f3 num = al - av, den = (sl - sv) * kLn2;
     const f3 absorb = f3{(fabsf(num.x) + 1e-3f) / (fabsf(den.x) + 1e-3f), (fabsf(num.y) + 1e-3f) / (fabsf(den.y) + 1e-3f),
                          (fabsf(num.z) + 1e-3f) / (fabsf(den.z) + 1e-3f)};
@@ -246,12 +315,23 @@ __device__ __forceinline__ MarchShade march_shade(f3 dir, f3 sun, f3 skyl) {
     return m;
 }
 
-// Position of march step i (:321-333: cp = start + inc * dither, then cp += inc per step) as one fma per
-// component, start + inc (i + dither): i + dither is exact (dither = k/256), so every step carries one
-// rounding instead of the reference's accumulated i additions (within the pass tolerance), and a lane
-// can evaluate any step directly. Every path (single-lane march, density, sunvis) uses this form, so
-// the pair path stays bit-identical to the single-lane march.
+// Position of march step i (:321-333): cp = inc * dither + start, then cp += inc per step.
+// SOC_CLOUDS_EXACT: the reference's accumulation (a pass over the steps carries cp along; a lane that needs step i alone
+// repeats the i additions: a few dozen VALU against a sun march's ~1,500). 0: one fma per component,
+// start + inc (i + dither) (i + dither is exact), which differs from the accumulated position by a few ulps.
+// Every path (single-lane march, density, sunvis) uses these, so the pair path stays bit-identical to the single-lane march.
+__device__ __forceinline__ f3 step_next(const MarchGeom& mg, float dither, int i, f3 cp) {
+    if constexpr (SOC_CLOUDS_EXACT != 0) return cp + mg.inc;   // the position of step i + 1
+    const float t = (float)(i + 1) + dither;
+    return f3{__builtin_fmaf(mg.inc.x, t, mg.start.x), __builtin_fmaf(mg.inc.y, t, mg.start.y),
+              __builtin_fmaf(mg.inc.z, t, mg.start.z)};
+}
 __device__ __forceinline__ f3 step_position(const MarchGeom& mg, float dither, int i) {
+    if constexpr (SOC_CLOUDS_EXACT != 0) {
+        f3 cp = mg.inc * dither + mg.start;
+        for (int k = 0; k < i; ++k) cp = cp + mg.inc;
+        return cp;
+    }
     const float t = (float)i + dither;
     return f3{__builtin_fmaf(mg.inc.x, t, mg.start.x), __builtin_fmaf(mg.inc.y, t, mg.start.y),
               __builtin_fmaf(mg.inc.z, t, mg.start.z)};
@@ -261,11 +341,11 @@ __device__ __forceinline__ f3 step_position(const MarchGeom& mg, float dither, i
 __device__ __forceinline__ void march_accumulate(const MarchShade& ms, f3 sun_color, float od, float vis, f3& scattering,
                                                  float& transmittance) {
     const float hPi = kPi * 0.5f, rLOG2 = 1.0f / kLn2;
-    const float integral = __expf(-1.11f * rLOG2 * od) * (-1.0f / 1.11f) + 1.0f / 1.11f;
-    const float beers = 1.0f - __expf(-(od * kLn2) * 2.0f);
+    const float integral = cl_exp(-1.11f * rLOG2 * od) * (-1.0f / 1.11f) + 1.0f / 1.11f;
+    const float beers = 1.0f - cl_exp(-(od * kLn2) * 2.0f);
     const f3 sunl = sun_color * vis * beers * ms.phase * hPi * kSunBrightness;
     scattering = scattering + (sunl + ms.skyl) * integral * kPi * transmittance;
-    transmittance *= __expf(-od);
+    transmittance *= cl_exp(-od);
 }
 
 __device__ __forceinline__ f3 march_finish(const MarchGeom& mg, f3 color, f3 scattering, float transmittance) {
@@ -282,8 +362,8 @@ __device__ f3 volumetric_clouds(const Ctx& cx, f3 dir, f3 sun, f3 color, float d
     const MarchShade ms = march_shade(dir, sun, sky_light(sun));
     f3 scattering = f3{0.0f, 0.0f, 0.0f};
     float transmittance = 1.0f;
-    for (int i = 0; i < 24; i++) {
-        const f3 cp = step_position(mg, dither, i);
+    f3 cp = step_position(mg, dither, 0);
+    for (int i = 0; i < 24; cp = step_next(mg, dither, i, cp), i++) {
         const float od = get_clouds(cx, cp) * mg.stepLength;
         if (od <= 0.0f) continue;
         march_accumulate(ms, sun_color, od, sun_visibility(cx, cp, sun), scattering, transmittance);
@@ -302,7 +382,7 @@ constexpr float kExpR = -1.44269504f / kShRlh, kExpM = -1.44269504f / kShMie;   
 __device__ __forceinline__ f2v secondary_od(float A, float PoD, float C2) {
     const float cR = -kRPlanet * kExpR, cM = -kRPlanet * kExpM;
     const float delta = PoD * PoD + kRAtmos * kRAtmos - A;
-    const float jStep = (delta < 0.0f ? -1.0f : -PoD + __builtin_amdgcn_sqrtf(delta)) / 8.0f;
+    const float jStep = (delta < 0.0f ? -1.0f : -PoD + cl_sqrt(delta)) / 8.0f;
     const float B = 2.0f * PoD, half = jStep * 0.5f;
     float jTime = 0.0f;
     f2v jOd = {0.0f, 0.0f};
@@ -313,10 +393,10 @@ __device__ __forceinline__ f2v secondary_od(float A, float PoD, float C2) {
         const float jT1 = jTime + jStep;
         const f2v t = f2v{jTime, jT1} + f2v{half, half};
         const f2v q = pfma(t, pfma(t, f2v{C2, C2}, f2v{B, B}), f2v{A, A});
-        const f2v len = {__builtin_amdgcn_sqrtf(q.x), __builtin_amdgcn_sqrtf(q.y)};
+        const f2v len = {cl_sqrt(q.x), cl_sqrt(q.y)};
         const f2v eR = pfma(len, f2v{kExpR, kExpR}, f2v{cR, cR}), eM = pfma(len, f2v{kExpM, kExpM}, f2v{cM, cM});
-        jOd = pfma(f2v{__builtin_amdgcn_exp2f(eR.x), __builtin_amdgcn_exp2f(eM.x)}, f2v{jStep, jStep}, jOd);
-        jOd = pfma(f2v{__builtin_amdgcn_exp2f(eR.y), __builtin_amdgcn_exp2f(eM.y)}, f2v{jStep, jStep}, jOd);
+        jOd = pfma(f2v{cl_exp2(eR.x), cl_exp2(eM.x)}, f2v{jStep, jStep}, jOd);
+        jOd = pfma(f2v{cl_exp2(eR.y), cl_exp2(eM.y)}, f2v{jStep, jStep}, jOd);
         jTime = jT1 + jStep;
     }
     return jOd;
@@ -385,14 +465,14 @@ __global__ __launch_bounds__(kWorkgroup) void clouds_od_lut(float2* __restrict__
     const f2v od = secondary_od(r * r, r * mu, C2);
     const float lo = 1e-30f;   // the top row (r = rAtmos: a zero-length ray)
     const bool ok = od.x < 3.0e38f && od.y < 3.0e38f && od.x >= 0.0f && od.y >= 0.0f;   // NaN / inf fail
-    lut[i] = ok ? float2{__builtin_amdgcn_logf(fmaxf(od.x, lo)), __builtin_amdgcn_logf(fmaxf(od.y, lo))}
+    lut[i] = ok ? float2{cl_log2(fmaxf(od.x, lo)), cl_log2(fmaxf(od.y, lo))}
                 : float2{__builtin_nanf(""), __builtin_nanf("")};
 }
 
 // The secondary depths of a sample from the table (bilinear in (r, mu), then exp2), or NaN where the table has none.
 __device__ __forceinline__ f2v secondary_od_lut(const OdLut& L, float iLen, float PoD) {
     const float fr = fminf(fmaxf((iLen - kRPlanet) * kOdRScale, 0.0f), (float)(kOdR - 1));
-    const float mu = PoD * __builtin_amdgcn_rcpf(iLen);
+    const float mu = PoD * cl_rcp(iLen);
     const float fm = fminf(fmaxf((mu + 1.0f) * kOdMScale, 0.0f), (float)(kOdM - 1));
     const int ir = min((int)fr, kOdR - 2), im = min((int)fm, kOdM - 2);
     const float wr = fr - (float)ir, wm = fm - (float)im;
@@ -401,7 +481,7 @@ __device__ __forceinline__ f2v secondary_od_lut(const OdLut& L, float iLen, floa
     const f2v top = pfma(f2v{wm, wm}, f2v{b.x - a.x, b.y - a.y}, f2v{a.x, a.y});
     const f2v bot = pfma(f2v{wm, wm}, f2v{d.x - c.x, d.y - c.y}, f2v{c.x, c.y});
     const f2v l = pfma(f2v{wr, wr}, bot - top, top);
-    return f2v{__builtin_amdgcn_exp2f(l.x), __builtin_amdgcn_exp2f(l.y)};
+    return f2v{cl_exp2(l.x), cl_exp2(l.y)};
 }
 
 constexpr float kAtmSun = 22.0f, kAtmMie = 21e-6f, kAtmG = 0.758f;
@@ -433,10 +513,10 @@ __device__ __forceinline__ bool atmosphere_integrals(f3 r, f3 r0, f3 pSun, float
     for (int i = 0; i < 16; i++) {
         const f3 iPos = r0 + r * (iTime + iStep * 0.5f);
         const float A = dot3(iPos, iPos), PoD = dot3(iPos, pSun);
-        const float iLen = __builtin_amdgcn_sqrtf(A);
+        const float iLen = cl_sqrt(A);
         // (odR, odM) and the accumulators as packed pairs: element-wise the scalar operations (the same bits)
         const f2v ea = pfma(f2v{iLen, iLen}, f2v{kExpR, kExpM}, f2v{cR, cM});
-        const f2v od = f2v{__builtin_amdgcn_exp2f(ea.x), __builtin_amdgcn_exp2f(ea.y)} * f2v{iStep, iStep};
+        const f2v od = f2v{cl_exp2(ea.x), cl_exp2(ea.y)} * f2v{iStep, iStep};
         const float odR = od.x, odM = od.y;
         iOd = iOd + od;
         f2v jOd;
@@ -451,7 +531,7 @@ __device__ __forceinline__ bool atmosphere_integrals(f3 r, f3 r0, f3 pSun, float
         const f2v od_sum = iOd + jOd;
         const float fm = kMie * od_sum.y;
         const float fr = od_sum.x;
-        const f3 attn = f3{__expf(-(fm + kRlh.x * fr)), __expf(-(fm + kRlh.y * fr)), __expf(-(fm + kRlh.z * fr))};
+        const f3 attn = f3{cl_exp(-(fm + kRlh.x * fr)), cl_exp(-(fm + kRlh.y * fr)), cl_exp(-(fm + kRlh.z * fr))};
         totalRlh = totalRlh + attn * odR;
         totalMie = totalMie + attn * odM;
         iTime += iStep;
@@ -902,8 +982,9 @@ __global__ __launch_bounds__(kWorkgroup) __attribute__((amdgpu_waves_per_eu(6)))
                     pb.geom[2 * i] = float4{mg.start.x, mg.start.y, mg.start.z, dither};
                     pb.geom[2 * i + 1] = float4{mg.inc.x, mg.inc.y, mg.inc.z, mg.stepLength};
                 }
-                for (int s = 0; s < 24; s++) {
-                    const float od = get_clouds(cx, step_position(mg, dither, s)) * mg.stepLength;
+                f3 cp = step_position(mg, dither, 0);
+                for (int s = 0; s < 24; cp = step_next(mg, dither, s, cp), s++) {
+                    const float od = get_clouds(cx, cp) * mg.stepLength;
                     if (!(od <= 0.0f)) {
                         mask |= 1u << s;
                         od_tmp[s * 256] = od;
@@ -1174,8 +1255,9 @@ namespace {
 // the secondary-ray optical-depth table (kOdR x kOdM float2, 1 MiB).
 // Pair capacity 2 per pixel of the image (8 shards).
 // Per 256-entry batch of the list: the physical index of its first pair (or kInline).
-// density workgroups the od scratch is sized for (the resident set: 6 per CU on 256 CUs is 1536)
-constexpr size_t kDensityBlocks = 4096;
+// density workgroups the od scratch is sized for: the resident set (6 per CU on 256 CUs is 1536) times the largest grid
+// multiplier used (2: a sky-bound frame's density grid), 24 KiB each (4096 held 48 MiB more than any grid uses)
+constexpr size_t kDensityBlocks = 3072;
 struct CloudWs {
     uint32_t* counter;
     uint32_t* list;

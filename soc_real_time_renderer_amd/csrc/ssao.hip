@@ -30,10 +30,131 @@ struct SsaoParams {
     float inv_radius;   // 1 / radius (the sparse path requires radius > 0)
 };
 
-// ssao_generation.inl:139-141 (no FMA contraction: keeps the sin argument as the oracle's)
+// Deterministic sin / cos / pow of the noise (quirk Q8). The hash fract(sin(a) * 43758.5453) turns a 1-ulp difference of
+// sin into ~3e-3 of the hash, and the device's sinf and the host libm's round differently on ~1 in 2 arguments, so both
+// the random-vector table below and the oracle (soc_oracle.c det_sin / det_cos / det_pow) evaluate these functions with
+// ONE operation sequence: double precision, IEEE add / mul / fma / div and rint only, rounded to float once (an accurate
+// sinf: correctly rounded on every argument the CPU KAT samples). The table is filled once per resolution, so the double
+// arithmetic costs nothing per frame. Cody-Waite reduction with fdlibm's three-part pi/2; Taylor kernels on |r| <= pi/4.
+__device__ double det_sin_poly(double r) {
+    const double r2 = r * r;
+    double p = 1.9572941063391263e-20;
+    p = __builtin_fma(p, r2, -8.22063524662433e-18);
+    p = __builtin_fma(p, r2, 2.8114572543455206e-15);
+    p = __builtin_fma(p, r2, -7.647163731819816e-13);
+    p = __builtin_fma(p, r2, 1.6059043836821613e-10);
+    p = __builtin_fma(p, r2, -2.505210838544172e-08);
+    p = __builtin_fma(p, r2, 2.7557319223985893e-06);
+    p = __builtin_fma(p, r2, -0.0001984126984126984);
+    p = __builtin_fma(p, r2, 0.008333333333333333);
+    p = __builtin_fma(p, r2, -0.16666666666666666);
+    return __builtin_fma(r * r2, p, r);
+}
+__device__ double det_cos_poly(double r) {
+    const double r2 = r * r;
+    double p = 4.110317623312165e-19;
+    p = __builtin_fma(p, r2, -1.5619206968586225e-16);
+    p = __builtin_fma(p, r2, 4.779477332387385e-14);
+    p = __builtin_fma(p, r2, -1.1470745597729725e-11);
+    p = __builtin_fma(p, r2, 2.08767569878681e-09);
+    p = __builtin_fma(p, r2, -2.755731922398589e-07);
+    p = __builtin_fma(p, r2, 2.48015873015873e-05);
+    p = __builtin_fma(p, r2, -0.001388888888888889);
+    p = __builtin_fma(p, r2, 0.041666666666666664);
+    p = __builtin_fma(p, r2, -0.5);
+    return __builtin_fma(r2, p, 1.0);
+}
+// x = q pi/2 + r
+__device__ double det_reduce(float x, long long& q) {
+    const double d = (double)x;
+    const double k = __builtin_rint(d * 6.36619772367581382433e-01);
+    double r = __builtin_fma(-k, 1.57079632673412561417e+00, d);
+    r = __builtin_fma(-k, 6.07710050630396597660e-11, r);
+    r = __builtin_fma(-k, 2.02226624879595063154e-21, r);
+    q = (long long)k;
+    return r;
+}
+__device__ float det_sin(float x) {
+    long long q;
+    const double r = det_reduce(x, q);
+    const int k = (int)(q & 3);
+    const double v = (k & 1) ? det_cos_poly(r) : det_sin_poly(r);
+    return (float)((k & 2) ? -v : v);
+}
+__device__ float det_cos(float x) {
+    long long q;
+    const double r = det_reduce(x, q);
+    const int k = (int)((q + 1) & 3);   // cos x = sin(x + pi/2)
+    const double v = (k & 1) ? det_cos_poly(r) : det_sin_poly(r);
+    return (float)((k & 2) ? -v : v);
+}
+// pow(x, y) for finite x > 0 (uv and 4.2 W): exp(y ln x), ln x = e ln2 + 2 atanh((m - 1) / (m + 1)), m in
+// [sqrt(1/2), sqrt(2)); exp by k ln2 + r
+__device__ float det_pow(float x, float y) {
+    if (!(x > 0.0f) || !__builtin_isfinite(x) || !__builtin_isfinite(y)) return powf(x, y);   // outside the noise's domain
+    uint32_t b = __float_as_uint(x);
+    int e = (int)((b >> 23) & 255u) - 127;
+    if (e == -127) {   // subnormal: scale by 2^32 first (exact)
+        b = __float_as_uint(x * 4294967296.0f);
+        e = (int)((b >> 23) & 255u) - 127 - 32;
+    }
+    double m = (double)__uint_as_float((b & 0x007fffffu) | 0x3f800000u);
+    if (m > 1.4142135623730951) {
+        m *= 0.5;
+        e += 1;
+    }
+    const double s = (m - 1.0) / (m + 1.0), s2 = s * s;
+    double p = 0.04;   // 1/25
+    p = __builtin_fma(p, s2, 0.043478260869565216);
+    p = __builtin_fma(p, s2, 0.047619047619047616);
+    p = __builtin_fma(p, s2, 0.05263157894736842);
+    p = __builtin_fma(p, s2, 0.058823529411764705);
+    p = __builtin_fma(p, s2, 0.06666666666666667);
+    p = __builtin_fma(p, s2, 0.07692307692307693);
+    p = __builtin_fma(p, s2, 0.09090909090909091);
+    p = __builtin_fma(p, s2, 0.1111111111111111);
+    p = __builtin_fma(p, s2, 0.14285714285714285);
+    p = __builtin_fma(p, s2, 0.2);
+    p = __builtin_fma(p, s2, 0.3333333333333333);
+    const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+    const double lnm = 2.0 * __builtin_fma(s * s2, p, s);
+    const double lnx = __builtin_fma((double)e, ln2_hi, __builtin_fma((double)e, ln2_lo, lnm));
+    const double z = (double)y * lnx;
+    const double k = __builtin_rint(z * 1.44269504088896338700e+00);
+    double r = __builtin_fma(-k, ln2_hi, z);
+    r = __builtin_fma(-k, ln2_lo, r);
+    double q = 8.896791392450574e-22;
+    q = __builtin_fma(q, r, 1.9572941063391263e-20);
+    q = __builtin_fma(q, r, 4.110317623312165e-19);
+    q = __builtin_fma(q, r, 8.22063524662433e-18);
+    q = __builtin_fma(q, r, 1.5619206968586225e-16);
+    q = __builtin_fma(q, r, 2.8114572543455206e-15);
+    q = __builtin_fma(q, r, 4.779477332387385e-14);
+    q = __builtin_fma(q, r, 7.647163731819816e-13);
+    q = __builtin_fma(q, r, 1.1470745597729725e-11);
+    q = __builtin_fma(q, r, 1.6059043836821613e-10);
+    q = __builtin_fma(q, r, 2.08767569878681e-09);
+    q = __builtin_fma(q, r, 2.505210838544172e-08);
+    q = __builtin_fma(q, r, 2.755731922398589e-07);
+    q = __builtin_fma(q, r, 2.7557319223985893e-06);
+    q = __builtin_fma(q, r, 2.48015873015873e-05);
+    q = __builtin_fma(q, r, 0.0001984126984126984);
+    q = __builtin_fma(q, r, 0.001388888888888889);
+    q = __builtin_fma(q, r, 0.008333333333333333);
+    q = __builtin_fma(q, r, 0.041666666666666664);
+    q = __builtin_fma(q, r, 0.16666666666666666);
+    q = __builtin_fma(q, r, 0.5);
+    q = __builtin_fma(q, r, 1.0);
+    q = __builtin_fma(q, r, 1.0);
+    if (!(k > -1000.0 && k < 1000.0)) return k > 0.0 ? __builtin_inff() : 0.0f;
+    const double sc = __longlong_as_double((long long)((unsigned long long)((long long)k + 1023) << 52));
+    return (float)(q * sc);
+}
+
+// ssao_generation.inl:139-141 (no FMA contraction: keeps the sin argument as the oracle's; sin: det_sin above)
 __device__ __forceinline__ float ssao_rand(float cx, float cy) {
 #pragma clang fp contract(off)
-    return fractf(sinf(cx * 12.9898f + cy * 78.233f) * 43758.5453f);
+    return fractf(det_sin(cx * 12.9898f + cy * 78.233f) * 43758.5453f);
 }
 
 // ssao_generation.inl:143-155
@@ -42,8 +163,8 @@ __device__ float ssao_noise(float px, float py, float freq) {
     float unit = 2560.0f / freq;
     float ix = floorf(px / unit), iy = floorf(py / unit);
     float xx = (px - unit * floorf(px / unit)) / unit, yy = (py - unit * floorf(py / unit)) / unit;
-    xx = 0.5f * (1.0f - cosf(3.14159265359f * xx));
-    yy = 0.5f * (1.0f - cosf(3.14159265359f * yy));
+    xx = 0.5f * (1.0f - det_cos(3.14159265359f * xx));
+    yy = 0.5f * (1.0f - det_cos(3.14159265359f * yy));
     float a = ssao_rand(ix + 0.0f, iy + 0.0f);
     float b = ssao_rand(ix + 1.0f, iy + 0.0f);
     float c = ssao_rand(ix + 0.0f, iy + 1.0f);
@@ -57,7 +178,7 @@ __device__ float ssao_noise(float px, float py, float freq) {
 __device__ float2 ssao_random_vec(float u, float v, int noise_w) {
 #pragma clang fp contract(off)
     float n1 = ssao_noise(u, v, (float)(noise_w * 2));
-    float n2 = ssao_noise(powf(u, 1.1f), powf(v, 1.1f), powf((float)noise_w * 4.2f, 1.5f + u / 10.0f));
+    float n2 = ssao_noise(det_pow(u, 1.1f), det_pow(v, 1.1f), det_pow((float)noise_w * 4.2f, 1.5f + u / 10.0f));
     float l = sqrtf(n1 * n1 + n2 * n2 + 0.0f * 0.0f);
     return float2{n1 / l, n2 / l};
 }

@@ -106,6 +106,27 @@ def test_deterministic_log2_accuracy(oracle):
     assert math.isnan(oracle.log2(float("nan")))
 
 
+def test_deterministic_noise_functions_correctly_rounded(oracle):
+    """Quirk Q8: the SSAO hash's sin / cos / pow (soc_oracle.c det_sin / det_cos / det_pow, restated operation for
+    operation by ssao.hip's random-vector table) against float64 numpy rounded to float32: correctly rounded on every
+    sampled argument, over the hash's range (sin of |a| <= ~1e5, the noise's cos(pi x), pow(uv, 1.1) and
+    pow(4.2 W, 1.5 + u / 10)); the GPU table equals these bits (GPU suite, frame_parity hash_differs = 0)."""
+    L = oracle.lib()
+    rng = np.random.default_rng(8)
+    f32 = np.float32
+    xs = np.concatenate([rng.uniform(-1.2e5, 1.2e5, 4000), rng.uniform(-8, 8, 2000), [0.0, -0.0, 1e-30, 3.1415927]]).astype(f32)
+    for x in xs:
+        assert L.soc_oracle_det_sin(float(x)) == f32(np.sin(np.float64(x))), x
+        assert L.soc_oracle_det_cos(float(x)) == f32(np.cos(np.float64(x))), x
+    for x, y in zip(rng.uniform(1e-4, 1.0, 3000).astype(f32), rng.uniform(1.0, 1.7, 3000).astype(f32)):
+        assert L.soc_oracle_det_pow(float(x), float(y)) == f32(np.float64(x) ** np.float64(y)), (x, y)
+    for w in (64, 512, 960, 1920, 2048, 3840, 8192):
+        for u in (0.0001, 0.25, 0.5, 0.999):
+            x, y = f32(w * 4.2), f32(f32(1.5) + f32(u) / f32(10.0))
+            assert L.soc_oracle_det_pow(float(x), float(y)) == f32(np.float64(x) ** np.float64(y)), (w, u)
+    assert L.soc_oracle_det_pow(1.0, 1.1) == 1.0
+
+
 # ------------------------------------------------------------------------------------------------ histogram (Q9)
 def test_luminance_bins_known_answers(soc, oracle):
     g = soc.globals_defaults(64, 64)
