@@ -1255,6 +1255,18 @@ static int ensure_side_lane(soc_renderer* r) {
         r->side = r->lane_q[0];
         r->side_queue = -1;
         r->probe_frames = 0;
+    } else if (const int cus = tuning_knob("SOC_RENDERER_SKY_CUS", 0); cus > 0 && cus < 32) {
+        // measurement knob: the sky lane on a CU-masked queue of its own, `cus` of every 32 mask bits:
+        // SOC_RENDERER_SKY_CU_LAYOUT 0 = bit i set when (i / 8) % 32 < cus (the driver hands mask bits to the XCDs
+        // round-robin, so cus CUs of every XCD), 1 = when i % 32 < cus
+        int dev_cus = 256;
+        (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, dev);
+        const int layout = tuning_knob("SOC_RENDERER_SKY_CU_LAYOUT", 0);
+        std::vector<uint32_t> mask((size_t)(dev_cus + 31) / 32, 0u);
+        for (int i = 0; i < dev_cus; ++i)
+            if ((layout ? i % 32 : (i / 8) % 32) < cus) mask[(size_t)i / 32] |= 1u << (i % 32);
+        se = hipExtStreamCreateWithCUMask(&r->side, (uint32_t)mask.size(), mask.data());
+        r->side_queue = 0;
     } else if (sq == 1 || sq == 2) {
         se = hipStreamCreateWithPriority(&r->side, hipStreamNonBlocking, sq == 2 ? least : greatest);
         r->side_queue = sq;

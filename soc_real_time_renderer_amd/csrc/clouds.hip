@@ -96,10 +96,44 @@ __device__ __forceinline__ float bayer4(float x, float y) { return bayer2(0.5f *
 __device__ __forceinline__ float bayer8(float x, float y) { return bayer4(0.5f * x, 0.5f * y) * 0.25f + bayer2(x, y); }
 __device__ __forceinline__ float bayer16(float x, float y) { return bayer8(0.5f * x, 0.5f * y) * 0.25f + bayer2(x, y); }
 
-__device__ __forceinline__ float2 rsi(f3 p, f3 d, float radius) {
-    const float PoD = dot3(p, d);
+// The view-ray -> noise-tap chain restates the oracle's operation order without implicit contraction (SOC_CLOUDS_EXACT):
+// these helpers carry `fp contract(off)` themselves (the rest of the file is compiled with contraction).
+__device__ __forceinline__ float dot3_rn(f3 a, f3 b) {
+#pragma clang fp contract(off)
+    return a.x * b.x + a.y * b.y + a.z * b.z;
+}
+__device__ __forceinline__ float length3_rn(f3 a) { return sqrtf(dot3_rn(a, a)); }
+__device__ __forceinline__ f3 normalize3_rn(f3 a) {
+    const float l = length3_rn(a);
+    return f3{a.x / l, a.y / l, a.z / l};
+}
+__device__ __forceinline__ f4 mul_rn(const Mat4& M, f4 v) {
+#pragma clang fp contract(off)
+    const float* m = M.m;
+    return f4{m[0] * v.x + m[4] * v.y + m[8] * v.z + m[12] * v.w, m[1] * v.x + m[5] * v.y + m[9] * v.z + m[13] * v.w,
+              m[2] * v.x + m[6] * v.y + m[10] * v.z + m[14] * v.w, m[3] * v.x + m[7] * v.y + m[11] * v.z + m[15] * v.w};
+}
+// sqrt(x) correctly rounded for a normal x > 0 (x = 0 gives 0): the hardware square root (within 1 ulp) and ocml's
+// correction (the neighbour whose residual x - r s has the right sign), without the denormal scaling and class checks of
+// sqrtf (the altitude's |p + R e_y|^2 ~ 4e13)
+__device__ __forceinline__ float sqrt_rn(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float dn = __uint_as_float(__float_as_uint(s) - 1u), up = __uint_as_float(__float_as_uint(s) + 1u);
+    float r = __builtin_fmaf(-dn, s, x) <= 0.0f ? dn : s;
+    r = __builtin_fmaf(-up, s, x) > 0.0f ? up : r;
+    return r;
+}
+
+// rsi's discriminant (every caller that branches on it uses this one expression)
+__device__ __forceinline__ float rsi_delta(f3 p, f3 d, float radius, float& PoD) {
+#pragma clang fp contract(off)
+    PoD = dot3_rn(p, d);
     const float r2 = radius * radius;
-    float delta = PoD * PoD + r2 - dot3(p, p);
+    return PoD * PoD + r2 - dot3_rn(p, p);
+}
+__device__ __forceinline__ float2 rsi(f3 p, f3 d, float radius) {
+    float PoD;
+    float delta = rsi_delta(p, d, radius, PoD);
     if (delta < 0.0f) return float2{-1.0f, -1.0f};
     delta = sqrtf(delta);
     return float2{-PoD - delta, -PoD + delta};
@@ -165,10 +199,25 @@ __device__ __forceinline__ float noise3(const CtxT<Q>& cx, f3 pos) {
     if constexpr (SOC_CLOUDS_EXACT != 0) {
         const float pz = p * 0.265625f;   // p * zStretch: exact
         const float ux = __builtin_fmaf(pos.x, 0.015625f, pz), uy = __builtin_fmaf(pos.y, 0.015625f, pz);
-        const float vx = ux + 0.265625f, vy = uy + 0.265625f;
-        auto fixed = [](float u) { return floor_to_int(__builtin_fmaf(__builtin_fmaf(u, 64.0f, -0.5f), 256.0f, 0.5f)); };
-        a = (float)noise_tap(cx.quads, fixed(ux), fixed(uy));
-        b = (float)noise_tap(cx.quads, fixed(vx), fixed(vy));
+        // the contract's t = RN(64 u - 0.5) is exact (|u| < 2^17) and 256 t is exact, so RN(256 t + 0.5) is the single
+        // rounding RN(16384 u - 127.5): one fma
+        const int fx = floor_to_int(__builtin_fmaf(ux, 16384.0f, -127.5f));
+        const int fy = floor_to_int(__builtin_fmaf(uy, 16384.0f, -127.5f));
+        const uint32_t wxp = ((uint32_t)fx & 255u) * 65535u + 256u, wyp = ((uint32_t)fy & 255u) * 65535u + 256u;
+        const uint32_t ix = ((uint32_t)fx >> 8) & kNoiseMask, iy = ((uint32_t)fy >> 8) & kNoiseMask;
+        const Q* t = cx.quads + (iy * (uint32_t)kTW + ix);
+        a = (float)quad_bilerp_u(t[0], wxp, wyp);
+        if constexpr (SOC_CLOUDS_EXACT >= 2) {
+            // the second tap at RN(coord + 17/64), its own fixed point
+            const int gx = floor_to_int(__builtin_fmaf(ux + 0.265625f, 16384.0f, -127.5f));
+            const int gy = floor_to_int(__builtin_fmaf(uy + 0.265625f, 16384.0f, -127.5f));
+            b = (float)noise_tap(cx.quads, gx, gy);
+        } else {
+            // the second tap at coord + 17/64 taken as the first + 17 texels: u + 17/64 and 16384 (u + 17/64) - 127.5
+            // are exact, or round as u's own terms do, except where a sum crosses into the next binade (there it may land
+            // one sub-texel step away)
+            b = (float)quad_bilerp_u(t[kTap2 * kTW + kTap2], wxp, wyp);
+        }
     } else {
         // fixed-point texel coordinate of the first tap: (u 64 - 0.5) 256 + 0.5 with u = pos.x / 64 + p 17/64,
         // i.e. 256 pos.x + 4352 p - 127.5 (one rounding instead of four)
@@ -194,7 +243,7 @@ __device__ __forceinline__ float hw_length3(f3 v) { return cl_sqrt(dot3(v, v)); 
 // altitude, which moves the y noise coordinate by ~0.13 sub-texel steps (the hardware square root's 1-ulp error flipped
 // taps in ~1 of 8 evaluations)
 __device__ __forceinline__ float alt_length3(f3 v) {
-    if constexpr (SOC_CLOUDS_EXACT != 0) return sqrtf(dot3(v, v));
+    if constexpr (SOC_CLOUDS_EXACT != 0) return sqrt_rn(dot3_rn(v, v));
     else return hw_length3(v);
 }
 
@@ -208,16 +257,27 @@ __device__ __forceinline__ float cloud_height(f3 p) { return alt_length3(f3{p.x,
 // fp32 rounding of the remainder, so the early exits never change a result. (Round 4 measured two more exact exits
 // -- after octave 1, and once the partial sum reaches the upper edge 0.6, where the smoothstep saturates -- on the C3
 // and C4 frames: they fire on 0.5 % and 0-8 % of the evaluations and cost 1-2 % more time, profiles/r04_probe_clouds.txt.)
+// a s + b and a s - b, each product and sum rounded (the GLSL expressions of get_clouds; no contraction)
+__device__ __forceinline__ f3 madd_rn(f3 a, float s, f3 b) {
+#pragma clang fp contract(off)
+    return f3{a.x * s + b.x, a.y * s + b.y, a.z * s + b.z};
+}
+__device__ __forceinline__ f3 msub_rn(f3 a, float s, f3 b) {
+#pragma clang fp contract(off)
+    return f3{a.x * s - b.x, a.y * s - b.y, a.z * s - b.z};
+}
+
 template <typename C>
 __device__ float clouds_at(const C& cx, f3 p, float h) {
     p = f3{p.x + cx.cam_x, h, p.z + cx.cam_z};
     const f3 mv = f3{cx.time, 0.0f, cx.time};
-    const f3 cc = p * 0.001f + mv;
+    const bool ex = SOC_CLOUDS_EXACT != 0;
+    const f3 cc = ex ? madd_rn(p, 0.001f, mv) : p * 0.001f + mv;
     // octave weight x noise normalisation as one constant per octave (powers of two apart: one fma per octave)
     float n = noise3(cx, cc) * (0.5f * kNoiseNorm);
-    n = __builtin_fmaf(noise3(cx, cc * 2.0f + mv), 0.25f * kNoiseNorm, n);
+    n = __builtin_fmaf(noise3(cx, cc * 2.0f + mv), 0.25f * kNoiseNorm, n);   // 2 cc exact: one fma is the same sum
     if (n < 0.55f - 0.1875f - 1e-4f) return 0.0f;
-    n = __builtin_fmaf(noise3(cx, cc * 7.0f - mv), 0.125f * kNoiseNorm, n);
+    n = __builtin_fmaf(noise3(cx, ex ? msub_rn(cc, 7.0f, mv) : cc * 7.0f - mv), 0.125f * kNoiseNorm, n);
     if (n < 0.55f - 0.0625f - 1e-4f) return 0.0f;
     // (cc + mv) 16 == fma(cc, 16, 16 mv) exactly: scaling by a power of two commutes with the rounding
     const f3 c4 = f3{__builtin_fmaf(cc.x, 16.0f, mv.x * 16.0f), __builtin_fmaf(cc.y, 16.0f, mv.y * 16.0f),
@@ -248,7 +308,7 @@ __device__ float sun_visibility(const C& cx, f3 p, f3 sun) {
     f3 pos = inc * 0.5f + p;
     float tr = 0.0f;
     if (SOC_CLOUDS_PROFILE == 3) return 1.0f;
-    const bool rising = dot3(f3{p.x, p.y + kEarthRadius, p.z}, sun) > 0.0f;
+    const bool rising = dot3_rn(f3{p.x, p.y + kEarthRadius, p.z}, sun) > 0.0f;
     for (int i = 0; i < 10; i++, pos = pos + inc) {
         const float h = cloud_height(pos);
         if (h > kMaxH && rising) break;
@@ -296,7 +356,7 @@ __device__ __forceinline__ MarchGeom march_geometry(f3 dir) {
     g.start = dir * bottom;
     const f3 end = dir * top;
     g.inc = (end - g.start) * (1.0f / 24.0f);
-    g.stepLength = length3(g.inc);
+    g.stepLength = length3_rn(g.inc);
     return g;
 }
 
@@ -320,6 +380,7 @@ __device__ __forceinline__ MarchShade march_shade(f3 dir, f3 sun, f3 skyl) {
 // repeats the i additions: a few dozen VALU against a sun march's ~1,500). 0: one fma per component,
 // start + inc (i + dither) (i + dither is exact), which differs from the accumulated position by a few ulps.
 // Every path (single-lane march, density, sunvis) uses these, so the pair path stays bit-identical to the single-lane march.
+__device__ __forceinline__ f3 step_first_rn(const MarchGeom& mg, float dither) { return madd_rn(mg.inc, dither, mg.start); }
 __device__ __forceinline__ f3 step_next(const MarchGeom& mg, float dither, int i, f3 cp) {
     if constexpr (SOC_CLOUDS_EXACT != 0) return cp + mg.inc;   // the position of step i + 1
     const float t = (float)(i + 1) + dither;
@@ -328,7 +389,7 @@ __device__ __forceinline__ f3 step_next(const MarchGeom& mg, float dither, int i
 }
 __device__ __forceinline__ f3 step_position(const MarchGeom& mg, float dither, int i) {
     if constexpr (SOC_CLOUDS_EXACT != 0) {
-        f3 cp = mg.inc * dither + mg.start;
+        f3 cp = step_first_rn(mg, dither);
         for (int k = 0; k < i; ++k) cp = cp + mg.inc;
         return cp;
     }
@@ -587,7 +648,8 @@ __device__ f3 atmosphere_table(f3 r, f3 r0, f3 pSun, const SkyTab& st) {
     const float2 pa = rsi(r0, r, kRAtmos);
     if (pa.x > pa.y) return f3{0.0f, 0.0f, 0.0f};
     // the branch atmosphere_integrals takes: rsi(r0, r, rPlanet)'s discriminant and the sign of r0.r
-    const float PoD = dot3(r0, r), delta = PoD * PoD + kRPlanet * kRPlanet - dot3(r0, r0);
+    float PoD;
+    const float delta = rsi_delta(r0, r, kRPlanet, PoD);
     const int b = delta < 0.0f ? 1 : (PoD >= 0.0f ? 2 : 0);
     const f3 up = f3{st.upx, st.upy, st.upz};
     const float e = dot3(r, up), eh = st.eh, dl = st.dl;
@@ -617,9 +679,9 @@ constexpr int TX = 16, TY = 16;
 __device__ __forceinline__ f3 sky_dir(const CloudParams& p, int x, int y) {
     const float ru = div_rn((float)x, p.res_x_m1, p.r_res_x_m1), rv = div_rn((float)y, p.res_y_m1, p.r_res_y_m1);
     const float ndx = ru * 2.0f - 1.0f, ndy = rv * 2.0f - 1.0f;
-    const f4 rvs = mul(p.inv_proj, f4{ndx, ndy, -1.0f, 0.0f});
-    const f4 rws = mul(p.inv_view, f4{rvs.x, rvs.y, -1.0f, 0.0f});
-    return normalize3(f3{rws.x, rws.y, rws.z});
+    const f4 rvs = mul_rn(p.inv_proj, f4{ndx, ndy, -1.0f, 0.0f});
+    const f4 rws = mul_rn(p.inv_view, f4{rvs.x, rvs.y, -1.0f, 0.0f});
+    return normalize3_rn(f3{rws.x, rws.y, rws.z});
 }
 
 __device__ __forceinline__ f3 sky_atmosphere(const CloudParams& p, f3 dir, const OdLut& L = OdLut{nullptr, 0.0f}) {

@@ -633,6 +633,110 @@ void ssao_lds_kernel(DImg depth, DImg normal, DImg target, const float2* __restr
     ssao_pixel<TABLE, SPARSE_IP, FULL, LdsQuad<TXP, TYP, HALO>, UNROLL, PK>(x, y, depth, normal, target, table, p, quad);
 }
 
+// ---- the software-pipelined tap loop (round 6) --------------------------------------------------------------------
+// ssao_lds_kernel's loop (not unrolled: unrolling let the compiler hoist every pair's loads, r04_probe_ssao_unroll)
+// waited three times per tap pair: a scalar load of the pair's kernel vectors from the constant table (s_waitcnt
+// lgkmcnt(0), which also drains the LDS queue), the LDS texel reads it had just issued, and, in a wave with any
+// out-of-tile lane, that lane's global texel loads. Here the 13 pairs are unrolled by template recursion (kernel vectors
+// as literal operands: no table load), each in two stages: ISSUE computes the pair's fixed-point tap coordinates and
+// issues its texel reads (LDS tile, or the image for an out-of-tile lane), CONSUME filters them and adds the occlusion;
+// pair p + 1 is issued before pair p is consumed, so each pair's LDS latency (and an out-of-tile lane's global latency)
+// overlaps the previous pair's arithmetic. Per tap the same operations in the same order as the PK loop: the same bits.
+struct TapPair {
+    float v[8];   // tap 0: t0 t1 b0 b1, tap 1: t0 t1 b0 b1
+    uint32_t w;   // sub-texel weights: bytes wx0, wx1, wy0, wy1
+};
+
+template <int I, int TXP, int TYP, int HALO>
+__device__ __forceinline__ TapPair ssao_issue_pair(const SsaoPixel& px, const SsaoParams& p, const LdsQuad<TXP, TYP, HALO>& quad) {
+#pragma clang fp contract(off)
+    const f2v kx = {kKernel.v[I][0], kKernel.v[I + 1][0]}, ky = {kKernel.v[I][1], kKernel.v[I + 1][1]},
+              kz = {kKernel.v[I][2], kKernel.v[I + 1][2]};
+    // the per-pixel affine forms as scalar fmas (their packed form needs every per-pixel coefficient duplicated into a
+    // register pair: 18 more VGPRs, and this kernel's 8 waves per SIMD have 64; element-wise the same operations)
+    const f2v ww = {aff(px.aw, kx.x, ky.x, kz.x), aff(px.aw, kx.y, ky.y, kz.y)};
+    const f2v rw = {fast_rcp(ww.x), fast_rcp(ww.y)};
+    const f2v X = {__builtin_fmaf(aff(px.ax, kx.x, ky.x, kz.x), rw.x, p.c0x), __builtin_fmaf(aff(px.ax, kx.y, ky.y, kz.y), rw.y, p.c0x)};
+    const f2v Y = {__builtin_fmaf(aff(px.ay, kx.x, ky.x, kz.x), rw.x, p.c0y), __builtin_fmaf(aff(px.ay, kx.y, ky.y, kz.y), rw.y, p.c0y)};
+    const int fx0 = (int)__builtin_amdgcn_fmed3f(X.x, 0.5f, p.tmx), fx1 = (int)__builtin_amdgcn_fmed3f(X.y, 0.5f, p.tmx);
+    const int fy0 = (int)__builtin_amdgcn_fmed3f(Y.x, 0.5f, p.tmy), fy1 = (int)__builtin_amdgcn_fmed3f(Y.y, 0.5f, p.tmy);
+    TapPair t;
+    t.w = ((uint32_t)fx0 & 255u) | ((uint32_t)fx1 & 255u) << 8 | ((uint32_t)fy0 & 255u) << 16 | (uint32_t)fy1 << 24;
+    quad(fx0 >> 8, fy0 >> 8, t.v[0], t.v[1], t.v[2], t.v[3]);
+    quad(fx1 >> 8, fy1 >> 8, t.v[4], t.v[5], t.v[6], t.v[7]);
+    return t;
+}
+
+template <int I>
+__device__ __forceinline__ void ssao_consume_pair(const TapPair& t, const SsaoPixel& px, const SsaoParams& p, float& occ) {
+#pragma clang fp contract(off)
+    const f2v kx = {kKernel.v[I][0], kKernel.v[I + 1][0]}, ky = {kKernel.v[I][1], kKernel.v[I + 1][1]},
+              kz = {kKernel.v[I][2], kKernel.v[I + 1][2]};
+    const float* ip = p.inv_proj.m;
+    const f2v wx = f2v{(float)(t.w & 255u), (float)((t.w >> 8) & 255u)} * bc2(1.0f / 256.0f);
+    const f2v wy = f2v{(float)((t.w >> 16) & 255u), (float)(t.w >> 24)} * bc2(1.0f / 256.0f);
+    const float atop = __builtin_fmaf(wx.x, t.v[1] - t.v[0], t.v[0]), abot = __builtin_fmaf(wx.x, t.v[3] - t.v[2], t.v[2]);
+    const float btop = __builtin_fmaf(wx.y, t.v[5] - t.v[4], t.v[4]), bbot = __builtin_fmaf(wx.y, t.v[7] - t.v[6], t.v[6]);
+    const f2v dd = {__builtin_fmaf(wy.x, abot - atop, atop), __builtin_fmaf(wy.y, bbot - btop, btop)};
+    const f2v vw = pfma(bc2(ip[11]), dd, bc2(ip[15]));
+    const f2v d1 = {__builtin_fmaf(dd.x, px.A1, px.B1), __builtin_fmaf(dd.y, px.A1, px.B1)};
+    const f2v q = vw * f2v{fast_rcp(fabsf(d1.x)), fast_rcp(fabsf(d1.y))};
+    const f2v rc = {__builtin_amdgcn_fmed3f(q.x, 0.0f, 1.0f), __builtin_amdgcn_fmed3f(q.y, 0.0f, 1.0f)};
+    const f2v range = rc * rc * pfma(bc2(-2.0f), rc, bc2(3.0f));   // smoothstep(0, 1, x)
+    const f2v d2 = {__builtin_fmaf(aff(px.dzr, kx.x, ky.x, kz.x), vw.x, d1.x), __builtin_fmaf(aff(px.dzr, kx.y, ky.y, kz.y), vw.y, d1.y)};
+    occ += (d2.x <= 0.0f) ? range.x : 0.0f;
+    occ += (d2.y <= 0.0f) ? range.y : 0.0f;
+}
+
+// Pair PR consumed after pair PR + 1 is issued.
+template <int PR, int TXP, int TYP, int HALO>
+__device__ __forceinline__ void ssao_pipe_step(const TapPair& cur, const SsaoPixel& px, const SsaoParams& p,
+                                               const LdsQuad<TXP, TYP, HALO>& quad, float& occ) {
+    constexpr int kPairs = SOC_SSAO_MAX_KERNEL / 2;
+    if constexpr (PR + 1 < kPairs) {
+        const TapPair nxt = ssao_issue_pair<2 * (PR + 1)>(px, p, quad);
+        ssao_consume_pair<2 * PR>(cur, px, p, occ);
+        // keeps the stages in this order: the occlusion sum of pair PR is complete here and no later pair's texel read
+        // moves above this point (without it the compiler sank every consume stage below the last issue stage: all 26
+        // taps' texels live at once, 200 VGPRs spilled)
+        asm volatile("" : "+v"(occ)::"memory");
+        ssao_pipe_step<PR + 1>(nxt, px, p, quad, occ);
+    } else {
+        ssao_consume_pair<2 * PR>(cur, px, p, occ);
+    }
+}
+
+// The LDS-tiled kernel (ssao_lds_kernel's tile, staging and per-pixel setup, EARLY = 2) with the pipelined tap loop;
+// the sparse inverse projection and the full 26-tap kernel (the host selects it only then).
+template <int TXP, int TYP, int HALO>
+__global__ __attribute__((amdgpu_flat_work_group_size(TXP * TYP, TXP * TYP)))
+__attribute__((amdgpu_waves_per_eu(TXP * TYP >= 1024 ? 8 : TXP * TYP >= 512 ? 4 : 2)))
+void ssao_pipe_kernel(DImg depth, DImg normal, DImg target, const float2* __restrict__ table, SsaoParams p) {
+    static_assert(SOC_SSAO_MAX_KERNEL % 2 == 0, "taps are paired");
+    using T = SsaoTile<TXP, TYP, HALO>;
+    __shared__ float4 tile4[T::TW * T::TH / 4];
+    int bx, by;
+    xcd_order(p.swz, bx, by);
+    const int tid = threadIdx.x;
+    const int gx0 = bx * 2 * TXP - HALO, gy0 = by * 2 * TYP - HALO;
+    const __amdgpu_buffer_rsrc_t rsrc = depth_rsrc(depth);
+    ssao_stage_tile<TXP, TYP, HALO>(tile4, rsrc, depth, gx0, gy0, tid);
+    __syncthreads();
+    const int w = tid >> 6, lane = tid & 63;
+    const int x = bx * TXP + (w % (TXP / 32)) * 32 + (lane & 31), y = by * TYP + (w / (TXP / 32)) * 2 + (lane >> 5);
+    if (x >= target.w || y >= target.h) return;
+    const SsaoPixel px = ssao_setup<true>(x, y, depth, normal, target, table, p);
+    if (px.skip) {
+        row_ptr_w<uint8_t>(target, y)[x] = 255;
+        return;
+    }
+    const LdsQuad<TXP, TYP, HALO> quad{reinterpret_cast<const float*>(tile4), gx0, gy0, GlobalQuad{rsrc, depth.pitch}};
+    float occ = 0.0f;
+    ssao_pipe_step<0>(ssao_issue_pair<0>(px, p, quad), px, p, quad, occ);
+    occ = 1.0f - occ * p.inv_ksize;
+    row_ptr_w<uint8_t>(target, y)[x] = (uint8_t)to_unorm8(occ);
+}
+
 // ssao_blur.inl:91-106: 4x4 box at offsets -2..+1 (x outer, y inner), all taps on texel centres.
 __global__ __launch_bounds__(kWorkgroup) void ssao_blur_kernel(DImg src, DImg dst) {
 #pragma clang fp contract(off)
@@ -741,7 +845,11 @@ extern "C" int soc_ssao_generation(const soc_globals* g, soc_img depth, soc_img 
         pt.swz = 1;
         const dim3 g(ceil_div(target.width, kSsaoTX), ceil_div(target.height, kSsaoTY));
         const int early = tuning_knob("SOC_SSAO_EARLY", 2);
-        if (early == 1)
+        // SOC_SSAO_PIPE (default 1): the software-pipelined tap loop (ssao_pipe_kernel; the same bits)
+        if (tuning_knob("SOC_SSAO_PIPE", 1))
+            launch("ssao_pipe_kernel", kSsaoTileLanes, ssao_pipe_kernel<kSsaoTX, kSsaoTY, kSsaoHalo>, g, kSsaoTileLanes, 0, st, dd,
+                   dn, dt, tb, pt);
+        else if (early == 1)
             launch("ssao_lds_kernel", kSsaoTileLanes,
                    ssao_lds_kernel<true, true, true, kSsaoTX, kSsaoTY, kSsaoHalo, 2, true, 1>, g, kSsaoTileLanes, 0, st, dd,
                    dn, dt, tb, pt);

@@ -33,7 +33,10 @@ def test_bench_frame_4k_vs_oracle(soc, oracle, config, sky_range):
     # stage inside Composition
     for hv in fr["history_velocity"]:
         hv.copy_(fr["velocity"])
-    r = soc.Renderer(fr, static_inputs=True, velocity_slots=True, bloom_in_composition=True)
+    # the bench's sky-lane queue for the config (bench.py --sky-lane-queue auto): low at C3, high (with the sky-bound
+    # variants: the bloom's last stage inside Composition, the clouds' doubled density grid, hoisted classification) at C2 / C4
+    r = soc.Renderer(fr, static_inputs=True, velocity_slots=True, bloom_in_composition=True,
+                     sky_lane_queue="low" if config == "c3" else "high")
     r.set_exposure_pixels(W * H, False)
     assert r.pass_names() == ["BloomDownsample - 0+1", "BloomDownsample - 2+3", "BloomUpsample - 3+2",
                               "BloomUpsample - 1+0", "SSAOGeneration", "SSAOBlur", "CloudRendering",
@@ -50,6 +53,7 @@ def test_bench_frame_4k_vs_oracle(soc, oracle, config, sky_range):
     for f in range(2):
         e0 = soc.exposure_of(fr["auto_exposure"])
         r.execute(g)
+        assert r.side_queue() == (2 if config == "c3" else 1)
         hf["emissive"][...] = gb["emissive"]          # the bench writes bloom into bloom_output (emissive kept)
         hist = oracle.frame(g, hf, ae, hist=hist)
         # where Composition computed the bloom in-kernel (a frame with a high-priority sky lane), its output
@@ -67,11 +71,11 @@ def test_bench_frame_4k_vs_oracle(soc, oracle, config, sky_range):
 def test_c3_linear_tonemap_tolerance(soc, oracle):
     """SURVEY.md §8d, "final tone-mapped linear RGB |d| <= 2e-3 for 99.9 %": the C3 bench frame with the tone map
     writing linear RGBA32F (tone_mapping.inl:145-176 before the swapchain's encode), two frames, against the oracle.
-    Asserted: the tone map given the GPU's own resolved colour and exposure within 2e-3 on every value, and the
-    end-to-end output within 2e-3 on >= 99.9 % of the pixels whose upstream inputs equal the oracle's (the AO texels and
-    clouds texels of frame_parity, dilated by the TAA footprint, over both frames). The end-to-end fraction over all
-    pixels is reported, not asserted: where SSAO's Q8 hash or a clouds texel differs by a level upstream, the difference
-    reaches the linear output."""
+    Asserted: the tone map given the GPU's own resolved colour and exposure within 2e-3 on every value, the end-to-end
+    output within 2e-3 on >= 99.9 % of ALL pixels (§8d as written; round 5 met it only on the pixels whose upstream inputs
+    equal the oracle's: 99.47 % over all, every miss a sky pixel whose clouds texel was a level off; round 6's noise hash
+    and clouds chain follow the oracle's roundings), and on >= 99.9 % of the pixels whose upstream inputs equal the
+    oracle's (the AO texels and clouds texels of frame_parity, dilated by the TAA footprint, over both frames)."""
     import bench
     from helpers import PARITY_REPORTS
     W, H = 3840, 2160
@@ -119,5 +123,6 @@ def test_c3_linear_tonemap_tolerance(soc, oracle):
         assert np.isfinite(out).all()
         assert rep["cond_max"] <= 2e-3, rep
         assert rep["e2e_within_2e-3_where_upstream_equal"] >= 0.999, rep
+        assert rep["e2e_within_2e-3"] >= 0.999, rep
         assert rep["exposure_delta"] <= 1e-5, rep
     r.close()

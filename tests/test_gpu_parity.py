@@ -173,8 +173,9 @@ def test_ssao_noise_table_is_bit_identical(soc):
 @pytest.mark.parametrize("W,H,inputs", [(97, 55, "boxes"), (1920, 1080, "boxes"), (1920, 1080, "mesh"), (3840, 2160, "mesh"),
                                          (130, 1200, "boxes"), (2000, 34, "boxes")])
 def test_ssao_tile_orders_bit_identical(soc, monkeypatch, W, H, inputs):
-    """The LDS-tiled kernel (default: depth tile + 32-texel halo in LDS, the other taps gathered) and the plain gather
-    kernel (SOC_SSAO_TILE=0) give the same bits (the tiled kernel with its per-pixel fetches issued before the barrier
+    """The LDS-tiled kernel (default: depth tile + 32-texel halo in LDS, the other taps gathered, the software-pipelined
+    tap loop, SOC_SSAO_PIPE=1) and the plain gather kernel (SOC_SSAO_TILE=0) give the same bits (the round-5 tap loop,
+    SOC_SSAO_PIPE=0, with its per-pixel fetches issued before the barrier
     and the centre depth from the tile, SOC_SSAO_EARLY=1; its staging loads all issued first, 2, the default; neither, 0), in every workgroup order of the gather kernel (row-major, XCD-aware
     eighths, horizontal and vertical XCD bands: SOC_SWZ_SSAO; the orders are bijections, also for ragged grids), on the
     box atrium and on the mesh (near geometry: many taps leave the tile), at odd, tall and wide extents (partial tiles,
@@ -191,10 +192,12 @@ def test_ssao_tile_orders_bit_identical(soc, monkeypatch, W, H, inputs):
         depth, normal = dev(gb["depth"]), dev(gb["normal"])
     table = torch.zeros((H // 2) * (W // 2) * 2, dtype=torch.float32, device=DEV)
     outs = []
-    for tile, swz, early in (("1", None, "1"), ("1", None, "0"), ("1", None, "2"), ("0", "0", "1"), ("0", "1", "1"),
-                             ("0", "4", "1"), ("0", "16", "1"), ("0", "-16", "1"), ("0", "-3", "1")):
+    for tile, swz, early, pipe in (("1", None, "2", "1"), ("1", None, "1", "0"), ("1", None, "0", "0"), ("1", None, "2", "0"),
+                                   ("0", "0", "1", "0"), ("0", "1", "1", "0"), ("0", "4", "1", "0"), ("0", "16", "1", "0"),
+                                   ("0", "-16", "1", "0"), ("0", "-3", "1", "0")):
         monkeypatch.setenv("SOC_SSAO_TILE", tile)
         monkeypatch.setenv("SOC_SSAO_EARLY", early)
+        monkeypatch.setenv("SOC_SSAO_PIPE", pipe)
         if swz is None:
             monkeypatch.delenv("SOC_SWZ_SSAO", raising=False)
         else:
@@ -206,6 +209,7 @@ def test_ssao_tile_orders_bit_identical(soc, monkeypatch, W, H, inputs):
         outs.append(host(out))
     monkeypatch.delenv("SOC_SSAO_TILE")
     monkeypatch.delenv("SOC_SSAO_EARLY")
+    monkeypatch.delenv("SOC_SSAO_PIPE")
     monkeypatch.delenv("SOC_SWZ_SSAO", raising=False)
     soc.reload_tuning()
     for o in outs[1:]:
@@ -1132,6 +1136,31 @@ def test_sky_lane_queue_probe_bit_identical(soc, monkeypatch, inputs):
     for o in outs[1:]:
         for f, (a, b) in enumerate(zip(outs[0], o)):
             assert torch.equal(a, b), f
+
+
+def test_sky_lane_queue_flags(soc):
+    """The sky lane's queue is fixed by the renderer flags (round 6, VERDICT r5 #2: the same kernels every run): low
+    priority by default, high with sky_lane_queue="high" (SOC_RENDERER_SKY_LANE_HIGH), the timed probe only with
+    "probe" (undecided after one frame); no tuning knob set. The frames have the same bits in every mode."""
+    W, H = 640, 360
+    g, gb = terrain_inputs(W, H, elapsed=10.0)
+    outs = []
+    for q, want in (("low", 2), ("high", 1), ("probe", -1)):
+        fr = soc.alloc_frame(W, H, DEV, bloom_output=True)
+        for k in ("albedo", "emissive", "normal", "velocity", "depth"):
+            fr[k].copy_(torch.from_numpy(gb[k]))
+        fr["shadow"] = dev(gb["shadow"])
+        fr["noise"].copy_(torch.from_numpy(gb["noise"]))
+        r = soc.Renderer(fr, static_inputs=True, sky_lane_queue=q)
+        r.execute(g)
+        torch.cuda.synchronize()
+        assert r.side_queue() == want, (q, r.side_queue())
+        outs.append(fr["output"].clone())
+        r.close()
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+    with pytest.raises(ValueError):
+        soc.Renderer(fr, sky_lane_queue="fast")
 
 
 def test_static_inputs_first_call_after_async_input_write(soc):

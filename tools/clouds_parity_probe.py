@@ -35,7 +35,9 @@ def compare(gpu, ref, sky):
     s = a[sky]
     return {"sky_px": int(sky.sum()), "differ": round(float((s > 0).mean()), 6), "differ2": round(float((s > 1).mean()), 6),
             "max": int(a.max()), "mean_signed": [round(float(d[..., c][sky].mean()), 5) for c in range(3)],
-            "nonsky_differ": int((a[~sky] > 0).sum())}
+            "nonsky_differ": int((a[~sky] > 0).sum()),
+            "worst": [[int(y), int(x), int(a[y, x]), gpu[y, x, :3].tolist(), ref[y, x, :3].tolist()]
+                      for y, x in zip(*np.unravel_index(np.argsort(a, axis=None)[::-1][:6], a.shape)) if a[y, x] > 1]}
 
 
 def main():
