@@ -47,17 +47,18 @@ int check_img(const soc_img& im, int fmt, const char* pass, const char* what) {
 // soc_tuning_reload() drops the cache so a changed environment takes effect.
 namespace {
 std::mutex g_knob_mu;
-std::vector<std::pair<std::string, int>> g_knobs;
+// the environment's value of each knob read so far: (name, (set, value)); a knob that is not set returns the caller's
+// default on every call (the default may differ between callers, e.g. per renderer flags)
+std::vector<std::pair<std::string, std::pair<bool, int>>> g_knobs;
 }  // namespace
 
 int tuning_knob(const char* name, int dflt) {
     std::lock_guard<std::mutex> lock(g_knob_mu);
     for (const auto& k : g_knobs)
-        if (k.first == name) return k.second;
+        if (k.first == name) return k.second.first ? k.second.second : dflt;
     const char* e = getenv(name);
-    const int v = e ? atoi(e) : dflt;
-    g_knobs.emplace_back(name, v);
-    return v;
+    g_knobs.emplace_back(name, std::make_pair(e != nullptr, e ? atoi(e) : 0));
+    return e ? atoi(e) : dflt;
 }
 
 namespace {

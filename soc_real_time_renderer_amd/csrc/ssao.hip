@@ -644,10 +644,11 @@ void ssao_lds_kernel(DImg depth, DImg normal, DImg target, const float2* __restr
 // overlaps the previous pair's arithmetic. Per tap the same operations in the same order as the PK loop: the same bits.
 struct TapPair {
     float v[8];   // tap 0: t0 t1 b0 b1, tap 1: t0 t1 b0 b1
-    uint32_t w;   // sub-texel weights: bytes wx0, wx1, wy0, wy1
+    int f[4];     // fixed-point coordinates fx0, fx1, fy0, fy1 (their low bytes: the sub-texel weights)
+    float w0, w1; // PERSP: the taps' w' (= -s.z), for the range test's sample depth
 };
 
-template <int I, int TXP, int TYP, int HALO>
+template <int I, bool PERSP, int TXP, int TYP, int HALO>
 __device__ __forceinline__ TapPair ssao_issue_pair(const SsaoPixel& px, const SsaoParams& p, const LdsQuad<TXP, TYP, HALO>& quad) {
 #pragma clang fp contract(off)
     const f2v kx = {kKernel.v[I][0], kKernel.v[I + 1][0]}, ky = {kKernel.v[I][1], kKernel.v[I + 1][1]},
@@ -661,20 +662,27 @@ __device__ __forceinline__ TapPair ssao_issue_pair(const SsaoPixel& px, const Ss
     const int fx0 = (int)__builtin_amdgcn_fmed3f(X.x, 0.5f, p.tmx), fx1 = (int)__builtin_amdgcn_fmed3f(X.y, 0.5f, p.tmx);
     const int fy0 = (int)__builtin_amdgcn_fmed3f(Y.x, 0.5f, p.tmy), fy1 = (int)__builtin_amdgcn_fmed3f(Y.y, 0.5f, p.tmy);
     TapPair t;
-    t.w = ((uint32_t)fx0 & 255u) | ((uint32_t)fx1 & 255u) << 8 | ((uint32_t)fy0 & 255u) << 16 | (uint32_t)fy1 << 24;
+    t.f[0] = fx0;
+    t.f[1] = fx1;
+    t.f[2] = fy0;
+    t.f[3] = fy1;
+    if (PERSP) {
+        t.w0 = ww.x;
+        t.w1 = ww.y;
+    }
     quad(fx0 >> 8, fy0 >> 8, t.v[0], t.v[1], t.v[2], t.v[3]);
     quad(fx1 >> 8, fy1 >> 8, t.v[4], t.v[5], t.v[6], t.v[7]);
     return t;
 }
 
-template <int I>
+template <int I, bool PERSP>
 __device__ __forceinline__ void ssao_consume_pair(const TapPair& t, const SsaoPixel& px, const SsaoParams& p, float& occ) {
 #pragma clang fp contract(off)
     const f2v kx = {kKernel.v[I][0], kKernel.v[I + 1][0]}, ky = {kKernel.v[I][1], kKernel.v[I + 1][1]},
               kz = {kKernel.v[I][2], kKernel.v[I + 1][2]};
     const float* ip = p.inv_proj.m;
-    const f2v wx = f2v{(float)(t.w & 255u), (float)((t.w >> 8) & 255u)} * bc2(1.0f / 256.0f);
-    const f2v wy = f2v{(float)((t.w >> 16) & 255u), (float)(t.w >> 24)} * bc2(1.0f / 256.0f);
+    const f2v wx = f2v{(float)(t.f[0] & 255), (float)(t.f[1] & 255)} * bc2(1.0f / 256.0f);
+    const f2v wy = f2v{(float)(t.f[2] & 255), (float)(t.f[3] & 255)} * bc2(1.0f / 256.0f);
     const float atop = __builtin_fmaf(wx.x, t.v[1] - t.v[0], t.v[0]), abot = __builtin_fmaf(wx.x, t.v[3] - t.v[2], t.v[2]);
     const float btop = __builtin_fmaf(wx.y, t.v[5] - t.v[4], t.v[4]), bbot = __builtin_fmaf(wx.y, t.v[7] - t.v[6], t.v[6]);
     const f2v dd = {__builtin_fmaf(wy.x, abot - atop, atop), __builtin_fmaf(wy.y, bbot - btop, btop)};
@@ -683,32 +691,36 @@ __device__ __forceinline__ void ssao_consume_pair(const TapPair& t, const SsaoPi
     const f2v q = vw * f2v{fast_rcp(fabsf(d1.x)), fast_rcp(fabsf(d1.y))};
     const f2v rc = {__builtin_amdgcn_fmed3f(q.x, 0.0f, 1.0f), __builtin_amdgcn_fmed3f(q.y, 0.0f, 1.0f)};
     const f2v range = rc * rc * pfma(bc2(-2.0f), rc, bc2(3.0f));   // smoothstep(0, 1, x)
-    const f2v d2 = {__builtin_fmaf(aff(px.dzr, kx.x, ky.x, kz.x), vw.x, d1.x), __builtin_fmaf(aff(px.dzr, kx.y, ky.y, kz.y), vw.y, d1.y)};
+    // (s.z + bias - frag.z) / r: the affine form, or PERSP (the projection's w row is (0, 0, -1, 0): w' = -s.z) one fma
+    // from the tap's w' (within the SSAO tolerance: w' carries its own rounding)
+    const float z0 = PERSP ? __builtin_fmaf(t.w0, -p.inv_radius, px.dzr.a0) : aff(px.dzr, kx.x, ky.x, kz.x);
+    const float z1 = PERSP ? __builtin_fmaf(t.w1, -p.inv_radius, px.dzr.a0) : aff(px.dzr, kx.y, ky.y, kz.y);
+    const f2v d2 = {__builtin_fmaf(z0, vw.x, d1.x), __builtin_fmaf(z1, vw.y, d1.y)};
     occ += (d2.x <= 0.0f) ? range.x : 0.0f;
     occ += (d2.y <= 0.0f) ? range.y : 0.0f;
 }
 
 // Pair PR consumed after pair PR + 1 is issued.
-template <int PR, int TXP, int TYP, int HALO>
+template <int PR, bool PERSP, int TXP, int TYP, int HALO>
 __device__ __forceinline__ void ssao_pipe_step(const TapPair& cur, const SsaoPixel& px, const SsaoParams& p,
                                                const LdsQuad<TXP, TYP, HALO>& quad, float& occ) {
     constexpr int kPairs = SOC_SSAO_MAX_KERNEL / 2;
     if constexpr (PR + 1 < kPairs) {
-        const TapPair nxt = ssao_issue_pair<2 * (PR + 1)>(px, p, quad);
-        ssao_consume_pair<2 * PR>(cur, px, p, occ);
+        const TapPair nxt = ssao_issue_pair<2 * (PR + 1), PERSP>(px, p, quad);
+        ssao_consume_pair<2 * PR, PERSP>(cur, px, p, occ);
         // keeps the stages in this order: the occlusion sum of pair PR is complete here and no later pair's texel read
         // moves above this point (without it the compiler sank every consume stage below the last issue stage: all 26
         // taps' texels live at once, 200 VGPRs spilled)
         asm volatile("" : "+v"(occ)::"memory");
-        ssao_pipe_step<PR + 1>(nxt, px, p, quad, occ);
+        ssao_pipe_step<PR + 1, PERSP>(nxt, px, p, quad, occ);
     } else {
-        ssao_consume_pair<2 * PR>(cur, px, p, occ);
+        ssao_consume_pair<2 * PR, PERSP>(cur, px, p, occ);
     }
 }
 
 // The LDS-tiled kernel (ssao_lds_kernel's tile, staging and per-pixel setup, EARLY = 2) with the pipelined tap loop;
 // the sparse inverse projection and the full 26-tap kernel (the host selects it only then).
-template <int TXP, int TYP, int HALO>
+template <int TXP, int TYP, int HALO, bool PERSP>
 __global__ __attribute__((amdgpu_flat_work_group_size(TXP * TYP, TXP * TYP)))
 __attribute__((amdgpu_waves_per_eu(TXP * TYP >= 1024 ? 8 : TXP * TYP >= 512 ? 4 : 2)))
 void ssao_pipe_kernel(DImg depth, DImg normal, DImg target, const float2* __restrict__ table, SsaoParams p) {
@@ -732,7 +744,9 @@ void ssao_pipe_kernel(DImg depth, DImg normal, DImg target, const float2* __rest
     }
     const LdsQuad<TXP, TYP, HALO> quad{reinterpret_cast<const float*>(tile4), gx0, gy0, GlobalQuad{rsrc, depth.pitch}};
     float occ = 0.0f;
-    ssao_pipe_step<0>(ssao_issue_pair<0>(px, p, quad), px, p, quad, occ);
+    SsaoPixel pxp = px;
+    if (PERSP) pxp.dzr.a0 = (p.bias - px.frag.z) * p.inv_radius;
+    ssao_pipe_step<0, PERSP>(ssao_issue_pair<0, PERSP>(pxp, p, quad), pxp, p, quad, occ);
     occ = 1.0f - occ * p.inv_ksize;
     row_ptr_w<uint8_t>(target, y)[x] = (uint8_t)to_unorm8(occ);
 }
@@ -846,9 +860,17 @@ extern "C" int soc_ssao_generation(const soc_globals* g, soc_img depth, soc_img 
         const dim3 g(ceil_div(target.width, kSsaoTX), ceil_div(target.height, kSsaoTY));
         const int early = tuning_knob("SOC_SSAO_EARLY", 2);
         // SOC_SSAO_PIPE (default 1): the software-pipelined tap loop (ssao_pipe_kernel; the same bits)
-        if (tuning_knob("SOC_SSAO_PIPE", 1))
-            launch("ssao_pipe_kernel", kSsaoTileLanes, ssao_pipe_kernel<kSsaoTX, kSsaoTY, kSsaoHalo>, g, kSsaoTileLanes, 0, st, dd,
-                   dn, dt, tb, pt);
+        // the projection's w row (0, 0, -1, 0) (the reference's perspective; jitter moves only the x / y rows): the
+        // range test's sample depth from the tap's w' (PERSP); SOC_SSAO_PIPE=2 forces the affine form
+        const float* P = pt.proj.m;
+        const int pipe = tuning_knob("SOC_SSAO_PIPE", 1);
+        const bool persp = pipe == 1 && P[3] == 0.0f && P[7] == 0.0f && P[11] == -1.0f && P[15] == 0.0f;
+        if (pipe && persp)
+            launch("ssao_pipe_kernel", kSsaoTileLanes, ssao_pipe_kernel<kSsaoTX, kSsaoTY, kSsaoHalo, true>, g, kSsaoTileLanes, 0, st,
+                   dd, dn, dt, tb, pt);
+        else if (pipe)
+            launch("ssao_pipe_kernel", kSsaoTileLanes, ssao_pipe_kernel<kSsaoTX, kSsaoTY, kSsaoHalo, false>, g, kSsaoTileLanes, 0, st,
+                   dd, dn, dt, tb, pt);
         else if (early == 1)
             launch("ssao_lds_kernel", kSsaoTileLanes,
                    ssao_lds_kernel<true, true, true, kSsaoTX, kSsaoTY, kSsaoHalo, 2, true, 1>, g, kSsaoTileLanes, 0, st, dd,

@@ -201,18 +201,6 @@ __device__ __forceinline__ void taa_pair_tail(const DImg& target, const DImg& pr
                                               const float (&D)[3][4], float exposure, const VelAt& vel_at,
                                               const OwnVel& own_vel, const Hist& hist) {
     const int W = target.w, H = target.h;
-    // column min / max (packed f16) and Gaussian column sums (fp32)
-    h2 nxy[4], nzw[4], xxy[4], xzw[4];
-    v2f sxy[4], szw[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        nxy[c] = __builtin_elementwise_min(__builtin_elementwise_min(Cxy[0][c], Cxy[1][c]), Cxy[2][c]);
-        nzw[c] = __builtin_elementwise_min(__builtin_elementwise_min(Czw[0][c], Czw[1][c]), Czw[2][c]);
-        xxy[c] = __builtin_elementwise_max(__builtin_elementwise_max(Cxy[0][c], Cxy[1][c]), Cxy[2][c]);
-        xzw[c] = __builtin_elementwise_max(__builtin_elementwise_max(Czw[0][c], Czw[1][c]), Czw[2][c]);
-        sxy[c] = gauss_col(Cxy[0][c], Cxy[1][c], Cxy[2][c]);
-        szw[c] = gauss_col(Czw[0][c], Czw[1][c], Czw[2][c]);
-    }
     const int colx[4] = {xl, x0, x0 + 1, xr};
     const float v = centre_uv_rn(y, H, p.rh);
     uint2 outp[2];
@@ -256,6 +244,20 @@ __device__ __forceinline__ void taa_pair_tail(const DImg& target, const DImg& pr
             hist(k, 0, hax_[k], hay_[k], ch0[k], ch1[k]);
             hist(k, 1, hax_[k], hay_[k], vh0[k], vh1[k]);
         }
+    }
+    // column min / max (packed f16) and Gaussian column sums (fp32), while the history loads are in flight (round 6:
+    // they depend on the closest-depth velocity, so issuing them first leaves this arithmetic to cover their latency;
+    // the same operations)
+    h2 nxy[4], nzw[4], xxy[4], xzw[4];
+    v2f sxy[4], szw[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        nxy[c] = __builtin_elementwise_min(__builtin_elementwise_min(Cxy[0][c], Cxy[1][c]), Cxy[2][c]);
+        nzw[c] = __builtin_elementwise_min(__builtin_elementwise_min(Czw[0][c], Czw[1][c]), Czw[2][c]);
+        xxy[c] = __builtin_elementwise_max(__builtin_elementwise_max(Cxy[0][c], Cxy[1][c]), Cxy[2][c]);
+        xzw[c] = __builtin_elementwise_max(__builtin_elementwise_max(Czw[0][c], Czw[1][c]), Czw[2][c]);
+        sxy[c] = gauss_col(Cxy[0][c], Cxy[1][c], Cxy[2][c]);
+        szw[c] = gauss_col(Czw[0][c], Czw[1][c], Czw[2][c]);
     }
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
