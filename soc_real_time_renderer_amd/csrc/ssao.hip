@@ -512,6 +512,11 @@ struct SsaoTile {
     static constexpr int TW = 2 * TXP + 2 * HALO, TH = 2 * TYP + 2 * HALO, THREADS = TXP * TYP;
 };
 
+// Profiling builds only (SOC_SSAO_PROBE, wrong results): 1 = every tap from the LDS tile (out-of-tile lanes read texel 0),
+// 2 = no texel reads at all (constant texels). The library is built with 0.
+#ifndef SOC_SSAO_PROBE
+#define SOC_SSAO_PROBE 0
+#endif
 template <int TXP, int TYP, int HALO>
 struct LdsQuad {
     const float* tile;
@@ -519,11 +524,16 @@ struct LdsQuad {
     GlobalQuad g;
     __device__ __forceinline__ void operator()(int x0, int y0, float& t0, float& t1, float& b0, float& b1) const {
         constexpr int TW = SsaoTile<TXP, TYP, HALO>::TW, TH = SsaoTile<TXP, TYP, HALO>::TH;
+        if (SOC_SSAO_PROBE == 2) {
+            t0 = t1 = b0 = b1 = __int_as_float(0x3f7f0000 | (x0 & 255) | (y0 & 255) << 8);
+            return;
+        }
         const int lx = x0 - gx0, ly = y0 - gy0;
-        const bool in = (unsigned)lx < (unsigned)(TW - 1) && (unsigned)ly < (unsigned)(TH - 1);
+        const bool in = SOC_SSAO_PROBE == 1 || ((unsigned)lx < (unsigned)(TW - 1) && (unsigned)ly < (unsigned)(TH - 1));
         // ly * TW + lx as one full-rate v_mad_u32_u24 (the compiler otherwise selects v_mad_u64_u32 for it)
         uint32_t i;
         asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(i) : "v"(ly), "s"((uint32_t)TW), "v"(lx));
+        if (SOC_SSAO_PROBE == 1) i = i % (uint32_t)(TW * (TH - 1) - 1);
         i = in ? i : 0u;
         t0 = tile[i];
         t1 = tile[i + 1];

@@ -5,6 +5,8 @@ Tolerances: bloom, SSAO blur and the histogram are bit-exact; RG
 exposure |d| <= 1e-5; tone-mapped RGBA8 within 1 level on >= 99.9 %; clouds RGBA8 within 2 levels on
 >= 99.5 %.
 """
+import ctypes as C
+
 import numpy as np
 import pytest
 import torch
@@ -1092,6 +1094,37 @@ def test_bloom_in_composition_bit_identical(soc, monkeypatch, inputs, lights):
     for a, b in zip(*outs):
         for k in a:
             assert torch.equal(a[k], b[k]), k
+
+
+def test_bloom_in_composition_generic_resolution_frame(soc):
+    """the in-Composition bloom stage is decided per frame. A frame whose globals resolution differs from the
+    image extent takes Composition's generic path, which cannot compute the bloom, so the chain's fourth pass must run:
+    with the sky split off, a high-priority sky lane and bloom_in_composition, such a frame executes (round 5 skipped the
+    fourth pass and Composition then returned SOC_E_SHAPE) and writes the bloom output, and a matching frame after it
+    computes the bloom in Composition again (the bloom output untouched)."""
+    W, H = 640, 360
+    g, gb = sponza_inputs(W, H, elapsed=10.0)
+    fr = soc.alloc_frame(W, H, DEV, bloom_output=True)
+    for k in ("albedo", "emissive", "normal", "velocity", "depth"):
+        fr[k].copy_(torch.from_numpy(gb[k]))
+    fr["shadow"] = dev(gb["shadow"])
+    fr["noise"].copy_(torch.from_numpy(gb["noise"]))
+    r = soc.Renderer(fr, static_inputs=True, sky_split=False, bloom_in_composition=True, sky_lane_queue="high")
+    r.execute(g)                                   # the lane takes its queue in the first call
+    torch.cuda.synchronize()
+    assert r.side_queue() == 1
+    g_generic = type(g)()
+    C.pointer(g_generic)[0] = g
+    g_generic.resolution[0] = W - 2                # the generic composition path
+    fr["bloom_output"].fill_(7.0)
+    r.execute(g_generic)
+    torch.cuda.synchronize()
+    assert not bool((fr["bloom_output"] == 7.0).all())   # the fourth pass ran
+    fr["bloom_output"].fill_(7.0)
+    r.execute(g)
+    torch.cuda.synchronize()
+    assert bool((fr["bloom_output"] == 7.0).all())       # in Composition again
+    r.close()
 
 
 @pytest.mark.parametrize("inputs", ["sponza", "terrain"])
