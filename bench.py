@@ -56,7 +56,7 @@ from soc_real_time_renderer_amd import multi_gpu, raster, scene  # noqa: E402
 from soc_real_time_renderer_amd.scene import sponza_mesh  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
-SSAO_KERNEL = "ssao_lds_kernel<true, true, true, 64, 16, 32, 2, true, 2>"   # the default SSAOGeneration kernel (ssao.hip)
+SSAO_KERNEL = "ssao_pipe_kernel<64, 16, 32, true>"   # the default SSAOGeneration kernel (ssao.hip)
 
 
 def make_globals(W, H, camera):
@@ -552,6 +552,7 @@ def main():
                                f"{' with 128 point lights' if args.config == 'c3b' else ''}, auto-exposure, "
                                f"TAA, AgX tone map",
                    "resolution": [W, H], "f_sky": round(f_sky, 4), "parallelism": f"frame-per-gpu x{world}",
+                   "profile_frames": args.profile_frames,
                    "histogram_allreduce": exchange,
                    "collective_backend": (dist.get_backend() if exchange else None),
                    "sky_lane": ("CloudRendering + SkyCompose on a concurrent stream; " +

@@ -22,7 +22,9 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-KERNELS = {"SSAOGeneration": "ssao_lds_kernel", "Composition+GenerateLuminanceHistogram": "composition_pair<true"}
+KERNELS = {"SSAOGeneration": "ssao_pipe_kernel", "Composition+GenerateLuminanceHistogram": "composition_pair<true"}
+# round 5's SSAO kernel (SOC_SSAO_PIPE=0): traces of that build
+KERNELS_R5 = {"SSAOGeneration": "ssao_lds_kernel"}
 
 
 def run(out, frames, warmup):
@@ -73,7 +75,10 @@ def compare(events_json, trace_csv):
     for name, key in KERNELS.items():
         e = ev["passes"][name]
         e0, e1 = np.array(e["start_ms"]) * 1e6, np.array(e["end_ms"]) * 1e6   # ns after the base event
-        tl = trace_launches(trace_csv, key)[ev["warmup"]:ev["warmup"] + n]
+        tl = trace_launches(trace_csv, key)
+        if len(tl) == 0 and name in KERNELS_R5:
+            tl = trace_launches(trace_csv, KERNELS_R5[name])
+        tl = tl[ev["warmup"]:ev["warmup"] + n]
         tb, te = tl[:, 0], tl[:, 1]
         offs[name] = float(np.median(te - e1))    # trace clock = event clock + offset, if end events mark kernel ends
         out["kernels"][name] = {"event_us": float((e1 - e0).mean() / 1e3), "trace_us": float((te - tb).mean() / 1e3),

@@ -17,7 +17,9 @@ import json
 import os
 import sys
 
-KERNELS = {"SSAOGeneration": "ssao_lds_kernel", "Composition+GenerateLuminanceHistogram": "composition_pair<true"}
+KERNELS = {"SSAOGeneration": "ssao_pipe_kernel", "Composition+GenerateLuminanceHistogram": "composition_pair<true"}
+# round 5's SSAO kernel (SOC_SSAO_PIPE=0): traces of that build
+KERNELS_R5 = {"SSAOGeneration": "ssao_lds_kernel"}
 
 
 def main():
@@ -43,10 +45,15 @@ def main():
     out = {"bench_line": bench_json, "kernel_trace": trace, "warmup": warmup, "untimed_lane_probe_frames": probe,
            "timed": steps, "kernels": {}}
     pair_events = pair_rocprof = 0.0
+    # the serial per-pass profile frames follow the timed ones; after them (round 6) the unfused renderer's frames of
+    # ms_per_group_unfused, which run the same SSAO kernel: excluded
+    profile = int(line.get("config", {}).get("profile_frames") or 20)
     for name, key in KERNELS.items():
         d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows if key in r["Kernel_Name"]]
+        if not d and name in KERNELS_R5:
+            d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows if KERNELS_R5[name] in r["Kernel_Name"]]
         timed = d[warmup:warmup + steps]
-        prof = d[warmup + steps:]
+        prof = d[warmup + steps:warmup + steps + profile]
         pk = line["roofline"]["per_kernel"][name]
         ev = pk["avg_launch_us"]                      # alone
         ev_frame = (pk.get("in_frame") or {}).get("avg_launch_us")
