@@ -15,6 +15,10 @@
 // Profiling builds only (tools/kernel_variants.py): 1 = atmosphere only, 2 = cloud march only,
 // 3 = cloud march without the sun-visibility march, 4 = classify only, 5 = classify only without the
 // list atomic. The library is always built with 0.
+// SOC_CLOUDS_EXITS (profiling only; 1 = the product): 0 evaluates every octave, 2 stops after the second (wrong results)
+#ifndef SOC_CLOUDS_EXITS
+#define SOC_CLOUDS_EXITS 1
+#endif
 #ifndef SOC_CLOUDS_PROFILE
 #define SOC_CLOUDS_PROFILE 0
 #endif
@@ -272,15 +276,33 @@ __device__ float clouds_at(const C& cx, f3 p, float h) {
     p = f3{p.x + cx.cam_x, h, p.z + cx.cam_z};
     const f3 mv = f3{cx.time, 0.0f, cx.time};
     const bool ex = SOC_CLOUDS_EXACT != 0;
-    const f3 cc = ex ? madd_rn(p, 0.001f, mv) : p * 0.001f + mv;
+    // mv.y == 0: the y terms' "+ 0" / "- 0" are dropped (they only map -0 to +0, and cc.y = 0.001 h > 0 for every caller,
+    // which passes an h inside the layer), so cc.y and its multiples are the same bits without the three adds
+    f3 cc;
+    if (ex) {
+        cc = madd_rn(p, 0.001f, mv);
+        cc.y = p.y * 0.001f;
+    } else {
+        cc = p * 0.001f + mv;
+    }
     // octave weight x noise normalisation as one constant per octave (powers of two apart: one fma per octave)
     float n = noise3(cx, cc) * (0.5f * kNoiseNorm);
-    n = __builtin_fmaf(noise3(cx, cc * 2.0f + mv), 0.25f * kNoiseNorm, n);   // 2 cc exact: one fma is the same sum
-    if (n < 0.55f - 0.1875f - 1e-4f) return 0.0f;
-    n = __builtin_fmaf(noise3(cx, ex ? msub_rn(cc, 7.0f, mv) : cc * 7.0f - mv), 0.125f * kNoiseNorm, n);
-    if (n < 0.55f - 0.0625f - 1e-4f) return 0.0f;
+    f3 c2 = cc * 2.0f + mv;   // 2 cc exact: one fma is the same sum
+    if (ex) c2.y = cc.y * 2.0f;
+    n = __builtin_fmaf(noise3(cx, c2), 0.25f * kNoiseNorm, n);
+    if (SOC_CLOUDS_EXITS == 2) return n;   // profiling only (wrong results): never the last two octaves
+    if (SOC_CLOUDS_EXITS != 0 && n < 0.55f - 0.1875f - 1e-4f) return 0.0f;
+    f3 c3;
+    if (ex) {
+        c3 = msub_rn(cc, 7.0f, mv);
+        c3.y = cc.y * 7.0f;
+    } else {
+        c3 = cc * 7.0f - mv;
+    }
+    n = __builtin_fmaf(noise3(cx, c3), 0.125f * kNoiseNorm, n);
+    if (SOC_CLOUDS_EXITS != 0 && n < 0.55f - 0.0625f - 1e-4f) return 0.0f;
     // (cc + mv) 16 == fma(cc, 16, 16 mv) exactly: scaling by a power of two commutes with the rounding
-    const f3 c4 = f3{__builtin_fmaf(cc.x, 16.0f, mv.x * 16.0f), __builtin_fmaf(cc.y, 16.0f, mv.y * 16.0f),
+    const f3 c4 = f3{__builtin_fmaf(cc.x, 16.0f, mv.x * 16.0f), ex ? cc.y * 16.0f : __builtin_fmaf(cc.y, 16.0f, mv.y * 16.0f),
                      __builtin_fmaf(cc.z, 16.0f, mv.z * 16.0f)};
     n = __builtin_fmaf(noise3(cx, c4), 0.0625f * kNoiseNorm, n);
     const float hh = p.y - kMinH;
@@ -1457,11 +1479,12 @@ int soc::cloud_rendering_launch(const soc_globals* g, soc_img depth, soc_img noi
                kWorkgroup, 0, s, dimg(depth), dimg(target), p, vec_store, counter, list);
     // One resident wave set per kernel, grid-stride over the list / pairs: the long per-item work is
     // balanced over all SIMDs instead of running as a second, partially filled round.
-    static int res_atmos = 0, res_density = 0, res_sunvis = 0, res_resolve = 0;
+    static int res_atmos = 0, res_density = 0, res_sunvis = 0, res_sunvis_n = 0, res_resolve = 0;
     if (!res_atmos) {
         res_atmos = resident_blocks(clouds_atmosphere<false>);
         res_density = resident_blocks(clouds_density<false>);
         res_sunvis = resident_blocks(clouds_sunvis<false, kSunvisLanes, true>, kSunvisLanes);
+        res_sunvis_n = resident_blocks(clouds_sunvis<false, kSunvisLanes, false, true>, kSunvisLanes);
         res_resolve = resident_blocks(clouds_resolve<false, true>);
     }
     const long long blocks = ((long long)W * H + 255) / 256;
@@ -1532,6 +1555,9 @@ int soc::cloud_rendering_launch(const soc_globals* g, soc_img depth, soc_img noi
     const int db = tuning_knob("SOC_CLOUDS_DENSITY_BATCH", 8);
     // the sun-visibility kernel's next pair word loaded one iteration ahead
     const bool sv_pf = tuning_knob("SOC_CLOUDS_SUNVIS_PF", 1) != 0;
+    // the sun-visibility kernel's noise table: 16-bit pairs (52 KiB of LDS per 512-lane workgroup, two byte permutes fewer
+    // per bilinear tap; r2.9) or the byte quads (26 KiB: more LDS left on the CU for the main lane's workgroups)
+    const bool sv_wide = tuning_knob("SOC_CLOUDS_SUNVIS_WIDE", 1) != 0;
     // one od scratch per workgroup; SOC_CLOUDS_DENSITY_MULT: the grid as this many times the resident set (as gmul).
     // Default 1: 2 measured C3 1710 -> 1697 fps, C4 1321 -> 1358 (profiles/r05_ab_clouds_density_mult.txt)
     const int dmul = sky_bound ? 2 : std::max(1, tuning_knob("SOC_CLOUDS_DENSITY_MULT", 1));
@@ -1542,7 +1568,9 @@ int soc::cloud_rendering_launch(const soc_globals* g, soc_img depth, soc_img noi
         else if (db == 8) launch("clouds_density", kWorkgroup, clouds_density<true, 8>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
         else launch("clouds_density", kWorkgroup, clouds_density<true>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
         if (apos == 1) atmos();
-        if (sv_pf)
+        if (!sv_wide)
+            launch("clouds_sunvis", kSunvisLanes, clouds_sunvis<true, kSunvisLanes, false, true>, grid_m(res_sunvis_n, blocks), kSunvisLanes, 0, s, nz, p, list, ws.pb);
+        else if (sv_pf)
             launch("clouds_sunvis", kSunvisLanes, clouds_sunvis<true, kSunvisLanes, true, true>, grid_m(res_sunvis, blocks), kSunvisLanes, 0, s, nz, p, list, ws.pb);
         else
             launch("clouds_sunvis", kSunvisLanes, clouds_sunvis<true, kSunvisLanes, true>, grid_m(res_sunvis, blocks), kSunvisLanes, 0, s, nz, p, list, ws.pb);
@@ -1556,7 +1584,9 @@ int soc::cloud_rendering_launch(const soc_globals* g, soc_img depth, soc_img noi
         else if (db == 8) launch("clouds_density", kWorkgroup, clouds_density<false, 8>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
         else launch("clouds_density", kWorkgroup, clouds_density<false>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
         if (apos == 1) atmos();
-        if (sv_pf)
+        if (!sv_wide)
+            launch("clouds_sunvis", kSunvisLanes, clouds_sunvis<false, kSunvisLanes, false, true>, grid_m(res_sunvis_n, blocks), kSunvisLanes, 0, s, nz, p, list, ws.pb);
+        else if (sv_pf)
             launch("clouds_sunvis", kSunvisLanes, clouds_sunvis<false, kSunvisLanes, true, true>, grid_m(res_sunvis, blocks), kSunvisLanes, 0, s, nz, p, list, ws.pb);
         else
             launch("clouds_sunvis", kSunvisLanes, clouds_sunvis<false, kSunvisLanes, true>, grid_m(res_sunvis, blocks), kSunvisLanes, 0, s, nz, p, list, ws.pb);
