@@ -81,8 +81,11 @@ struct CloudParams {
     int res_x, res_y;
 };
 
-// Q = uint32_t: LDS quads of 4 bytes (c0 c1 / c2 c3); Q = uint2: the same quad pre-expanded to 16-bit pairs
-// (c0 | c1 << 16, c2 | c3 << 16), which saves the two byte permutes per bilinear tap (twice the LDS).
+// Q = uint32_t: LDS quads of 4 bytes (c0 c1 / c2 c3), filtered in integers (v_dot2_u32_u16); Q = uint2: the same quad
+// in float form, two f16 pairs (256 c0 | (c1 - c0) << 16, 256 c2 | (c3 - c2) << 16) filtered by v_fma_mix_f32 (twice
+// the LDS; every value and partial sum is an integer, or an integer / 256, below 2^24, so exact: the same bits as the
+// integer form, scaled by 1 / 256, NoiseScale). On gfx950 the fp32 FMA issues at about twice the rate of the 32-bit
+// integer, permute and dot-product opcodes (tools/microbench/valu_ops.hip), so the float form is the cheaper one.
 template <typename Q>
 struct CtxT {
     const Q* quads;   // LDS
@@ -90,6 +93,24 @@ struct CtxT {
 };
 using Ctx = CtxT<uint32_t>;
 using CtxW = CtxT<uint2>;
+// noise3's value per unit of the noise (the u32 form's 65536 x 255 x bilinear; the f16 form's 256 x 255 x bilinear)
+template <typename Q> struct NoiseScale { static constexpr float v = 1.0f; };
+template <> struct NoiseScale<uint2> { static constexpr float v = 256.0f; };
+
+// The float-form table entry of quad texels (c0, c1, c2, c3) (bytes): 256 c0, c1 - c0, 256 c2, c3 - c2 as f16 (exact)
+__device__ __forceinline__ uint2 wide_quad_entry(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
+    auto h = [](int v) { return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)(float)v); };
+    return uint2{h(256 * (int)c0) | (h((int)c1 - (int)c0) << 16), h(256 * (int)c2) | (h((int)c3 - (int)c2) << 16)};
+}
+// (bilinear of the quad) / 256 from its float-form entry with wx = the x weight (0..255) and wys = the y weight / 256:
+// top = 256 c0 + (c1 - c0) wx and bot are integers below 2^16, (bot - top) wy / 256 + top is the integer bilinear / 256
+__device__ __forceinline__ float bilerp_wide(uint2 q, float wx, float wys) {
+    const float top = __builtin_fmaf((float)__builtin_bit_cast(_Float16, (uint16_t)(q.x >> 16)), wx,
+                                     (float)__builtin_bit_cast(_Float16, (uint16_t)(q.x & 0xffffu)));
+    const float bot = __builtin_fmaf((float)__builtin_bit_cast(_Float16, (uint16_t)(q.y >> 16)), wx,
+                                     (float)__builtin_bit_cast(_Float16, (uint16_t)(q.y & 0xffffu)));
+    return __builtin_fmaf(bot - top, wys, top);
+}
 
 __device__ __forceinline__ float bayer2(float ax, float ay) {
     ax = floorf(ax);
@@ -180,10 +201,13 @@ __device__ __forceinline__ f2v pfma(f2v a, f2v b, f2v c) { return __builtin_elem
 // One bilinear REPEAT tap of the noise .x at the fixed-point texel coordinate (fx, fy) (8 fractional bits), from the LDS
 // quad table: 65536 x 255 x the bilinear (exact in integers).
 template <typename Q>
-__device__ __forceinline__ uint32_t noise_tap(const Q* quads, int fx, int fy) {
+__device__ __forceinline__ float noise_tap(const Q* quads, int fx, int fy) {
     const uint32_t wx = (uint32_t)fx & 255u, wy = (uint32_t)fy & 255u;
     const uint32_t ix = ((uint32_t)fx >> 8) & kNoiseMask, iy = ((uint32_t)fy >> 8) & kNoiseMask;
-    return quad_bilerp_u(quads[iy * (uint32_t)kTW + ix], wx * 65535u + 256u, wy * 65535u + 256u);
+    if constexpr (std::is_same<Q, uint2>::value)
+        return bilerp_wide(quads[iy * (uint32_t)kTW + ix], (float)wx, (float)wy * (1.0f / 256.0f));
+    else
+        return (float)quad_bilerp_u(quads[iy * (uint32_t)kTW + ix], wx * 65535u + 256u, wy * 65535u + 256u);
 }
 
 // get_3d_noise, :219-233.
@@ -207,20 +231,25 @@ __device__ __forceinline__ float noise3(const CtxT<Q>& cx, f3 pos) {
         // rounding RN(16384 u - 127.5): one fma
         const int fx = floor_to_int(__builtin_fmaf(ux, 16384.0f, -127.5f));
         const int fy = floor_to_int(__builtin_fmaf(uy, 16384.0f, -127.5f));
-        const uint32_t wxp = ((uint32_t)fx & 255u) * 65535u + 256u, wyp = ((uint32_t)fy & 255u) * 65535u + 256u;
         const uint32_t ix = ((uint32_t)fx >> 8) & kNoiseMask, iy = ((uint32_t)fy >> 8) & kNoiseMask;
         const Q* t = cx.quads + (iy * (uint32_t)kTW + ix);
-        a = (float)quad_bilerp_u(t[0], wxp, wyp);
+        // the second tap at coord + 17/64 taken as the first + 17 texels: u + 17/64 and 16384 (u + 17/64) - 127.5
+        // are exact, or round as u's own terms do, except where a sum crosses into the next binade (there it may land
+        // one sub-texel step away)
+        if constexpr (std::is_same<Q, uint2>::value) {
+            const float wx = (float)((uint32_t)fx & 255u), wys = (float)((uint32_t)fy & 255u) * (1.0f / 256.0f);
+            a = bilerp_wide(t[0], wx, wys);
+            b = bilerp_wide(t[kTap2 * kTW + kTap2], wx, wys);
+        } else {
+            const uint32_t wxp = ((uint32_t)fx & 255u) * 65535u + 256u, wyp = ((uint32_t)fy & 255u) * 65535u + 256u;
+            a = (float)quad_bilerp_u(t[0], wxp, wyp);
+            b = (float)quad_bilerp_u(t[kTap2 * kTW + kTap2], wxp, wyp);
+        }
         if constexpr (SOC_CLOUDS_EXACT >= 2) {
             // the second tap at RN(coord + 17/64), its own fixed point
             const int gx = floor_to_int(__builtin_fmaf(ux + 0.265625f, 16384.0f, -127.5f));
             const int gy = floor_to_int(__builtin_fmaf(uy + 0.265625f, 16384.0f, -127.5f));
-            b = (float)noise_tap(cx.quads, gx, gy);
-        } else {
-            // the second tap at coord + 17/64 taken as the first + 17 texels: u + 17/64 and 16384 (u + 17/64) - 127.5
-            // are exact, or round as u's own terms do, except where a sum crosses into the next binade (there it may land
-            // one sub-texel step away)
-            b = (float)quad_bilerp_u(t[kTap2 * kTW + kTap2], wxp, wyp);
+            b = noise_tap(cx.quads, gx, gy);
         }
     } else {
         // fixed-point texel coordinate of the first tap: (u 64 - 0.5) 256 + 0.5 with u = pos.x / 64 + p 17/64,
@@ -233,10 +262,16 @@ __device__ __forceinline__ float noise3(const CtxT<Q>& cx, f3 pos) {
         const uint32_t ix = ((uint32_t)fx >> 8) & kNoiseMask, iy = ((uint32_t)fy >> 8) & kNoiseMask;
         const Q* t = cx.quads + (iy * (uint32_t)kTW + ix);
         const Q q0 = t[0], q1 = t[kTap2 * kTW + kTap2];
-        a = (float)quad_bilerp_u(q0, wxp, wyp);
-        b = (float)quad_bilerp_u(q1, wxp, wyp);
+        if constexpr (std::is_same<Q, uint2>::value) {
+            a = bilerp_wide(q0, (float)wx, (float)wy * (1.0f / 256.0f));
+            b = bilerp_wide(q1, (float)wx, (float)wy * (1.0f / 256.0f));
+        } else {
+            a = (float)quad_bilerp_u(q0, wxp, wyp);
+            b = (float)quad_bilerp_u(q1, wxp, wyp);
+        }
     }
-    return __builtin_fmaf(f, b - a, a);   // x 1 / (255 65536) = the noise value; the caller folds it into the octave weight
+    return __builtin_fmaf(f, b - a, a);   // x 1 / (255 65536) = the noise value (Q = uint2: x 1 / (255 256)); the caller
+                                          // folds it into the octave weight
 }
 constexpr float kNoiseNorm = 1.0f / (255.0f * 65536.0f);
 
@@ -285,11 +320,14 @@ __device__ float clouds_at(const C& cx, f3 p, float h) {
     } else {
         cc = p * 0.001f + mv;
     }
-    // octave weight x noise normalisation as one constant per octave (powers of two apart: one fma per octave)
-    float n = noise3(cx, cc) * (0.5f * kNoiseNorm);
+    // octave weight x noise normalisation as one constant per octave (powers of two apart: one fma per octave); the
+    // float-form table's values are the integer form's / 256 and its constants x 256 (exact: the same products)
+    using Q = typename std::remove_cv<typename std::remove_pointer<decltype(cx.quads)>::type>::type;
+    constexpr float kS = NoiseScale<Q>::v;
+    float n = noise3(cx, cc) * (0.5f * kNoiseNorm * kS);
     f3 c2 = cc * 2.0f + mv;   // 2 cc exact: one fma is the same sum
     if (ex) c2.y = cc.y * 2.0f;
-    n = __builtin_fmaf(noise3(cx, c2), 0.25f * kNoiseNorm, n);
+    n = __builtin_fmaf(noise3(cx, c2), 0.25f * kNoiseNorm * kS, n);
     if (SOC_CLOUDS_EXITS == 2) return n;   // profiling only (wrong results): never the last two octaves
     if (SOC_CLOUDS_EXITS != 0 && n < 0.55f - 0.1875f - 1e-4f) return 0.0f;
     f3 c3;
@@ -299,12 +337,12 @@ __device__ float clouds_at(const C& cx, f3 p, float h) {
     } else {
         c3 = cc * 7.0f - mv;
     }
-    n = __builtin_fmaf(noise3(cx, c3), 0.125f * kNoiseNorm, n);
+    n = __builtin_fmaf(noise3(cx, c3), 0.125f * kNoiseNorm * kS, n);
     if (SOC_CLOUDS_EXITS != 0 && n < 0.55f - 0.0625f - 1e-4f) return 0.0f;
     // (cc + mv) 16 == fma(cc, 16, 16 mv) exactly: scaling by a power of two commutes with the rounding
     const f3 c4 = f3{__builtin_fmaf(cc.x, 16.0f, mv.x * 16.0f), ex ? cc.y * 16.0f : __builtin_fmaf(cc.y, 16.0f, mv.y * 16.0f),
                      __builtin_fmaf(cc.z, 16.0f, mv.z * 16.0f)};
-    n = __builtin_fmaf(noise3(cx, c4), 0.0625f * kNoiseNorm, n);
+    n = __builtin_fmaf(noise3(cx, c4), 0.0625f * kNoiseNorm * kS, n);
     const float hh = p.y - kMinH;
     const float th = (1.0f - cl_exp(-0.01f * hh)) * cl_exp(-0.004f * hh);
     const float t = clampf((n - 0.55f) * (1.0f / (0.6f - 0.55f)), 0.0f, 1.0f);
@@ -522,7 +560,7 @@ __device__ __forceinline__ uint4 noise_quad_texels(const DImg& noise, int i) {
 
 // zero: the frame's 256-B counter block, cleared here (the lane's first kernel) instead of by a separate fill launch
 // Blocks past the table's (lut_blocks) build the frame's noise quad tables (noise_quads: 4 bytes per entry, as
-// stage_noise; noise_wide: 16-bit pairs, as stage_noise_wide; the padding entries zero) for the march kernels' LDS.
+// stage_noise; noise_wide: the float-form f16 pairs, as stage_noise_wide; the padding entries zero) for the march kernels' LDS.
 template <bool NOISE_R8>
 __global__ __launch_bounds__(kWorkgroup) void clouds_od_lut(float2* __restrict__ lut, float C2, uint32_t* __restrict__ zero,
                                                      int lut_blocks, DImg noise, uint32_t* __restrict__ noise_quads,
@@ -533,7 +571,7 @@ __global__ __launch_bounds__(kWorkgroup) void clouds_od_lut(float2* __restrict__
         uint4 t = uint4{0u, 0u, 0u, 0u};
         if (e < kTable) t = noise_quad_texels<NOISE_R8>(noise, e);
         noise_quads[e] = t.x | (t.y << 8) | (t.z << 16) | (t.w << 24);
-        if (e < kTableU2) noise_wide[e] = uint2{t.x | (t.y << 16), t.z | (t.w << 16)};
+        if (e < kTableU2) noise_wide[e] = e < kTable ? wide_quad_entry(t.x, t.y, t.z, t.w) : uint2{0u, 0u};
         return;
     }
     const int i = (int)(blockIdx.x * kWorkgroup + threadIdx.x);
@@ -757,7 +795,7 @@ __device__ __forceinline__ void stage_noise_wide(const DImg& noise, uint2* quads
             if (NOISE_R8) return row_ptr<uint8_t>(noise, ty)[tx];
             return row_ptr<uint32_t>(noise, ty)[tx] & 0xffu;
         };
-        quads[i] = uint2{texel(nx, nyw) | (texel(nx1, nyw) << 16), texel(nx, ny1) | (texel(nx1, ny1) << 16)};
+        quads[i] = wide_quad_entry(texel(nx, nyw), texel(nx1, nyw), texel(nx, ny1), texel(nx1, ny1));
     }
 }
 
@@ -961,7 +999,7 @@ struct PairBufs {
     float* od_tmp;        // [od_blocks][24][256]: per density workgroup, the od of its current batch's dense steps until
                           // their pair slots are known; density then stores od in od[slot], and sunvis only adds vis
     const uint32_t* noise_quads;  // [kTableU32] the frame's noise quad table (clouds_od_lut), or nullptr: stage_noise
-    const uint2* noise_wide;      // [kTableU2] the same as 16-bit pairs (stage_noise_wide)
+    const uint2* noise_wide;      // [kTableU2] the same quads in float form (stage_noise_wide)
     uint32_t store_geom;  // tuning knob SOC_CLOUDS_GEOM
     uint32_t od_blocks;   // density workgroups the od scratch holds (the density grid is clamped to it)
     uint32_t n;           // list capacity (W*H)
