@@ -66,6 +66,9 @@ constexpr int kNoise = 64, kNoiseMask = 63;
 constexpr int kTap2 = 17, kTW = kNoise + kTap2, kTable = kTW * kTW;
 // the quad tables padded to whole 16-B chunks (prebuilt in the workspace by clouds_od_lut, copied into LDS)
 constexpr int kTableU32 = (kTable + 3) & ~3, kTableU2 = (kTable + 1) & ~1;
+// the row table (RowF): one f16 pair per texel position of 82 rows (a quad's bottom row is the next row's entry)
+constexpr int kRowTable = (kTW + 1) * kTW, kRowU32 = (kRowTable + 3) & ~3;
+constexpr int kTableBuild = kRowU32 > kTableU32 ? kRowU32 : kTableU32;   // entries clouds_od_lut builds
 constexpr float kEarthRadius = 6371000.0f, kMinH = 1600.0f, kMaxH = 500.0f + 1600.0f, kSunBrightness = 3.0f;
 constexpr float kPi = 3.14159265358979f;   // acos(-1.0) in fp32
 constexpr float kLn2 = 0.693147182f;       // log(2.0) in fp32
@@ -94,13 +97,23 @@ struct CtxT {
 using Ctx = CtxT<uint32_t>;
 using CtxW = CtxT<uint2>;
 // noise3's value per unit of the noise (the u32 form's 65536 x 255 x bilinear; the f16 form's 256 x 255 x bilinear)
+// Q = RowF: the float form with half the LDS: one f16 pair (256 c0 | (c1 - c0) << 16) per texel position of a row table,
+// the quad's bottom row read from the entry kTW further (two 4-B LDS reads per tap instead of one 8-B read)
+struct RowF {
+    uint32_t h;
+};
 template <typename Q> struct NoiseScale { static constexpr float v = 1.0f; };
 template <> struct NoiseScale<uint2> { static constexpr float v = 256.0f; };
+template <> struct NoiseScale<RowF> { static constexpr float v = 256.0f; };
 
 // The float-form table entry of quad texels (c0, c1, c2, c3) (bytes): 256 c0, c1 - c0, 256 c2, c3 - c2 as f16 (exact)
 __device__ __forceinline__ uint2 wide_quad_entry(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
     auto h = [](int v) { return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)(float)v); };
     return uint2{h(256 * (int)c0) | (h((int)c1 - (int)c0) << 16), h(256 * (int)c2) | (h((int)c3 - (int)c2) << 16)};
+}
+__device__ __forceinline__ uint32_t row_entry(uint32_t c0, uint32_t c1) {
+    auto h = [](int v) { return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)(float)v); };
+    return h(256 * (int)c0) | (h((int)c1 - (int)c0) << 16);
 }
 // (bilinear of the quad) / 256 from its float-form entry with wx = the x weight (0..255) and wys = the y weight / 256:
 // top = 256 c0 + (c1 - c0) wx and bot are integers below 2^16, (bot - top) wy / 256 + top is the integer bilinear / 256
@@ -110,6 +123,10 @@ __device__ __forceinline__ float bilerp_wide(uint2 q, float wx, float wys) {
     const float bot = __builtin_fmaf((float)__builtin_bit_cast(_Float16, (uint16_t)(q.y >> 16)), wx,
                                      (float)__builtin_bit_cast(_Float16, (uint16_t)(q.y & 0xffffu)));
     return __builtin_fmaf(bot - top, wys, top);
+}
+// the same from the row table's two entries (top row, bottom row)
+__device__ __forceinline__ float bilerp_rows(RowF t, RowF b, float wx, float wys) {
+    return bilerp_wide(uint2{t.h, b.h}, wx, wys);
 }
 
 __device__ __forceinline__ float bayer2(float ax, float ay) {
@@ -206,6 +223,9 @@ __device__ __forceinline__ float noise_tap(const Q* quads, int fx, int fy) {
     const uint32_t ix = ((uint32_t)fx >> 8) & kNoiseMask, iy = ((uint32_t)fy >> 8) & kNoiseMask;
     if constexpr (std::is_same<Q, uint2>::value)
         return bilerp_wide(quads[iy * (uint32_t)kTW + ix], (float)wx, (float)wy * (1.0f / 256.0f));
+    else if constexpr (std::is_same<Q, RowF>::value)
+        return bilerp_rows(quads[iy * (uint32_t)kTW + ix], quads[(iy + 1u) * (uint32_t)kTW + ix], (float)wx,
+                           (float)wy * (1.0f / 256.0f));
     else
         return (float)quad_bilerp_u(quads[iy * (uint32_t)kTW + ix], wx * 65535u + 256u, wy * 65535u + 256u);
 }
@@ -240,6 +260,10 @@ __device__ __forceinline__ float noise3(const CtxT<Q>& cx, f3 pos) {
             const float wx = (float)((uint32_t)fx & 255u), wys = (float)((uint32_t)fy & 255u) * (1.0f / 256.0f);
             a = bilerp_wide(t[0], wx, wys);
             b = bilerp_wide(t[kTap2 * kTW + kTap2], wx, wys);
+        } else if constexpr (std::is_same<Q, RowF>::value) {
+            const float wx = (float)((uint32_t)fx & 255u), wys = (float)((uint32_t)fy & 255u) * (1.0f / 256.0f);
+            a = bilerp_rows(t[0], t[kTW], wx, wys);
+            b = bilerp_rows(t[kTap2 * kTW + kTap2], t[(kTap2 + 1) * kTW + kTap2], wx, wys);
         } else {
             const uint32_t wxp = ((uint32_t)fx & 255u) * 65535u + 256u, wyp = ((uint32_t)fy & 255u) * 65535u + 256u;
             a = (float)quad_bilerp_u(t[0], wxp, wyp);
@@ -265,6 +289,9 @@ __device__ __forceinline__ float noise3(const CtxT<Q>& cx, f3 pos) {
         if constexpr (std::is_same<Q, uint2>::value) {
             a = bilerp_wide(q0, (float)wx, (float)wy * (1.0f / 256.0f));
             b = bilerp_wide(q1, (float)wx, (float)wy * (1.0f / 256.0f));
+        } else if constexpr (std::is_same<Q, RowF>::value) {
+            a = bilerp_rows(q0, t[kTW], (float)wx, (float)wy * (1.0f / 256.0f));
+            b = bilerp_rows(q1, t[(kTap2 + 1) * kTW + kTap2], (float)wx, (float)wy * (1.0f / 256.0f));
         } else {
             a = (float)quad_bilerp_u(q0, wxp, wyp);
             b = (float)quad_bilerp_u(q1, wxp, wyp);
@@ -564,14 +591,22 @@ __device__ __forceinline__ uint4 noise_quad_texels(const DImg& noise, int i) {
 template <bool NOISE_R8>
 __global__ __launch_bounds__(kWorkgroup) void clouds_od_lut(float2* __restrict__ lut, float C2, uint32_t* __restrict__ zero,
                                                      int lut_blocks, DImg noise, uint32_t* __restrict__ noise_quads,
-                                                     uint2* __restrict__ noise_wide) {
+                                                     uint2* __restrict__ noise_wide, uint32_t* __restrict__ noise_rows) {
     if ((int)blockIdx.x >= lut_blocks) {
         const int e = (int)(blockIdx.x - lut_blocks) * kWorkgroup + (int)threadIdx.x;
-        if (e >= kTableU32) return;
+        if (e >= kTableBuild) return;
         uint4 t = uint4{0u, 0u, 0u, 0u};
         if (e < kTable) t = noise_quad_texels<NOISE_R8>(noise, e);
-        noise_quads[e] = t.x | (t.y << 8) | (t.z << 16) | (t.w << 24);
+        if (e < kTableU32) noise_quads[e] = t.x | (t.y << 8) | (t.z << 16) | (t.w << 24);
         if (e < kTableU2) noise_wide[e] = e < kTable ? wide_quad_entry(t.x, t.y, t.z, t.w) : uint2{0u, 0u};
+        if (e < kRowU32) {
+            uint32_t r = 0u;
+            if (e < kRowTable) {   // row e / kTW (wrapped), texels x and x + 1 (wrapped)
+                const uint4 q = noise_quad_texels<NOISE_R8>(noise, e % kTW + ((e / kTW) & kNoiseMask) * kTW);
+                r = row_entry(q.x, q.y);
+            }
+            noise_rows[e] = r;
+        }
         return;
     }
     const int i = (int)(blockIdx.x * kWorkgroup + threadIdx.x);
@@ -799,6 +834,18 @@ __device__ __forceinline__ void stage_noise_wide(const DImg& noise, uint2* quads
     }
 }
 
+template <bool NOISE_R8>
+__device__ __forceinline__ void stage_noise_rows(const DImg& noise, RowF* rows, int tid, int nthreads) {
+    for (int i = tid; i < kRowTable; i += nthreads) {
+        const int ny = (i / kTW) & kNoiseMask, nx = (i % kTW) & kNoiseMask, nx1 = (nx + 1) & kNoiseMask;
+        auto texel = [&](int tx, int ty) -> uint32_t {
+            if (NOISE_R8) return row_ptr<uint8_t>(noise, ty)[tx];
+            return row_ptr<uint32_t>(noise, ty)[tx] & 0xffu;
+        };
+        rows[i] = RowF{row_entry(texel(nx, ny), texel(nx1, ny))};
+    }
+}
+
 // Copy a prebuilt quad table (N16 16-B chunks) into LDS: each lane issues its loads in batches of 4 before their LDS
 // stores (the per-texel staging loop took 4 byte loads per entry and waited on every round: 26 rounds for a
 // 256-lane workgroup).
@@ -1000,6 +1047,7 @@ struct PairBufs {
                           // their pair slots are known; density then stores od in od[slot], and sunvis only adds vis
     const uint32_t* noise_quads;  // [kTableU32] the frame's noise quad table (clouds_od_lut), or nullptr: stage_noise
     const uint2* noise_wide;      // [kTableU2] the same quads in float form (stage_noise_wide)
+    const uint32_t* noise_rows;   // [kRowU32] the row table (stage_noise_rows)
     uint32_t store_geom;  // tuning knob SOC_CLOUDS_GEOM
     uint32_t od_blocks;   // density workgroups the od scratch holds (the density grid is clamped to it)
     uint32_t n;           // list capacity (W*H)
@@ -1068,21 +1116,26 @@ __device__ __forceinline__ MarchGeom pair_geometry(const CloudParams& p, const u
     return march_geometry(sky_dir(p, x, y));
 }
 
-template <bool NOISE_R8, int DB = 1>
+// ROWS: the noise from the float-form row table (RowF: the same 26 KiB of LDS, half the bilinear's issue time)
+template <bool NOISE_R8, int DB = 1, bool ROWS = false>
 // 6 waves/SIMD: 80 VGPRs with 20 B of scratch, measured faster than 5 waves without a spill (profiles/r04_probe_clouds_scan.txt)
 __global__ __launch_bounds__(kWorkgroup) __attribute__((amdgpu_waves_per_eu(6))) void clouds_density(
     DImg noise, CloudParams p, const uint32_t* __restrict__ counter, const uint32_t* __restrict__ list, PairBufs pb) {
-    __shared__ uint4 quads4[kTableU32 / 4];
-    uint32_t* quads = reinterpret_cast<uint32_t*>(quads4);
+    using Q = typename std::conditional<ROWS, RowF, uint32_t>::type;
+    constexpr int kN16 = ROWS ? kRowU32 / 4 : kTableU32 / 4;
+    __shared__ uint4 quads4[kN16];
+    Q* quads = reinterpret_cast<Q*>(quads4);
     __shared__ uint32_t offs[25][4];
     __shared__ uint32_t wg_base;
     const uint32_t count = *counter;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (blockIdx.x * 256u >= count) return;
-    if (pb.noise_quads) stage_noise_table<kTableU32 / 4>(reinterpret_cast<const uint4*>(pb.noise_quads), quads4, tid, 256);
+    const uint32_t* pre_tab = ROWS ? pb.noise_rows : pb.noise_quads;
+    if (pre_tab) stage_noise_table<kN16>(reinterpret_cast<const uint4*>(pre_tab), quads4, tid, 256);
+    else if constexpr (ROWS) stage_noise_rows<NOISE_R8>(noise, quads, tid, 256);
     else stage_noise<NOISE_R8>(noise, quads, tid, 256);
     __syncthreads();
-    Ctx cx;
+    CtxT<Q> cx;
     cx.quads = quads;
     cx.cam_x = p.cam[0];
     cx.cam_z = p.cam[2];
@@ -1175,11 +1228,13 @@ __global__ __launch_bounds__(kWorkgroup) __attribute__((amdgpu_waves_per_eu(6)))
 
 // 512-lane workgroups: the 26 KiB noise table per workgroup caps residency at 6 workgroups per CU, so 256 lanes
 // give 6 waves per SIMD and 512 lanes give the full 8 (one table per 8 waves).
-template <bool NOISE_R8, uint32_t kSunvisThreads, bool WIDE = false, bool PF = false>
+// ROWS: the float-form row table (RowF, 26 KiB: 8 waves per SIMD) instead of WIDE's quads (52 KiB: 6)
+template <bool NOISE_R8, uint32_t kSunvisThreads, bool WIDE = false, bool PF = false, bool ROWS = false>
 __global__ __launch_bounds__(kSunvisThreads) __attribute__((amdgpu_waves_per_eu(kSunvisThreads == 512 && !WIDE ? 8 : 6))) void clouds_sunvis(
     DImg noise, CloudParams p, const uint32_t* __restrict__ list, PairBufs pb) {
-    using Q = typename std::conditional<WIDE, uint2, uint32_t>::type;
-    constexpr int kN16 = WIDE ? kTableU2 / 2 : kTableU32 / 4;
+    static_assert(!(ROWS && WIDE), "one table form");
+    using Q = typename std::conditional<ROWS, RowF, typename std::conditional<WIDE, uint2, uint32_t>::type>::type;
+    constexpr int kN16 = ROWS ? kRowU32 / 4 : WIDE ? kTableU2 / 2 : kTableU32 / 4;
     __shared__ uint4 quads4[kN16];
     Q* quads = reinterpret_cast<Q*>(quads4);
     __shared__ uint32_t pre[kShards + 1];
@@ -1195,8 +1250,10 @@ __global__ __launch_bounds__(kSunvisThreads) __attribute__((amdgpu_waves_per_eu(
     __syncthreads();
     const uint32_t total = pre[kShards];
     if (blockIdx.x * kSunvisThreads >= total) return;
-    const void* pre_tab = WIDE ? static_cast<const void*>(pb.noise_wide) : static_cast<const void*>(pb.noise_quads);
+    const void* pre_tab = ROWS ? static_cast<const void*>(pb.noise_rows)
+                               : WIDE ? static_cast<const void*>(pb.noise_wide) : static_cast<const void*>(pb.noise_quads);
     if (pre_tab) stage_noise_table<kN16>(static_cast<const uint4*>(pre_tab), quads4, tid, kSunvisThreads);
+    else if constexpr (ROWS) stage_noise_rows<NOISE_R8>(noise, quads, tid, kSunvisThreads);
     else if constexpr (WIDE) stage_noise_wide<NOISE_R8>(noise, quads, tid, kSunvisThreads);
     else stage_noise<NOISE_R8>(noise, quads, tid, kSunvisThreads);
     __syncthreads();
@@ -1388,6 +1445,7 @@ struct CloudWs {
     float2* od_lut;   // secondary-ray optical-depth table (kOdR x kOdM)
     uint32_t* noise_quads;   // [kTableU32] noise quad tables (clouds_od_lut)
     uint2* noise_wide;       // [kTableU2]
+    uint32_t* noise_rows;    // [kRowU32]
     float4* sky_tab;  // sky-view table (kSvEntries x 2 float4)
     size_t bytes;
 };
@@ -1427,6 +1485,8 @@ CloudWs cloud_ws_layout(void* base, size_t n) {
     off = al(off + (size_t)kTableU32 * 4);
     w.noise_wide = reinterpret_cast<uint2*>(b + off);
     off = al(off + (size_t)kTableU2 * 8);
+    w.noise_rows = reinterpret_cast<uint32_t*>(b + off);
+    off = al(off + (size_t)kRowU32 * 4);
     w.bytes = off;
     return w;
 }
@@ -1496,16 +1556,17 @@ int soc::cloud_rendering_launch(const soc_globals* g, soc_img depth, soc_img noi
     if (use_lut) lut = OdLut{ws.od_lut, C2};
     ws.pb.noise_quads = noise_tab ? ws.noise_quads : nullptr;
     ws.pb.noise_wide = noise_tab ? ws.noise_wide : nullptr;
+    ws.pb.noise_rows = noise_tab ? ws.noise_rows : nullptr;
     {
         const int lut_blocks = use_lut ? ceil_div(kOdR * kOdM, kWorkgroup) : 1;
-        const int blocks_all = lut_blocks + (noise_tab ? ceil_div(kTableU32, kWorkgroup) : 0);
+        const int blocks_all = lut_blocks + (noise_tab ? ceil_div(kTableBuild, kWorkgroup) : 0);
         float2* lt = use_lut ? ws.od_lut : nullptr;
         if (noise.format == SOC_FMT_R8_UNORM)
             launch("clouds_od_lut", kWorkgroup, clouds_od_lut<true>, blocks_all, kWorkgroup, 0, s, lt, C2, counter, lut_blocks,
-                   dimg(noise), ws.noise_quads, ws.noise_wide);
+                   dimg(noise), ws.noise_quads, ws.noise_wide, ws.noise_rows);
         else
             launch("clouds_od_lut", kWorkgroup, clouds_od_lut<false>, blocks_all, kWorkgroup, 0, s, lt, C2, counter, lut_blocks,
-                   dimg(noise), ws.noise_quads, ws.noise_wide);
+                   dimg(noise), ws.noise_quads, ws.noise_wide, ws.noise_rows);
     }
     const int vec_store = (target.pitch_bytes % 16 == 0) && (reinterpret_cast<uintptr_t>(target.data) % 16 == 0);
     const bool hoist = sky_bound || tuning_knob("SOC_CLOUDS_CLASSIFY_HOIST", 0);
@@ -1517,12 +1578,13 @@ int soc::cloud_rendering_launch(const soc_globals* g, soc_img depth, soc_img noi
                kWorkgroup, 0, s, dimg(depth), dimg(target), p, vec_store, counter, list);
     // One resident wave set per kernel, grid-stride over the list / pairs: the long per-item work is
     // balanced over all SIMDs instead of running as a second, partially filled round.
-    static int res_atmos = 0, res_density = 0, res_sunvis = 0, res_sunvis_n = 0, res_resolve = 0;
+    static int res_atmos = 0, res_density = 0, res_sunvis = 0, res_sunvis_n = 0, res_sunvis_r = 0, res_resolve = 0;
     if (!res_atmos) {
         res_atmos = resident_blocks(clouds_atmosphere<false>);
         res_density = resident_blocks(clouds_density<false>);
         res_sunvis = resident_blocks(clouds_sunvis<false, kSunvisLanes, true>, kSunvisLanes);
         res_sunvis_n = resident_blocks(clouds_sunvis<false, kSunvisLanes, false, true>, kSunvisLanes);
+        res_sunvis_r = resident_blocks(clouds_sunvis<false, kSunvisLanes, false, true, true>, kSunvisLanes);
         res_resolve = resident_blocks(clouds_resolve<false, true>);
     }
     const long long blocks = ((long long)W * H + 255) / 256;
@@ -1593,20 +1655,27 @@ int soc::cloud_rendering_launch(const soc_globals* g, soc_img depth, soc_img noi
     const int db = tuning_knob("SOC_CLOUDS_DENSITY_BATCH", 8);
     // the sun-visibility kernel's next pair word loaded one iteration ahead
     const bool sv_pf = tuning_knob("SOC_CLOUDS_SUNVIS_PF", 1) != 0;
-    // the sun-visibility kernel's noise table: 16-bit pairs (52 KiB of LDS per 512-lane workgroup, two byte permutes fewer
-    // per bilinear tap; r2.9) or the byte quads (26 KiB: more LDS left on the CU for the main lane's workgroups)
-    const bool sv_wide = tuning_knob("SOC_CLOUDS_SUNVIS_WIDE", 1) != 0;
+    // the sun-visibility kernel's noise table (SOC_CLOUDS_SUNVIS_WIDE): 2 (default) the float-form row table (RowF, 26 KiB
+    // per 512-lane workgroup: 8 waves per SIMD, and room on the CU for the main lane's SSAO tile; C3 1728 -> 1799 fps),
+    // 1 the float-form quads (52 KiB, 6 waves per SIMD), 0 the byte quads (integer form, 26 KiB). The same bits.
+    const int sv_table = tuning_knob("SOC_CLOUDS_SUNVIS_WIDE", 2);
+    const bool sv_wide = sv_table != 0;
     // one od scratch per workgroup; SOC_CLOUDS_DENSITY_MULT: the grid as this many times the resident set (as gmul).
     // Default 1: 2 measured C3 1710 -> 1697 fps, C4 1321 -> 1358 (profiles/r05_ab_clouds_density_mult.txt)
     const int dmul = sky_bound ? 2 : std::max(1, tuning_knob("SOC_CLOUDS_DENSITY_MULT", 1));
     const int density_grid = std::min((int)std::max(1LL, std::min<long long>((long long)res_density * dmul, blocks)),
                                       (int)ws.pb.od_blocks);
+    // SOC_CLOUDS_DENSITY_ROWS (default 1): the density kernel's noise from the float-form row table (RowF; the same bits)
+    const bool drows = tuning_knob("SOC_CLOUDS_DENSITY_ROWS", 1) != 0;
     if (r8) {
-        if (db == 4) launch("clouds_density", kWorkgroup, clouds_density<true, 4>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
+        if (drows) launch("clouds_density", kWorkgroup, clouds_density<true, 8, true>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
+        else if (db == 4) launch("clouds_density", kWorkgroup, clouds_density<true, 4>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
         else if (db == 8) launch("clouds_density", kWorkgroup, clouds_density<true, 8>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
         else launch("clouds_density", kWorkgroup, clouds_density<true>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
         if (apos == 1) atmos();
-        if (!sv_wide)
+        if (sv_table == 2)
+            launch("clouds_sunvis", kSunvisLanes, clouds_sunvis<true, kSunvisLanes, false, true, true>, grid_m(res_sunvis_r, blocks), kSunvisLanes, 0, s, nz, p, list, ws.pb);
+        else if (!sv_wide)
             launch("clouds_sunvis", kSunvisLanes, clouds_sunvis<true, kSunvisLanes, false, true>, grid_m(res_sunvis_n, blocks), kSunvisLanes, 0, s, nz, p, list, ws.pb);
         else if (sv_pf)
             launch("clouds_sunvis", kSunvisLanes, clouds_sunvis<true, kSunvisLanes, true, true>, grid_m(res_sunvis, blocks), kSunvisLanes, 0, s, nz, p, list, ws.pb);
@@ -1618,11 +1687,14 @@ int soc::cloud_rendering_launch(const soc_globals* g, soc_img depth, soc_img noi
         else if (fold) resolve(clouds_resolve<true, true>);
         else resolve(clouds_resolve<true, false>);
     } else {
-        if (db == 4) launch("clouds_density", kWorkgroup, clouds_density<false, 4>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
+        if (drows) launch("clouds_density", kWorkgroup, clouds_density<false, 8, true>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
+        else if (db == 4) launch("clouds_density", kWorkgroup, clouds_density<false, 4>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
         else if (db == 8) launch("clouds_density", kWorkgroup, clouds_density<false, 8>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
         else launch("clouds_density", kWorkgroup, clouds_density<false>, density_grid, kWorkgroup, 0, s, nz, p, counter, list, ws.pb);
         if (apos == 1) atmos();
-        if (!sv_wide)
+        if (sv_table == 2)
+            launch("clouds_sunvis", kSunvisLanes, clouds_sunvis<false, kSunvisLanes, false, true, true>, grid_m(res_sunvis_r, blocks), kSunvisLanes, 0, s, nz, p, list, ws.pb);
+        else if (!sv_wide)
             launch("clouds_sunvis", kSunvisLanes, clouds_sunvis<false, kSunvisLanes, false, true>, grid_m(res_sunvis_n, blocks), kSunvisLanes, 0, s, nz, p, list, ws.pb);
         else if (sv_pf)
             launch("clouds_sunvis", kSunvisLanes, clouds_sunvis<false, kSunvisLanes, true, true>, grid_m(res_sunvis, blocks), kSunvisLanes, 0, s, nz, p, list, ws.pb);

@@ -574,20 +574,24 @@ def test_clouds_pair_path_equals_single_lane(soc, monkeypatch, W, H, pitch, all_
     ws = soc.cloud_rendering_workspace(W, H)
     soc.cloud_rendering(g, dev(depth), dev(gb["noise"]), a, None)
     monkeypatch.setenv("SOC_CLOUDS_OD_LUT", "0")   # every secondary ray marched, as the single-lane kernel does
-    # wide: the sun-visibility kernel over the float-form noise table (f16 pairs, v_fma_mix_f32; default) or the byte
-    # quads' integer form, as the density and single-lane kernels
-    for pos, geom, ntab, wide in (("0", "1", "1", "1"), ("1", "1", "1", "1"), ("2", "1", "1", "1"), ("2", "0", "1", "1"),
-                                  ("2", "1", "0", "1"), ("2", "1", "1", "0"), ("2", "1", "0", "0")):
+    # wide: the sun-visibility kernel over the float-form row table (2, default; f16 pairs, v_fma_mix_f32), the float-form
+    # quads (1) or the byte quads' integer form (0, as the single-lane kernel); the density over the row table or the
+    # byte quads (0)
+    for pos, geom, ntab, wide in (("0", "1", "1", "2"), ("1", "1", "1", "2"), ("2", "1", "1", "2"), ("2", "0", "1", "2"),
+                                  ("2", "1", "0", "2"), ("2", "1", "1", "1"), ("2", "1", "0", "1"), ("2", "1", "1", "0"),
+                                  ("2", "1", "0", "0")):
         monkeypatch.setenv("SOC_CLOUDS_ATMOS_POS", pos)
         monkeypatch.setenv("SOC_CLOUDS_GEOM", geom)   # the march geometry stored by density, or re-derived per pair
         monkeypatch.setenv("SOC_CLOUDS_NOISE_TABLE", ntab)   # noise quads prebuilt once per frame, or staged per workgroup
         monkeypatch.setenv("SOC_CLOUDS_SUNVIS_WIDE", wide)
+        monkeypatch.setenv("SOC_CLOUDS_DENSITY_ROWS", "0" if wide == "0" else "1")
         soc.reload_tuning()
         b = torch.zeros_like(a)
         soc.cloud_rendering(g, dev(depth), dev(gb["noise"]), b, ws)
         torch.cuda.synchronize()
         assert torch.equal(a, b), (pos, geom, ntab, wide, (a != b).float().mean().item())
     monkeypatch.delenv("SOC_CLOUDS_SUNVIS_WIDE")
+    monkeypatch.delenv("SOC_CLOUDS_DENSITY_ROWS")
     # with the secondary-ray table (the default) the prebuilt noise quads give the per-workgroup staging's bits too, for
     # the R8 and the RGBA8 noise image
     monkeypatch.delenv("SOC_CLOUDS_OD_LUT")

@@ -43,7 +43,17 @@ constexpr int kChains = 16;
     X(PK_MUL, "v_pk_mul_f32 %0, %1, %0", P)                                                                       \
     X(ADD3, "v_add3_u32 %0, %1, %2, %0", U)                                                                       \
     X(MUL_U24, "v_mul_u32_u24 %0, %1, %0", U)                                                                     \
-    X(FMAC, "v_fmac_f32 %0, %1, %2", F)
+    X(FMAC, "v_fmac_f32 %0, %1, %2", F)                                                                           \
+    X(MAD_I64_I32, "v_mad_i64_i32 %0, s[0:1], %1, %2, %0", D)                                                     \
+    X(LSHL_ADD_U64, "v_lshl_add_u64 %0, %0, 0, %1", D64)                                                          \
+    X(ADD_CO_U32, "v_add_co_u32 %0, vcc, %1, %0", U)                                                              \
+    X(PK_MAX_F16, "v_pk_max_f16 %0, %1, %0", U)                                                                   \
+    X(CVT_F32_F16, "v_cvt_f32_f16 %0, %1\n v_add_u32 %1, %2, %1", C)                                            \
+    X(LDEXP, "v_ldexp_f32 %0, %0, %1", FI)                                                                        \
+    X(MAX_F32, "v_max_f32 %0, %1, %0", F)                                                                         \
+    X(MIN_F32, "v_min_f32 %0, %1, %0", F)                                                                         \
+    X(CVT_PKRTZ, "v_cvt_pkrtz_f16_f32 %1, %0, %0\n v_fma_f32 %0, %0, %3, %4", FU)                                \
+    X(LOG, "v_log_f32 %0, %0", F1)
 
 #define ASM_F(s) asm volatile(s : "+v"(x[c]) : "v"(a), "v"(b))
 #define ASM_F1(s) asm volatile(s : "+v"(x[c]))
@@ -51,6 +61,9 @@ constexpr int kChains = 16;
 #define ASM_U1(s) asm volatile(s : "+v"(n[c]))
 #define ASM_C(s) asm volatile(s : "=v"(x[c]), "+v"(n[c]) : "v"(ua))
 #define ASM_FU(s) asm volatile(s : "+v"(x[c]), "=v"(n[c]) : "v"(ua), "v"(a), "v"(b))
+#define ASM_D(s) asm volatile(s : "+v"(w[c]) : "v"(ua), "v"(ub) : "s0", "s1")
+#define ASM_D64(s) asm volatile(s : "+v"(w[c]) : "v"(w2))
+#define ASM_FI(s) asm volatile(s : "+v"(x[c]) : "v"(ua))
 #define ASM_F2(s) asm volatile(s : "+v"(x[c]) : "v"(a), "v"(b) : "vcc")
 #define ASM_P(s) if (c < kChains / 2) asm volatile(s : "+v"(p[c]) : "v"(a2), "v"(b2))
 #define STEPS_F 1
@@ -60,6 +73,9 @@ constexpr int kChains = 16;
 #define STEPS_C 2
 #define STEPS_FU 2
 #define STEPS_F2 2
+#define STEPS_D 1
+#define STEPS_D64 1
+#define STEPS_FI 1
 #define STEPS_P 1   // 8 chains: the printed figure is half the per-instruction cost
 
 enum Kind {
@@ -85,6 +101,10 @@ __global__ __launch_bounds__(256) void chains(const float* __restrict__ in, unsi
 #pragma unroll
     for (int c = 0; c < kChains / 2; ++c) p[c] = v2{x[2 * c], x[2 * c + 1]};
     const v2 a2 = v2{a, a}, b2 = v2{b, b};
+    unsigned long long w[kChains];
+#pragma unroll
+    for (int c = 0; c < kChains; ++c) w[c] = n[c] * 3ull;
+    const unsigned long long w2 = ua * 7ull;
     __syncthreads();
     unsigned long long t0 = 0, r0 = 0;
     if (threadIdx.x == 0) {
@@ -111,6 +131,8 @@ __global__ __launch_bounds__(256) void chains(const float* __restrict__ in, unsi
     for (int c = 0; c < kChains; ++c) s += x[c] + (float)n[c];
 #pragma unroll
     for (int c = 0; c < kChains / 2; ++c) s += p[c].x + p[c].y;
+#pragma unroll
+    for (int c = 0; c < kChains; ++c) s += (float)w[c];
     out[blockIdx.x * 256 + threadIdx.x] = s;
 }
 
@@ -154,7 +176,7 @@ int main() {
     (void)hipMalloc(&d_in, sizeof(float) * 256);
     (void)hipMemcpy(d_in, h.data(), sizeof(float) * 256, hipMemcpyHostToDevice);
     for (int wps : {8}) {
-#define RUN(name, s, t) run<name>(d_in, wps, #name, STEPS_##t);
+#define RUN(name, s, t) if (name == FMA || name >= MAD_I64_I32) run<name>(d_in, wps, #name, STEPS_##t);
         OPS(RUN)
 #undef RUN
     }
