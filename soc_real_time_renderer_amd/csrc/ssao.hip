@@ -698,8 +698,10 @@ __device__ __forceinline__ void ssao_consume_pair(const TapPair& t, const SsaoPi
     const f2v dd = {__builtin_fmaf(wy.x, abot - atop, atop), __builtin_fmaf(wy.y, bbot - btop, btop)};
     const f2v vw = pfma(bc2(ip[11]), dd, bc2(ip[15]));
     const f2v d1 = {__builtin_fmaf(dd.x, px.A1, px.B1), __builtin_fmaf(dd.y, px.A1, px.B1)};
-    const f2v q = vw * f2v{fast_rcp(fabsf(d1.x)), fast_rcp(fabsf(d1.y))};
-    const f2v rc = {__builtin_amdgcn_fmed3f(q.x, 0.0f, 1.0f), __builtin_amdgcn_fmed3f(q.y, 0.0f, 1.0f)};
+    // two scalar multiplies whose clamp is an output modifier (a packed multiply then two clamping v_max_f32 issue ~2.5x
+    // the time: tools/microbench/valu_ops.hip); the same products
+    const f2v rc = {__builtin_amdgcn_fmed3f(vw.x * fast_rcp(fabsf(d1.x)), 0.0f, 1.0f),
+                    __builtin_amdgcn_fmed3f(vw.y * fast_rcp(fabsf(d1.y)), 0.0f, 1.0f)};
     const f2v range = rc * rc * pfma(bc2(-2.0f), rc, bc2(3.0f));   // smoothstep(0, 1, x)
     // (s.z + bias - frag.z) / r: the affine form, or PERSP (the projection's w row is (0, 0, -1, 0): w' = -s.z) one fma
     // from the tap's w' (within the SSAO tolerance: w' carries its own rounding)
