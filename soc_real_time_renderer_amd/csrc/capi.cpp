@@ -720,7 +720,10 @@ bool sky_lane_high(const soc_renderer* r) {
 // bloom pass then recording nothing. Both callbacks of a frame see the same lane (set before the passes are issued).
 // Re-checked every frame: a frame whose globals resolution differs from the images takes Composition's generic
 // path, which cannot compute the bloom, so the fourth pass must run then.
-bool bloom_in_comp_active(const soc_renderer* r) { return r->bloom_in_comp && r->bloom_in_comp_ok && sky_lane_high(r); }
+bool bloom_in_comp_active(const soc_renderer* r) {
+    // SOC_RENDERER_BLOOM_IN_COMP_ANY_LANE=1: also beside the low-priority sky lane (measurement knob)
+    return r->bloom_in_comp && r->bloom_in_comp_ok && (sky_lane_high(r) || tuning_knob("SOC_RENDERER_BLOOM_IN_COMP_ANY_LANE", 0));
+}
 
 soc_renderer::Pass& add_pass(soc_renderer* r, std::string name, std::string group, int phase, uint64_t reads,
                              uint64_t writes, PassFn fn, uint32_t flags = 0) {
