@@ -1513,7 +1513,10 @@ extern "C" int soc_renderer_execute(soc_renderer* r, const soc_globals* g, int32
             if (L == 0 && !r->main_after_side && r->passes[j].done_recorded &&
                 hipStreamWaitEvent(ls, r->passes[j].done, 0) != hipSuccess)
                 return abort_frame(r, s, lanes, set_error(SOC_E_HIP, "soc_renderer_execute: %s: ring-edge wait failed", p.name.c_str()));
-        int rc = run_pass(p, g, ls);
+        // SOC_RENDERER_PROBE_SKIP_PASS=<pass name>: profiling only (wrong results), that pass launches nothing; bounds
+        // what removing it (e.g. by fusing it into a neighbour) could gain in the frame
+        static const char* probe_skip = getenv("SOC_RENDERER_PROBE_SKIP_PASS");
+        int rc = (probe_skip && p.name == probe_skip) ? (int)SOC_OK : run_pass(p, g, ls);
         if (rc) return abort_frame(r, s, lanes, rc);
         pos[i] = next_pos[L]++;
         if (p.signal) {
