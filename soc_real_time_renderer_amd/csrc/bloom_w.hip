@@ -416,6 +416,104 @@ __global__ __launch_bounds__(kWorkgroup) void bloomw_up10s(DImg S1, DImg O, bool
     }
 }
 
+// W4 in register form (SOC_BLOOM_UP10_REG, default): no LDS and no barriers. Each wave owns a strip of 62 output columns
+// (lanes 1..62; lanes 0 and 63 hold the clamped neighbour columns) and walks down R_TH output rows; a lane keeps its
+// column's last five 1:2-horizontal sums (one mip1 row more every second output row) and the last three 1:1-horizontal
+// sums in registers, and takes its neighbours' mip0 texels by DPP wave shifts. The same operations in the same order as
+// Up10Tile (bloomw_up10s), so the same bits, without its four LDS phases (~180 B of LDS traffic per output pixel). Alone
+// at C3 36.4-36.8 us against 38.3-39.3 for bloomw_up10s, in the frame within noise; 8 / 32 rows per wave and 64-column
+// aligned strips measured the same (the 66 MB output stream is what is left).
+#ifndef SOC_BLOOM_UP10_ROWS
+#define SOC_BLOOM_UP10_ROWS 16
+#endif
+constexpr int R_OW = 62, R_TH = SOC_BLOOM_UP10_ROWS;
+__device__ __forceinline__ uint32_t up_from_left(uint32_t v) {   // lane i <- lane i-1 (wave_shr:1)
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t up_from_right(uint32_t v) {  // lane i <- lane i+1 (wave_shl:1)
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, false);
+}
+__global__ __launch_bounds__(kWorkgroup) void bloomw_up10r(DImg S1, DImg O, int nwx, int nwaves) {
+    const int lane = (int)(threadIdx.x & 63);
+    const int wid = (int)blockIdx.x * (kWorkgroup / 64) + (int)(threadIdx.x >> 6);
+    if (wid >= nwaves) return;   // wave-uniform
+    const int W0 = O.w, H0 = O.h, W1 = S1.w, H1 = S1.h;
+    const int wx = wid % nwx, Y0 = (wid / nwx) * R_TH;
+    const int x = wx * R_OW - 1 + lane;
+    const int cx = clampi(x, 0, W0 - 1);
+    const int px = cx & 1, c0 = (cx >> 1) - 2 + px;
+    int tc[4];
+    float wk[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        tc[k] = clampi(c0 + k, 0, W1 - 1);
+        wk[k] = px ? u12_w(1, k) : u12_w(0, k);
+    }
+    // the 1:2 horizontal sum of mip1 row clamp(s) at this lane's mip0 column (Up10Tile::build's first pass): the row's
+    // four taps are loaded one mip1 row ahead of their use (two output rows of arithmetic cover their latency)
+    auto taps = [&](int s, uint2 (&t)[4]) {
+        const uint2* row = row_ptr<uint2>(S1, clampi(s, 0, H1 - 1));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) t[k] = row[tc[k]];
+    };
+    auto h12 = [&](const uint2 (&t)[4]) {
+        C3 a{0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) madd(a, t[k], wk[k]);
+        return a;
+    };
+    // ring[i]: the sum of mip1 row base + i; pend: the taps of row base + 5
+    C3 ring[5];
+    uint2 pend[4];
+    int base = (max(Y0 - 1, 0) >> 1) - 2;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        taps(base + i, pend);
+        ring[i] = h12(pend);
+    }
+    taps(base + 5, pend);
+    // this lane's mip0 texel of row cy (the second pass, rounded to RGBA16F), then the row's 1:1 horizontal sum
+    auto hrow = [&](int cy) {
+        const int jb = (cy >> 1) - 2;   // rows only move down, at most one mip1 row per call
+        if (jb > base) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) ring[i] = ring[i + 1];
+            ring[4] = h12(pend);   // row base + 5 = jb + 4
+            base = jb;
+            taps(base + 5, pend);
+        }
+        const int py = cy & 1;
+        C3 a{0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float w = u12_w(py, k);
+            const C3 h = py ? ring[k + 1] : ring[k];
+            a.r = __builtin_fmaf(h.r, w, a.r);
+            a.g = __builtin_fmaf(h.g, w, a.g);
+            a.b = __builtin_fmaf(h.b, w, a.b);
+        }
+        const uint2 m = pack3(a);
+        const uint2 l = uint2{up_from_left(m.x), up_from_left(m.y)}, r = uint2{up_from_right(m.x), up_from_right(m.y)};
+        C3 hs{0.0f, 0.0f, 0.0f};
+        madd(hs, l, 1.0f);
+        madd(hs, m, 2.0f);
+        madd(hs, r, 1.0f);
+        return hs;
+    };
+    C3 hq0 = hrow(max(Y0 - 1, 0)), hq1 = hrow(min(Y0, H0 - 1));
+    const bool out_lane = lane >= 1 && lane <= R_OW && x < W0;
+    for (int y = Y0; y < min(Y0 + R_TH, H0); ++y) {
+        const C3 hq2 = hrow(min(y + 1, H0 - 1));
+        C3 o;
+        o.r = __builtin_fmaf(hq2.r, 1.0f / 16.0f, __builtin_fmaf(hq1.r, 2.0f / 16.0f, hq0.r * (1.0f / 16.0f)));
+        o.g = __builtin_fmaf(hq2.g, 1.0f / 16.0f, __builtin_fmaf(hq1.g, 2.0f / 16.0f, hq0.g * (1.0f / 16.0f)));
+        o.b = __builtin_fmaf(hq2.b, 1.0f / 16.0f, __builtin_fmaf(hq1.b, 2.0f / 16.0f, hq0.b * (1.0f / 16.0f)));
+        if (out_lane) row_ptr_w<uint2>(O, y)[x] = pack3(o);
+        hq0 = hq1;
+        hq1 = hq2;
+    }
+}
+
 // Workgroups of 256 lanes of bloomw_down01p resident on the whole device at once (the persistent kernel's grid bound),
 // queried once per device and cached (the occupancy query is not on the per-frame enqueue path).
 int down01p_resident_set() {
@@ -457,7 +555,10 @@ int launch_bloom_weighted(const soc_img& emissive, const soc_img* mips, const so
     }
     if (stage == 0 || stage == 4) {
         dim3 g(ceil_div(output.width, U_OW), ceil_div(output.height, U_OH));
-        if (tuning_knob("SOC_BLOOM_UP_SEP", 1))
+        if (tuning_knob("SOC_BLOOM_UP10_REG", 1)) {
+            const int nwx = ceil_div(output.width, R_OW), nwaves = nwx * ceil_div(output.height, R_TH);
+            launch("bloomw_up10r", kWorkgroup, bloomw_up10r, ceil_div(nwaves, kWorkgroup / 64), kWorkgroup, 0, s, M1, O, nwx, nwaves);
+        } else if (tuning_knob("SOC_BLOOM_UP_SEP", 1))
             launch("bloomw_up10s", kWorkgroup, bloomw_up10s, g, kWorkgroup, 0, s, M1, O, a16(output), swz);
         else
             launch("bloomw_up10", kWorkgroup, bloomw_up10, g, kWorkgroup, 0, s, M1, O, a16(output), swz);

@@ -131,6 +131,28 @@ def test_bloom_weighted_chain(soc, monkeypatch, W, H, sep):
     assert torch.all(mips[0] == 7.0) and torch.all(mips[2] == 7.0)   # scratch mips are not written
 
 
+@pytest.mark.parametrize("W,H", [(64, 40), (200, 136), (968, 552), (3840, 2160)])
+def test_bloom_up10_register_form_bit_identical(soc, monkeypatch, W, H):
+    """The last upsample in register form (bloomw_up10r: a wave walks a 62-column strip down 16 rows, sliding sums in
+    registers, neighbours by DPP) gives the tiled separable kernel's bits (bloomw_up10s: the same operations in the same
+    order), borders included."""
+    g = globals_for(W, H)
+    em = dev(random_rgba16(H, W, seed=29, hi=16.0))
+    shapes = [(H >> i, W >> i, 4) for i in range(4)]
+    outs = []
+    for reg in ("1", "0"):
+        monkeypatch.setenv("SOC_BLOOM_UP10_REG", reg)
+        soc.reload_tuning()
+        mips = [torch.zeros(sh, dtype=torch.float16, device=DEV) for sh in shapes]
+        out = torch.zeros_like(em)
+        soc.bloom_weighted_stage(g, em, mips, out, 0)
+        outs.append(out)
+    torch.cuda.synchronize()
+    monkeypatch.delenv("SOC_BLOOM_UP10_REG")
+    soc.reload_tuning()
+    assert torch.equal(outs[0], outs[1]), (outs[0] != outs[1]).float().mean().item()
+
+
 def test_bloom_weighted_in_place(soc):
     """output == emissive (the reference's in-place bloom) gives the separate-output result."""
     W, H = 968, 552
