@@ -414,8 +414,15 @@ constexpr int kTaaLdsRows = 4;                                   // rows per wor
 constexpr int kTaaLdsLanes = 64 * kTaaLdsRows;                    // (profiles/r03_ab_taa_lds.txt); the launch bound
 // SF (SOC_TAA_NBR=4, default): every staging load of a lane is issued before its first LDS store, so the staging costs
 // one memory latency instead of one per loop round (2 colour / velocity rounds and a depth round); the same values.
+#ifndef SOC_TAA_WAVES_PER_EU
+#define SOC_TAA_WAVES_PER_EU 0   // A/B builds: a VGPR budget for taa_lds (0: the compiler's choice, 86 VGPRs = 5 waves)
+#endif
 template <bool TM, int kTaaRows = kTaaLdsRows, bool SF = false>
-__global__ __launch_bounds__(64 * kTaaRows) void taa_lds(DImg target, DImg cur, DImg prev, DImg vel, DImg pvel, DImg depth,
+__global__ __launch_bounds__(64 * kTaaRows)
+#if SOC_TAA_WAVES_PER_EU
+__attribute__((amdgpu_waves_per_eu(SOC_TAA_WAVES_PER_EU)))
+#endif
+void taa_lds(DImg target, DImg cur, DImg prev, DImg vel, DImg pvel, DImg depth,
                                                          DImg vel_out, TaaParams p, TmOut tm) {
     constexpr int kTaaTR = kTaaRows + 2, NT = 64 * kTaaRows;   // staged rows y0 - 1 .. y0 + kTaaRows
     __shared__ uint4 ct[kTaaTR][kTaaTP];   // colour pairs
