@@ -118,10 +118,11 @@ __device__ __forceinline__ float bilerp_h(uint32_t a, uint32_t b, uint32_t c, ui
     const float bot = __builtin_fmaf(wx, sub_h<HI>(d, c), half_f<HI>(c));
     return __builtin_fmaf(wy, bot - top, top);
 }
-// 1/4 a + 1/2 b + 1/4 c of two f16 channels, fp32 (v_fma_mix_f32 straight from the packed halves)
-__device__ __forceinline__ v2f gauss_col(h2 a, h2 b, h2 c) {
-    return v2f{__builtin_fmaf((float)c.x, 0.25f, __builtin_fmaf((float)b.x, 0.5f, (float)a.x * 0.25f)),
-               __builtin_fmaf((float)c.y, 0.25f, __builtin_fmaf((float)b.y, 0.5f, (float)a.y * 0.25f))};
+// 4 x (1/4 a + 1/2 b + 1/4 c) of two f16 channels, fp32: c + (2 b + a), two v_fma_mix_f32 straight from the packed
+// halves. The bits of 4 x fma(c, 1/4, fma(b, 1/2, a / 4)) (round 5's form, one conversion and one multiply more):
+// scaling by a power of two commutes with each rounding (f16 inputs: no fp32 underflow or overflow), zeros' signs too.
+__device__ __forceinline__ v2f gauss_col4(h2 a, h2 b, h2 c) {
+    return v2f{(float)c.x + __builtin_fmaf((float)b.x, 2.0f, (float)a.x), (float)c.y + __builtin_fmaf((float)b.y, 2.0f, (float)a.y)};
 }
 
 // Same per-pixel result as taa_fast within the RGBA16F tolerance: the neighbourhood min/max run on
@@ -149,6 +150,8 @@ typedef uint32_t u3a4 __attribute__((ext_vector_type(3))) __attribute__((aligned
 #ifndef SOC_TAA_HIST_PAIR
 #define SOC_TAA_HIST_PAIR 1
 #endif
+// The history images as buffer resources with 32-bit row offsets (one v_mad_u32_u24 per row address instead of the
+// 64-bit pointer arithmetic: the launch checks that every image of the pair path fits the offset range, buf_ok).
 struct HistLoad {
     const DImg& prev;
     const DImg& pvel;
@@ -167,6 +170,9 @@ struct HistLoad {
     // Both pixels of the pair on the same history rows with adjacent footprints (texels i0, i0 + 1 and i0 + 1, i0 + 2):
     // the three texels of each row in one 16-B + one 8-B load (colour) or one 16-B + one 4-B load (velocity RG words),
     // instead of two 16-B (two 12-B) loads. The same texels.
+    // (Global loads: the same loads through a buffer resource with 32-bit offsets, 8 fewer VALU address operations,
+    // made the kernel ~4 % slower, DESIGN.md §11 r6.14: these scattered 16-B gathers cost more in the texture-address
+    // path as MUBUF loads.)
     __device__ __forceinline__ void pair(int which, const Axis& ax, const Axis& ay, u4a8 (&r0)[2], u4a8 (&r1)[2]) const {
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
@@ -189,21 +195,26 @@ struct HistLoad {
         }
     }
 };
-
 // The part of the pair kernels after the neighbourhood is loaded (:156-189 and the fused tone map): column min / max,
 // Gaussian column sums, the closest-depth texel, the history resolve and the stores. Cxy / Czw / D: the 3 x 4
-// neighbourhood (rows y+1, y, y-1; columns xl, x0, x0+1, xr); vel_at(x, y): the RG word of the current velocity texel;
+// neighbourhood (rows y+1, y, y-1; columns xl, x0, x0+1, xr); Sel::off(r, c): neighbourhood tap (r, c) as the
+// compile-time constant the closest-depth selection carries, vel(sel): the RG word of that tap's current velocity texel;
 // own_vel(): the lane's own velocity pair (the fused velocity-history copy); hist: the history row loads (HistLoad).
-template <bool TM, class VelAt, class OwnVel, class Hist>
+template <bool TM, class Sel, class VelAt, class OwnVel, class Hist>
 __device__ __forceinline__ void taa_pair_tail(const DImg& target, const DImg& prev, const DImg& pvel, const DImg& vel_out,
-                                              const TaaParams& p, const TmOut& tm, int x0, int y, int xl, int xr,
-                                              const int (&rows)[3], const h2 (&Cxy)[3][4], const h2 (&Czw)[3][4],
-                                              const float (&D)[3][4], float exposure, const VelAt& vel_at,
-                                              const OwnVel& own_vel, const Hist& hist) {
+                                              const TaaParams& p, const TmOut& tm, int x0, int y,
+                                              const h2 (&Cxy)[3][4], const h2 (&Czw)[3][4], const float (&D)[3][4],
+                                              float exposure, const VelAt& vel, const OwnVel& own_vel, const Hist& hist) {
     const int W = target.w, H = target.h;
-    const int colx[4] = {xl, x0, x0 + 1, xr};
     const float v = centre_uv_rn(y, H, p.rh);
     uint2 outp[2];
+    // closest depth in the reference order (oy = +1..-1, ox = +1..-1, from 1.0), last equal wins. The running form takes
+    // a tap iff it is <= every earlier tap (and 1.0); the last such tap is the last one equal to the minimum over all
+    // nine and 1.0, and no tap is taken iff that minimum is the 1.0 no tap equals. So: the minimum first (min3 chains;
+    // the six taps of the two shared columns once for the pair), then one compare + select per tap.
+    const float dshared = fminf(fminf(fminf(D[0][1], D[0][2]), fminf(D[1][1], D[1][2])), fminf(D[2][1], D[2][2]));
+    const float dmin[2] = {fminf(fminf(fminf(D[0][0], D[1][0]), fminf(D[2][0], 1.0f)), dshared),
+                           fminf(fminf(fminf(D[0][3], D[1][3]), fminf(D[2][3], 1.0f)), dshared)};
     // per pixel: the closest-depth velocity and the history footprint; then the history loads of the pair (combined
     // when the footprints are adjacent on the same rows, SOC_TAA_HIST_PAIR); then the resolve
     float velx_[2], vely_[2], vx_[2], vy_[2];
@@ -212,21 +223,15 @@ __device__ __forceinline__ void taa_pair_tail(const DImg& target, const DImg& pr
     for (int k = 0; k < 2; ++k) {
         const int x = x0 + k;
         const float u = centre_uv_rn(x, W, p.rw);
-        // closest depth in the reference order (oy = +1..-1, ox = +1..-1), last equal wins
-        // the winning tap as one index r * 4 + c (one select per tap instead of two)
-        float closest = 1.0f;
-        int bi = 4 + k + 1;
+        int sel = Sel::off(1, k + 1);   // the centre tap when no tap is taken
 #pragma unroll
         for (int r = 0; r < 3; ++r)
 #pragma unroll
             for (int ox = 1; ox > -2; --ox) {
                 const int c = k + 1 + ox;
-                const float d = D[r][c];
-                closest = fminf(d, closest);
-                bi = closest == d ? r * 4 + c : bi;
+                sel = D[r][c] == dmin[k] ? Sel::off(r, c) : sel;
             }
-        const int bx = colx[bi & 3], by = rows[bi >> 2];
-        const uint32_t vv = vel_at(bx, by);
+        const uint32_t vv = vel(sel);
         velx_[k] = half_f<0>(vv);
         vely_[k] = half_f<1>(vv);
         vx_[k] = u - velx_[k];
@@ -247,27 +252,31 @@ __device__ __forceinline__ void taa_pair_tail(const DImg& target, const DImg& pr
     }
     // column min / max (packed f16) and Gaussian column sums (fp32), while the history loads are in flight (round 6:
     // they depend on the closest-depth velocity, so issuing them first leaves this arithmetic to cover their latency;
-    // the same operations)
+    // the same operations). The min / max as IEEE minimum / maximum of three: one v_pk_minimum3_f16 / v_pk_maximum3_f16
+    // (gfx950) where min / max take two v_pk_min_f16 / v_pk_max_f16; the same values (the file is built without NaNs;
+    // -0 orders below +0, which min may not: a zero's sign in the clamp bounds at most).
     h2 nxy[4], nzw[4], xxy[4], xzw[4];
-    v2f sxy[4], szw[4];
+    v2f sxy[4], szw[4];   // 4 x the Gaussian column sums
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-        nxy[c] = __builtin_elementwise_min(__builtin_elementwise_min(Cxy[0][c], Cxy[1][c]), Cxy[2][c]);
-        nzw[c] = __builtin_elementwise_min(__builtin_elementwise_min(Czw[0][c], Czw[1][c]), Czw[2][c]);
-        xxy[c] = __builtin_elementwise_max(__builtin_elementwise_max(Cxy[0][c], Cxy[1][c]), Cxy[2][c]);
-        xzw[c] = __builtin_elementwise_max(__builtin_elementwise_max(Czw[0][c], Czw[1][c]), Czw[2][c]);
-        sxy[c] = gauss_col(Cxy[0][c], Cxy[1][c], Cxy[2][c]);
-        szw[c] = gauss_col(Czw[0][c], Czw[1][c], Czw[2][c]);
+        nxy[c] = __builtin_elementwise_minimum(__builtin_elementwise_minimum(Cxy[0][c], Cxy[1][c]), Cxy[2][c]);
+        nzw[c] = __builtin_elementwise_minimum(__builtin_elementwise_minimum(Czw[0][c], Czw[1][c]), Czw[2][c]);
+        xxy[c] = __builtin_elementwise_maximum(__builtin_elementwise_maximum(Cxy[0][c], Cxy[1][c]), Cxy[2][c]);
+        xzw[c] = __builtin_elementwise_maximum(__builtin_elementwise_maximum(Czw[0][c], Czw[1][c]), Czw[2][c]);
+        sxy[c] = gauss_col4(Cxy[0][c], Cxy[1][c], Cxy[2][c]);
+        szw[c] = gauss_col4(Czw[0][c], Czw[1][c], Czw[2][c]);
     }
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-        const h2 mnxy = __builtin_elementwise_min(__builtin_elementwise_min(nxy[k], nxy[k + 1]), nxy[k + 2]);
-        const h2 mnzw = __builtin_elementwise_min(__builtin_elementwise_min(nzw[k], nzw[k + 1]), nzw[k + 2]);
-        const h2 mxxy = __builtin_elementwise_max(__builtin_elementwise_max(xxy[k], xxy[k + 1]), xxy[k + 2]);
-        const h2 mxzw = __builtin_elementwise_max(__builtin_elementwise_max(xzw[k], xzw[k + 1]), xzw[k + 2]);
-        const v2f q = v2f{0.25f, 0.25f}, hlf = v2f{0.5f, 0.5f};
-        const v2f bxy = __builtin_elementwise_fma(sxy[k + 2], q, __builtin_elementwise_fma(sxy[k + 1], hlf, sxy[k] * q));
-        const v2f bzw = __builtin_elementwise_fma(szw[k + 2], q, __builtin_elementwise_fma(szw[k + 1], hlf, szw[k] * q));
+        const h2 mnxy = __builtin_elementwise_minimum(__builtin_elementwise_minimum(nxy[k], nxy[k + 1]), nxy[k + 2]);
+        const h2 mnzw = __builtin_elementwise_minimum(__builtin_elementwise_minimum(nzw[k], nzw[k + 1]), nzw[k + 2]);
+        const h2 mxxy = __builtin_elementwise_maximum(__builtin_elementwise_maximum(xxy[k], xxy[k + 1]), xxy[k + 2]);
+        const h2 mxzw = __builtin_elementwise_maximum(__builtin_elementwise_maximum(xzw[k], xzw[k + 1]), xzw[k + 2]);
+        // 16 x the blurred colour: (s2 + (2 s1 + s0)) of the 4x column sums, whose 1/16 is taken exactly in (b - o) below
+        // (round 5: fma(s2, 1/4, fma(s1, 1/2, s0 / 4)) of the column sums; the same bits, see gauss_col4)
+        const v2f two = v2f{2.0f, 2.0f};
+        const v2f bxy = __builtin_elementwise_fma(sxy[k + 1], two, sxy[k]) + sxy[k + 2];
+        const v2f bzw = __builtin_elementwise_fma(szw[k + 1], two, szw[k]) + szw[k + 2];
         const uint32_t cxy = __builtin_bit_cast(uint32_t, Cxy[1][k + 2]), czw = __builtin_bit_cast(uint32_t, Czw[1][k + 2]);
         // quirk Q7: the (+1, 0) neighbour is "the" colour
         const float velx = velx_[k], vely = vely_[k];
@@ -300,7 +309,9 @@ __device__ __forceinline__ void taa_pair_tail(const DImg& target, const DImg& pr
         const float vlen = __builtin_amdgcn_sqrtf(__builtin_fmaf(dvx, dvx, dvy * dvy));
         const float dis = clampf((vlen - 0.001f) * 10.0f, 0.0f, 1.0f);
         const v2f dd = v2f{dis, dis};
-        const v2f rxy = __builtin_elementwise_fma(bxy - oxy, dd, oxy), rzw = __builtin_elementwise_fma(bzw - ozw, dd, ozw);
+        const v2f sixteenth = v2f{0.0625f, 0.0625f};
+        const v2f rxy = __builtin_elementwise_fma(__builtin_elementwise_fma(bxy, sixteenth, -oxy), dd, oxy),
+                  rzw = __builtin_elementwise_fma(__builtin_elementwise_fma(bzw, sixteenth, -ozw), dd, ozw);
         outp[k] = pack_h4(f4{rxy.x, rxy.y, rzw.x, rzw.y});
     }
     row_ptr_w<uint4>(target, y)[x0 >> 1] = uint4{outp[0].x, outp[0].y, outp[1].x, outp[1].y};
@@ -317,6 +328,11 @@ __device__ __forceinline__ void taa_pair_tail(const DImg& target, const DImg& pr
             uint2{pack_unorm8x4(f4{c0.x, c0.y, c0.z, 1.0f}), pack_unorm8x4(f4{c1.x, c1.y, c1.z, 1.0f})};
     }
 }
+
+// The closest-depth tap as r * 4 + c (taa_pair2: the row and column are looked up from it).
+struct SelRC {
+    static constexpr int off(int r, int c) { return r * 4 + c; }
+};
 
 // Lane i's left neighbour column (x0 - 1) is lane i-1's second pixel and its right one (x0 + 2) lane
 // i+1's first: with NBR the neighbourhood's side columns come from the adjacent lanes through DPP wave
@@ -395,9 +411,10 @@ __global__ __launch_bounds__(kWorkgroup) void taa_pair2(DImg target, DImg cur, D
         D[r][3] = dr;
     }
     if (NBR && !inside_x) return;   // past the image: only fed its neighbours' shifts
-    taa_pair_tail<TM>(target, prev, pvel, vel_out, p, tm, x0, y, xl, xr, rows, Cxy, Czw, D, exposure,
-                      [&](int bx, int by) { return row_ptr<uint32_t>(vel, by)[2 * bx]; },
-                      [&]() { return row_ptr<uint4>(vel, y)[x0 >> 1]; }, HistLoad{prev, pvel});
+    const int colx[4] = {xl, x0, x0 + 1, xr};
+    taa_pair_tail<TM, SelRC>(target, prev, pvel, vel_out, p, tm, x0, y, Cxy, Czw, D, exposure,
+                             [&](int s) { return row_ptr<uint32_t>(vel, rows[s >> 2])[2 * colx[s & 3]]; },
+                             [&]() { return row_ptr<uint4>(vel, y)[x0 >> 1]; }, HistLoad{prev, pvel});
 }
 
 // LDS-staged neighbourhood: a workgroup of 64 x 4 lanes (128 x 4 output pixels, a pixel pair per lane) stages the
@@ -412,6 +429,27 @@ constexpr int kTaaTQ = kTaaPairs / 2 + 2;                         // staged dept
 
 constexpr int kTaaLdsRows = 4;                                   // rows per workgroup: 4 measured against 2 and 8
 constexpr int kTaaLdsLanes = 64 * kTaaLdsRows;                    // (profiles/r03_ab_taa_lds.txt); the launch bound
+// Image-border copies in the tiles: the staged pair left of the image holds texel 0 twice and the one right of it texel
+// W - 1 twice, the depth quads likewise (and the last quad of a row with W % 4 == 2 has texel W - 1 at column W), so the
+// lanes at a border read their clamped side columns and closest-depth velocity texels from the tiles like every other
+// lane: no per-lane border selects (round 5: 18 per lane). Applied in the border workgroups only (a uniform branch).
+__device__ __forceinline__ uint4 border_pair(uint4 v, int p, int npairs) {
+    if (p < 0) return uint4{v.x, v.y, v.x, v.y};            // v: pair 0 (the clamped staging)
+    if (p >= npairs) return uint4{v.z, v.w, v.z, v.w};      // v: pair npairs - 1
+    return v;
+}
+__device__ __forceinline__ float4 border_quad(float4 d, int q, int nquads, int W) {
+    if (q < 0) return float4{d.x, d.x, d.x, d.x};
+    if (q >= nquads) return float4{d.w, d.w, d.w, d.w};     // read only when W % 4 == 0: d.w is texel W - 1
+    if (4 * q + 2 == W) d.z = d.y;
+    return d;
+}
+// The closest-depth tap (r, c) as its word offset in the velocity tile from the lane's (ty, pl) base: tile row ty + 2 - r,
+// column c = 0..3 at pair pl word 2, pair pl + 1 words 0 / 2, pair pl + 2 word 0 (the RG word of the texel).
+struct SelTile {
+    static constexpr int off(int r, int c) { return (2 - r) * kTaaTP * 4 + 2 * c; }
+};
+
 // SF (SOC_TAA_NBR=4, default): every staging load of a lane is issued before its first LDS store, so the staging costs
 // one memory latency instead of one per loop round (2 colour / velocity rounds and a depth round); the same values.
 #ifndef SOC_TAA_WAVES_PER_EU
@@ -434,8 +472,8 @@ void taa_lds(DImg target, DImg cur, DImg prev, DImg vel, DImg pvel, DImg depth,
     const int tid = threadIdx.x + threadIdx.y * 64;
     const int p0 = tbx * kTaaPairs, y0 = tby * kTaaRows, q0 = tbx * (kTaaPairs / 2);
     const int npairs = W >> 1, nquads = (W + 3) >> 2;
-    // staging: rows clamped into the image, pairs / quads clamped into the row (the clamped copies are never read:
-    // the border columns come from the lane's own pixels, as in taa_pair2)
+    // staging: rows clamped into the image, pairs / quads clamped into the row (border_pair / border_quad)
+    const bool edge = p0 == 0 || 2 * (p0 + kTaaTP) + 8 >= W;   // the tiles reach an image border
     auto depth_quad = [&](int i) {
         const int r = i / kTaaTQ, c = i - r * kTaaTQ;
         const int sy = min(max(y0 - 1 + r, 0), H - 1), sq = min(max(q0 - 1 + c, 0), nquads - 1);
@@ -446,30 +484,41 @@ void taa_lds(DImg target, DImg cur, DImg prev, DImg vel, DImg pvel, DImg depth,
     if constexpr (SF) {
         constexpr int NP = kTaaTR * kTaaTP, ND = kTaaTR * kTaaTQ;
         static_assert(NP > NT && NP <= 2 * NT && ND <= NT, "two colour / velocity rounds and one depth round");
-        auto pair_off = [&](int i, int& r, int& c, const uint4*& cs, const uint4*& vs) {
+        // 32-bit byte offsets from the image bases (the launch checks their range: buf_ok)
+        auto pair_off = [&](int i, int& r, int& c, int& oc, int& ov) {
             r = i / kTaaTP;
             c = i - r * kTaaTP;
             const int sy = min(max(y0 - 1 + r, 0), H - 1), sp = min(max(p0 - 1 + c, 0), npairs - 1);
-            cs = row_ptr<uint4>(cur, sy) + sp;
-            vs = row_ptr<uint4>(vel, sy) + sp;
+            oc = __mul24(sy, cur.pitch) + sp * 16;
+            ov = __mul24(sy, vel.pitch) + sp * 16;
         };
-        int r0, c0, r1, c1;
-        const uint4 *cs0, *vs0, *cs1, *vs1;
-        pair_off(tid, r0, c0, cs0, vs0);
+        auto ldc = [&](int o) { return *reinterpret_cast<const uint4*>(cur.data + o); };
+        auto ldv = [&](int o) { return *reinterpret_cast<const uint4*>(vel.data + o); };
+        int r0, c0, r1, c1, oc0, ov0, oc1, ov1;
+        pair_off(tid, r0, c0, oc0, ov0);
         const bool second = tid + NT < NP, hasd = tid < ND;
-        pair_off(second ? tid + NT : tid, r1, c1, cs1, vs1);
-        const uint4 ca = *cs0, va = *vs0;
-        uint4 cb = uint4{0u, 0u, 0u, 0u}, vb = cb;
-        if (second) { cb = *cs1; vb = *vs1; }
+        pair_off(second ? tid + NT : tid, r1, c1, oc1, ov1);
+        uint4 ca = ldc(oc0), va = ldv(ov0);
+        uint4 cb, vb;   // set and stored only when second
+        if (second) { cb = ldc(oc1); vb = ldv(ov1); }
         // the depth quad as one 16-B buffer load even for the last quad of a row with W % 4 != 0: its texels past the
         // row end (the next row's, or 0 past the image) are never read (the border columns come from the pair itself)
-        float4 dq = float4{0.0f, 0.0f, 0.0f, 0.0f};
+        float4 dq;   // set and stored only when hasd
         if (hasd) {
             const int r = tid / kTaaTQ, c = tid - r * kTaaTQ;
             const int sy = min(max(y0 - 1 + r, 0), H - 1), sq = min(max(q0 - 1 + c, 0), nquads - 1);
             const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(depth.data, 0, depth.pitch * depth.h, 0x00020000);
             const auto w = __builtin_amdgcn_raw_buffer_load_b128(rs, __mul24(sy, depth.pitch) + 16 * sq, 0, 0);
             dq = make_float4(__uint_as_float(w[0]), __uint_as_float(w[1]), __uint_as_float(w[2]), __uint_as_float(w[3]));
+        }
+        if (edge) {
+            ca = border_pair(ca, p0 - 1 + c0, npairs);
+            va = border_pair(va, p0 - 1 + c0, npairs);
+            if (second) {
+                cb = border_pair(cb, p0 - 1 + c1, npairs);
+                vb = border_pair(vb, p0 - 1 + c1, npairs);
+            }
+            if (hasd) dq = border_quad(dq, q0 - 1 + tid % kTaaTQ, nquads, W);
         }
         ct[r0][c0] = ca;
         vt[r0][c0] = va;
@@ -479,35 +528,37 @@ void taa_lds(DImg target, DImg cur, DImg prev, DImg vel, DImg pvel, DImg depth,
         for (int i = tid; i < kTaaTR * kTaaTP; i += NT) {
             const int r = i / kTaaTP, c = i - r * kTaaTP;
             const int sy = min(max(y0 - 1 + r, 0), H - 1), sp = min(max(p0 - 1 + c, 0), npairs - 1);
-            ct[r][c] = row_ptr<uint4>(cur, sy)[sp];
-            vt[r][c] = row_ptr<uint4>(vel, sy)[sp];
+            uint4 cv = row_ptr<uint4>(cur, sy)[sp], vv = row_ptr<uint4>(vel, sy)[sp];
+            if (edge) {
+                cv = border_pair(cv, p0 - 1 + c, npairs);
+                vv = border_pair(vv, p0 - 1 + c, npairs);
+            }
+            ct[r][c] = cv;
+            vt[r][c] = vv;
         }
         for (int i = tid; i < kTaaTR * kTaaTQ; i += NT) {
             const int r = i / kTaaTQ, c = i - r * kTaaTQ;
-            dt[r][c] = depth_quad(i);
+            float4 dq = depth_quad(i);
+            if (edge) dq = border_quad(dq, q0 - 1 + c, nquads, W);
+            dt[r][c] = dq;
         }
     }
     __syncthreads();
     const int pl = threadIdx.x, ty = threadIdx.y;
     const int x0 = 2 * (p0 + pl), y = y0 + ty;
     if (x0 >= W || y >= H) return;
-    const int xl = max(x0 - 1, 0), xr = min(x0 + 2, W - 1);
     const float* dtf = reinterpret_cast<const float*>(dt);
     const int dbase = 4 * (q0 - 1);   // image column of dtf[r * 4 * kTaaTQ + 0]
     h2 Cxy[3][4], Czw[3][4];
     float D[3][4];
-    int rows[3];
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
-        const int tr = ty + 2 - r;   // tile row of image row y + 1 - r
-        rows[r] = min(max(y + 1 - r, 0), H - 1);
+        const int tr = ty + 2 - r;   // tile row of image row y + 1 - r (clamped)
         const uint4 mid = ct[tr][pl + 1];
-        uint2 L = uint2{ct[tr][pl].z, ct[tr][pl].w}, R = uint2{ct[tr][pl + 2].x, ct[tr][pl + 2].y};
+        const uint2 L = uint2{ct[tr][pl].z, ct[tr][pl].w}, R = uint2{ct[tr][pl + 2].x, ct[tr][pl + 2].y};   // border copies
         const float* drow = dtf + tr * 4 * kTaaTQ - dbase;
         const float2 dmid = *reinterpret_cast<const float2*>(drow + x0);
-        float dl = drow[x0 - 1], dr = drow[x0 + 2];
-        if (x0 == 0) { L = uint2{mid.x, mid.y}; dl = dmid.x; }           // image borders: the clamped side column is the
-        if (x0 + 2 >= W) { R = uint2{mid.z, mid.w}; dr = dmid.y; }      // pair's own pixel
+        const float dl = drow[x0 - 1], dr = drow[x0 + 2];
         Cxy[r][0] = as_h2(L.x);
         Czw[r][0] = as_h2(L.y);
         Cxy[r][1] = as_h2(mid.x);
@@ -523,12 +574,10 @@ void taa_lds(DImg target, DImg cur, DImg prev, DImg vel, DImg pvel, DImg depth,
     }
     const float exposure = TM ? tm.ae->exposure : 0.0f;
     const uint32_t* vtw = reinterpret_cast<const uint32_t*>(vt);
-    taa_pair_tail<TM>(target, prev, pvel, vel_out, p, tm, x0, y, xl, xr, rows, Cxy, Czw, D, exposure,
-                      [&](int bx, int by) {   // the RG word of texel (bx, by): pair bx / 2, word 2 (bx & 1)
-                          const int tr = by - (y0 - 1), c = (bx >> 1) - (p0 - 1);
-                          return vtw[(tr * kTaaTP + c) * 4 + 2 * (bx & 1)];
-                      },
-                      [&]() { return vt[ty + 1][pl + 1]; }, HistLoad{prev, pvel});
+    const int vbase = (ty * kTaaTP + pl) * 4 + 2;
+    taa_pair_tail<TM, SelTile>(target, prev, pvel, vel_out, p, tm, x0, y, Cxy, Czw, D, exposure,
+                               [&](int s) { return vtw[vbase + s]; },
+                               [&]() { return vt[ty + 1][pl + 1]; }, HistLoad{prev, pvel});
 }
 
 __global__ __launch_bounds__(kWorkgroup) void taa_generic(DImg target, DImg cur, DImg prev, DImg vel, DImg pvel, DImg depth,
@@ -616,10 +665,14 @@ int taa_launch(const soc_globals* g, soc_img target, soc_img current_color, soc_
     dim3 blk(BX, BY), grd(ceil_div(W, BX), ceil_div(H, BY));
     DImg vo = velocity_history_out.data ? dimg(velocity_history_out) : DImg{nullptr, 0, 0, 0};
     auto a16 = [](const soc_img& im) { return (reinterpret_cast<uintptr_t>(im.data) & 15u) == 0 && (im.pitch_bytes & 15) == 0; };
+    // the pair kernels address the staged images (and the depth quads through a buffer resource) with 32-bit offsets
+    // (a signed 24-bit row x pitch product)
+    auto buf_ok = [](const soc_img& im) { return (long long)im.pitch_bytes * im.height < (1ll << 31) && im.pitch_bytes < (1 << 23); };
     const bool pair = fast && W % 2 == 0 && a16(target) && a16(current_color) && a16(current_velocity) &&
                       (reinterpret_cast<uintptr_t>(depth.data) & 7u) == 0 && (depth.pitch_bytes & 7) == 0 &&
                       (!velocity_history_out.data || a16(velocity_history_out)) && previous_color.width >= 2 &&
-                      previous_velocity.width == previous_color.width && previous_velocity.height == previous_color.height;
+                      previous_velocity.width == previous_color.width && previous_velocity.height == previous_color.height &&
+                      buf_ok(current_color) && buf_ok(current_velocity) && buf_ok(depth);
     if (tm && !pair) return 1;
     if (pair) {
         // 32 x 8 lanes (64 x 8 pixels): the 3-row neighbourhood reloads 10 rows per 8 instead of 6 per 4
