@@ -180,7 +180,7 @@ struct HistLoad {
             u4a8 a, b;
             if (which) {
                 const uint32_t* w = reinterpret_cast<const uint32_t*>(row_ptr<uint2>(pvel, row) + ax.i0);
-                const u4a8 q = *reinterpret_cast<const u4a8*>(w);
+                const u3a4 q = *reinterpret_cast<const u3a4*>(w);   // words 0..2 (the RG words are 0, 2, 4): 12 B, not 16
                 const uint32_t w4 = w[4];
                 a = u4a8{q.x, q.y, q.z, 0u};
                 b = u4a8{q.z, 0u, w4, 0u};
