@@ -122,9 +122,64 @@ __device__ __forceinline__ void up11_pair(const uint2 (*t)[TW], int cx, int cy, 
 // ================================================================================================
 // W1: emissive (W x H) -> [mip0, W x H, LDS] -> mip1 (W/2 x H/2)
 // ================================================================================================
-constexpr int W1_OW = 32, W1_OH = 8;                          // mip1 outputs per workgroup
-constexpr int W1_MW = 2 * W1_OW + 4, W1_MH = 2 * W1_OH + 4;   // mip0 tile 68 x 20, origin (2 X0 - 2, 2 Y0 - 2)
-constexpr int W1_EW = W1_MW + 4, W1_EH = W1_MH + 4;           // emissive tile 72 x 24, origin (2 X0 - 4, 2 Y0 - 4)
+// SOC_BLOOM_W1_REG (default 1): the 1:1 stage register-blocked (down11_runs): 30 x 8 mip1 outputs per workgroup, so the
+// mip0 tile is 64 x 20 and each lane filters a run of 5 mip0 entries of one column at row stride 2 (r, r + 2, ...),
+// whose footprints share 3 of their 5 rows: 5 new LDS reads per entry instead of 13 (the stage is bound by its LDS
+// reads); the same taps in down11's order, so the same bits. 0 = 32 x 8 outputs, every entry from its 13 LDS taps.
+#ifndef SOC_BLOOM_W1_REG
+#define SOC_BLOOM_W1_REG 1
+#endif
+constexpr int W1_OW = SOC_BLOOM_W1_REG ? 30 : 32, W1_OH = 8;   // mip1 outputs per workgroup
+constexpr int W1_MW = 2 * W1_OW + 4, W1_MH = 2 * W1_OH + 4;   // mip0 tile 64 (68) x 20, origin (2 X0 - 2, 2 Y0 - 2)
+constexpr int W1_EW = W1_MW + 4, W1_EH = W1_MH + 4;           // emissive tile 68 (72) x 24, origin (2 X0 - 4, 2 Y0 - 4)
+static_assert(!SOC_BLOOM_W1_REG || (W1_MW == 64 && W1_MH == 20), "down11_runs: 64 columns x 2 row parities x 2 runs of 5");
+
+// down11 of the mip0 entries (c, r), (c, r + 2), ..., (c, r + 8) of the tile (rows r..r+8 inside the tile: no vertical
+// clamping in this workgroup), centre column cx (the clamped image column, tile-relative): a sliding window of the five
+// footprint rows (three texels on the centre's row parity, two on the other), two rows loaded per entry after the first.
+// Each entry's 13 fmas in down11's order.
+template <int TW, int MW>
+__device__ __forceinline__ void down11_runs(const uint2 (*t)[TW], uint2 (*mt)[MW], int c, int r, int cx) {
+    uint2 e0[3], o1[2], e2[3], o3[2], e4[3];
+    const int cy0 = r + 2;   // emissive-tile row of the first entry's centre
+    auto even = [&](int y, uint2 (&e)[3]) { e[0] = t[y][cx - 2]; e[1] = t[y][cx]; e[2] = t[y][cx + 2]; };
+    auto odd = [&](int y, uint2 (&o)[2]) { o[0] = t[y][cx - 1]; o[1] = t[y][cx + 1]; };
+    even(cy0 - 2, e0);
+    odd(cy0 - 1, o1);
+    even(cy0, e2);
+    odd(cy0 + 1, o3);
+    even(cy0 + 2, e4);
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        C3 a{0.0f, 0.0f, 0.0f};
+        madd(a, e2[1], 0.125f);
+        madd(a, e0[0], 0.03125f);
+        madd(a, e0[2], 0.03125f);
+        madd(a, e4[0], 0.03125f);
+        madd(a, e4[2], 0.03125f);
+        madd(a, e0[1], 0.0625f);
+        madd(a, e2[0], 0.0625f);
+        madd(a, e2[2], 0.0625f);
+        madd(a, e4[1], 0.0625f);
+        madd(a, o1[0], 0.125f);
+        madd(a, o1[1], 0.125f);
+        madd(a, o3[0], 0.125f);
+        madd(a, o3[1], 0.125f);
+        mt[r + 2 * j][c] = pack3(a);
+        if (j < 4) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                e0[k] = e2[k];
+                e2[k] = e4[k];
+            }
+            o1[0] = o3[0];
+            o1[1] = o3[1];
+            const int cy = cy0 + 2 * (j + 1);
+            odd(cy + 1, o3);
+            even(cy + 2, e4);
+        }
+    }
+}
 
 // W1, persistent: each workgroup walks tiles t = blockIdx.x, + gridDim.x, ... (XCD-aware contiguous eighths, as
 // swz = 1), and loads the NEXT tile's emissive texels into registers while it filters the current one from LDS, so
@@ -171,15 +226,22 @@ __global__ __launch_bounds__(kWorkgroup) void bloomw_down01p(DImg E, DImg M1, in
         int X0, Y0;
         tile_origin(t, X0, Y0);
         const int mx0 = 2 * X0 - 2, my0 = 2 * Y0 - 2, ex0 = mx0 - 2, ey0 = my0 - 2;
+        // register-blocked runs unless the tile's mip0 rows reach past the image's top or bottom (there a clamped row
+        // repeats, which the fixed row stride does not follow): a uniform branch
+        if (SOC_BLOOM_W1_REG && my0 >= 0 && my0 + W1_MH <= E.h) {
+            const int c = tid & 63, par = (tid >> 6) & 1, half = tid >> 7;
+            if constexpr (SOC_BLOOM_W1_REG)
+                down11_runs<W1_EW, W1_MW>(et, mt, c, par + 10 * half, clampi(mx0 + c, 0, E.w - 1) - ex0);
+        } else
         for (int i = tid; i < W1_MW * W1_MH; i += 256) {
             const int r = i / W1_MW, c = i - r * W1_MW;
             const int cx = clampi(mx0 + c, 0, E.w - 1) - ex0, cy = clampi(my0 + r, 0, E.h - 1) - ey0;
             mt[r][c] = pack3(down11<W1_EW>(et, cx, cy));
         }
         __syncthreads();
-        const int ox = tid & (W1_OW - 1), oy = tid / W1_OW;
+        const int oy = tid / W1_OW, ox = tid - oy * W1_OW;
         const int X = X0 + ox, Y = Y0 + oy;
-        if (X < M1.w && Y < M1.h) row_ptr_w<uint2>(M1, Y)[X] = pack3(down21<W1_MW>(mt, 2 * ox, 2 * oy));
+        if (oy < W1_OH && X < M1.w && Y < M1.h) row_ptr_w<uint2>(M1, Y)[X] = pack3(down21<W1_MW>(mt, 2 * ox, 2 * oy));
         __syncthreads();   // et / mt are rewritten by the next tile
     }
 }
