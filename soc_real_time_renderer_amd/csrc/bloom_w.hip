@@ -122,17 +122,18 @@ __device__ __forceinline__ void up11_pair(const uint2 (*t)[TW], int cx, int cy, 
 // ================================================================================================
 // W1: emissive (W x H) -> [mip0, W x H, LDS] -> mip1 (W/2 x H/2)
 // ================================================================================================
-// SOC_BLOOM_W1_REG (default 1): the 1:1 stage register-blocked (down11_runs): 30 x 8 mip1 outputs per workgroup, so the
-// mip0 tile is 64 x 20 and each lane filters a run of 5 mip0 entries of one column at row stride 2 (r, r + 2, ...),
-// whose footprints share 3 of their 5 rows: 5 new LDS reads per entry instead of 13 (the stage is bound by its LDS
-// reads); the same taps in down11's order, so the same bits. 0 = 32 x 8 outputs, every entry from its 13 LDS taps.
-#ifndef SOC_BLOOM_W1_REG
-#define SOC_BLOOM_W1_REG 1
-#endif
-constexpr int W1_OW = SOC_BLOOM_W1_REG ? 30 : 32, W1_OH = 8;   // mip1 outputs per workgroup
-constexpr int W1_MW = 2 * W1_OW + 4, W1_MH = 2 * W1_OH + 4;   // mip0 tile 64 (68) x 20, origin (2 X0 - 2, 2 Y0 - 2)
-constexpr int W1_EW = W1_MW + 4, W1_EH = W1_MH + 4;           // emissive tile 68 (72) x 24, origin (2 X0 - 4, 2 Y0 - 4)
-static_assert(!SOC_BLOOM_W1_REG || (W1_MW == 64 && W1_MH == 20), "down11_runs: 64 columns x 2 row parities x 2 runs of 5");
+// REG (tuning knob SOC_BLOOM_W1_REG, default 1): the 1:1 stage register-blocked (down11_runs): 30 x 8 mip1 outputs per
+// workgroup, so the mip0 tile is 64 x 20 and each lane filters a run of 5 mip0 entries of one column at row stride 2
+// (r, r + 2, ...), whose footprints share 3 of their 5 rows: 5 new LDS reads per entry instead of 13 (the stage is bound
+// by its LDS reads); the same taps in down11's order, so the same bits (tests/test_gpu_parity.py). 0 = 32 x 8 outputs,
+// every entry from its 13 LDS taps.
+template <bool REG>
+struct W1 {
+    static constexpr int OW = REG ? 30 : 32, OH = 8;       // mip1 outputs per workgroup
+    static constexpr int MW = 2 * OW + 4, MH = 2 * OH + 4;  // mip0 tile 64 (68) x 20, origin (2 X0 - 2, 2 Y0 - 2)
+    static constexpr int EW = MW + 4, EH = MH + 4;          // emissive tile 68 (72) x 24, origin (2 X0 - 4, 2 Y0 - 4)
+    static_assert(!REG || (MW == 64 && MH == 20), "down11_runs: 64 columns x 2 row parities x 2 runs of 5");
+};
 
 // down11 of the mip0 entries (c, r), (c, r + 2), ..., (c, r + 8) of the tile (rows r..r+8 inside the tile: no vertical
 // clamping in this workgroup), centre column cx (the clamped image column, tile-relative): a sliding window of the five
@@ -186,7 +187,10 @@ __device__ __forceinline__ void down11_runs(const uint2 (*t)[TW], uint2 (*mt)[MW
 // the tile loads' latency hides behind the filter instead of being waited on (the one-tile kernel waits on its
 // loads and barriers for 61 % of its wave cycles, profiles/r03_sq_stalls.json: 47.5 -> 42.9 us serial at 4K). The
 // same arithmetic and bits as that one-tile-per-workgroup kernel.
+template <bool REG>
 __global__ __launch_bounds__(kWorkgroup) void bloomw_down01p(DImg E, DImg M1, int ntx, int nty) {
+    constexpr int W1_OW = W1<REG>::OW, W1_OH = W1<REG>::OH, W1_MW = W1<REG>::MW, W1_MH = W1<REG>::MH, W1_EW = W1<REG>::EW,
+                  W1_EH = W1<REG>::EH;
     __shared__ uint2 et[W1_EH][W1_EW];
     __shared__ uint2 mt[W1_MH][W1_MW];
     constexpr int NT = W1_EW * W1_EH, KR = (NT + 255) / 256;
@@ -228,9 +232,9 @@ __global__ __launch_bounds__(kWorkgroup) void bloomw_down01p(DImg E, DImg M1, in
         const int mx0 = 2 * X0 - 2, my0 = 2 * Y0 - 2, ex0 = mx0 - 2, ey0 = my0 - 2;
         // register-blocked runs unless the tile's mip0 rows reach past the image's top or bottom (there a clamped row
         // repeats, which the fixed row stride does not follow): a uniform branch
-        if (SOC_BLOOM_W1_REG && my0 >= 0 && my0 + W1_MH <= E.h) {
+        if (REG && my0 >= 0 && my0 + W1_MH <= E.h) {
             const int c = tid & 63, par = (tid >> 6) & 1, half = tid >> 7;
-            if constexpr (SOC_BLOOM_W1_REG)
+            if constexpr (REG)
                 down11_runs<W1_EW, W1_MW>(et, mt, c, par + 10 * half, clampi(mx0 + c, 0, E.w - 1) - ex0);
         } else
         for (int i = tid; i < W1_MW * W1_MH; i += 256) {
@@ -578,6 +582,7 @@ __global__ __launch_bounds__(kWorkgroup) void bloomw_up10r(DImg S1, DImg O, int 
 
 // Workgroups of 256 lanes of bloomw_down01p resident on the whole device at once (the persistent kernel's grid bound),
 // queried once per device and cached (the occupancy query is not on the per-frame enqueue path).
+template <bool REG>
 int down01p_resident_set() {
     constexpr int kMaxDevices = 64;
     static int cached[kMaxDevices] = {};
@@ -585,7 +590,7 @@ int down01p_resident_set() {
     (void)hipGetDevice(&dev);
     if (dev >= 0 && dev < kMaxDevices && cached[dev]) return cached[dev];
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, bloomw_down01p, 256, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, bloomw_down01p<REG>, 256, 0);
     const int n = std::max(per, 1) * cus;
     if (dev >= 0 && dev < kMaxDevices) cached[dev] = n;
     return n;
@@ -600,9 +605,14 @@ int launch_bloom_weighted(const soc_img& emissive, const soc_img* mips, const so
     const int swz = 1;   // XCD-aware order: halo re-reads served by L2 (2.0x -> 1.0x HBM traffic)
     if (stage == 0 || stage == 1) {
         // persistent: one resident set of workgroups (a multiple of 8, so a workgroup's tiles stay on its XCD)
-        const int ntx = ceil_div(mips[1].width, W1_OW), nty = ceil_div(mips[1].height, W1_OH);
-        const int grid = std::max(8, (std::min(ntx * nty, down01p_resident_set()) / 8) * 8);
-        launch("bloomw_down01p", kWorkgroup, bloomw_down01p, grid, kWorkgroup, 0, s, E, M1, ntx, nty);
+        auto w1 = [&](auto reg) {
+            constexpr bool R = decltype(reg)::value;
+            const int ntx = ceil_div(mips[1].width, W1<R>::OW), nty = ceil_div(mips[1].height, W1<R>::OH);
+            const int grid = std::max(8, (std::min(ntx * nty, down01p_resident_set<R>()) / 8) * 8);
+            launch("bloomw_down01p", kWorkgroup, bloomw_down01p<R>, grid, kWorkgroup, 0, s, E, M1, ntx, nty);
+        };
+        if (tuning_knob("SOC_BLOOM_W1_REG", 1)) w1(std::true_type{});
+        else w1(std::false_type{});
     }
     if (stage == 0 || stage == 2) {
         dim3 g(ceil_div(mips[3].width, W2_OW), ceil_div(mips[3].height, W2_OH));
