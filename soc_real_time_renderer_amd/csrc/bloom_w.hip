@@ -122,24 +122,27 @@ __device__ __forceinline__ void up11_pair(const uint2 (*t)[TW], int cx, int cy, 
 // ================================================================================================
 // W1: emissive (W x H) -> [mip0, W x H, LDS] -> mip1 (W/2 x H/2)
 // ================================================================================================
-// REG (tuning knob SOC_BLOOM_W1_REG, default 1): the 1:1 stage register-blocked (down11_runs): 30 x 8 mip1 outputs per
+// MODE (tuning knob SOC_BLOOM_W1_REG): 1 = the 1:1 stage register-blocked (down11_runs): 30 x 8 mip1 outputs per
 // workgroup, so the mip0 tile is 64 x 20 and each lane filters a run of 5 mip0 entries of one column at row stride 2
 // (r, r + 2, ...), whose footprints share 3 of their 5 rows: 5 new LDS reads per entry instead of 13 (the stage is bound
-// by its LDS reads); the same taps in down11's order, so the same bits (tests/test_gpu_parity.py). 0 = 32 x 8 outputs,
-// every entry from its 13 LDS taps.
-template <bool REG>
+// by its LDS reads); 2 = 30 x 16 outputs (mip0 tile 64 x 36, runs of 9) and the 2:1 stage in vertical output pairs
+// (down21_vpair: 240 lanes, 48 LDS reads per pair instead of 72); 0 = 32 x 8 outputs, every mip0 entry from its 13 LDS
+// taps and every output from its 36. Each entry's and output's fmas in down11's / down21's order: the same bits in every
+// mode (tests/test_gpu_parity.py).
+template <int MODE>
 struct W1 {
-    static constexpr int OW = REG ? 30 : 32, OH = 8;       // mip1 outputs per workgroup
-    static constexpr int MW = 2 * OW + 4, MH = 2 * OH + 4;  // mip0 tile 64 (68) x 20, origin (2 X0 - 2, 2 Y0 - 2)
-    static constexpr int EW = MW + 4, EH = MH + 4;          // emissive tile 68 (72) x 24, origin (2 X0 - 4, 2 Y0 - 4)
-    static_assert(!REG || (MW == 64 && MH == 20), "down11_runs: 64 columns x 2 row parities x 2 runs of 5");
+    static constexpr int OW = MODE ? 30 : 32, OH = MODE == 2 ? 16 : 8;   // mip1 outputs per workgroup
+    static constexpr int MW = 2 * OW + 4, MH = 2 * OH + 4;  // mip0 tile, origin (2 X0 - 2, 2 Y0 - 2)
+    static constexpr int EW = MW + 4, EH = MH + 4;          // emissive tile, origin (2 X0 - 4, 2 Y0 - 4)
+    static constexpr int RUN = MH / 4;                      // mip0 entries per lane run (64 columns x 2 parities x 2 runs)
+    static_assert(!MODE || (MW == 64 && MH % 4 == 0), "down11_runs: 64 columns x 2 row parities x 2 runs");
 };
 
 // down11 of the mip0 entries (c, r), (c, r + 2), ..., (c, r + 8) of the tile (rows r..r+8 inside the tile: no vertical
 // clamping in this workgroup), centre column cx (the clamped image column, tile-relative): a sliding window of the five
 // footprint rows (three texels on the centre's row parity, two on the other), two rows loaded per entry after the first.
 // Each entry's 13 fmas in down11's order.
-template <int TW, int MW>
+template <int TW, int MW, int RUN>
 __device__ __forceinline__ void down11_runs(const uint2 (*t)[TW], uint2 (*mt)[MW], int c, int r, int cx) {
     uint2 e0[3], o1[2], e2[3], o3[2], e4[3];
     const int cy0 = r + 2;   // emissive-tile row of the first entry's centre
@@ -151,7 +154,7 @@ __device__ __forceinline__ void down11_runs(const uint2 (*t)[TW], uint2 (*mt)[MW
     odd(cy0 + 1, o3);
     even(cy0 + 2, e4);
 #pragma unroll
-    for (int j = 0; j < 5; ++j) {
+    for (int j = 0; j < RUN; ++j) {
         C3 a{0.0f, 0.0f, 0.0f};
         madd(a, e2[1], 0.125f);
         madd(a, e0[0], 0.03125f);
@@ -167,7 +170,7 @@ __device__ __forceinline__ void down11_runs(const uint2 (*t)[TW], uint2 (*mt)[MW
         madd(a, o3[0], 0.125f);
         madd(a, o3[1], 0.125f);
         mt[r + 2 * j][c] = pack3(a);
-        if (j < 4) {
+        if (j < RUN - 1) {
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
                 e0[k] = e2[k];
@@ -182,15 +185,37 @@ __device__ __forceinline__ void down11_runs(const uint2 (*t)[TW], uint2 (*mt)[MW
     }
 }
 
+// down21 of the vertically adjacent outputs whose 6x6 blocks start at tile rows r0 and r0 + 2 (column c0): the 8 rows
+// r0..r0+7 read once (6 texels each, 48 reads instead of 72), each row's texels added to the outputs it belongs to, so
+// each output still sums its 36 taps in down21's order (rows outer, columns inner): the same bits.
+template <int TW>
+__device__ __forceinline__ void down21_vpair(const uint2 (*t)[TW], int c0, int r0, C3& a, C3& b) {
+    a = C3{0.0f, 0.0f, 0.0f};
+    b = C3{0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        uint2 v[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) v[i] = t[r0 + j][c0 + i];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            if (j < 6) madd(a, v[i], d21_w(i, j));
+            if (j >= 2) madd(b, v[i], d21_w(i, j - 2));
+        }
+        // one row's texels live at a time (without it the compiler hoists all 48 reads: 168 VGPRs)
+        asm volatile("" : "+v"(a.r), "+v"(a.g), "+v"(a.b), "+v"(b.r), "+v"(b.g), "+v"(b.b)::"memory");
+    }
+}
+
 // W1, persistent: each workgroup walks tiles t = blockIdx.x, + gridDim.x, ... (XCD-aware contiguous eighths, as
 // swz = 1), and loads the NEXT tile's emissive texels into registers while it filters the current one from LDS, so
 // the tile loads' latency hides behind the filter instead of being waited on (the one-tile kernel waits on its
 // loads and barriers for 61 % of its wave cycles, profiles/r03_sq_stalls.json: 47.5 -> 42.9 us serial at 4K). The
 // same arithmetic and bits as that one-tile-per-workgroup kernel.
-template <bool REG>
+template <int MODE>
 __global__ __launch_bounds__(kWorkgroup) void bloomw_down01p(DImg E, DImg M1, int ntx, int nty) {
-    constexpr int W1_OW = W1<REG>::OW, W1_OH = W1<REG>::OH, W1_MW = W1<REG>::MW, W1_MH = W1<REG>::MH, W1_EW = W1<REG>::EW,
-                  W1_EH = W1<REG>::EH;
+    constexpr int W1_OW = W1<MODE>::OW, W1_OH = W1<MODE>::OH, W1_MW = W1<MODE>::MW, W1_MH = W1<MODE>::MH,
+                  W1_EW = W1<MODE>::EW, W1_EH = W1<MODE>::EH, RUN = W1<MODE>::RUN;
     __shared__ uint2 et[W1_EH][W1_EW];
     __shared__ uint2 mt[W1_MH][W1_MW];
     constexpr int NT = W1_EW * W1_EH, KR = (NT + 255) / 256;
@@ -232,10 +257,10 @@ __global__ __launch_bounds__(kWorkgroup) void bloomw_down01p(DImg E, DImg M1, in
         const int mx0 = 2 * X0 - 2, my0 = 2 * Y0 - 2, ex0 = mx0 - 2, ey0 = my0 - 2;
         // register-blocked runs unless the tile's mip0 rows reach past the image's top or bottom (there a clamped row
         // repeats, which the fixed row stride does not follow): a uniform branch
-        if (REG && my0 >= 0 && my0 + W1_MH <= E.h) {
+        if (MODE && my0 >= 0 && my0 + W1_MH <= E.h) {
             const int c = tid & 63, par = (tid >> 6) & 1, half = tid >> 7;
-            if constexpr (REG)
-                down11_runs<W1_EW, W1_MW>(et, mt, c, par + 10 * half, clampi(mx0 + c, 0, E.w - 1) - ex0);
+            if constexpr (MODE != 0)
+                down11_runs<W1_EW, W1_MW, RUN>(et, mt, c, par + 2 * RUN * half, clampi(mx0 + c, 0, E.w - 1) - ex0);
         } else
         for (int i = tid; i < W1_MW * W1_MH; i += 256) {
             const int r = i / W1_MW, c = i - r * W1_MW;
@@ -243,9 +268,20 @@ __global__ __launch_bounds__(kWorkgroup) void bloomw_down01p(DImg E, DImg M1, in
             mt[r][c] = pack3(down11<W1_EW>(et, cx, cy));
         }
         __syncthreads();
-        const int oy = tid / W1_OW, ox = tid - oy * W1_OW;
-        const int X = X0 + ox, Y = Y0 + oy;
-        if (oy < W1_OH && X < M1.w && Y < M1.h) row_ptr_w<uint2>(M1, Y)[X] = pack3(down21<W1_MW>(mt, 2 * ox, 2 * oy));
+        if constexpr (MODE == 2) {   // vertical output pairs: lanes 0..239, outputs (ox, 2 q) and (ox, 2 q + 1)
+            if (tid < W1_OW * W1_OH / 2) {
+                const int q = tid / W1_OW, ox = tid - q * W1_OW;
+                const int X = X0 + ox, Y = Y0 + 2 * q;
+                C3 a, b;
+                down21_vpair<W1_MW>(mt, 2 * ox, 4 * q, a, b);
+                if (X < M1.w && Y < M1.h) row_ptr_w<uint2>(M1, Y)[X] = pack3(a);
+                if (X < M1.w && Y + 1 < M1.h) row_ptr_w<uint2>(M1, Y + 1)[X] = pack3(b);
+            }
+        } else {
+            const int oy = tid / W1_OW, ox = tid - oy * W1_OW;
+            const int X = X0 + ox, Y = Y0 + oy;
+            if (oy < W1_OH && X < M1.w && Y < M1.h) row_ptr_w<uint2>(M1, Y)[X] = pack3(down21<W1_MW>(mt, 2 * ox, 2 * oy));
+        }
         __syncthreads();   // et / mt are rewritten by the next tile
     }
 }
@@ -582,7 +618,7 @@ __global__ __launch_bounds__(kWorkgroup) void bloomw_up10r(DImg S1, DImg O, int 
 
 // Workgroups of 256 lanes of bloomw_down01p resident on the whole device at once (the persistent kernel's grid bound),
 // queried once per device and cached (the occupancy query is not on the per-frame enqueue path).
-template <bool REG>
+template <int MODE>
 int down01p_resident_set() {
     constexpr int kMaxDevices = 64;
     static int cached[kMaxDevices] = {};
@@ -590,7 +626,7 @@ int down01p_resident_set() {
     (void)hipGetDevice(&dev);
     if (dev >= 0 && dev < kMaxDevices && cached[dev]) return cached[dev];
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, bloomw_down01p<REG>, 256, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, bloomw_down01p<MODE>, 256, 0);
     const int n = std::max(per, 1) * cus;
     if (dev >= 0 && dev < kMaxDevices) cached[dev] = n;
     return n;
@@ -605,14 +641,16 @@ int launch_bloom_weighted(const soc_img& emissive, const soc_img* mips, const so
     const int swz = 1;   // XCD-aware order: halo re-reads served by L2 (2.0x -> 1.0x HBM traffic)
     if (stage == 0 || stage == 1) {
         // persistent: one resident set of workgroups (a multiple of 8, so a workgroup's tiles stay on its XCD)
-        auto w1 = [&](auto reg) {
-            constexpr bool R = decltype(reg)::value;
+        auto w1 = [&](auto mode) {
+            constexpr int R = decltype(mode)::value;
             const int ntx = ceil_div(mips[1].width, W1<R>::OW), nty = ceil_div(mips[1].height, W1<R>::OH);
             const int grid = std::max(8, (std::min(ntx * nty, down01p_resident_set<R>()) / 8) * 8);
             launch("bloomw_down01p", kWorkgroup, bloomw_down01p<R>, grid, kWorkgroup, 0, s, E, M1, ntx, nty);
         };
-        if (tuning_knob("SOC_BLOOM_W1_REG", 1)) w1(std::true_type{});
-        else w1(std::false_type{});
+        const int mode = tuning_knob("SOC_BLOOM_W1_REG", 1);
+        if (mode == 2) w1(std::integral_constant<int, 2>{});
+        else if (mode == 1) w1(std::integral_constant<int, 1>{});
+        else w1(std::integral_constant<int, 0>{});
     }
     if (stage == 0 || stage == 2) {
         dim3 g(ceil_div(mips[3].width, W2_OW), ceil_div(mips[3].height, W2_OH));
