@@ -293,6 +293,42 @@ constexpr int W2_OW = 16, W2_OH = 8;                          // mip3 outputs pe
 constexpr int W2_MW = 2 * W2_OW + 4, W2_MH = 2 * W2_OH + 4;   // mip2 tile 36 x 20
 constexpr int W2_SW = 2 * W2_MW + 4, W2_SH = 2 * W2_MH + 4;   // mip1 tile 76 x 44
 
+// down21 of the mip2 entries (c, r0 .. r0 + K - 1) of one column (no vertical clamping in this workgroup): the run's
+// 6 + 2 (K - 1) mip1 rows read once (6 texels each; entries one row apart share 4 of their 6 rows), each row's texels
+// added to the entries whose block holds it, so each entry sums its 36 taps in down21's order: the same bits.
+template <int TW, int MW, int K>
+__device__ __forceinline__ void down21_runs(const uint2 (*t)[TW], uint2 (*mt)[MW], int c, int r0, int n, int sc) {
+    C3 acc[K];
+#pragma unroll
+    for (int e = 0; e < K; ++e) acc[e] = C3{0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int R = 0; R < 6 + 2 * (K - 1); ++R) {
+        // a shorter last run (n < K entries) skips the rows only its missing entries need (reads inside the tile)
+        if (R >= 6 + 2 * (n - 1)) continue;
+        uint2 v[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) v[i] = t[2 * r0 + R][sc + i];
+#pragma unroll
+        for (int e = 0; e < K; ++e) {
+            const int j = R - 2 * e;
+            if (j >= 0 && j < 6) {
+#pragma unroll
+                for (int i = 0; i < 6; ++i) madd(acc[e], v[i], d21_w(i, j));
+            }
+        }
+        // one row's texels live at a time (the row's fmas complete before the next row's reads)
+#pragma unroll
+        for (int e = 0; e < K; ++e) asm volatile("" : "+v"(acc[e].r), "+v"(acc[e].g), "+v"(acc[e].b)::"memory");
+    }
+#pragma unroll
+    for (int e = 0; e < K; ++e)
+        if (e < n) mt[r0 + e][c] = pack3(acc[e]);
+}
+
+// REG (tuning knob SOC_BLOOM_W2_REG, default 1): the 2:1 mip1 -> mip2 stage in vertical runs of 3 entries per lane
+// (down21_runs: 36 columns x 7 runs, 60 LDS reads per run instead of 108) unless the tile's mip2 rows reach past the
+// image's top or bottom; the same bits (tests/test_gpu_parity.py).
+template <bool REG>
 __global__ __launch_bounds__(kWorkgroup) void bloomw_down23(DImg S1, DImg M3, int W2, int H2, int swz) {
     __shared__ uint2 st[W2_SH][W2_SW];
     __shared__ uint2 mt[W2_MH][W2_MW];
@@ -303,6 +339,15 @@ __global__ __launch_bounds__(kWorkgroup) void bloomw_down23(DImg S1, DImg M3, in
     const int mx0 = 2 * X0 - 2, my0 = 2 * Y0 - 2, sx0 = 2 * mx0 - 2, sy0 = 2 * my0 - 2;
     load_tile<W2_SW, W2_SH>(S1, sx0, sy0, st, tid);
     __syncthreads();
+    constexpr int K = 3, NR = (W2_MH + K - 1) / K;   // 7 runs per column, the last one of 2
+    static_assert(W2_MW * NR <= 256, "one run per lane");
+    if (REG && my0 >= 0 && my0 + W2_MH <= H2) {
+        if (tid < W2_MW * NR) {
+            const int c = tid % W2_MW, k = tid / W2_MW, r0 = k * K;
+            const int qx = clampi(mx0 + c, 0, W2 - 1);
+            down21_runs<W2_SW, W2_MW, K>(st, mt, c, r0, min(K, W2_MH - r0), 2 * qx - 2 - sx0);
+        }
+    } else
     for (int i = tid; i < W2_MW * W2_MH; i += 256) {
         const int r = i / W2_MW, c = i - r * W2_MW;
         const int qx = clampi(mx0 + c, 0, W2 - 1), qy = clampi(my0 + r, 0, H2 - 1);
@@ -654,7 +699,10 @@ int launch_bloom_weighted(const soc_img& emissive, const soc_img* mips, const so
     }
     if (stage == 0 || stage == 2) {
         dim3 g(ceil_div(mips[3].width, W2_OW), ceil_div(mips[3].height, W2_OH));
-        launch("bloomw_down23", kWorkgroup, bloomw_down23, g, kWorkgroup, 0, s, M1, M3, mips[2].width, mips[2].height, swz);
+        if (tuning_knob("SOC_BLOOM_W2_REG", 1))
+            launch("bloomw_down23", kWorkgroup, bloomw_down23<true>, g, kWorkgroup, 0, s, M1, M3, mips[2].width, mips[2].height, swz);
+        else
+            launch("bloomw_down23", kWorkgroup, bloomw_down23<false>, g, kWorkgroup, 0, s, M1, M3, mips[2].width, mips[2].height, swz);
     }
     if (stage == 0 || stage == 3) {
         dim3 g(ceil_div(mips[1].width, U_OW), ceil_div(mips[1].height, U_OH));

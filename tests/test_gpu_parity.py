@@ -179,6 +179,29 @@ def test_bloom_w1_register_runs_bit_identical(soc, monkeypatch, W, H):
         assert torch.equal(res[0][1], out)
 
 
+@pytest.mark.parametrize("W,H", [(3840, 2160), (1920, 1080), (968, 552), (136, 40), (512, 64)])
+def test_bloom_w2_register_runs_bit_identical(soc, monkeypatch, W, H):
+    """The second downsample's 2:1 mip1 -> mip2 stage in vertical runs of 3 entries per lane (bloomw_down23<true>: each
+    run's mip1 rows read once) gives the per-entry kernel's bits (the same 36 fmas per entry in the same order): mip3
+    and the chain's output; small extents: tiles at the image's top and bottom (the per-entry fallback)."""
+    g = globals_for(W, H)
+    em = dev(random_rgba16(H, W, seed=37, hi=16.0))
+    shapes = [(H >> i, W >> i, 4) for i in range(4)]
+    res = []
+    for reg in ("0", "1"):
+        monkeypatch.setenv("SOC_BLOOM_W2_REG", reg)
+        soc.reload_tuning()
+        mips = [torch.zeros(sh, dtype=torch.float16, device=DEV) for sh in shapes]
+        out = torch.zeros_like(em)
+        soc.bloom_weighted_stage(g, em, mips, out, 0)
+        res.append((mips[3], out))
+    torch.cuda.synchronize()
+    monkeypatch.delenv("SOC_BLOOM_W2_REG")
+    soc.reload_tuning()
+    assert torch.equal(res[0][0], res[1][0]), (res[0][0] != res[1][0]).float().mean().item()
+    assert torch.equal(res[0][1], res[1][1])
+
+
 def test_bloom_weighted_in_place(soc):
     """output == emissive (the reference's in-place bloom) gives the separate-output result."""
     W, H = 968, 552
