@@ -296,8 +296,9 @@ def test_ssao_tile_orders_bit_identical(soc, monkeypatch, W, H, inputs):
     assert (d > 0).mean() <= 1e-4 and d.max() <= 10, ((d > 0).sum(), d.max())
 
 
-@pytest.mark.parametrize("W,H", [(64, 36), (97, 55), (1920, 1080)])
+@pytest.mark.parametrize("W,H", [(64, 36), (97, 55), (1920, 1080), (3840, 2160), (100, 40), (16, 8)])
 def test_ssao_blur_bit_exact(soc, oracle, W, H):
+    """Up to the 4K frame's 1920 x 1080 half-res image, and extents of 8 and 50 half-res pixels (every lane near a border)."""
     g = globals_for(W, H)
     rng = np.random.default_rng(3)
     src = rng.integers(0, 256, (H // 2, W // 2), dtype=np.uint8)
