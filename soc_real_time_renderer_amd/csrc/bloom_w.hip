@@ -427,6 +427,7 @@ __global__ __launch_bounds__(kWorkgroup) void bloomw_up32(DImg S3, DImg M1, int 
 struct P3u {
     float r[W3_MH][U_OW], g[W3_MH][U_OW], b[W3_MH][U_OW];   // 10 x 36 (first stage) and 12 x 64 (second) fit
 };
+template <bool RUNS>
 __global__ __launch_bounds__(kWorkgroup) void bloomw_up32s(DImg S3, DImg M1, int W2, int H2, bool vec, int swz) {
     __shared__ uint2 st[W3_SH][W3_SW];
     __shared__ uint2 mt[W3_MH][W3_MW];
@@ -475,6 +476,34 @@ __global__ __launch_bounds__(kWorkgroup) void bloomw_up32s(DImg S3, DImg M1, int
         hp.b[r][ox] = a.b;
     }
     __syncthreads();
+    if constexpr (RUNS) {
+        static_assert(U_OW == 64 && U_OH == 16, "64 columns x 4 runs of 4 output rows");
+        // SOC_BLOOM_W3_RUNS (default 1): the last vertical 1:2 phase in runs of 4 outputs of one column per lane
+        // (outputs Y0 + 4 m .. + 3 read the hp rows 2 m .. 2 m + 5 once: 18 LDS reads instead of 48); each output's 4
+        // fmas in the same order: the same bits
+        const int ox = tid & 63, m = tid >> 6, x = X0 + ox;
+        float hr[6], hg[6], hb[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            hr[k] = hp.r[2 * m + k][ox];
+            hg[k] = hp.g[2 * m + k][ox];
+            hb[k] = hp.b[2 * m + k][ox];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int y = Y0 + 4 * m + i, py = i & 1, rr = (i >> 1) + (i & 1);
+            C3 a{0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float w = u12_w(py, j);
+                a.r = __builtin_fmaf(hr[rr + j], w, a.r);
+                a.g = __builtin_fmaf(hg[rr + j], w, a.g);
+                a.b = __builtin_fmaf(hb[rr + j], w, a.b);
+            }
+            if (x < M1.w && y < M1.h) row_ptr_w<uint2>(M1, y)[x] = pack3(a);
+        }
+        return;
+    }
     for (int i = tid; i < (U_OW / 2) * U_OH; i += 256) {
         const int r = i / (U_OW / 2), pc = i - r * (U_OW / 2);
         const int x = X0 + 2 * pc, y = Y0 + r;
@@ -707,7 +736,10 @@ int launch_bloom_weighted(const soc_img& emissive, const soc_img* mips, const so
     if (stage == 0 || stage == 3) {
         dim3 g(ceil_div(mips[1].width, U_OW), ceil_div(mips[1].height, U_OH));
         if (tuning_knob("SOC_BLOOM_UP_SEP", 1))
-            launch("bloomw_up32s", kWorkgroup, bloomw_up32s, g, kWorkgroup, 0, s, M3, M1, mips[2].width, mips[2].height, a16(mips[1]), swz);
+            if (tuning_knob("SOC_BLOOM_W3_RUNS", 1))
+                launch("bloomw_up32s", kWorkgroup, bloomw_up32s<true>, g, kWorkgroup, 0, s, M3, M1, mips[2].width, mips[2].height, a16(mips[1]), swz);
+            else
+                launch("bloomw_up32s", kWorkgroup, bloomw_up32s<false>, g, kWorkgroup, 0, s, M3, M1, mips[2].width, mips[2].height, a16(mips[1]), swz);
         else
             launch("bloomw_up32", kWorkgroup, bloomw_up32, g, kWorkgroup, 0, s, M3, M1, mips[2].width, mips[2].height, a16(mips[1]), swz);
     }

@@ -202,6 +202,27 @@ def test_bloom_w2_register_runs_bit_identical(soc, monkeypatch, W, H):
     assert torch.equal(res[0][1], res[1][1])
 
 
+@pytest.mark.parametrize("W,H", [(3840, 2160), (1920, 1080), (968, 552), (136, 40)])
+def test_bloom_w3_runs_bit_identical(soc, monkeypatch, W, H):
+    """The first upsample's last vertical 1:2 phase in runs of 4 output rows per lane (bloomw_up32s<true>) gives the
+    per-pair loop's bits (the same 4 fmas per output in the same order): mip1 after stage 3 and the chain's output."""
+    g = globals_for(W, H)
+    em = dev(random_rgba16(H, W, seed=41, hi=16.0))
+    shapes = [(H >> i, W >> i, 4) for i in range(4)]
+    res = []
+    for runs in ("0", "1"):
+        monkeypatch.setenv("SOC_BLOOM_W3_RUNS", runs)
+        soc.reload_tuning()
+        mips = [torch.zeros(sh, dtype=torch.float16, device=DEV) for sh in shapes]
+        out = torch.zeros_like(em)
+        soc.bloom_weighted_stage(g, em, mips, out, 0)
+        res.append(out)
+    torch.cuda.synchronize()
+    monkeypatch.delenv("SOC_BLOOM_W3_RUNS")
+    soc.reload_tuning()
+    assert torch.equal(res[0], res[1]), (res[0] != res[1]).float().mean().item()
+
+
 def test_bloom_weighted_in_place(soc):
     """output == emissive (the reference's in-place bloom) gives the separate-output result."""
     W, H = 968, 552
